@@ -1,0 +1,170 @@
+"""Deterministic synthetic inputs and weights for the SCFlow refinement hot path.
+
+There is no dataset, renderer or checkpoint in this environment,
+so every test, golden fixture and benchmark draws its inputs from here:
+
+* decoder inputs shaped like ``SCFlowRefiner.get_pose`` hands them to the decoder
+  (``/root/reference/models/refiner/scflow_refiner.py:108-138``): render/real features
+  ``[B,256,S/8,S/8]``, ``h=tanh(.)``, ``cxt=relu(.)`` (``scflow_refiner.py:101-104``),
+  reference pose, rendered depth ``[B,S,S]``, intrinsics ``[B,3,3]``, labels, zero init flow;
+* a YCB-V-like scene: object diameters from ``configs/refine_models/scflow_ycbv_real.py:19-21``,
+  t_z ~ U(600, 1200) mm, K with f = S·t_z/(1.1·d_obj) (crop/resize maths of
+  ``datasets/pipelines/geometry_transform.py`` ``Crop``/``RemapPose``), depth of an analytic
+  ellipsoid standing in for the pytorch3d zbuf (``models/utils/rendering.py:185-248``);
+* deterministic per-parameter weights (PCG64 seeded by the crc32 of the state-dict key),
+  with the pose head's zero-initialised output layers (``models/head/pose_head.py:187-198``)
+  perturbed so the pose actually moves (SURVEY.md §7 "Hard parts" 5).
+
+Everything is generated in float64 with numpy's PCG64 and cast to float32, so the same
+arrays come out on every machine (here, and on the GPU box).
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from typing import Dict, Iterable, Tuple
+
+import numpy as np
+
+# YCB-V object diameters (mm), configs/refine_models/scflow_ycbv_real.py:19-21
+YCBV_DIAMETERS = (172.16, 269.58, 198.38, 120.66, 199.79, 90.17, 142.58, 114.39, 129.73,
+                  198.40, 263.60, 260.76, 162.27, 126.86, 230.44, 237.30, 204.11, 121.46,
+                  183.08, 231.39, 102.92)
+
+
+def _rot_zyx(az: float, ay: float, ax: float) -> np.ndarray:
+    cz, sz = math.cos(az), math.sin(az)
+    cy, sy = math.cos(ay), math.sin(ay)
+    cx, sx = math.cos(ax), math.sin(ax)
+    rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    return rz @ ry @ rx
+
+
+def _random_rotation(rng: np.random.Generator) -> np.ndarray:
+    q = rng.standard_normal(4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    return np.array([
+        [1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+        [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+        [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)],
+    ])
+
+
+def ellipsoid_depth(R: np.ndarray, t: np.ndarray, K: np.ndarray, size: int,
+                    semi_axes: np.ndarray) -> np.ndarray:
+    """z-buffer depth of an ellipsoid (object frame semi-axes ``semi_axes``) posed at (R, t).
+
+    Pixel (u, v) casts the ray X = s·K⁻¹[u, v, 1]ᵀ (z-component 1, so s is the depth);
+    the nearest intersection with (Rᵀ(X−t))ᵀ D (Rᵀ(X−t)) = 1 is the depth; 0 = background,
+    matching the renderer's zbuf convention (models/utils/rendering.py, decoder uses depth>0).
+    """
+    v, u = np.meshgrid(np.arange(size, dtype=np.float64), np.arange(size, dtype=np.float64),
+                       indexing="ij")
+    rays = np.stack([u, v, np.ones_like(u)], -1) @ np.linalg.inv(K).T  # [S,S,3], z = 1
+    D = np.diag(1.0 / semi_axes ** 2)
+    dr = rays @ R  # Rᵀ d for every ray (row vectors)
+    tr = R.T @ t
+    a = np.einsum("hwi,ij,hwj->hw", dr, D, dr)
+    b = -2.0 * np.einsum("hwi,ij,j->hw", dr, D, tr)
+    c = float(tr @ D @ tr - 1.0)
+    disc = b * b - 4 * a * c
+    hit = disc > 0
+    s = np.where(hit, (-b - np.sqrt(np.where(hit, disc, 0.0))) / (2 * a), 0.0)
+    return np.where(hit & (s > 0), s, 0.0)
+
+
+def make_scene(batch: int, size: int, seed: int = 0, num_class: int = 21) -> Dict[str, np.ndarray]:
+    """Labels, reference poses, intrinsics and rendered depth for ``batch`` image pairs."""
+    rng = np.random.default_rng(seed + 7919)
+    labels = rng.integers(0, num_class, batch)
+    Rs, ts, Ks, depths = [], [], [], []
+    for b in range(batch):
+        d_obj = YCBV_DIAMETERS[int(labels[b]) % len(YCBV_DIAMETERS)]
+        tz = rng.uniform(600.0, 1200.0)
+        txy = rng.normal(0.0, 15.0, 2)
+        t = np.array([txy[0], txy[1], tz])
+        # reference pose = a random orientation jittered like PoseJitter (datasets/pipelines/jitter.py:51-79)
+        ang = np.clip(rng.normal(0.0, math.radians(15.0), 3), -math.radians(45), math.radians(45))
+        R = _rot_zyx(*ang) @ _random_rotation(rng)
+        f = size * tz / (1.1 * d_obj)
+        # principal point at the patch centre, shifted so the object centre projects near it
+        K = np.array([[f, 0.0, size / 2.0 - f * t[0] / t[2]],
+                      [0.0, f, size / 2.0 - f * t[1] / t[2]],
+                      [0.0, 0.0, 1.0]])
+        semi = np.array([0.5, 0.38, 0.3]) * d_obj
+        depths.append(ellipsoid_depth(R, t, K, size, semi))
+        Rs.append(R)
+        ts.append(t)
+        Ks.append(K)
+    return dict(labels=labels.astype(np.int64), ref_rotation=np.stack(Rs).astype(np.float32),
+                ref_translation=np.stack(ts).astype(np.float32),
+                internel_k=np.stack(Ks).astype(np.float32),
+                depth=np.stack(depths).astype(np.float32))
+
+
+def make_decoder_inputs(batch: int, size: int, seed: int = 0, feat_channels: int = 256,
+                        h_channels: int = 128, cxt_channels: int = 128,
+                        num_class: int = 21) -> Dict[str, np.ndarray]:
+    """All inputs of ``SCFlowDecoder.forward`` (scflow_decoder.py:151-156) as float32 numpy."""
+    rng = np.random.default_rng(seed)
+    h = w = size // 8
+    feat_render = rng.standard_normal((batch, feat_channels, h, w))
+    # the real image is the rendered one moved by a couple of feature cells plus noise, so the
+    # correlation volume has a real peak away from the identity
+    feat_real = np.roll(feat_render, shift=(1, -2), axis=(2, 3)) + 0.3 * rng.standard_normal(
+        feat_render.shape)
+    h_feat = np.tanh(rng.standard_normal((batch, h_channels, h, w)))
+    cxt_feat = np.maximum(rng.standard_normal((batch, cxt_channels, h, w)), 0.0)
+    out = dict(feat_render=feat_render.astype(np.float32), feat_real=feat_real.astype(np.float32),
+               h_feat=h_feat.astype(np.float32), cxt_feat=cxt_feat.astype(np.float32))
+    out.update(make_scene(batch, size, seed, num_class))
+    out["init_flow"] = np.zeros((batch, 2, size, size), np.float32)
+    return out
+
+
+def _param_rng(key: str, seed: int) -> np.random.Generator:
+    return np.random.default_rng(zlib.crc32(key.encode()) ^ (seed * 0x9E3779B1 & 0xFFFFFFFF))
+
+
+def param_value(key: str, shape: Tuple[int, ...], seed: int = 0) -> np.ndarray:
+    """Deterministic value for one decoder parameter, by its reference state-dict key.
+
+    conv/linear weights: U(-1,1)·√(3/fan_in) (unit-variance pre-activations);
+    biases: U(-0.1, 0.1); GroupNorm affine: 1+U(-.1,.1) / U(-.1,.1).
+    The pose head's output layers (zero-initialised in the reference, pose_head.py:187-198)
+    get small weights and the identity ortho6d bias plus a perturbation, so Δpose ≠ identity.
+    """
+    rng = _param_rng(key, seed)
+    u = rng.uniform(-1.0, 1.0, size=shape)
+    if "rotation_pred" in key or "translation_pred" in key:
+        if key.endswith("weight"):
+            return (u * 2e-3).astype(np.float32)
+        if "rotation_pred" in key:  # ortho6d identity [1,0,0,0,1,0] per class + noise
+            base = np.tile(np.array([1.0, 0, 0, 0, 1.0, 0]), shape[0] // 6)
+            return (base + 2e-2 * u).astype(np.float32)
+        return (2e-2 * u).astype(np.float32)
+    if key.endswith(".gn.weight"):
+        return (1.0 + 0.1 * u).astype(np.float32)
+    if key.endswith(".gn.bias") or key.endswith("bias"):
+        return (0.1 * u).astype(np.float32)
+    fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else int(shape[0])
+    return (u * math.sqrt(3.0 / max(fan_in, 1))).astype(np.float32)
+
+
+def make_state_dict(shapes: Iterable[Tuple[str, Tuple[int, ...]]], seed: int = 0) -> Dict[str, np.ndarray]:
+    """Values for every (key, shape) pair; keys are the reference decoder's state-dict keys."""
+    return {k: param_value(k, tuple(s), seed) for k, s in shapes}
+
+
+def fill_module_(module, seed: int = 0) -> None:
+    """Overwrite every parameter of a torch module with ``param_value`` (in place)."""
+    import torch
+    with torch.no_grad():
+        for k, p in module.state_dict().items():
+            if not p.is_floating_point():
+                continue
+            v = torch.from_numpy(param_value(k, tuple(p.shape), seed))
+            p.copy_(v.to(p.dtype))

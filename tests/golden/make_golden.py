@@ -1,0 +1,268 @@
+"""Generate golden vectors by running the REFERENCE's own hot-path modules on CPU.
+
+Run in the development container only (needs ``/root/reference``; never on the GPU box):
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+
+The reference (GiaKhangLuu/SCFlow) is pure Python/PyTorch; its hot-path modules import
+mmcv / mmengine / kornia / cv2 / turtle / a registry, none of which are installed here
+(SURVEY.md §8(c)).  This script installs minimal test-only stand-ins for those imports
+*in this process only*, then loads the reference files straight from ``/root/reference``
+by path (bypassing ``models/__init__.py``, which would import pytorch3d):
+
+* ``mmcv.cnn.ConvModule`` — restated as conv → (norm) → act with ``bias = norm is None``
+  (mmcv's documented ``bias='auto'`` behaviour; layer names ``conv``/``gn`` so the
+  state-dict keys are the reference's);
+* ``mmengine.model.BaseModule`` — ``nn.Module`` accepting ``init_cfg``;
+* ``registry.MODELS`` — ``register_module()`` / ``build(cfg)``;
+* ``kornia``, ``cv2``, ``datasets.pose``, ``turtle`` — empty modules (only used off-path:
+  quaternion mode, PnP, ``from turtle import forward`` at raft_decoder.py:3).
+
+Everything arithmetic on the path — CorrelationPyramid, CorrLookup, MotionEncoder,
+ConvGRU, XHead, MultiClassPoseHead, pose.py, SCFlowDecoder.forward — is the reference's
+own code.  Inputs and weights come from ``scflow_amd.synthetic`` (deterministic), so the
+fixtures store outputs (and small inputs); nothing of the reference's source is stored.
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from scflow_amd import synthetic  # noqa: E402
+
+
+# ------------------------------------------------------------------ test-only stand-ins
+class _BaseModule(nn.Module):
+    def __init__(self, init_cfg=None):
+        super().__init__()
+        self.init_cfg = init_cfg
+
+
+class _ConvModule(nn.Module):
+    """mmcv ConvModule as used on the path: conv → norm → act, bias iff no norm."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0,
+                 conv_cfg=None, norm_cfg=None, act_cfg=dict(type="ReLU"), **kw):
+        super().__init__()
+        self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride=stride,
+                              padding=padding, bias=norm_cfg is None)
+        self.norm_name = None
+        if norm_cfg is not None:
+            assert norm_cfg["type"] == "GN"
+            self.norm_name = "gn"
+            self.gn = nn.GroupNorm(norm_cfg["num_groups"], out_channels)
+        self.act = None
+        if act_cfg is not None:
+            self.act = {"ReLU": nn.ReLU, "Sigmoid": nn.Sigmoid, "Tanh": nn.Tanh}[act_cfg["type"]]()
+
+    def forward(self, x):
+        x = self.conv(x)
+        if self.norm_name:
+            x = self.gn(x)
+        if self.act is not None:
+            x = self.act(x)
+        return x
+
+
+class _Registry:
+    def __init__(self):
+        self._m = {}
+
+    def register_module(self, name=None, module=None, force=False):
+        def deco(cls):
+            self._m[cls.__name__] = cls
+            return cls
+        return deco
+
+    def build(self, cfg):
+        cfg = dict(cfg)
+        typ = cfg.pop("type")
+        cls = self._m[typ] if isinstance(typ, str) else typ
+        return cls(**cfg)
+
+
+def _stub(name, **attrs):
+    m = types.ModuleType(name)
+    m.__dict__.update(attrs)
+    sys.modules[name] = m
+    return m
+
+
+def _pkg(name, path):
+    m = _stub(name)
+    m.__path__ = [path]
+    return m
+
+
+def _load(name, relpath):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, relpath))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_reference():
+    """Import the reference hot-path modules; returns a namespace of them."""
+    _stub("mmcv")
+    _stub("mmcv.cnn", ConvModule=_ConvModule)
+    _stub("mmengine")
+    _stub("mmengine.model", BaseModule=_BaseModule, Sequential=nn.Sequential)
+    MODELS = _Registry()
+    _stub("registry", MODELS=MODELS)
+    _stub("kornia")
+    _stub("cv2")
+    _stub("turtle", forward=None)
+    _pkg("datasets", os.path.join(REF, "datasets"))
+    _stub("datasets.pose", remap_pose=None)
+    _pkg("models", os.path.join(REF, "models"))
+    utils = _pkg("models.utils", os.path.join(REF, "models/utils"))
+    _pkg("models.decoder", os.path.join(REF, "models/decoder"))
+    _pkg("models.head", os.path.join(REF, "models/head"))
+    cl = _load("models.utils.corr_lookup", "models/utils/corr_lookup.py")
+    pose = _load("models.utils.pose", "models/utils/pose.py")
+    for k in ("CorrLookup", "coords_grid"):
+        setattr(utils, k, getattr(cl, k))
+    for k in ("get_flow_from_delta_pose_and_points", "get_pose_from_delta_pose",
+              "cal_3d_2d_corr", "get_flow_from_delta_pose_and_depth"):
+        setattr(utils, k, getattr(pose, k))
+    rd = _load("models.decoder.raft_decoder", "models/decoder/raft_decoder.py")
+    sd = _load("models.decoder.scflow_decoder", "models/decoder/scflow_decoder.py")
+    ph = _load("models.head.pose_head", "models/head/pose_head.py")
+    return types.SimpleNamespace(MODELS=MODELS, corr_lookup=cl, pose=pose, raft=rd, scflow=sd,
+                                 pose_head=ph)
+
+
+# decoder block of configs/refine_models/scflow_ycbv_real.py:207-230
+def decoder_cfg(ref, iters=4, feat_size=None):
+    head = dict(type=ref.pose_head.MultiClassPoseHead, num_class=21, in_channels=224,
+                net_type="Basic", rotation_mode="ortho6d",
+                norm_cfg=dict(type="GN", num_groups=32, requires_grad=True),
+                act_cfg=dict(type="ReLU"))
+    if feat_size is not None:
+        head["feat_size"] = feat_size
+    return dict(net_type="Basic", num_levels=4, radius=4, iters=iters, detach_flow=True,
+                detach_mask=True, detach_pose=True, detach_depth_for_xy=True, mask_flow=False,
+                mask_corr=False, pose_head_cfg=head, corr_lookup_cfg=dict(align_corners=True),
+                gru_type="SeqConv", act_cfg=dict(type="ReLU"))
+
+
+def t32(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def gen_ops(ref, out):
+    rng = np.random.default_rng(123)
+    # (1) correlation pyramid, N=2 C=8 H=W=8
+    f1 = rng.standard_normal((2, 8, 8, 8)).astype(np.float32)
+    f2 = rng.standard_normal((2, 8, 8, 8)).astype(np.float32)
+    pyr = ref.raft.CorrelationPyramid(num_levels=4)(t32(f1), t32(f2))
+    out["pyr_f1"], out["pyr_f2"] = f1, f2
+    for i, p in enumerate(pyr):
+        out[f"pyr_l{i}"] = p.numpy()
+    # (2) lookup on that pyramid, flow in ±6 px (hits zero padding), r=4 and r=1
+    flow = rng.uniform(-6, 6, (2, 2, 8, 8)).astype(np.float32)
+    out["lk_flow"] = flow
+    for r in (4, 1):
+        lk = ref.corr_lookup.CorrLookup(radius=r, align_corners=True)
+        out[f"lk_r{r}"] = lk([p.clone() for p in pyr], t32(flow)).numpy()
+    # (3) one SeqConv GRU step, h/x at 2×8×8 (h 8 ch, x 16 ch)
+    gru = ref.raft.ConvGRU(8, 16, net_type="SeqConv")
+    synthetic.fill_module_(gru, seed=3)
+    h = np.tanh(rng.standard_normal((2, 8, 8, 8))).astype(np.float32)
+    x = rng.standard_normal((2, 16, 8, 8)).astype(np.float32)
+    with torch.no_grad():
+        out["gru_h"], out["gru_x"] = h, x
+        out["gru_out"] = gru(t32(h), t32(x)).numpy()
+    # (4) pose update + pose-induced flow: B=3 poses, analytic depth 64², f chosen per scene
+    scene = synthetic.make_scene(3, 64, seed=5)
+    drot = (np.tile([1.0, 0, 0, 0, 1.0, 0], (3, 1)) + 0.05 * rng.standard_normal((3, 6))).astype(np.float32)
+    dtr = (np.array([[0.5, -0.3, 0.02]]) * rng.standard_normal((3, 3))).astype(np.float32)
+    R1, t1 = ref.pose.get_pose_from_delta_pose(t32(drot), t32(dtr), t32(scene["ref_rotation"]),
+                                              t32(scene["ref_translation"]), depth_transform="exp",
+                                              detach_depth_for_xy=True)
+    p2d, p3d = [], []
+    for i in range(3):
+        a, b = ref.pose.cal_3d_2d_corr(t32(scene["depth"][i]), t32(scene["internel_k"][i]),
+                                       t32(scene["ref_rotation"][i]), t32(scene["ref_translation"][i]))
+        p2d.append(a)
+        p3d.append(b)
+    for k, v in scene.items():
+        out[f"pose_{k}"] = v
+    out["pose_drot"], out["pose_dt"] = drot, dtr
+    out["pose_R1"], out["pose_t1"] = R1.numpy(), t1.numpy()
+    for inv in (0.0, 400.0):
+        fl = ref.pose.get_flow_from_delta_pose_and_points(R1, t1, t32(scene["internel_k"]), p2d, p3d,
+                                                          64, 64, invalid_num=inv)
+        out[f"pose_flow_inv{int(inv)}"] = fl.numpy()
+    gtf = ref.pose.get_flow_from_delta_pose_and_depth(
+        t32(scene["ref_rotation"]), t32(scene["ref_translation"]), R1, t1, t32(scene["depth"]),
+        t32(scene["internel_k"]), invalid_num=400)
+    out["pose_gtflow"] = gtf.numpy()
+
+
+def run_decoder(ref, inputs, iters, feat_size=None, dtype=torch.float32, seed=0):
+    dec = ref.MODELS.build(dict(type=ref.scflow.SCFlowDecoder, **decoder_cfg(ref, iters, feat_size)))
+    synthetic.fill_module_(dec, seed=seed)
+    dec = dec.to(dtype).eval()
+    t = {k: t32(v) for k, v in inputs.items()}
+    for k, v in t.items():
+        if v.is_floating_point():
+            t[k] = v.to(dtype)
+    with torch.no_grad():
+        res = dec(t["feat_render"], t["feat_real"], t["h_feat"], t["cxt_feat"], t["ref_rotation"],
+                  t["ref_translation"], t["depth"], t["internel_k"], label=t["labels"],
+                  init_flow=t["init_flow"], invalid_flow_num=0.0)
+    return dec, res
+
+
+def gen_e2e(ref, out, B=2, S=256, iters=4):
+    inputs = synthetic.make_decoder_inputs(B, S, seed=11)
+    dec, res = run_decoder(ref, inputs, iters)
+    flow_pose, flow_pred, Rs, ts, masks, drs, dts = res
+    for k, v in inputs.items():
+        if k not in ("feat_render", "feat_real", "h_feat", "cxt_feat", "init_flow"):
+            out[f"in_{k}"] = v
+    # big inputs regenerated from the seed in the test; store checksums to pin generation
+    for k in ("feat_render", "feat_real", "h_feat", "cxt_feat"):
+        out[f"sum_{k}"] = np.array([inputs[k].astype(np.float64).sum(),
+                                    np.abs(inputs[k]).astype(np.float64).sum()])
+    out["flow_pose_last"] = flow_pose[-1].numpy()
+    out["flow_pred_last"] = flow_pred[-1].numpy()
+    out["mask_last"] = masks[-1].numpy()
+    out["R"] = torch.stack(Rs).numpy()
+    out["t"] = torch.stack(ts).numpy()
+    out["drot"] = torch.stack(drs).numpy()
+    out["dt"] = torch.stack(dts).numpy()
+    out["flow_pose_absmean"] = np.array([f.abs().double().mean().item() for f in flow_pose])
+    out["flow_pred_absmean"] = np.array([f.abs().double().mean().item() for f in flow_pred])
+    out["meta"] = np.array([B, S, iters, 11])
+    out["state_keys"] = np.array(list(dec.state_dict().keys()))
+    out["state_shapes"] = np.array([",".join(map(str, v.shape)) for v in dec.state_dict().values()])
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    ref = load_reference()
+    ops = {}
+    gen_ops(ref, ops)
+    np.savez_compressed(os.path.join(HERE, "golden_ops.npz"), **ops)
+    e2e = {}
+    gen_e2e(ref, e2e)
+    np.savez_compressed(os.path.join(HERE, "golden_e2e_b2_s256_it4.npz"), **e2e)
+    for name, d in (("ops", ops), ("e2e", e2e)):
+        print(name, {k: getattr(v, "shape", None) for k, v in d.items()})
+
+
+if __name__ == "__main__":
+    main()

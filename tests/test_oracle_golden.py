@@ -1,0 +1,81 @@
+"""CPU: the oracle (oracle/scflow_oracle.py) against golden vectors produced by the reference.
+
+Pins the oracle before anything else trusts it (tests/golden/make_golden.py ran the
+reference's own modules to produce these fixtures).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import GOLDEN, golden, oracle_state_dict, t
+
+orc = pytest.importorskip("oracle.scflow_oracle")
+
+
+def test_corr_pyramid_matches_reference():
+    g = golden("ops")
+    pyr = orc.corr_pyramid(t(g["pyr_f1"]), t(g["pyr_f2"]), 4)
+    for i, p in enumerate(pyr):
+        np.testing.assert_allclose(p.numpy(), g[f"pyr_l{i}"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("radius", [4, 1])
+def test_corr_lookup_matches_reference(radius):
+    g = golden("ops")
+    pyr = [t(g[f"pyr_l{i}"]) for i in range(4)]
+    out = orc.corr_lookup(pyr, t(g["lk_flow"]), radius)
+    np.testing.assert_allclose(out.numpy(), g[f"lk_r{radius}"], rtol=1e-5, atol=1e-6)
+
+
+def test_conv_gru_matches_reference():
+    g = golden("ops")
+    from scflow_amd import synthetic
+    shapes = []
+    for gate in "zrq":
+        for i, (k, _) in enumerate(orc.GRU_KERNELS["SeqConv"]):
+            shapes.append((f"conv_{gate}.{i}.conv.weight", (8, 24) + k))
+            shapes.append((f"conv_{gate}.{i}.conv.bias", (8,)))
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(shapes, seed=3).items()}
+    out = orc.conv_gru(sd, t(g["gru_h"]), t(g["gru_x"]), prefix="")
+    np.testing.assert_allclose(out.numpy(), g["gru_out"], rtol=1e-5, atol=1e-5)
+
+
+def test_pose_update_and_flow_match_reference():
+    g = golden("ops")
+    R1, t1 = orc.pose_update(t(g["pose_drot"]), t(g["pose_dt"]), t(g["pose_ref_rotation"]),
+                             t(g["pose_ref_translation"]))
+    np.testing.assert_allclose(R1.numpy(), g["pose_R1"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(t1.numpy(), g["pose_t1"], rtol=1e-6, atol=1e-4)
+    pts, valid = orc.lift_points(t(g["pose_depth"]), t(g["pose_internel_k"]),
+                                 t(g["pose_ref_rotation"]), t(g["pose_ref_translation"]))
+    assert valid.any() and (~valid).any()
+    for inv in (0, 400):
+        fl = orc.pose_flow(t(g["pose_R1"]), t(g["pose_t1"]), t(g["pose_internel_k"]), pts, valid,
+                           float(inv))
+        np.testing.assert_allclose(fl.numpy(), g[f"pose_flow_inv{inv}"], rtol=1e-4, atol=2e-3)
+    gt = orc.flow_from_delta_pose_and_depth(t(g["pose_ref_rotation"]), t(g["pose_ref_translation"]),
+                                            t(g["pose_R1"]), t(g["pose_t1"]), t(g["pose_depth"]),
+                                            t(g["pose_internel_k"]))
+    np.testing.assert_allclose(gt.numpy(), g["pose_gtflow"], rtol=1e-4, atol=2e-3)
+
+
+def test_decoder_e2e_matches_reference():
+    """Full SCFlowDecoder forward (B=2, 256², 4 iters): mean EPE ≤ 1e-3 px vs the reference."""
+    g = golden("e2e")
+    B, S, iters, seed = (int(v) for v in g["meta"])
+    from tests.helpers import decoder_inputs
+    inp = decoder_inputs(B, S, seed, g)
+    sd = oracle_state_dict()
+    outs = orc.decoder_forward(sd, **inp, iters=iters)
+    fp, fpred, Rs, ts, masks, drs, dts = outs
+    epe_pose = orc.cal_epe_mean(t(g["flow_pose_last"]), fp[-1])
+    epe_pred = orc.cal_epe_mean(t(g["flow_pred_last"]), fpred[-1])
+    assert float(epe_pose.max()) <= 1e-3, epe_pose
+    assert float(epe_pred.max()) <= 1e-3, epe_pred
+    np.testing.assert_allclose(torch.stack(Rs).numpy(), g["R"], atol=1e-5)
+    np.testing.assert_allclose(torch.stack(ts).numpy(), g["t"], rtol=1e-5, atol=1e-3)
+    np.testing.assert_allclose(torch.stack(drs).numpy(), g["drot"], atol=1e-5)
+    np.testing.assert_allclose(torch.stack(dts).numpy(), g["dt"], atol=1e-5)
+    np.testing.assert_allclose(masks[-1].numpy(), g["mask_last"], atol=1e-5)
+    # the fixture is not degenerate: the pose moves and the flow is non-trivial
+    assert g["flow_pose_absmean"][-1] > 0.05
