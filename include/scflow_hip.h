@@ -1,0 +1,137 @@
+/*
+ * scflow_hip.h — C ABI of the MI355X (gfx950) SCFlow refinement hot path.
+ *
+ * One shared library, libscflow_hip.so (scflow_amd/lib/), built with
+ * `hipcc --offload-arch=gfx950`.  Every entry point:
+ *   - takes plain device pointers (fp32 unless stated), sizes and a hipStream_t passed as void*;
+ *   - enqueues work on that stream and returns immediately (no host sync, no allocation, so
+ *     callers may capture the calls into a hipGraph);
+ *   - returns 0 on success, a negative SCFLOW_E* code for an argument/shape error (nothing
+ *     launched), or a positive hipError_t if the launch failed;
+ *   - is stateless and re-entrant (one process per GPU is the intended deployment).
+ * The caller owns every buffer.  Tensors are contiguous unless a stride argument says otherwise.
+ *
+ * Reference interfaces replaced (GiaKhangLuu/SCFlow, /root/reference):
+ *   scflow_corr_pyramid      <- CorrelationPyramid.forward      models/decoder/raft_decoder.py:35-58
+ *   scflow_corr_lookup       <- CorrLookup.forward              models/utils/corr_lookup.py:102-136
+ *   scflow_conv2d (+ GRU epilogues) <- ConvGRU.forward          models/decoder/raft_decoder.py:235-253
+ *                               and the ConvModule convs of MotionEncoder / XHead / the decoder's
+ *                               delta-flow and mask encoders (raft_decoder.py:152-166, 256-294;
+ *                               scflow_decoder.py:103-124)
+ *   scflow_pose_update       <- get_pose_from_delta_pose (ortho6d, exp)  models/utils/pose.py:124-169
+ *   scflow_lift_points       <- cal_3d_2d_corr / lift_2d_to_3d            models/utils/pose.py:26-64
+ *   scflow_pose_flow         <- get_flow_from_delta_pose_and_points       models/utils/pose.py:66-88
+ *   scflow_pose_update_flow  <- the two calls above fused, as used at     scflow_decoder.py:231-244
+ *   scflow_flow_downsample   <- 1/8·F.interpolate(flow, 1/8, bilinear, align_corners=True)  scflow_decoder.py:197-198
+ *   scflow_flow_upsample     <- 8·F.interpolate(flow+Δflow, ×8) and mask ×8 (same)          scflow_decoder.py:223-228
+ *   scflow_transpose         <- layout plumbing (NCHW <-> channels-last slices), no reference equivalent
+ */
+#ifndef SCFLOW_HIP_H
+#define SCFLOW_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCFLOW_OK 0
+#define SCFLOW_EINVAL (-1)      /* null pointer / non-positive size / bad enum */
+#define SCFLOW_EUNSUPPORTED (-2) /* valid call, but a shape this build has no kernel for */
+#define SCFLOW_EALIGN (-3)      /* pointer or stride not 16-byte aligned where float4 access is used */
+
+#define SCFLOW_ACT_NONE 0
+#define SCFLOW_ACT_RELU 1
+#define SCFLOW_ACT_SIGMOID 2
+#define SCFLOW_ACT_TANH 3
+
+#define SCFLOW_EPI_PLAIN 0  /* out = act(conv + bias) */
+#define SCFLOW_EPI_GRU_ZR 1 /* cout = 2·hc: z = σ(.) -> gate[:, :hc];  r = σ(.), rh = r·h -> rh   */
+#define SCFLOW_EPI_GRU_Q 2  /* cout = hc:   q = tanh(.);  hid <- (1-z)·hid + z·q  (z from gate)     */
+
+#define SCFLOW_LAYOUT_NCHW 0 /* [N][C][H][W] */
+#define SCFLOW_LAYOUT_NHWC 1 /* [N][H][W][stride], channels contiguous */
+
+int scflow_version(void);
+const char* scflow_strerror(int code);
+
+/* a1: all-pairs correlation volume and its average-pooled pyramid.
+ * f1, f2: [n][c][h][w] (render, real).  pyr: one buffer holding the levels back to back;
+ * level l is [n·h·w][h>>l][w>>l] (AvgPool2d(2,2) floors), starting at float offset
+ * n·h·w·Σ_{j<l}(h>>j)(w>>j).  level0 = (f1ᵀ f2)/sqrt(c).  num_levels in [1, 8]. */
+long long scflow_corr_pyramid_size(int n, int h, int w, int num_levels);
+int scflow_corr_pyramid(const float* f1, const float* f2, float* pyr, int n, int c, int h, int w,
+                        int num_levels, void* stream);
+
+/* a2: multi-scale (2r+1)² bilinear window lookup, align_corners=True, zero padding.
+ * flow: [n][2][h][w] (flow_layout NCHW) or [n·h·w][2] (NHWC).  out channel
+ * k = lvl·(2r+1)² + a·(2r+1) + b samples x+Δx=a−r, y+Δy=b−r.  out: NCHW [n][L(2r+1)²][h][w]
+ * or NHWC with pixel stride out_stride (>= L(2r+1)²). */
+int scflow_corr_lookup(const float* pyr, const float* flow, int flow_layout, float* out,
+                       int out_layout, int out_stride, int n, int h, int w, int num_levels,
+                       int radius, void* stream);
+
+/* Channels-last convolution (cross-correlation, like nn.Conv2d) with fused bias/activation and
+ * optional ConvGRU gate epilogues.  Input channels = c0 (src0) ++ c1 (src1, may be 0).
+ * Weights must be packed by scflow_conv_pack_weights for the same shape. */
+typedef struct scflow_conv_args {
+  const float* src0; int c0; int s0;     /* first input, channels, pixel stride (floats)      */
+  const float* src1; int c1; int s1;     /* optional second input concatenated on channels     */
+  const float* weight;                   /* packed, see scflow_conv_pack_weights               */
+  const float* bias;                     /* [cout] or NULL                                     */
+  float* out; int so;                    /* output (channel 0 of this conv), pixel stride      */
+  int n, h, w;                           /* input batch and spatial size                       */
+  int cout, kh, kw, ph, pw, stride;      /* output channels, kernel, padding, stride           */
+  int act;                               /* SCFLOW_ACT_*                                       */
+  int epilogue;                          /* SCFLOW_EPI_*                                       */
+  float* gate; int sg;                   /* GRU z buffer and its pixel stride                  */
+  float* rh; int srh;                    /* GRU_ZR: r·h output                                 */
+  float* hid; int sh;                    /* GRU: hidden state (read by ZR, updated by Q)       */
+} scflow_conv_args;
+
+/* Number of floats of the packed weight buffer; w_oihw is nn.Conv2d's [cout][c0+c1][kh][kw]. */
+long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, int kw, int stride, int w);
+int scflow_conv_pack_weights(const float* w_oihw, float* packed, int cout, int c0, int c1, int kh,
+                             int kw, int stride, int w, void* stream);
+int scflow_conv2d(const scflow_conv_args* args, void* stream);
+
+/* a8: R_dst = R(ortho6d Δ)·R_src; t_z' = t_z/exp(Δt_z) (depth_transform 0) or t_z·(Δt_z+1) (1);
+ * t_xy' = t_z'·(Δt_xy/weight + t_xy/t_z).  drot6 [n][6], dt [n][3], R [n][3][3], t [n][3]. */
+int scflow_pose_update(const float* drot6, const float* dt, const float* R_src, const float* t_src,
+                       float* R_dst, float* t_dst, int n, float weight, int depth_transform,
+                       void* stream);
+
+/* a9: object-frame point of every pixel: points[n][y][x] = {R⁻¹(K⁻¹[x·d,y·d,d] − t), valid},
+ * valid = (depth>0) ? 1 : 0, float4 per pixel. */
+int scflow_lift_points(const float* depth, const float* K, const float* R, const float* t,
+                       float* points, int n, int h, int w, void* stream);
+
+/* a10: flow[n][2][h][w] = proj(K(R·P+t)) − (x,y) where valid, else invalid_num. */
+int scflow_pose_flow(const float* R, const float* t, const float* K, const float* points,
+                     float* flow, int n, int h, int w, float invalid_num, void* stream);
+
+/* a8+a10 fused (one launch per refinement iteration). */
+int scflow_pose_update_flow(const float* drot6, const float* dt, const float* R_src,
+                            const float* t_src, const float* K, const float* points, float* R_dst,
+                            float* t_dst, float* flow, int n, int h, int w, float weight,
+                            int depth_transform, float invalid_num, void* stream);
+
+/* a11 down: out = value_scale · bilinear(flow[n][2][H][W] -> h×w, align_corners=True) written
+ * channels-last to out0 (pixel stride s0) and, if out1 != NULL, also to out1 (stride s1). */
+int scflow_flow_downsample(const float* flow, float* out0, int s0, float* out1, int s1, int n,
+                           int H, int W, int h, int w, float value_scale, void* stream);
+
+/* a11 up: flow_out[n][2][H][W] = value_scale·bilinear(lr + delta) and mask_out[n][1][H][W] =
+ * bilinear(mask); lr/delta are channels-last [n·h·w][2] (delta may be NULL), mask [n·h·w][1]
+ * (may be NULL, then mask_out is not written). */
+int scflow_flow_upsample(const float* lr, const float* delta, const float* mask, float* flow_out,
+                         float* mask_out, int n, int h, int w, int H, int W, float value_scale,
+                         void* stream);
+
+/* out[n·ons + b·obs + a] = in[n·ins + a·ias + b] for a < A, b < B (batched 2-D transpose; e.g.
+ * NCHW -> a channel slice of an NHWC buffer, or back). */
+int scflow_transpose(const float* in, float* out, int n, int A, int B, long long ins, int ias,
+                     long long ons, int obs, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCFLOW_HIP_H */

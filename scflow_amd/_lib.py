@@ -1,0 +1,91 @@
+"""ctypes binding of libscflow_hip.so (the C ABI declared in include/scflow_hip.h).
+
+The library is loaded AFTER torch, so its ``libamdhip64.so.7`` dependency resolves to the HIP
+runtime torch already loaded (same SONAME): one HIP runtime per process, and the ``hipStream_t``
+handles torch hands out are valid here.  There is no fallback: if the library is missing the
+product path raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library is loaded)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libscflow_hip.so")
+
+c_int, c_float, c_ll, c_vp = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ctypes.c_void_p
+
+SCFLOW_ACT = {None: 0, "ReLU": 1, "Sigmoid": 2, "Tanh": 3}
+EPI_PLAIN, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2
+LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
+
+
+class ConvArgs(ctypes.Structure):
+    """Mirror of ``scflow_conv_args`` (include/scflow_hip.h)."""
+    _fields_ = [
+        ("src0", c_vp), ("c0", c_int), ("s0", c_int),
+        ("src1", c_vp), ("c1", c_int), ("s1", c_int),
+        ("weight", c_vp), ("bias", c_vp),
+        ("out", c_vp), ("so", c_int),
+        ("n", c_int), ("h", c_int), ("w", c_int),
+        ("cout", c_int), ("kh", c_int), ("kw", c_int), ("ph", c_int), ("pw", c_int), ("stride", c_int),
+        ("act", c_int), ("epilogue", c_int),
+        ("gate", c_vp), ("sg", c_int),
+        ("rh", c_vp), ("srh", c_int),
+        ("hid", c_vp), ("sh", c_int),
+    ]
+
+
+# name -> (restype, argtypes); every function the header declares
+SIGNATURES = {
+    "scflow_version": (c_int, []),
+    "scflow_strerror": (ctypes.c_char_p, [c_int]),
+    "scflow_corr_pyramid_size": (c_ll, [c_int, c_int, c_int, c_int]),
+    "scflow_corr_pyramid": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_corr_lookup": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                   c_int, c_vp]),
+    "scflow_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "scflow_conv_pack_weights": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                         c_vp]),
+    "scflow_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_vp]),
+    "scflow_pose_update": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp]),
+    "scflow_lift_points": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_pose_flow": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp]),
+    "scflow_pose_update_flow": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                        c_int, c_int, c_float, c_int, c_float, c_vp]),
+    "scflow_flow_downsample": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                       c_int, c_float, c_vp]),
+    "scflow_flow_upsample": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                     c_float, c_vp]),
+    "scflow_transpose": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_int, c_ll, c_int, c_vp]),
+}
+
+_lib = None
+
+
+class ScflowError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise ScflowError(
+                f"HIP library not found at {path}: build it with `python -m scflow_amd.build` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        msg = load().scflow_strerror(code)
+        raise ScflowError(f"{what} failed with code {code}: {msg.decode() if msg else '?'}")

@@ -1,0 +1,31 @@
+// Shared helpers for the gfx950 SCFlow kernels.  Wave64, CDNA4 only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/scflow_hip.h"
+
+#define SCFLOW_API extern "C" __attribute__((visibility("default")))
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+static inline int scflow_launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? SCFLOW_OK : (int)e;
+}
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+static inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+__device__ __forceinline__ float act_apply(float v, int act) {
+  switch (act) {
+    case SCFLOW_ACT_RELU: return v > 0.f ? v : 0.f;
+    case SCFLOW_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    case SCFLOW_ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }

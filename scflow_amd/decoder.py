@@ -1,0 +1,240 @@
+"""SCFlowDecoder — drop-in replacement for the reference decoder, running on gfx950 HIP kernels.
+
+Reference: ``/root/reference/models/decoder/scflow_decoder.py:19-252``.  Same constructor
+kwargs (:48-68), same submodules and state-dict keys (so reference checkpoints load), same
+``forward`` signature (:151-156) and the same 7-list return (:252).  ``iters`` is re-read on
+every call (the refiner overwrites it temporarily, ``scflow_refiner.py:150-158``).
+
+Forward, per call (B pairs, features h×w = image/8, M = B·h·w):
+
+* a1  ``scflow_corr_pyramid``: correlation GEMM (fp32 MFMA) + pooled levels, once;
+* a9  ``scflow_lift_points``: dense per-pixel object-frame points, once (no ``nonzero``, no
+  host sync);
+* then ``iters`` times, with every activation channels-last in a handful of buffers
+  (``HX = [h | cxt | motion | flow]`` is exactly the GRU's ``cat[h, x]``):
+  a11↓ downsample → a2 lookup → a3 motion encoder (5 convs) → a4 GRU (4 launches: z/r fused,
+  q with the state update fused) → a5 heads (hidden convs of both heads in one launch, thin
+  predictors) → a6 Δflow/mask encoders → a7 pose head (PyTorch-ROCm) → a11↑ upsample →
+  a8+a10 pose update + reprojection (one launch).
+
+No host synchronisation happens inside ``forward``; the whole call can be captured into a
+HIP graph (``graph.py``).  There is no CPU path: inputs must be on a ROCm device.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Sequence, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import ScflowError
+from .modules import (ConvGRU, ConvModule, ConvRunner, CorrelationPyramid, CorrLookup,
+                      MotionEncoder, XHead, run_chain)
+from .ops import Chan
+from .registry import MODELS
+
+Tensor = torch.Tensor
+
+
+@MODELS.register_module()
+class SCFlowDecoder(nn.Module):
+    _h_channels = {"Basic": 128, "Small": 96}
+    _cxt_channels = {"Basic": 128, "Small": 64}
+
+    def __init__(self, net_type: str, num_levels: int, radius: int, iters: int, detach_flow: bool,
+                 detach_mask: bool, detach_pose: bool, mask_flow: bool, mask_corr: bool,
+                 pose_head_cfg: dict, depth_transform: str = "exp", detach_depth_for_xy: bool = False,
+                 corr_lookup_cfg: dict = dict(align_corners=True), gru_type: str = "SeqConv",
+                 feat_channels: Union[int, Sequence[int]] = 256, conv_cfg: Optional[dict] = None,
+                 norm_cfg: Optional[dict] = None, act_cfg: Optional[dict] = None) -> None:
+        super().__init__()
+        assert net_type in ["Basic", "Small"]
+        assert type(feat_channels) in (int, tuple, list)
+        self.corr_block = CorrelationPyramid(num_levels=num_levels)
+        feat_channels = list(feat_channels) if isinstance(feat_channels, (tuple, list)) else [feat_channels]
+        self.net_type = net_type
+        self.num_levels = num_levels
+        self.radius = radius
+        self.detach_flow = detach_flow
+        self.detach_mask = detach_mask
+        self.detach_pose = detach_pose
+        self.detach_depth_for_xy = detach_depth_for_xy
+        self.mask_flow = mask_flow
+        self.mask_corr = mask_corr
+        self.depth_transform = depth_transform
+        self.h_channels = self._h_channels.get(net_type)
+        self.cxt_channels = self._cxt_channels.get(net_type)
+        self.iters = iters
+        corr_lookup_cfg = dict(corr_lookup_cfg)
+        corr_lookup_cfg["radius"] = radius
+        self.corr_lookup = CorrLookup(**corr_lookup_cfg)
+        self.encoder = MotionEncoder(num_levels=num_levels, radius=radius, net_type=net_type,
+                                     conv_cfg=conv_cfg, norm_cfg=norm_cfg, act_cfg=act_cfg)
+        self.gru_type = gru_type
+        self.gru = ConvGRU(self.h_channels, self.encoder.out_channels[0] + 2 + self.cxt_channels,
+                           net_type=gru_type)
+        self.pose_pred = MODELS.build(pose_head_cfg)
+        self.flow_pred = XHead(self.h_channels, feat_channels, 2, x="flow")
+        self.mask_pred = XHead(self.h_channels, feat_channels, 1, x="mask")
+        mk = dict(conv_cfg=conv_cfg, norm_cfg=norm_cfg, act_cfg=act_cfg)
+        self.delta_flow_encoder = nn.Sequential(
+            ConvModule(2, 128, 7, padding=3, **mk), ConvModule(128, 64, 3, padding=1, **mk))
+        self.mask_encoder = nn.Sequential(
+            ConvModule(1, 64, 3, padding=1, **mk), ConvModule(64, 32, 3, padding=1, **mk))
+        self._head_runner = None
+        # optional per-kernel timing hooks (bench.py): name -> callable(start: bool)
+        self.kernel_hooks: Dict[str, object] = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _hidden_heads(self):
+        """Both XHeads' first hidden conv as one launch when they have the same shape."""
+        fl, ml = self.flow_pred.layers, self.mask_pred.layers
+        if len(fl) == 1 and len(ml) == 1 and fl[0].conv.kernel_size == ml[0].conv.kernel_size \
+                and fl[0].conv.padding == ml[0].conv.padding:
+            if self._head_runner is None:
+                self._head_runner = ConvRunner([fl[0].conv, ml[0].conv], "ReLU")
+            return self._head_runner
+        return None
+
+    def _hook(self, name: str, start: bool) -> None:
+        h = self.kernel_hooks.get(name)
+        if h is not None:
+            h(start)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, feat_render: Tensor, feat_real: Tensor, h_feat: Tensor, cxt_feat: Tensor,
+                ref_rotation: Tensor, ref_translation: Tensor, depth: Tensor, internel_k: Tensor,
+                label: Tensor, init_flow: Tensor, invalid_flow_num: float):
+        if feat_render.device.type != "cuda":
+            raise ScflowError("SCFlowDecoder runs on the gfx950 HIP kernels only; move inputs to a "
+                              "ROCm device (there is no CPU fallback)")
+        with torch.no_grad():
+            return self._forward(feat_render, feat_real, h_feat, cxt_feat, ref_rotation,
+                                 ref_translation, depth, internel_k, label, init_flow,
+                                 float(invalid_flow_num))
+
+    def _forward(self, feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label, init_flow,
+                 invalid):
+        dev = feat_render.device
+        f32 = torch.float32
+        feat_render = feat_render.contiguous().float()
+        feat_real = feat_real.contiguous().float()
+        N, C, h, w = feat_render.shape
+        _, H, W = depth.shape
+        scale = 2 ** (self.num_levels - 1)
+        M = N * h * w
+        hc, xc = self.h_channels, self.cxt_channels
+        co = self.encoder.out_channels[0]
+        hx_c = hc + xc + co + 2
+        iters = int(self.iters)
+
+        # a1 + a9 (once per forward)
+        pyr, _ = ops.corr_pyramid(feat_render, feat_real, self.num_levels)
+        depth = depth.contiguous().float()
+        K = K.contiguous().float()
+        R_prev = R0.contiguous().float()
+        t_prev = t0.contiguous().float()
+        points = ops.lift_points(depth, K, R_prev, t_prev)
+
+        # channels-last working set
+        HX = torch.empty(M, hx_c, device=dev, dtype=f32)
+        ops.nchw_into(h_feat.contiguous().float(), Chan(HX, 0, hc))
+        ops.nchw_into(cxt_feat.contiguous().float(), Chan(HX, hc, xc))
+        F2 = torch.empty(M, 2, device=dev, dtype=f32)
+        K_look = self.num_levels * (2 * self.radius + 1) ** 2
+        CORR = torch.empty(M, K_look, device=dev, dtype=f32)
+        cc = self.encoder.corr_net[-1].conv.out_channels
+        cf = self.encoder.flow_net[-1].conv.out_channels
+        MF = torch.empty(M, cc + cf, device=dev, dtype=f32)
+        Z = torch.empty(M, hc, device=dev, dtype=f32)
+        RH = torch.empty(M, hc, device=dev, dtype=f32)
+        fh = self.flow_pred.layers[-1].conv.out_channels
+        mh = self.mask_pred.layers[-1].conv.out_channels
+        HEAD = torch.empty(M, fh + mh, device=dev, dtype=f32)
+        D2 = torch.empty(M, 2, device=dev, dtype=f32)
+        MASK = torch.empty(M, 1, device=dev, dtype=f32)
+        dfc = self.delta_flow_encoder[-1].conv.out_channels
+        mfc = self.mask_encoder[-1].conv.out_channels
+        PH = torch.empty(M, hc + dfc + mfc, device=dev, dtype=f32)
+
+        def scratch(mods):
+            return [torch.empty(M, m.conv.out_channels, device=dev, dtype=f32) for m in mods[:-1]]
+
+        s_corr = scratch(self.encoder.corr_net)
+        s_flow = scratch(self.encoder.flow_net)
+        s_out = scratch(self.encoder.out_net)
+        s_dfe = scratch(self.delta_flow_encoder)
+        s_me = scratch(self.mask_encoder)
+
+        # outputs (stacked; the lists returned are views)
+        o_flow_pose = torch.empty(iters, N, 2, H, W, device=dev, dtype=f32)
+        o_flow_pred = torch.empty(iters, N, 2, H, W, device=dev, dtype=f32)
+        o_mask = torch.empty(iters, N, 1, H, W, device=dev, dtype=f32)
+        o_R = torch.empty(iters, N, 3, 3, device=dev, dtype=f32)
+        o_t = torch.empty(iters, N, 3, device=dev, dtype=f32)
+        drots, dts = [], []
+
+        head_runner = self._hidden_heads()
+        flow_pred_r = ConvRunner.of(self.flow_pred.predict_layer, None)
+        mask_pred_r = ConvRunner.of(self.mask_pred.predict_layer, "Sigmoid")
+        label = label.to(dev).long()
+        mask_lr = None
+        if self.mask_corr or self.mask_flow:
+            mask_lr = torch.ones(M, 1, device=dev, dtype=f32)  # interpolate(ones, 1/8) == ones
+        flow_full = init_flow.contiguous().float()
+        hx_flow = Chan(HX, hx_c - 2, 2)
+        hx_motion = Chan(HX, hc + xc, co)
+        hid = Chan(HX, 0, hc)
+
+        for it in range(iters):
+            # a11 ↓: flow at feature resolution → F2 (and the motion-feature flow channels)
+            ops.flow_downsample(flow_full, Chan.whole(F2), h, w, 1.0 / scale,
+                                out1=None if self.mask_flow else hx_flow)
+            # a2
+            ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
+                            flow_layout="nhwc")
+            if self.mask_corr:
+                CORR.mul_(mask_lr)
+            flow_in = F2
+            if self.mask_flow:
+                flow_in = F2 * mask_lr
+                HX[:, hx_c - 2:].copy_(flow_in)
+            # a3 motion encoder → HX[hc+xc : hc+xc+co]
+            run_chain(self.encoder.corr_net, Chan.whole(CORR), Chan(MF, 0, cc), N, h, w, s_corr)
+            run_chain(self.encoder.flow_net, Chan.whole(flow_in), Chan(MF, cc, cf), N, h, w, s_flow)
+            run_chain(self.encoder.out_net, Chan.whole(MF), hx_motion, N, h, w, s_out)
+            # a4 GRU (in place on HX[:, :hc])
+            self.gru.step(Chan.whole(HX), Chan.whole(Z), Chan.whole(RH), N, h, w,
+                          hooks=self.kernel_hooks)
+            # a5 heads
+            if head_runner is not None:
+                head_runner.run(hid, Chan.whole(HEAD), N, h, w)
+            else:
+                run_chain(self.flow_pred.layers, hid, Chan(HEAD, 0, fh), N, h, w)
+                run_chain(self.mask_pred.layers, hid, Chan(HEAD, fh, mh), N, h, w)
+            flow_pred_r.run(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w)
+            mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MASK), N, h, w)
+            if mask_lr is not None:
+                mask_lr = MASK
+            # a6 Δflow / mask encoders → PH[hc:]
+            run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(PH, hc, dfc), N, h, w, s_dfe)
+            run_chain(self.mask_encoder, Chan.whole(MASK), Chan(PH, hc + dfc, mfc), N, h, w, s_me)
+            PH[:, :hc].copy_(HX[:, :hc])
+            # a7 pose head (stock PyTorch-ROCm), input cat[h, Δflow feat, mask feat] NCHW view
+            ph_in = PH.view(N, h, w, -1).permute(0, 3, 1, 2)
+            drot, dtr = self.pose_pred(ph_in, label)
+            drot = drot.contiguous().float()
+            dtr = dtr.contiguous().float()
+            # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
+            ops.flow_upsample(F2, D2, MASK, N, h, w, H, W, float(scale), o_flow_pred[it], o_mask[it])
+            # a8 + a10: pose update + pose-induced flow (one launch)
+            ops.pose_update_flow(drot, dtr, R_prev, t_prev, K, points, o_R[it], o_t[it],
+                                 o_flow_pose[it], invalid, depth_transform=self.depth_transform)
+            R_prev, t_prev = o_R[it], o_t[it]
+            flow_full = o_flow_pose[it]
+            drots.append(drot)
+            dts.append(dtr)
+
+        return (list(o_flow_pose.unbind(0)), list(o_flow_pred.unbind(0)), list(o_R.unbind(0)),
+                list(o_t.unbind(0)), list(o_mask.unbind(0)), drots, dts)

@@ -1,0 +1,435 @@
+"""Drop-in modules of SCFlow's update block, backed by the gfx950 HIP kernels.
+
+Same class names, constructor arguments, forward signatures and state-dict keys as the
+reference, so configs, checkpoints and callers work unchanged:
+
+=====================  =====================================================================
+module                 reference
+=====================  =====================================================================
+ConvModule             mmcv ConvModule (conv → norm → act; ``bias = norm is None``)
+CorrelationPyramid     models/decoder/raft_decoder.py:19-58
+CorrLookup             models/utils/corr_lookup.py:71-136
+MotionEncoder          models/decoder/raft_decoder.py:61-166
+ConvGRU                models/decoder/raft_decoder.py:168-253
+XHead                  models/decoder/raft_decoder.py:256-294
+MultiClassPoseHead     models/head/pose_head.py:110-211
+=====================  =====================================================================
+
+The NCHW ``forward`` of each module is the reference API (it converts to channels-last,
+runs the HIP kernels, converts back).  ``SCFlowDecoder`` (decoder.py) does not go through
+these per-module forwards: it keeps every activation channels-last in a few shared buffers
+and calls the kernels directly (``ConvRunner``), so no NCHW round trips happen in the loop.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple, Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from ._lib import EPI_GRU_Q, EPI_GRU_ZR, EPI_PLAIN
+from .ops import Chan
+from .registry import MODELS
+
+Tensor = torch.Tensor
+
+
+def _pair(v) -> Tuple[int, int]:
+    return (v, v) if isinstance(v, int) else (int(v[0]), int(v[1]))
+
+
+class ConvModule(nn.Module):
+    """mmcv ``ConvModule`` as SCFlow uses it: conv (+GroupNorm) (+act), key layout
+    ``conv.weight``/``conv.bias``/``gn.weight``/``gn.bias``; ``act_cfg=None`` → identity."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size, stride=1, padding=0,
+                 conv_cfg: Optional[dict] = None, norm_cfg: Optional[dict] = None,
+                 act_cfg: Optional[dict] = dict(type="ReLU"), **kwargs):
+        super().__init__()
+        if conv_cfg is not None and conv_cfg.get("type", "Conv2d") != "Conv2d":
+            raise NotImplementedError(f"conv_cfg {conv_cfg} is not supported")
+        self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride=stride, padding=padding,
+                              bias=norm_cfg is None)
+        self.norm_type = None
+        if norm_cfg is not None:
+            if norm_cfg["type"] != "GN":
+                raise NotImplementedError(f"norm {norm_cfg['type']} is not on the SCFlow decoder path")
+            self.norm_type = "GN"
+            self.gn = nn.GroupNorm(norm_cfg["num_groups"], out_channels)
+        self.act_type = None if act_cfg is None else act_cfg["type"]
+        if self.act_type not in (None, "ReLU", "Sigmoid", "Tanh"):
+            raise NotImplementedError(f"activation {self.act_type}")
+
+    @property
+    def kernel_size(self) -> Tuple[int, int]:
+        return _pair(self.conv.kernel_size)
+
+    @property
+    def padding(self) -> Tuple[int, int]:
+        return _pair(self.conv.padding)
+
+    def forward_torch(self, x: Tensor) -> Tensor:
+        """Stock PyTorch-ROCm path (MIOpen conv + GN) — used only by the pose head."""
+        y = self.conv(x)
+        if self.norm_type == "GN":
+            y = self.gn(y)
+        if self.act_type == "ReLU":
+            y = torch.relu(y)
+        elif self.act_type == "Sigmoid":
+            y = torch.sigmoid(y)
+        elif self.act_type == "Tanh":
+            y = torch.tanh(y)
+        return y
+
+    def forward(self, x: Tensor) -> Tensor:
+        if self.norm_type is not None or self.conv.stride != (1, 1):
+            return self.forward_torch(x)
+        n, c, h, w = x.shape
+        r = ConvRunner.of(self.conv, self.act_type)
+        src = torch.empty(n * h * w, c, device=x.device)
+        ops.nchw_into(x.contiguous(), Chan.whole(src))
+        dst = torch.empty(n * h * w, self.conv.out_channels, device=x.device)
+        r.run(Chan.whole(src), Chan.whole(dst), n, h, w)
+        return ops.chan_to_nchw(Chan.whole(dst), n, h, w)
+
+
+class ConvRunner:
+    """Packs one (or several cout-concatenated) nn.Conv2d weights for scflow_conv2d and runs it.
+
+    The packed copy is cached and re-packed whenever a weight's data pointer or version
+    changes (optimizer step, load_state_dict, .to())."""
+
+    def __init__(self, convs: Sequence[nn.Conv2d], act: Optional[str], split: Optional[int] = None):
+        self.convs = list(convs)
+        c0 = self.convs[0]
+        self.kh, self.kw = _pair(c0.kernel_size)
+        self.ph, self.pw = _pair(c0.padding)
+        self.stride = _pair(c0.stride)[0]
+        self.cout = sum(c.out_channels for c in self.convs)
+        self.cin = c0.in_channels
+        self.act = act
+        self.split = split
+        self._key = None
+        self._packed = None
+        self._bias = None
+
+    @staticmethod
+    def of(conv: nn.Conv2d, act: Optional[str]) -> "ConvRunner":
+        r = getattr(conv, "_scflow_runner", None)
+        if r is None or r.act != act:
+            r = ConvRunner([conv], act)
+            conv._scflow_runner = r
+        return r
+
+    def packed(self, c0: int, c1: int, w: int) -> Tuple[Tensor, Optional[Tensor]]:
+        key = (c0, c1, w) + tuple((c.weight.data_ptr(), c.weight._version,
+                                   None if c.bias is None else (c.bias.data_ptr(), c.bias._version))
+                                  for c in self.convs)
+        if key != self._key:
+            wt = torch.cat([c.weight.detach() for c in self.convs], 0) if len(self.convs) > 1 \
+                else self.convs[0].weight.detach()
+            self._packed = ops.pack_conv_weight(wt.float(), c0, c1, w, self.stride)
+            if all(c.bias is not None for c in self.convs):
+                self._bias = torch.cat([c.bias.detach().float() for c in self.convs]).contiguous()
+            elif any(c.bias is not None for c in self.convs):
+                raise ValueError("cannot fuse convs with and without bias")
+            else:
+                self._bias = None
+            self._key = key
+        return self._packed, self._bias
+
+    def run(self, src0: Chan, out: Optional[Chan], n: int, h: int, w: int,
+            src1: Optional[Chan] = None, epilogue: int = EPI_PLAIN, gate: Optional[Chan] = None,
+            rh: Optional[Chan] = None, hid: Optional[Chan] = None) -> None:
+        c1 = 0 if src1 is None else src1.c
+        if src0.c + c1 != self.cin:
+            raise ValueError(f"conv expects {self.cin} input channels, got {src0.c}+{c1}")
+        packed, bias = self.packed(src0.c, c1, w)
+        ops.conv2d(src0, packed, bias, n, h, w, self.cout, self.kh, self.kw, self.ph, self.pw,
+                   self.act, out=out, src1=src1, epilogue=epilogue, gate=gate, rh=rh, hid=hid,
+                   stride=self.stride)
+
+
+# ---------------------------------------------------------------------------------- a1 / a2
+class CorrelationPyramid(nn.Module):
+    """raft_decoder.py:19-58; returns the levels as views of one HIP-built buffer."""
+
+    def __init__(self, num_levels: int = 4) -> None:
+        super().__init__()
+        self.num_levels = num_levels
+
+    def forward(self, feat1: Tensor, feat2: Tensor) -> List[Tensor]:
+        _, levels = ops.corr_pyramid(feat1.contiguous(), feat2.contiguous(), self.num_levels)
+        return levels
+
+
+class CorrLookup(nn.Module):
+    """corr_lookup.py:71-136.  Only the configuration SCFlow uses exists as a kernel:
+    bilinear, zero padding, align_corners=True."""
+
+    def __init__(self, radius: int = 4, mode: str = "bilinear", padding_mode: str = "zeros",
+                 align_corners: bool = True) -> None:
+        super().__init__()
+        if mode != "bilinear" or padding_mode != "zeros" or not align_corners:
+            raise NotImplementedError("CorrLookup kernel: bilinear / zeros / align_corners=True only")
+        self.r = radius
+        self.mode = mode
+        self.padding_mode = padding_mode
+        self.align_corners = align_corners
+
+    def forward(self, corr_pyramid: Sequence[Tensor], flow: Tensor) -> Tensor:
+        B, _, H, W = flow.shape
+        buf = ops.pyramid_buffer(corr_pyramid, B, H, W)
+        return ops.corr_lookup(buf, flow.contiguous().float(), B, H, W, len(corr_pyramid), self.r)
+
+
+# ---------------------------------------------------------------------------------- a3
+class MotionEncoder(nn.Module):
+    """raft_decoder.py:61-166 (same channel tables)."""
+    _corr_channels = {"Basic": (256, 192), "Small": 96, "Large": (256, 192)}
+    _corr_kernel = {"Basic": (1, 3), "Small": 1, "Large": (1, 3)}
+    _corr_padding = {"Basic": (0, 1), "Small": 0, "Large": (0, 1)}
+    _flow_channels = {"Basic": (128, 64), "Small": (64, 32), "Large": (128, 64)}
+    _flow_kernel = {"Basic": (7, 3), "Small": (7, 3), "Large": (7, 3)}
+    _flow_padding = {"Basic": (3, 1), "Small": (3, 1), "Large": (3, 1)}
+    _out_channels = {"Basic": 126, "Small": 80, "Large": 126}
+    _out_kernel = {"Basic": 3, "Small": 3, "Large": 3}
+    _out_padding = {"Basic": 1, "Small": 1, "Large": 1}
+
+    def __init__(self, num_levels: int = 4, radius: int = 4, net_type: str = "Basic",
+                 conv_cfg=None, norm_cfg=None, act_cfg=None, **kwargs) -> None:
+        super().__init__()
+        assert net_type in ["Basic", "Small", "Large"]
+
+        def lst(v):
+            return list(v) if isinstance(v, (tuple, list)) else [v]
+
+        corr_ch, corr_k, corr_p = (lst(self._corr_channels[net_type]), lst(self._corr_kernel[net_type]),
+                                   lst(self._corr_padding[net_type]))
+        self.out_channels = lst(self._out_channels[net_type])
+        self.act_cfg = act_cfg
+        mk = dict(conv_cfg=conv_cfg, norm_cfg=norm_cfg, act_cfg=act_cfg)
+        self.corr_net = nn.Sequential(*self._make(num_levels * (2 * radius + 1) ** 2, corr_ch, corr_k,
+                                                  corr_p, mk))
+        self.flow_net = nn.Sequential(*self._make(2, lst(self._flow_channels[net_type]),
+                                                  lst(self._flow_kernel[net_type]),
+                                                  lst(self._flow_padding[net_type]), mk))
+        self.out_net = nn.Sequential(*self._make(corr_ch[-1] + lst(self._flow_channels[net_type])[-1],
+                                                 self.out_channels, lst(self._out_kernel[net_type]),
+                                                 lst(self._out_padding[net_type]), mk))
+
+    @staticmethod
+    def _make(cin, chans, kernels, pads, mk):
+        layers = []
+        for ch, k, p in zip(chans, kernels, pads):
+            layers.append(ConvModule(cin, ch, k, padding=p, **mk))
+            cin = ch
+        return layers
+
+    def forward(self, corr: Tensor, flow: Tensor) -> Tensor:
+        n, _, h, w = corr.shape
+        dev = corr.device
+        M = n * h * w
+        cc = self.corr_net[-1].conv.out_channels
+        cf = self.flow_net[-1].conv.out_channels
+        co = self.out_channels[0]
+        cbuf = torch.empty(M, corr.shape[1], device=dev)
+        ops.nchw_into(corr.contiguous(), Chan.whole(cbuf))
+        fbuf = torch.empty(M, 2, device=dev)
+        ops.nchw_into(flow.contiguous(), Chan.whole(fbuf))
+        mf = torch.empty(M, cc + cf, device=dev)
+        run_chain(self.corr_net, Chan.whole(cbuf), Chan(mf, 0, cc), n, h, w)
+        run_chain(self.flow_net, Chan.whole(fbuf), Chan(mf, cc, cf), n, h, w)
+        out = torch.empty(M, co + 2, device=dev)
+        run_chain(self.out_net, Chan.whole(mf), Chan(out, 0, co), n, h, w)
+        out[:, co:].copy_(fbuf)
+        return ops.chan_to_nchw(Chan.whole(out), n, h, w)
+
+
+def run_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int, w: int,
+              scratch: Optional[List[Tensor]] = None) -> None:
+    """Run a Sequential of stride-1 ConvModules channels-last; the last one writes ``dst``."""
+    cur = src
+    for i, m in enumerate(layers):
+        r = ConvRunner.of(m.conv, m.act_type)
+        if i == len(layers) - 1:
+            out = dst
+        else:
+            buf = scratch[i] if scratch is not None else torch.empty(n * h * w, m.conv.out_channels,
+                                                                      device=src.buf.device)
+            out = Chan.whole(buf)
+        r.run(cur, out, n, h, w)
+        cur = out
+
+
+# ---------------------------------------------------------------------------------- a4
+class ConvGRU(nn.Module):
+    """raft_decoder.py:168-253.  z and r share one conv launch (cout = 2·h_channels) whose
+    epilogue writes z and r·h; the q launch's epilogue applies h ← (1−z)h + z·tanh(q)."""
+    _kernel = {"Conv": 3, "SeqConv": ((1, 5), (5, 1))}
+    _padding = {"Conv": 1, "SeqConv": ((0, 2), (2, 0))}
+
+    def __init__(self, h_channels: int, x_channels: int, net_type: str = "SeqConv") -> None:
+        super().__init__()
+        assert net_type in ["Conv", "SeqConv"]
+        ks = self._kernel[net_type] if isinstance(self._kernel[net_type], (tuple, list)) \
+            else [self._kernel[net_type]]
+        ps = self._padding[net_type] if isinstance(self._padding[net_type], (tuple, list)) \
+            else [self._padding[net_type]]
+        cz, cr, cq = [], [], []
+        for k, p in zip(ks, ps):
+            for lst_, act in ((cz, "Sigmoid"), (cr, "Sigmoid"), (cq, "Tanh")):
+                lst_.append(ConvModule(h_channels + x_channels, h_channels, k, padding=p,
+                                       act_cfg=dict(type=act)))
+        self.conv_z = nn.ModuleList(cz)
+        self.conv_r = nn.ModuleList(cr)
+        self.conv_q = nn.ModuleList(cq)
+        self.h_channels = h_channels
+        self.x_channels = x_channels
+        self._runners = None
+
+    def init_weights(self) -> None:
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.orthogonal_(m.weight)
+
+    def runners(self):
+        if self._runners is None:
+            self._runners = [(ConvRunner([z.conv, r.conv], "Sigmoid"), ConvRunner([q.conv], "Tanh"))
+                             for z, r, q in zip(self.conv_z, self.conv_r, self.conv_q)]
+        return self._runners
+
+    def step(self, hx: Chan, z: Chan, rh: Chan, n: int, h: int, w: int, hooks=None) -> None:
+        """In-place GRU update of channels [0, hc) of ``hx`` (= cat[h, x] channels-last).
+
+        ``hooks`` (optional dict name -> callable(start)) brackets the z|r and q launches."""
+        hc = self.h_channels
+        hid = Chan(hx.buf, hx.off, hc)
+        x = Chan(hx.buf, hx.off + hc, hx.c - hc)
+        hzr = hooks.get("gru_zr") if hooks else None
+        hq = hooks.get("gru_q") if hooks else None
+        for rzr, rq in self.runners():
+            if hzr:
+                hzr(True)
+            rzr.run(hx, None, n, h, w, epilogue=EPI_GRU_ZR, gate=z, rh=rh, hid=hid)
+            if hzr:
+                hzr(False)
+            if hq:
+                hq(True)
+            rq.run(rh, None, n, h, w, src1=x, epilogue=EPI_GRU_Q, gate=z, hid=hid)
+            if hq:
+                hq(False)
+
+    def forward(self, h: Tensor, x: Tensor) -> Tensor:
+        n, hc, hh, ww = h.shape
+        xc = x.shape[1]
+        dev = h.device
+        M = n * hh * ww
+        hx = torch.empty(M, hc + xc, device=dev)
+        ops.nchw_into(h.contiguous(), Chan(hx, 0, hc))
+        ops.nchw_into(x.contiguous(), Chan(hx, hc, xc))
+        z = torch.empty(M, hc, device=dev)
+        rh = torch.empty(M, hc, device=dev)
+        self.step(Chan.whole(hx), Chan.whole(z), Chan.whole(rh), n, hh, ww)
+        return ops.chan_to_nchw(Chan(hx, 0, hc), n, hh, ww)
+
+
+# ---------------------------------------------------------------------------------- a5
+class XHead(nn.Module):
+    """raft_decoder.py:256-294."""
+
+    def __init__(self, in_channels: int, feat_channels: Sequence[int], x_channels: int, x: str) -> None:
+        super().__init__()
+        layers = []
+        for ch in feat_channels:
+            layers.append(ConvModule(in_channels, ch, 3, padding=1))
+            in_channels = ch
+        self.layers = nn.Sequential(*layers)
+        if x in ("flow", "tradeoff"):
+            self.predict_layer = nn.Conv2d(feat_channels[-1], x_channels, kernel_size=3, padding=1)
+        elif x == "mask":
+            self.predict_layer = nn.Conv2d(feat_channels[-1], x_channels, kernel_size=1, padding=0)
+        else:
+            raise ValueError(f"x must be 'flow' or 'mask', but got {x}")
+        self.x = x
+
+    def forward(self, x: Tensor) -> Tensor:
+        n, c, h, w = x.shape
+        src = torch.empty(n * h * w, c, device=x.device)
+        ops.nchw_into(x.contiguous(), Chan.whole(src))
+        hid = torch.empty(n * h * w, self.layers[-1].conv.out_channels, device=x.device)
+        run_chain(self.layers, Chan.whole(src), Chan.whole(hid), n, h, w)
+        out = torch.empty(n * h * w, self.predict_layer.out_channels, device=x.device)
+        ConvRunner.of(self.predict_layer, None).run(Chan.whole(hid), Chan.whole(out), n, h, w)
+        return ops.chan_to_nchw(Chan.whole(out), n, h, w)
+
+
+# ---------------------------------------------------------------------------------- a7
+@MODELS.register_module()
+class MultiClassPoseHead(nn.Module):
+    """pose_head.py:110-211.  Stride-2 conv + GroupNorm + FC stack run on stock PyTorch-ROCm
+    (MIOpen / hipBLASLt): 0.16 GFLOP per pair-iteration, 2.5% of the step."""
+    _conv_feat_channels = {"Basic": [128, 128, 128], "Large": [128, 128, 128]}
+    _conv_strides = {"Basic": [2, 2, 2], "Large": [2, 2, 2]}
+    _conv_paddings = {"Basic": [1, 1, 1], "Large": [1, 1, 1]}
+    _conv_kernel_sizes = {"Basic": [3, 3, 3], "Large": [3, 3, 3]}
+    _fc_feat_channels = {"Basic": [1024, 256], "Large": [1024, 256]}
+    _feat_size = {"Basic": (32, 32), "Large": (64, 64)}
+
+    def __init__(self, num_class: int, in_channels: int, net_type: str, norm_cfg: dict,
+                 act_cfg: dict, feat_size: tuple = None, rotation_mode: str = "quaternion",
+                 init_cfg=None):
+        super().__init__()
+        self.num_class = num_class
+        assert net_type in ["Basic", "Small", "Large"]
+        if feat_size is None:
+            feat_size = self._feat_size.get(net_type)
+        conv_layers = []
+        conv_out_size = feat_size[0] * feat_size[1]
+        for ch, k, s, p in zip(self._conv_feat_channels[net_type], self._conv_kernel_sizes[net_type],
+                               self._conv_strides[net_type], self._conv_paddings[net_type]):
+            conv_layers.append(ConvModule(in_channels, ch, k, stride=s, padding=p, norm_cfg=norm_cfg,
+                                          act_cfg=act_cfg))
+            in_channels = ch
+            conv_out_size = int(conv_out_size / (s ** 2))
+        self.conv_layers = nn.Sequential(*conv_layers)
+        fc_in = in_channels * conv_out_size
+        fcs = []
+        for ch in self._fc_feat_channels[net_type]:
+            fcs.append(nn.Sequential(nn.Linear(fc_in, ch), nn.ReLU()))
+            fc_in = ch
+        self.flatten_op = nn.Flatten(start_dim=1, end_dim=-1)
+        self.fc_layers = nn.Sequential(*fcs)
+        if rotation_mode == "quaternion":
+            self.rotation_out_channels = 4
+        elif rotation_mode == "ortho6d":
+            self.rotation_out_channels = 6
+        else:
+            raise RuntimeError(f"Not supported rotation mode:{rotation_mode}")
+        self.rotation_mode = rotation_mode
+        self.rotation_pred = nn.Linear(fc_in, self.rotation_out_channels * num_class)
+        self.translation_pred = nn.Linear(fc_in, 3 * num_class)
+        self.init_weights()
+
+    def init_weights(self):
+        nn.init.zeros_(self.translation_pred.weight)
+        nn.init.zeros_(self.translation_pred.bias)
+        nn.init.zeros_(self.rotation_pred.weight)
+        with torch.no_grad():
+            base = [0.0, 0.0, 0.0, 1.0] if self.rotation_mode == "quaternion" else [1.0, 0, 0, 0, 1.0, 0]
+            self.rotation_pred.bias.copy_(torch.tensor(base * self.num_class))
+
+    def forward(self, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
+        for m in self.conv_layers:
+            x = m.forward_torch(x)
+        x = self.flatten_op(x)
+        x = self.fc_layers(x)
+        t = self.translation_pred(x).view(-1, self.num_class, 3)
+        r = self.rotation_pred(x).view(-1, self.num_class, self.rotation_out_channels)
+        # reference quirk kept (pose_head.py:208-209): index_select over ALL labels then [:, 0],
+        # i.e. every sample uses label[0]'s class head
+        t = torch.index_select(t, dim=1, index=label)[:, 0, :]
+        r = torch.index_select(r, dim=1, index=label)[:, 0, :]
+        return r, t

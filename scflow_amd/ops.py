@@ -1,0 +1,275 @@
+"""Tensor-level wrappers over the C ABI (include/scflow_hip.h).
+
+Each wrapper validates devices/dtypes/contiguity, passes raw device pointers and the current
+HIP stream of the tensor's device, and raises ``ScflowError`` on any non-zero status.  Inputs
+must live on a ROCm device: there is deliberately no CPU path here.
+
+Channels-last activations are described by ``Chan`` = (buffer, first channel, channel count):
+the buffer is a contiguous ``[..., C_total]`` tensor, so a ``Chan`` is a channel slice of an
+NHWC image with pixel stride ``C_total`` — how the decoder keeps cat[h, cxt, motion, flow] in
+one buffer without ever materialising a concatenation.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import ScflowError, check
+
+Tensor = torch.Tensor
+
+
+def _stream(t: Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _require(t: Tensor, name: str, dtype=torch.float32, contiguous=True) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.device.type != "cuda":
+        raise ScflowError(f"{name} is on {t.device}: the SCFlow HIP path only runs on a ROCm GPU "
+                          "(no CPU fallback)")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if contiguous and not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _p(t: Optional[Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+@dataclass
+class Chan:
+    """A channel slice [off, off+c) of a contiguous channels-last buffer ``buf[..., C_total]``."""
+    buf: Tensor
+    off: int
+    c: int
+
+    @property
+    def stride(self) -> int:
+        return self.buf.shape[-1]
+
+    @property
+    def ptr(self) -> int:
+        return self.buf.data_ptr() + 4 * self.off
+
+    @staticmethod
+    def whole(buf: Tensor) -> "Chan":
+        return Chan(buf, 0, buf.shape[-1])
+
+
+# ------------------------------------------------------------------------------- a1 pyramid
+def pyramid_level_shapes(h: int, w: int, num_levels: int) -> List[Tuple[int, int]]:
+    return [(h >> l, w >> l) for l in range(num_levels)]
+
+
+def corr_pyramid(feat1: Tensor, feat2: Tensor, num_levels: int = 4) -> Tuple[Tensor, List[Tensor]]:
+    """Returns (one flat buffer, list of level views ``[N·H·W,1,H_l,W_l]``) — the reference's
+    CorrelationPyramid output (raft_decoder.py:35-58) as views of one allocation."""
+    _require(feat1, "feat1")
+    _require(feat2, "feat2")
+    if feat1.shape != feat2.shape or feat1.dim() != 4:
+        raise ValueError(f"feature shapes differ or are not 4-D: {feat1.shape} {feat2.shape}")
+    n, c, h, w = feat1.shape
+    lib = _lib.load()
+    size = lib.scflow_corr_pyramid_size(n, h, w, num_levels)
+    if size <= 0:
+        raise ScflowError(f"bad pyramid geometry n={n} h={h} w={w} L={num_levels}")
+    buf = torch.empty(size, device=feat1.device, dtype=torch.float32)
+    check(lib.scflow_corr_pyramid(_p(feat1), _p(feat2), _p(buf), n, c, h, w, num_levels,
+                                  _stream(feat1)), "scflow_corr_pyramid")
+    return buf, pyramid_views(buf, n, h, w, num_levels)
+
+
+def pyramid_views(buf: Tensor, n: int, h: int, w: int, num_levels: int) -> List[Tensor]:
+    views, off, P = [], 0, h * w
+    for hl, wl in pyramid_level_shapes(h, w, num_levels):
+        views.append(buf[off: off + n * P * hl * wl].view(n * P, 1, hl, wl))
+        off += n * P * hl * wl
+    return views
+
+
+def pyramid_buffer(levels: Sequence[Tensor], n: int, h: int, w: int) -> Tensor:
+    """The flat buffer behind ``levels``; copies on device if they are not views of one."""
+    L = len(levels)
+    base = levels[0]
+    if base.device.type == "cuda" and base.dtype == torch.float32:
+        st = base.untyped_storage()
+        ok = all(lv.is_contiguous() and lv.untyped_storage().data_ptr() == st.data_ptr()
+                 for lv in levels)
+        if ok:
+            sizes = [n * h * w * hl * wl for hl, wl in pyramid_level_shapes(h, w, L)]
+            off0 = base.storage_offset()
+            offs = [off0 + sum(sizes[:i]) for i in range(L)]
+            if all(lv.storage_offset() == o for lv, o in zip(levels, offs)):
+                total = sum(sizes)
+                return torch.as_strided(base, (total,), (1,), off0)
+    for i, lv in enumerate(levels):
+        _require(lv, f"pyramid level {i}", contiguous=False)
+    return torch.cat([lv.reshape(-1) for lv in levels])
+
+
+# ------------------------------------------------------------------------------- a2 lookup
+def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: int, radius: int,
+                out: Optional[Chan] = None, flow_layout: str = "nchw") -> Tensor:
+    """Window lookup.  ``out=None`` → NCHW ``[n, L(2r+1)², h, w]`` (the reference's layout,
+    corr_lookup.py:135-136); otherwise written channels-last into ``out``."""
+    _require(pyr, "pyramid")
+    _require(flow, "flow")
+    K = num_levels * (2 * radius + 1) ** 2
+    lay = _lib.LAYOUT_NCHW if flow_layout == "nchw" else _lib.LAYOUT_NHWC
+    if out is None:
+        res = torch.empty(n, K, h, w, device=flow.device, dtype=torch.float32)
+        ptr, olay, ostride = res.data_ptr(), _lib.LAYOUT_NCHW, K
+    else:
+        res = out.buf
+        ptr, olay, ostride = out.ptr, _lib.LAYOUT_NHWC, out.stride
+    check(_lib.load().scflow_corr_lookup(_p(pyr), _p(flow), lay, ptr, olay, ostride, n, h, w,
+                                         num_levels, radius, _stream(flow)), "scflow_corr_lookup")
+    return res
+
+
+# ------------------------------------------------------------------------------- convolutions
+def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1) -> Tensor:
+    """Pack an nn.Conv2d weight ``[cout, c0+c1, kh, kw]`` for scflow_conv2d."""
+    _require(weight, "conv weight", contiguous=False)
+    weight = weight.detach().contiguous()
+    cout, cin, kh, kw = weight.shape
+    if cin != c0 + c1:
+        raise ValueError(f"weight has {cin} input channels, expected {c0}+{c1}")
+    lib = _lib.load()
+    size = lib.scflow_conv_packed_size(cout, c0, c1, kh, kw, stride, w)
+    if size < 0:
+        raise ScflowError(f"no conv kernel for cout={cout} cin={c0}+{c1} k={kh}x{kw} w={w}")
+    packed = torch.empty(size, device=weight.device, dtype=torch.float32)
+    check(lib.scflow_conv_pack_weights(_p(weight), _p(packed), cout, c0, c1, kh, kw, stride, w,
+                                       _stream(weight)), "scflow_conv_pack_weights")
+    return packed
+
+
+def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int, cout: int,
+           kh: int, kw: int, ph: int, pw: int, act: Optional[str] = None, out: Optional[Chan] = None,
+           src1: Optional[Chan] = None, epilogue: int = _lib.EPI_PLAIN, gate: Optional[Chan] = None,
+           rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1) -> None:
+    for nm, ch in (("src0", src0), ("src1", src1), ("out", out), ("gate", gate), ("rh", rh),
+                   ("hid", hid)):
+        if ch is not None:
+            _require(ch.buf, nm)
+    _require(packed, "packed weight")
+    if bias is not None:
+        _require(bias, "bias")
+    a = _lib.ConvArgs()
+    a.src0, a.c0, a.s0 = src0.ptr, src0.c, src0.stride
+    if src1 is not None:
+        a.src1, a.c1, a.s1 = src1.ptr, src1.c, src1.stride
+    a.weight = packed.data_ptr()
+    a.bias = None if bias is None else bias.data_ptr()
+    if out is not None:
+        a.out, a.so = out.ptr, out.stride
+    a.n, a.h, a.w = n, h, w
+    a.cout, a.kh, a.kw, a.ph, a.pw, a.stride = cout, kh, kw, ph, pw, stride
+    a.act = _lib.SCFLOW_ACT[act]
+    a.epilogue = epilogue
+    if gate is not None:
+        a.gate, a.sg = gate.ptr, gate.stride
+    if rh is not None:
+        a.rh, a.srh = rh.ptr, rh.stride
+    if hid is not None:
+        a.hid, a.sh = hid.ptr, hid.stride
+    check(_lib.load().scflow_conv2d(ctypes.byref(a), _stream(src0.buf)), "scflow_conv2d")
+
+
+# ------------------------------------------------------------------------------- pose
+def lift_points(depth: Tensor, K: Tensor, R: Tensor, t: Tensor) -> Tensor:
+    """[N,H,W,4] float32: object-frame point + validity (pose.py:26-64, dense)."""
+    for nm, x in (("depth", depth), ("K", K), ("R", R), ("t", t)):
+        _require(x, nm)
+    n, h, w = depth.shape
+    pts = torch.empty(n, h, w, 4, device=depth.device, dtype=torch.float32)
+    check(_lib.load().scflow_lift_points(_p(depth), _p(K), _p(R), _p(t), _p(pts), n, h, w,
+                                         _stream(depth)), "scflow_lift_points")
+    return pts
+
+
+def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 10.0,
+                depth_transform: str = "exp") -> Tuple[Tensor, Tensor]:
+    for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t)):
+        _require(x, nm)
+    if drot.shape[1] != 6:
+        raise NotImplementedError("only ortho6d delta rotations are on the SCFlow path")
+    n = drot.shape[0]
+    Ro, to = torch.empty_like(R), torch.empty_like(t)
+    check(_lib.load().scflow_pose_update(_p(drot), _p(dt), _p(R), _p(t), _p(Ro), _p(to), n,
+                                         float(weight), 0 if depth_transform == "exp" else 1,
+                                         _stream(drot)), "scflow_pose_update")
+    return Ro, to
+
+
+def pose_flow(R: Tensor, t: Tensor, K: Tensor, points: Tensor, invalid_num: float,
+              out: Optional[Tensor] = None) -> Tensor:
+    for nm, x in (("R", R), ("t", t), ("K", K), ("points", points)):
+        _require(x, nm)
+    n, h, w, _ = points.shape
+    flow = out if out is not None else torch.empty(n, 2, h, w, device=R.device, dtype=torch.float32)
+    check(_lib.load().scflow_pose_flow(_p(R), _p(t), _p(K), _p(points), _p(flow), n, h, w,
+                                       float(invalid_num), _stream(R)), "scflow_pose_flow")
+    return flow
+
+
+def pose_update_flow(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points: Tensor,
+                     R_out: Tensor, t_out: Tensor, flow_out: Tensor, invalid_num: float,
+                     weight: float = 10.0, depth_transform: str = "exp") -> None:
+    for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t), ("K", K), ("points", points),
+                  ("R_out", R_out), ("t_out", t_out), ("flow_out", flow_out)):
+        _require(x, nm)
+    n, h, w, _ = points.shape
+    check(_lib.load().scflow_pose_update_flow(
+        _p(drot), _p(dt), _p(R), _p(t), _p(K), _p(points), _p(R_out), _p(t_out), _p(flow_out), n, h,
+        w, float(weight), 0 if depth_transform == "exp" else 1, float(invalid_num), _stream(drot)),
+        "scflow_pose_update_flow")
+
+
+# ------------------------------------------------------------------------------- resampling
+def flow_downsample(flow: Tensor, out0: Chan, h: int, w: int, value_scale: float,
+                    out1: Optional[Chan] = None) -> None:
+    _require(flow, "flow")
+    n, _, H, W = flow.shape
+    check(_lib.load().scflow_flow_downsample(
+        _p(flow), out0.ptr, out0.stride, None if out1 is None else out1.ptr,
+        0 if out1 is None else out1.stride, n, H, W, h, w, float(value_scale), _stream(flow)),
+        "scflow_flow_downsample")
+
+
+def flow_upsample(lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], n: int, h: int,
+                  w: int, H: int, W: int, value_scale: float, flow_out: Tensor,
+                  mask_out: Optional[Tensor]) -> None:
+    _require(lr, "lr flow")
+    check(_lib.load().scflow_flow_upsample(_p(lr), _p(delta), _p(mask), _p(flow_out), _p(mask_out),
+                                           n, h, w, H, W, float(value_scale), _stream(lr)),
+          "scflow_flow_upsample")
+
+
+# ------------------------------------------------------------------------------- layout
+def nchw_into(x: Tensor, dst: Chan) -> None:
+    """x [N,C,H,W] → channels [off, off+C) of channels-last ``dst.buf`` ([N,H,W,Ct] or [NHW,Ct])."""
+    _require(x, "x")
+    n, c, h, w = x.shape
+    if c != dst.c:
+        raise ValueError(f"channel mismatch {c} vs {dst.c}")
+    st = dst.stride
+    check(_lib.load().scflow_transpose(_p(x), dst.ptr, n, c, h * w, c * h * w, h * w,
+                                       h * w * st, st, _stream(x)), "scflow_transpose")
+
+
+def chan_to_nchw(src: Chan, n: int, h: int, w: int, out: Optional[Tensor] = None) -> Tensor:
+    res = out if out is not None else torch.empty(n, src.c, h, w, device=src.buf.device,
+                                                   dtype=torch.float32)
+    st = src.stride
+    check(_lib.load().scflow_transpose(src.ptr, _p(res), n, h * w, src.c, h * w * st, st,
+                                       src.c * h * w, h * w, _stream(src.buf)), "scflow_transpose")
+    return res

@@ -1,0 +1,51 @@
+"""CPU: the drop-in boundary — registry, constructor kwargs, state-dict keys/shapes."""
+import pytest
+import torch
+
+from tests.helpers import golden, reference_state_shapes
+
+
+def test_registry_builds_by_class_and_by_name():
+    from scflow_amd import MODELS
+    from scflow_amd.decoder import SCFlowDecoder
+    from tests.test_gpu_decoder import decoder_cfg
+    a = MODELS.build(dict(type=SCFlowDecoder, **decoder_cfg()))
+    b = MODELS.build(dict(type="SCFlowDecoder", **decoder_cfg()))
+    assert type(a) is type(b) is SCFlowDecoder
+    assert a.h_channels == 128 and a.cxt_channels == 128 and a.iters == 4
+    with pytest.raises(KeyError):
+        MODELS.build(dict(type="NoSuchDecoder"))
+
+
+def test_state_dict_keys_and_shapes_match_reference():
+    """Reference checkpoints load unchanged: identical keys and shapes."""
+    from tests.test_gpu_decoder import build_decoder
+    dec = build_decoder(4)
+    ours = {k: tuple(v.shape) for k, v in dec.state_dict().items()}
+    ref = dict(reference_state_shapes())
+    assert set(ours) == set(ref)
+    for k in ref:
+        assert ours[k] == ref[k], k
+    assert sum(v.numel() for v in dec.state_dict().values()) == 6_041_630
+
+
+def test_load_state_dict_strict_roundtrip():
+    from tests.test_gpu_decoder import build_decoder
+    a = build_decoder(4, seed=0)
+    b = build_decoder(4, seed=1)
+    b.load_state_dict(a.state_dict(), strict=True)
+    for (k, x), (_, y) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(x, y), k
+
+
+def test_module_surface_matches_reference():
+    from scflow_amd.modules import ConvGRU, CorrLookup, CorrelationPyramid, MotionEncoder, XHead
+    assert CorrLookup(radius=4).r == 4
+    with pytest.raises(NotImplementedError):
+        CorrLookup(radius=4, align_corners=False)
+    assert CorrelationPyramid(num_levels=4).num_levels == 4
+    me = MotionEncoder(num_levels=4, radius=4, net_type="Basic", act_cfg=dict(type="ReLU"))
+    assert me.out_channels == [126]
+    gru = ConvGRU(128, 256, "SeqConv")
+    assert len(gru.conv_z) == 2 and gru.conv_z[0].conv.kernel_size == (1, 5)
+    assert XHead(128, [256], 2, x="flow").predict_layer.kernel_size == (3, 3)

@@ -1,0 +1,111 @@
+"""GPU parity of the whole SCFlowDecoder forward (the drop-in boundary) vs the reference.
+
+Bar (BASELINE.json north_star): flow endpoint error within 1e-3 px of the reference, fp32.
+* golden fixture produced by the reference itself (B=2, 256², 4 iterations);
+* the CPU oracle (pinned to the reference) at B=4 / 8 iterations and at 512² (pose head
+  feat_size=(64,64));
+* poses: rotations within 1e-5, translations within 1e-3 mm.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import decoder_inputs, golden, t
+
+orc = pytest.importorskip("oracle.scflow_oracle")
+
+EPE_TOL = 1e-3  # px, mean EPE per sample (cal_epe 'mean', models/utils/flow.py:64-78)
+
+
+def decoder_cfg(iters=4, feat_size=None):
+    """The decoder block of configs/refine_models/scflow_ycbv_real.py:207-230."""
+    from scflow_amd.modules import MultiClassPoseHead
+    head = dict(type=MultiClassPoseHead, num_class=21, in_channels=224, net_type="Basic",
+                rotation_mode="ortho6d", norm_cfg=dict(type="GN", num_groups=32, requires_grad=True),
+                act_cfg=dict(type="ReLU"))
+    if feat_size is not None:
+        head["feat_size"] = feat_size
+    return dict(net_type="Basic", num_levels=4, radius=4, iters=iters, detach_flow=True,
+                detach_mask=True, detach_pose=True, detach_depth_for_xy=True, mask_flow=False,
+                mask_corr=False, pose_head_cfg=head, corr_lookup_cfg=dict(align_corners=True),
+                gru_type="SeqConv", act_cfg=dict(type="ReLU"))
+
+
+def build_decoder(iters=4, feat_size=None, seed=0):
+    from scflow_amd import MODELS, synthetic
+    from scflow_amd.decoder import SCFlowDecoder
+    dec = MODELS.build(dict(type="SCFlowDecoder", **decoder_cfg(iters, feat_size)))
+    assert isinstance(dec, SCFlowDecoder)
+    synthetic.fill_module_(dec, seed=seed)
+    return dec.eval()
+
+
+def run_gpu(dec, inp):
+    gi = {k: v.cuda() for k, v in inp.items()}
+    out = dec.cuda()(**gi, invalid_flow_num=0.0)
+    torch.cuda.synchronize()
+    return [[x.cpu() for x in lst] for lst in out]
+
+
+def check_against(out, ref_flow_pose, ref_flow_pred, ref_R=None, ref_t=None):
+    epe_pose = orc.cal_epe_mean(ref_flow_pose, out[0][-1])
+    epe_pred = orc.cal_epe_mean(ref_flow_pred, out[1][-1])
+    assert float(epe_pose.max()) <= EPE_TOL, f"pose-flow EPE {epe_pose}"
+    assert float(epe_pred.max()) <= EPE_TOL, f"pred-flow EPE {epe_pred}"
+    if ref_R is not None:
+        np.testing.assert_allclose(torch.stack(out[2]).numpy(), ref_R, atol=1e-5)
+        np.testing.assert_allclose(torch.stack(out[3]).numpy(), ref_t, rtol=1e-6, atol=1e-3)
+    return float(epe_pose.max()), float(epe_pred.max())
+
+
+@pytest.mark.gpu
+def test_decoder_matches_reference_golden():
+    g = golden("e2e")
+    B, S, iters, seed = (int(v) for v in g["meta"])
+    inp = decoder_inputs(B, S, seed, g)
+    out = run_gpu(build_decoder(iters), inp)
+    assert len(out) == 7 and all(len(l) == iters for l in out)
+    check_against(out, t(g["flow_pose_last"]), t(g["flow_pred_last"]), g["R"], g["t"])
+    np.testing.assert_allclose(torch.stack(out[5]).numpy(), g["drot"], atol=1e-5)
+    np.testing.assert_allclose(torch.stack(out[6]).numpy(), g["dt"], atol=1e-5)
+    np.testing.assert_allclose(out[4][-1].numpy(), g["mask_last"], atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_decoder_matches_oracle_b4_8iters():
+    inp = decoder_inputs(4, 256, seed=21)
+    dec = build_decoder(8, seed=1)
+    out = run_gpu(dec, inp)
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    ref = orc.decoder_forward(sd, **inp, iters=8)
+    check_against(out, ref[0][-1], ref[1][-1], torch.stack(ref[2]).numpy(), torch.stack(ref[3]).numpy())
+    # every iteration, not just the last
+    for i in range(8):
+        assert float(orc.cal_epe_mean(ref[0][i], out[0][i]).max()) <= EPE_TOL
+
+
+@pytest.mark.gpu
+def test_decoder_512_feat64():
+    inp = decoder_inputs(1, 512, seed=5)
+    dec = build_decoder(2, feat_size=(64, 64), seed=2)
+    out = run_gpu(dec, inp)
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    ref = orc.decoder_forward(sd, **inp, iters=2)
+    check_against(out, ref[0][-1], ref[1][-1])
+
+
+@pytest.mark.gpu
+def test_decoder_iters_attribute_is_reread():
+    inp = decoder_inputs(1, 256, seed=2)
+    dec = build_decoder(4)
+    dec.iters = 2
+    out = run_gpu(dec, inp)
+    assert all(len(l) == 2 for l in out)
+
+
+def test_decoder_rejects_cpu_inputs():
+    from scflow_amd._lib import ScflowError
+    inp = decoder_inputs(1, 64, seed=2)
+    dec = build_decoder(1)
+    with pytest.raises(ScflowError):
+        dec(**inp, invalid_flow_num=0.0)

@@ -1,0 +1,240 @@
+"""GPU parity: every C-ABI kernel against the CPU oracle / a plain fp32 PyTorch reference.
+
+Tolerances (fp32 throughout):
+* corr pyramid: |Δ| ≤ 2e-5·(1+|ref|) — a K=C fp32 dot product, different summation order;
+* lookup: |Δ| ≤ 1e-5 (+ golden fixture from the reference itself);
+* convolutions: |Δ| ≤ 2e-5·sqrt(K) relative to the output scale (fp32, K-long sums);
+* pose / resampling: ≤ 1e-4 px (float32 projective division).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests.helpers import golden, t
+
+pytestmark = pytest.mark.gpu
+
+orc = pytest.importorskip("oracle.scflow_oracle")
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from scflow_amd import ops as o
+    return o
+
+
+def close(a, b, atol, rtol=0.0, what=""):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    err = (a - b).abs()
+    lim = atol + rtol * b.abs()
+    bad = (err > lim)
+    assert not bad.any(), f"{what}: max err {err.max().item():.3e} at {bad.nonzero()[0].tolist()}"
+
+
+# ------------------------------------------------------------------------------ a1
+@pytest.mark.parametrize("shape", [(2, 8, 8, 8), (2, 256, 32, 32), (1, 64, 24, 40), (1, 32, 64, 64)])
+def test_corr_pyramid(ops, shape):
+    g = torch.Generator().manual_seed(1)
+    f1 = torch.randn(*shape, generator=g)
+    f2 = torch.randn(*shape, generator=g)
+    buf, lv = ops.corr_pyramid(f1.cuda(), f2.cuda(), 4)
+    ref = orc.corr_pyramid(f1.double(), f2.double(), 4)
+    for i, (a, b) in enumerate(zip(lv, ref)):
+        close(a, b, 2e-5, 2e-5, f"level {i}")
+
+
+def test_corr_pyramid_golden(ops):
+    gd = golden("ops")
+    _, lv = ops.corr_pyramid(t(gd["pyr_f1"]).cuda(), t(gd["pyr_f2"]).cuda(), 4)
+    for i, a in enumerate(lv):
+        close(a, t(gd[f"pyr_l{i}"]), 1e-5, 1e-5, f"golden level {i}")
+
+
+# ------------------------------------------------------------------------------ a2
+@pytest.mark.parametrize("radius", [4, 1])
+def test_corr_lookup_golden(ops, radius):
+    gd = golden("ops")
+    _, lv = ops.corr_pyramid(t(gd["pyr_f1"]).cuda(), t(gd["pyr_f2"]).cuda(), 4)
+    buf = ops.pyramid_buffer(lv, 2, 8, 8)
+    out = ops.corr_lookup(buf, t(gd["lk_flow"]).cuda(), 2, 8, 8, 4, radius)
+    close(out, t(gd[f"lk_r{radius}"]), 2e-5, 2e-5, "lookup vs reference fixture")
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 32, 32), (1, 64, 64), (3, 20, 28)])
+def test_corr_lookup_random(ops, n, h, w):
+    g = torch.Generator().manual_seed(2)
+    f1 = torch.randn(n, 16, h, w, generator=g)
+    f2 = torch.randn(n, 16, h, w, generator=g)
+    flow = (torch.rand(n, 2, h, w, generator=g) - 0.5) * 2 * (h / 2)  # hits every padding case
+    flow[:, :, 0, 0] = torch.tensor([0.5, -0.25])  # exact half-pixel taps
+    buf, lv = ops.corr_pyramid(f1.cuda(), f2.cuda(), 4)
+    ref = orc.corr_lookup([x.cpu() for x in lv], flow, 4)
+    out = ops.corr_lookup(buf, flow.cuda(), n, h, w, 4, 4)
+    close(out, ref, 1e-5, 1e-5, "lookup NCHW")
+    # channels-last variant into a wider buffer at an offset
+    K = 4 * 81
+    wide = torch.full((n * h * w, K + 8), 7.0, device="cuda")
+    nhwc_flow = flow.permute(0, 2, 3, 1).contiguous().cuda()
+    ops.corr_lookup(buf, nhwc_flow, n, h, w, 4, 4, out=ops.Chan(wide, 4, K), flow_layout="nhwc")
+    got = wide[:, 4:4 + K].view(n, h, w, K).permute(0, 3, 1, 2)
+    close(got, ref, 1e-5, 1e-5, "lookup NHWC")
+    assert (wide[:, :4] == 7).all() and (wide[:, 4 + K:] == 7).all()
+
+
+# ------------------------------------------------------------------------------ convs
+def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0):
+    from scflow_amd.modules import ConvRunner
+    g = torch.Generator().manual_seed(seed)
+    x0 = torch.randn(n, c0, h, w, generator=g)
+    x1 = torch.randn(n, c1, h, w, generator=g) if c1 else None
+    conv = torch.nn.Conv2d(c0 + c1, cout, k, padding=pad)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(conv.weight[0].numel()))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+    xin = torch.cat([x0, x1], 1) if c1 else x0
+    ref = F.conv2d(xin.double(), conv.weight.double(), conv.bias.double(), padding=pad)
+    ref = {None: lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Tanh": torch.tanh}[act](ref)
+    convc = conv.cuda()
+    M = n * h * w
+    # inputs as channel slices of wider buffers (exercises pixel strides and offsets)
+    b0 = torch.zeros(M, c0 + 4, device="cuda")
+    ops.nchw_into(x0.cuda(), ops.Chan(b0, 4, c0))
+    src1 = None
+    if c1:
+        b1 = torch.zeros(M, c1 + 8, device="cuda")
+        ops.nchw_into(x1.cuda(), ops.Chan(b1, 8, c1))
+        src1 = ops.Chan(b1, 8, c1)
+    out = torch.full((M, cout + 3), -5.0, device="cuda")
+    ConvRunner([convc], act).run(ops.Chan(b0, 4, c0), ops.Chan(out, 3, cout), n, h, w, src1=src1)
+    got = ops.chan_to_nchw(ops.Chan(out, 3, cout), n, h, w)
+    assert (out[:, :3] == -5).all()
+    return got, ref
+
+
+@pytest.mark.parametrize("case", [
+    # (n, h, w, c0, c1, cout, k, pad, act)          variant
+    (2, 32, 32, 324, 0, 256, 1, 0, "ReLU"),        # mfma 1×1 (corr_net.0, cin not a multiple of 16)
+    (2, 32, 32, 256, 0, 192, 3, 1, "ReLU"),        # mfma 3×3 (corr_net.1)
+    (2, 32, 32, 128, 256, 128, (1, 5), (0, 2), "Tanh"),  # mfma 1×5, two sources (GRU q)
+    (2, 32, 32, 384, 0, 256, (5, 1), (2, 0), "Sigmoid"),  # mfma 5×1 (GRU z|r)
+    (2, 32, 32, 192, 64, 126, 3, 1, "ReLU"),       # mfma, cout not a multiple of 64 (out_net)
+    (2, 32, 32, 64, 0, 32, 3, 1, None),            # mfma, cout 32
+    (1, 64, 64, 128, 0, 64, 3, 1, "ReLU"),         # mfma at the 512² feature size
+    (2, 32, 32, 2, 0, 128, 7, 3, "ReLU"),          # small-cin 7×7
+    (2, 32, 32, 1, 0, 64, 3, 1, "ReLU"),           # small-cin 3×3, 1 channel
+    (2, 32, 32, 256, 0, 2, 3, 1, None),            # thin 3×3 → 2
+    (2, 32, 32, 256, 0, 1, 1, 0, "Sigmoid"),       # thin 1×1 → 1
+])
+def test_conv2d_variants(ops, case):
+    n, h, w, c0, c1, cout, k, pad, act = case
+    got, ref = _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act)
+    kk = (c0 + c1) * (np.prod(k) if isinstance(k, tuple) else k * k)
+    close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"conv {case}")
+
+
+def test_conv_gru_module(ops):
+    """ConvGRU (SeqConv, 128 hidden, 256 input) through the fused z|r and q launches."""
+    from scflow_amd import synthetic
+    from scflow_amd.modules import ConvGRU
+    gru = ConvGRU(128, 256, "SeqConv")
+    synthetic.fill_module_(gru, seed=4)
+    g = torch.Generator().manual_seed(5)
+    h = torch.tanh(torch.randn(2, 128, 32, 32, generator=g))
+    x = torch.randn(2, 256, 32, 32, generator=g)
+    sd = {k: v for k, v in gru.state_dict().items()}
+    ref = orc.conv_gru({k: v.double() for k, v in sd.items()}, h.double(), x.double(), prefix="")
+    out = gru.cuda()(h.cuda(), x.cuda())
+    close(out, ref, 5e-5, 1e-5, "ConvGRU")
+
+
+def test_conv_unsupported_shape_raises(ops):
+    from scflow_amd._lib import ScflowError
+    from scflow_amd.modules import ConvRunner
+    conv = torch.nn.Conv2d(64, 64, 3, padding=1).cuda()
+    b = torch.zeros(1 * 20 * 20, 64, device="cuda")
+    with pytest.raises(ScflowError):
+        ConvRunner([conv], None).run(ops.Chan.whole(b), ops.Chan.whole(b.clone()), 1, 20, 20)
+
+
+# ------------------------------------------------------------------------------ pose / resampling
+def test_pose_golden(ops):
+    gd = golden("ops")
+    R0, t0, K = (t(gd["pose_ref_rotation"]), t(gd["pose_ref_translation"]), t(gd["pose_internel_k"]))
+    depth = t(gd["pose_depth"])
+    Ro, to = ops.pose_update(t(gd["pose_drot"]).cuda(), t(gd["pose_dt"]).cuda(), R0.cuda(), t0.cuda())
+    close(Ro, t(gd["pose_R1"]), 1e-6, 1e-6, "R")
+    close(to, t(gd["pose_t1"]), 1e-4, 1e-6, "t")
+    pts = ops.lift_points(depth.cuda(), K.cuda(), R0.cuda(), t0.cuda())
+    for inv in (0, 400):
+        fl = ops.pose_flow(Ro, to, K.cuda(), pts, float(inv))
+        close(fl, t(gd[f"pose_flow_inv{inv}"]), 2e-3, 1e-4, f"pose flow inv={inv}")
+    # fused update + flow
+    Rf, tf = torch.empty_like(Ro), torch.empty_like(to)
+    flf = torch.empty(3, 2, 64, 64, device="cuda")
+    ops.pose_update_flow(t(gd["pose_drot"]).cuda(), t(gd["pose_dt"]).cuda(), R0.cuda(), t0.cuda(),
+                         K.cuda(), pts, Rf, tf, flf, 400.0)
+    close(Rf, Ro, 0, 0, "fused R")
+    close(flf, t(gd["pose_flow_inv400"]), 2e-3, 1e-4, "fused flow")
+
+
+def test_pose_full_res_vs_oracle(ops):
+    from scflow_amd import synthetic
+    sc = synthetic.make_scene(4, 256, seed=9)
+    R0, t0, K, depth = (t(sc[k]) for k in ("ref_rotation", "ref_translation", "internel_k", "depth"))
+    g = torch.Generator().manual_seed(3)
+    drot = torch.tensor([[1.0, 0, 0, 0, 1.0, 0]]).repeat(4, 1) + 0.03 * torch.randn(4, 6, generator=g)
+    dt = 0.05 * torch.randn(4, 3, generator=g)
+    Rr, tr = orc.pose_update(drot.double(), dt.double(), R0.double(), t0.double())
+    pts_r, valid = orc.lift_points(depth.double(), K.double(), R0.double(), t0.double())
+    ref = orc.pose_flow(Rr, tr, K.double(), pts_r, valid, 0.0)
+    pts = ops.lift_points(depth.cuda(), K.cuda(), R0.cuda(), t0.cuda())
+    Ro, to = torch.empty(4, 3, 3, device="cuda"), torch.empty(4, 3, device="cuda")
+    fl = torch.empty(4, 2, 256, 256, device="cuda")
+    ops.pose_update_flow(drot.cuda(), dt.cuda(), R0.cuda(), t0.cuda(), K.cuda(), pts, Ro, to, fl, 0.0)
+    close(Ro, Rr, 2e-6, 0, "R")
+    close(fl, ref, 5e-3, 1e-5, "flow")
+    assert ((fl.cpu() == 0) == ~valid[:, None].expand(-1, 2, -1, -1)).all()
+
+
+@pytest.mark.parametrize("S,s", [(256, 32), (512, 64), (100, 13)])
+def test_flow_resampling(ops, S, s):
+    g = torch.Generator().manual_seed(4)
+    flow = torch.randn(2, 2, S, S, generator=g) * 5
+    F2 = torch.empty(2 * s * s, 2, device="cuda")
+    wide = torch.zeros(2 * s * s, 10, device="cuda")
+    ops.flow_downsample(flow.cuda(), ops.Chan.whole(F2), s, s, 0.125, out1=ops.Chan(wide, 8, 2))
+    # fp32 reference: ATen computes the align_corners source index (in-1)/(out-1)·dst in fp32 too
+    ref = 0.125 * F.interpolate(flow, size=(s, s), mode="bilinear", align_corners=True)
+    close(F2.view(2, s, s, 2).permute(0, 3, 1, 2), ref, 2e-6, 2e-6, "downsample")
+    close(wide[:, 8:], F2, 0, 0, "downsample second output")
+    if S == 8 * s:  # the decoder's own call form: 1/8 · interpolate(scale_factor=1/8)
+        close(F2.view(2, s, s, 2).permute(0, 3, 1, 2), orc.downsample_flow(flow, 8), 2e-6,
+              2e-6, "downsample (scale form)")
+    delta = torch.randn(2 * s * s, 2, generator=g).cuda()
+    mask = torch.rand(2 * s * s, 1, generator=g).cuda()
+    fo = torch.empty(2, 2, S, S, device="cuda")
+    mo = torch.empty(2, 1, S, S, device="cuda")
+    ops.flow_upsample(F2, delta, mask, 2, s, s, S, S, 8.0, fo, mo)
+    lr = (F2 + delta).view(2, s, s, 2).permute(0, 3, 1, 2).cpu()
+    ref_up = 8 * F.interpolate(lr, size=(S, S), mode="bilinear", align_corners=True)
+    close(fo, ref_up, 2e-5, 2e-6, "upsample flow")
+    ref_m = F.interpolate(mask.view(2, s, s, 1).permute(0, 3, 1, 2).cpu(), size=(S, S),
+                          mode="bilinear", align_corners=True)
+    close(mo, ref_m, 1e-6, 1e-6, "upsample mask")
+
+
+def test_transpose_roundtrip(ops):
+    x = torch.randn(3, 37, 9, 11, device="cuda")
+    buf = torch.zeros(3 * 9 * 11, 50, device="cuda")
+    ops.nchw_into(x, ops.Chan(buf, 5, 37))
+    back = ops.chan_to_nchw(ops.Chan(buf, 5, 37), 3, 9, 11)
+    close(back, x, 0, 0, "roundtrip")
+    close(buf[:, 5:42].view(3, 9, 11, 37).permute(0, 3, 1, 2), x, 0, 0, "nhwc")
+
+
+def test_cpu_tensor_rejected(ops):
+    from scflow_amd._lib import ScflowError
+    with pytest.raises(ScflowError):
+        ops.corr_pyramid(torch.randn(1, 8, 8, 8), torch.randn(1, 8, 8, 8), 4)
