@@ -1,0 +1,196 @@
+#!/usr/bin/env python
+"""Benchmark: SCFlow refinement iters/s (batch × GRU steps / s) at 256×256 on MI355X.
+
+Workload (BASELINE.json configs[1]): a "step" is one full ``SCFlowDecoder.forward`` over a
+batch of 16 synthetic 256×256 image pairs per GPU with 8 GRU refinement iterations —
+correlation pyramid build, lift, and 8 × (lookup, motion encoder, SepConvGRU, heads, pose
+head, pose update, reprojection, resampling) — fp32 throughout, inputs already in HBM.
+Weak scaling: every rank runs its own 16 pairs (the batch shards with no collective,
+SURVEY.md §8(e)); ``value`` = all pairs·iterations of all ranks ÷ the slowest rank's time.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Extra JSON fields:
+* ``roofline``: the dominant kernel, ``conv_mfma_kernel<GRU_ZR>`` (the fused z|r SepConvGRU
+  convolution: 2 launches per iteration, 16.1 GFLOP each at B=16), timed live with HIP events
+  around each of its launches in the timed region; bound = fp32 MFMA, peak 157.3 TFLOP/s.
+* ``cpu_baseline``: the CPU oracle (oracle/scflow_oracle.py, a parity-pinned PyTorch-CPU
+  restatement of the reference decoder) on a bounded sample, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "refinement iters/s (batch×GRU-steps/s) at 256×256, 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector rate
+
+
+def decoder_cfg(iters, feat_size=None):
+    from scflow_amd.modules import MultiClassPoseHead
+    head = dict(type=MultiClassPoseHead, num_class=21, in_channels=224, net_type="Basic",
+                rotation_mode="ortho6d", norm_cfg=dict(type="GN", num_groups=32, requires_grad=True),
+                act_cfg=dict(type="ReLU"))
+    if feat_size is not None:
+        head["feat_size"] = feat_size
+    # configs/refine_models/scflow_ycbv_real.py:207-230
+    return dict(type="SCFlowDecoder", net_type="Basic", num_levels=4, radius=4, iters=iters,
+                detach_flow=True, detach_mask=True, detach_pose=True, detach_depth_for_xy=True,
+                mask_flow=False, mask_corr=False, pose_head_cfg=head,
+                corr_lookup_cfg=dict(align_corners=True), gru_type="SeqConv",
+                act_cfg=dict(type="ReLU"))
+
+
+def make_inputs(batch, size, seed, device):
+    from scflow_amd import synthetic
+    raw = synthetic.make_decoder_inputs(batch, size, seed=seed)
+    out = {k: torch.from_numpy(v).to(device) for k, v in raw.items()}
+    out["label"] = out.pop("labels")
+    return out
+
+
+def gru_zr_flops(batch, size, hc=128, x_ch=256, taps=5):
+    """Algorithmic FLOPs of one fused z|r launch: 2·M·(2·hc)·(taps·(hc+x))."""
+    m = batch * (size // 8) ** 2
+    return 2.0 * m * (2 * hc) * taps * (hc + x_ch)
+
+
+def cpu_baseline(seconds: float, iters: int, size: int):
+    """Time the CPU oracle on a bounded sample: B=2 pairs, `iters` iterations, repeated."""
+    from oracle import scflow_oracle as orc
+    from scflow_amd import MODELS, synthetic
+    threads = torch.get_num_threads()
+    dec = MODELS.build(decoder_cfg(iters))
+    synthetic.fill_module_(dec)
+    sd = {k: v.detach() for k, v in dec.state_dict().items()}
+    inp = make_inputs(2, size, 100, "cpu")
+    orc.decoder_forward(sd, **inp, iters=1)  # warm up allocator / threads
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        orc.decoder_forward(sd, **inp, iters=iters)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(reps * 2 * iters / el, 3), "unit": "iters/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle decoder (PyTorch CPU fp32), B=2 pairs x {iters} iters at {size}x{size}, "
+                      f"{reps} reps in {el:.1f}s, torch threads={threads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="pairs per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_gru_zr.json"),
+                    help="HBM bytes per launch of the dominant kernel from a rocprofv3 PMC pass")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from scflow_amd import MODELS, synthetic
+    from scflow_amd.profiling import KernelTimer
+
+    feat = (args.size // 8, args.size // 8) if args.size != 256 else None
+    dec = MODELS.build(decoder_cfg(args.iters, feat))
+    synthetic.fill_module_(dec)
+    dec = dec.to(dev).eval()
+    inp = make_inputs(args.batch, args.size, seed=rank, device=dev)
+
+    def step():
+        return dec(**inp, invalid_flow_num=0.0)
+
+    for _ in range(args.warmup):
+        step()
+    timer = KernelTimer()
+    dec.kernel_hooks["gru_zr"] = timer
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    dec.kernel_hooks.clear()
+
+    units = world * args.batch * args.iters * args.steps
+    value = units / elapsed
+    zr_ms = timer.mean_ms()
+    flops = gru_zr_flops(args.batch, args.size)
+    achieved = flops / (zr_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("batch") == args.batch and tj.get("size") == args.size:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded features, YCB-V-like poses/intrinsics, analytic ellipsoid depth; "
+                    "deterministic random-init weights)",
+            "config": {"workload": f"SCFlowDecoder forward, {args.batch} pairs/GPU, "
+                                   f"{args.size}x{args.size}, {args.iters} GRU iters (BASELINE configs[1])",
+                       "global_batch": args.batch * world, "image": args.size, "iters": args.iters,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"kernel": "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r conv)",
+                         "bound": "mfma", "achieved": round(achieved, 2),
+                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "avg_launch_ms": round(zr_ms, 4), "launches": timer.count(),
+                         "flops_per_launch": flops},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.iters, args.size)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,9 +17,19 @@ from typing import Any, Callable, Dict, Optional
 
 
 class Registry:
-    def __init__(self, name: str):
+    def __init__(self, name: str, locations=()):
         self.name = name
         self._modules: Dict[str, type] = {}
+        # like mmengine's ``locations``: modules imported on the first lookup miss
+        self._locations = list(locations)
+        self._imported = False
+
+    def _import_locations(self) -> None:
+        if not self._imported:
+            import importlib
+            self._imported = True
+            for loc in self._locations:
+                importlib.import_module(loc)
 
     def __contains__(self, key: str) -> bool:
         return key in self._modules
@@ -28,6 +38,8 @@ class Registry:
         return f"Registry({self.name}, {sorted(self._modules)})"
 
     def get(self, key: str) -> Optional[type]:
+        if key not in self._modules:
+            self._import_locations()
         return self._modules.get(key)
 
     def register_module(self, name: Optional[str] = None, force: bool = False,
@@ -65,4 +77,4 @@ class Registry:
             target.register_module(name=key, module=cls, force=True)
 
 
-MODELS = Registry("model")
+MODELS = Registry("model", locations=["scflow_amd.modules", "scflow_amd.decoder"])

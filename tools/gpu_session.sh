@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel-trace summary.
+# Stops at the first step that faults / aborts / times out (rc other than 0 or 1 for pytest).
+# usage: tools/gpu_session.sh [tag] [what: all|test|bench|prof]
+TAG=${1:-r01}
+WHAT=${2:-all}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
+
+if [ $WHAT = all ] || [ $WHAT = test ]; then
+  timeout -k 10 600 python -m pytest $R/tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1
+  rc=$?; echo "pytest rc=$rc" | tee -a $OUT/pytest_gpu_$TAG.log
+  ok $rc || exit $rc
+fi
+if [ $WHAT = all ] || [ $WHAT = bench ]; then
+  timeout -k 10 400 python $R/bench.py --steps 10 --warmup 3 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
+  rc=$?; echo "bench rc=$rc"; cat $OUT/bench_$TAG.json
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ $WHAT = all ] || [ $WHAT = prof ]; then
+  cd /tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run -- \
+      python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err
+  rc=$?; echo "rocprof rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+  find $OUT/prof_$TAG -name "*stats*" | head
+fi
