@@ -6,38 +6,51 @@
 //   XHead flow / mask                                  models/decoder/raft_decoder.py:256-294
 //   delta_flow_encoder / mask_encoder                  models/decoder/scflow_decoder.py:103-124
 //
-// Three kernels, chosen by shape (select_variant, shared by packing and launching):
-//  * conv_mfma  — implicit GEMM on v_mfma_f32_32x32x2_f32 (exact fp32, the chip's f32 matrix
+// Three kernel families, chosen by shape (select_variant, shared by packing and launching):
+//
+//  * conv_mfma — implicit GEMM on v_mfma_f32_32x32x2_f32 (exact fp32; gfx950's only f32 matrix
 //    rate).  Workgroup tile = 128 output pixels (128/W whole image rows) × 64 output channels;
-//    4 waves, each 64 px × 32 ch (two 32×32 MFMA accumulators).  Per K-stage (16 input channels
-//    of one source) the workgroup stages the input HALO of its rows once — (rows+kh−1)×(W+kw−1)
-//    pixels — plus the weights of every tap, so each input pixel is fetched once per stage
-//    instead of kh·kw times; all taps then run out of LDS (pixel rows padded to 20 floats:
-//    ds_read_b128 conflict-free).  Second input source = channel concat without a copy
-//    (GRU's cat[h,x] / cat[r·h,x], MotionEncoder's cat[corr,flow]).  Epilogues: bias+act, or the
-//    GRU gates: ZR writes z and r·h; Q computes h ← (1−z)·h + z·tanh(q) in place.
-//  * conv_smallcin — VALU direct conv for cin ≤ 4 (the 7×7 2→128 flow encoders, 3×3 1→64 mask
-//    encoder): one thread per pixel × 16 output channels, weights wave-uniform.
-//  * conv_thin — cout ≤ 4 (flow head 3×3 256→2, mask head 1×1 256→1): one wave per pixel,
-//    lanes split the channels (float4 each), wave reduction; weights staged in LDS.
+//    4 waves, each 64 px × 32 ch (two 32×32 accumulators).  K is walked in stages of 16 input
+//    channels of one source; per stage the workgroup stages the input HALO of its rows once —
+//    (rows+kh−1)×(W+kw−1) pixels — plus the stage's weights for every tap (packed contiguous per
+//    stage, so that is one coalesced block), and all kh·kw taps then run out of LDS (pixel rows
+//    padded to 20 floats: ds_read_b128 conflict-free).  Software pipeline: the next stage's
+//    global loads are issued into registers before this stage's MFMAs and written to LDS after
+//    them, so L2/HBM latency hides under ≥ 2.5k cycles of matrix work.  A second input source
+//    is a channel concat without a copy (GRU cat[h,x] / cat[r·h,x], MotionEncoder cat[c,f]).
+//    Epilogues: bias+act; GRU ZR writes z and r·h; GRU Q computes h ← (1−z)·h + z·tanh(q) in
+//    place (the reference's three ConvModules + elementwise ops in two launches).
+//  * conv_smallcin — cin ≤ 4 (7×7 2→128 flow encoders, 3×3 1→64 mask encoder): one LANE per
+//    output channel with its kh·kw·cin weights in VGPRs, the pixel tile's input halo in LDS and
+//    read as wave-uniform broadcasts; stores are 64 contiguous channels per pixel.
+//  * conv_thin — cout ≤ 4 (flow head 3×3 256→2, mask head 1×1 256→1): one LANE per output
+//    pixel, channels streamed through an LDS halo in chunks of 32, weights wave-uniform.
 #include "common.h"
+
+#include <stdlib.h>
 
 namespace {
 
-constexpr int BM = 128;  // output pixels per workgroup
-constexpr int BN = 64;   // output channels per workgroup
-constexpr int BK = 16;   // input channels per K-stage
+constexpr int BM = 128;  // output pixels per workgroup (mfma)
+constexpr int BN = 64;   // output channels per workgroup (mfma)
+constexpr int BK = 16;   // input channels per K-stage (mfma)
 constexpr int LDA = BK + 4;
+constexpr int THIN_CC = 32;        // channels per LDS chunk (thin)
+constexpr int THIN_LD = THIN_CC + 4;
 
 enum Variant { V_MFMA = 0, V_SMALLCIN = 1, V_THIN = 2, V_NONE = -1 };
 
 struct Geometry {
   int variant;
-  int oh, ow, tr, hr, hc, taps, cp0, cp1, ktot, npad;
+  int oh, ow, tr, hr, hc, taps, cp0, cp1, nst, ktot, npad;
   size_t lds;
 };
 
 int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+bool mfma_shape(int kh, int kw) {
+  return (kh == 1 && kw == 1) || (kh == 3 && kw == 3) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1);
+}
 
 Geometry select_variant(int cout, int c0, int c1, int kh, int kw, int stride, int h, int w, int ph,
                         int pw) {
@@ -51,114 +64,153 @@ Geometry select_variant(int cout, int c0, int c1, int kh, int kw, int stride, in
   if (cin <= 4 && c1 == 0) {
     g.variant = V_SMALLCIN;
     g.ktot = g.taps * cin;
-    g.npad = round_up(cout, 16);
+    g.npad = round_up(cout, 64);
     return g;
   }
   if (cout <= 4) {
-    if (cin % 4 || cin > 1024 || (long long)cout * g.taps * cin * 4 > 64 * 1024) return g;
+    if (cin % 4 || c0 % 4) return g;
     g.variant = V_THIN;
     g.ktot = g.taps * cin;
     g.npad = cout;
     return g;
   }
-  if (c0 % 4 || c1 % 4) return g;
-  if (w != g.ow || (BM % g.ow) != 0 || (g.ow % 32) != 0) return g;  // tile = whole image rows
+  if (c0 % 4 || c1 % 4 || !mfma_shape(kh, kw)) return g;
+  if (w != g.ow || h != g.oh || (g.ow != 32 && g.ow != 64)) return g;  // tile = whole rows
   g.tr = BM / g.ow;
   if (g.oh % g.tr) return g;
   g.hr = g.tr + kh - 1;
   g.hc = g.ow + kw - 1;
   g.cp0 = round_up(c0, BK);
   g.cp1 = round_up(c1, BK);
+  g.nst = (g.cp0 + g.cp1) / BK;
   g.ktot = g.taps * (g.cp0 + g.cp1);
   g.npad = round_up(cout, BN);
   g.lds = sizeof(float) * ((size_t)g.hr * g.hc * LDA + (size_t)g.taps * BN * LDA);
-  if (g.lds > 160 * 1024) return g;
   g.variant = V_MFMA;
   return g;
 }
 
 // ------------------------------------------------------------------------------------------
 // MFMA implicit-GEMM conv
+// packed weights: [npad/BN][nst][taps][BN][BK] — one contiguous block per (n-tile, stage)
 // ------------------------------------------------------------------------------------------
 struct MfmaParams {
   scflow_conv_args a;
-  int oh, ow, tr, hr, hc, taps, cp0, cp1, ktot;
+  int oh, ow, tr, hr, hc, cp0, nst;
 };
 
-template <int EPI>
+// max float4 of the A halo per thread over the supported widths (32, 64)
+constexpr int na_max(int bm, int kh, int kw) {
+  const int a32 = (bm / 32 + kh - 1) * (32 + kw - 1) * (BK / 4);
+  const int a64 = ((bm / 64 > 0 ? bm / 64 : 1) + kh - 1) * (64 + kw - 1) * (BK / 4);
+  const int m = a32 > a64 ? a32 : a64;
+  return (m + 255) / 256;
+}
+
+// TILE_M output pixels × BN channels per workgroup; 4 waves as 2 (M) × 2 (N); each wave owns
+// TILE_M/2 pixels (RB = TILE_M/64 row blocks of 32) × 32 channels.
+template <int EPI, int KH, int KW, int TILE_M>
 __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
+  constexpr int TAPS = KH * KW;
+  constexpr int RB = TILE_M / 64;
+  constexpr int NA = na_max(TILE_M, KH, KW);
+  constexpr int NB = TAPS * BN * (BK / 4) / 256;  // = TAPS
   extern __shared__ float smem[];
   const scflow_conv_args& a = P.a;
-  float* As = smem;                                  // [hr*hc][LDA]
-  float* Bs = smem + (size_t)P.hr * P.hc * LDA;      // [taps][BN][LDA]
+  const int hc = P.hc, ow = P.ow;
+  float* As = smem;                             // [hr*hc][LDA]
+  float* Bs = smem + (size_t)P.hr * hc * LDA;   // [TAPS][BN][LDA]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
   const int tiles_per_img = P.oh / P.tr;
   const int img = blockIdx.x / tiles_per_img;
   const int oy0 = (blockIdx.x % tiles_per_img) * P.tr;
   const int n0 = blockIdx.y * BN;
-  const int ow = P.ow, hc = P.hc;
+  const int na = P.hr * hc * (BK / 4);
+  const int nst0 = P.cp0 / BK;
 
-  // this lane's two A rows (output pixels) as (row, col) inside the tile
-  int pr[2], pc[2];
+  // stage-invariant halo addressing, computed once: input pixel index (or -1 = zero padding)
+  int apix[NA], acq[NA];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    const int m = wm * 64 + rb * 32 + li;
-    pr[rb] = m / ow;
-    pc[rb] = m % ow;
+  for (int j = 0; j < NA; ++j) {
+    const int idx = tid + 256 * j;
+    const int q = idx & 3, pix = idx >> 2;
+    const int hr = pix / hc, hcol = pix - hr * hc;
+    const int iy = oy0 - a.ph + hr, ix = hcol - a.pw;
+    const bool ok = idx < na && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+    apix[j] = ok ? (img * a.h + iy) * a.w + ix : -1;
+    acq[j] = 4 * q;
   }
 
-  floatx16 acc[2];
+  floatx4 ra[NA], rb[NB];
+  auto gload = [&](int s) {
+    const bool s1 = s >= nst0;
+    const float* src = s1 ? a.src1 : a.src0;
+    const int cs = s1 ? a.c1 : a.c0;
+    const int ss = s1 ? a.s1 : a.s0;
+    const int cc = (s1 ? s - nst0 : s) * BK;
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+    for (int j = 0; j < NA; ++j) {
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      const int c = cc + acq[j];
+      if (apix[j] >= 0 && c < cs) v = *(const floatx4*)(src + (size_t)apix[j] * ss + c);
+      ra[j] = v;
+    }
+    const float* wb = a.weight + ((size_t)blockIdx.y * P.nst + s) * (TAPS * BN * BK);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[rb][r] = 0.f;
+    for (int j = 0; j < NB; ++j) rb[j] = *(const floatx4*)(wb + (size_t)(tid + 256 * j) * 4);
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int idx = tid + 256 * j;
+      if (idx < na) *(floatx4*)(As + (idx >> 2) * LDA + 4 * (idx & 3)) = ra[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int idx = tid + 256 * j;
+      *(floatx4*)(Bs + (idx >> 2) * LDA + 4 * (idx & 3)) = rb[j];
+    }
+  };
 
-  const int nsrc = a.c1 > 0 ? 2 : 1;
-  for (int s = 0; s < nsrc; ++s) {
-    const float* src = s ? a.src1 : a.src0;
-    const int cs = s ? a.c1 : a.c0;
-    const int ss = s ? a.s1 : a.s0;
-    const int koff = s ? P.cp0 : 0;
-    for (int cc = 0; cc < cs; cc += BK) {
-      __syncthreads();
-      // input halo: (hr × hc) pixels × BK channels
-      const int na = P.hr * hc * (BK / 4);
-      for (int idx = tid; idx < na; idx += 256) {
-        const int q = idx & 3, pix = idx >> 2;
-        const int hr = pix / hc, hcol = pix - hr * hc;
-        const int iy = oy0 - a.ph + hr, ix = hcol - a.pw;
-        const int c = cc + 4 * q;
-        floatx4 v = {0.f, 0.f, 0.f, 0.f};
-        if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w && c < cs)
-          v = *(const floatx4*)(src + ((size_t)(img * a.h + iy) * a.w + ix) * ss + c);
-        *(floatx4*)(As + pix * LDA + 4 * q) = v;
-      }
-      // weights of every tap for this K-stage
-      const int nb = P.taps * BN * (BK / 4);
-      const int cpt = P.cp0 + P.cp1;
-      for (int idx = tid; idx < nb; idx += 256) {
-        const int q = idx & 3, row = idx >> 2;
-        const int tap = row / BN, col = row - tap * BN;
-        *(floatx4*)(Bs + row * LDA + 4 * q) =
-            *(const floatx4*)(a.weight + (size_t)(n0 + col) * P.ktot + tap * cpt + koff + cc + 4 * q);
-      }
-      __syncthreads();
-      for (int tap = 0; tap < P.taps; ++tap) {
-        const int ty = tap / a.kw, tx = tap - ty * a.kw;
-        const float* Ab0 = As + ((pr[0] + ty) * hc + pc[0] + tx) * LDA + 4 * hh;
-        const float* Ab1 = As + ((pr[1] + ty) * hc + pc[1] + tx) * LDA + 4 * hh;
-        const float* Bb = Bs + (tap * BN + wn * 32 + li) * LDA + 4 * hh;
+  // this lane's RB A rows (output pixels) as halo offsets
+  int abase[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int m = wm * (TILE_M / 2) + r * 32 + li;
+    abase[r] = ((m / ow) * hc + (m % ow)) * LDA + 4 * hh;
+  }
+  const int bbase = (wn * 32 + li) * LDA + 4 * hh;
+
+  floatx16 acc[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
+
+  gload(0);
+  for (int s = 0; s < P.nst; ++s) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (s + 1 < P.nst) gload(s + 1);
+#pragma unroll
+    for (int ty = 0; ty < KH; ++ty) {
+#pragma unroll
+      for (int tx = 0; tx < KW; ++tx) {
+        const int aoff = (ty * hc + tx) * LDA;
+        const float* Bb = Bs + (ty * KW + tx) * BN * LDA + bbase;
 #pragma unroll
         for (int kb = 0; kb < BK; kb += 8) {
-          const floatx4 a0 = *(const floatx4*)(Ab0 + kb);
-          const floatx4 a1 = *(const floatx4*)(Ab1 + kb);
+          floatx4 av[RB];
+#pragma unroll
+          for (int r = 0; r < RB; ++r) av[r] = *(const floatx4*)(As + abase[r] + aoff + kb);
           const floatx4 b0 = *(const floatx4*)(Bb + kb);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], b0[e], acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b0[e], acc[1], 0, 0, 0);
-          }
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+              acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][e], b0[e], acc[r], 0, 0, 0);
         }
       }
     }
@@ -169,13 +221,13 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
   if (col >= a.cout) return;
   const float bias = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
+  for (int rr = 0; rr < RB; ++rr) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = wm * 64 + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const int m = wm * (TILE_M / 2) + rr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
       const int oy = oy0 + m / ow, ox = m % ow;
       const size_t pix = ((size_t)img * P.oh + oy) * ow + ox;
-      const float v = acc[rb][r] + bias;
+      const float v = acc[rr][r] + bias;
       if constexpr (EPI == SCFLOW_EPI_PLAIN) {
         a.out[pix * a.so + col] = act_apply(v, a.act);
       } else if constexpr (EPI == SCFLOW_EPI_GRU_ZR) {
@@ -198,11 +250,58 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
 }
 
 // ------------------------------------------------------------------------------------------
-// small-cin direct conv (VALU): thread = output pixel, 16 output channels per thread
-// weights packed [npad][kh][kw][cin]
+// small-cin conv: lane = output channel, weights in VGPRs, input halo in LDS (broadcast reads)
+// packed weights: [taps*cin][npad]  (channel-contiguous)
+// block: 256 threads; tile = 32 consecutive output pixels of one row; wave w handles channel
+// group (w % G) (G = npad/64 ≤ 4) and a share of the 32 pixels.
 // ------------------------------------------------------------------------------------------
+template <int CIN, int KH, int KW>
+__global__ __launch_bounds__(256) void conv_smallcin_kernel(scflow_conv_args a, int oh, int ow,
+                                                            int npad) {
+  constexpr int HCOLS = 32 + KW - 1;
+  __shared__ float halo[KH][HCOLS][CIN];
+  const int tiles_x = (ow + 31) / 32;
+  const int t = blockIdx.x;
+  const int tx0 = (t % tiles_x) * 32;
+  const int oy = (t / tiles_x) % oh;
+  const int img = t / (tiles_x * oh);
+  for (int i = threadIdx.x; i < KH * HCOLS * CIN; i += 256) {
+    const int c = i % CIN, col = (i / CIN) % HCOLS, row = i / (CIN * HCOLS);
+    const int iy = oy - a.ph + row, ix = tx0 - a.pw + col;
+    float v = 0.f;
+    if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) v = a.src0[((size_t)(img * a.h + iy) * a.w + ix) * a.s0 + c];
+    halo[row][col][c] = v;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = npad / 64;               // channel groups (1, 2 or 4)
+  const int grp = wave % G;
+  const int pshare = 4 / G;              // waves per channel group
+  const int pw_ = 32 / pshare;           // pixels per wave
+  const int p0 = (wave / G) * pw_;
+  const int co = grp * 64 + lane;
+  float wr[KH * KW * CIN];
+#pragma unroll
+  for (int k = 0; k < KH * KW * CIN; ++k) wr[k] = a.weight[(size_t)k * npad + co];
+  const float bias = (a.bias && co < a.cout) ? a.bias[co] : 0.f;
+  __syncthreads();
+  for (int p = p0; p < p0 + pw_; ++p) {
+    const int ox = tx0 + p;
+    if (ox >= ow) break;
+    float acc = bias;
+#pragma unroll
+    for (int ty = 0; ty < KH; ++ty)
+#pragma unroll
+      for (int tx = 0; tx < KW; ++tx)
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) acc += wr[(ty * KW + tx) * CIN + c] * halo[ty][p + tx][c];
+    if (co < a.cout) a.out[((size_t)(img * oh + oy) * ow + ox) * a.so + co] = act_apply(acc, a.act);
+  }
+}
+
+// generic small-cin fallback (any kernel size): thread = pixel, 16 channels per thread
 template <int CIN>
-__global__ __launch_bounds__(256) void conv_smallcin_kernel(scflow_conv_args a, int oh, int ow) {
+__global__ __launch_bounds__(256) void conv_smallcin_generic(scflow_conv_args a, int oh, int ow,
+                                                             int npad) {
   const long long M = (long long)a.n * oh * ow;
   const long long pix = blockIdx.x * 256LL + threadIdx.x;
   const int co0 = blockIdx.y * 16;
@@ -214,22 +313,19 @@ __global__ __launch_bounds__(256) void conv_smallcin_kernel(scflow_conv_args a, 
   float acc[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = (a.bias && co0 + j < a.cout) ? a.bias[co0 + j] : 0.f;
-  const int taps = a.kh * a.kw;
-  const float* wb = a.weight + (size_t)co0 * taps * CIN;
   for (int ty = 0; ty < a.kh; ++ty) {
     const int iy = oy - a.ph + ty;
     for (int tx = 0; tx < a.kw; ++tx) {
       const int ix = ox - a.pw + tx;
-      float v[CIN];
       const bool ok = iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
       const float* sp = a.src0 + ((size_t)(img * a.h + iy) * a.w + ix) * a.s0;
 #pragma unroll
-      for (int c = 0; c < CIN; ++c) v[c] = ok ? sp[c] : 0.f;
-      const float* wt = wb + (ty * a.kw + tx) * CIN;
+      for (int c = 0; c < CIN; ++c) {
+        const float v = ok ? sp[c] : 0.f;
+        const float* wk = a.weight + (size_t)((ty * a.kw + tx) * CIN + c) * npad + co0;
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-#pragma unroll
-        for (int c = 0; c < CIN; ++c) acc[j] += wt[(size_t)j * taps * CIN + c] * v[c];
+        for (int j = 0; j < 16; ++j) acc[j] += wk[j] * v;
+      }
     }
   }
   float* op = a.out + (size_t)pix * a.so + co0;
@@ -239,115 +335,252 @@ __global__ __launch_bounds__(256) void conv_smallcin_kernel(scflow_conv_args a, 
 }
 
 // ------------------------------------------------------------------------------------------
-// thin conv (cout ≤ 4): one wave per output pixel, lanes split the input channels
-// weights packed [cout][kh][kw][cin]
+// thin conv (cout ≤ 4): lane = output pixel of a 64-pixel tile (64/W whole rows); the 4 waves
+// split every 32-channel chunk 4 ways (8 channels each) and reduce through LDS at the end.
+// The chunk's input halo is staged in LDS (coalesced 16-B loads), the next chunk's halo is
+// prefetched into registers while this one is consumed; weights are wave-uniform (s_load).
+// packed weights: [cout][taps][cin]
 // ------------------------------------------------------------------------------------------
-template <int COUT>
-__global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int oh, int ow,
-                                                        int px_per_wave) {
-  extern __shared__ float wsh[];
+constexpr int thin_na(int kh, int kw) {  // float4 per thread of one chunk's halo, W ∈ {32, 64}
+  const int a32 = (2 + kh - 1) * (32 + kw - 1) * (THIN_CC / 4);
+  const int a64 = (1 + kh - 1) * (64 + kw - 1) * (THIN_CC / 4);
+  const int m = a32 > a64 ? a32 : a64;
+  return (m + 255) / 256;
+}
+
+template <int COUT, int KH, int KW>
+__global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int oh, int ow) {
+  constexpr int NA = thin_na(KH, KW);
+  extern __shared__ float halo[];  // [(tr+KH-1)*(ow+KW-1)][THIN_LD], reused for the reduction
+  const int tr = 64 / ow;
+  const int hcols = ow + KW - 1;
+  const int nh = (tr + KH - 1) * hcols * (THIN_CC / 4);
+  const int tiles_per_img = oh / tr;
+  const int img = blockIdx.x / tiles_per_img;
+  const int oy0 = (blockIdx.x % tiles_per_img) * tr;
   const int cin = a.c0 + a.c1;
-  const int taps = a.kh * a.kw;
-  const int nw = COUT * taps * cin;
-  for (int i = threadIdx.x * 4; i < nw; i += 256 * 4) *(floatx4*)(wsh + i) = *(const floatx4*)(a.weight + i);
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long M = (long long)a.n * oh * ow;
-  const long long pbase = ((long long)blockIdx.x * 4 + wave) * px_per_wave;
-  for (int pp = 0; pp < px_per_wave; ++pp) {
-    const long long pix = pbase + pp;
-    if (pix >= M) break;
-    const int ox = (int)(pix % ow);
-    const long long t = pix / ow;
-    const int oy = (int)(t % oh);
-    const int img = (int)(t / oh);
-    float acc[COUT];
+  const int py = lane / ow, px = lane % ow;
+  floatx4 ra[NA];
+  auto gload = [&](int cc) {
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
-    for (int ty = 0; ty < a.kh; ++ty) {
-      const int iy = oy - a.ph + ty;
-      if (iy < 0 || iy >= a.h) continue;
-      for (int tx = 0; tx < a.kw; ++tx) {
-        const int ix = ox - a.pw + tx;
-        if (ix < 0 || ix >= a.w) continue;
-        const size_t ipix = (size_t)(img * a.h + iy) * a.w + ix;
-        const int tap = ty * a.kw + tx;
-        for (int c = lane * 4; c < cin; c += 256) {
-          const floatx4 v = c < a.c0 ? *(const floatx4*)(a.src0 + ipix * a.s0 + c)
-                                     : *(const floatx4*)(a.src1 + ipix * a.s1 + (c - a.c0));
+    for (int j = 0; j < NA; ++j) {
+      const int idx = threadIdx.x + 256 * j;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (idx < nh) {
+        const int q = idx % (THIN_CC / 4), pix = idx / (THIN_CC / 4);
+        const int hr = pix / hcols, hcol = pix % hcols;
+        const int iy = oy0 - a.ph + hr, ix = hcol - a.pw;
+        const int c = cc + 4 * q;
+        if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w && c < cin) {
+          const size_t ip = (size_t)(img * a.h + iy) * a.w + ix;
+          v = c < a.c0 ? *(const floatx4*)(a.src0 + ip * a.s0 + c)
+                       : *(const floatx4*)(a.src1 + ip * a.s1 + (c - a.c0));
+        }
+      }
+      ra[j] = v;
+    }
+  };
+  float acc[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
+  gload(0);
+  for (int cc = 0; cc < cin; cc += THIN_CC) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int idx = threadIdx.x + 256 * j;
+      if (idx < nh) *(floatx4*)(halo + (idx / (THIN_CC / 4)) * THIN_LD + 4 * (idx % (THIN_CC / 4))) = ra[j];
+    }
+    __syncthreads();
+    if (cc + THIN_CC < cin) gload(cc + THIN_CC);
+    const int c0 = wave * 8;  // this wave's 8 channels of the chunk
+    if (cc + c0 < cin) {
+#pragma unroll
+      for (int ty = 0; ty < KH; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < KW; ++tx) {
+          const float* hp = halo + ((py + ty) * hcols + px + tx) * THIN_LD + c0;
+          const floatx4 v0 = *(const floatx4*)(hp);
+          const floatx4 v1 = *(const floatx4*)(hp + 4);
+          const float* wp = a.weight + (size_t)(ty * KW + tx) * cin + cc + c0;
 #pragma unroll
           for (int o = 0; o < COUT; ++o) {
-            const floatx4 wv = *(const floatx4*)(wsh + ((size_t)o * taps + tap) * cin + c);
-            acc[o] += v[0] * wv[0] + v[1] * wv[1] + v[2] * wv[2] + v[3] * wv[3];
+            const float* w = wp + (size_t)o * KH * KW * cin;
+            acc[o] += v0[0] * w[0] + v0[1] * w[1] + v0[2] * w[2] + v0[3] * w[3] +
+                      v1[0] * w[4] + v1[1] * w[5] + v1[2] * w[6] + v1[3] * w[7];
           }
+        }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) halo[(wave * COUT + o) * 64 + lane] = acc[o];
+  __syncthreads();
+  if (wave == 0) {
+    const size_t pix = ((size_t)img * oh + oy0 + py) * ow + px;
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) {
+      float v = halo[(0 * COUT + o) * 64 + lane];
+      v += halo[(1 * COUT + o) * 64 + lane];
+      v += halo[(2 * COUT + o) * 64 + lane];
+      v += halo[(3 * COUT + o) * 64 + lane];
+      const float b = a.bias ? a.bias[o] : 0.f;
+      a.out[pix * a.so + o] = act_apply(v + b, a.act);
+    }
+  }
+}
+
+// generic thin fallback: one wave per output pixel, lanes split the channels
+template <int COUT>
+__global__ __launch_bounds__(256) void conv_thin_generic(scflow_conv_args a, int oh, int ow) {
+  const int cin = a.c0 + a.c1;
+  const int taps = a.kh * a.kw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long M = (long long)a.n * oh * ow;
+  const long long pix = blockIdx.x * 4LL + wave;
+  if (pix >= M) return;
+  const int ox = (int)(pix % ow);
+  const long long t = pix / ow;
+  const int oy = (int)(t % oh);
+  const int img = (int)(t / oh);
+  float acc[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
+  for (int ty = 0; ty < a.kh; ++ty) {
+    const int iy = oy - a.ph + ty;
+    if (iy < 0 || iy >= a.h) continue;
+    for (int tx = 0; tx < a.kw; ++tx) {
+      const int ix = ox - a.pw + tx;
+      if (ix < 0 || ix >= a.w) continue;
+      const size_t ip = (size_t)(img * a.h + iy) * a.w + ix;
+      const int tap = ty * a.kw + tx;
+      for (int c = lane * 4; c < cin; c += 256) {
+        const floatx4 v = c < a.c0 ? *(const floatx4*)(a.src0 + ip * a.s0 + c)
+                                   : *(const floatx4*)(a.src1 + ip * a.s1 + (c - a.c0));
+#pragma unroll
+        for (int o = 0; o < COUT; ++o) {
+          const float* w = a.weight + ((size_t)o * taps + tap) * cin + c;
+          acc[o] += v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
         }
       }
     }
+  }
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) {
+    float v = acc[o];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    acc[o] = v;
+  }
+  if (lane == 0) {
 #pragma unroll
     for (int o = 0; o < COUT; ++o) {
-      float v = acc[o];
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-      acc[o] = v;
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int o = 0; o < COUT; ++o) {
-        const float b = a.bias ? a.bias[o] : 0.f;
-        a.out[(size_t)pix * a.so + o] = act_apply(acc[o] + b, a.act);
-      }
+      const float b = a.bias ? a.bias[o] : 0.f;
+      a.out[(size_t)pix * a.so + o] = act_apply(acc[o] + b, a.act);
     }
   }
 }
 
 // packing: w_oihw [cout][cin][kh][kw] → variant layout
 __global__ void pack_kernel(const float* __restrict__ w, float* __restrict__ out, int variant,
-                            int cout, int c0, int c1, int kh, int kw, int cp0, int cp1, int ktot,
-                            int npad) {
-  const long long total = (long long)npad * ktot;
+                            int cout, int c0, int c1, int kh, int kw, int cp0, int nst, int npad,
+                            long long total) {
   const int cin = c0 + c1, taps = kh * kw;
   for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
-    const int o = (int)(idx / ktot);
-    const int k = (int)(idx % ktot);
     float v = 0.f;
     if (variant == V_MFMA) {
-      const int cpt = cp0 + cp1;
-      const int tap = k / cpt, cc = k % cpt;
+      // [nt][s][tap][col][k]
+      long long r = idx;
+      const int k = (int)(r % BK); r /= BK;
+      const int col = (int)(r % BN); r /= BN;
+      const int tap = (int)(r % taps); r /= taps;
+      const int s = (int)(r % nst);
+      const int nt = (int)(r / nst);
+      const int o = nt * BN + col;
+      const int kc = s * BK + k;  // channel index in the padded concat space
       int ci = -1;
-      if (cc < cp0) {
-        if (cc < c0) ci = cc;
-      } else if (cc - cp0 < c1) {
-        ci = c0 + (cc - cp0);
+      if (kc < cp0) {
+        if (kc < c0) ci = kc;
+      } else if (kc - cp0 < c1) {
+        ci = c0 + (kc - cp0);
       }
       if (o < cout && ci >= 0) v = w[((size_t)o * cin + ci) * taps + tap];
-    } else {  // [o][tap][ci]
+    } else if (variant == V_SMALLCIN) {  // [tap*cin + ci][npad]
+      const int o = (int)(idx % npad);
+      const int k = (int)(idx / npad);
       const int tap = k / cin, ci = k % cin;
       if (o < cout) v = w[((size_t)o * cin + ci) * taps + tap];
+    } else {  // thin: [o][tap][ci]
+      const int ktot = taps * cin;
+      const int o = (int)(idx / ktot);
+      const int k = (int)(idx % ktot);
+      const int tap = k / cin, ci = k % cin;
+      v = w[((size_t)o * cin + ci) * taps + tap];
     }
     out[idx] = v;
   }
 }
 
-bool lds_attr_done[3] = {false, false, false};
+// Workgroup-count heuristic (measured on MI355X, tools/conv_bench.py): 128-pixel tiles when
+// that still gives ≥ 2 workgroups per CU (≥ 512), else 64-pixel tiles (GRU q: 103 vs 94 TF,
+// N=64 convs: 85 vs 54 TF, N=192: 94 vs 91 TF; z|r and the 512-wide heads prefer 128).
+// SCFLOW_CONV_TILE_M=64|128 forces one (tuning only).
+int pick_tile_m(long long m, int ntiles) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("SCFLOW_CONV_TILE_M");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 64 || forced == 128) return forced;
+  const long long wg = (m / 128) * ntiles;
+  if (wg >= 512) return 128;
+  return 64;
+}
 
-template <int EPI>
-int launch_mfma(const MfmaParams& p, const Geometry& g, hipStream_t st) {
-  if (g.lds > 64 * 1024 && !lds_attr_done[EPI]) {
-    hipFuncSetAttribute((const void*)conv_mfma_kernel<EPI>,
+template <int EPI, int KH, int KW, int TM>
+int launch_mfma_tm(MfmaParams p, Geometry g, hipStream_t st) {
+  g.tr = TM / g.ow;
+  if (g.tr < 1 || g.oh % g.tr) return SCFLOW_EUNSUPPORTED;
+  g.hr = g.tr + KH - 1;
+  g.lds = sizeof(float) * ((size_t)g.hr * g.hc * LDA + (size_t)g.taps * BN * LDA);
+  p.tr = g.tr;
+  p.hr = g.hr;
+  static bool attr = false;
+  if (g.lds > 64 * 1024 && !attr) {
+    hipFuncSetAttribute((const void*)conv_mfma_kernel<EPI, KH, KW, TM>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    lds_attr_done[EPI] = true;
+    attr = true;
   }
   dim3 grid(p.a.n * (g.oh / g.tr), g.npad / BN);
-  conv_mfma_kernel<EPI><<<grid, 256, g.lds, st>>>(p);
+  conv_mfma_kernel<EPI, KH, KW, TM><<<grid, 256, g.lds, st>>>(p);
   return scflow_launch_status();
+}
+
+template <int EPI, int KH, int KW>
+int launch_mfma(const MfmaParams& p, const Geometry& g, hipStream_t st) {
+  const long long m = (long long)p.a.n * g.oh * g.ow;
+  if (pick_tile_m(m, g.npad / BN) == 64 && g.ow <= 64) return launch_mfma_tm<EPI, KH, KW, 64>(p, g, st);
+  return launch_mfma_tm<EPI, KH, KW, 128>(p, g, st);
+}
+
+template <int EPI>
+int dispatch_mfma(const MfmaParams& p, const Geometry& g, hipStream_t st) {
+  const int kh = p.a.kh, kw = p.a.kw;
+  if (kh == 1 && kw == 1) return launch_mfma<EPI, 1, 1>(p, g, st);
+  if (kh == 3 && kw == 3) return launch_mfma<EPI, 3, 3>(p, g, st);
+  if (kh == 1 && kw == 5) return launch_mfma<EPI, 1, 5>(p, g, st);
+  if (kh == 5 && kw == 1) return launch_mfma<EPI, 5, 1>(p, g, st);
+  return SCFLOW_EUNSUPPORTED;
 }
 
 }  // namespace
 
 SCFLOW_API long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, int kw, int stride,
                                              int w) {
-  // packing does not depend on padding or height; use a 'same' geometry for the selection
-  Geometry g = select_variant(cout, c0, c1, kh, kw, stride, 4 * 128, w, (kh - 1) / 2, (kw - 1) / 2);
+  // packing depends on the width (tile = whole rows) but not on the height or padding
+  Geometry g = select_variant(cout, c0, c1, kh, kw, stride, w == 64 ? 64 : 32 * 4, w, (kh - 1) / 2,
+                              (kw - 1) / 2);
   if (g.variant == V_NONE) return SCFLOW_EUNSUPPORTED;
   return (long long)g.npad * g.ktot;
 }
@@ -355,12 +588,13 @@ SCFLOW_API long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, i
 SCFLOW_API int scflow_conv_pack_weights(const float* w_oihw, float* packed, int cout, int c0,
                                         int c1, int kh, int kw, int stride, int w, void* stream) {
   if (!w_oihw || !packed || cout <= 0 || c0 <= 0 || c1 < 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
-  Geometry g = select_variant(cout, c0, c1, kh, kw, stride, 4 * 128, w, (kh - 1) / 2, (kw - 1) / 2);
+  Geometry g = select_variant(cout, c0, c1, kh, kw, stride, w == 64 ? 64 : 32 * 4, w, (kh - 1) / 2,
+                              (kw - 1) / 2);
   if (g.variant == V_NONE) return SCFLOW_EUNSUPPORTED;
   const long long total = (long long)g.npad * g.ktot;
   const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
   pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, g.variant, cout, c0, c1, kh,
-                                                       kw, g.cp0, g.cp1, g.ktot, g.npad);
+                                                       kw, g.cp0, g.nst, g.npad, total);
   return scflow_launch_status();
 }
 
@@ -394,41 +628,69 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     p.tr = g.tr;
     p.hr = g.hr;
     p.hc = g.hc;
-    p.taps = g.taps;
     p.cp0 = g.cp0;
-    p.cp1 = g.cp1;
-    p.ktot = g.ktot;
+    p.nst = g.nst;
     switch (a.epilogue) {
-      case SCFLOW_EPI_GRU_ZR: return launch_mfma<SCFLOW_EPI_GRU_ZR>(p, g, st);
-      case SCFLOW_EPI_GRU_Q: return launch_mfma<SCFLOW_EPI_GRU_Q>(p, g, st);
-      default: return launch_mfma<SCFLOW_EPI_PLAIN>(p, g, st);
+      case SCFLOW_EPI_GRU_ZR: return dispatch_mfma<SCFLOW_EPI_GRU_ZR>(p, g, st);
+      case SCFLOW_EPI_GRU_Q: return dispatch_mfma<SCFLOW_EPI_GRU_Q>(p, g, st);
+      default: return dispatch_mfma<SCFLOW_EPI_PLAIN>(p, g, st);
     }
   }
   if (a.epilogue != SCFLOW_EPI_PLAIN) return SCFLOW_EUNSUPPORTED;
   const long long M = (long long)a.n * g.oh * g.ow;
   if (g.variant == V_SMALLCIN) {
+    const unsigned tiles = (unsigned)((long long)a.n * g.oh * ((g.ow + 31) / 32));
+    if (g.npad == 64 || g.npad == 128 || g.npad == 256) {
+      if (a.c0 == 2 && a.kh == 7 && a.kw == 7) {
+        conv_smallcin_kernel<2, 7, 7><<<tiles, 256, 0, st>>>(a, g.oh, g.ow, g.npad);
+        return scflow_launch_status();
+      }
+      if (a.c0 == 1 && a.kh == 3 && a.kw == 3) {
+        conv_smallcin_kernel<1, 3, 3><<<tiles, 256, 0, st>>>(a, g.oh, g.ow, g.npad);
+        return scflow_launch_status();
+      }
+      if (a.c0 == 2 && a.kh == 3 && a.kw == 3) {
+        conv_smallcin_kernel<2, 3, 3><<<tiles, 256, 0, st>>>(a, g.oh, g.ow, g.npad);
+        return scflow_launch_status();
+      }
+    }
     dim3 grid((unsigned)((M + 255) / 256), g.npad / 16);
     switch (a.c0) {
-      case 1: conv_smallcin_kernel<1><<<grid, 256, 0, st>>>(a, g.oh, g.ow); break;
-      case 2: conv_smallcin_kernel<2><<<grid, 256, 0, st>>>(a, g.oh, g.ow); break;
-      case 3: conv_smallcin_kernel<3><<<grid, 256, 0, st>>>(a, g.oh, g.ow); break;
-      case 4: conv_smallcin_kernel<4><<<grid, 256, 0, st>>>(a, g.oh, g.ow); break;
+      case 1: conv_smallcin_generic<1><<<grid, 256, 0, st>>>(a, g.oh, g.ow, g.npad); break;
+      case 2: conv_smallcin_generic<2><<<grid, 256, 0, st>>>(a, g.oh, g.ow, g.npad); break;
+      case 3: conv_smallcin_generic<3><<<grid, 256, 0, st>>>(a, g.oh, g.ow, g.npad); break;
+      case 4: conv_smallcin_generic<4><<<grid, 256, 0, st>>>(a, g.oh, g.ow, g.npad); break;
       default: return SCFLOW_EUNSUPPORTED;
     }
     return scflow_launch_status();
   }
   // thin
-  if (!aligned16(a.src0) || (a.s0 & 3) || (a.c1 > 0 && (!aligned16(a.src1) || (a.s1 & 3))) ||
-      !aligned16(a.weight) || (a.c0 & 3))
+  if (!aligned16(a.src0) || (a.s0 & 3) || (a.c1 > 0 && (!aligned16(a.src1) || (a.s1 & 3))))
     return SCFLOW_EALIGN;
-  const int ppw = 16;
-  const int blocks = (int)((M + 4 * ppw - 1) / (4 * ppw));
-  const size_t lds = sizeof(float) * (size_t)a.cout * g.taps * (a.c0 + a.c1);
+  const bool tiled = (g.ow == 32 || g.ow == 64) && (a.c0 % 8) == 0 && (a.c1 % 8) == 0 &&
+                     g.oh % (64 / g.ow) == 0 && g.ow == a.w && g.oh == a.h;
+  if (tiled) {
+    const int tr = 64 / g.ow;
+    const unsigned blocks = (unsigned)(a.n * (g.oh / tr));
+#define SCFLOW_THIN(CO, KH_, KW_)                                                               \
+  if (a.cout == CO && a.kh == KH_ && a.kw == KW_) {                                             \
+    size_t lds = sizeof(float) * (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * THIN_LD;           \
+    if (lds < sizeof(float) * 4 * CO * 64) lds = sizeof(float) * 4 * CO * 64;                    \
+    conv_thin_kernel<CO, KH_, KW_><<<blocks, 256, lds, st>>>(a, g.oh, g.ow);                    \
+    return scflow_launch_status();                                                              \
+  }
+    SCFLOW_THIN(1, 1, 1)
+    SCFLOW_THIN(2, 1, 1)
+    SCFLOW_THIN(1, 3, 3)
+    SCFLOW_THIN(2, 3, 3)
+#undef SCFLOW_THIN
+  }
+  const unsigned blocks = (unsigned)((M + 3) / 4);
   switch (a.cout) {
-    case 1: conv_thin_kernel<1><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, ppw); break;
-    case 2: conv_thin_kernel<2><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, ppw); break;
-    case 3: conv_thin_kernel<3><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, ppw); break;
-    case 4: conv_thin_kernel<4><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, ppw); break;
+    case 1: conv_thin_generic<1><<<blocks, 256, 0, st>>>(a, g.oh, g.ow); break;
+    case 2: conv_thin_generic<2><<<blocks, 256, 0, st>>>(a, g.oh, g.ow); break;
+    case 3: conv_thin_generic<3><<<blocks, 256, 0, st>>>(a, g.oh, g.ow); break;
+    case 4: conv_thin_generic<4><<<blocks, 256, 0, st>>>(a, g.oh, g.ow); break;
     default: return SCFLOW_EUNSUPPORTED;
   }
   return scflow_launch_status();

@@ -1,0 +1,95 @@
+"""Time every convolution shape of the decoder in isolation (B pairs, 32×32 features).
+
+usage: python tools/conv_bench.py [--batch 16] [--reps 20]
+Prints one line per shape: µs per launch and achieved TFLOP/s (algorithmic FLOPs, fp32).
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from scflow_amd import ops  # noqa: E402
+from scflow_amd._lib import EPI_GRU_Q, EPI_GRU_ZR  # noqa: E402
+from scflow_amd.modules import ConvRunner  # noqa: E402
+from scflow_amd.ops import Chan  # noqa: E402
+
+# name, cin0, cin1, cout, k, pad, act, epilogue
+SHAPES = [
+    ("corr_net.0 1x1 324->256", 324, 0, 256, (1, 1), (0, 0), "ReLU", None),
+    ("corr_net.1 3x3 256->192", 256, 0, 192, (3, 3), (1, 1), "ReLU", None),
+    ("flow_net.0 7x7 2->128", 2, 0, 128, (7, 7), (3, 3), "ReLU", None),
+    ("flow_net.1 3x3 128->64", 128, 0, 64, (3, 3), (1, 1), "ReLU", None),
+    ("out_net 3x3 256->126", 192, 64, 126, (3, 3), (1, 1), "ReLU", None),
+    ("gru zr 1x5 384->256", 384, 0, 256, (1, 5), (0, 2), "Sigmoid", "zr"),
+    ("gru q 1x5 128+256->128", 128, 256, 128, (1, 5), (0, 2), "Tanh", "q"),
+    ("gru zr 5x1 384->256", 384, 0, 256, (5, 1), (2, 0), "Sigmoid", "zr"),
+    ("gru q 5x1 128+256->128", 128, 256, 128, (5, 1), (2, 0), "Tanh", "q"),
+    ("heads 3x3 128->512", 128, 0, 512, (3, 3), (1, 1), "ReLU", None),
+    ("flow_pred 3x3 256->2", 256, 0, 2, (3, 3), (1, 1), None, None),
+    ("mask_pred 1x1 256->1", 256, 0, 1, (1, 1), (0, 0), "Sigmoid", None),
+    ("dflow.1 3x3 128->64", 128, 0, 64, (3, 3), (1, 1), "ReLU", None),
+    ("mask_enc.0 3x3 1->64", 1, 0, 64, (3, 3), (1, 1), "ReLU", None),
+    ("mask_enc.1 3x3 64->32", 64, 0, 32, (3, 3), (1, 1), "ReLU", None),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--size", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    n, h, w = a.batch, a.size, a.size
+    M = n * h * w
+    dev = "cuda"
+    res = []
+    tot_us = 0.0
+    for name, c0, c1, cout, k, pad, act, epi in SHAPES:
+        conv = torch.nn.Conv2d(c0 + c1, cout, k, padding=pad).to(dev)
+        x0 = torch.randn(M, c0, device=dev)
+        x1 = torch.randn(M, c1, device=dev) if c1 else None
+        r = ConvRunner([conv], act)
+        kw = {}
+        if epi == "zr":
+            hid = torch.randn(M, 128, device=dev)
+            kw = dict(epilogue=EPI_GRU_ZR, gate=Chan.whole(torch.empty(M, 128, device=dev)),
+                      rh=Chan.whole(torch.empty(M, 128, device=dev)), hid=Chan.whole(hid))
+            out = None
+        elif epi == "q":
+            kw = dict(epilogue=EPI_GRU_Q, gate=Chan.whole(torch.rand(M, 128, device=dev)),
+                      hid=Chan.whole(torch.randn(M, 128, device=dev)))
+            out = None
+        else:
+            out = Chan.whole(torch.empty(M, cout, device=dev))
+        src1 = Chan.whole(x1) if x1 is not None else None
+
+        def run():
+            r.run(Chan.whole(x0), out, n, h, w, src1=src1, **kw)
+
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.reps):
+            run()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) * 1e3 / a.reps
+        flops = 2.0 * M * cout * (c0 + c1) * k[0] * k[1]
+        tf = flops / us / 1e6
+        tot_us += us
+        res.append(dict(name=name, us=round(us, 2), tflops=round(tf, 2)))
+        print(f"{name:28s} {us:9.2f} us  {tf:7.2f} TFLOP/s", flush=True)
+    print(f"{'sum (one of each)':28s} {tot_us:9.2f} us")
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
