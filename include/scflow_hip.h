@@ -25,6 +25,7 @@
  *   scflow_flow_downsample   <- 1/8·F.interpolate(flow, 1/8, bilinear, align_corners=True)  scflow_decoder.py:197-198
  *   scflow_flow_upsample     <- 8·F.interpolate(flow+Δflow, ×8) and mask ×8 (same)          scflow_decoder.py:223-228
  *   scflow_transpose         <- layout plumbing (NCHW <-> channels-last slices), no reference equivalent
+ *   scflow_ph_*              <- MultiClassPoseHead.forward                models/head/pose_head.py:201-211
  */
 #ifndef SCFLOW_HIP_H
 #define SCFLOW_HIP_H
@@ -130,6 +131,35 @@ int scflow_flow_upsample(const float* lr, const float* delta, const float* mask,
  * NCHW -> a channel slice of an NHWC buffer, or back). */
 int scflow_transpose(const float* in, float* out, int n, int A, int B, long long ins, int ias,
                      long long ons, int obs, void* stream);
+
+/* a7: MultiClassPoseHead (pose_head.py:110-211) as 9 launches.
+ * scflow_ph_conv: x (two channel sources, channels-last, pixel strides s0/s1) → raw conv output
+ *   out [n][oh][ow][cout] (channels-last, + bias if given).  If scale/shift are given, the input
+ *   is first mapped x ← relu(x·scale[n][c] + shift[n][c]) (the previous GroupNorm + ReLU).
+ *   Weights packed by scflow_ph_conv_pack ([cout][kh·kw][roundup(cin,16)]).
+ * scflow_ph_gn_stats: GroupNorm(groups) statistics of x [n][hw][c] → scale/shift [n][c] with
+ *   scale = γ/sqrt(var+eps), shift = β − mean·scale (biased variance, like F.group_norm).
+ * scflow_ph_fc: y [m][n] = act(x [m][k] · Wᵀ + b), W = nn.Linear weight [n][k] (k % 16 == 0).
+ *   gn_c > 0: x is a raw conv output [m][hw][gn_c] (channels-last) mapped through scale/shift +
+ *   ReLU; W's columns must then be in channels-last order — scflow_ph_fc_permute turns the
+ *   reference's NCHW-flatten columns (k = c·hw + p, nn.Flatten) into that order.
+ * scflow_ph_heads: drot [m][rch] and dt [m][3] from x [m][k] using only class label[0]'s rows of
+ *   the rotation [num_class·rch][k] and translation [num_class·3][k] heads (index_select quirk). */
+long long scflow_ph_conv_packed_size(int cout, int cin, int kh, int kw);
+int scflow_ph_conv_pack(const float* w_oihw, float* packed, int cout, int cin, int kh, int kw,
+                        void* stream);
+int scflow_ph_conv(const float* src0, int c0, int s0, const float* src1, int c1, int s1,
+                   const float* scale, const float* shift, const float* packed, const float* bias,
+                   float* out, int n, int h, int w, int cout, int kh, int kw, int stride, int pad,
+                   void* stream);
+int scflow_ph_gn_stats(const float* x, int n, int hw, int c, int groups, const float* gamma,
+                       const float* beta, float eps, float* scale, float* shift, void* stream);
+int scflow_ph_fc_permute(const float* W, float* Wp, int n, int c, int hw, void* stream);
+int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias, float* y,
+                 int n, int relu, int gn_c, const float* scale, const float* shift, void* stream);
+int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* br, int rch,
+                    const float* Wt, const float* bt, const long long* label, int num_class,
+                    float* drot, float* dt, void* stream);
 
 #ifdef __cplusplus
 }

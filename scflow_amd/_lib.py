@@ -59,6 +59,17 @@ SIGNATURES = {
     "scflow_flow_upsample": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
                                      c_float, c_vp]),
     "scflow_transpose": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_int, c_ll, c_int, c_vp]),
+    "scflow_ph_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
+    "scflow_ph_conv_pack": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_ph_conv": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_ph_gn_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_vp,
+                                   c_vp]),
+    "scflow_ph_fc_permute": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_ph_fc": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
+                             c_vp, c_vp]),
+    "scflow_ph_heads": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp,
+                                c_vp, c_vp]),
 }
 
 _lib = None

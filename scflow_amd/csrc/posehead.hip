@@ -1,0 +1,413 @@
+// a7 — MultiClassPoseHead (/root/reference/models/head/pose_head.py:110-211) on gfx950.
+//
+//   3 × [3×3 stride-2 conv (no bias) → GroupNorm(32) → ReLU] → flatten (NCHW order)
+//   → FC 2048→1024 + ReLU → FC 1024→256 + ReLU → rotation / translation heads
+//   → index_select(label)[:, 0]  (every sample uses label[0]'s class head — reference quirk)
+//
+// Stock PyTorch runs this as ~15 small launches per refinement iteration (MIOpen conv +
+// layout transposes, GroupNorm's moments / fused-params / apply kernels, ReLU clamps, copies,
+// hipBLASLt GEMMs, index_select).  Here: 9 launches, no torch ops, no concatenation:
+//
+//  * scflow_ph_conv — gather-A implicit GEMM on v_mfma_f32_32x32x2_f32 for the strided convs.
+//    Workgroup tile = 32 output pixels × 32 output channels; the 4 waves split K (16-deep
+//    chunks, round robin) and reduce their 32×32 partials through LDS.  A (im2col rows) is
+//    gathered straight from L2 per lane, two input sources concatenated on channels
+//    (cat[h, Δflow-feat, mask-feat] never materialises), and the PREVIOUS layer's GroupNorm +
+//    ReLU is applied on load (per-(sample, channel) scale/shift) — so GN never rewrites memory.
+//    conv1 at B=16: 512 workgroups.
+//  * scflow_ph_gn_stats — one workgroup per sample: group mean/var (fp64 accumulation) →
+//    scale = γ·rstd, shift = β − mean·γ·rstd per channel.
+//  * scflow_ph_fc — weight-streaming FC for M ≤ 16 rows: a wave per output neuron pair,
+//    lanes split K, inputs staged once per workgroup in LDS; optional GN+ReLU+NCHW-flatten
+//    gather of the input (FC1 reads conv3's raw output).
+//  * scflow_ph_heads — the label[0] class's 6 rotation and 3 translation rows only.
+#include "common.h"
+
+namespace {
+
+constexpr int PH_K = 16;  // K chunk per MFMA group
+
+struct PhConvArgs {
+  const float* src0; int c0; int s0;
+  const float* src1; int c1; int s1;
+  const float* scale;   // [n][c0+c1] GN scale of the input (NULL: raw input)
+  const float* shift;   // [n][c0+c1]
+  const float* weight;  // packed [cout][taps][cinp], cinp = roundup(c0+c1, 16)
+  const float* bias;    // [cout] or NULL
+  float* out;           // [n][oh][ow][cout]
+  int n, h, w, oh, ow, cout, kh, kw, stride, pad, cinp;
+};
+
+__device__ __forceinline__ floatx4 ph_load_a(const PhConvArgs& a, int img, int iy, int ix, int c) {
+  floatx4 v = {0.f, 0.f, 0.f, 0.f};
+  if (iy < 0 || iy >= a.h || ix < 0 || ix >= a.w) return v;
+  const size_t pix = (size_t)(img * a.h + iy) * a.w + ix;
+  const int cin = a.c0 + a.c1;
+  if (c >= cin) return v;
+  v = c < a.c0 ? *(const floatx4*)(a.src0 + pix * a.s0 + c)
+               : *(const floatx4*)(a.src1 + pix * a.s1 + (c - a.c0));
+  if (a.scale) {
+    const floatx4 sc = *(const floatx4*)(a.scale + (size_t)img * cin + c);
+    const floatx4 sh = *(const floatx4*)(a.shift + (size_t)img * cin + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+  }
+  return v;
+}
+
+constexpr int PH_WAVES = 16;  // waves per workgroup; they split K
+constexpr int PH_BATCH = 4;   // K chunks whose loads a wave issues together
+
+__global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
+  __shared__ float red[PH_WAVES / 2][32][33];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, hh = lane >> 5;
+  const int M = a.n * a.oh * a.ow;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  // this lane's A row (output pixel) and B column (output channel)
+  const int m = m0 + li;
+  const bool mvalid = m < M;
+  const int ox = mvalid ? m % a.ow : 0;
+  const int oy = mvalid ? (m / a.ow) % a.oh : 0;
+  const int img = mvalid ? m / (a.ow * a.oh) : 0;
+  const int col = n0 + li;
+  const bool nvalid = col < a.cout;
+  const int taps = a.kh * a.kw;
+  const int cchunks = a.cinp / PH_K;
+  const int nchunks = taps * cchunks;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int base = wave; base < nchunks; base += PH_WAVES * PH_BATCH) {
+    floatx4 A0[PH_BATCH], A1[PH_BATCH], B0[PH_BATCH], B1[PH_BATCH];
+#pragma unroll
+    for (int c = 0; c < PH_BATCH; ++c) {  // issue every load of the batch first
+      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+      A0[c] = A1[c] = B0[c] = B1[c] = z;
+      const int kc = base + c * PH_WAVES;
+      if (kc < nchunks) {
+        const int tap = kc / cchunks, c0 = (kc % cchunks) * PH_K;
+        const int ty = tap / a.kw, tx = tap % a.kw;
+        const int iy = oy * a.stride - a.pad + ty, ix = ox * a.stride - a.pad + tx;
+        if (mvalid) {
+          A0[c] = ph_load_a(a, img, iy, ix, c0 + 4 * hh);
+          A1[c] = ph_load_a(a, img, iy, ix, c0 + 8 + 4 * hh);
+        }
+        if (nvalid) {
+          const float* wp = a.weight + ((size_t)col * taps + tap) * a.cinp + c0 + 4 * hh;
+          B0[c] = *(const floatx4*)wp;
+          B1[c] = *(const floatx4*)(wp + 8);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < PH_BATCH; ++c) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[c][e], B0[c][e], acc, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c][e], B1[c][e], acc, 0, 0, 0);
+    }
+  }
+  // deterministic tree reduction of the waves' partial tiles
+  for (int half = PH_WAVES / 2; half >= 1; half >>= 1) {
+    if (wave >= half && wave < 2 * half) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[wave - half][(r & 3) + 8 * (r >> 2) + 4 * hh][li] = acc[r];
+    }
+    __syncthreads();
+    if (wave < half) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += red[wave][(r & 3) + 8 * (r >> 2) + 4 * hh][li];
+    }
+    __syncthreads();
+  }
+  if (wave == 0 && nvalid) {
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (mm < M) a.out[(size_t)mm * a.cout + col] = acc[r] + b;
+    }
+  }
+}
+
+// GroupNorm statistics of x [n][hw][c] → per-channel scale/shift for y = relu(x·scale + shift).
+// One workgroup per sample; thread (g, slice) accumulates group g over pixels ≡ slice (mod
+// 256/groups) in fp64, then the slices are reduced in LDS in a fixed order.
+__global__ __launch_bounds__(256) void ph_gn_stats_kernel(const float* __restrict__ x, int hw, int c,
+                                                          int groups, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float* __restrict__ scale,
+                                                          float* __restrict__ shift) {
+  __shared__ double s1[256], s2[256];
+  const int img = blockIdx.x;
+  const int cpg = c / groups;
+  const int slices = 256 / groups;  // groups ≤ 256
+  const int g = threadIdx.x % groups, sl = threadIdx.x / groups;
+  const float* xs = x + (size_t)img * hw * c + g * cpg;
+  double a = 0.0, b = 0.0;
+  if (sl < slices) {
+    for (int p = sl; p < hw; p += slices)
+      for (int k = 0; k < cpg; ++k) {
+        const double v = xs[(size_t)p * c + k];
+        a += v;
+        b += v * v;
+      }
+  }
+  s1[threadIdx.x] = a;
+  s2[threadIdx.x] = b;
+  __syncthreads();
+  if (threadIdx.x < groups) {
+    double A = 0.0, Bq = 0.0;
+    for (int t = 0; t < slices; ++t) {
+      A += s1[t * groups + threadIdx.x];
+      Bq += s2[t * groups + threadIdx.x];
+    }
+    const double cnt = (double)hw * cpg;
+    const double mean = A / cnt;
+    double var = Bq / cnt - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    for (int k = 0; k < cpg; ++k) {
+      const int ch = threadIdx.x * cpg + k;
+      const float sc = gamma[ch] * rstd;
+      scale[(size_t)img * c + ch] = sc;
+      shift[(size_t)img * c + ch] = beta[ch] - (float)mean * sc;
+    }
+  }
+}
+
+// FC on v_mfma_f32_16x16x4_f32: D[neuron i][row j] = Σ_k W[i][k]·X[j][k] for a 16-neuron
+// tile (grid.x) and up to FC_RT·16 batch rows; PH_WAVES waves split K in 16-wide groups and
+// issue all their loads before the MFMAs, then reduce through LDS (fixed order).
+// Lane l: A = W[i0 + (l&15)][k..k+3], B = X[l&15][k..k+3] with k = 16g + 4(l>>4) — MFMA e
+// consumes element e of both (a permutation of K, identical on both operands).
+// Modes: plain X [m][ldx]; GN (gn_c > 0): X = relu(Y·scale + shift), Y [m][k] channels-last
+// with channel = k % gn_c (W's columns must be in that order: scflow_ph_fc_permute);
+// heads (label != NULL): neuron i < rch → Wr row label[0]·rch + i, i < rch+3 → Wt row
+// label[0]·3 + i − rch; outputs drot [m][rch], dt [m][3].
+
+struct FcArgs {
+  const float* x; int ldx; int m; int k;
+  const float* W; const float* bias; float* y; int n; int relu;
+  int gn_c; const float* scale; const float* shift;
+  const float* Wt; const float* bt; const long long* label; int num_class; int rch; float* dt;
+};
+
+template <int FC_RT>  // row tiles of 16 per pass
+__global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
+  constexpr int FB = FC_RT == 1 ? PH_BATCH : 2;  // K groups whose loads are issued together
+  __shared__ float red[PH_WAVES / 2][FC_RT][64][5];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, kq = lane >> 4;
+  const int i0 = blockIdx.x * 16;
+  // weight row of this lane's neuron
+  const int ni = i0 + li;
+  const float* wrow = nullptr;
+  if (f.label) {
+    long long cls = f.label[0];
+    if (cls < 0 || cls >= f.num_class) cls = 0;
+    if (ni < f.rch) wrow = f.W + ((size_t)cls * f.rch + ni) * f.k;
+    else if (ni < f.rch + 3) wrow = f.Wt + ((size_t)cls * 3 + (ni - f.rch)) * f.k;
+  } else if (ni < f.n) {
+    wrow = f.W + (size_t)ni * f.k;
+  }
+  const int groups = f.k / 16;
+  for (int r0 = 0; r0 < f.m; r0 += 16 * FC_RT) {
+    floatx4 acc[FC_RT];
+#pragma unroll
+    for (int t = 0; t < FC_RT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
+    for (int base = wave; base < groups; base += PH_WAVES * FB) {
+      floatx4 wv[FB], xv[FB][FC_RT];
+#pragma unroll
+      for (int c = 0; c < FB; ++c) {
+        const int g = base + c * PH_WAVES;
+        const int kk = g * 16 + 4 * kq;
+        const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+        wv[c] = (g < groups && wrow) ? *(const floatx4*)(wrow + kk) : z;
+#pragma unroll
+        for (int t = 0; t < FC_RT; ++t) {
+          const int row = r0 + t * 16 + li;
+          floatx4 v = z;
+          if (g < groups && row < f.m) {
+            v = *(const floatx4*)(f.x + (size_t)row * f.ldx + kk);
+            if (f.gn_c > 0) {
+              const int ch = kk % f.gn_c;
+              const floatx4 sc = *(const floatx4*)(f.scale + (size_t)row * f.gn_c + ch);
+              const floatx4 sh = *(const floatx4*)(f.shift + (size_t)row * f.gn_c + ch);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+            }
+          }
+          xv[c][t] = v;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < FB; ++c)
+#pragma unroll
+        for (int t = 0; t < FC_RT; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[c][e], xv[c][t][e], acc[t], 0, 0, 0);
+    }
+    for (int half = PH_WAVES / 2; half >= 1; half >>= 1) {
+      if (wave >= half && wave < 2 * half) {
+#pragma unroll
+        for (int t = 0; t < FC_RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[wave - half][t][lane][r] = acc[t][r];
+      }
+      __syncthreads();
+      if (wave < half) {
+#pragma unroll
+        for (int t = 0; t < FC_RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[t][r] += red[wave][t][lane][r];
+      }
+      __syncthreads();
+    }
+    if (wave == 0) {
+      // C/D layout (16x16): col = lane&15 (batch row), row = 4(lane>>4) + r (neuron)
+#pragma unroll
+      for (int t = 0; t < FC_RT; ++t) {
+        const int row = r0 + t * 16 + li;
+        if (row >= f.m) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + 4 * kq + r;
+          float v = acc[t][r];
+          if (f.label) {
+            long long cls = f.label[0];
+            if (cls < 0 || cls >= f.num_class) cls = 0;
+            if (i < f.rch)
+              f.y[(size_t)row * f.rch + i] = v + f.bias[cls * f.rch + i];
+            else if (i < f.rch + 3)
+              f.dt[(size_t)row * 3 + (i - f.rch)] = v + f.bt[cls * 3 + (i - f.rch)];
+          } else if (i < f.n) {
+            v += f.bias ? f.bias[i] : 0.f;
+            if (f.relu) v = fmaxf(v, 0.f);
+            f.y[(size_t)row * f.n + i] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// W [n][c·hw] with columns in NCHW-flatten order (c·hw + p) → Wp [n][hw·c] channels-last order
+__global__ void ph_fc_permute_kernel(const float* __restrict__ W, float* __restrict__ Wp, int n,
+                                     int c, int hw) {
+  const long long total = (long long)n * c * hw;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int kk = (int)(i % ((long long)c * hw));
+    const long long row = i / ((long long)c * hw);
+    const int p = kk / c, ch = kk % c;
+    Wp[i] = W[row * c * hw + (size_t)ch * hw + p];
+  }
+}
+
+__global__ void ph_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,
+                               int cin, int taps, int cinp) {
+  const long long total = (long long)cout * taps * cinp;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % cinp);
+    const int tap = (int)((i / cinp) % taps);
+    const int o = (int)(i / ((long long)cinp * taps));
+    out[i] = c < cin ? w[((size_t)o * cin + c) * taps + tap] : 0.f;
+  }
+}
+
+}  // namespace
+
+SCFLOW_API long long scflow_ph_conv_packed_size(int cout, int cin, int kh, int kw) {
+  if (cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  return (long long)cout * kh * kw * ((cin + PH_K - 1) / PH_K * PH_K);
+}
+
+SCFLOW_API int scflow_ph_conv_pack(const float* w_oihw, float* packed, int cout, int cin, int kh,
+                                   int kw, void* stream) {
+  if (!w_oihw || !packed || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  const int cinp = (cin + PH_K - 1) / PH_K * PH_K;
+  const long long total = (long long)cout * kh * kw * cinp;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  ph_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, cin, kh * kw, cinp);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_conv(const float* src0, int c0, int s0, const float* src1, int c1, int s1,
+                              const float* scale, const float* shift, const float* packed,
+                              const float* bias, float* out, int n, int h, int w, int cout, int kh,
+                              int kw, int stride, int pad, void* stream) {
+  if (!src0 || !packed || !out || n <= 0 || h <= 0 || w <= 0 || cout <= 0 || c0 <= 0 || c1 < 0 ||
+      (c1 > 0 && !src1) || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 || (scale && !shift))
+    return SCFLOW_EINVAL;
+  if ((c0 & 3) || (c1 & 3) || (s0 & 3) || (c1 && (s1 & 3)) || !aligned16(src0) ||
+      (c1 && !aligned16(src1)) || !aligned16(packed))
+    return SCFLOW_EALIGN;
+  PhConvArgs a;
+  a.src0 = src0; a.c0 = c0; a.s0 = s0;
+  a.src1 = src1; a.c1 = c1; a.s1 = s1;
+  a.scale = scale; a.shift = shift;
+  a.weight = packed; a.bias = bias; a.out = out;
+  a.n = n; a.h = h; a.w = w;
+  a.oh = (h + 2 * pad - kh) / stride + 1;
+  a.ow = (w + 2 * pad - kw) / stride + 1;
+  if (a.oh <= 0 || a.ow <= 0) return SCFLOW_EINVAL;
+  a.cout = cout; a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad;
+  a.cinp = (c0 + c1 + PH_K - 1) / PH_K * PH_K;
+  const long long M = (long long)n * a.oh * a.ow;
+  dim3 grid((unsigned)((M + 31) / 32), (unsigned)((cout + 31) / 32));
+  ph_conv_kernel<<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_gn_stats(const float* x, int n, int hw, int c, int groups,
+                                  const float* gamma, const float* beta, float eps, float* scale,
+                                  float* shift, void* stream) {
+  if (!x || !gamma || !beta || !scale || !shift || n <= 0 || hw <= 0 || c <= 0 || groups <= 0 ||
+      c % groups || c / groups > 256)
+    return SCFLOW_EINVAL;
+  ph_gn_stats_kernel<<<n, 256, 0, (hipStream_t)stream>>>(x, hw, c, groups, gamma, beta, eps, scale,
+                                                         shift);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_fc_permute(const float* W, float* Wp, int n, int c, int hw, void* stream) {
+  if (!W || !Wp || n <= 0 || c <= 0 || hw <= 0) return SCFLOW_EINVAL;
+  const long long total = (long long)n * c * hw;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  ph_fc_permute_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(W, Wp, n, c, hw);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias,
+                            float* y, int n, int relu, int gn_c, const float* scale,
+                            const float* shift, void* stream) {
+  if (!x || !W || !y || m <= 0 || k <= 0 || n <= 0 || (k & 15) || (ldx & 3) || !aligned16(W) ||
+      !aligned16(x) || (gn_c > 0 && (!scale || !shift || (gn_c & 3))))
+    return SCFLOW_EINVAL;
+  FcArgs f{};
+  f.x = x; f.ldx = ldx; f.m = m; f.k = k; f.W = W; f.bias = bias; f.y = y; f.n = n; f.relu = relu;
+  f.gn_c = gn_c; f.scale = scale; f.shift = shift;
+  if (m <= 16)
+    ph_fc_kernel<1><<<(n + 15) / 16, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  else
+    ph_fc_kernel<2><<<(n + 15) / 16, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* br,
+                               int rch, const float* Wt, const float* bt, const long long* label,
+                               int num_class, float* drot, float* dt, void* stream) {
+  if (!x || !Wr || !br || !Wt || !bt || !label || !drot || !dt || m <= 0 || k <= 0 || (k & 15) ||
+      rch <= 0 || rch + 3 > 16 || num_class <= 0 || !aligned16(x) || !aligned16(Wr) || !aligned16(Wt))
+    return SCFLOW_EINVAL;
+  FcArgs f{};
+  f.x = x; f.ldx = k; f.m = m; f.k = k; f.W = Wr; f.bias = br; f.y = drot; f.n = rch + 3;
+  f.Wt = Wt; f.bt = bt; f.label = label; f.num_class = num_class; f.rch = rch; f.dt = dt;
+  if (m <= 16)
+    ph_fc_kernel<1><<<1, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  else
+    ph_fc_kernel<2><<<1, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  return scflow_launch_status();
+}

@@ -156,7 +156,7 @@ class SCFlowDecoder(nn.Module):
         MASK = torch.empty(M, 1, device=dev, dtype=f32)
         dfc = self.delta_flow_encoder[-1].conv.out_channels
         mfc = self.mask_encoder[-1].conv.out_channels
-        PH = torch.empty(M, hc + dfc + mfc, device=dev, dtype=f32)
+        FM = torch.empty(M, dfc + mfc, device=dev, dtype=f32)  # [Δflow feat | mask feat]
 
         def scratch(mods):
             return [torch.empty(M, m.conv.out_channels, device=dev, dtype=f32) for m in mods[:-1]]
@@ -217,15 +217,11 @@ class SCFlowDecoder(nn.Module):
             mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MASK), N, h, w)
             if mask_lr is not None:
                 mask_lr = MASK
-            # a6 Δflow / mask encoders → PH[hc:]
-            run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(PH, hc, dfc), N, h, w, s_dfe)
-            run_chain(self.mask_encoder, Chan.whole(MASK), Chan(PH, hc + dfc, mfc), N, h, w, s_me)
-            PH[:, :hc].copy_(HX[:, :hc])
-            # a7 pose head (stock PyTorch-ROCm), input cat[h, Δflow feat, mask feat] NCHW view
-            ph_in = PH.view(N, h, w, -1).permute(0, 3, 1, 2)
-            drot, dtr = self.pose_pred(ph_in, label)
-            drot = drot.contiguous().float()
-            dtr = dtr.contiguous().float()
+            # a6 Δflow / mask encoders → FM
+            run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe)
+            run_chain(self.mask_encoder, Chan.whole(MASK), Chan(FM, dfc, mfc), N, h, w, s_me)
+            # a7 pose head on cat[h, Δflow feat, mask feat] (two channel sources, no concat)
+            drot, dtr = self.pose_pred.forward_hip(hid, Chan.whole(FM), N, h, w, label)
             # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
             ops.flow_upsample(F2, D2, MASK, N, h, w, H, W, float(scale), o_flow_pred[it], o_mask[it])
             # a8 + a10: pose update + pose-induced flow (one launch)

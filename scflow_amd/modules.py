@@ -421,7 +421,73 @@ class MultiClassPoseHead(nn.Module):
             base = [0.0, 0.0, 0.0, 1.0] if self.rotation_mode == "quaternion" else [1.0, 0, 0, 0, 1.0, 0]
             self.rotation_pred.bias.copy_(torch.tensor(base * self.num_class))
 
+    # ------------------------------------------------------------------ HIP path
+    def _packs(self, c_last: int, hw_last: int):
+        w1 = self.fc_layers[0][0].weight
+        key = tuple((m.conv.weight.data_ptr(), m.conv.weight._version) for m in self.conv_layers) + (
+            w1.data_ptr(), w1._version, c_last, hw_last)
+        if getattr(self, "_pack_key", None) != key:
+            self._packed = [ops.ph_conv_pack(m.conv.weight) for m in self.conv_layers]
+            self._fc1_perm = ops.ph_fc_permute(w1, c_last, hw_last)
+            self._pack_key = key
+        return self._packed, self._fc1_perm
+
+    def forward_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
+                    label: Tensor) -> Tuple[Tensor, Tensor]:
+        """Channels-last input cat[src0, src1] of n samples at h×w → (Δrot, Δt), 9 launches."""
+        if any(m.norm_type != "GN" or m.act_type != "ReLU" for m in self.conv_layers):
+            raise NotImplementedError("HIP pose head: conv + GroupNorm + ReLU layers only")
+        dev = src0.buf.device
+        hl, wl = h, w
+        for m in self.conv_layers:
+            k, st, p = m.conv.kernel_size[0], m.conv.stride[0], m.conv.padding[0]
+            hl, wl = (hl + 2 * p - k) // st + 1, (wl + 2 * p - k) // st + 1
+        packs, fc1_w = self._packs(self.conv_layers[-1].conv.out_channels, hl * wl)
+        cur0, cur1, hh, ww = src0, src1, h, w
+        scale = shift = None
+        for i, m in enumerate(self.conv_layers):
+            conv = m.conv
+            k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            oh, ow = (hh + 2 * p - k) // s + 1, (ww + 2 * p - k) // s + 1
+            cout = conv.out_channels
+            y = torch.empty(n * oh * ow, cout, device=dev)
+            ops.ph_conv(cur0, cur1, packs[i], None if conv.bias is None else conv.bias.detach(), n, hh,
+                        ww, cout, k, s, p, y, scale, shift)
+            scale = torch.empty(n, cout, device=dev)
+            shift = torch.empty(n, cout, device=dev)
+            ops.ph_gn_stats(y, n, oh * ow, cout, m.gn.num_groups, m.gn.weight.detach(),
+                            m.gn.bias.detach(), m.gn.eps, scale, shift)
+            cur0, cur1, hh, ww = Chan.whole(y), None, oh, ow
+        c = cur0.c
+        x = cur0.buf
+        k_in = c * hh * ww
+        for i, fc in enumerate(self.fc_layers):
+            lin = fc[0]
+            y = torch.empty(n, lin.out_features, device=dev)
+            if i == 0:
+                ops.ph_fc(x, k_in, n, k_in, fc1_w, lin.bias.detach(), y, lin.out_features, True,
+                          gn_c=c, scale=scale, shift=shift)
+            else:
+                ops.ph_fc(x, x.shape[1], n, x.shape[1], lin.weight.detach(), lin.bias.detach(), y,
+                          lin.out_features, True)
+            x = y
+        drot = torch.empty(n, self.rotation_out_channels, device=dev)
+        dt = torch.empty(n, 3, device=dev)
+        ops.ph_heads(x, n, x.shape[1], self.rotation_pred.weight.detach(),
+                     self.rotation_pred.bias.detach(), self.rotation_out_channels,
+                     self.translation_pred.weight.detach(), self.translation_pred.bias.detach(),
+                     label.long(), self.num_class, drot, dt)
+        return drot, dt
+
     def forward(self, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
+        """Reference API (NCHW in).  Runs the HIP kernels (inference; no autograd graph)."""
+        n, c, h, w = x.shape
+        src = torch.empty(n * h * w, c, device=x.device)
+        ops.nchw_into(x.contiguous().float(), Chan.whole(src))
+        return self.forward_hip(Chan.whole(src), None, n, h, w, label.to(x.device))
+
+    def forward_torch(self, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
+        """Stock PyTorch-ROCm path (autograd-capable); the reference's own composition."""
         for m in self.conv_layers:
             x = m.forward_torch(x)
         x = self.flatten_op(x)

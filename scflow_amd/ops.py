@@ -273,3 +273,56 @@ def chan_to_nchw(src: Chan, n: int, h: int, w: int, out: Optional[Tensor] = None
     check(_lib.load().scflow_transpose(src.ptr, _p(res), n, h * w, src.c, h * w * st, st,
                                        src.c * h * w, h * w, _stream(src.buf)), "scflow_transpose")
     return res
+
+
+# ------------------------------------------------------------------------------- a7 pose head
+def ph_conv_pack(weight: Tensor) -> Tensor:
+    _require(weight, "pose conv weight", contiguous=False)
+    w = weight.detach().contiguous().float()
+    cout, cin, kh, kw = w.shape
+    lib = _lib.load()
+    packed = torch.empty(lib.scflow_ph_conv_packed_size(cout, cin, kh, kw), device=w.device)
+    check(lib.scflow_ph_conv_pack(_p(w), _p(packed), cout, cin, kh, kw, _stream(w)),
+          "scflow_ph_conv_pack")
+    return packed
+
+
+def ph_conv(src0: Chan, src1: Optional[Chan], packed: Tensor, bias: Optional[Tensor], n: int, h: int,
+            w: int, cout: int, k: int, stride: int, pad: int, out: Tensor,
+            scale: Optional[Tensor] = None, shift: Optional[Tensor] = None) -> None:
+    check(_lib.load().scflow_ph_conv(
+        src0.ptr, src0.c, src0.stride, None if src1 is None else src1.ptr,
+        0 if src1 is None else src1.c, 0 if src1 is None else src1.stride, _p(scale), _p(shift),
+        _p(packed), _p(bias), _p(out), n, h, w, cout, k, k, stride, pad, _stream(out)),
+        "scflow_ph_conv")
+
+
+def ph_gn_stats(x: Tensor, n: int, hw: int, c: int, groups: int, gamma: Tensor, beta: Tensor,
+                eps: float, scale: Tensor, shift: Tensor) -> None:
+    check(_lib.load().scflow_ph_gn_stats(_p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps),
+                                         _p(scale), _p(shift), _stream(x)), "scflow_ph_gn_stats")
+
+
+def ph_fc_permute(W: Tensor, c: int, hw: int) -> Tensor:
+    """nn.Linear weight with NCHW-flatten columns → channels-last column order."""
+    _require(W, "fc weight", contiguous=False)
+    W = W.detach().contiguous().float()
+    Wp = torch.empty_like(W)
+    check(_lib.load().scflow_ph_fc_permute(_p(W), _p(Wp), W.shape[0], c, hw, _stream(W)),
+          "scflow_ph_fc_permute")
+    return Wp
+
+
+def ph_fc(x: Tensor, ldx: int, m: int, k: int, W: Tensor, bias: Optional[Tensor], y: Tensor, n: int,
+          relu: bool, gn_c: int = 0, scale: Optional[Tensor] = None,
+          shift: Optional[Tensor] = None) -> None:
+    check(_lib.load().scflow_ph_fc(_p(x), ldx, m, k, _p(W), _p(bias), _p(y), n, int(relu), gn_c,
+                                   _p(scale), _p(shift), _stream(x)), "scflow_ph_fc")
+
+
+def ph_heads(x: Tensor, m: int, k: int, Wr: Tensor, br: Tensor, rch: int, Wt: Tensor, bt: Tensor,
+             label: Tensor, num_class: int, drot: Tensor, dt: Tensor) -> None:
+    if label.dtype != torch.int64 or label.device != x.device:
+        raise TypeError("label must be an int64 tensor on the same device")
+    check(_lib.load().scflow_ph_heads(_p(x), m, k, _p(Wr), _p(br), rch, _p(Wt), _p(bt), _p(label),
+                                      num_class, _p(drot), _p(dt), _stream(x)), "scflow_ph_heads")

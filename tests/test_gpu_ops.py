@@ -238,3 +238,31 @@ def test_cpu_tensor_rejected(ops):
     from scflow_amd._lib import ScflowError
     with pytest.raises(ScflowError):
         ops.corr_pyramid(torch.randn(1, 8, 8, 8), torch.randn(1, 8, 8, 8), 4)
+
+
+# ------------------------------------------------------------------------------ a7 pose head
+@pytest.mark.parametrize("n,feat", [(16, 32), (32, 32), (3, 64)])
+def test_pose_head_hip_vs_oracle(ops, n, feat):
+    from scflow_amd import synthetic
+    from scflow_amd.modules import MultiClassPoseHead
+    head = MultiClassPoseHead(21, 224, "Basic", dict(type="GN", num_groups=32),
+                              dict(type="ReLU"), feat_size=(feat, feat), rotation_mode="ortho6d")
+    synthetic.fill_module_(head, seed=7)
+    g = torch.Generator().manual_seed(8)
+    x = torch.relu(torch.randn(n, 224, feat, feat, generator=g))
+    label = torch.randint(0, 21, (n,), generator=g)
+    sd = {f"pose_pred.{k}": v.double() for k, v in head.state_dict().items()}
+    r_ref, t_ref = orc.pose_head(sd, x.double(), label, 21)
+    head = head.cuda()
+    # two-source form (h | features) as the decoder calls it
+    hbuf = torch.zeros(n * feat * feat, 384, device="cuda")
+    fbuf = torch.zeros(n * feat * feat, 96, device="cuda")
+    ops.nchw_into(x[:, :128].contiguous().cuda(), ops.Chan(hbuf, 0, 128))
+    ops.nchw_into(x[:, 128:].contiguous().cuda(), ops.Chan.whole(fbuf))
+    r, tt = head.forward_hip(ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf), n, feat, feat,
+                             label.cuda())
+    close(r, r_ref, 2e-5, 1e-5, "pose head rotation")
+    close(tt, t_ref, 2e-5, 1e-5, "pose head translation")
+    # NCHW module API
+    r2, t2 = head(x.cuda(), label.cuda())
+    close(r2, r, 1e-6, 1e-6, "pose head NCHW api")
