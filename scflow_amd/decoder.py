@@ -97,6 +97,15 @@ class SCFlowDecoder(nn.Module):
             return self._head_runner
         return None
 
+    def _side_stream(self, dev) -> torch.cuda.Stream:
+        """A second HIP stream for the decoder's independent branches (created once per device)."""
+        ss = getattr(self, "_streams", None)
+        if ss is None:
+            ss = self._streams = {}
+        if dev not in ss:
+            ss[dev] = torch.cuda.Stream(device=dev)
+        return ss[dev]
+
     def _hook(self, name: str, start: bool) -> None:
         h = self.kernel_hooks.get(name)
         if h is not None:
@@ -186,23 +195,43 @@ class SCFlowDecoder(nn.Module):
         hx_flow = Chan(HX, hx_c - 2, 2)
         hx_motion = Chan(HX, hc + xc, co)
         hid = Chan(HX, 0, hc)
+        # independent branches run concurrently on a second stream, joined with events:
+        # flow_net ‖ (lookup, corr_net); mask predictor + mask encoder ‖ flow predictor +
+        # Δflow encoder.  Every buffer is allocated above on the main stream and outlives the
+        # forward, and the main stream always waits for the side branch before reusing them.
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+
+        def fork():
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+
+        def join():
+            ev = torch.cuda.Event()
+            ev.record(side)
+            main.wait_event(ev)
 
         for it in range(iters):
             # a11 ↓: flow at feature resolution → F2 (and the motion-feature flow channels)
             ops.flow_downsample(flow_full, Chan.whole(F2), h, w, 1.0 / scale,
                                 out1=None if self.mask_flow else hx_flow)
-            # a2
-            ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
-                            flow_layout="nhwc")
-            if self.mask_corr:
-                CORR.mul_(mask_lr)
             flow_in = F2
             if self.mask_flow:
                 flow_in = F2 * mask_lr
                 HX[:, hx_c - 2:].copy_(flow_in)
-            # a3 motion encoder → HX[hc+xc : hc+xc+co]
+            # a3 (flow branch) on the side stream
+            fork()
+            with torch.cuda.stream(side):
+                run_chain(self.encoder.flow_net, Chan.whole(flow_in), Chan(MF, cc, cf), N, h, w,
+                          s_flow)
+            # a2 + a3 (correlation branch)
+            ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
+                            flow_layout="nhwc")
+            if self.mask_corr:
+                CORR.mul_(mask_lr)
             run_chain(self.encoder.corr_net, Chan.whole(CORR), Chan(MF, 0, cc), N, h, w, s_corr)
-            run_chain(self.encoder.flow_net, Chan.whole(flow_in), Chan(MF, cc, cf), N, h, w, s_flow)
+            join()
             run_chain(self.encoder.out_net, Chan.whole(MF), hx_motion, N, h, w, s_out)
             # a4 GRU (in place on HX[:, :hc])
             self.gru.step(Chan.whole(HX), Chan.whole(Z), Chan.whole(RH), N, h, w,
@@ -213,13 +242,17 @@ class SCFlowDecoder(nn.Module):
             else:
                 run_chain(self.flow_pred.layers, hid, Chan(HEAD, 0, fh), N, h, w)
                 run_chain(self.mask_pred.layers, hid, Chan(HEAD, fh, mh), N, h, w)
+            # mask predictor + mask encoder (a5, a6) on the side stream
+            fork()
+            with torch.cuda.stream(side):
+                mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MASK), N, h, w)
+                run_chain(self.mask_encoder, Chan.whole(MASK), Chan(FM, dfc, mfc), N, h, w, s_me)
+            # flow predictor + Δflow encoder
             flow_pred_r.run(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w)
-            mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MASK), N, h, w)
+            run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe)
+            join()
             if mask_lr is not None:
                 mask_lr = MASK
-            # a6 Δflow / mask encoders → FM
-            run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe)
-            run_chain(self.mask_encoder, Chan.whole(MASK), Chan(FM, dfc, mfc), N, h, w, s_me)
             # a7 pose head on cat[h, Δflow feat, mask feat] (two channel sources, no concat)
             drot, dtr = self.pose_pred.forward_hip(hid, Chan.whole(FM), N, h, w, label)
             # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑

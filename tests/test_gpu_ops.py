@@ -266,3 +266,21 @@ def test_pose_head_hip_vs_oracle(ops, n, feat):
     # NCHW module API
     r2, t2 = head(x.cuda(), label.cuda())
     close(r2, r, 1e-6, 1e-6, "pose head NCHW api")
+
+
+def test_corr_lookup_far_out_of_bounds(ops):
+    """Flows that push every window off the map (and half-pixel / integer edge cases) give the
+    reference's zero padding, not garbage."""
+    g = torch.Generator().manual_seed(9)
+    f1 = torch.randn(1, 8, 16, 16, generator=g)
+    f2 = torch.randn(1, 8, 16, 16, generator=g)
+    buf, lv = ops.corr_pyramid(f1.cuda(), f2.cuda(), 4)
+    flow = torch.zeros(1, 2, 16, 16)
+    flow[0, 0, :4] = 1e4
+    flow[0, 1, 4:8] = -1e4
+    flow[0, :, 8:12] = torch.arange(4 * 16 * 2, dtype=torch.float32).view(2, 4, 16) * 0.25 - 8
+    flow[0, :, 12:] = 15.0
+    ref = orc.corr_lookup([x.cpu() for x in lv], flow, 4)
+    out = ops.corr_lookup(buf, flow.cuda(), 1, 16, 16, 4, 4)
+    close(out, ref, 1e-5, 1e-5, "lookup far / edge flows")
+    assert (out[0, :, :8].abs().max() == 0)

@@ -86,6 +86,37 @@ def main():
         res.append(dict(name=name, us=round(us, 2), tflops=round(tf, 2)))
         print(f"{name:28s} {us:9.2f} us  {tf:7.2f} TFLOP/s", flush=True)
     print(f"{'sum (one of each)':28s} {tot_us:9.2f} us")
+    # a1 pyramid + a2 lookup (algorithmic bytes: SURVEY.md §8(d))
+    C, P = 256, h * w
+    f1 = torch.randn(n, C, h, w, device=dev)
+    f2 = torch.randn(n, C, h, w, device=dev)
+    flow = (torch.rand(n * P, 2, device=dev) - 0.5) * 8
+
+    def timed(fn, reps):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        s0, e0 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        for _ in range(reps):
+            fn()
+        e0.record()
+        torch.cuda.synchronize()
+        return s0.elapsed_time(e0) * 1e3 / reps
+
+    holder = {}
+
+    def build():
+        holder["pyr"], _ = ops.corr_pyramid(f1, f2, 4)
+
+    us = timed(build, a.reps)
+    fl = 2.0 * n * P * P * C
+    print(f"{'corr pyramid (GEMM+pool)':28s} {us:9.2f} us  {fl / us / 1e6:7.2f} TFLOP/s")
+    out = Chan.whole(torch.empty(n * P, 324, device=dev))
+    us = timed(lambda: ops.corr_lookup(holder["pyr"], flow, n, h, w, 4, 4, out=out, flow_layout="nhwc"),
+               a.reps)
+    byts = n * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
+    print(f"{'corr lookup r=4':28s} {us:9.2f} us  {byts / us / 1e3:7.2f} GB/s (algorithmic)")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)
