@@ -26,6 +26,7 @@
  *   scflow_flow_upsample     <- 8·F.interpolate(flow+Δflow, ×8) and mask ×8 (same)          scflow_decoder.py:223-228
  *   scflow_transpose         <- layout plumbing (NCHW <-> channels-last slices), no reference equivalent
  *   scflow_ph_*              <- MultiClassPoseHead.forward                models/head/pose_head.py:201-211
+ *   scflow_enc_*             <- RAFTEncoder.forward (Basic; IN / BN)      models/encoder/raft_encoder.py:286-314
  */
 #ifndef SCFLOW_HIP_H
 #define SCFLOW_HIP_H
@@ -160,6 +161,58 @@ int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const fl
 int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* br, int rch,
                     const float* Wt, const float* bt, const long long* label, int num_class,
                     float* drot, float* dt, void* stream);
+
+/* §8(f)-1: RAFTEncoder (Basic) — feature encoder (InstanceNorm) and context encoder (BatchNorm,
+ * eval statistics), models/encoder/raft_encoder.py:286-314, BasicBlock models/backbone/resnet.py:
+ * 12-92, ResLayer resnet.py:676-771, called from SCFlowRefiner.extract_feat
+ * (models/refiner/scflow_refiner.py:84-106).  Activations are channels-last [n][h][w][c].
+ *
+ * scflow_enc_conv: implicit-GEMM conv (fp32 MFMA), 1×1 or 3×3, stride 1 or 2, cin % 16 == 0;
+ *   output width 16, 32, 64 or a multiple of the tile (128 for stride 1, 64 for stride 2), and
+ *   output height a multiple of the tile's rows (tile / width when the width is smaller).  Per element of the output:
+ *     v = conv(x') + bias;  v = v·out_scale[c] + out_shift[c] (if given: eval BatchNorm);
+ *     v += res[pix][c] (if given);  out = act(v) for c < act_split, act2(v) otherwise,
+ *   where x' = relu(x·in_scale[img][c] + in_shift[img][c]) if in_scale is given (the previous
+ *   InstanceNorm + ReLU applied on load; zero padding stays zero), else x.
+ *   Weights packed by scflow_enc_conv_pack (same shape).
+ * scflow_enc_stem: 7×7 (any kh,kw ≤ 7) conv of an NCHW image batch [n][cin≤4][h][w], stride s,
+ *   written channels-last with the same bias / out_scale / act epilogue (the stem conv1).
+ *   Weights packed by scflow_enc_stem_pack ([kh·kw·cin][roundup(cout,64)]).
+ * scflow_enc_stats + scflow_enc_norm_finalize: InstanceNorm statistics of x [n][hw][c]
+ *   (fp64 partial sums over `chunks` pixel chunks per image, then per (img, c))
+ *   → scale = 1/sqrt(var+eps), shift = −mean·scale (biased variance, affine=False);
+ *   partial must hold n·chunks·2·c doubles.
+ * scflow_enc_apply: out[p][c] = relu(x·scale[img][c] + shift[img][c] + id'), with
+ *   id' = 0 (id NULL), id (id_scale NULL) or id·id_scale[img][c] + id_shift[img][c]. */
+typedef struct scflow_enc_conv_args {
+  const float* src; int cin; int s_in;            /* input, channels, pixel stride           */
+  const float* in_scale; const float* in_shift;    /* [n][cin] or NULL                        */
+  const float* weight; const float* bias;          /* packed; bias [cout] or NULL             */
+  const float* out_scale; const float* out_shift;  /* [cout] or NULL                          */
+  const float* res; int s_res;                     /* residual or NULL, pixel stride          */
+  float* out; int s_out;                           /* output, pixel stride                    */
+  int n, h, w, cout, kh, kw, stride, pad;
+  int act, act2, act_split;                        /* SCFLOW_ACT_* and the channel split      */
+} scflow_enc_conv_args;
+
+long long scflow_enc_conv_packed_size(int cout, int cin, int kh, int kw);
+int scflow_enc_conv_pack(const float* w_oihw, float* packed, int cout, int cin, int kh, int kw,
+                         void* stream);
+int scflow_enc_conv(const scflow_enc_conv_args* args, void* stream);
+long long scflow_enc_stem_packed_size(int cout, int cin, int kh, int kw);
+int scflow_enc_stem_pack(const float* w_oihw, float* packed, int cout, int cin, int kh, int kw,
+                         void* stream);
+int scflow_enc_stem(const float* img, const float* packed, const float* bias,
+                    const float* out_scale, const float* out_shift, float* out, int n, int cin,
+                    int h, int w, int cout, int kh, int kw, int stride, int pad, int act,
+                    void* stream);
+int scflow_enc_stats(const float* x, int n, int hw, int c, int chunks, double* partial,
+                     void* stream);
+int scflow_enc_norm_finalize(const double* partial, int n, int chunks, int c, int hw, float eps,
+                             float* scale, float* shift, void* stream);
+int scflow_enc_apply(const float* x, const float* scale, const float* shift, const float* id,
+                     const float* id_scale, const float* id_shift, float* out, int n, int hw,
+                     int c, void* stream);
 
 #ifdef __cplusplus
 }

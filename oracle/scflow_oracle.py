@@ -348,3 +348,55 @@ def cal_epe_mean(flow_tgt: Tensor, flow_pred: Tensor, mask: Tensor | None = None
     valid = (mag < max_flow) if mask is None else ((mag < max_flow) & (mask >= 0.5))
     err = torch.sum((flow_tgt - flow_pred) ** 2, dim=1).sqrt()
     return (err * valid.to(err)).sum(dim=(-1, -2)) / (valid.sum(dim=(-1, -2)) + 1e-10)
+
+
+# ---------------------------------------------------------------------------------------------
+# §8(f)-1 — RAFTEncoder 'Basic' (models/encoder/raft_encoder.py:286-314) and the refiner's
+# feature extraction (models/refiner/scflow_refiner.py:84-106, 108-138)
+# ---------------------------------------------------------------------------------------------
+def _enc_norm(x: Tensor, sd: StateDict, key: str, norm: str, eps: float = 1e-5) -> Tensor:
+    """mmcv build_norm_layer: IN → InstanceNorm2d(affine=False), BN → BatchNorm2d (eval stats)."""
+    if norm == "IN":
+        return F.instance_norm(x, eps=eps)
+    return F.batch_norm(x, sd[key + ".running_mean"], sd[key + ".running_var"], sd[key + ".weight"],
+                        sd[key + ".bias"], training=False, eps=eps)
+
+
+def _basic_block(sd: StateDict, p: str, x: Tensor, stride: int, norm: str) -> Tensor:
+    """BasicBlock.forward (models/backbone/resnet.py:65-92); downsample = ResLayer's
+    1×1/stride conv + norm (resnet.py:707-729)."""
+    ab = "in" if norm == "IN" else "bn"
+    out = F.conv2d(x, sd[p + "conv1.weight"], sd[p + "conv1.bias"], stride=stride, padding=1)
+    out = F.relu(_enc_norm(out, sd, p + ab + "1", norm))
+    out = F.conv2d(out, sd[p + "conv2.weight"], sd[p + "conv2.bias"], padding=1)
+    out = _enc_norm(out, sd, p + ab + "2", norm)
+    if p + "downsample.0.weight" in sd:
+        identity = F.conv2d(x, sd[p + "downsample.0.weight"], sd[p + "downsample.0.bias"], stride=stride)
+        identity = _enc_norm(identity, sd, p + "downsample.1", norm)
+    else:
+        identity = x
+    return F.relu(out + identity)
+
+
+def raft_encoder(sd: StateDict, x: Tensor, norm: str, prefix: str = "",
+                 strides: Sequence[int] = (1, 2, 2), blocks: Sequence[int] = (2, 2, 2)) -> Tensor:
+    """RAFTEncoder.forward, net_type='Basic', scale 1/8 (stem stride 2)."""
+    ab = "in" if norm == "IN" else "bn"
+    x = F.conv2d(x, sd[prefix + "conv1.weight"], sd[prefix + "conv1.bias"], stride=2, padding=3)
+    x = F.relu(_enc_norm(x, sd, prefix + ab + "1", norm))
+    for i, (s, nb) in enumerate(zip(strides, blocks)):
+        for b in range(nb):
+            x = _basic_block(sd, f"{prefix}res_layer{i + 1}.{b}.", x, s if b == 0 else 1, norm)
+    return F.conv2d(x, sd[prefix + "conv2.weight"], sd[prefix + "conv2.bias"])
+
+
+def extract_feat(sd: StateDict, render_images: Tensor, real_images: Tensor,
+                 h_channels: int = 128, cxt_channels: int = 128):
+    """SCFlowRefiner.extract_feat (scflow_refiner.py:84-106): one shared feature encoder
+    (``real_encoder`` is ``render_encoder`` when ``seperate_encoder=False``,
+    base_refiner.py:33-40), context encoder on the rendered image, split + tanh / relu."""
+    real = raft_encoder(sd, real_images, "IN", "real_encoder.")
+    render = raft_encoder(sd, render_images, "IN", "render_encoder.")
+    cxt = raft_encoder(sd, render_images, "BN", "context.")
+    h, c = torch.split(cxt, [h_channels, cxt_channels], dim=1)
+    return render, real, torch.tanh(h), torch.relu(c)

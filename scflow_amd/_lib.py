@@ -37,6 +37,21 @@ class ConvArgs(ctypes.Structure):
     ]
 
 
+class EncConvArgs(ctypes.Structure):
+    """Mirror of ``scflow_enc_conv_args`` (include/scflow_hip.h)."""
+    _fields_ = [
+        ("src", c_vp), ("cin", c_int), ("s_in", c_int),
+        ("in_scale", c_vp), ("in_shift", c_vp),
+        ("weight", c_vp), ("bias", c_vp),
+        ("out_scale", c_vp), ("out_shift", c_vp),
+        ("res", c_vp), ("s_res", c_int),
+        ("out", c_vp), ("s_out", c_int),
+        ("n", c_int), ("h", c_int), ("w", c_int), ("cout", c_int), ("kh", c_int), ("kw", c_int),
+        ("stride", c_int), ("pad", c_int),
+        ("act", c_int), ("act2", c_int), ("act_split", c_int),
+    ]
+
+
 # name -> (restype, argtypes); every function the header declares
 SIGNATURES = {
     "scflow_version": (c_int, []),
@@ -70,6 +85,16 @@ SIGNATURES = {
                              c_vp, c_vp]),
     "scflow_ph_heads": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp,
                                 c_vp, c_vp]),
+    "scflow_enc_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
+    "scflow_enc_conv_pack": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_enc_conv": (c_int, [ctypes.POINTER(EncConvArgs), c_vp]),
+    "scflow_enc_stem_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
+    "scflow_enc_stem_pack": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_enc_stem": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_enc_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "scflow_enc_norm_finalize": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp]),
+    "scflow_enc_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
 }
 
 _lib = None

@@ -548,7 +548,7 @@ int launch_mfma_tm(MfmaParams p, Geometry g, hipStream_t st) {
   p.hr = g.hr;
   static bool attr = false;
   if (g.lds > 64 * 1024 && !attr) {
-    hipFuncSetAttribute((const void*)conv_mfma_kernel<EPI, KH, KW, TM>,
+    (void)hipFuncSetAttribute((const void*)conv_mfma_kernel<EPI, KH, KW, TM>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }

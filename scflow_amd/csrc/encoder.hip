@@ -1,0 +1,509 @@
+// §8(f)-1 — RAFTEncoder ('Basic'): the feature encoder (InstanceNorm) and the context encoder
+// (BatchNorm with eval statistics) of SCFlowRefiner.extract_feat.
+//
+// Reference (/root/reference): RAFTEncoder.forward models/encoder/raft_encoder.py:286-314 (stem
+// conv1 7×7/2 → norm1 → ReLU, res_layer1..3, conv2 1×1), BasicBlock models/backbone/resnet.py:
+// 65-92 (conv3×3 → norm → ReLU → conv3×3 → norm, + identity or downsample(1×1/2 conv → norm),
+// ReLU), ResLayer resnet.py:676-771; the encoder is run on the real and the rendered image and
+// the context encoder on the rendered one (models/refiner/scflow_refiner.py:96-106).
+//
+// Kernels:
+//  * enc_conv_kernel — implicit GEMM on v_mfma_f32_32x32x2_f32 for every 1×1 / 3×3 conv of the
+//    residual stages.  Workgroup tile = TILE_M output pixels (whole output rows, width 32/64/128)
+//    × 64 output channels, 4 waves of 32×32 MFMA blocks.  K walks stages of 16 input channels;
+//    per stage the input HALO of the tile's rows — ((tr−1)·s + kh) × ((ow−1)·s + kw) pixels —
+//    is staged once in LDS (rows padded to 20 floats) together with the stage's weights for
+//    every tap, and all taps run out of LDS, with the next stage prefetched into registers.
+//    The previous InstanceNorm + ReLU is applied to the staged halo (per (image, channel) scale
+//    and shift; padding stays zero) so normalised activations are never written to HBM;
+//    the epilogue fuses bias, an eval-BatchNorm affine, the residual add and the activation
+//    (or a split tanh | relu for the context output).
+//  * enc_stem_kernel — the 3-channel 7×7/2 stem: lane = output channel with its 147 weights in
+//    VGPRs, the tile's input halo staged from the NCHW image in LDS and read as broadcasts.
+//  * enc_stats_kernel / enc_norm_finalize_kernel — InstanceNorm statistics in fp64 (partial sums
+//    over pixel chunks, deterministic order), → per (image, channel) scale/shift.
+//  * enc_apply_kernel — relu(norm(x) + identity') where the block output must be materialised
+//    (the next block's identity), float4-vectorised.
+#include "common.h"
+
+namespace {
+
+constexpr int EBN = 64;  // output channels per workgroup
+constexpr int EBK = 16;  // input channels per K stage
+constexpr int ELDA = EBK + 4;
+
+// float4 of the A halo per thread, worst case over tile widths tc = 16..TILE_M (tr = TILE_M/tc
+// output rows of tc pixels)
+constexpr int enc_na(int tm, int kh, int kw, int s) {
+  int m = 0;
+  for (int tc = 16; tc <= tm; tc *= 2) {
+    const int tr = tm / tc;
+    const int v = ((tr - 1) * s + kh) * ((tc - 1) * s + kw) * (EBK / 4);
+    if (v > m) m = v;
+  }
+  return (m + 255) / 256;
+}
+
+struct EncParams {
+  scflow_enc_conv_args a;
+  int oh, ow, tr, tc, hr, hc, nst;  // output size, tile rows × cols, halo rows × cols, K stages
+};
+
+template <int KH, int KW, int S, int TILE_M, bool NORM>
+__global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
+  constexpr int TAPS = KH * KW;
+  constexpr int RB = TILE_M / 64;
+  constexpr int NA = enc_na(TILE_M, KH, KW, S);
+  constexpr int NB = TAPS * EBN * (EBK / 4) / 256;
+  extern __shared__ float smem[];
+  const scflow_enc_conv_args& a = P.a;
+  const int hc = P.hc, ow = P.ow, tc = P.tc;
+  float* As = smem;                            // [hr*hc][ELDA]
+  float* Bs = smem + (size_t)P.hr * hc * ELDA;  // [TAPS][EBN][ELDA]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
+  const int tiles_x = ow / tc;
+  const int tiles_per_img = (P.oh / P.tr) * tiles_x;
+  const int img = blockIdx.x / tiles_per_img;
+  const int tin = blockIdx.x % tiles_per_img;
+  const int oy0 = (tin / tiles_x) * P.tr, ox0 = (tin % tiles_x) * tc;
+  const int n0 = blockIdx.y * EBN;
+  const int na = P.hr * hc * (EBK / 4);
+  const int cq = 4 * (tid & 3);  // this thread's 4 channels within every stage (stage-invariant)
+
+  int apix[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int idx = tid + 256 * j;
+    const int pix = idx >> 2;
+    const int hr = pix / hc, hcol = pix - hr * hc;
+    const int iy = oy0 * S - a.pad + hr, ix = ox0 * S - a.pad + hcol;
+    const bool ok = idx < na && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+    apix[j] = ok ? (img * a.h + iy) * a.w + ix : -1;
+  }
+
+  floatx4 ra[NA], rb[NB], rsc, rsh;
+  auto gload = [&](int s) {
+    const int c = s * EBK + cq;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (apix[j] >= 0) v = *(const floatx4*)(a.src + (size_t)apix[j] * a.s_in + c);
+      ra[j] = v;
+    }
+    if constexpr (NORM) {
+      rsc = *(const floatx4*)(a.in_scale + (size_t)img * a.cin + c);
+      rsh = *(const floatx4*)(a.in_shift + (size_t)img * a.cin + c);
+    }
+    const float* wb = a.weight + ((size_t)blockIdx.y * P.nst + s) * (TAPS * EBN * EBK);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) rb[j] = *(const floatx4*)(wb + (size_t)(tid + 256 * j) * 4);
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int idx = tid + 256 * j;
+      floatx4 v = ra[j];
+      if constexpr (NORM) {
+        if (apix[j] >= 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * rsc[e] + rsh[e], 0.f);
+        }
+      }
+      if (idx < na) *(floatx4*)(As + (idx >> 2) * ELDA + cq) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int idx = tid + 256 * j;
+      *(floatx4*)(Bs + (idx >> 2) * ELDA + 4 * (idx & 3)) = rb[j];
+    }
+  };
+
+  int abase[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const int m = wm * (TILE_M / 2) + r * 32 + li;
+    abase[r] = ((m / tc) * S * hc + (m % tc) * S) * ELDA + 4 * hh;
+  }
+  const int bbase = (wn * 32 + li) * ELDA + 4 * hh;
+
+  floatx16 acc[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
+
+  gload(0);
+  for (int s = 0; s < P.nst; ++s) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (s + 1 < P.nst) gload(s + 1);
+#pragma unroll
+    for (int ty = 0; ty < KH; ++ty) {
+#pragma unroll
+      for (int tx = 0; tx < KW; ++tx) {
+        const int aoff = (ty * hc + tx) * ELDA;
+        const float* Bb = Bs + (ty * KW + tx) * EBN * ELDA + bbase;
+#pragma unroll
+        for (int kb = 0; kb < EBK; kb += 8) {
+          floatx4 av[RB];
+#pragma unroll
+          for (int r = 0; r < RB; ++r) av[r] = *(const floatx4*)(As + abase[r] + aoff + kb);
+          const floatx4 b0 = *(const floatx4*)(Bb + kb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+              acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[r][e], b0[e], acc[r], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  const int col = n0 + wn * 32 + li;
+  if (col >= a.cout) return;
+  const float bias = a.bias ? a.bias[col] : 0.f;
+  const float osc = a.out_scale ? a.out_scale[col] : 1.f;
+  const float osh = a.out_scale ? a.out_shift[col] : 0.f;
+  const int act = col < a.act_split ? a.act : a.act2;
+#pragma unroll
+  for (int rr = 0; rr < RB; ++rr) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = wm * (TILE_M / 2) + rr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const int oy = oy0 + m / tc, ox = ox0 + m % tc;
+      const size_t pix = ((size_t)img * P.oh + oy) * ow + ox;
+      float v = acc[rr][r] + bias;
+      if (a.out_scale) v = v * osc + osh;
+      if (a.res) v += a.res[pix * a.s_res + col];
+      a.out[pix * a.s_out + col] = act_apply(v, act);
+    }
+  }
+}
+
+// packed weights: [npad/EBN][nst][taps][EBN][EBK]
+__global__ void enc_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,
+                                int cin, int taps, int nst, long long total) {
+  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * 256) {
+    long long r = idx;
+    const int k = (int)(r % EBK); r /= EBK;
+    const int col = (int)(r % EBN); r /= EBN;
+    const int tap = (int)(r % taps); r /= taps;
+    const int s = (int)(r % nst);
+    const int nt = (int)(r / nst);
+    const int o = nt * EBN + col, ci = s * EBK + k;
+    out[idx] = (o < cout && ci < cin) ? w[((size_t)o * cin + ci) * taps + tap] : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// stem: NCHW image → channels-last; tile = 32 consecutive output pixels of one row; wave w
+// takes channel group w % G (G = npad/64) and a share of the pixels.  packed [taps·cin][npad].
+// ------------------------------------------------------------------------------------------
+template <int CIN, int KH, int KW, int S>
+__global__ __launch_bounds__(256) void enc_stem_kernel(const float* __restrict__ img_in,
+                                                       const float* __restrict__ wpk,
+                                                       const float* __restrict__ bias,
+                                                       const float* __restrict__ osc_,
+                                                       const float* __restrict__ osh_,
+                                                       float* __restrict__ out, int h, int w,
+                                                       int oh, int ow, int cout, int npad, int pad,
+                                                       int act) {
+  constexpr int HCOLS = 31 * S + KW;
+  __shared__ float halo[KH][HCOLS][CIN];
+  const int tiles_x = (ow + 31) / 32;
+  const int t = blockIdx.x;
+  const int tx0 = (t % tiles_x) * 32;
+  const int oy = (t / tiles_x) % oh;
+  const int img = t / (tiles_x * oh);
+  for (int i = threadIdx.x; i < KH * HCOLS * CIN; i += 256) {
+    const int col = i % HCOLS, row = (i / HCOLS) % KH, c = i / (HCOLS * KH);
+    const int iy = oy * S - pad + row, ix = tx0 * S - pad + col;
+    float v = 0.f;
+    if (iy >= 0 && iy < h && ix >= 0 && ix < w) v = img_in[(((size_t)img * CIN + c) * h + iy) * w + ix];
+    halo[row][col][c] = v;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = npad / 64;
+  const int grp = wave % G;
+  const int pw_ = 32 / (4 / G);
+  const int p0 = (wave / G) * pw_;
+  const int co = grp * 64 + lane;
+  float wr[KH * KW * CIN];
+#pragma unroll
+  for (int k = 0; k < KH * KW * CIN; ++k) wr[k] = wpk[(size_t)k * npad + co];
+  const bool okc = co < cout;
+  const float b = (bias && okc) ? bias[co] : 0.f;
+  const float osc = (osc_ && okc) ? osc_[co] : 1.f;
+  const float osh = (osc_ && okc) ? osh_[co] : 0.f;
+  __syncthreads();
+  for (int p = p0; p < p0 + pw_; ++p) {
+    const int ox = tx0 + p;
+    if (ox >= ow) break;
+    float acc = 0.f;
+#pragma unroll
+    for (int ty = 0; ty < KH; ++ty)
+#pragma unroll
+      for (int tx = 0; tx < KW; ++tx)
+#pragma unroll
+        for (int c = 0; c < CIN; ++c) acc += wr[(ty * KW + tx) * CIN + c] * halo[ty][p * S + tx][c];
+    float v = acc + b;
+    if (osc_) v = v * osc + osh;
+    if (okc) out[((size_t)(img * oh + oy) * ow + ox) * cout + co] = act_apply(v, act);
+  }
+}
+
+__global__ void enc_stem_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,
+                                     int cin, int taps, int npad, long long total) {
+  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * 256) {
+    const int o = (int)(idx % npad);
+    const int k = (int)(idx / npad);
+    const int tap = k / cin, ci = k % cin;
+    out[idx] = o < cout ? w[((size_t)o * cin + ci) * taps + tap] : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// InstanceNorm statistics: grid (chunks, n); thread = 4 channels × a pixel lane; fp64 sums
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void enc_stats_kernel(const float* __restrict__ x, int hw, int c,
+                                                        int chunks, double* __restrict__ partial) {
+  __shared__ double red[2][256][4];
+  const int img = blockIdx.y, ch = blockIdx.x;
+  const int tpp = c / 4;          // threads per pixel
+  const int ppp = 256 / tpp;      // pixels per pass
+  const int q = threadIdx.x % tpp, ps = threadIdx.x / tpp;
+  const int p_begin = (int)((long long)hw * ch / chunks), p_end = (int)((long long)hw * (ch + 1) / chunks);
+  double s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (ps < ppp) {
+    const float* xb = x + (size_t)img * hw * c + 4 * q;
+    for (int p = p_begin + ps; p < p_end; p += ppp) {
+      const floatx4 v = *(const floatx4*)(xb + (size_t)p * c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[e] += (double)v[e];
+        s2[e] += (double)v[e] * (double)v[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][threadIdx.x][e] = s[e];
+    red[1][threadIdx.x][e] = s2[e];
+  }
+  __syncthreads();
+  // thread t < c: channel t = 4q + e, summed over the pixel slots in a fixed order
+  if (threadIdx.x < c) {
+    const int qq = threadIdx.x / 4, e = threadIdx.x % 4;
+    double a0 = 0, a1 = 0;
+    for (int k = 0; k < ppp; ++k) {
+      a0 += red[0][k * tpp + qq][e];
+      a1 += red[1][k * tpp + qq][e];
+    }
+    double* o = partial + (((size_t)img * chunks + ch) * 2) * c;
+    o[threadIdx.x] = a0;
+    o[c + threadIdx.x] = a1;
+  }
+}
+
+__global__ void enc_norm_finalize_kernel(const double* __restrict__ partial, int n, int chunks,
+                                         int c, int hw, float eps, float* __restrict__ scale,
+                                         float* __restrict__ shift) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * c) return;
+  const int img = i / c, ch = i % c;
+  double s = 0, s2 = 0;
+  for (int k = 0; k < chunks; ++k) {
+    const double* o = partial + (((size_t)img * chunks + k) * 2) * c;
+    s += o[ch];
+    s2 += o[c + ch];
+  }
+  const double mean = s / hw;
+  double var = s2 / hw - mean * mean;
+  if (var < 0) var = 0;
+  const float sc = (float)(1.0 / sqrt(var + (double)eps));
+  scale[i] = sc;
+  shift[i] = (float)(-mean) * sc;
+}
+
+__global__ __launch_bounds__(256) void enc_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ sc, const float* __restrict__ sh,
+    const float* __restrict__ id, const float* __restrict__ isc, const float* __restrict__ ish,
+    float* __restrict__ out, int hw, int c, long long total4) {
+  const int c4 = c / 4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const int cq = (int)(i % c4) * 4;
+    const long long pix = i / c4;
+    const int img = (int)(pix / hw);
+    const size_t so = (size_t)img * c + cq;
+    const floatx4 v = ((const floatx4*)x)[i];
+    const floatx4 a = *(const floatx4*)(sc + so), b = *(const floatx4*)(sh + so);
+    floatx4 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = v[e] * a[e] + b[e];
+    if (id) {
+      floatx4 u = ((const floatx4*)id)[i];
+      if (isc) {
+        const floatx4 ua = *(const floatx4*)(isc + so), ub = *(const floatx4*)(ish + so);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = u[e] * ua[e] + ub[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] += u[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = fmaxf(r[e], 0.f);
+    ((floatx4*)out)[i] = r;
+  }
+}
+
+int rup(int a, int b) { return (a + b - 1) / b * b; }
+
+template <int KH, int KW, int S, int TM, bool NORM>
+int launch_enc(EncParams p, hipStream_t st) {
+  p.tc = p.ow < TM ? p.ow : TM;
+  if (p.tc < 16 || TM % p.tc || p.ow % p.tc) return SCFLOW_EUNSUPPORTED;
+  p.tr = TM / p.tc;
+  if (p.oh % p.tr) return SCFLOW_EUNSUPPORTED;
+  p.hr = (p.tr - 1) * S + KH;
+  p.hc = (p.tc - 1) * S + KW;
+  const size_t lds = sizeof(float) * ((size_t)p.hr * p.hc * ELDA + (size_t)KH * KW * EBN * ELDA);
+  if ((size_t)p.hr * p.hc * (EBK / 4) > (size_t)256 * enc_na(TM, KH, KW, S)) return SCFLOW_EUNSUPPORTED;
+  static bool attr = false;
+  if (lds > 64 * 1024 && !attr) {
+    (void)hipFuncSetAttribute((const void*)enc_conv_kernel<KH, KW, S, TM, NORM>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  dim3 grid(p.a.n * (p.oh / p.tr) * (p.ow / p.tc), rup(p.a.cout, EBN) / EBN);
+  enc_conv_kernel<KH, KW, S, TM, NORM><<<grid, 256, lds, st>>>(p);
+  return scflow_launch_status();
+}
+
+template <int KH, int KW, int S, int TM>
+int launch_enc_norm(const EncParams& p, hipStream_t st) {
+  return p.a.in_scale ? launch_enc<KH, KW, S, TM, true>(p, st) : launch_enc<KH, KW, S, TM, false>(p, st);
+}
+
+}  // namespace
+
+SCFLOW_API long long scflow_enc_conv_packed_size(int cout, int cin, int kh, int kw) {
+  if (cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  return (long long)rup(cout, EBN) * rup(cin, EBK) * kh * kw;
+}
+
+SCFLOW_API int scflow_enc_conv_pack(const float* w_oihw, float* packed, int cout, int cin, int kh,
+                                    int kw, void* stream) {
+  if (!w_oihw || !packed || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  const long long total = scflow_enc_conv_packed_size(cout, cin, kh, kw);
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  enc_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, cin, kh * kw,
+                                                           rup(cin, EBK) / EBK, total);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_enc_conv(const scflow_enc_conv_args* args, void* stream) {
+  if (!args) return SCFLOW_EINVAL;
+  const scflow_enc_conv_args& a = *args;
+  if (!a.src || !a.weight || !a.out || a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 ||
+      a.cin <= 0 || a.pad < 0 || a.stride < 1 || a.s_in < a.cin || a.s_out < a.cout ||
+      (a.res && a.s_res < a.cout) || (!a.in_scale) != (!a.in_shift) ||
+      (!a.out_scale) != (!a.out_shift))
+    return SCFLOW_EINVAL;
+  if (a.cin % EBK) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(a.src) || (a.s_in & 3) || !aligned16(a.weight) ||
+      (a.in_scale && (!aligned16(a.in_scale) || !aligned16(a.in_shift))))
+    return SCFLOW_EALIGN;
+  EncParams p{};
+  p.a = a;
+  p.oh = (a.h + 2 * a.pad - a.kh) / a.stride + 1;
+  p.ow = (a.w + 2 * a.pad - a.kw) / a.stride + 1;
+  p.nst = a.cin / EBK;
+  if (p.oh <= 0 || p.ow <= 0) return SCFLOW_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (a.kh == 3 && a.kw == 3 && a.stride == 1) return launch_enc_norm<3, 3, 1, 128>(p, st);
+  if (a.kh == 3 && a.kw == 3 && a.stride == 2) return launch_enc_norm<3, 3, 2, 64>(p, st);
+  if (a.kh == 1 && a.kw == 1 && a.stride == 1) return launch_enc_norm<1, 1, 1, 128>(p, st);
+  if (a.kh == 1 && a.kw == 1 && a.stride == 2) return launch_enc_norm<1, 1, 2, 64>(p, st);
+  return SCFLOW_EUNSUPPORTED;
+}
+
+SCFLOW_API long long scflow_enc_stem_packed_size(int cout, int cin, int kh, int kw) {
+  if (cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  return (long long)kh * kw * cin * rup(cout, 64);
+}
+
+SCFLOW_API int scflow_enc_stem_pack(const float* w_oihw, float* packed, int cout, int cin, int kh,
+                                    int kw, void* stream) {
+  if (!w_oihw || !packed || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  const long long total = scflow_enc_stem_packed_size(cout, cin, kh, kw);
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  enc_stem_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, cin, kh * kw,
+                                                                rup(cout, 64), total);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_enc_stem(const float* img, const float* packed, const float* bias,
+                               const float* out_scale, const float* out_shift, float* out, int n,
+                               int cin, int h, int w, int cout, int kh, int kw, int stride,
+                               int pad, int act, void* stream) {
+  if (!img || !packed || !out || n <= 0 || h <= 0 || w <= 0 || cout <= 0 || pad < 0 ||
+      (!out_scale) != (!out_shift))
+    return SCFLOW_EINVAL;
+  const int npad = rup(cout, 64);
+  if (npad > 256 || npad == 192) return SCFLOW_EUNSUPPORTED;
+  const int oh = (h + 2 * pad - kh) / stride + 1, ow = (w + 2 * pad - kw) / stride + 1;
+  if (oh <= 0 || ow <= 0) return SCFLOW_EINVAL;
+  const unsigned tiles = (unsigned)((long long)n * oh * ((ow + 31) / 32));
+  hipStream_t st = (hipStream_t)stream;
+  if (cin == 3 && kh == 7 && kw == 7 && stride == 2) {
+    enc_stem_kernel<3, 7, 7, 2><<<tiles, 256, 0, st>>>(img, packed, bias, out_scale, out_shift, out,
+                                                       h, w, oh, ow, cout, npad, pad, act);
+    return scflow_launch_status();
+  }
+  if (cin == 3 && kh == 7 && kw == 7 && stride == 1) {
+    enc_stem_kernel<3, 7, 7, 1><<<tiles, 256, 0, st>>>(img, packed, bias, out_scale, out_shift, out,
+                                                       h, w, oh, ow, cout, npad, pad, act);
+    return scflow_launch_status();
+  }
+  return SCFLOW_EUNSUPPORTED;
+}
+
+SCFLOW_API int scflow_enc_stats(const float* x, int n, int hw, int c, int chunks, double* partial,
+                                void* stream) {
+  if (!x || !partial || n <= 0 || hw <= 0 || c <= 0 || chunks <= 0) return SCFLOW_EINVAL;
+  if (c % 4 || c > 256) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(x)) return SCFLOW_EALIGN;
+  dim3 grid(chunks, n);
+  enc_stats_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(x, hw, c, chunks, partial);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_enc_norm_finalize(const double* partial, int n, int chunks, int c, int hw,
+                                        float eps, float* scale, float* shift, void* stream) {
+  if (!partial || !scale || !shift || n <= 0 || chunks <= 0 || c <= 0 || hw <= 0) return SCFLOW_EINVAL;
+  enc_norm_finalize_kernel<<<ceil_div((long long)n * c, 256), 256, 0, (hipStream_t)stream>>>(
+      partial, n, chunks, c, hw, eps, scale, shift);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_enc_apply(const float* x, const float* scale, const float* shift,
+                                const float* id, const float* id_scale, const float* id_shift,
+                                float* out, int n, int hw, int c, void* stream) {
+  if (!x || !scale || !shift || !out || n <= 0 || hw <= 0 || c <= 0 ||
+      (!id_scale) != (!id_shift) || (id_scale && !id))
+    return SCFLOW_EINVAL;
+  if (c % 4) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(x) || !aligned16(out) || !aligned16(scale) || !aligned16(shift) ||
+      (id && !aligned16(id)) || (id_scale && (!aligned16(id_scale) || !aligned16(id_shift))))
+    return SCFLOW_EALIGN;
+  const long long total4 = (long long)n * hw * c / 4;
+  const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
+  enc_apply_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, scale, shift, id, id_scale, id_shift,
+                                                            out, hw, c, total4);
+  return scflow_launch_status();
+}

@@ -97,6 +97,11 @@ class SCFlowDecoder(nn.Module):
             return self._head_runner
         return None
 
+    @property
+    def hx_channels(self) -> int:
+        """Channels of the channels-last GRU working buffer: [h | cxt | motion | flow]."""
+        return self.h_channels + self.cxt_channels + self.encoder.out_channels[0] + 2
+
     def _side_stream(self, dev) -> torch.cuda.Stream:
         """A second HIP stream for the decoder's independent branches (created once per device)."""
         ss = getattr(self, "_streams", None)
@@ -124,7 +129,10 @@ class SCFlowDecoder(nn.Module):
                                  float(invalid_flow_num))
 
     def _forward(self, feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label, init_flow,
-                 invalid):
+                 invalid, hx: Optional[Tensor] = None):
+        """``hx``: optional channels-last [N·h·w, ≥ hc+xc+co+2] buffer whose first hc+xc channels
+        already hold tanh(h) | relu(cxt) (SCFlowRefiner writes the context encoder's output
+        there directly); h_feat / cxt_feat are then ignored."""
         dev = feat_render.device
         f32 = torch.float32
         feat_render = feat_render.contiguous().float()
@@ -135,7 +143,7 @@ class SCFlowDecoder(nn.Module):
         M = N * h * w
         hc, xc = self.h_channels, self.cxt_channels
         co = self.encoder.out_channels[0]
-        hx_c = hc + xc + co + 2
+        hx_c = self.hx_channels
         iters = int(self.iters)
 
         # a1 + a9 (once per forward)
@@ -147,9 +155,14 @@ class SCFlowDecoder(nn.Module):
         points = ops.lift_points(depth, K, R_prev, t_prev)
 
         # channels-last working set
-        HX = torch.empty(M, hx_c, device=dev, dtype=f32)
-        ops.nchw_into(h_feat.contiguous().float(), Chan(HX, 0, hc))
-        ops.nchw_into(cxt_feat.contiguous().float(), Chan(HX, hc, xc))
+        if hx is not None:
+            if hx.shape != (M, hx_c) or hx.dtype != f32 or not hx.is_contiguous():
+                raise ValueError(f"hx must be a contiguous float32 [{M}, {hx_c}] buffer")
+            HX = hx
+        else:
+            HX = torch.empty(M, hx_c, device=dev, dtype=f32)
+            ops.nchw_into(h_feat.contiguous().float(), Chan(HX, 0, hc))
+            ops.nchw_into(cxt_feat.contiguous().float(), Chan(HX, hc, xc))
         F2 = torch.empty(M, 2, device=dev, dtype=f32)
         K_look = self.num_levels * (2 * self.radius + 1) ** 2
         CORR = torch.empty(M, K_look, device=dev, dtype=f32)

@@ -326,3 +326,83 @@ def ph_heads(x: Tensor, m: int, k: int, Wr: Tensor, br: Tensor, rch: int, Wt: Te
         raise TypeError("label must be an int64 tensor on the same device")
     check(_lib.load().scflow_ph_heads(_p(x), m, k, _p(Wr), _p(br), rch, _p(Wt), _p(bt), _p(label),
                                       num_class, _p(drot), _p(dt), _stream(x)), "scflow_ph_heads")
+
+
+# ------------------------------------------------------------------------------- §8(f)-1 encoder
+def enc_conv_pack(weight: Tensor) -> Tensor:
+    _require(weight, "encoder conv weight", contiguous=False)
+    w = weight.detach().contiguous().float()
+    cout, cin, kh, kw = w.shape
+    lib = _lib.load()
+    size = lib.scflow_enc_conv_packed_size(cout, cin, kh, kw)
+    if size < 0:
+        check(int(size), "scflow_enc_conv_packed_size")
+    packed = torch.empty(size, device=w.device)
+    check(lib.scflow_enc_conv_pack(_p(w), _p(packed), cout, cin, kh, kw, _stream(w)),
+          "scflow_enc_conv_pack")
+    return packed
+
+
+def enc_stem_pack(weight: Tensor) -> Tensor:
+    _require(weight, "encoder stem weight", contiguous=False)
+    w = weight.detach().contiguous().float()
+    cout, cin, kh, kw = w.shape
+    lib = _lib.load()
+    packed = torch.empty(lib.scflow_enc_stem_packed_size(cout, cin, kh, kw), device=w.device)
+    check(lib.scflow_enc_stem_pack(_p(w), _p(packed), cout, cin, kh, kw, _stream(w)),
+          "scflow_enc_stem_pack")
+    return packed
+
+
+def enc_conv(src: Tensor, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int, cin: int,
+             cout: int, k: int, stride: int, pad: int, out: Tensor,
+             in_scale: Optional[Tensor] = None, in_shift: Optional[Tensor] = None,
+             out_scale: Optional[Tensor] = None, out_shift: Optional[Tensor] = None,
+             res: Optional[Tensor] = None, act: Optional[str] = None, act2: Optional[str] = None,
+             act_split: Optional[int] = None) -> None:
+    """One channels-last encoder conv (see scflow_enc_conv in include/scflow_hip.h)."""
+    _require(src, "src")
+    _require(out, "out")
+    a = _lib.EncConvArgs()
+    a.src, a.cin, a.s_in = src.data_ptr(), cin, src.shape[-1]
+    a.in_scale, a.in_shift = _p(in_scale), _p(in_shift)
+    a.weight, a.bias = packed.data_ptr(), _p(bias)
+    a.out_scale, a.out_shift = _p(out_scale), _p(out_shift)
+    a.res, a.s_res = _p(res), (res.shape[-1] if res is not None else 0)
+    a.out, a.s_out = out.data_ptr(), out.shape[-1]
+    a.n, a.h, a.w, a.cout, a.kh, a.kw, a.stride, a.pad = n, h, w, cout, k, k, stride, pad
+    a.act = _lib.SCFLOW_ACT[act]
+    a.act2 = _lib.SCFLOW_ACT[act2 if act2 is not None else act]
+    a.act_split = cout if act_split is None else act_split
+    check(_lib.load().scflow_enc_conv(ctypes.byref(a), _stream(out)), "scflow_enc_conv")
+
+
+def enc_stem(img: Tensor, packed: Tensor, bias: Optional[Tensor], cout: int, k: int, stride: int,
+             pad: int, out: Tensor, out_scale: Optional[Tensor] = None,
+             out_shift: Optional[Tensor] = None, act: Optional[str] = None) -> None:
+    _require(img, "image")
+    n, cin, h, w = img.shape
+    check(_lib.load().scflow_enc_stem(_p(img), _p(packed), _p(bias), _p(out_scale), _p(out_shift),
+                                      _p(out), n, cin, h, w, cout, k, k, stride, pad,
+                                      _lib.SCFLOW_ACT[act], _stream(img)), "scflow_enc_stem")
+
+
+def enc_instance_norm_stats(x: Tensor, n: int, hw: int, c: int, scale: Tensor, shift: Tensor,
+                            eps: float = 1e-5, partial: Optional[Tensor] = None) -> None:
+    """InstanceNorm2d(affine=False) statistics of channels-last x → per (image, channel) affine."""
+    chunks = max(1, min(64, hw // 256))
+    need = n * chunks * 2 * c
+    if partial is None or partial.numel() < need:
+        partial = torch.empty(need, dtype=torch.float64, device=x.device)
+    lib = _lib.load()
+    check(lib.scflow_enc_stats(_p(x), n, hw, c, chunks, _p(partial), _stream(x)), "scflow_enc_stats")
+    check(lib.scflow_enc_norm_finalize(_p(partial), n, chunks, c, hw, float(eps), _p(scale),
+                                       _p(shift), _stream(x)), "scflow_enc_norm_finalize")
+
+
+def enc_apply(x: Tensor, scale: Tensor, shift: Tensor, out: Tensor, n: int, hw: int, c: int,
+              id: Optional[Tensor] = None, id_scale: Optional[Tensor] = None,
+              id_shift: Optional[Tensor] = None) -> None:
+    check(_lib.load().scflow_enc_apply(_p(x), _p(scale), _p(shift), _p(id), _p(id_scale),
+                                       _p(id_shift), _p(out), n, hw, c, _stream(x)),
+          "scflow_enc_apply")

@@ -77,4 +77,5 @@ class Registry:
             target.register_module(name=key, module=cls, force=True)
 
 
-MODELS = Registry("model", locations=["scflow_amd.modules", "scflow_amd.decoder"])
+MODELS = Registry("model", locations=["scflow_amd.modules", "scflow_amd.decoder", "scflow_amd.encoder",
+                                       "scflow_amd.refiner"])

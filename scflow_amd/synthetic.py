@@ -125,6 +125,16 @@ def make_decoder_inputs(batch: int, size: int, seed: int = 0, feat_channels: int
     return out
 
 
+def make_images(batch: int, size: int, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Rendered / real image pair batch: rendered ~ U[0,1) (the config's
+    Normalize is mean 0 / std 255, scflow_ycbv_real.py:42-43, so images enter in [0, 1]),
+    real = rendered rolled by (3, −2) px plus N(0, 0.02) noise."""
+    rng = np.random.default_rng(seed + 7919)
+    render = rng.uniform(0.0, 1.0, (batch, 3, size, size))
+    real = np.roll(render, shift=(3, -2), axis=(2, 3)) + 0.02 * rng.standard_normal(render.shape)
+    return dict(render_images=render.astype(np.float32), real_images=real.astype(np.float32))
+
+
 def _param_rng(key: str, seed: int) -> np.random.Generator:
     return np.random.default_rng(zlib.crc32(key.encode()) ^ (seed * 0x9E3779B1 & 0xFFFFFFFF))
 
@@ -146,7 +156,11 @@ def param_value(key: str, shape: Tuple[int, ...], seed: int = 0) -> np.ndarray:
             base = np.tile(np.array([1.0, 0, 0, 0, 1.0, 0]), shape[0] // 6)
             return (base + 2e-2 * u).astype(np.float32)
         return (2e-2 * u).astype(np.float32)
-    if key.endswith(".gn.weight"):
+    if key.endswith("running_var"):  # encoder BatchNorm statistics (context encoder)
+        return (1.0 + 0.25 * u).astype(np.float32)
+    if key.endswith("running_mean"):
+        return (0.1 * u).astype(np.float32)
+    if key.endswith(".gn.weight") or (key.endswith("weight") and len(shape) == 1):
         return (1.0 + 0.1 * u).astype(np.float32)
     if key.endswith(".gn.bias") or key.endswith("bias"):
         return (0.1 * u).astype(np.float32)

@@ -91,6 +91,28 @@ class _Registry:
         return cls(**cfg)
 
 
+def _build_conv_layer(cfg, *args, **kwargs):
+    """mmcv build_conv_layer with cfg None / Conv2d → nn.Conv2d."""
+    assert cfg is None or cfg.get("type", "Conv2d") == "Conv2d"
+    return nn.Conv2d(*args, **kwargs)
+
+
+def _build_norm_layer(cfg, num_features, postfix=""):
+    """mmcv build_norm_layer: (abbr + postfix, layer); IN → InstanceNorm2d, BN → BatchNorm2d,
+    GN → GroupNorm; ``requires_grad`` dropped, eps defaults to 1e-5."""
+    cfg = dict(cfg)
+    typ = cfg.pop("type")
+    cfg.pop("requires_grad", None)
+    cfg.setdefault("eps", 1e-5)
+    if typ == "IN":
+        return f"in{postfix}", nn.InstanceNorm2d(num_features, **cfg)
+    if typ == "BN":
+        return f"bn{postfix}", nn.BatchNorm2d(num_features, **cfg)
+    if typ == "GN":
+        return f"gn{postfix}", nn.GroupNorm(num_channels=num_features, **cfg)
+    raise KeyError(typ)
+
+
 def _stub(name, **attrs):
     m = types.ModuleType(name)
     m.__dict__.update(attrs)
@@ -115,7 +137,8 @@ def _load(name, relpath):
 def load_reference():
     """Import the reference hot-path modules; returns a namespace of them."""
     _stub("mmcv")
-    _stub("mmcv.cnn", ConvModule=_ConvModule)
+    _stub("mmcv.cnn", ConvModule=_ConvModule, build_conv_layer=_build_conv_layer,
+          build_norm_layer=_build_norm_layer, build_plugin_layer=None)
     _stub("mmengine")
     _stub("mmengine.model", BaseModule=_BaseModule, Sequential=nn.Sequential)
     MODELS = _Registry()
@@ -139,8 +162,17 @@ def load_reference():
     rd = _load("models.decoder.raft_decoder", "models/decoder/raft_decoder.py")
     sd = _load("models.decoder.scflow_decoder", "models/decoder/scflow_decoder.py")
     ph = _load("models.head.pose_head", "models/head/pose_head.py")
+    _pkg("models.backbone", os.path.join(REF, "models/backbone"))
+    _pkg("models.encoder", os.path.join(REF, "models/encoder"))
+    _load("models.backbone.resnet", "models/backbone/resnet.py")
+    enc = _load("models.encoder.raft_encoder", "models/encoder/raft_encoder.py")
     return types.SimpleNamespace(MODELS=MODELS, corr_lookup=cl, pose=pose, raft=rd, scflow=sd,
-                                 pose_head=ph)
+                                 pose_head=ph, encoder=enc)
+
+
+# encoder blocks of configs/refine_models/scflow_ycbv_real.py:179-206
+def encoder_cfg(norm):
+    return dict(in_channels=3, out_channels=256, net_type="Basic", norm_cfg=dict(type=norm))
 
 
 # decoder block of configs/refine_models/scflow_ycbv_real.py:207-230
@@ -251,6 +283,64 @@ def gen_e2e(ref, out, B=2, S=256, iters=4):
     out["state_shapes"] = np.array([",".join(map(str, v.shape)) for v in dec.state_dict().values()])
 
 
+def build_encoder(ref, norm, seed):
+    enc = ref.encoder.RAFTEncoder(**encoder_cfg(norm))
+    synthetic.fill_module_(enc, seed=seed)
+    return enc.eval()
+
+
+def gen_enc(ref, out, B=1, S=128):
+    """Both encoders at 128² (features 16²); images regenerated from the seed in the test."""
+    imgs = synthetic.make_images(B, S, seed=5)
+    x = t32(imgs["render_images"])
+    out["sum_images"] = np.array([imgs["render_images"].astype(np.float64).sum()])
+    with torch.no_grad():
+        for norm, seed in (("IN", 1), ("BN", 2)):
+            enc = build_encoder(ref, norm, seed)
+            out[f"enc_{norm}"] = enc(x).numpy()
+            out[f"keys_{norm}"] = np.array(list(enc.state_dict().keys()))
+            out[f"shapes_{norm}"] = np.array([",".join(map(str, v.shape))
+                                              for v in enc.state_dict().values()])
+    out["meta"] = np.array([B, S, 5])
+
+
+def gen_refine(ref, out, B=2, S=256, iters=4):
+    """Images → encoders → decoder, the reference's SCFlowRefiner.get_pose data flow
+    (scflow_refiner.py:108-138 with extract_feat :84-106; seperate_encoder=False shares one
+    feature encoder, base_refiner.py:33-40).  Encoder seed 1, context seed 2, decoder seed 0."""
+    imgs = synthetic.make_images(B, S, seed=13)
+    scene = synthetic.make_scene(B, S, seed=13)
+    enc, ctx = build_encoder(ref, "IN", 1), build_encoder(ref, "BN", 2)
+    dec = ref.MODELS.build(dict(type=ref.scflow.SCFlowDecoder, **decoder_cfg(ref, iters)))
+    synthetic.fill_module_(dec, seed=0)
+    dec.eval()
+    render, real = t32(imgs["render_images"]), t32(imgs["real_images"])
+    with torch.no_grad():
+        real_feat = enc(real)
+        render_feat = enc(render)
+        cxt = ctx(render)
+        h_feat, cxt_feat = torch.split(cxt, [128, 128], dim=1)
+        h_feat, cxt_feat = torch.tanh(h_feat), torch.relu(cxt_feat)
+        init_flow = torch.zeros(B, 2, S, S)
+        res = dec(render_feat, real_feat, h_feat, cxt_feat, t32(scene["ref_rotation"]),
+                  t32(scene["ref_translation"]), t32(scene["depth"]), t32(scene["internel_k"]),
+                  init_flow=init_flow, label=t32(scene["labels"]), invalid_flow_num=0.)
+    flow_pose, flow_pred, Rs, ts, masks, drs, dts = res
+    out["sum_images"] = np.array([imgs["render_images"].astype(np.float64).sum(),
+                                  imgs["real_images"].astype(np.float64).sum()])
+    for k, v in (("render_feat", render_feat), ("real_feat", real_feat), ("h_feat", h_feat),
+                 ("cxt_feat", cxt_feat)):
+        out[f"stat_{k}"] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    out["render_feat_s0c0"] = render_feat[0, :8].numpy()
+    out["cxt_feat_s1"] = cxt_feat[1, :8].numpy()
+    out["flow_pose_last"] = flow_pose[-1].numpy()
+    out["flow_pred_last"] = flow_pred[-1].numpy()
+    out["R"] = torch.stack(Rs).numpy()
+    out["t"] = torch.stack(ts).numpy()
+    out["flow_pred_absmean"] = np.array([f.abs().double().mean().item() for f in flow_pred])
+    out["meta"] = np.array([B, S, iters, 13])
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = load_reference()
@@ -260,7 +350,13 @@ def main():
     e2e = {}
     gen_e2e(ref, e2e)
     np.savez_compressed(os.path.join(HERE, "golden_e2e_b2_s256_it4.npz"), **e2e)
-    for name, d in (("ops", ops), ("e2e", e2e)):
+    enc = {}
+    gen_enc(ref, enc)
+    np.savez_compressed(os.path.join(HERE, "golden_enc_b1_s128.npz"), **enc)
+    rf = {}
+    gen_refine(ref, rf)
+    np.savez_compressed(os.path.join(HERE, "golden_refine_b2_s256_it4.npz"), **rf)
+    for name, d in (("ops", ops), ("e2e", e2e), ("enc", enc), ("refine", rf)):
         print(name, {k: getattr(v, "shape", None) for k, v in d.items()})
 
 

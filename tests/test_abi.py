@@ -49,26 +49,33 @@ def test_host_side_queries_need_no_gpu():
     # argument errors return codes, they do not crash
     assert lib.scflow_corr_pyramid(None, None, None, 1, 1, 8, 8, 4, None) == -1
     assert lib.scflow_conv2d(None, None) == -1
+    # encoder conv packing: 3×3 96→96 (cout padded to 128), stem 7×7·3 → 64
+    assert lib.scflow_enc_conv_packed_size(96, 96, 3, 3) == 128 * 96 * 9
+    assert lib.scflow_enc_stem_packed_size(64, 3, 7, 7) == 147 * 64
+    assert lib.scflow_enc_conv(None, None) == -1
 
 
-def test_struct_layout_matches_header(tmp_path):
-    """ctypes ConvArgs has the C compiler's size and field offsets for scflow_conv_args."""
+@pytest.mark.parametrize("pyname,cname", [("ConvArgs", "scflow_conv_args"),
+                                           ("EncConvArgs", "scflow_enc_conv_args")])
+def test_struct_layout_matches_header(tmp_path, pyname, cname):
+    """ctypes argument structs have the C compiler's size and field offsets."""
     import shutil
     import subprocess
-    from scflow_amd._lib import ConvArgs
+    from scflow_amd import _lib
+    S = getattr(_lib, pyname)
     cc = shutil.which("gcc") or shutil.which("cc")
     if cc is None:
         pytest.skip("no C compiler")
-    fields = [f for f, _ in ConvArgs._fields_]
+    fields = [f for f, _ in S._fields_]
     prog = tmp_path / "layout.c"
     prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "scflow_hip.h"\nint main(){\n'
-                    'printf("%zu\\n", sizeof(scflow_conv_args));\n' +
-                    "".join(f'printf("%zu\\n", offsetof(scflow_conv_args, {f}));\n' for f in fields) +
+                    f'printf("%zu\\n", sizeof({cname}));\n' +
+                    "".join(f'printf("%zu\\n", offsetof({cname}, {f}));\n' for f in fields) +
                     "return 0;}\n")
     exe = tmp_path / "layout"
     subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
                                            check=True).stdout.split()]
-    assert vals[0] == ctypes.sizeof(ConvArgs)
+    assert vals[0] == ctypes.sizeof(S)
     for f, off in zip(fields, vals[1:]):
-        assert getattr(ConvArgs, f).offset == off, f
+        assert getattr(S, f).offset == off, f

@@ -79,3 +79,37 @@ def test_decoder_e2e_matches_reference():
     np.testing.assert_allclose(masks[-1].numpy(), g["mask_last"], atol=1e-5)
     # the fixture is not degenerate: the pose moves and the flow is non-trivial
     assert g["flow_pose_absmean"][-1] > 0.05
+
+
+@pytest.mark.parametrize("norm,seed", [("IN", 1), ("BN", 2)])
+def test_raft_encoder_matches_reference(norm, seed):
+    """RAFTEncoder 'Basic' (feature encoder IN / context encoder BN eval) at 128²."""
+    from scflow_amd import synthetic
+    from tests.helpers import encoder_state_dict
+    g = golden("enc")
+    B, S, iseed = (int(v) for v in g["meta"])
+    x = t(synthetic.make_images(B, S, seed=iseed)["render_images"])
+    assert abs(float(x.double().sum()) - float(g["sum_images"][0])) < 1e-6
+    out = orc.raft_encoder(encoder_state_dict(norm, seed), x, norm)
+    np.testing.assert_allclose(out.numpy(), g[f"enc_{norm}"], rtol=1e-4, atol=1e-4)
+
+
+def test_refine_e2e_matches_reference():
+    """Images → encoders → decoder (B=2, 256², 4 iters): mean EPE ≤ 1e-3 px vs the reference."""
+    from tests.helpers import refine_inputs, refiner_state_dict
+    g = golden("refine")
+    B, S, iters, seed = (int(v) for v in g["meta"])
+    inp = refine_inputs(B, S, seed, g)
+    sd = refiner_state_dict()
+    render, real, h, c = orc.extract_feat(sd, inp["render_images"], inp["real_images"])
+    for k, v in (("render_feat", render), ("real_feat", real), ("h_feat", h), ("cxt_feat", c)):
+        got = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        np.testing.assert_allclose(got, g[f"stat_{k}"], rtol=1e-4)
+    np.testing.assert_allclose(render[0, :8].numpy(), g["render_feat_s0c0"], rtol=1e-4, atol=1e-4)
+    dsd = {k: v for k, v in sd.items() if not k.startswith(("real_encoder.", "render_encoder.", "context."))}
+    fp, fpred, Rs, ts, *_ = orc.decoder_forward(
+        dsd, render, real, h, c, inp["ref_rotation"], inp["ref_translation"], inp["depth"],
+        inp["internel_k"], label=inp["label"], init_flow=torch.zeros(B, 2, S, S), iters=iters)
+    assert float(orc.cal_epe_mean(t(g["flow_pose_last"]), fp[-1]).max()) <= 1e-3
+    assert float(orc.cal_epe_mean(t(g["flow_pred_last"]), fpred[-1]).max()) <= 1e-3
+    np.testing.assert_allclose(torch.stack(ts).numpy(), g["t"], rtol=1e-5, atol=1e-3)
