@@ -13,8 +13,10 @@ SURVEY.md §8(e)); ``value`` = all pairs·iterations of all ranks ÷ the slowest
 
 Extra JSON fields:
 * ``roofline``: the dominant kernel, ``conv_mfma_kernel<GRU_ZR>`` (the fused z|r SepConvGRU
-  convolution: 2 launches per iteration, 16.1 GFLOP each at B=16), timed live with HIP events
-  around each of its launches in the timed region; bound = fp32 MFMA, peak 157.3 TFLOP/s.
+  convolution: 2 launches per iteration; with the loop-invariant context contribution hoisted
+  out of the loop it contracts h and the motion features, 2·M·256·5·256 = 10.7 GFLOP per launch
+  at B=16), timed live with HIP events around each of its launches in the timed region;
+  bound = fp32 MFMA, peak 157.3 TFLOP/s.
 * ``cpu_baseline``: the CPU oracle (oracle/scflow_oracle.py, a parity-pinned PyTorch-CPU
   restatement of the reference decoder) on a bounded sample, rank 0 at N=1 only.
 """
@@ -59,10 +61,50 @@ def make_inputs(batch, size, seed, device):
     return out
 
 
-def gru_zr_flops(batch, size, hc=128, x_ch=256, taps=5):
-    """Algorithmic FLOPs of one fused z|r launch: 2·M·(2·hc)·(taps·(hc+x))."""
-    m = batch * (size // 8) ** 2
-    return 2.0 * m * (2 * hc) * taps * (hc + x_ch)
+def encoder_cfg(norm):
+    # configs/refine_models/scflow_ycbv_real.py:179-206
+    return dict(type="RAFTEncoder", in_channels=3, out_channels=256, net_type="Basic",
+                norm_cfg=dict(type=norm))
+
+
+def build_refiner(iters, device, feat=None):
+    """SCFlowRefiner (shared IN feature encoder, BN context encoder, decoder), random-init."""
+    from scflow_amd import MODELS, synthetic
+    r = MODELS.build(dict(type="SCFlowRefiner", cxt_channels=128, h_channels=128,
+                          seperate_encoder=False, encoder=encoder_cfg("IN"),
+                          cxt_encoder=encoder_cfg("BN"), decoder=decoder_cfg(iters, feat)))
+    synthetic.fill_module_(r)
+    return r.to(device).eval()
+
+
+def make_refine_inputs(batch, size, seed, device):
+    from scflow_amd import synthetic
+    raw = {**synthetic.make_images(batch, size, seed=seed), **synthetic.make_scene(batch, size, seed)}
+    out = {k: torch.from_numpy(v).to(device) for k, v in raw.items()}
+    out["label"] = out.pop("labels")
+    out.pop("init_flow", None)
+    return out
+
+
+def time_steps(step, steps, warmup, world, dev):
+    """Warmup, then time exactly `steps` calls between barrier + synchronize; max over ranks."""
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def cpu_baseline(seconds: float, iters: int, size: int):
@@ -98,6 +140,10 @@ def main():
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-batch", type=int, default=32,
+                    help="pairs/GPU of the extra end-to-end (images → encoders → decoder) "
+                         "measurement, BASELINE configs[2]; 0 disables it")
+    ap.add_argument("--e2e-steps", type=int, default=5)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_gru_zr.json"),
                     help="HBM bytes per launch of the dominant kernel from a rocprofv3 PMC pass")
     args = ap.parse_args()
@@ -144,10 +190,25 @@ def main():
         elapsed = float(t.item())
     dec.kernel_hooks.clear()
 
+    e2e = None
+    if args.e2e_batch > 0:
+        ref = build_refiner(args.iters, dev, feat)
+        rin = make_refine_inputs(args.e2e_batch, args.size, seed=1000 + rank, device=dev)
+        el2 = time_steps(lambda: ref.get_pose(**rin), args.e2e_steps, 2, world, dev)
+        e2e = {"workload": f"SCFlowRefiner.get_pose: images -> shared IN feature encoder (2 images/pair) "
+                           f"+ BN context encoder + decoder, {args.e2e_batch} pairs/GPU, "
+                           f"{args.size}x{args.size}, {args.iters} iters (BASELINE configs[2], "
+                           f"jittered synthetic poses in place of PoseCNN init)",
+               "value": round(world * args.e2e_batch * args.iters * args.e2e_steps / el2, 2),
+               "unit": "iters/s", "ms_per_step": round(el2 / args.e2e_steps * 1e3, 3),
+               "steps": args.e2e_steps, "warmup": 2}
+        del ref, rin
+
     units = world * args.batch * args.iters * args.steps
     value = units / elapsed
     zr_ms = timer.mean_ms()
-    flops = gru_zr_flops(args.batch, args.size)
+    flops = dec.gru.zr_flops(args.batch * (args.size // 8) ** 2,
+                             dec.cxt_channels if dec.hoist_context else 0)
     achieved = flops / (zr_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -185,6 +246,8 @@ def main():
                          "avg_launch_ms": round(zr_ms, 4), "launches": timer.count(),
                          "flops_per_launch": flops},
         }
+        if e2e is not None:
+            res["end_to_end"] = e2e
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.iters, args.size)
         print(json.dumps(res), flush=True)

@@ -87,6 +87,10 @@ typedef struct scflow_conv_args {
   float* gate; int sg;                   /* GRU z buffer and its pixel stride                  */
   float* rh; int srh;                    /* GRU_ZR: r·h output                                 */
   float* hid; int sh;                    /* GRU: hidden state (read by ZR, updated by Q)       */
+  const float* bias_map; int sbm;        /* optional per-pixel additive term [pix][sbm] (MFMA  */
+                                         /* variant): pre-activation += bias_map[pix·sbm + o]; */
+                                         /* the decoder passes the loop-invariant context      */
+                                         /* contribution of the GRU convs here                 */
 } scflow_conv_args;
 
 /* Number of floats of the packed weight buffer; w_oihw is nn.Conv2d's [cout][c0+c1][kh][kw]. */

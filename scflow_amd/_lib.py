@@ -34,6 +34,7 @@ class ConvArgs(ctypes.Structure):
         ("gate", c_vp), ("sg", c_int),
         ("rh", c_vp), ("srh", c_int),
         ("hid", c_vp), ("sh", c_int),
+        ("bias_map", c_vp), ("sbm", c_int),
     ]
 
 

@@ -216,36 +216,67 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
     }
   }
 
-  // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  // All global reads (bias map, h, z) are issued before any store: the stores may alias them
+  // as far as the compiler knows, so interleaving would serialise every read's latency.
   const int col = n0 + wn * 32 + li;
   if (col >= a.cout) return;
   const float bias = a.bias ? a.bias[col] : 0.f;
+  size_t pixv[RB][16];
 #pragma unroll
-  for (int rr = 0; rr < RB; ++rr) {
+  for (int rr = 0; rr < RB; ++rr)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = wm * (TILE_M / 2) + rr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      const int oy = oy0 + m / ow, ox = m % ow;
-      const size_t pix = ((size_t)img * P.oh + oy) * ow + ox;
-      const float v = acc[rr][r] + bias;
-      if constexpr (EPI == SCFLOW_EPI_PLAIN) {
-        a.out[pix * a.so + col] = act_apply(v, a.act);
-      } else if constexpr (EPI == SCFLOW_EPI_GRU_ZR) {
-        const int hcn = a.cout >> 1;
-        const float g = sigmoidf_(v);
-        if (col < hcn) {
-          a.gate[pix * a.sg + col] = g;
-        } else {
-          const int c = col - hcn;
-          a.rh[pix * a.srh + c] = g * a.hid[pix * a.sh + c];
-        }
-      } else {  // GRU_Q
-        const float q = tanhf(v);
-        const float z = a.gate[pix * a.sg + col];
-        const float h = a.hid[pix * a.sh + col];
-        a.hid[pix * a.sh + col] = (1.f - z) * h + z * q;
-      }
+      pixv[rr][r] = ((size_t)img * P.oh + oy0 + m / ow) * ow + m % ow;
     }
+  if (a.bias_map) {
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[rr][r] += a.bias_map[pixv[rr][r] * a.sbm + col];
+  }
+  if constexpr (EPI == SCFLOW_EPI_PLAIN) {
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a.out[pixv[rr][r] * a.so + col] = act_apply(acc[rr][r] + bias, a.act);
+  } else if constexpr (EPI == SCFLOW_EPI_GRU_ZR) {
+    const int hcn = a.cout >> 1;
+    if (col < hcn) {
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a.gate[pixv[rr][r] * a.sg + col] = sigmoidf_(acc[rr][r] + bias);
+    } else {
+      const int c = col - hcn;
+      float hv[RB][16];
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hv[rr][r] = a.hid[pixv[rr][r] * a.sh + c];
+#pragma unroll
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          a.rh[pixv[rr][r] * a.srh + c] = sigmoidf_(acc[rr][r] + bias) * hv[rr][r];
+    }
+  } else {  // GRU_Q
+    float zv[RB][16], hv[RB][16];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        zv[rr][r] = a.gate[pixv[rr][r] * a.sg + col];
+        hv[rr][r] = a.hid[pixv[rr][r] * a.sh + col];
+      }
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float q = tanhf(acc[rr][r] + bias);
+        a.hid[pixv[rr][r] * a.sh + col] = (1.f - zv[rr][r]) * hv[rr][r] + zv[rr][r] * q;
+      }
   }
 }
 
@@ -636,7 +667,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
       default: return dispatch_mfma<SCFLOW_EPI_PLAIN>(p, g, st);
     }
   }
-  if (a.epilogue != SCFLOW_EPI_PLAIN) return SCFLOW_EUNSUPPORTED;
+  if (a.epilogue != SCFLOW_EPI_PLAIN || a.bias_map) return SCFLOW_EUNSUPPORTED;
   const long long M = (long long)a.n * g.oh * g.ow;
   if (g.variant == V_SMALLCIN) {
     const unsigned tiles = (unsigned)((long long)a.n * g.oh * ((g.ow + 31) / 32));

@@ -85,6 +85,8 @@ class SCFlowDecoder(nn.Module):
         self._head_runner = None
         # optional per-kernel timing hooks (bench.py): name -> callable(start: bool)
         self.kernel_hooks: Dict[str, object] = {}
+        # compute the context features' (loop-invariant) GRU contribution once per forward
+        self.hoist_context = True
 
     # ------------------------------------------------------------------ helpers
     def _hidden_heads(self):
@@ -163,6 +165,8 @@ class SCFlowDecoder(nn.Module):
             HX = torch.empty(M, hx_c, device=dev, dtype=f32)
             ops.nchw_into(h_feat.contiguous().float(), Chan(HX, 0, hc))
             ops.nchw_into(cxt_feat.contiguous().float(), Chan(HX, hc, xc))
+        # loop-invariant context share of the GRU pre-activations (once per forward)
+        ctx_map = self.gru.context_map(Chan(HX, hc, xc), N, h, w) if self.hoist_context else None
         F2 = torch.empty(M, 2, device=dev, dtype=f32)
         K_look = self.num_levels * (2 * self.radius + 1) ** 2
         CORR = torch.empty(M, K_look, device=dev, dtype=f32)
@@ -248,7 +252,7 @@ class SCFlowDecoder(nn.Module):
             run_chain(self.encoder.out_net, Chan.whole(MF), hx_motion, N, h, w, s_out)
             # a4 GRU (in place on HX[:, :hc])
             self.gru.step(Chan.whole(HX), Chan.whole(Z), Chan.whole(RH), N, h, w,
-                          hooks=self.kernel_hooks)
+                          hooks=self.kernel_hooks, ctx_map=ctx_map, cxt_channels=xc)
             # a5 heads
             if head_runner is not None:
                 head_runner.run(hid, Chan.whole(HEAD), N, h, w)

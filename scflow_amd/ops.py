@@ -155,9 +155,10 @@ def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1) 
 def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int, cout: int,
            kh: int, kw: int, ph: int, pw: int, act: Optional[str] = None, out: Optional[Chan] = None,
            src1: Optional[Chan] = None, epilogue: int = _lib.EPI_PLAIN, gate: Optional[Chan] = None,
-           rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1) -> None:
+           rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1,
+           bias_map: Optional[Chan] = None) -> None:
     for nm, ch in (("src0", src0), ("src1", src1), ("out", out), ("gate", gate), ("rh", rh),
-                   ("hid", hid)):
+                   ("hid", hid), ("bias_map", bias_map)):
         if ch is not None:
             _require(ch.buf, nm)
     _require(packed, "packed weight")
@@ -181,6 +182,8 @@ def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w
         a.rh, a.srh = rh.ptr, rh.stride
     if hid is not None:
         a.hid, a.sh = hid.ptr, hid.stride
+    if bias_map is not None:
+        a.bias_map, a.sbm = bias_map.ptr, bias_map.stride
     check(_lib.load().scflow_conv2d(ctypes.byref(a), _stream(src0.buf)), "scflow_conv2d")
 
 

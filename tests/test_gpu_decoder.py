@@ -72,9 +72,13 @@ def test_decoder_matches_reference_golden():
 
 
 @pytest.mark.gpu
-def test_decoder_matches_oracle_b4_8iters():
+@pytest.mark.parametrize("hoist", [True, False])
+def test_decoder_matches_oracle_b4_8iters(hoist):
+    """hoist: the context's GRU contribution computed once per forward (default) or the
+    reference's full-width GRU convs every iteration."""
     inp = decoder_inputs(4, 256, seed=21)
     dec = build_decoder(8, seed=1)
+    dec.hoist_context = hoist
     out = run_gpu(dec, inp)
     sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
     ref = orc.decoder_forward(sd, **inp, iters=8)

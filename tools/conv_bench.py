@@ -27,6 +27,11 @@ SHAPES = [
     ("gru q 1x5 128+256->128", 128, 256, 128, (1, 5), (0, 2), "Tanh", "q"),
     ("gru zr 5x1 384->256", 384, 0, 256, (5, 1), (2, 0), "Sigmoid", "zr"),
     ("gru q 5x1 128+256->128", 128, 256, 128, (5, 1), (2, 0), "Tanh", "q"),
+    ("gru zr 1x5 128+128->256 +map", 128, 128, 256, (1, 5), (0, 2), "Sigmoid", "zrm"),
+    ("gru q 1x5 128+128->128 +map", 128, 128, 128, (1, 5), (0, 2), "Tanh", "qm"),
+    ("gru zr 5x1 128+128->256 +map", 128, 128, 256, (5, 1), (2, 0), "Sigmoid", "zrm"),
+    ("gru q 5x1 128+128->128 +map", 128, 128, 128, (5, 1), (2, 0), "Tanh", "qm"),
+    ("gru ctx map 1x5 128->384", 128, 0, 384, (1, 5), (0, 2), None, None),
     ("heads 3x3 128->512", 128, 0, 512, (3, 3), (1, 1), "ReLU", None),
     ("flow_pred 3x3 256->2", 256, 0, 2, (3, 3), (1, 1), None, None),
     ("mask_pred 1x1 256->1", 256, 0, 1, (1, 1), (0, 0), "Sigmoid", None),
@@ -54,13 +59,17 @@ def main():
         x1 = torch.randn(M, c1, device=dev) if c1 else None
         r = ConvRunner([conv], act)
         kw = {}
+        bmap = torch.randn(M, 768, device=dev) if epi in ("zrm", "qm") else None
+        if epi in ("zrm", "qm"):
+            kw["bias_map"] = Chan(bmap, 0, 256 if epi == "zrm" else 128)
+            epi = epi[:-1]
         if epi == "zr":
             hid = torch.randn(M, 128, device=dev)
-            kw = dict(epilogue=EPI_GRU_ZR, gate=Chan.whole(torch.empty(M, 128, device=dev)),
+            kw.update(epilogue=EPI_GRU_ZR, gate=Chan.whole(torch.empty(M, 128, device=dev)),
                       rh=Chan.whole(torch.empty(M, 128, device=dev)), hid=Chan.whole(hid))
             out = None
         elif epi == "q":
-            kw = dict(epilogue=EPI_GRU_Q, gate=Chan.whole(torch.rand(M, 128, device=dev)),
+            kw.update(epilogue=EPI_GRU_Q, gate=Chan.whole(torch.rand(M, 128, device=dev)),
                       hid=Chan.whole(torch.randn(M, 128, device=dev)))
             out = None
         else:
