@@ -144,6 +144,11 @@ def main():
                     help="pairs/GPU of the extra end-to-end (images → encoders → decoder) "
                          "measurement, BASELINE configs[2]; 0 disables it")
     ap.add_argument("--e2e-steps", type=int, default=5)
+    ap.add_argument("--no-kernel-timer", action="store_true",
+                    help="do not bracket the roofline kernel (throughput without timer overhead)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay a captured hipGraph per step instead of launching kernel by kernel "
+                         "(measured slower on MI355X/ROCm 7: 14.38k vs 14.66k iters/s)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_gru_zr.json"),
                     help="HBM bytes per launch of the dominant kernel from a rocprofv3 PMC pass")
     args = ap.parse_args()
@@ -157,7 +162,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from scflow_amd import MODELS, synthetic
-    from scflow_amd.profiling import KernelTimer
+    from scflow_amd.profiling import EventTimer, KernelTimer
 
     feat = (args.size // 8, args.size // 8) if args.size != 256 else None
     dec = MODELS.build(decoder_cfg(args.iters, feat))
@@ -165,36 +170,40 @@ def main():
     dec = dec.to(dev).eval()
     inp = make_inputs(args.batch, args.size, seed=rank, device=dev)
 
-    def step():
-        return dec(**inp, invalid_flow_num=0.0)
+    timer = KernelTimer() if args.graph else EventTimer()
+    timer.enabled = False
+    if not args.no_kernel_timer:
+        dec.kernel_hooks["gru_zr"] = timer
+    if not args.graph:
+        def step():
+            return dec(**inp, invalid_flow_num=0.0)
+        for _ in range(args.warmup):
+            step()
+        timer.enabled = True
+    else:
+        # one hipGraph per forward: captured after `warmup` eager passes, replayed per step
+        from scflow_amd.graph import GraphedForward
 
-    for _ in range(args.warmup):
-        step()
-    timer = KernelTimer()
-    dec.kernel_hooks["gru_zr"] = timer
+        def arm():
+            timer.enabled = True
+        g = GraphedForward(dec, inp, warmup=args.warmup, before_capture=arm, invalid_flow_num=0.0)
+        step = g.replay
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = time_steps(step, args.steps, 0, world, dev)
+    timer.enabled = False
     dec.kernel_hooks.clear()
 
     e2e = None
     if args.e2e_batch > 0:
         ref = build_refiner(args.iters, dev, feat)
         rin = make_refine_inputs(args.e2e_batch, args.size, seed=1000 + rank, device=dev)
-        el2 = time_steps(lambda: ref.get_pose(**rin), args.e2e_steps, 2, world, dev)
+        if not args.graph:
+            el2 = time_steps(lambda: ref.get_pose(**rin), args.e2e_steps, 2, world, dev)
+        else:
+            from scflow_amd.graph import GraphedForward
+            g2 = GraphedForward(ref, rin, warmup=2, fn=ref.get_pose)
+            el2 = time_steps(g2.replay, args.e2e_steps, 0, world, dev)
+            del g2
         e2e = {"workload": f"SCFlowRefiner.get_pose: images -> shared IN feature encoder (2 images/pair) "
                            f"+ BN context encoder + decoder, {args.e2e_batch} pairs/GPU, "
                            f"{args.size}x{args.size}, {args.iters} iters (BASELINE configs[2], "
@@ -238,6 +247,7 @@ def main():
             "config": {"workload": f"SCFlowDecoder forward, {args.batch} pairs/GPU, "
                                    f"{args.size}x{args.size}, {args.iters} GRU iters (BASELINE configs[1])",
                        "global_batch": args.batch * world, "image": args.size, "iters": args.iters,
+                       "launch": "hipGraph replay" if args.graph else "eager",
                        "parallelism": f"dp{world}"},
             "roofline": {"kernel": "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r conv)",
                          "bound": "mfma", "achieved": round(achieved, 2),

@@ -218,6 +218,13 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
                      const float* id_scale, const float* id_shift, float* out, int n, int hw,
                      int c, void* stream);
 
+/* Profiling helper (bench.py roofline timing; no reference equivalent): a one-thread kernel
+ * that stores the GPU's constant-rate wall clock (s_memrealtime) into stamps[idx].  Enqueued on
+ * the stream of the kernel being timed, before and after it; as an ordinary kernel it is also a
+ * node of a captured hipGraph, so every replay re-stamps.  scflow_wallclock_khz: its rate. */
+int scflow_timestamp(unsigned long long* stamps, int idx, void* stream);
+long long scflow_wallclock_khz(void);
+
 #ifdef __cplusplus
 }
 #endif

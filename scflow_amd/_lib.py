@@ -96,6 +96,8 @@ SIGNATURES = {
     "scflow_enc_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "scflow_enc_norm_finalize": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp]),
     "scflow_enc_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_timestamp": (c_int, [c_vp, c_int, c_vp]),
+    "scflow_wallclock_khz": (c_ll, []),
 }
 
 _lib = None

@@ -356,3 +356,23 @@ SCFLOW_API const char* scflow_strerror(int code) {
     default: return hipGetErrorString((hipError_t)code);
   }
 }
+
+// ------------------------------------------------------------------------------------------
+// profiling helper: GPU wall-clock timestamps as graph-capturable kernel nodes
+// ------------------------------------------------------------------------------------------
+__global__ void timestamp_kernel(unsigned long long* stamps, int idx) {
+  stamps[idx] = __builtin_amdgcn_s_memrealtime();
+}
+
+SCFLOW_API int scflow_timestamp(unsigned long long* stamps, int idx, void* stream) {
+  if (!stamps || idx < 0) return SCFLOW_EINVAL;
+  timestamp_kernel<<<1, 1, 0, (hipStream_t)stream>>>(stamps, idx);
+  return scflow_launch_status();
+}
+
+SCFLOW_API long long scflow_wallclock_khz(void) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return SCFLOW_EINVAL;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return SCFLOW_EINVAL;
+  return khz;
+}

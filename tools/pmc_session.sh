@@ -16,5 +16,5 @@ run() {  # name, counters..., -- cmd
 }
 run conv_p1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -- python3 $R/tools/conv_bench.py --reps 3 || exit 1
 run conv_p2 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU -- python3 $R/tools/conv_bench.py --reps 3 || exit 1
-run bench_fetch FETCH_SIZE -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline || exit 1
-run bench_write WRITE_SIZE -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline || exit 1
+run bench_fetch FETCH_SIZE -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --e2e-batch 0 || exit 1
+run bench_write WRITE_SIZE -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --e2e-batch 0 || exit 1
