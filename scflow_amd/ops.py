@@ -357,17 +357,23 @@ def enc_stem_pack(weight: Tensor) -> Tensor:
     return packed
 
 
-def enc_conv(src: Tensor, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int, cin: int,
+def enc_conv(src, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int, cin: int,
              cout: int, k: int, stride: int, pad: int, out: Tensor,
              in_scale: Optional[Tensor] = None, in_shift: Optional[Tensor] = None,
              out_scale: Optional[Tensor] = None, out_shift: Optional[Tensor] = None,
              res: Optional[Tensor] = None, act: Optional[str] = None, act2: Optional[str] = None,
              act_split: Optional[int] = None) -> None:
-    """One channels-last encoder conv (see scflow_enc_conv in include/scflow_hip.h)."""
-    _require(src, "src")
+    """One channels-last MFMA conv (see scflow_enc_conv in include/scflow_hip.h); ``src`` is a
+    contiguous channels-last tensor or a ``Chan`` (channel slice with its pixel stride)."""
+    if isinstance(src, Chan):
+        _require(src.buf, "src")
+        sptr, sstride = src.ptr, src.stride
+    else:
+        _require(src, "src")
+        sptr, sstride = src.data_ptr(), src.shape[-1]
     _require(out, "out")
     a = _lib.EncConvArgs()
-    a.src, a.cin, a.s_in = src.data_ptr(), cin, src.shape[-1]
+    a.src, a.cin, a.s_in = sptr, cin, sstride
     a.in_scale, a.in_shift = _p(in_scale), _p(in_shift)
     a.weight, a.bias = packed.data_ptr(), _p(bias)
     a.out_scale, a.out_shift = _p(out_scale), _p(out_shift)
