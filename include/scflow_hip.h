@@ -91,12 +91,19 @@ typedef struct scflow_conv_args {
                                          /* variant): pre-activation += bias_map[pix·sbm + o]; */
                                          /* the decoder passes the loop-invariant context      */
                                          /* contribution of the GRU convs here                 */
+  int bk;                                /* K-stage depth the weights were packed for: 0 or 16 */
+                                         /* (default) or 8 — see scflow_conv_pick_bk           */
 } scflow_conv_args;
 
-/* Number of floats of the packed weight buffer; w_oihw is nn.Conv2d's [cout][c0+c1][kh][kw]. */
+/* Number of floats of the packed weight buffer (the same for bk 8 and 16); w_oihw is
+ * nn.Conv2d's [cout][c0+c1][kh][kw]. */
 long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, int kw, int stride, int w);
+/* bk: K-stage depth to pack for (0 → 16, or 8); pass the same value in scflow_conv_args.bk. */
 int scflow_conv_pack_weights(const float* w_oihw, float* packed, int cout, int c0, int c1, int kh,
-                             int kw, int stride, int w, void* stream);
+                             int kw, int stride, int w, int bk, void* stream);
+/* Preferred K-stage depth (8 or 16) for this launch shape (batch, sizes, channels, kernel):
+ * 8 when the grid needs more resident workgroups than 16-deep stages' LDS allows. */
+int scflow_conv_pick_bk(const scflow_conv_args* args);
 int scflow_conv2d(const scflow_conv_args* args, void* stream);
 
 /* a8: R_dst = R(ortho6d Δ)·R_src; t_z' = t_z/exp(Δt_z) (depth_transform 0) or t_z·(Δt_z+1) (1);

@@ -12,7 +12,8 @@ import os
 
 import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libscflow_hip.so")
+LIB_PATH = os.environ.get("SCFLOW_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                       "lib", "libscflow_hip.so")
 
 c_int, c_float, c_ll, c_vp = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ctypes.c_void_p
 
@@ -35,6 +36,7 @@ class ConvArgs(ctypes.Structure):
         ("rh", c_vp), ("srh", c_int),
         ("hid", c_vp), ("sh", c_int),
         ("bias_map", c_vp), ("sbm", c_int),
+        ("bk", c_int),
     ]
 
 
@@ -63,7 +65,8 @@ SIGNATURES = {
                                    c_int, c_vp]),
     "scflow_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     "scflow_conv_pack_weights": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                         c_vp]),
+                                         c_int, c_vp]),
+    "scflow_conv_pick_bk": (c_int, [ctypes.POINTER(ConvArgs)]),
     "scflow_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_vp]),
     "scflow_pose_update": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp]),
     "scflow_lift_points": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),

@@ -29,3 +29,4 @@ __device__ __forceinline__ float act_apply(float v, int act) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
+

@@ -20,9 +20,10 @@
 //    is a channel concat without a copy (GRU cat[h,x] / cat[r·h,x], MotionEncoder cat[c,f]).
 //    Epilogues: bias+act; GRU ZR writes z and r·h; GRU Q computes h ← (1−z)·h + z·tanh(q) in
 //    place (the reference's three ConvModules + elementwise ops in two launches).
-//  * conv_smallcin — cin ≤ 4 (7×7 2→128 flow encoders, 3×3 1→64 mask encoder): one LANE per
-//    output channel with its kh·kw·cin weights in VGPRs, the pixel tile's input halo in LDS and
-//    read as wave-uniform broadcasts; stores are 64 contiguous channels per pixel.
+//  * conv_smallcin — cin ≤ 4 (7×7 2→128 flow encoders, 3×3 1→64 mask encoder): on MFMA with
+//    K = taps·cin in k-pairs (conv_smallcin_mfma_kernel) for W ∈ {32, 64}; otherwise one LANE
+//    per output channel with its kh·kw·cin weights in VGPRs, the input halo in LDS read as
+//    wave-uniform broadcasts.
 //  * conv_thin — cout ≤ 4 (flow head 3×3 256→2, mask head 1×1 256→1): one LANE per output
 //    pixel, channels streamed through an LDS halo in chunks of 32, weights wave-uniform.
 #include "common.h"
@@ -33,8 +34,8 @@ namespace {
 
 constexpr int BM = 128;  // output pixels per workgroup (mfma)
 constexpr int BN = 64;   // output channels per workgroup (mfma)
-constexpr int BK = 16;   // input channels per K-stage (mfma)
-constexpr int LDA = BK + 4;
+constexpr int BK = 16;   // default input channels per K-stage (mfma); 8 on request (scflow_conv_args.bk)
+constexpr int CPAD = 16; // each source's channels are padded to a multiple of 16 (either depth)
 constexpr int THIN_CC = 32;        // channels per LDS chunk (thin)
 constexpr int THIN_LD = THIN_CC + 4;
 
@@ -80,19 +81,19 @@ Geometry select_variant(int cout, int c0, int c1, int kh, int kw, int stride, in
   if (g.oh % g.tr) return g;
   g.hr = g.tr + kh - 1;
   g.hc = g.ow + kw - 1;
-  g.cp0 = round_up(c0, BK);
-  g.cp1 = round_up(c1, BK);
+  g.cp0 = round_up(c0, CPAD);
+  g.cp1 = round_up(c1, CPAD);
   g.nst = (g.cp0 + g.cp1) / BK;
   g.ktot = g.taps * (g.cp0 + g.cp1);
   g.npad = round_up(cout, BN);
-  g.lds = sizeof(float) * ((size_t)g.hr * g.hc * LDA + (size_t)g.taps * BN * LDA);
   g.variant = V_MFMA;
   return g;
 }
 
 // ------------------------------------------------------------------------------------------
 // MFMA implicit-GEMM conv
-// packed weights: [npad/BN][nst][taps][BN][BK] — one contiguous block per (n-tile, stage)
+// packed weights: [npad/BN][nst][taps][BN][bk] — one contiguous block per (n-tile, stage),
+// bk = the stage depth the weights are packed for (16 by default, 8 on request)
 // ------------------------------------------------------------------------------------------
 struct MfmaParams {
   scflow_conv_args a;
@@ -100,21 +101,26 @@ struct MfmaParams {
 };
 
 // max float4 of the A halo per thread over the supported widths (32, 64)
-constexpr int na_max(int bm, int kh, int kw) {
-  const int a32 = (bm / 32 + kh - 1) * (32 + kw - 1) * (BK / 4);
-  const int a64 = ((bm / 64 > 0 ? bm / 64 : 1) + kh - 1) * (64 + kw - 1) * (BK / 4);
+constexpr int na_max(int bm, int kh, int kw, int bk) {
+  const int a32 = (bm / 32 + kh - 1) * (32 + kw - 1) * (bk / 4);
+  const int a64 = ((bm / 64 > 0 ? bm / 64 : 1) + kh - 1) * (64 + kw - 1) * (bk / 4);
   const int m = a32 > a64 ? a32 : a64;
   return (m + 255) / 256;
 }
 
 // TILE_M output pixels × BN channels per workgroup; 4 waves as 2 (M) × 2 (N); each wave owns
 // TILE_M/2 pixels (RB = TILE_M/64 row blocks of 32) × 32 channels.
-template <int EPI, int KH, int KW, int TILE_M>
+// BKS = stage depth: 16 (fewer barriers per MFMA) or 8 (half the LDS, so more workgroups are
+// resident when the grid needs it; the weights must then be packed with bk = 8).
+template <int EPI, int KH, int KW, int TILE_M, int BKS>
 __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
+  constexpr int BK = BKS;
+  constexpr int LDA = BK + 4;
   constexpr int TAPS = KH * KW;
   constexpr int RB = TILE_M / 64;
-  constexpr int NA = na_max(TILE_M, KH, KW);
-  constexpr int NB = TAPS * BN * (BK / 4) / 256;  // = TAPS
+  constexpr int NA = na_max(TILE_M, KH, KW, BK);
+  constexpr int NBT = TAPS * BN * (BK / 4);  // float4 of one stage's weights
+  constexpr int NB = (NBT + 255) / 256;
   extern __shared__ float smem[];
   const scflow_conv_args& a = P.a;
   const int hc = P.hc, ow = P.ow;
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     const int idx = tid + 256 * j;
-    const int q = idx & 3, pix = idx >> 2;
+    const int q = idx % (BK / 4), pix = idx / (BK / 4);
     const int hr = pix / hc, hcol = pix - hr * hc;
     const int iy = oy0 - a.ph + hr, ix = hcol - a.pw;
     const bool ok = idx < na && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
@@ -158,18 +164,19 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
     }
     const float* wb = a.weight + ((size_t)blockIdx.y * P.nst + s) * (TAPS * BN * BK);
 #pragma unroll
-    for (int j = 0; j < NB; ++j) rb[j] = *(const floatx4*)(wb + (size_t)(tid + 256 * j) * 4);
+    for (int j = 0; j < NB; ++j)
+      if (NBT % 256 == 0 || tid + 256 * j < NBT) rb[j] = *(const floatx4*)(wb + (size_t)(tid + 256 * j) * 4);
   };
   auto lstore = [&]() {
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int idx = tid + 256 * j;
-      if (idx < na) *(floatx4*)(As + (idx >> 2) * LDA + 4 * (idx & 3)) = ra[j];
+      if (idx < na) *(floatx4*)(As + (idx / (BK / 4)) * LDA + 4 * (idx % (BK / 4))) = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int idx = tid + 256 * j;
-      *(floatx4*)(Bs + (idx >> 2) * LDA + 4 * (idx & 3)) = rb[j];
+      if (NBT % 256 == 0 || idx < NBT) *(floatx4*)(Bs + (idx / (BK / 4)) * LDA + 4 * (idx % (BK / 4))) = rb[j];
     }
   };
 
@@ -326,6 +333,73 @@ __global__ __launch_bounds__(256) void conv_smallcin_kernel(scflow_conv_args a, 
 #pragma unroll
         for (int c = 0; c < CIN; ++c) acc += wr[(ty * KW + tx) * CIN + c] * halo[ty][p + tx][c];
     if (co < a.cout) a.out[((size_t)(img * oh + oy) * ow + ox) * a.so + co] = act_apply(acc, a.act);
+  }
+}
+
+// small-cin conv on MFMA: K = taps·cin (≤ 98) walked in k-pairs — one v_mfma_f32_32x32x2_f32
+// per pair (for cin = 2 a pair is the two channels of one tap, for cin = 1 two taps).  Tile =
+// 64 output pixels (64/W whole rows) × npad (64 or 128) channels; 4 waves as 2 (M) × 2 (N), each
+// 32 px × npad/2 channels.  The tile's input halo (rows+kh−1)×(W+kw−1)×cin sits in LDS; the
+// wave's B fragments (its columns' weights for every k) are loaded once into VGPRs from the
+// small-cin packing [taps·cin][npad].
+template <int CIN, int KH, int KW, int NBW>
+__global__ __launch_bounds__(256) void conv_smallcin_mfma_kernel(scflow_conv_args a, int oh, int ow,
+                                                                 int npad) {
+  constexpr int K = KH * KW * CIN;
+  constexpr int KP = (K + 1) / 2;  // MFMA k-steps
+  extern __shared__ float halo[];  // [(tr+KH-1)][(ow+KW-1)][CIN]
+  const int tr = 64 / ow;
+  const int hc = ow + KW - 1, hr = tr + KH - 1;
+  const int tiles_per_img = oh / tr;
+  const int img = blockIdx.x / tiles_per_img;
+  const int oy0 = (blockIdx.x % tiles_per_img) * tr;
+  for (int i = threadIdx.x; i < hr * hc * CIN; i += 256) {
+    const int c = i % CIN, col = (i / CIN) % hc, row = i / (CIN * hc);
+    const int iy = oy0 - a.ph + row, ix = col - a.pw;
+    float v = 0.f;
+    if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) v = a.src0[((size_t)(img * a.h + iy) * a.w + ix) * a.s0 + c];
+    halo[i] = v;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
+  // B fragments: k = 2·kp + hh, column = wn·NBW·32 + nb·32 + li
+  float bw[NBW][KP];
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const int k = 2 * kp + hh;
+      bw[nb][kp] = k < K ? a.weight[(size_t)k * npad + (wn * NBW + nb) * 32 + li] : 0.f;
+    }
+  __syncthreads();
+  const int m = wm * 32 + li;  // this lane's A row (output pixel of the tile)
+  const int pbase = ((m / ow) * hc + (m % ow)) * CIN;
+  floatx16 acc[NBW];
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[nb][e] = 0.f;
+#pragma unroll
+  for (int kp = 0; kp < KP; ++kp) {
+    const int k = 2 * kp + hh;
+    const int tap = (k < K ? k : 0) / CIN, c = (k < K ? k : 0) % CIN;
+    const float av = k < K ? halo[pbase + ((tap / KW) * hc + tap % KW) * CIN + c] : 0.f;
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb)
+      acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw[nb][kp], acc[nb], 0, 0, 0);
+  }
+  // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb) {
+    const int col = (wn * NBW + nb) * 32 + li;
+    if (col >= a.cout) continue;
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const size_t pix = ((size_t)img * oh + oy0 + mm / ow) * ow + mm % ow;
+      a.out[pix * a.so + col] = act_apply(acc[nb][r] + b, a.act);
+    }
   }
 }
 
@@ -516,20 +590,20 @@ __global__ __launch_bounds__(256) void conv_thin_generic(scflow_conv_args a, int
 // packing: w_oihw [cout][cin][kh][kw] → variant layout
 __global__ void pack_kernel(const float* __restrict__ w, float* __restrict__ out, int variant,
                             int cout, int c0, int c1, int kh, int kw, int cp0, int nst, int npad,
-                            long long total) {
+                            int bk, long long total) {
   const int cin = c0 + c1, taps = kh * kw;
   for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
     float v = 0.f;
     if (variant == V_MFMA) {
       // [nt][s][tap][col][k]
       long long r = idx;
-      const int k = (int)(r % BK); r /= BK;
+      const int k = (int)(r % bk); r /= bk;
       const int col = (int)(r % BN); r /= BN;
       const int tap = (int)(r % taps); r /= taps;
       const int s = (int)(r % nst);
       const int nt = (int)(r / nst);
       const int o = nt * BN + col;
-      const int kc = s * BK + k;  // channel index in the padded concat space
+      const int kc = s * bk + k;  // channel index in the padded concat space
       int ci = -1;
       if (kc < cp0) {
         if (kc < c0) ci = kc;
@@ -569,29 +643,83 @@ int pick_tile_m(long long m, int ntiles) {
   return 64;
 }
 
+size_t mfma_lds(int hr, int hc, int taps, int bk) {
+  return sizeof(float) * ((size_t)hr * hc + (size_t)taps * BN) * (bk + 4);
+}
+
+// Stage depth for a launch: 16 (fewer barriers per MFMA) unless the grid needs more resident
+// workgroups than 16-deep stages' LDS allows and 8-deep ones would take fewer rounds
+// (measured on the decoder's 3×3 256→192 conv at B=16: 768 workgroups, 2 per CU at 16 =
+// 1.5 rounds; 85 → 101 TFLOP/s at 8).  Resident workgroups per CU are capped by VGPRs at
+// 2 (128-pixel tiles) / 3 (64).  SCFLOW_CONV_BK=8|16 forces one (tuning only).
+int pick_bk(int kh, int kw, int tm, int hr, int hc, long long wgs, int cus) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("SCFLOW_CONV_BK");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 8 || forced == 16) return forced;
+  auto rounds = [&](int bk) {
+    long long per_cu = (long long)(160 * 1024 / mfma_lds(hr, hc, kh * kw, bk));
+    const long long cap = tm == 64 ? 3 : 2;
+    if (per_cu > cap) per_cu = cap;
+    if (per_cu < 1) per_cu = 1;
+    return (wgs + per_cu * cus - 1) / (per_cu * cus);
+  };
+  return rounds(8) < rounds(16) ? 8 : 16;
+}
+
+int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// tile rows / halo rows / tile size for a launch (shared by the launcher and scflow_conv_pick_bk)
+int launch_tile(const scflow_conv_args& a, const Geometry& g, int* tr, int* hr) {
+  const long long m = (long long)a.n * g.oh * g.ow;
+  const int tm = (pick_tile_m(m, g.npad / BN) == 64 && g.ow <= 64) ? 64 : 128;
+  *tr = tm / g.ow;
+  *hr = *tr + a.kh - 1;
+  return tm;
+}
+
+template <int EPI, int KH, int KW, int TM, int BKS>
+int launch_mfma_bk(MfmaParams p, Geometry g, hipStream_t st) {
+  p.nst = (g.cp0 + g.cp1) / BKS;
+  const size_t lds = mfma_lds(g.hr, g.hc, g.taps, BKS);
+  static bool attr = false;
+  if (lds > 64 * 1024 && !attr) {
+    (void)hipFuncSetAttribute((const void*)conv_mfma_kernel<EPI, KH, KW, TM, BKS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  dim3 grid(p.a.n * (g.oh / g.tr), g.npad / BN);
+  conv_mfma_kernel<EPI, KH, KW, TM, BKS><<<grid, 256, lds, st>>>(p);
+  return scflow_launch_status();
+}
+
 template <int EPI, int KH, int KW, int TM>
 int launch_mfma_tm(MfmaParams p, Geometry g, hipStream_t st) {
   g.tr = TM / g.ow;
   if (g.tr < 1 || g.oh % g.tr) return SCFLOW_EUNSUPPORTED;
   g.hr = g.tr + KH - 1;
-  g.lds = sizeof(float) * ((size_t)g.hr * g.hc * LDA + (size_t)g.taps * BN * LDA);
   p.tr = g.tr;
   p.hr = g.hr;
-  static bool attr = false;
-  if (g.lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)conv_mfma_kernel<EPI, KH, KW, TM>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  dim3 grid(p.a.n * (g.oh / g.tr), g.npad / BN);
-  conv_mfma_kernel<EPI, KH, KW, TM><<<grid, 256, g.lds, st>>>(p);
-  return scflow_launch_status();
+  if (p.a.bk == 8) return launch_mfma_bk<EPI, KH, KW, TM, 8>(p, g, st);
+  return launch_mfma_bk<EPI, KH, KW, TM, 16>(p, g, st);
 }
 
 template <int EPI, int KH, int KW>
 int launch_mfma(const MfmaParams& p, const Geometry& g, hipStream_t st) {
-  const long long m = (long long)p.a.n * g.oh * g.ow;
-  if (pick_tile_m(m, g.npad / BN) == 64 && g.ow <= 64) return launch_mfma_tm<EPI, KH, KW, 64>(p, g, st);
+  int tr, hr;
+  if (launch_tile(p.a, g, &tr, &hr) == 64) return launch_mfma_tm<EPI, KH, KW, 64>(p, g, st);
   return launch_mfma_tm<EPI, KH, KW, 128>(p, g, st);
 }
 
@@ -617,16 +745,33 @@ SCFLOW_API long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, i
 }
 
 SCFLOW_API int scflow_conv_pack_weights(const float* w_oihw, float* packed, int cout, int c0,
-                                        int c1, int kh, int kw, int stride, int w, void* stream) {
+                                        int c1, int kh, int kw, int stride, int w, int bk,
+                                        void* stream) {
   if (!w_oihw || !packed || cout <= 0 || c0 <= 0 || c1 < 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  if (bk == 0) bk = BK;
+  if (bk != 8 && bk != 16) return SCFLOW_EINVAL;
   Geometry g = select_variant(cout, c0, c1, kh, kw, stride, w == 64 ? 64 : 32 * 4, w, (kh - 1) / 2,
                               (kw - 1) / 2);
   if (g.variant == V_NONE) return SCFLOW_EUNSUPPORTED;
   const long long total = (long long)g.npad * g.ktot;
   const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
   pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, g.variant, cout, c0, c1, kh,
-                                                       kw, g.cp0, g.nst, g.npad, total);
+                                                       kw, g.cp0, (g.cp0 + g.cp1) / bk, g.npad, bk,
+                                                       total);
   return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_conv_pick_bk(const scflow_conv_args* args) {
+  if (!args) return SCFLOW_EINVAL;
+  const scflow_conv_args& a = *args;
+  if (a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 || a.c1 < 0) return SCFLOW_EINVAL;
+  Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
+  if (g.variant != V_MFMA) return BK;  // other variants ignore the stage depth
+  int tr, hr;
+  const int tm = launch_tile(a, g, &tr, &hr);
+  if (tr < 1 || g.oh % tr) return BK;
+  const long long wgs = (long long)a.n * (g.oh / tr) * (g.npad / BN);
+  return pick_bk(a.kh, a.kw, tm, hr, g.hc, wgs, device_cus());
 }
 
 SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
@@ -644,6 +789,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
   } else {
     return SCFLOW_EINVAL;
   }
+  if (a.bk != 0 && a.bk != 8 && a.bk != 16) return SCFLOW_EINVAL;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
   if (g.variant == V_NONE) return SCFLOW_EUNSUPPORTED;
   if (g.oh <= 0 || g.ow <= 0) return SCFLOW_EINVAL;
@@ -670,6 +816,24 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
   if (a.epilogue != SCFLOW_EPI_PLAIN || a.bias_map) return SCFLOW_EUNSUPPORTED;
   const long long M = (long long)a.n * g.oh * g.ow;
   if (g.variant == V_SMALLCIN) {
+    const bool mfma_ok = (g.ow == 32 || g.ow == 64) && g.ow == a.w && g.oh == a.h &&
+                         g.oh % (64 / g.ow) == 0 && (g.npad == 64 || g.npad == 128);
+    if (mfma_ok) {
+      const unsigned blocks = (unsigned)(a.n * (g.oh / (64 / g.ow)));
+      const size_t lds = sizeof(float) * (size_t)(64 / g.ow + a.kh - 1) * (g.ow + a.kw - 1) * a.c0;
+#define SCFLOW_SCM(CI, KH_, KW_)                                                                   \
+  if (a.c0 == CI && a.kh == KH_ && a.kw == KW_) {                                                  \
+    if (g.npad == 128)                                                                             \
+      conv_smallcin_mfma_kernel<CI, KH_, KW_, 2><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad);  \
+    else                                                                                           \
+      conv_smallcin_mfma_kernel<CI, KH_, KW_, 1><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad);  \
+    return scflow_launch_status();                                                                 \
+  }
+      SCFLOW_SCM(2, 7, 7)
+      SCFLOW_SCM(1, 3, 3)
+      SCFLOW_SCM(2, 3, 3)
+#undef SCFLOW_SCM
+    }
     const unsigned tiles = (unsigned)((long long)a.n * g.oh * ((g.ow + 31) / 32));
     if (g.npad == 64 || g.npad == 128 || g.npad == 256) {
       if (a.c0 == 2 && a.kh == 7 && a.kw == 7) {

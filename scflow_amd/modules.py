@@ -100,6 +100,7 @@ class ConvRunner:
 
     The packed copy is cached and re-packed whenever a weight's data pointer or version
     changes (optimizer step, load_state_dict, .to())."""
+    force_bk = 0  # 8 / 16 overrides the library's per-launch K-stage depth (tuning only)
 
     def __init__(self, convs: Sequence[nn.Conv2d], act: Optional[str], split: Optional[int] = None,
                  in_select: Optional[Sequence[Tuple[int, int]]] = None, with_bias: bool = True):
@@ -129,8 +130,8 @@ class ConvRunner:
             conv._scflow_runner = r
         return r
 
-    def packed(self, c0: int, c1: int, w: int) -> Tuple[Tensor, Optional[Tensor]]:
-        key = (c0, c1, w) + tuple((c.weight.data_ptr(), c.weight._version,
+    def packed(self, c0: int, c1: int, w: int, bk: int = 16) -> Tuple[Tensor, Optional[Tensor]]:
+        key = (c0, c1, w, bk) + tuple((c.weight.data_ptr(), c.weight._version,
                                    None if c.bias is None else (c.bias.data_ptr(), c.bias._version))
                                   for c in self.convs)
         if key != self._key:
@@ -138,7 +139,7 @@ class ConvRunner:
                 else self.convs[0].weight.detach()
             if self.in_select is not None:
                 wt = torch.cat([wt[:, a:b] for a, b in self.in_select], 1).contiguous()
-            self._packed = ops.pack_conv_weight(wt.float(), c0, c1, w, self.stride)
+            self._packed = ops.pack_conv_weight(wt.float(), c0, c1, w, self.stride, bk)
             if not self.with_bias:
                 self._bias = None
             elif all(c.bias is not None for c in self.convs):
@@ -157,10 +158,17 @@ class ConvRunner:
         c1 = 0 if src1 is None else src1.c
         if src0.c + c1 != self.cin:
             raise ValueError(f"conv expects {self.cin} input channels, got {src0.c}+{c1}")
-        packed, bias = self.packed(src0.c, c1, w)
+        shape = (n, h, w, src0.c, c1)
+        if ConvRunner.force_bk:  # tuning / A-B only
+            self._bk_shape, self._bk = shape, ConvRunner.force_bk
+        if getattr(self, "_bk_shape", None) != shape:  # host-only query, once per launch shape
+            self._bk = ops.conv_pick_bk(n, h, w, src0.c, c1, self.cout, self.kh, self.kw, self.ph,
+                                        self.pw, self.stride)
+            self._bk_shape = shape
+        packed, bias = self.packed(src0.c, c1, w, self._bk)
         ops.conv2d(src0, packed, bias, n, h, w, self.cout, self.kh, self.kw, self.ph, self.pw,
                    self.act, out=out, src1=src1, epilogue=epilogue, gate=gate, rh=rh, hid=hid,
-                   stride=self.stride, bias_map=bias_map)
+                   stride=self.stride, bias_map=bias_map, bk=self._bk)
 
     def flops(self, m: int) -> float:
         """Algorithmic FLOPs of one launch over m output pixels (2·m·cout·taps·cin)."""

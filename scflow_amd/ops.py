@@ -135,8 +135,8 @@ def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: i
 
 
 # ------------------------------------------------------------------------------- convolutions
-def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1) -> Tensor:
-    """Pack an nn.Conv2d weight ``[cout, c0+c1, kh, kw]`` for scflow_conv2d."""
+def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1, bk: int = 16) -> Tensor:
+    """Pack an nn.Conv2d weight ``[cout, c0+c1, kh, kw]`` for scflow_conv2d (K-stage depth bk)."""
     _require(weight, "conv weight", contiguous=False)
     weight = weight.detach().contiguous()
     cout, cin, kh, kw = weight.shape
@@ -147,16 +147,28 @@ def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1) 
     if size < 0:
         raise ScflowError(f"no conv kernel for cout={cout} cin={c0}+{c1} k={kh}x{kw} w={w}")
     packed = torch.empty(size, device=weight.device, dtype=torch.float32)
-    check(lib.scflow_conv_pack_weights(_p(weight), _p(packed), cout, c0, c1, kh, kw, stride, w,
+    check(lib.scflow_conv_pack_weights(_p(weight), _p(packed), cout, c0, c1, kh, kw, stride, w, bk,
                                        _stream(weight)), "scflow_conv_pack_weights")
     return packed
+
+
+def conv_pick_bk(n: int, h: int, w: int, c0: int, c1: int, cout: int, kh: int, kw: int, ph: int,
+                 pw: int, stride: int = 1) -> int:
+    """The library's preferred K-stage depth (8 or 16) for this launch shape (host-only query)."""
+    a = _lib.ConvArgs()
+    a.c0, a.c1, a.n, a.h, a.w = c0, c1, n, h, w
+    a.cout, a.kh, a.kw, a.ph, a.pw, a.stride = cout, kh, kw, ph, pw, stride
+    bk = _lib.load().scflow_conv_pick_bk(ctypes.byref(a))
+    if bk not in (8, 16):
+        check(bk if bk < 0 else -2, "scflow_conv_pick_bk")
+    return bk
 
 
 def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int, cout: int,
            kh: int, kw: int, ph: int, pw: int, act: Optional[str] = None, out: Optional[Chan] = None,
            src1: Optional[Chan] = None, epilogue: int = _lib.EPI_PLAIN, gate: Optional[Chan] = None,
            rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1,
-           bias_map: Optional[Chan] = None) -> None:
+           bias_map: Optional[Chan] = None, bk: int = 16) -> None:
     for nm, ch in (("src0", src0), ("src1", src1), ("out", out), ("gate", gate), ("rh", rh),
                    ("hid", hid), ("bias_map", bias_map)):
         if ch is not None:
@@ -184,6 +196,7 @@ def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w
         a.hid, a.sh = hid.ptr, hid.stride
     if bias_map is not None:
         a.bias_map, a.sbm = bias_map.ptr, bias_map.stride
+    a.bk = bk
     check(_lib.load().scflow_conv2d(ctypes.byref(a), _stream(src0.buf)), "scflow_conv2d")
 
 

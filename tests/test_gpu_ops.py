@@ -84,7 +84,7 @@ def test_corr_lookup_random(ops, n, h, w):
 
 
 # ------------------------------------------------------------------------------ convs
-def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0):
+def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0, bk=None):
     from scflow_amd.modules import ConvRunner
     g = torch.Generator().manual_seed(seed)
     x0 = torch.randn(n, c0, h, w, generator=g)
@@ -107,7 +107,10 @@ def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0):
         ops.nchw_into(x1.cuda(), ops.Chan(b1, 8, c1))
         src1 = ops.Chan(b1, 8, c1)
     out = torch.full((M, cout + 3), -5.0, device="cuda")
-    ConvRunner([convc], act).run(ops.Chan(b0, 4, c0), ops.Chan(out, 3, cout), n, h, w, src1=src1)
+    runner = ConvRunner([convc], act)
+    if bk is not None:  # force the K-stage depth (otherwise the library's pick for the shape)
+        runner._bk_shape, runner._bk = (n, h, w, c0, c1), bk
+    runner.run(ops.Chan(b0, 4, c0), ops.Chan(out, 3, cout), n, h, w, src1=src1)
     got = ops.chan_to_nchw(ops.Chan(out, 3, cout), n, h, w)
     assert (out[:, :3] == -5).all()
     return got, ref
@@ -132,6 +135,29 @@ def test_conv2d_variants(ops, case):
     got, ref = _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act)
     kk = (c0 + c1) * (np.prod(k) if isinstance(k, tuple) else k * k)
     close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"conv {case}")
+
+
+@pytest.mark.parametrize("bk", [8, 16])
+@pytest.mark.parametrize("case", [
+    (2, 32, 32, 324, 0, 256, 1, 0, "ReLU"),
+    (2, 32, 32, 256, 0, 192, 3, 1, "ReLU"),
+    (2, 32, 32, 128, 256, 128, (1, 5), (0, 2), "Tanh"),
+    (2, 32, 32, 200, 56, 126, 3, 1, "ReLU"),        # source boundary inside an 8-deep stage pair
+    (1, 64, 64, 128, 0, 64, 3, 1, "ReLU"),
+])
+def test_conv2d_mfma_stage_depths(ops, case, bk):
+    """Both K-stage depths (weights packed for 8- and 16-channel stages) give the conv."""
+    n, h, w, c0, c1, cout, k, pad, act = case
+    got, ref = _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, bk=bk)
+    kk = (c0 + c1) * (np.prod(k) if isinstance(k, tuple) else k * k)
+    close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"conv {case} bk={bk}")
+
+
+def test_conv_pick_bk_prefers_resident_grids(ops):
+    """Host query: the 3×3 256→192 conv at B=16 (768 workgroups of 64 px) picks 8-deep stages,
+    the GRU z|r conv (512 workgroups of 128 px) 16."""
+    assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == 8
+    assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == 16
 
 
 def test_conv_gru_module(ops):

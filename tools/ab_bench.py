@@ -35,20 +35,32 @@ def main():
     dec = dec.to(dev).eval()
     inp = bench.make_inputs(a.batch, a.size, seed=0, device=dev)
     names, values = [], []
+    import importlib
+
+    def target(k):  # "attr" → the decoder; "pkg.module.Class.attr" → that class/module
+        if "." not in k:
+            return dec, k
+        path, attr = k.rsplit(".", 1)
+        mod, _, cls = path.rpartition(".")
+        return getattr(importlib.import_module(mod), cls), attr
+
     for t in a.toggles:
         k, v = t.split("=")
         names.append(k)
         values.append([int(x) if x.lstrip("-").isdigit() else x for x in v.split(",")])
     combos = list(itertools.product(*values)) if names else [()]
     res = {c: [] for c in combos}
-    for c in combos:  # warm every variant (packing, allocator)
+
+    def apply(c):
         for k, v in zip(names, c):
-            setattr(dec, k, v)
+            obj, attr = target(k)
+            setattr(obj, attr, v)
+    for c in combos:  # warm every variant (packing, allocator)
+        apply(c)
         dec(**inp, invalid_flow_num=0.0)
     for _ in range(a.rounds):
         for c in combos:
-            for k, v in zip(names, c):
-                setattr(dec, k, v)
+            apply(c)
             dec(**inp, invalid_flow_num=0.0)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
