@@ -166,6 +166,11 @@ int scflow_ph_conv(const float* src0, int c0, int s0, const float* src1, int c1,
                    void* stream);
 int scflow_ph_gn_stats(const float* x, int n, int hw, int c, int groups, const float* gamma,
                        const float* beta, float eps, float* scale, float* shift, void* stream);
+/* scflow_ph_gn_reduce: y = Σ_z parts[z] (nsplit slabs, split_stride floats apart; y written when
+ *   nsplit > 1) and its GroupNorm scale/shift like scflow_ph_gn_stats (c % 32 == 0). */
+int scflow_ph_gn_reduce(const float* parts, int nsplit, long long split_stride, float* y, int n,
+                        int hw, int c, int groups, const float* gamma, const float* beta, float eps,
+                        float* scale, float* shift, void* stream);
 int scflow_ph_fc_permute(const float* W, float* Wp, int n, int c, int hw, void* stream);
 int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias, float* y,
                  int n, int relu, int gn_c, const float* scale, const float* shift, void* stream);
@@ -179,7 +184,7 @@ int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* 
  * (models/refiner/scflow_refiner.py:84-106).  Activations are channels-last [n][h][w][c].
  *
  * scflow_enc_conv: implicit-GEMM conv (fp32 MFMA), 1×1 or 3×3, stride 1 or 2, cin % 16 == 0;
- *   output width 16, 32, 64 or a multiple of the tile (128 for stride 1, 64 for stride 2), and
+ *   output width 8, 16, 32, 64 or a multiple of the tile (128 for stride 1, 64 for stride 2), and
  *   output height a multiple of the tile's rows (tile / width when the width is smaller).  Per element of the output:
  *     v = conv(x') + bias;  v = v·out_scale[c] + out_shift[c] (if given: eval BatchNorm);
  *     v += res[pix][c] (if given);  out = act(v) for c < act_split, act2(v) otherwise,
@@ -189,6 +194,8 @@ int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* 
  * scflow_enc_stem: 7×7 (any kh,kw ≤ 7) conv of an NCHW image batch [n][cin≤4][h][w], stride s,
  *   written channels-last with the same bias / out_scale / act epilogue (the stem conv1).
  *   Weights packed by scflow_enc_stem_pack ([kh·kw·cin][roundup(cout,64)]).
+ *   With src1 the input is cat[src, src1] (both normalised on load when in_scale is given,
+ *   in_scale then covering cin + cin1 channels).
  * scflow_enc_stats + scflow_enc_norm_finalize: InstanceNorm statistics of x [n][hw][c]
  *   (fp64 partial sums over `chunks` pixel chunks per image, then per (img, c))
  *   → scale = 1/sqrt(var+eps), shift = −mean·scale (biased variance, affine=False);
@@ -197,6 +204,12 @@ int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* 
  *   id' = 0 (id NULL), id (id_scale NULL) or id·id_scale[img][c] + id_shift[img][c]. */
 typedef struct scflow_enc_conv_args {
   const float* src; int cin; int s_in;            /* input, channels, pixel stride           */
+  const float* src1; int cin1; int s_in1;          /* optional 2nd input, concatenated on     */
+                                                   /* channels (cin1 % 16 == 0; 0 = none)     */
+  int ksplit;                                      /* ≥ 2: K (channel stages) split over      */
+                                                   /* grid.z; split z writes a raw partial    */
+                                                   /* to out + z·n·oh·ow·s_out (no bias /     */
+                                                   /* affine / residual / act allowed)        */
   const float* in_scale; const float* in_shift;    /* [n][cin] or NULL                        */
   const float* weight; const float* bias;          /* packed; bias [cout] or NULL             */
   const float* out_scale; const float* out_shift;  /* [cout] or NULL                          */

@@ -44,6 +44,8 @@ class EncConvArgs(ctypes.Structure):
     """Mirror of ``scflow_enc_conv_args`` (include/scflow_hip.h)."""
     _fields_ = [
         ("src", c_vp), ("cin", c_int), ("s_in", c_int),
+        ("src1", c_vp), ("cin1", c_int), ("s_in1", c_int),
+        ("ksplit", c_int),
         ("in_scale", c_vp), ("in_shift", c_vp),
         ("weight", c_vp), ("bias", c_vp),
         ("out_scale", c_vp), ("out_shift", c_vp),
@@ -84,6 +86,8 @@ SIGNATURES = {
                                c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "scflow_ph_gn_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_vp,
                                    c_vp]),
+    "scflow_ph_gn_reduce": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp,
+                                    c_float, c_vp, c_vp, c_vp]),
     "scflow_ph_fc_permute": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_ph_fc": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                              c_vp, c_vp]),

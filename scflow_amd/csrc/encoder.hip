@@ -32,11 +32,11 @@ constexpr int EBN = 64;  // output channels per workgroup
 constexpr int EBK = 16;  // input channels per K stage
 constexpr int ELDA = EBK + 4;
 
-// float4 of the A halo per thread, worst case over tile widths tc = 16..TILE_M (tr = TILE_M/tc
+// float4 of the A halo per thread, worst case over tile widths tc = 8..TILE_M (tr = TILE_M/tc
 // output rows of tc pixels)
 constexpr int enc_na(int tm, int kh, int kw, int s) {
   int m = 0;
-  for (int tc = 16; tc <= tm; tc *= 2) {
+  for (int tc = 8; tc <= tm; tc *= 2) {
     const int tr = tm / tc;
     const int v = ((tr - 1) * s + kh) * ((tc - 1) * s + kw) * (EBK / 4);
     if (v > m) m = v;
@@ -47,6 +47,7 @@ constexpr int enc_na(int tm, int kh, int kw, int s) {
 struct EncParams {
   scflow_enc_conv_args a;
   int oh, ow, tr, tc, hr, hc, nst;  // output size, tile rows × cols, halo rows × cols, K stages
+  int nst0;                         // stages of the first source
 };
 
 template <int KH, int KW, int S, int TILE_M, bool NORM>
@@ -82,18 +83,28 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
     apix[j] = ok ? (img * a.h + iy) * a.w + ix : -1;
   }
 
+  // K split (grid.z): this workgroup's stage range
+  const int z = blockIdx.z, nsplit = gridDim.z;
+  const int s_begin = (int)((long long)P.nst * z / nsplit);
+  const int s_end = (int)((long long)P.nst * (z + 1) / nsplit);
+  const int ctot = a.cin + a.cin1;
+
   floatx4 ra[NA], rb[NB], rsc, rsh;
   auto gload = [&](int s) {
-    const int c = s * EBK + cq;
+    const bool second = s >= P.nst0;
+    const float* src = second ? a.src1 : a.src;
+    const int sin = second ? a.s_in1 : a.s_in;
+    const int c = (second ? s - P.nst0 : s) * EBK + cq;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (apix[j] >= 0) v = *(const floatx4*)(a.src + (size_t)apix[j] * a.s_in + c);
+      if (apix[j] >= 0) v = *(const floatx4*)(src + (size_t)apix[j] * sin + c);
       ra[j] = v;
     }
     if constexpr (NORM) {
-      rsc = *(const floatx4*)(a.in_scale + (size_t)img * a.cin + c);
-      rsh = *(const floatx4*)(a.in_shift + (size_t)img * a.cin + c);
+      const int cn = s * EBK + cq;  // channel in the concatenation
+      rsc = *(const floatx4*)(a.in_scale + (size_t)img * ctot + cn);
+      rsh = *(const floatx4*)(a.in_shift + (size_t)img * ctot + cn);
     }
     const float* wb = a.weight + ((size_t)blockIdx.y * P.nst + s) * (TAPS * EBN * EBK);
 #pragma unroll
@@ -133,12 +144,12 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
 
-  gload(0);
-  for (int s = 0; s < P.nst; ++s) {
+  gload(s_begin);
+  for (int s = s_begin; s < s_end; ++s) {
     __syncthreads();
     lstore();
     __syncthreads();
-    if (s + 1 < P.nst) gload(s + 1);
+    if (s + 1 < s_end) gload(s + 1);
 #pragma unroll
     for (int ty = 0; ty < KH; ++ty) {
 #pragma unroll
@@ -168,6 +179,7 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
   const float osc = a.out_scale ? a.out_scale[col] : 1.f;
   const float osh = a.out_scale ? a.out_shift[col] : 0.f;
   const int act = col < a.act_split ? a.act : a.act2;
+  float* outz = a.out + (size_t)z * ((size_t)a.n * P.oh * P.ow * a.s_out);
 #pragma unroll
   for (int rr = 0; rr < RB; ++rr) {
 #pragma unroll
@@ -178,7 +190,7 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
       float v = acc[rr][r] + bias;
       if (a.out_scale) v = v * osc + osh;
       if (a.res) v += a.res[pix * a.s_res + col];
-      a.out[pix * a.s_out + col] = act_apply(v, act);
+      outz[pix * a.s_out + col] = act_apply(v, act);
     }
   }
 }
@@ -366,7 +378,7 @@ int rup(int a, int b) { return (a + b - 1) / b * b; }
 template <int KH, int KW, int S, int TM, bool NORM>
 int launch_enc(EncParams p, hipStream_t st) {
   p.tc = p.ow < TM ? p.ow : TM;
-  if (p.tc < 16 || TM % p.tc || p.ow % p.tc) return SCFLOW_EUNSUPPORTED;
+  if (p.tc < 8 || TM % p.tc || p.ow % p.tc) return SCFLOW_EUNSUPPORTED;
   p.tr = TM / p.tc;
   if (p.oh % p.tr) return SCFLOW_EUNSUPPORTED;
   p.hr = (p.tr - 1) * S + KH;
@@ -379,7 +391,8 @@ int launch_enc(EncParams p, hipStream_t st) {
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  dim3 grid(p.a.n * (p.oh / p.tr) * (p.ow / p.tc), rup(p.a.cout, EBN) / EBN);
+  dim3 grid(p.a.n * (p.oh / p.tr) * (p.ow / p.tc), rup(p.a.cout, EBN) / EBN,
+            p.a.ksplit > 1 ? p.a.ksplit : 1);
   enc_conv_kernel<KH, KW, S, TM, NORM><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }
@@ -392,6 +405,7 @@ int launch_enc_norm(const EncParams& p, hipStream_t st) {
 }  // namespace
 
 SCFLOW_API long long scflow_enc_conv_packed_size(int cout, int cin, int kh, int kw) {
+  // cin = all input channels (cin + cin1 of the conv args)
   if (cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
   return (long long)rup(cout, EBN) * rup(cin, EBK) * kh * kw;
 }
@@ -414,15 +428,20 @@ SCFLOW_API int scflow_enc_conv(const scflow_enc_conv_args* args, void* stream) {
       (a.res && a.s_res < a.cout) || (!a.in_scale) != (!a.in_shift) ||
       (!a.out_scale) != (!a.out_shift))
     return SCFLOW_EINVAL;
-  if (a.cin % EBK) return SCFLOW_EUNSUPPORTED;
+  if (a.cin1 < 0 || (a.cin1 > 0 && (!a.src1 || a.s_in1 < a.cin1)) || a.ksplit < 0) return SCFLOW_EINVAL;
+  if (a.ksplit > 1 && (a.bias || a.out_scale || a.res || a.act || a.act2)) return SCFLOW_EINVAL;
+  if (a.cin % EBK || a.cin1 % EBK) return SCFLOW_EUNSUPPORTED;
   if (!aligned16(a.src) || (a.s_in & 3) || !aligned16(a.weight) ||
+      (a.cin1 > 0 && (!aligned16(a.src1) || (a.s_in1 & 3))) ||
       (a.in_scale && (!aligned16(a.in_scale) || !aligned16(a.in_shift))))
     return SCFLOW_EALIGN;
   EncParams p{};
   p.a = a;
   p.oh = (a.h + 2 * a.pad - a.kh) / a.stride + 1;
   p.ow = (a.w + 2 * a.pad - a.kw) / a.stride + 1;
-  p.nst = a.cin / EBK;
+  p.nst0 = a.cin / EBK;
+  p.nst = (a.cin + a.cin1) / EBK;
+  if (a.ksplit > p.nst) return SCFLOW_EINVAL;
   if (p.oh <= 0 || p.ow <= 0) return SCFLOW_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   if (a.kh == 3 && a.kw == 3 && a.stride == 1) return launch_enc_norm<3, 3, 1, 128>(p, st);

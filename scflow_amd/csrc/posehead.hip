@@ -15,8 +15,10 @@
 //    (cat[h, Δflow-feat, mask-feat] never materialises), and the PREVIOUS layer's GroupNorm +
 //    ReLU is applied on load (per-(sample, channel) scale/shift) — so GN never rewrites memory.
 //    conv1 at B=16: 512 workgroups.
-//  * scflow_ph_gn_stats — one workgroup per sample: group mean/var (fp64 accumulation) →
-//    scale = γ·rstd, shift = β − mean·γ·rstd per channel.
+//  * scflow_ph_gn_stats / scflow_ph_gn_reduce — group mean/var (fp64 accumulation) over a
+//    (sample, 32-channel) grid → scale = γ·rstd, shift = β − mean·γ·rstd per channel; the reduce
+//    form first sums conv1's K-split partial slabs (scflow_enc_conv with ksplit) and writes the
+//    sum.
 //  * scflow_ph_fc — weight-streaming FC for M ≤ 16 rows: a wave per output neuron pair,
 //    lanes split K, inputs staged once per workgroup in LDS; optional GN+ReLU+NCHW-flatten
 //    gather of the input (FC1 reads conv3's raw output).
@@ -55,8 +57,14 @@ __device__ __forceinline__ floatx4 ph_load_a(const PhConvArgs& a, int img, int i
   return v;
 }
 
-constexpr int PH_WAVES = 16;  // waves per workgroup; they split K
-constexpr int PH_BATCH = 4;   // K chunks whose loads a wave issues together
+#ifndef SCFLOW_PH_WAVES
+#define SCFLOW_PH_WAVES 16
+#endif
+#ifndef SCFLOW_PH_BATCH
+#define SCFLOW_PH_BATCH 2  // tuned (tools/ph_bench.py): 4 → 2 is 2–3 µs faster per launch
+#endif
+constexpr int PH_WAVES = SCFLOW_PH_WAVES;  // waves per workgroup; they split K
+constexpr int PH_BATCH = SCFLOW_PH_BATCH;  // K chunks whose loads a wave issues together
 
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
   __shared__ float red[PH_WAVES / 2][32][33];
@@ -131,49 +139,66 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
   }
 }
 
-// GroupNorm statistics of x [n][hw][c] → per-channel scale/shift for y = relu(x·scale + shift).
-// One workgroup per sample; thread (g, slice) accumulates group g over pixels ≡ slice (mod
-// 256/groups) in fp64, then the slices are reduced in LDS in a fixed order.
-__global__ __launch_bounds__(256) void ph_gn_stats_kernel(const float* __restrict__ x, int hw, int c,
-                                                          int groups, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps,
-                                                          float* __restrict__ scale,
-                                                          float* __restrict__ shift) {
-  __shared__ double s1[256], s2[256];
-  const int img = blockIdx.x;
-  const int cpg = c / groups;
-  const int slices = 256 / groups;  // groups ≤ 256
-  const int g = threadIdx.x % groups, sl = threadIdx.x / groups;
-  const float* xs = x + (size_t)img * hw * c + g * cpg;
-  double a = 0.0, b = 0.0;
-  if (sl < slices) {
-    for (int p = sl; p < hw; p += slices)
-      for (int k = 0; k < cpg; ++k) {
-        const double v = xs[(size_t)p * c + k];
-        a += v;
-        b += v * v;
-      }
-  }
-  s1[threadIdx.x] = a;
-  s2[threadIdx.x] = b;
-  __syncthreads();
-  if (threadIdx.x < groups) {
-    double A = 0.0, Bq = 0.0;
-    for (int t = 0; t < slices; ++t) {
-      A += s1[t * groups + threadIdx.x];
-      Bq += s2[t * groups + threadIdx.x];
+// GroupNorm statistics of x [n][hw][c] → per-channel scale/shift for y = relu(x·scale + shift),
+// optionally first summing nsplit K-split partial slabs (x + z·split_stride) and writing the sum
+// to y.  Grid (n, c/32): a workgroup takes one sample's 32-channel block; thread t holds channel
+// quad t%8 of pixel slot t/8 (32 slots), float4 loads; per-channel sums in fp64 reduced over the
+// slots in a fixed order, then per group (c/groups channels) → mean, biased variance.
+__global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restrict__ x, int nsplit,
+                                                           long long split_stride, float* __restrict__ y,
+                                                           int hw, int c, int groups,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps,
+                                                           float* __restrict__ scale,
+                                                           float* __restrict__ shift) {
+  __shared__ double s1[32][33], s2[32][33];
+  __shared__ double gmean[32], grstd[32];
+  const int img = blockIdx.x, cb = blockIdx.y * 32;
+  const int q = threadIdx.x & 7, slot = threadIdx.x >> 3;
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  for (int p = slot; p < hw; p += 32) {
+    const size_t off = ((size_t)img * hw + p) * c + cb + 4 * q;
+    floatx4 v = *(const floatx4*)(x + off);
+    for (int z = 1; z < nsplit; ++z) {
+      const floatx4 u = *(const floatx4*)(x + (size_t)z * split_stride + off);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += u[e];
     }
+    if (y) *(floatx4*)(y + off) = v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] += (double)v[e];
+      b[e] += (double)v[e] * (double)v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    s1[slot][4 * q + e] = a[e];
+    s2[slot][4 * q + e] = b[e];
+  }
+  __syncthreads();
+  const int cpg = c / groups;       // channels per group (divides 32)
+  const int ng = 32 / cpg;          // groups in this block
+  if (threadIdx.x < ng) {
+    double A = 0, B = 0;
+    for (int k = 0; k < cpg; ++k)
+      for (int sl = 0; sl < 32; ++sl) {
+        A += s1[sl][threadIdx.x * cpg + k];
+        B += s2[sl][threadIdx.x * cpg + k];
+      }
     const double cnt = (double)hw * cpg;
     const double mean = A / cnt;
-    double var = Bq / cnt - mean * mean;
+    double var = B / cnt - mean * mean;
     if (var < 0) var = 0;
-    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-    for (int k = 0; k < cpg; ++k) {
-      const int ch = threadIdx.x * cpg + k;
-      const float sc = gamma[ch] * rstd;
-      scale[(size_t)img * c + ch] = sc;
-      shift[(size_t)img * c + ch] = beta[ch] - (float)mean * sc;
-    }
+    gmean[threadIdx.x] = mean;
+    grstd[threadIdx.x] = 1.0 / sqrt(var + (double)eps);
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int ch = cb + threadIdx.x, g = threadIdx.x / cpg;
+    const float sc = gamma[ch] * (float)grstd[g];
+    scale[(size_t)img * c + ch] = sc;
+    shift[(size_t)img * c + ch] = beta[ch] - (float)gmean[g] * sc;
   }
 }
 
@@ -364,11 +389,23 @@ SCFLOW_API int scflow_ph_conv(const float* src0, int c0, int s0, const float* sr
 SCFLOW_API int scflow_ph_gn_stats(const float* x, int n, int hw, int c, int groups,
                                   const float* gamma, const float* beta, float eps, float* scale,
                                   float* shift, void* stream) {
-  if (!x || !gamma || !beta || !scale || !shift || n <= 0 || hw <= 0 || c <= 0 || groups <= 0 ||
-      c % groups || c / groups > 256)
+  return scflow_ph_gn_reduce(x, 1, 0, nullptr, n, hw, c, groups, gamma, beta, eps, scale, shift,
+                             stream);
+}
+
+SCFLOW_API int scflow_ph_gn_reduce(const float* parts, int nsplit, long long split_stride, float* y,
+                                   int n, int hw, int c, int groups, const float* gamma,
+                                   const float* beta, float eps, float* scale, float* shift,
+                                   void* stream) {
+  if (!parts || !gamma || !beta || !scale || !shift || n <= 0 || hw <= 0 || c <= 0 ||
+      groups <= 0 || nsplit <= 0 || c % groups || (nsplit > 1 && (!y || split_stride <= 0)))
     return SCFLOW_EINVAL;
-  ph_gn_stats_kernel<<<n, 256, 0, (hipStream_t)stream>>>(x, hw, c, groups, gamma, beta, eps, scale,
-                                                         shift);
+  const int cpg = c / groups;
+  if (c % 32 || 32 % cpg) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(parts) || (y && !aligned16(y)) || (split_stride & 3)) return SCFLOW_EALIGN;
+  dim3 grid(n, c / 32);
+  ph_gn_reduce_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(parts, nsplit, split_stride, y, hw, c,
+                                                             groups, gamma, beta, eps, scale, shift);
   return scflow_launch_status();
 }
 

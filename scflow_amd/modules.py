@@ -505,9 +505,44 @@ class MultiClassPoseHead(nn.Module):
             self._pack_key = key
         return self._packed, self._fc1_perm
 
+    def _conv_mfma(self, i: int, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
+                   scale: Optional[Tensor], shift: Optional[Tensor]):
+        """conv_layers[i] on the MFMA halo conv (scflow_enc_conv; the previous GroupNorm + ReLU
+        applied on load) with a K split over grid.z so that ≥ 512 workgroups run, when the shape
+        allows it: returns (partial slabs [ksplit·n·oh·ow, cout], ksplit) or None."""
+        conv = self.conv_layers[i].conv
+        c1 = 0 if src1 is None else src1.c
+        if conv.kernel_size != (3, 3) or conv.padding[0] != 1 or conv.stride[0] not in (1, 2) \
+                or src0.c % 16 or c1 % 16 or conv.bias is not None:
+            return None
+        s = conv.stride[0]
+        oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+        tm = 128 if s == 1 else 64
+        tc = min(ow, tm)
+        if tc < 8 or tm % tc or ow % tc or oh % (tm // tc):
+            return None
+        wt = conv.weight
+        packs = getattr(self, "_mfma_packs", None)
+        if packs is None:
+            packs = self._mfma_packs = {}
+        key = (wt.data_ptr(), wt._version)
+        if packs.get(i, (None,))[0] != key:
+            packs[i] = (key, ops.enc_conv_pack(wt))
+        tiles = n * (oh // (tm // tc)) * (ow // tc) * ((conv.out_channels + 63) // 64)
+        nst = (src0.c + c1) // 16
+        ksplit = max(1, min(nst, -(-512 // tiles)))
+        parts = torch.empty(ksplit * n * oh * ow, conv.out_channels, device=src0.buf.device)
+        ops.enc_conv(src0, packs[i][1], None, n, h, w, src0.c, conv.out_channels, 3, s, 1, parts,
+                     src1=src1, ksplit=ksplit, in_scale=scale, in_shift=shift)
+        return parts, ksplit
+
     def forward_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
                     label: Tensor) -> Tuple[Tensor, Tensor]:
-        """Channels-last input cat[src0, src1] of n samples at h×w → (Δrot, Δt), 9 launches."""
+        """Channels-last input cat[src0, src1] of n samples at h×w → (Δrot, Δt).
+
+        Each conv runs on the MFMA halo conv with a K split into partial slabs when its shape
+        allows (conv1 and conv2 at SCFlow's sizes; summed by the GroupNorm-statistics kernel),
+        else on the gather conv (conv3's 4×4 output)."""
         if any(m.norm_type != "GN" or m.act_type != "ReLU" for m in self.conv_layers):
             raise NotImplementedError("HIP pose head: conv + GroupNorm + ReLU layers only")
         dev = src0.buf.device
@@ -524,12 +559,18 @@ class MultiClassPoseHead(nn.Module):
             oh, ow = (hh + 2 * p - k) // s + 1, (ww + 2 * p - k) // s + 1
             cout = conv.out_channels
             y = torch.empty(n * oh * ow, cout, device=dev)
-            ops.ph_conv(cur0, cur1, packs[i], None if conv.bias is None else conv.bias.detach(), n, hh,
-                        ww, cout, k, s, p, y, scale, shift)
+            split = self._conv_mfma(i, cur0, cur1, n, hh, ww, scale, shift)
+            if split is None:
+                ops.ph_conv(cur0, cur1, packs[i], None if conv.bias is None else conv.bias.detach(), n,
+                            hh, ww, cout, k, s, p, y, scale, shift)
             scale = torch.empty(n, cout, device=dev)
             shift = torch.empty(n, cout, device=dev)
-            ops.ph_gn_stats(y, n, oh * ow, cout, m.gn.num_groups, m.gn.weight.detach(),
-                            m.gn.bias.detach(), m.gn.eps, scale, shift)
+            if split is not None:
+                ops.ph_gn_reduce(split[0], split[1], y, n, oh * ow, cout, m.gn.num_groups,
+                                 m.gn.weight.detach(), m.gn.bias.detach(), m.gn.eps, scale, shift)
+            else:
+                ops.ph_gn_stats(y, n, oh * ow, cout, m.gn.num_groups, m.gn.weight.detach(),
+                                m.gn.bias.detach(), m.gn.eps, scale, shift)
             cur0, cur1, hh, ww = Chan.whole(y), None, oh, ow
         c = cur0.c
         x = cur0.buf

@@ -319,6 +319,14 @@ def ph_gn_stats(x: Tensor, n: int, hw: int, c: int, groups: int, gamma: Tensor, 
                                          _p(scale), _p(shift), _stream(x)), "scflow_ph_gn_stats")
 
 
+def ph_gn_reduce(parts: Tensor, nsplit: int, y: Tensor, n: int, hw: int, c: int, groups: int,
+                 gamma: Tensor, beta: Tensor, eps: float, scale: Tensor, shift: Tensor) -> None:
+    """y = sum of the nsplit partial slabs of ``parts`` [nsplit, n·hw, c]; GN scale/shift of y."""
+    check(_lib.load().scflow_ph_gn_reduce(_p(parts), nsplit, n * hw * c, _p(y), n, hw, c, groups,
+                                          _p(gamma), _p(beta), float(eps), _p(scale), _p(shift),
+                                          _stream(parts)), "scflow_ph_gn_reduce")
+
+
 def ph_fc_permute(W: Tensor, c: int, hw: int) -> Tensor:
     """nn.Linear weight with NCHW-flatten columns → channels-last column order."""
     _require(W, "fc weight", contiguous=False)
@@ -375,7 +383,7 @@ def enc_conv(src, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int
              in_scale: Optional[Tensor] = None, in_shift: Optional[Tensor] = None,
              out_scale: Optional[Tensor] = None, out_shift: Optional[Tensor] = None,
              res: Optional[Tensor] = None, act: Optional[str] = None, act2: Optional[str] = None,
-             act_split: Optional[int] = None) -> None:
+             act_split: Optional[int] = None, src1: Optional[Chan] = None, ksplit: int = 1) -> None:
     """One channels-last MFMA conv (see scflow_enc_conv in include/scflow_hip.h); ``src`` is a
     contiguous channels-last tensor or a ``Chan`` (channel slice with its pixel stride)."""
     if isinstance(src, Chan):
@@ -387,6 +395,10 @@ def enc_conv(src, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int
     _require(out, "out")
     a = _lib.EncConvArgs()
     a.src, a.cin, a.s_in = sptr, cin, sstride
+    if src1 is not None:
+        _require(src1.buf, "src1")
+        a.src1, a.cin1, a.s_in1 = src1.ptr, src1.c, src1.stride
+    a.ksplit = ksplit
     a.in_scale, a.in_shift = _p(in_scale), _p(in_shift)
     a.weight, a.bias = packed.data_ptr(), _p(bias)
     a.out_scale, a.out_shift = _p(out_scale), _p(out_shift)
