@@ -22,9 +22,15 @@ if [ $WHAT = all ] || [ $WHAT = bench ]; then
 fi
 if [ $WHAT = all ] || [ $WHAT = prof ]; then
   cd /tmp
+  # decoder-only (the bench's roofline kernel averages must agree with this profile)
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run -- \
-      python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err
+      python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-batch 0 > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err
   rc=$?; echo "rocprof rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+  # end-to-end refiner (configs[2]) kernels
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_e2e_$TAG -o run -- \
+      python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --e2e-steps 3 > $OUT/bench_prof_e2e_$TAG.json 2> $OUT/prof_e2e_$TAG.err
+  rc=$?; echo "rocprof e2e rc=$rc"
   [ $rc -eq 0 ] || exit $rc
   find $OUT/prof_$TAG -name "*stats*" | head
 fi
