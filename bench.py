@@ -107,6 +107,40 @@ def time_steps(step, steps, warmup, world, dev):
     return elapsed
 
 
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
+
+
+def secondary_rooflines(timers, batch, size):
+    """The other hot-path kernels, timed live like the primary one (same events, same timed
+    region): the pyramid lookup and the pose-induced-flow reprojection are HBM/gather-bound
+    (algorithmic bytes per launch from SURVEY.md §8(d)), the correlation GEMM is MFMA-bound.
+    At B=16, 256² the 86 MB pyramid is Infinity-Cache resident, so the lookup's GB/s is an
+    on-die rate; --size 512 --batch 32 (configs[4]) puts it in HBM."""
+    h = w = size // 8
+    P = h * w
+    lookup_bytes = batch * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
+    flow_bytes = batch * 20 * size * size
+    corr_flops = 2.0 * batch * P * P * 256
+    out = []
+    for name, kernel, bound, amount in (
+            ("corr_lookup", "corr_lookup_lds_kernel<4> (a2)", "hbm", lookup_bytes),
+            ("pose_flow", "pose_flow_kernel (a8+a10)", "hbm", flow_bytes),
+            ("corr_pyramid", "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma", corr_flops)):
+        t = timers[name]
+        if t.count() == 0:
+            continue
+        ms = t.mean_ms()
+        if bound == "hbm":
+            ach, peak, unit = amount / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+        else:
+            ach, peak, unit = amount / (ms * 1e-3) / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+        out.append({"kernel": kernel, "bound": bound, "achieved": round(ach, 2), "peak": peak,
+                    "unit": unit, "frac": round(ach / peak, 4), "avg_launch_ms": round(ms, 4),
+                    "launches": t.count(),
+                    ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): amount})
+    return out
+
+
 def cpu_baseline(seconds: float, iters: int, size: int):
     """Time the CPU oracle on a bounded sample: B=2 pairs, `iters` iterations, repeated."""
     from oracle import scflow_oracle as orc
@@ -170,27 +204,33 @@ def main():
     dec = dec.to(dev).eval()
     inp = make_inputs(args.batch, args.size, seed=rank, device=dev)
 
-    timer = KernelTimer() if args.graph else EventTimer()
-    timer.enabled = False
+    timers = {name: (KernelTimer() if args.graph else EventTimer())
+              for name in ("gru_zr", "corr_lookup", "pose_flow", "corr_pyramid")}
+    timer = timers["gru_zr"]
+    for t in timers.values():
+        t.enabled = False
     if not args.no_kernel_timer:
-        dec.kernel_hooks["gru_zr"] = timer
+        dec.kernel_hooks.update(timers)
     if not args.graph:
         def step():
             return dec(**inp, invalid_flow_num=0.0)
         for _ in range(args.warmup):
             step()
-        timer.enabled = True
+        for t in timers.values():
+            t.enabled = True
     else:
         # one hipGraph per forward: captured after `warmup` eager passes, replayed per step
         from scflow_amd.graph import GraphedForward
 
         def arm():
-            timer.enabled = True
+            for t in timers.values():
+                t.enabled = True
         g = GraphedForward(dec, inp, warmup=args.warmup, before_capture=arm, invalid_flow_num=0.0)
         step = g.replay
 
     elapsed = time_steps(step, args.steps, 0, world, dev)
-    timer.enabled = False
+    for t in timers.values():
+        t.enabled = False
     dec.kernel_hooks.clear()
 
     e2e = None
@@ -256,6 +296,7 @@ def main():
                          "avg_launch_ms": round(zr_ms, 4), "launches": timer.count(),
                          "flops_per_launch": flops},
         }
+        res["rooflines_secondary"] = secondary_rooflines(timers, args.batch, args.size)
         if e2e is not None:
             res["end_to_end"] = e2e
         if world == 1 and not args.no_cpu_baseline:

@@ -84,6 +84,8 @@ class SCFlowDecoder(nn.Module):
             ConvModule(1, 64, 3, padding=1, **mk), ConvModule(64, 32, 3, padding=1, **mk))
         self._head_runner = None
         # optional per-kernel timing hooks (bench.py): name -> callable(start: bool)
+        # name -> callable(start: bool) bracketing one launch (bench.py's live kernel timing):
+        # gru_zr, gru_q, corr_pyramid, corr_lookup, pose_flow
         self.kernel_hooks: Dict[str, object] = {}
         # compute the context features' (loop-invariant) GRU contribution once per forward
         self.hoist_context = True
@@ -149,7 +151,9 @@ class SCFlowDecoder(nn.Module):
         iters = int(self.iters)
 
         # a1 + a9 (once per forward)
+        self._hook("corr_pyramid", True)
         pyr, _ = ops.corr_pyramid(feat_render, feat_real, self.num_levels)
+        self._hook("corr_pyramid", False)
         depth = depth.contiguous().float()
         K = K.contiguous().float()
         R_prev = R0.contiguous().float()
@@ -243,8 +247,10 @@ class SCFlowDecoder(nn.Module):
                 run_chain(self.encoder.flow_net, Chan.whole(flow_in), Chan(MF, cc, cf), N, h, w,
                           s_flow)
             # a2 + a3 (correlation branch)
+            self._hook("corr_lookup", True)
             ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
                             flow_layout="nhwc")
+            self._hook("corr_lookup", False)
             if self.mask_corr:
                 CORR.mul_(mask_lr)
             run_chain(self.encoder.corr_net, Chan.whole(CORR), Chan(MF, 0, cc), N, h, w, s_corr)
@@ -275,8 +281,10 @@ class SCFlowDecoder(nn.Module):
             # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
             ops.flow_upsample(F2, D2, MASK, N, h, w, H, W, float(scale), o_flow_pred[it], o_mask[it])
             # a8 + a10: pose update + pose-induced flow (one launch)
+            self._hook("pose_flow", True)
             ops.pose_update_flow(drot, dtr, R_prev, t_prev, K, points, o_R[it], o_t[it],
                                  o_flow_pose[it], invalid, depth_transform=self.depth_transform)
+            self._hook("pose_flow", False)
             R_prev, t_prev = o_R[it], o_t[it]
             flow_full = o_flow_pose[it]
             drots.append(drot)
