@@ -238,6 +238,20 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
                      const float* id_scale, const float* id_shift, float* out, int n, int hw,
                      int c, void* stream);
 
+/* Training (§8(f)-2) building blocks.
+ * scflow_im2col: cols[p][(ty·kw + tx)·cin + c] = x[n][oy·s − ph + ty][ox·s − pw + tx][c] (0 outside),
+ *   p = (n·oh + oy)·ow + ox; x channels-last with pixel stride sx.  The conv weight gradient is
+ *   then dW[o][tap·cin + c] = Σ_p dY[p][o] · cols[p][tap·cin + c] (a plain GEMM).
+ * scflow_corr_lookup_backward: scatter-add of the lookup's output gradient (same layout options
+ *   as scflow_corr_lookup) into the pyramid gradient (same layout as the pyramid; must be
+ *   zeroed by the caller), with grid_sample's bilinear weights — the flow input is detached in
+ *   SCFlow (scflow_decoder.py:193-194), so no flow gradient. */
+int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh, int kw,
+                  int stride, int ph, int pw, void* stream);
+int scflow_corr_lookup_backward(const float* dout, int out_layout, int out_stride, const float* flow,
+                                int flow_layout, float* dpyr, int n, int h, int w, int num_levels,
+                                int radius, void* stream);
+
 /* Profiling helper (bench.py roofline timing; no reference equivalent): a one-thread kernel
  * that stores the GPU's constant-rate wall clock (s_memrealtime) into stamps[idx].  Enqueued on
  * the stream of the kernel being timed, before and after it; as an ordinary kernel it is also a

@@ -103,6 +103,10 @@ SIGNATURES = {
     "scflow_enc_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "scflow_enc_norm_finalize": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp]),
     "scflow_enc_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_vp]),
+    "scflow_corr_lookup_backward": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int,
+                                            c_int, c_int, c_vp]),
     "scflow_timestamp": (c_int, [c_vp, c_int, c_vp]),
     "scflow_wallclock_khz": (c_ll, []),
 }

@@ -440,3 +440,35 @@ def enc_apply(x: Tensor, scale: Tensor, shift: Tensor, out: Tensor, n: int, hw: 
     check(_lib.load().scflow_enc_apply(_p(x), _p(scale), _p(shift), _p(id), _p(id_scale),
                                        _p(id_shift), _p(out), n, hw, c, _stream(x)),
           "scflow_enc_apply")
+
+
+# ------------------------------------------------------------------------------- §8(f)-2 training
+def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, ph: int, pw: int,
+           out: Optional[Tensor] = None) -> Tensor:
+    """Patch matrix [n·oh·ow, kh·kw·cin] of a channels-last input (tensor or Chan)."""
+    if isinstance(x, Chan):
+        _require(x.buf, "x")
+        ptr, sx, dev = x.ptr, x.stride, x.buf.device
+    else:
+        _require(x, "x")
+        ptr, sx, dev = x.data_ptr(), x.shape[-1], x.device
+    oh, ow = (h + 2 * ph - kh) // stride + 1, (w + 2 * pw - kw) // stride + 1
+    if out is None:
+        out = torch.empty(n * oh * ow, kh * kw * cin, device=dev)
+    check(_lib.load().scflow_im2col(ptr, sx, _p(out), n, h, w, cin, kh, kw, stride, ph, pw,
+                                    torch.cuda.current_stream(dev).cuda_stream), "scflow_im2col")
+    return out
+
+
+def corr_lookup_backward(dout: Tensor, flow: Tensor, dpyr: Tensor, n: int, h: int, w: int,
+                         num_levels: int, radius: int, out_layout: str = "nhwc",
+                         flow_layout: str = "nhwc") -> None:
+    """dpyr (zeroed, pyramid layout) += adjoint of corr_lookup applied to dout."""
+    for nm, t in (("dout", dout), ("flow", flow), ("dpyr", dpyr)):
+        _require(t, nm)
+    lay = {"nchw": _lib.LAYOUT_NCHW, "nhwc": _lib.LAYOUT_NHWC}
+    stride = dout.shape[-1] if out_layout == "nhwc" else 0
+    check(_lib.load().scflow_corr_lookup_backward(_p(dout), lay[out_layout], stride, _p(flow),
+                                                  lay[flow_layout], _p(dpyr), n, h, w, num_levels,
+                                                  radius, _stream(dout)),
+          "scflow_corr_lookup_backward")
