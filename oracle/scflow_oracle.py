@@ -222,7 +222,8 @@ def rotation_from_ortho6d(o6: Tensor) -> Tensor:
 
 
 def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 10.0,
-                depth_transform: str = "exp") -> Tuple[Tensor, Tensor]:
+                depth_transform: str = "exp", detach_depth_for_xy: bool = False) -> Tuple[Tensor, Tensor]:
+    """get_pose_from_delta_pose (pose.py:124-149); detach_depth_for_xy only changes gradients."""
     if drot.shape[1] != 6:
         raise NotImplementedError("quaternion delta rotation (kornia) is not on the configured path")
     Rd = torch.bmm(rotation_from_ortho6d(drot), R)
@@ -230,8 +231,9 @@ def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 
         vz = t[:, 2] / torch.exp(dt[:, 2])
     else:
         vz = t[:, 2] * (dt[:, 2] + 1)
-    vx = vz * (dt[:, 0] / weight + t[:, 0] / t[:, 2])
-    vy = vz * (dt[:, 1] / weight + t[:, 1] / t[:, 2])
+    vzxy = vz.detach() if detach_depth_for_xy else vz
+    vx = vzxy * (dt[:, 0] / weight + t[:, 0] / t[:, 2])
+    vy = vzxy * (dt[:, 1] / weight + t[:, 1] / t[:, 2])
     return Rd, torch.stack([vx, vy, vz], dim=-1)
 
 
@@ -298,8 +300,10 @@ def decoder_forward(sd: StateDict, feat_render: Tensor, feat_real: Tensor, h_fea
                     invalid_flow_num: float = 0.0, iters: int = 8, num_levels: int = 4,
                     radius: int = 4, act: str | None = "ReLU", gru_type: str = "SeqConv",
                     num_class: int = 21, depth_transform: str = "exp", mask_flow: bool = False,
-                    mask_corr: bool = False, hooks: dict | None = None):
-    """Returns the reference's 7 lists (scflow_decoder.py:252)."""
+                    mask_corr: bool = False, hooks: dict | None = None, train: bool = False):
+    """Returns the reference's 7 lists (scflow_decoder.py:252).  ``train``: apply the configured
+    detaches for autograd (detach_flow / detach_pose / detach_depth_for_xy = True,
+    scflow_decoder.py:193-196,231-236; config scflow_ycbv_real.py:211-214) — values unchanged."""
     dt = feat_render.dtype
     sd = {k: v.to(dt) if v.is_floating_point() else v for k, v in sd.items()}
     pyr = corr_pyramid(feat_render, feat_real, num_levels)
@@ -315,6 +319,8 @@ def decoder_forward(sd: StateDict, feat_render: Tensor, feat_real: Tensor, h_fea
     h = h_feat
     outs = ([], [], [], [], [], [], [])
     for it in range(iters):
+        if train:
+            flow = flow.detach()
         flow = downsample_flow(flow, scale)
         corr = corr_lookup(pyr, flow, radius)
         if mask_corr:
@@ -331,7 +337,10 @@ def decoder_forward(sd: StateDict, feat_render: Tensor, feat_real: Tensor, h_fea
         drot, dtr = pose_head(sd, torch.cat([h, dff, mf], 1), label, num_class)
         flow_pred = scale * upsample(flow + dflow, scale)
         up_mask = upsample(mask, scale)
-        R, t = pose_update(drot, dtr, R, t, depth_transform=depth_transform)
+        if train:
+            R, t = R.detach(), t.detach()
+        R, t = pose_update(drot, dtr, R, t, depth_transform=depth_transform,
+                           detach_depth_for_xy=train)
         flow = pose_flow(R, t, K, points, valid, invalid_flow_num)
         if hooks is not None:
             hooks.setdefault("h", []).append(h)
@@ -354,49 +363,164 @@ def cal_epe_mean(flow_tgt: Tensor, flow_pred: Tensor, mask: Tensor | None = None
 # §8(f)-1 — RAFTEncoder 'Basic' (models/encoder/raft_encoder.py:286-314) and the refiner's
 # feature extraction (models/refiner/scflow_refiner.py:84-106, 108-138)
 # ---------------------------------------------------------------------------------------------
-def _enc_norm(x: Tensor, sd: StateDict, key: str, norm: str, eps: float = 1e-5) -> Tensor:
-    """mmcv build_norm_layer: IN → InstanceNorm2d(affine=False), BN → BatchNorm2d (eval stats)."""
+def _enc_norm(x: Tensor, sd: StateDict, key: str, norm: str, eps: float = 1e-5,
+              train: bool = False) -> Tensor:
+    """mmcv build_norm_layer: IN → InstanceNorm2d(affine=False), BN → BatchNorm2d (eval: running
+    stats; ``train``: batch statistics, running stats left untouched here)."""
     if norm == "IN":
         return F.instance_norm(x, eps=eps)
+    if train:
+        return F.batch_norm(x, None, None, sd[key + ".weight"], sd[key + ".bias"], training=True, eps=eps)
     return F.batch_norm(x, sd[key + ".running_mean"], sd[key + ".running_var"], sd[key + ".weight"],
                         sd[key + ".bias"], training=False, eps=eps)
 
 
-def _basic_block(sd: StateDict, p: str, x: Tensor, stride: int, norm: str) -> Tensor:
+def _basic_block(sd: StateDict, p: str, x: Tensor, stride: int, norm: str,
+                 train: bool = False) -> Tensor:
     """BasicBlock.forward (models/backbone/resnet.py:65-92); downsample = ResLayer's
     1×1/stride conv + norm (resnet.py:707-729)."""
     ab = "in" if norm == "IN" else "bn"
     out = F.conv2d(x, sd[p + "conv1.weight"], sd[p + "conv1.bias"], stride=stride, padding=1)
-    out = F.relu(_enc_norm(out, sd, p + ab + "1", norm))
+    out = F.relu(_enc_norm(out, sd, p + ab + "1", norm, train=train))
     out = F.conv2d(out, sd[p + "conv2.weight"], sd[p + "conv2.bias"], padding=1)
-    out = _enc_norm(out, sd, p + ab + "2", norm)
+    out = _enc_norm(out, sd, p + ab + "2", norm, train=train)
     if p + "downsample.0.weight" in sd:
         identity = F.conv2d(x, sd[p + "downsample.0.weight"], sd[p + "downsample.0.bias"], stride=stride)
-        identity = _enc_norm(identity, sd, p + "downsample.1", norm)
+        identity = _enc_norm(identity, sd, p + "downsample.1", norm, train=train)
     else:
         identity = x
     return F.relu(out + identity)
 
 
 def raft_encoder(sd: StateDict, x: Tensor, norm: str, prefix: str = "",
-                 strides: Sequence[int] = (1, 2, 2), blocks: Sequence[int] = (2, 2, 2)) -> Tensor:
+                 strides: Sequence[int] = (1, 2, 2), blocks: Sequence[int] = (2, 2, 2),
+                 train: bool = False) -> Tensor:
     """RAFTEncoder.forward, net_type='Basic', scale 1/8 (stem stride 2)."""
     ab = "in" if norm == "IN" else "bn"
     x = F.conv2d(x, sd[prefix + "conv1.weight"], sd[prefix + "conv1.bias"], stride=2, padding=3)
-    x = F.relu(_enc_norm(x, sd, prefix + ab + "1", norm))
+    x = F.relu(_enc_norm(x, sd, prefix + ab + "1", norm, train=train))
     for i, (s, nb) in enumerate(zip(strides, blocks)):
         for b in range(nb):
-            x = _basic_block(sd, f"{prefix}res_layer{i + 1}.{b}.", x, s if b == 0 else 1, norm)
+            x = _basic_block(sd, f"{prefix}res_layer{i + 1}.{b}.", x, s if b == 0 else 1, norm, train)
     return F.conv2d(x, sd[prefix + "conv2.weight"], sd[prefix + "conv2.bias"])
 
 
 def extract_feat(sd: StateDict, render_images: Tensor, real_images: Tensor,
-                 h_channels: int = 128, cxt_channels: int = 128):
+                 h_channels: int = 128, cxt_channels: int = 128, train: bool = False):
     """SCFlowRefiner.extract_feat (scflow_refiner.py:84-106): one shared feature encoder
     (``real_encoder`` is ``render_encoder`` when ``seperate_encoder=False``,
     base_refiner.py:33-40), context encoder on the rendered image, split + tanh / relu."""
     real = raft_encoder(sd, real_images, "IN", "real_encoder.")
     render = raft_encoder(sd, render_images, "IN", "render_encoder.")
-    cxt = raft_encoder(sd, render_images, "BN", "context.")
+    cxt = raft_encoder(sd, render_images, "BN", "context.", train=train)
     h, c = torch.split(cxt, [h_channels, cxt_channels], dim=1)
     return render, real, torch.tanh(h), torch.relu(c)
+
+
+# ---------------------------------------------------------------------------------------------
+# §8(f)-2 — training losses (models/loss/sequence_loss.py:7-80, point_matching_loss.py:106-218,
+# the SCFlowRefiner.loss composition scflow_refiner.py:182-256; weights from
+# configs/refine_models/scflow_ycbv_real.py:231-262)
+# ---------------------------------------------------------------------------------------------
+SYMMETRIC_CLASSES = (12, 15, 18)  # 0-based labels of 'cls_13', 'cls_16', 'cls_19' (config :34-38)
+
+
+def raft_loss(pred: Tensor, gt: Tensor, valid: Tensor, weight: float = 0.1, max_flow: float = 400.,
+              eps: float = 1e-10) -> Tensor:
+    """RAFTLoss.forward (sequence_loss.py:15-23)."""
+    mag = torch.sum(gt ** 2, dim=1).sqrt()
+    v = ((valid >= 0.5) & (mag < max_flow)).to(gt)
+    loss = (v[:, None] * (pred - gt).abs()).sum() / (v.sum() + eps)
+    return weight * loss
+
+
+def l1_loss(pred: Tensor, gt: Tensor, weight: float = 10.0) -> Tensor:
+    """L1Loss.forward (sequence_loss.py:34-36)."""
+    return weight * torch.mean(torch.abs(pred - gt))
+
+
+def point_matching_loss(pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tensor, labels: Tensor,
+                        points: Sequence[Tensor], diameters: Sequence[float],
+                        weight: float = 10.0) -> Tensor:
+    """DisentanglePointMatchingLoss.forward, l1, disentangle_z, no xy/depth scaling
+    (point_matching_loss.py:159-218); symmetric classes match each GT point to its nearest
+    predicted point (brute force in place of pytorch3d knn_points, :183-186)."""
+    loss = 0.
+    B = len(pred_r)
+    for i in range(B):
+        P = points[int(labels[i])]
+        gt_rot = P @ gt_r[i].T
+        gt_rt = gt_rot + gt_t[i][None]
+        pred_rot = P @ pred_r[i].T + gt_t[i][None]
+        if int(labels[i]) in SYMMETRIC_CLASSES:
+            idx = torch.cdist(gt_rt, pred_rot).argmin(dim=1)
+            pred_rot = pred_rot[idx]
+        l_rot = torch.mean(torch.linalg.norm(pred_rot - gt_rt, dim=-1, ord=1))
+        tz = torch.cat([gt_t[i][:2], pred_t[i][2:]])
+        l_z = torch.mean(torch.linalg.norm(gt_rot + tz[None] - gt_rt, dim=-1, ord=1))
+        txy = torch.cat([pred_t[i][:2], gt_t[i][2:]])
+        l_xy = torch.mean(torch.linalg.norm(gt_rot + txy[None] - gt_rt, dim=-1, ord=1))
+        loss = loss + (l_z + l_xy + l_rot) / diameters[int(labels[i])]
+    return weight * loss / B
+
+
+def filter_flow_by_mask(flow: Tensor, gt_mask: Tensor, invalid_num: float = 400.) -> Tensor:
+    """filter_flow_by_mask (models/utils/flow.py:6-26): a flow whose target falls outside the
+    target mask (bilinear sample < 0.9, align_corners=False, zero padding) becomes invalid."""
+    N, _, H, W = flow.shape
+    bad = (flow[:, 0] >= invalid_num) & (flow[:, 1] >= invalid_num)
+    yy, xx = torch.meshgrid(torch.arange(H, dtype=flow.dtype), torch.arange(W, dtype=flow.dtype),
+                            indexing="ij")
+    gx = (xx[None] + flow[:, 0]) * 2. / max(W - 1, 1) - 1.
+    gy = (yy[None] + flow[:, 1]) * 2. / max(H - 1, 1) - 1.
+    m = F.grid_sample(gt_mask[:, None].to(flow.dtype), torch.stack([gx, gy], -1), mode="bilinear",
+                      padding_mode="zeros", align_corners=False)
+    bad = (m[:, 0] < 0.9) | bad
+    return torch.where(bad[:, None].expand_as(flow), torch.full_like(flow, invalid_num), flow)
+
+
+def sequence_loss(values: Sequence[Tensor], gamma: float = 0.8) -> Tensor:
+    """SequenceLoss.forward (sequence_loss.py:59-80): Σ γ^(n−i−1)·loss_i."""
+    n = len(values)
+    return sum(gamma ** (n - i - 1) * v for i, v in enumerate(values))
+
+
+def refine_train_loss(outs, gt_R: Tensor, gt_t: Tensor, gt_flow: Tensor, render_mask: Tensor,
+                      labels: Tensor, points: Sequence[Tensor], diameters: Sequence[float],
+                      max_flow: float = 400.) -> Tuple[Tensor, Tensor, Tensor]:
+    """(loss_pose, loss_flow, loss_mask) of SCFlowRefiner.loss (scflow_refiner.py:200-242)
+    from the decoder's 7 lists; gt_flow already filtered (filter_flow_by_mask)."""
+    fp, fpred, Rs, ts, masks, _, _ = outs
+    loss_pose = sequence_loss([point_matching_loss(R, t, gt_R, gt_t, labels, points, diameters)
+                               for R, t in zip(Rs, ts)])
+    loss_flow = sequence_loss([raft_loss(f, gt_flow, render_mask) for f in fpred])
+    occ = (torch.sum(gt_flow, dim=1) < max_flow).to(gt_flow)
+    loss_mask = sequence_loss([l1_loss(m[:, 0], occ) for m in masks])
+    return loss_pose, loss_flow, loss_mask
+
+
+def refine_train_forward(sd: StateDict, render_images: Tensor, real_images: Tensor,
+                         ref_rotation: Tensor, ref_translation: Tensor, gt_rotation: Tensor,
+                         gt_translation: Tensor, depth: Tensor, internel_k: Tensor, label: Tensor,
+                         points: Sequence[Tensor], diameters: Sequence[float],
+                         gt_masks: Tensor | None = None, iters: int = 8, max_flow: float = 400.):
+    """SCFlowRefiner.loss (scflow_refiner.py:182-256) for the configured model: features (BN in
+    train mode), decoder with the training detaches, GT flow (lift with the reference pose,
+    project with the GT pose, invalid = max_flow; filter by the GT mask), the three losses.
+    Returns (loss, loss_pose, loss_flow, loss_mask, outs, gt_flow)."""
+    dt = render_images.dtype
+    render, real, h, c = extract_feat(sd, render_images, real_images, train=True)
+    N, H, W = depth.shape
+    outs = decoder_forward(sd, render, real, h, c, ref_rotation, ref_translation, depth, internel_k,
+                           label, torch.zeros(N, 2, H, W, dtype=dt), iters=iters, train=True)
+    with torch.no_grad():
+        pts, valid = lift_points(depth.to(dt), internel_k.to(dt), ref_rotation.to(dt),
+                                 ref_translation.to(dt))
+        gt_flow = pose_flow(gt_rotation.to(dt), gt_translation.to(dt), internel_k.to(dt), pts, valid,
+                            max_flow)
+        if gt_masks is not None:
+            gt_flow = filter_flow_by_mask(gt_flow, gt_masks, max_flow)
+    lp, lf, lm = refine_train_loss(outs, gt_rotation.to(dt), gt_translation.to(dt), gt_flow,
+                                   (depth > 0).to(dt), label, [p.to(dt) for p in points], diameters,
+                                   max_flow)
+    return lp + lf + lm, lp, lf, lm, outs, gt_flow

@@ -182,3 +182,41 @@ def fill_module_(module, seed: int = 0) -> None:
                 continue
             v = torch.from_numpy(param_value(k, tuple(p.shape), seed))
             p.copy_(v.to(p.dtype))
+
+
+ELLIPSOID_AXES = (0.5, 0.38, 0.3)  # semi-axes / diameter of the stand-in object (make_scene)
+
+
+def make_model_points(num_points: int = 512, num_class: int = 21, seed: int = 0) -> np.ndarray:
+    """[num_class, P, 3] model points on each class's stand-in ellipsoid surface (mm) — the
+    meshes the point-matching loss reads (point_matching_loss.py:148-155) are absent here."""
+    rng = np.random.default_rng(seed + 104729)
+    out = np.empty((num_class, num_points, 3))
+    for c in range(num_class):
+        d = rng.standard_normal((num_points, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        out[c] = d * np.array(ELLIPSOID_AXES) * YCBV_DIAMETERS[c % len(YCBV_DIAMETERS)]
+    return out.astype(np.float32)
+
+
+def make_train_targets(scene: Dict[str, np.ndarray], size: int, seed: int = 0,
+                       rot_deg: float = 5.0, trans_xy: float = 8.0, trans_z: float = 0.03
+                       ) -> Dict[str, np.ndarray]:
+    """Ground-truth pose (the reference pose perturbed like PoseJitter,
+    datasets/pipelines/jitter.py:51-79, here small so the GT flow stays in range) and the GT
+    mask (the stand-in ellipsoid rendered at the GT pose) for a ``make_scene`` batch."""
+    rng = np.random.default_rng(seed + 15485863)
+    Rs, ts, masks = [], [], []
+    for b in range(len(scene["labels"])):
+        ang = rng.normal(0.0, math.radians(rot_deg), 3)
+        R = _rot_zyx(*ang) @ scene["ref_rotation"][b].astype(np.float64)
+        t = scene["ref_translation"][b].astype(np.float64).copy()
+        t[:2] += rng.normal(0.0, trans_xy, 2)
+        t[2] *= 1.0 + rng.normal(0.0, trans_z)
+        d_obj = YCBV_DIAMETERS[int(scene["labels"][b]) % len(YCBV_DIAMETERS)]
+        masks.append(ellipsoid_depth(R, t, scene["internel_k"][b].astype(np.float64), size,
+                                     np.array(ELLIPSOID_AXES) * d_obj) > 0)
+        Rs.append(R)
+        ts.append(t)
+    return dict(gt_rotation=np.stack(Rs).astype(np.float32),
+                gt_translation=np.stack(ts).astype(np.float32), gt_masks=np.stack(masks))

@@ -1,0 +1,106 @@
+"""Training losses of SCFlowRefiner (models/loss/sequence_loss.py:7-80,
+point_matching_loss.py:106-218; composition scflow_refiner.py:182-256; weights from
+configs/refine_models/scflow_ycbv_real.py:231-262), batched over the samples.
+
+The point-matching loss runs all B samples at once when every class's model-point set has the
+same size (one [B, P, 3] gather + batched matmuls); ragged point sets fall back to a per-sample
+loop.  Symmetric classes (SYMMETRIC_CLASSES) replace pytorch3d ``knn_points(K=1)`` by a
+brute-force nearest neighbour (cdist + argmin; indices carry no gradient, as with knn_points).
+"""
+from __future__ import annotations
+
+from typing import Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+Tensor = torch.Tensor
+
+SYMMETRIC_CLASSES = (12, 15, 18)  # 0-based labels of cls_13, cls_16, cls_19 (config :34-38)
+POSE_WEIGHT, FLOW_WEIGHT, MASK_WEIGHT, GAMMA = 10.0, 0.1, 10.0, 0.8
+
+
+def flow_l1_loss(pred: Tensor, gt: Tensor, valid: Tensor, max_flow: float = 400.,
+                 weight: float = FLOW_WEIGHT, eps: float = 1e-10) -> Tensor:
+    """RAFTLoss (sequence_loss.py:15-23): valid-masked L1 of the flow."""
+    v = ((valid >= 0.5) & (gt.pow(2).sum(1).sqrt() < max_flow)).to(gt)
+    return weight * (v[:, None] * (pred - gt).abs()).sum() / (v.sum() + eps)
+
+
+def mask_l1_loss(pred: Tensor, gt: Tensor, weight: float = MASK_WEIGHT) -> Tensor:
+    """L1Loss (sequence_loss.py:34-36)."""
+    return weight * (pred - gt).abs().mean()
+
+
+def _pm_terms(pts: Tensor, pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tensor,
+              sym: Tensor) -> Tensor:
+    """[B] per-sample (l_rot + l_z + l_xy), l1 norms, disentangle_z."""
+    gt_rot = torch.bmm(pts, gt_r.transpose(1, 2))
+    gt_rt = gt_rot + gt_t[:, None]
+    pred_rot = torch.bmm(pts, pred_r.transpose(1, 2)) + gt_t[:, None]
+    if bool(sym.any()):
+        with torch.no_grad():
+            idx = torch.cdist(gt_rt[sym], pred_rot[sym]).argmin(-1)  # [Bs, P]
+        matched = torch.gather(pred_rot[sym], 1, idx[..., None].expand(-1, -1, 3))
+        pred_rot = pred_rot.clone()
+        pred_rot[sym] = matched
+    l_rot = (pred_rot - gt_rt).abs().sum(-1).mean(-1)
+    tz = torch.cat([gt_t[:, :2], pred_t[:, 2:]], 1)
+    txy = torch.cat([pred_t[:, :2], gt_t[:, 2:]], 1)
+    l_z = (gt_rot + tz[:, None] - gt_rt).abs().sum(-1).mean(-1)
+    l_xy = (gt_rot + txy[:, None] - gt_rt).abs().sum(-1).mean(-1)
+    return l_rot + l_z + l_xy
+
+
+def point_matching_loss(pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tensor, labels: Tensor,
+                        points: Sequence[Tensor], diameters: Tensor,
+                        weight: float = POSE_WEIGHT) -> Tensor:
+    """DisentanglePointMatchingLoss (point_matching_loss.py:159-218) with loss_type l1,
+    disentangle_z, no xy/depth scaling, reduction mean."""
+    B = pred_r.shape[0]
+    labels = labels.long()
+    sym = torch.zeros(B, dtype=torch.bool, device=labels.device)
+    for c in SYMMETRIC_CLASSES:
+        sym |= labels == c
+    diam = diameters[labels]
+    if len({int(p.shape[0]) for p in points}) == 1:
+        pts = torch.stack(list(points))[labels]
+        per = _pm_terms(pts, pred_r, pred_t, gt_r, gt_t, sym)
+    else:
+        per = torch.cat([_pm_terms(points[int(labels[i])][None], pred_r[i:i + 1], pred_t[i:i + 1],
+                                   gt_r[i:i + 1], gt_t[i:i + 1], sym[i:i + 1]) for i in range(B)])
+    return weight * (per / diam).sum() / B
+
+
+def sequence_loss(values: Sequence[Tensor], gamma: float = GAMMA) -> Tensor:
+    """SequenceLoss (sequence_loss.py:59-80): Σ γ^(n−i−1)·loss_i."""
+    n = len(values)
+    return sum(gamma ** (n - i - 1) * v for i, v in enumerate(values))
+
+
+def filter_flow_by_mask(flow: Tensor, gt_mask: Tensor, invalid_num: float = 400.) -> Tensor:
+    """filter_flow_by_mask (models/utils/flow.py:6-26)."""
+    N, _, H, W = flow.shape
+    bad = (flow[:, 0] >= invalid_num) & (flow[:, 1] >= invalid_num)
+    yy = torch.arange(H, device=flow.device, dtype=flow.dtype)[:, None]
+    xx = torch.arange(W, device=flow.device, dtype=flow.dtype)[None]
+    gx = (xx + flow[:, 0]) * 2. / max(W - 1, 1) - 1.
+    gy = (yy + flow[:, 1]) * 2. / max(H - 1, 1) - 1.
+    m = F.grid_sample(gt_mask[:, None].to(flow.dtype), torch.stack([gx, gy], -1), mode="bilinear",
+                      padding_mode="zeros", align_corners=False)
+    bad = (m[:, 0] < 0.9) | bad
+    return torch.where(bad[:, None].expand_as(flow), torch.full_like(flow, invalid_num), flow)
+
+
+def refine_losses(outs, gt_r: Tensor, gt_t: Tensor, gt_flow: Tensor, render_mask: Tensor,
+                  labels: Tensor, points: Sequence[Tensor], diameters, max_flow: float = 400.
+                  ) -> Tuple[Tensor, Tensor, Tensor]:
+    """(loss_pose, loss_flow, loss_mask) from the decoder's 7 lists (scflow_refiner.py:200-242)."""
+    _, flow_pred, Rs, ts, masks, _, _ = outs
+    diam = torch.as_tensor(diameters, dtype=gt_r.dtype, device=gt_r.device)
+    lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam)
+                        for R, t in zip(Rs, ts)])
+    lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow) for f in flow_pred])
+    occ = (gt_flow.sum(1) < max_flow).to(gt_flow)
+    lm = sequence_loss([mask_l1_loss(m[:, 0], occ) for m in masks])
+    return lp, lf, lm

@@ -1,0 +1,235 @@
+"""Training forward of SCFlowRefiner on the HIP autograd Functions.
+
+``refiner_train_forward`` reproduces ``SCFlowRefiner.loss`` (models/refiner/scflow_refiner.py:
+182-256) for synthetic batches: shared feature encoder on real + rendered images, context
+encoder (BatchNorm in train mode), the decoder loop with the configured detaches
+(detach_flow / detach_pose / detach_depth_for_xy, scflow_decoder.py:193-236) and back-prop
+through the 8 GRU steps, then the three sequence losses.  Activations are channels-last; every
+convolution is ``conv2d_nhwc`` (HIP forward + backward); the correlation pyramid and lookup are
+HIP Functions; the detached per-iteration geometry (2D-3D lift, pose-induced flow, flow
+downsampling, GT flow) runs on the inference kernels without autograd.  Normalisations,
+activations, the GRU gate algebra, the pose update and the losses are torch ops (pointwise /
+per-sample); FCs are plain library GEMMs.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import Chan
+from .functions import conv2d_nhwc, corr_lookup, corr_pyramid
+from .losses import filter_flow_by_mask, refine_losses
+
+Tensor = torch.Tensor
+
+
+def _act(x: Tensor, act) -> Tensor:
+    if act == "ReLU":
+        return torch.relu(x)
+    if act == "Sigmoid":
+        return torch.sigmoid(x)
+    if act == "Tanh":
+        return torch.tanh(x)
+    return x
+
+
+def _cm(x: Tensor, m) -> Tensor:
+    """mmcv ConvModule (conv → act; the decoder's ConvModules have no norm)."""
+    c = m.conv
+    return _act(conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding), m.act_type)
+
+
+def _conv(x: Tensor, c) -> Tensor:
+    return conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding)
+
+
+# ------------------------------------------------------------------------------- encoders
+def _norm(x: Tensor, mod) -> Tensor:
+    """InstanceNorm2d (affine=False) or BatchNorm2d (train mode: batch statistics, running-stat
+    update) on a channels-last tensor."""
+    if isinstance(mod, torch.nn.InstanceNorm2d):
+        m = x.mean(dim=(1, 2), keepdim=True)
+        v = x.var(dim=(1, 2), unbiased=False, keepdim=True)
+        return (x - m) / torch.sqrt(v + mod.eps)
+    y = F.batch_norm(x.permute(0, 3, 1, 2), mod.running_mean, mod.running_var, mod.weight, mod.bias,
+                     training=mod.training, momentum=mod.momentum, eps=mod.eps)
+    if mod.training and mod.num_batches_tracked is not None:
+        mod.num_batches_tracked.add_(1)
+    return y.permute(0, 2, 3, 1)
+
+
+def encoder_train(enc, x_nhwc: Tensor) -> Tensor:
+    """RAFTEncoder.forward (raft_encoder.py:286-314) with autograd; channels-last in and out."""
+    x = torch.relu(_norm(_conv(x_nhwc, enc.conv1), enc.norm1))
+    for name in enc.res_layers:
+        for blk in getattr(enc, name):
+            out = torch.relu(_norm(_conv(x, blk.conv1), blk.norm1))
+            out = _norm(_conv(out, blk.conv2), blk.norm2)
+            ident = x if blk.downsample is None else _norm(_conv(x, blk.downsample[0]), blk.downsample[1])
+            x = torch.relu(out + ident)
+    return _conv(x, enc.conv2)
+
+
+# ------------------------------------------------------------------------------- pose head
+def pose_head_train(head, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
+    """MultiClassPoseHead.forward (pose_head.py:201-211), label[0] quirk kept."""
+    for m in head.conv_layers:
+        c = m.conv
+        y = conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding)
+        y = F.group_norm(y.permute(0, 3, 1, 2), m.gn.num_groups, m.gn.weight, m.gn.bias, m.gn.eps)
+        x = torch.relu(y).permute(0, 2, 3, 1)
+    v = x.permute(0, 3, 1, 2).reshape(x.shape[0], -1)  # nn.Flatten of NCHW
+    for fc in head.fc_layers:
+        v = torch.relu(F.linear(v, fc[0].weight, fc[0].bias))
+    n = v.shape[0]
+    t = F.linear(v, head.translation_pred.weight, head.translation_pred.bias).view(n, head.num_class, 3)
+    r = F.linear(v, head.rotation_pred.weight, head.rotation_pred.bias).view(
+        n, head.num_class, head.rotation_out_channels)
+    t = torch.index_select(t, 1, label)[:, 0]
+    r = torch.index_select(r, 1, label)[:, 0]
+    return r, t
+
+
+# ------------------------------------------------------------------------------- pose maths
+def _normalize(v: Tensor) -> Tensor:
+    return v / v.norm(dim=1, keepdim=True).clamp_min(1e-12)
+
+
+def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 10.0,
+                depth_transform: str = "exp", detach_depth_for_xy: bool = True) -> Tuple[Tensor, Tensor]:
+    """get_pose_from_delta_pose + get_rotation_matrix_from_ortho6d (pose.py:124-169)."""
+    x = _normalize(drot[:, 0:3])
+    z = _normalize(torch.cross(x, drot[:, 3:6], dim=1))
+    y = torch.cross(z, x, dim=1)
+    Rd = torch.bmm(torch.stack([x, y, z], dim=2), R)
+    vz = t[:, 2] / torch.exp(dt[:, 2]) if depth_transform == "exp" else t[:, 2] * (dt[:, 2] + 1)
+    vzxy = vz.detach() if detach_depth_for_xy else vz
+    vx = vzxy * (dt[:, 0] / weight + t[:, 0] / t[:, 2])
+    vy = vzxy * (dt[:, 1] / weight + t[:, 1] / t[:, 2])
+    return Rd, torch.stack([vx, vy, vz], dim=-1)
+
+
+# ------------------------------------------------------------------------------- decoder
+def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: Tensor, R0: Tensor,
+                  t0: Tensor, depth: Tensor, K: Tensor, label: Tensor, iters: int,
+                  invalid_flow_num: float = 0.0) -> Tuple[List[Tensor], ...]:
+    """SCFlowDecoder.forward with autograd (scflow_decoder.py:151-252); features channels-last
+    [N, h, w, C].  Returns (flow_from_pose, flow_from_pred, R, t, mask, Δrot, Δt) lists."""
+    if not dec.detach_flow or dec.mask_flow or dec.mask_corr:
+        raise NotImplementedError("training path follows the configured decoder: detach_flow=True, "
+                                  "mask_flow=mask_corr=False (scflow_ycbv_real.py:213-218)")
+    N, hh, ww, _ = feat_render.shape
+    _, H, W = depth.shape
+    dt = feat_render.dtype
+    L, r = dec.num_levels, dec.radius
+    scale = 2 ** (L - 1)
+    pyr = corr_pyramid(feat_render.permute(0, 3, 1, 2), feat_real.permute(0, 3, 1, 2), L)
+    depth = depth.contiguous().to(dt)
+    K = K.contiguous().to(dt)
+    with torch.no_grad():
+        points = ops.lift_points(depth, K, R0.contiguous().to(dt), t0.contiguous().to(dt))
+    flow_full = torch.zeros(N, 2, H, W, device=depth.device, dtype=dt)
+    R, t = R0.to(dt), t0.to(dt)
+    label = label.long()
+    outs = ([], [], [], [], [], [], [])
+    enc = dec.encoder
+    zr_w = [torch.cat([z.conv.weight, rr.conv.weight], 0) for z, rr in zip(dec.gru.conv_z, dec.gru.conv_r)]
+    zr_b = [torch.cat([z.conv.bias, rr.conv.bias], 0) for z, rr in zip(dec.gru.conv_z, dec.gru.conv_r)]
+    hc = dec.h_channels
+    for _ in range(iters):
+        with torch.no_grad():  # flow is detached every iteration (detach_flow=True)
+            f2 = torch.empty(N * hh * ww, 2, device=depth.device, dtype=dt)
+            ops.flow_downsample(flow_full.contiguous(), Chan.whole(f2), hh, ww, 1.0 / scale)
+        f2 = f2.view(N, hh, ww, 2)
+        corr = corr_lookup(pyr, f2, N, hh, ww, L, r)
+        c = corr
+        for m in enc.corr_net:
+            c = _cm(c, m)
+        f = f2
+        for m in enc.flow_net:
+            f = _cm(f, m)
+        out = torch.cat([c, f], -1)
+        for m in enc.out_net:
+            out = _cm(out, m)
+        motion = torch.cat([out, f2], -1)
+        x = torch.cat([cxt, motion], -1)
+        for s, q in enumerate(dec.gru.conv_q):  # SeqConv: 1×5 then 5×1
+            hx = torch.cat([h, x], -1)
+            zr = torch.sigmoid(conv2d_nhwc(hx, zr_w[s], zr_b[s], 1, q.conv.padding))
+            z, rg = zr[..., :hc], zr[..., hc:]
+            qq = torch.tanh(conv2d_nhwc(torch.cat([rg * h, x], -1), q.conv.weight, q.conv.bias, 1,
+                                        q.conv.padding))
+            h = (1 - z) * h + z * qq
+        fh = h
+        for m in dec.flow_pred.layers:
+            fh = _cm(fh, m)
+        dflow = _conv(fh, dec.flow_pred.predict_layer)
+        mh = h
+        for m in dec.mask_pred.layers:
+            mh = _cm(mh, m)
+        mask = torch.sigmoid(_conv(mh, dec.mask_pred.predict_layer))
+        dff = dflow
+        for m in dec.delta_flow_encoder:
+            dff = _cm(dff, m)
+        mf = mask
+        for m in dec.mask_encoder:
+            mf = _cm(mf, m)
+        drot, dtr = pose_head_train(dec.pose_pred, torch.cat([h, dff, mf], -1), label)
+        flow_pred = scale * F.interpolate((f2 + dflow).permute(0, 3, 1, 2), scale_factor=(scale, scale),
+                                          mode="bilinear", align_corners=True)
+        up_mask = F.interpolate(mask.permute(0, 3, 1, 2), scale_factor=(scale, scale), mode="bilinear",
+                                align_corners=True)
+        if dec.detach_pose:
+            R, t = R.detach(), t.detach()
+        R, t = pose_update(drot, dtr, R, t, depth_transform=dec.depth_transform,
+                           detach_depth_for_xy=dec.detach_depth_for_xy)
+        with torch.no_grad():
+            flow_full = torch.empty(N, 2, H, W, device=depth.device, dtype=dt)
+            ops.pose_flow(R.detach().contiguous(), t.detach().contiguous(), K, points,
+                          float(invalid_flow_num), out=flow_full)
+        for lst, v in zip(outs, (flow_full, flow_pred, R, t, up_mask, drot, dtr)):
+            lst.append(v)
+    return outs
+
+
+def refiner_train_forward(refiner, batch: Dict[str, Tensor], model_points: Sequence[Tensor],
+                          diameters: Sequence[float], iters: int = None) -> Dict[str, Tensor]:
+    """Images → losses (SCFlowRefiner.loss), autograd graph attached.  ``batch`` keys:
+    render_images, real_images [N,3,S,S]; ref_rotation, ref_translation, gt_rotation,
+    gt_translation, internel_k, depth, label."""
+    dec = refiner.decoder
+    iters = int(dec.iters if iters is None else iters)
+    real = batch["real_images"].permute(0, 2, 3, 1).contiguous()
+    render = batch["render_images"].permute(0, 2, 3, 1).contiguous()
+    N = real.shape[0]
+    dt = real.dtype
+    if refiner.real_encoder is refiner.render_encoder:  # shared: one batch of 2N images
+        feats = encoder_train(refiner.real_encoder, torch.cat([real, render], 0))
+        feat_real, feat_render = feats[:N], feats[N:]
+    else:
+        feat_real = encoder_train(refiner.real_encoder, real)
+        feat_render = encoder_train(refiner.render_encoder, render)
+    cx = encoder_train(refiner.context, render)
+    hc = refiner.h_channels
+    h, cxt = torch.tanh(cx[..., :hc]), torch.relu(cx[..., hc:])
+    outs = decoder_train(dec, feat_render, feat_real, h, cxt, batch["ref_rotation"],
+                         batch["ref_translation"], batch["depth"], batch["internel_k"], batch["label"],
+                         iters)
+    with torch.no_grad():  # GT flow: lift with the reference pose, project with the GT pose
+        depth = batch["depth"].contiguous().to(dt)
+        K = batch["internel_k"].contiguous().to(dt)
+        pts = ops.lift_points(depth, K, batch["ref_rotation"].contiguous().to(dt),
+                              batch["ref_translation"].contiguous().to(dt))
+        gt_flow = torch.empty(N, 2, *depth.shape[1:], device=depth.device, dtype=dt)
+        ops.pose_flow(batch["gt_rotation"].contiguous().to(dt), batch["gt_translation"].contiguous().to(dt),
+                      K, pts, refiner.max_flow, out=gt_flow)
+        if refiner.filter_invalid_flow and "gt_masks" in batch:
+            gt_flow = filter_flow_by_mask(gt_flow, batch["gt_masks"], refiner.max_flow)
+        render_mask = (depth > 0).to(dt)
+    lp, lf, lm = refine_losses(outs, batch["gt_rotation"].to(dt), batch["gt_translation"].to(dt),
+                               gt_flow, render_mask, batch["label"], model_points, diameters,
+                               refiner.max_flow)
+    return dict(loss=lp + lf + lm, loss_pose=lp, loss_flow=lf, loss_mask=lm, outs=outs, gt_flow=gt_flow)

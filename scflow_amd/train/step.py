@@ -1,0 +1,132 @@
+"""One training iteration of the refinement model (the reference runs it
+through mmengine's OptimWrapper: configs/refine_models/scflow_ycbv_real.py:285-305 — AdamW
+lr 4e-4, betas (0.9, 0.999), eps 1e-8, weight decay 1e-4, clip_grad max_norm 10, OneCycleLR).
+
+Data parallel = one process per GPU (torch.distributed over RCCL).  Gradients live in a few
+flat fp32 buckets (every ``param.grad`` is a view into one), so the exchange is one all-reduce
+per bucket; each bucket's all-reduce is issued asynchronously from a post-accumulate-grad hook
+as soon as its last gradient is written, overlapping the exchange with the rest of the backward
+pass.  Buckets are filled in reverse registration order (≈ the order backward produces
+gradients), sized for xGMI (default 32 MB: large enough that the ring is link-bound, small
+enough that the first buckets start early).  No per-parameter collectives, no DDP wrapper.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .model import refiner_train_forward
+
+Tensor = torch.Tensor
+
+
+class GradBuckets:
+    """Flat gradient buckets with overlapped all-reduce (average over the process group)."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], bucket_bytes: int = 32 << 20,
+                 group=None) -> None:
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.buckets: List[Tensor] = []
+        self.members: List[List[torch.nn.Parameter]] = []
+        cur: List[torch.nn.Parameter] = []
+        size = 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= bucket_bytes:
+                self.members.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.members.append(cur)
+        self._bucket_of = {}
+        for bi, mem in enumerate(self.members):
+            dev = mem[0].device
+            flat = torch.zeros(sum(p.numel() for p in mem), device=dev, dtype=mem[0].dtype)
+            off = 0
+            for p in mem:
+                p.grad = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+                self._bucket_of[p] = bi
+            self.buckets.append(flat)
+        self._pending = [0] * len(self.members)
+        self._work: List[Optional[object]] = [None] * len(self.members)
+        self._hooks = []
+        if self.world > 1:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p) -> None:
+        bi = self._bucket_of[p]
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._work[bi] = dist.all_reduce(self.buckets[bi], op=dist.ReduceOp.SUM, group=self.group,
+                                             async_op=True)
+
+    def zero(self) -> None:
+        for b in self.buckets:
+            b.zero_()
+        for bi, mem in enumerate(self.members):
+            self._pending[bi] = len(mem)
+            self._work[bi] = None
+
+    def finish(self) -> None:
+        """Wait for every bucket's all-reduce (issuing any whose hooks did not all fire — a
+        parameter without a gradient this step) and average."""
+        if self.world == 1:
+            return
+        for bi, flat in enumerate(self.buckets):
+            if self._work[bi] is None:
+                self._work[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group,
+                                                 async_op=True)
+        for bi, flat in enumerate(self.buckets):
+            self._work[bi].wait()
+            flat.mul_(1.0 / self.world)
+            self._work[bi] = None
+
+    def clip_(self, max_norm: float) -> Tensor:
+        """clip_grad_norm_ (L2 over all parameters) on the flat buckets."""
+        norms = torch.stack([b.norm() for b in self.buckets])
+        total = norms.norm()
+        coef = (max_norm / (total + 1e-6)).clamp(max=1.0)
+        for b in self.buckets:
+            b.mul_(coef)
+        return total
+
+
+class TrainStep:
+    """forward (HIP) → losses → backward (HIP) → bucketed all-reduce → clip → AdamW."""
+
+    def __init__(self, refiner, model_points: Sequence[Tensor], diameters: Sequence[float],
+                 lr: float = 4e-4, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 max_norm: float = 10.0, bucket_bytes: int = 32 << 20, iters: Optional[int] = None,
+                 group=None) -> None:
+        self.refiner = refiner
+        self.model_points = list(model_points)
+        self.diameters = list(diameters)
+        self.max_norm = max_norm
+        self.iters = iters
+        params = list(dict.fromkeys(refiner.parameters()))  # the shared encoder appears twice
+        self.grads = GradBuckets(params, bucket_bytes, group)
+        self.opt = torch.optim.AdamW(self.grads.params, lr=lr, betas=betas, eps=eps,
+                                     weight_decay=weight_decay, foreach=True)
+        if dist.is_initialized() and dist.get_world_size(group) > 1:
+            self.broadcast_parameters()
+
+    def broadcast_parameters(self, src: int = 0) -> None:
+        """Start every rank from rank 0's weights and BN statistics."""
+        for t in list(self.refiner.parameters()) + list(self.refiner.buffers()):
+            dist.broadcast(t.data, src, group=self.grads.group)
+
+    def __call__(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        self.refiner.train()
+        self.grads.zero()
+        out = refiner_train_forward(self.refiner, batch, self.model_points, self.diameters, self.iters)
+        out["loss"].backward()
+        self.grads.finish()
+        out["grad_norm"] = self.grads.clip_(self.max_norm)
+        self.opt.step()
+        return out

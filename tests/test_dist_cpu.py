@@ -43,7 +43,7 @@ def _worker(rank, world, port, q):
         flow, pred, R, t = gather_results(out)
         x = gather_shards(torch.arange(rank * 10, rank * 10 + mine["depth"].shape[0]).float())
         if rank == 0:
-            q.put((flow, pred, R, t, x))
+            q.put(tuple(a.numpy() for a in (flow, pred, R, t, x)))  # by value: the sender exits
     finally:
         dist.destroy_process_group()
 
@@ -55,7 +55,7 @@ def test_sharded_decode_equals_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    flow, pred, R, t, x = q.get(timeout=240)
+    flow, pred, R, t, x = (torch.from_numpy(a) for a in q.get(timeout=240))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

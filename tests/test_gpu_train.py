@@ -1,0 +1,69 @@
+"""GPU: the HIP training step (§8(f) rank 2) — SCFlowRefiner.loss forward + backward on the HIP
+autograd Functions against fp64 CPU autograd of the oracle's restatement, then the optimizer step.
+
+Tolerances (fp32 HIP vs fp64): losses rtol 1e-4; per-parameter gradient error
+‖g − g_ref‖ / max(‖g_ref‖, 1e-4·‖G_ref‖) (G = all gradients; the floor covers the conv biases that
+feed a normalisation, whose true gradient is 0) ≤ 1e-3 for the decoder's parameters and ≤ 1e-2 for
+the encoders', which sit behind the correlation volume and the instance / batch norms: plain
+PyTorch fp32 autograd of the same graph on the CPU lands at 6e-3 on the encoder weights and 2e-2
+on the context stem's bias (tests/test_train_host.py wiring, measured when this test was written)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.test_train_host import build_train_refiner, oracle_loss_and_grads, train_batch
+
+pytestmark = pytest.mark.gpu
+orc = pytest.importorskip("oracle.scflow_oracle")
+
+
+def test_train_forward_backward_matches_oracle():
+    from scflow_amd.train.model import refiner_train_forward
+    iters = 2
+    r = build_train_refiner(iters).cuda()
+    batch, points, diam = train_batch(2, 256, seed=5, labels=[12, 4])
+    gb = {k: v.cuda() for k, v in batch.items()}
+    res = refiner_train_forward(r, gb, [p.cuda() for p in points], diam)
+    res["loss"].backward()
+    torch.cuda.synchronize()
+    names = [n for n, _ in r.named_parameters()]
+    (loss, lp, lf, lm), outs, gt_flow, grads = oracle_loss_and_grads(batch, points, diam, iters, names)
+    assert float(orc.cal_epe_mean(gt_flow.float(), res["gt_flow"].cpu()).max()) <= 1e-3
+    for a, b in ((res["loss_pose"], lp), (res["loss_flow"], lf), (res["loss_mask"], lm)):
+        np.testing.assert_allclose(a.item(), b.item(), rtol=1e-4)
+    G = sum(float(g.double().norm()) ** 2 for g in grads.values() if g is not None) ** 0.5
+    errs = {}
+    for n, p in r.named_parameters():
+        g = grads[n]
+        if g is None:
+            continue
+        ref = g.double()
+        errs[n] = float((p.grad.double().cpu() - ref).norm() / max(float(ref.norm()), 1e-4 * G))
+    out = os.environ.get("SCFLOW_TRAIN_ERRS")
+    if out:
+        with open(out, "w") as f:
+            json.dump(dict(sorted(errs.items(), key=lambda kv: -kv[1])), f, indent=1)
+    assert len(errs) > 100
+    for part, tol in (("decoder.", 1e-3), ("", 1e-2)):
+        sub = {k: v for k, v in errs.items() if k.startswith(part)}
+        worst = max(sub, key=sub.get)
+        assert sub[worst] <= tol, f"{worst}: relative gradient error {sub[worst]:.3e}"
+
+
+def test_train_step_reduces_loss():
+    """A few AdamW steps (lr 4e-4, clip 10) on one fixed batch lower the loss; BN running stats
+    move; every parameter stays finite."""
+    from scflow_amd.train.step import TrainStep
+    r = build_train_refiner(2).cuda()
+    batch, points, diam = train_batch(2, 256, seed=6)
+    gb = {k: v.cuda() for k, v in batch.items()}
+    rm0 = r.context.norm1.running_mean.clone()
+    step = TrainStep(r, [p.cuda() for p in points], diam)
+    losses = [float(step(gb)["loss"].detach()) for _ in range(4)]
+    torch.cuda.synchronize()
+    assert losses[-1] < losses[0], losses
+    assert not torch.equal(rm0, r.context.norm1.running_mean)
+    assert all(bool(torch.isfinite(p).all()) for p in r.parameters())

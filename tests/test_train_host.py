@@ -1,0 +1,139 @@
+"""CPU: the training forward's host composition (scflow_amd/train/model.py + losses.py) against
+the oracle's SCFlowRefiner.loss restatement (oracle.refine_train_forward), fp64.
+
+The HIP pieces the model calls (conv Function, correlation pyramid / lookup Functions, the 2D-3D
+lift, pose-induced flow and flow downsampling kernels) are swapped for plain torch equivalents
+here — this test checks the wiring (detaches, BN train mode, the GRU split, pose-head quirk, GT
+flow + mask filtering, the loss weights and the sequence weighting) and the gradients that flow
+through it; the HIP Functions themselves are covered by tests/test_gpu_train_ops.py and the whole
+HIP training step by tests/test_gpu_train.py."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests.helpers import refiner_state_dict
+
+orc = pytest.importorskip("oracle.scflow_oracle")
+
+
+def _patch_torch_ops(monkeypatch):
+    from scflow_amd import ops
+    from scflow_amd.train import model
+
+    def conv(x, w, b=None, stride=1, padding=0):
+        return F.conv2d(x.permute(0, 3, 1, 2), w, b, stride, padding).permute(0, 2, 3, 1)
+
+    def pyramid(f1, f2, L=4):
+        return orc.corr_pyramid(f1, f2, L)
+
+    def lookup(levels, flow_nhwc, n, h, w, L=4, r=4):
+        return orc.corr_lookup(levels, flow_nhwc.detach().permute(0, 3, 1, 2), r).permute(0, 2, 3, 1)
+
+    def lift(depth, K, R, t):
+        p, v = orc.lift_points(depth, K, R, t)
+        return torch.cat([p, v[..., None].to(p)], -1)
+
+    def pose_flow(R, t, K, pts, inv, out=None):
+        f = orc.pose_flow(R, t, K, pts[..., :3], pts[..., 3] > 0, inv)
+        if out is None:
+            return f
+        out.copy_(f)
+        return out
+
+    def downsample(flow, out0, h, w, value_scale, out1=None):
+        f = orc.downsample_flow(flow, int(round(1 / value_scale)))
+        out0.buf.view(-1, out0.buf.shape[-1])[:, out0.off:out0.off + 2] = f.permute(0, 2, 3, 1).reshape(-1, 2)
+
+    monkeypatch.setattr(model, "conv2d_nhwc", conv)
+    monkeypatch.setattr(model, "corr_pyramid", pyramid)
+    monkeypatch.setattr(model, "corr_lookup", lookup)
+    monkeypatch.setattr(ops, "lift_points", lift)
+    monkeypatch.setattr(ops, "pose_flow", pose_flow)
+    monkeypatch.setattr(ops, "flow_downsample", downsample)
+
+
+def build_train_refiner(iters, dtype=torch.float32):
+    from scflow_amd import MODELS
+    from tests.test_gpu_decoder import decoder_cfg
+    enc = dict(type="RAFTEncoder", in_channels=3, out_channels=256, net_type="Basic",
+               norm_cfg=dict(type="IN"))
+    ctx = dict(type="RAFTEncoder", in_channels=3, out_channels=256, net_type="Basic",
+               norm_cfg=dict(type="BN"))
+    r = MODELS.build(dict(type="SCFlowRefiner", cxt_channels=128, h_channels=128,
+                          seperate_encoder=False, encoder=enc, cxt_encoder=ctx,
+                          decoder=dict(type="SCFlowDecoder", **decoder_cfg(iters))))
+    missing, unexpected = r.load_state_dict(
+        {("decoder." + k if not k.startswith(("real_encoder.", "render_encoder.", "context.")) else k): v
+         for k, v in refiner_state_dict().items()}, strict=False)
+    assert not unexpected and all(k.endswith("num_batches_tracked") for k in missing), missing
+    return r.to(dtype).train()
+
+
+def train_batch(B, S, seed, labels=None, dtype=torch.float32, device="cpu"):
+    """Synthetic training batch (images, reference + GT pose, depth, K, GT mask) + model points."""
+    from scflow_amd import synthetic
+    scene = synthetic.make_scene(B, S, seed=seed)
+    if labels is not None:
+        scene["labels"] = np.asarray(labels, np.int64)
+    tgt = synthetic.make_train_targets(scene, S, seed=seed)
+    imgs = synthetic.make_images(B, S, seed=seed)
+    batch = {**imgs, **{k: v for k, v in scene.items() if k != "labels"}, **tgt}
+    out = {}
+    for k, v in batch.items():
+        x = torch.from_numpy(np.ascontiguousarray(v))
+        out[k] = (x.to(dtype) if x.is_floating_point() else x).to(device)
+    out["label"] = torch.from_numpy(scene["labels"]).to(device)
+    pts = torch.from_numpy(synthetic.make_model_points(256)).to(dtype).to(device)
+    return out, list(pts), list(synthetic.YCBV_DIAMETERS)
+
+
+def oracle_loss_and_grads(batch, points, diameters, iters, names):
+    """fp64 CPU autograd of the oracle's SCFlowRefiner.loss restatement; grads keyed by the
+    product module's parameter names."""
+    sd = {k: v.double().requires_grad_(v.is_floating_point()) for k, v in refiner_state_dict().items()}
+    b = {k: (v.double() if v.is_floating_point() else v).cpu() for k, v in batch.items()}
+    loss, lp, lf, lm, outs, gt_flow = orc.refine_train_forward(
+        sd, b["render_images"], b["real_images"], b["ref_rotation"], b["ref_translation"],
+        b["gt_rotation"], b["gt_translation"], b["depth"], b["internel_k"], b["label"],
+        [p.double().cpu() for p in points], diameters, gt_masks=b["gt_masks"], iters=iters)
+    loss.backward()
+    grads = {}
+    for n in names:
+        k = n if n.startswith(("real_encoder.", "render_encoder.", "context.")) else n[len("decoder."):]
+        if k.startswith(("real_encoder.", "render_encoder.")):  # shared: both oracle copies
+            tail = k.split(".", 1)[1]
+            g = sd["real_encoder." + tail].grad
+            gr = sd["render_encoder." + tail].grad
+            grads[n] = None if g is None and gr is None else (
+                (g if g is not None else 0) + (gr if gr is not None else 0))
+        else:
+            grads[n] = sd[k].grad
+    return (loss, lp, lf, lm), outs, gt_flow, grads
+
+
+def test_train_forward_host_matches_oracle(monkeypatch):
+    from scflow_amd.train.model import refiner_train_forward
+    _patch_torch_ops(monkeypatch)
+    iters = 2
+    r = build_train_refiner(iters, torch.float64)
+    batch, points, diam = train_batch(2, 256, seed=5, labels=[12, 4], dtype=torch.float64)
+    res = refiner_train_forward(r, batch, points, diam)
+    res["loss"].backward()
+    names = [n for n, _ in r.named_parameters()]
+    (loss, lp, lf, lm), outs, gt_flow, grads = oracle_loss_and_grads(batch, points, diam, iters, names)
+    np.testing.assert_allclose(res["gt_flow"].numpy(), gt_flow.numpy(), rtol=1e-9, atol=1e-6)
+    for a, b in ((res["loss_pose"], lp), (res["loss_flow"], lf), (res["loss_mask"], lm)):
+        np.testing.assert_allclose(a.item(), b.item(), rtol=1e-9)
+    checked = 0
+    for n, p in r.named_parameters():
+        g = grads[n]
+        if g is None:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, n
+            continue
+        np.testing.assert_allclose(p.grad.numpy(), g.numpy(), rtol=1e-7, atol=1e-9 * (1 + float(g.abs().max())),
+                                   err_msg=n)
+        checked += 1
+    assert checked > 100
+    # BN running stats were updated in train mode (SCFlowRefiner.train())
+    assert int(r.context.norm1.num_batches_tracked) == 1
