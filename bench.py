@@ -141,6 +141,36 @@ def secondary_rooflines(timers, batch, size):
     return out
 
 
+def bench_train(args, world, rank, dev, feat):
+    """BASELINE configs[3]: the training step — SCFlowRefiner.loss forward on the HIP kernels,
+    backward through the HIP adjoint kernels, bucketed gradient all-reduce over RCCL (world > 1,
+    overlapped with the backward pass), clip 10, AdamW — `train_batch` pairs per GPU."""
+    from scflow_amd import synthetic
+    from scflow_amd.train.step import TrainStep
+    ref = build_refiner(args.iters, dev, feat).train()
+    raw = synthetic.make_train_batch(args.train_batch, args.size, seed=2000 + rank)
+    batch = {k: torch.from_numpy(v).to(dev) for k, v in raw.items()}
+    pts = [torch.from_numpy(p).to(dev) for p in synthetic.make_model_points(1024)]
+    step = TrainStep(ref, pts, synthetic.YCBV_DIAMETERS)
+    losses = []
+
+    def one():
+        losses.append(step(batch)["loss"].detach())
+    el = time_steps(one, args.train_steps, 2, world, dev)
+    nparam = sum(p.numel() for p in step.grads.params)
+    out = {"workload": f"training step (SCFlowRefiner.loss fwd+bwd, 3 losses, grad all-reduce, clip, "
+                       f"AdamW), {args.train_batch} pairs/GPU, {args.size}x{args.size}, {args.iters} "
+                       f"iters (BASELINE configs[3] at N=8: global batch {8 * args.train_batch})",
+           "value": round(world * args.train_batch * args.iters * args.train_steps / el, 2),
+           "unit": "iters/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
+           "steps": args.train_steps, "warmup": 2, "global_batch": world * args.train_batch,
+           "allreduce_bytes": 4 * nparam if world > 1 else 0,
+           "buckets": len(step.grads.buckets),
+           "loss_first_last": [round(float(losses[0]), 4), round(float(losses[-1]), 4)]}
+    del step, ref, batch
+    return out
+
+
 def cpu_baseline(seconds: float, iters: int, size: int):
     """Time the CPU oracle on a bounded sample: B=2 pairs, `iters` iterations, repeated."""
     from oracle import scflow_oracle as orc
@@ -178,6 +208,10 @@ def main():
                     help="pairs/GPU of the extra end-to-end (images → encoders → decoder) "
                          "measurement, BASELINE configs[2]; 0 disables it")
     ap.add_argument("--e2e-steps", type=int, default=5)
+    ap.add_argument("--train-batch", type=int, default=16,
+                    help="pairs/GPU of the extra training-step measurement (BASELINE configs[3]); "
+                         "0 disables it")
+    ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="do not bracket the roofline kernel (throughput without timer overhead)")
     ap.add_argument("--graph", action="store_true",
@@ -253,6 +287,8 @@ def main():
                "steps": args.e2e_steps, "warmup": 2}
         del ref, rin
 
+    train = bench_train(args, world, rank, dev, feat) if args.train_batch > 0 else None
+
     units = world * args.batch * args.iters * args.steps
     value = units / elapsed
     zr_ms = timer.mean_ms()
@@ -299,6 +335,8 @@ def main():
         res["rooflines_secondary"] = secondary_rooflines(timers, args.batch, args.size)
         if e2e is not None:
             res["end_to_end"] = e2e
+        if train is not None:
+            res["training_step"] = train
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.iters, args.size)
         print(json.dumps(res), flush=True)

@@ -220,3 +220,15 @@ def make_train_targets(scene: Dict[str, np.ndarray], size: int, seed: int = 0,
         ts.append(t)
     return dict(gt_rotation=np.stack(Rs).astype(np.float32),
                 gt_translation=np.stack(ts).astype(np.float32), gt_masks=np.stack(masks))
+
+
+def make_train_batch(batch: int, size: int, seed: int = 0, labels=None) -> Dict[str, np.ndarray]:
+    """One supervised training batch (the fields SCFlowRefiner.loss reads after
+    format_data_train_sup, base_refiner.py:154-225): image pair, reference + GT pose, rendered
+    depth, intrinsics, labels, GT mask."""
+    scene = make_scene(batch, size, seed=seed)
+    if labels is not None:
+        scene["labels"] = np.asarray(labels, np.int64)
+    out = {**make_images(batch, size, seed=seed), **scene, **make_train_targets(scene, size, seed=seed)}
+    out["label"] = out.pop("labels")
+    return out

@@ -73,17 +73,10 @@ def build_train_refiner(iters, dtype=torch.float32):
 def train_batch(B, S, seed, labels=None, dtype=torch.float32, device="cpu"):
     """Synthetic training batch (images, reference + GT pose, depth, K, GT mask) + model points."""
     from scflow_amd import synthetic
-    scene = synthetic.make_scene(B, S, seed=seed)
-    if labels is not None:
-        scene["labels"] = np.asarray(labels, np.int64)
-    tgt = synthetic.make_train_targets(scene, S, seed=seed)
-    imgs = synthetic.make_images(B, S, seed=seed)
-    batch = {**imgs, **{k: v for k, v in scene.items() if k != "labels"}, **tgt}
     out = {}
-    for k, v in batch.items():
+    for k, v in synthetic.make_train_batch(B, S, seed=seed, labels=labels).items():
         x = torch.from_numpy(np.ascontiguousarray(v))
         out[k] = (x.to(dtype) if x.is_floating_point() else x).to(device)
-    out["label"] = torch.from_numpy(scene["labels"]).to(device)
     pts = torch.from_numpy(synthetic.make_model_points(256)).to(dtype).to(device)
     return out, list(pts), list(synthetic.YCBV_DIAMETERS)
 

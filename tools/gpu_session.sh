@@ -24,13 +24,25 @@ if [ $WHAT = all ] || [ $WHAT = prof ]; then
   cd /tmp
   # decoder-only (the bench's roofline kernel averages must agree with this profile)
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run -- \
-      python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-batch 0 > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err
+      python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --e2e-batch 0 --train-batch 0 > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err
   rc=$?; echo "rocprof rc=$rc"
   [ $rc -eq 0 ] || exit $rc
   # end-to-end refiner (configs[2]) kernels
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_e2e_$TAG -o run -- \
-      python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --e2e-steps 3 > $OUT/bench_prof_e2e_$TAG.json 2> $OUT/prof_e2e_$TAG.err
+      python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --e2e-steps 3 --train-batch 0 > $OUT/bench_prof_e2e_$TAG.json 2> $OUT/prof_e2e_$TAG.err
   rc=$?; echo "rocprof e2e rc=$rc"
   [ $rc -eq 0 ] || exit $rc
   find $OUT/prof_$TAG -name "*stats*" | head
+fi
+if [ $WHAT = all ] || [ $WHAT = prof ] || [ $WHAT = trainprof ]; then
+  cd /tmp
+  # training step (configs[3] per GPU)
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_train_$TAG -o run -- \
+      python $R/tools/train_bench.py --steps 3 --warmup 2 > $OUT/bench_prof_train_$TAG.json 2> $OUT/prof_train_$TAG.err
+  rc=$?; echo "rocprof train rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+  db=$(find $OUT/prof_train_$TAG -name "*.db" | head -1)
+  python $R/tools/stats_file.py $db "python tools/train_bench.py --steps 3 --warmup 2 (5 training steps, B=16, 256x256, 8 iters)" > $OUT/train_stats_$TAG.txt
+  python $R/tools/busy.py $db > $OUT/train_busy_$TAG.txt 2>&1 || true
+  rm -rf $OUT/prof_train_$TAG
 fi
