@@ -248,6 +248,32 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
  *   SCFlow (scflow_decoder.py:193-194), so no flow gradient. */
 int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh, int kw,
                   int stride, int ph, int pw, void* stream);
+
+/* scflow_conv_wgrad: weight (and bias) gradient of a channels-last conv without an im2col
+ * matrix — dw[co][ci][ty][tx] (+)= Σ_p dy[p][co] · x[n][oy·s − ph + ty][ox·s − pw + tx][ci],
+ * db[co] (+)= Σ_p dy[p][co] (db may be NULL); x = the channel concat of src0 (cin0) and src1
+ * (cin1, optional).  Replaces the weight-gradient half of the reference's autograd for every
+ * nn.Conv2d on the training path (torch.nn.grad.conv2d_weight, called by
+ * SCFlowRefiner.loss → backward, scflow_refiner.py:182-256).  Shapes: 1×1 and 3×3 (stride 1
+ * or 2), 1×5 and 5×1 (stride 1); others return SCFLOW_EUNSUPPORTED.  `workspace` holds the
+ * per-split partial sums: at least scflow_conv_wgrad_workspace() floats.  The split count
+ * follows the device's CU count; the reduction order is fixed (deterministic). */
+typedef struct {
+  const float* dy;
+  int sdy;
+  const float* src0;
+  int cin0, s0;
+  const float* src1;
+  int cin1, s1;
+  float* dw;
+  float* db;
+  float* workspace;
+  long long workspace_floats;
+  int n, h, w, cout, kh, kw, stride, ph, pw;
+  int accumulate;
+} scflow_wgrad_args;
+int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats);
+int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream);
 int scflow_corr_lookup_backward(const float* dout, int out_layout, int out_stride, const float* flow,
                                 int flow_layout, float* dpyr, int n, int h, int w, int num_levels,
                                 int radius, void* stream);

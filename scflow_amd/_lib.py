@@ -57,6 +57,20 @@ class EncConvArgs(ctypes.Structure):
     ]
 
 
+class WgradArgs(ctypes.Structure):
+    """Mirror of ``scflow_wgrad_args`` (include/scflow_hip.h)."""
+    _fields_ = [
+        ("dy", c_vp), ("sdy", c_int),
+        ("src0", c_vp), ("cin0", c_int), ("s0", c_int),
+        ("src1", c_vp), ("cin1", c_int), ("s1", c_int),
+        ("dw", c_vp), ("db", c_vp),
+        ("workspace", c_vp), ("workspace_floats", c_ll),
+        ("n", c_int), ("h", c_int), ("w", c_int), ("cout", c_int), ("kh", c_int), ("kw", c_int),
+        ("stride", c_int), ("ph", c_int), ("pw", c_int),
+        ("accumulate", c_int),
+    ]
+
+
 # name -> (restype, argtypes); every function the header declares
 SIGNATURES = {
     "scflow_version": (c_int, []),
@@ -103,6 +117,8 @@ SIGNATURES = {
     "scflow_enc_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "scflow_enc_norm_finalize": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp]),
     "scflow_enc_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_conv_wgrad_workspace": (c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_ll)]),
+    "scflow_conv_wgrad": (c_int, [ctypes.POINTER(WgradArgs), c_vp]),
     "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_vp]),
     "scflow_corr_lookup_backward": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int,

@@ -19,6 +19,19 @@ static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; 
 
 static inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// compute units of the current device (256 on MI355X; also the fallback without a device)
+static inline int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
 __device__ __forceinline__ float act_apply(float v, int act) {
   switch (act) {
     case SCFLOW_ACT_RELU: return v > 0.f ? v : 0.f;

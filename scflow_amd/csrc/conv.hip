@@ -669,18 +669,6 @@ int pick_bk(int kh, int kw, int tm, int hr, int hc, long long wgs, int cus) {
   return rounds(8) < rounds(16) ? 8 : 16;
 }
 
-int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-  }
-  return cus;
-}
-
 // tile rows / halo rows / tile size for a launch (shared by the launcher and scflow_conv_pick_bk)
 int launch_tile(const scflow_conv_args& a, const Geometry& g, int* tr, int* hr) {
   const long long m = (long long)a.n * g.oh * g.ow;

@@ -9,6 +9,19 @@
 //    the same weights grid_sample used (same fp32 coordinate arithmetic as lookup.hip, FP
 //    contraction off, so the taps and weights are bit-identical to the forward's).  fp32
 //    atomics: the order of additions is not deterministic (training only).
+//  * wgrad_kernel — the conv weight (and bias) gradient as an implicit GEMM on
+//    v_mfma_f32_32x32x2_f32 with the PIXELS as the reduction dimension:
+//        dW[co][ty][tx][ci] = Σ_p dY[p][co] · X[pix(p) + (ty, tx)][ci]
+//    A workgroup owns a 64 (co) × 64 (ci) tile for ALL kh·kw taps (4 waves, each 32 co × 32 ci
+//    × taps accumulators) and a contiguous run of pixel chunks (split-K over the grid's y).
+//    Per chunk (TR×TC output pixels) it stages dY[chunk][64 co] and the input HALO of the chunk
+//    ((TR−1)·s+kh rows × (TC−1)·s+kw cols × 64 ci) in LDS once; every tap then reads its
+//    shifted window out of the same halo — no im2col matrix in HBM.  k = 2 pixels per MFMA
+//    (lane half hh supplies pixel p0+hh): A = dY_lds[p][co] and B = halo[p+tap][ci] are both
+//    32 consecutive floats per half-wave (ds_read_b32, conflict-free).  Partial sums go to a
+//    per-split slab; wgrad_reduce_kernel sums the slabs in a fixed order (deterministic) and
+//    writes dW in the torch [cout][cin][kh][kw] layout, plus db = Σ_p dY when asked.  Two input
+//    sources = a channel concat without a copy (GRU cat[h, x]).
 #include "common.h"
 
 namespace {
@@ -111,7 +124,298 @@ __global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------ wgrad
+struct WgParams {
+  scflow_wgrad_args a;
+  int oh, ow, tr, tc, ltc, hr, hc, cp, nchunks, cps, co_tiles, copad, cinp;
+};
+
+constexpr int WT = 64;  // co and ci tile of a workgroup
+
+// float4 per thread needed to stage the largest halo a (KH, KW, S) launch can have
+constexpr int wg_nx(int kh, int kw, int s) {
+  const int cp = s == 1 ? 64 : 32;
+  int best = 0;
+  for (int tc = 2; tc <= 32; tc *= 2) {
+    const int tr = cp / tc;
+    const int hr = (tr - 1) * s + kh, hc = (tc - 1) * s + kw;
+    const int v = (hr * hc * (WT / 4) + 255) / 256;
+    if (v > best) best = v;
+  }
+  return best;
+}
+
+template <int KH, int KW, int S, bool VEC>
+__global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgParams P, float* __restrict__ slab,
+                                                        float* __restrict__ bslab) {
+  constexpr int TAPS = KH * KW;
+  constexpr int NX = VEC ? wg_nx(KH, KW, S) : 1;
+  constexpr int ND = VEC ? (S == 1 ? 64 : 32) * (WT / 4) / 256 : 1;
+  extern __shared__ float smem[];
+  const scflow_wgrad_args& a = P.a;
+  float* Ds = smem;                 // [cp][64]   dY chunk
+  float* Xs = smem + P.cp * WT;     // [hr*hc][64] input halo
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, hh = lane >> 5, wco = wave & 1, wci = wave >> 1;
+  const int co_t = blockIdx.x % P.co_tiles, ci_t = blockIdx.x / P.co_tiles;
+  const int co0 = co_t * WT, ci0 = ci_t * WT;
+  const int cin = a.cin0 + a.cin1;
+  const int c_begin = blockIdx.y * P.cps;
+  const int c_end = min(P.nchunks, c_begin + P.cps);
+  const int tiles_c = P.ow / P.tc, tiles_r = P.oh / P.tr;
+  const bool do_bias = bslab != nullptr && ci_t == 0;
+  const int nh = P.hr * P.hc;
+
+  floatx16 acc[TAPS];
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  float bsum = 0.f;
+
+  // global → register prefetch of one chunk (float4 path)
+  floatx4 rd[ND], rx[NX];
+  auto chunk_origin = [&](int ch, int* img, int* oy0, int* ox0) {
+    *img = ch / (tiles_r * tiles_c);
+    const int rem = ch - *img * tiles_r * tiles_c;
+    *oy0 = (rem / tiles_c) * P.tr;
+    *ox0 = (rem % tiles_c) * P.tc;
+  };
+  auto gload = [&](int ch) {
+    int img, oy0, ox0;
+    chunk_origin(ch, &img, &oy0, &ox0);
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int idx = tid + 256 * j;
+      const int p = idx >> 4, co = co0 + 4 * (idx & 15);
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < P.cp && co < a.cout) {
+        const size_t m = ((size_t)img * P.oh + oy0 + (p >> P.ltc)) * P.ow + ox0 + (p & (P.tc - 1));
+        v = *(const floatx4*)(a.dy + m * a.sdy + co);
+      }
+      rd[j] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int idx = tid + 256 * j;
+      const int hp = idx >> 4, c = ci0 + 4 * (idx & 15);
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (hp < nh && c < cin) {
+        const int hy = hp / P.hc, hx = hp - hy * P.hc;
+        const int iy = oy0 * S - a.ph + hy, ix = ox0 * S - a.pw + hx;
+        if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) {
+          const size_t pix = ((size_t)img * a.h + iy) * a.w + ix;
+          v = c < a.cin0 ? *(const floatx4*)(a.src0 + pix * a.s0 + c)
+                         : *(const floatx4*)(a.src1 + pix * a.s1 + (c - a.cin0));
+        }
+      }
+      rx[j] = v;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int idx = tid + 256 * j;
+      if (idx < P.cp * (WT / 4)) *(floatx4*)(Ds + (idx >> 4) * WT + 4 * (idx & 15)) = rd[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const int idx = tid + 256 * j;
+      if (idx < nh * (WT / 4)) *(floatx4*)(Xs + (idx >> 4) * WT + 4 * (idx & 15)) = rx[j];
+    }
+  };
+  auto stage_scalar = [&](int ch) {  // cin or cout not a multiple of 4: element-wise staging
+    int img, oy0, ox0;
+    chunk_origin(ch, &img, &oy0, &ox0);
+    for (int idx = tid; idx < P.cp * WT; idx += 256) {
+      const int p = idx >> 6, co = co0 + (idx & 63);
+      const size_t m = ((size_t)img * P.oh + oy0 + (p >> P.ltc)) * P.ow + ox0 + (p & (P.tc - 1));
+      Ds[idx] = co < a.cout ? a.dy[m * a.sdy + co] : 0.f;
+    }
+    for (int idx = tid; idx < nh * WT; idx += 256) {
+      const int hp = idx >> 6, c = ci0 + (idx & 63);
+      const int hy = hp / P.hc, hx = hp - hy * P.hc;
+      const int iy = oy0 * S - a.ph + hy, ix = ox0 * S - a.pw + hx;
+      float v = 0.f;
+      if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w && c < cin) {
+        const size_t pix = ((size_t)img * a.h + iy) * a.w + ix;
+        v = c < a.cin0 ? a.src0[pix * a.s0 + c] : a.src1[pix * a.s1 + (c - a.cin0)];
+      }
+      Xs[idx] = v;
+    }
+  };
+
+  const float* Da = Ds + wco * 32 + li;
+  const float* Xb = Xs + wci * 32 + li;
+  if (VEC && c_begin < c_end) gload(c_begin);
+  for (int ch = c_begin; ch < c_end; ++ch) {
+    __syncthreads();
+    if (VEC) lstore();
+    else stage_scalar(ch);
+    __syncthreads();
+    if (VEC && ch + 1 < c_end) gload(ch + 1);  // in flight under this chunk's MFMAs
+    if (do_bias && tid < WT)
+      for (int p = 0; p < P.cp; ++p) bsum += Ds[p * WT + tid];
+#pragma unroll 2
+    for (int p0 = 0; p0 < P.cp; p0 += 2) {
+      const int pix = p0 + hh;
+      const int r = pix >> P.ltc, c = pix & (P.tc - 1);
+      const float av = Da[pix * WT];
+      const float* xb = Xb + ((r * S) * P.hc + c * S) * WT;
+      float bv[TAPS];
+#pragma unroll
+      for (int ty = 0; ty < KH; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < KW; ++tx) bv[ty * KW + tx] = xb[(ty * P.hc + tx) * WT];
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
+    }
+  }
+  // partial slab [split][copad][TAPS][cinp]; C/D layout: col = lane&31, row = (r&3)+8(r>>2)+4hh
+  float* sl = slab + (size_t)blockIdx.y * P.copad * TAPS * P.cinp;
+  const int ci = ci0 + wci * 32 + li;
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      sl[((size_t)co * TAPS + t) * P.cinp + ci] = acc[t][r];
+    }
+  if (do_bias && tid < WT) bslab[(size_t)blockIdx.y * P.copad + co0 + tid] = bsum;
+}
+
+// Σ over the splits, fixed order.  Block = one (co, tap) row × 64 ci: 4 groups of 64 threads
+// each sum every 4th split (independent loads in flight), then an LDS reduction of the 4.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+    const float* __restrict__ slab, const float* __restrict__ bslab, float* __restrict__ dw,
+    float* __restrict__ db, int splits, int cout, int cin, int taps, int copad, int cinp,
+    int accumulate) {
+  __shared__ float part[4][64];
+  const int cblocks = cinp / 64;
+  const int row = blockIdx.x / cblocks;            // co * taps + t
+  const int ci = (blockIdx.x % cblocks) * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  const size_t sstride = (size_t)copad * taps * cinp;
+  const bool bias_row = db && row < cout && blockIdx.x % cblocks == 0;
+  if (row < cout * taps) {
+    const float* src = slab + (size_t)row * cinp + ci;
+    float s0 = 0.f, s1 = 0.f;
+    int k = grp;
+    for (; k + 4 < splits; k += 8) {
+      s0 += src[k * sstride];
+      s1 += src[(k + 4) * sstride];
+    }
+    if (k < splits) s0 += src[k * sstride];
+    part[grp][threadIdx.x & 63] = s0 + s1;
+  }
+  __syncthreads();
+  if (grp == 0 && row < cout * taps && ci < cin) {
+    const float s = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+    const int co = row / taps, t = row % taps;
+    float* d = dw + ((size_t)co * cin + ci) * taps + t;
+    *d = accumulate ? *d + s : s;
+  }
+  if (bias_row && threadIdx.x == 64) {  // bias of channel `row` (rows < cout exist as taps ≥ 1)
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += bslab[(size_t)k * copad + row];
+    db[row] = accumulate ? db[row] + s : s;
+  }
+}
+
+bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
+  if (a.stride != 1 && a.stride != 2) return false;
+  const bool shape_ok = (a.kh == 1 && a.kw == 1) || (a.kh == 3 && a.kw == 3) ||
+                        (a.stride == 1 && ((a.kh == 1 && a.kw == 5) || (a.kh == 5 && a.kw == 1)));
+  if (!shape_ok) return false;
+  P->a = a;
+  P->oh = (a.h + 2 * a.ph - a.kh) / a.stride + 1;
+  P->ow = (a.w + 2 * a.pw - a.kw) / a.stride + 1;
+  if (P->oh <= 0 || P->ow <= 0) return false;
+  const int tcmax = a.stride == 1 ? 32 : 16, cpmax = a.stride == 1 ? 64 : 32;
+  P->tc = P->ow < tcmax ? P->ow : tcmax;
+  if (P->tc & (P->tc - 1)) return false;  // power of two
+  P->ltc = 0;
+  while ((1 << P->ltc) < P->tc) ++P->ltc;
+  P->tr = cpmax / P->tc < P->oh ? cpmax / P->tc : P->oh;
+  if (P->ow % P->tc || P->oh % P->tr) return false;
+  P->cp = P->tr * P->tc;
+  if (P->cp & 1) return false;
+  P->hr = (P->tr - 1) * a.stride + a.kh;
+  P->hc = (P->tc - 1) * a.stride + a.kw;
+  P->nchunks = a.n * (P->oh / P->tr) * (P->ow / P->tc);
+  P->co_tiles = (a.cout + WT - 1) / WT;
+  const int cin = a.cin0 + a.cin1;
+  const int ci_tiles = (cin + WT - 1) / WT;
+  P->copad = P->co_tiles * WT;
+  P->cinp = ci_tiles * WT;
+  // split the pixel reduction until the grid has ~2 workgroups per CU (the 3×3 kernel's
+  // occupancy), each ≥ 8 chunks (the slab traffic is splits × the weight size)
+  const int tiles = P->co_tiles * ci_tiles;
+  int want = (2 * device_cus() + tiles - 1) / tiles;
+  int maxs = P->nchunks / 8 > 0 ? P->nchunks / 8 : 1;
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  P->cps = (P->nchunks + want - 1) / want;
+  *splits = (P->nchunks + P->cps - 1) / P->cps;
+  return true;
+}
+
 }  // namespace
+
+SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats) {
+  if (!args || !floats) return SCFLOW_EINVAL;
+  WgParams P;
+  int splits = 0;
+  if (!wgrad_geometry(*args, &P, &splits)) return SCFLOW_EUNSUPPORTED;
+  const int taps = args->kh * args->kw;
+  *floats = (long long)splits * P.copad * taps * P.cinp + (long long)splits * P.copad;
+  return SCFLOW_OK;
+}
+
+SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
+  if (!args) return SCFLOW_EINVAL;
+  const scflow_wgrad_args& a = *args;
+  if (!a.dy || !a.src0 || !a.dw || !a.workspace || a.n <= 0 || a.h <= 0 || a.w <= 0 ||
+      a.cout <= 0 || a.cin0 <= 0 || a.cin1 < 0 || (a.cin1 > 0 && !a.src1) || a.sdy < a.cout ||
+      a.s0 < a.cin0 || (a.cin1 > 0 && a.s1 < a.cin1) || a.ph < 0 || a.pw < 0)
+    return SCFLOW_EINVAL;
+  WgParams P;
+  int splits = 0;
+  if (!wgrad_geometry(a, &P, &splits)) return SCFLOW_EUNSUPPORTED;
+  const int taps = a.kh * a.kw;
+  const long long need = (long long)splits * P.copad * taps * P.cinp + (long long)splits * P.copad;
+  if (a.workspace_floats < need) return SCFLOW_EINVAL;
+  float* slab = a.workspace;
+  float* bslab = a.db ? a.workspace + (size_t)splits * P.copad * taps * P.cinp : nullptr;
+  const bool vec = a.cout % 4 == 0 && a.sdy % 4 == 0 && aligned16(a.dy) && a.cin0 % 4 == 0 &&
+                   a.s0 % 4 == 0 && aligned16(a.src0) &&
+                   (a.cin1 == 0 || (a.cin1 % 4 == 0 && a.s1 % 4 == 0 && aligned16(a.src1)));
+  const size_t lds = sizeof(float) * (size_t)(P.cp + P.hr * P.hc) * WT;
+  if (lds > 160 * 1024) return SCFLOW_EUNSUPPORTED;
+  const dim3 grid((unsigned)(P.co_tiles * (P.cinp / WT)), (unsigned)splits);
+  hipStream_t st = (hipStream_t)stream;
+#define SCFLOW_WG(KH_, KW_, S_)                                                                  \
+  if (a.kh == KH_ && a.kw == KW_ && a.stride == S_) {                                            \
+    if (vec)                                                                                     \
+      wgrad_kernel<KH_, KW_, S_, true><<<grid, 256, lds, st>>>(P, slab, bslab);                  \
+    else                                                                                         \
+      wgrad_kernel<KH_, KW_, S_, false><<<grid, 256, lds, st>>>(P, slab, bslab);                 \
+  } else
+  SCFLOW_WG(3, 3, 1)
+  SCFLOW_WG(1, 1, 1)
+  SCFLOW_WG(1, 5, 1)
+  SCFLOW_WG(5, 1, 1)
+  SCFLOW_WG(3, 3, 2)
+  SCFLOW_WG(1, 1, 2)
+  return SCFLOW_EUNSUPPORTED;
+#undef SCFLOW_WG
+  int rc = scflow_launch_status();
+  if (rc != SCFLOW_OK) return rc;
+  const unsigned rblocks = (unsigned)((long long)a.cout * taps * (P.cinp / WT));
+  wgrad_reduce_kernel<<<rblocks, 256, 0, st>>>(slab, bslab, a.dw, a.db, splits, a.cout,
+                                               a.cin0 + a.cin1, taps, P.copad, P.cinp, a.accumulate);
+  return scflow_launch_status();
+}
 
 SCFLOW_API int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin,
                              int kh, int kw, int stride, int ph, int pw, void* stream) {

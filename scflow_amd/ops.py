@@ -443,6 +443,39 @@ def enc_apply(x: Tensor, scale: Tensor, shift: Tensor, out: Tensor, n: int, hw: 
 
 
 # ------------------------------------------------------------------------------- §8(f)-2 training
+def conv_wgrad(dy: Tensor, src0, src1: Optional[Chan], dw: Tensor, db: Optional[Tensor], n: int,
+               h: int, w: int, kh: int, kw: int, stride: int, ph: int, pw: int,
+               accumulate: bool = False) -> None:
+    """dw [cout, cin0+cin1, kh, kw] (+)= conv weight gradient; db [cout] (+)= Σ dy (optional).
+    dy: [n·oh·ow, cout] contiguous; src0 / src1: channels-last tensors or ``Chan`` slices.
+    Raises ScflowError(SCFLOW_EUNSUPPORTED) for shapes outside the kernel's set."""
+    _require(dy, "dy")
+    _require(dw, "dw")
+    srcs = []
+    for nm, x in (("src0", src0), ("src1", src1)):
+        if x is None:
+            srcs.append((None, 0, 0))
+        elif isinstance(x, Chan):
+            _require(x.buf, nm)
+            srcs.append((x.ptr, x.c, x.stride))
+        else:
+            _require(x, nm)
+            srcs.append((x.data_ptr(), x.shape[-1], x.shape[-1]))
+    a = _lib.WgradArgs()
+    a.dy, a.sdy = dy.data_ptr(), dy.shape[-1]
+    (a.src0, a.cin0, a.s0), (a.src1, a.cin1, a.s1) = srcs
+    a.dw, a.db = dw.data_ptr(), _p(db)
+    a.n, a.h, a.w, a.cout, a.kh, a.kw = n, h, w, dy.shape[-1], kh, kw
+    a.stride, a.ph, a.pw, a.accumulate = stride, ph, pw, int(accumulate)
+    lib = _lib.load()
+    need = ctypes.c_longlong(0)
+    check(lib.scflow_conv_wgrad_workspace(ctypes.byref(a), ctypes.byref(need)),
+          "scflow_conv_wgrad_workspace")
+    ws = torch.empty(max(1, need.value), device=dy.device)
+    a.workspace, a.workspace_floats = ws.data_ptr(), need.value
+    check(lib.scflow_conv_wgrad(ctypes.byref(a), _stream(dy)), "scflow_conv_wgrad")
+
+
 def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, ph: int, pw: int,
            out: Optional[Tensor] = None) -> Tensor:
     """Patch matrix [n·oh·ow, kh·kw·cin] of a channels-last input (tensor or Chan)."""

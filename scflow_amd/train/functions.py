@@ -3,11 +3,14 @@
 Activations are channels-last [N, H, W, C] contiguous fp32 tensors on the ROCm device.
 
 * ``conv2d_nhwc`` — forward on the HIP conv variants (MFMA implicit GEMM for the decoder's
-  shapes, the encoder MFMA conv for strided / wide ones, the gather conv otherwise).  Backward:
-  dX = the same HIP conv of the output gradient with the flipped, in/out-transposed weights
-  (for stride s > 1 over the gradient zero-inserted to the input grid — a transposed conv as a
-  'same' convolution); dW = HIP im2col of the input + one plain GEMM dYᵀ·cols (hipBLASLt via
-  ``torch.matmul``: the "plain library GEMM" case); db = Σ dY.
+  shapes, the encoder MFMA conv for strided / wide ones, the gather conv otherwise), with the
+  activation and an optional pre-activation bias map fused into the epilogue, and an optional
+  second input source (channel concat without a copy).  Backward: the activation's derivative
+  from the saved output; dX = the same HIP conv of the output gradient with the flipped,
+  in/out-transposed weights (for stride s > 1 over the gradient zero-inserted to the input
+  grid — a transposed conv as a 'same' convolution); dW and db = ``scflow_conv_wgrad`` (MFMA
+  implicit GEMM over the pixels, no im2col matrix); 7×7 kernels fall back to HIP im2col + one
+  plain GEMM dYᵀ·cols (hipBLASLt via ``torch.matmul``).
 * ``corr_pyramid`` — forward ``scflow_corr_pyramid``; backward: average-pool adjoints (¼ to each
   of the 4 children) down to level 0, then dF1 = dC·F2ᵀ/√C, dF2 = dCᵀ·F1/√C as batched GEMMs
   (hipBLASLt).  (raft_decoder.py:35-58)
@@ -37,93 +40,154 @@ def _flip_t(w: Tensor) -> Tensor:
     return w.flip(2, 3).transpose(0, 1).contiguous()
 
 
-def _conv_forward(x: Tensor, w: Tensor, b: Optional[Tensor], stride: int, pad: Tuple[int, int]) -> Tensor:
-    """HIP conv of a channels-last input, choosing the variant that supports the shape."""
-    n, h, wd, cin = x.shape
+_ACT_FN = {None: lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Tanh": torch.tanh}
+
+
+def _act_backward(dy: Tensor, y: Tensor, act: Optional[str]) -> Tensor:
+    """Gradient through act given its OUTPUT y (ReLU: y > 0; sigmoid: y(1−y); tanh: 1−y²)."""
+    if act is None:
+        return dy
+    if act == "ReLU":
+        return torch.ops.aten.threshold_backward(dy, y, 0.0)
+    if act == "Sigmoid":
+        return torch.ops.aten.sigmoid_backward(dy, y)
+    if act == "Tanh":
+        return torch.ops.aten.tanh_backward(dy, y)
+    raise ValueError(act)
+
+
+def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tensor], stride: int,
+                  pad: Tuple[int, int], act: Optional[str] = None,
+                  bias_map: Optional[Tensor] = None) -> Tensor:
+    """act(conv(cat[x0, x1]) + b + bias_map) of channels-last inputs on the HIP conv variant
+    that supports the shape; act and bias_map are fused into the epilogue where the variant has
+    one, applied after it otherwise."""
+    n, h, wd, c0 = x0.shape
+    c1 = 0 if x1 is None else x1.shape[-1]
+    cin = c0 + c1
     cout, _, kh, kw = w.shape
     ph, pw = pad
     oh, ow = (h + 2 * ph - kh) // stride + 1, (wd + 2 * pw - kw) // stride + 1
-    out = torch.empty(n, oh, ow, cout, device=x.device)
+    out = torch.empty(n, oh, ow, cout, device=x0.device)
     same = stride == 1 and oh == h and ow == wd
     lib_ok = same and (
-        (cin <= 4) or (cout <= 4 and cin % 8 == 0) or
-        (cin % 4 == 0 and wd in (32, 64) and (kh, kw) in ((1, 1), (3, 3), (1, 5), (5, 1))
+        (cin <= 4 and x1 is None) or (cout <= 4 and cin % 8 == 0) or
+        (c0 % 4 == 0 and c1 % 4 == 0 and wd in (32, 64) and (kh, kw) in ((1, 1), (3, 3), (1, 5), (5, 1))
          and oh % (128 // wd if wd <= 128 else 1) == 0))
     if lib_ok:
-        bk = ops.conv_pick_bk(n, h, wd, cin, 0, cout, kh, kw, ph, pw, 1)
+        bk = ops.conv_pick_bk(n, h, wd, c0, c1, cout, kh, kw, ph, pw, 1)
         try:
-            packed = ops.pack_conv_weight(w.float(), cin, 0, wd, 1, bk)
-            ops.conv2d(Chan.whole(x.view(-1, cin)), packed, b, n, h, wd, cout, kh, kw, ph, pw, None,
-                       out=Chan.whole(out.view(-1, cout)), bk=bk)
+            packed = ops.pack_conv_weight(w.float(), c0, c1, wd, 1, bk)
+            ops.conv2d(Chan.whole(x0.view(-1, c0)), packed, b, n, h, wd, cout, kh, kw, ph, pw, act,
+                       out=Chan.whole(out.view(-1, cout)), bk=bk,
+                       src1=None if x1 is None else Chan.whole(x1.view(-1, c1)),
+                       bias_map=None if bias_map is None else Chan.whole(bias_map.reshape(-1, cout)))
             return out
         except ScflowError:
             pass
-    if cin % 16 == 0 and kh == kw and kh in (1, 3) and ph == pw == kh // 2 and stride in (1, 2):
+    post = True  # act / bias_map still to apply
+    if (c0 % 16 == 0 and c1 % 16 == 0 and kh == kw and kh in (1, 3) and ph == pw == kh // 2
+            and stride in (1, 2)):
         try:
-            ops.enc_conv(x, ops.enc_conv_pack(w), b, n, h, wd, cin, cout, kh, stride, ph, out)
-            return out
+            fuse = bias_map is None
+            ops.enc_conv(Chan.whole(x0.view(-1, c0)), ops.enc_conv_pack(w), b, n, h, wd, c0, cout, kh,
+                         stride, ph, out, act=act if fuse else None,
+                         src1=None if x1 is None else Chan.whole(x1.view(-1, c1)))
+            post = not fuse
+            x0 = None
         except ScflowError:
             pass
-    if ph != pw or kh != kw:
-        raise ScflowError(f"no HIP conv for kernel {kh}x{kw} pad {pad} stride {stride}")
-    if cin == 3 and kh == 7 and stride in (1, 2) and cout <= 256 and cout != 192:
-        # the encoder stem kernel (NCHW image in, channels-last out)
-        ops.enc_stem(x.permute(0, 3, 1, 2).contiguous(), ops.enc_stem_pack(w), b, cout, 7, stride,
-                     ph, out)
-        return out
-    if cin % 4:  # the gather conv reads float4 channel groups: zero-pad the channels
-        pad4 = 4 - cin % 4
-        x = F.pad(x, (0, pad4))
-        w = F.pad(w, (0, 0, 0, 0, 0, pad4))
-        cin += pad4
-    ops.ph_conv(Chan.whole(x.reshape(-1, cin)), None, ops.ph_conv_pack(w.contiguous()), b, n, h, wd,
-                cout, kh, stride, ph, out.view(-1, cout))
+    if x0 is not None:
+        x = x0 if x1 is None else torch.cat([x0, x1], -1)
+        if ph != pw or kh != kw:
+            raise ScflowError(f"no HIP conv for kernel {kh}x{kw} pad {pad} stride {stride}")
+        if cin == 3 and kh == 7 and stride in (1, 2) and cout <= 256 and cout != 192:
+            # the encoder stem kernel (NCHW image in, channels-last out)
+            ops.enc_stem(x.permute(0, 3, 1, 2).contiguous(), ops.enc_stem_pack(w), b, cout, 7, stride,
+                         ph, out)
+        else:
+            if cin % 4:  # the gather conv reads float4 channel groups: zero-pad the channels
+                pad4 = 4 - cin % 4
+                x = F.pad(x, (0, pad4))
+                w = F.pad(w, (0, 0, 0, 0, 0, pad4))
+                cin += pad4
+            ops.ph_conv(Chan.whole(x.reshape(-1, cin)), None, ops.ph_conv_pack(w.contiguous()), b, n, h,
+                        wd, cout, kh, stride, ph, out.view(-1, cout))
+    if post:
+        if bias_map is not None:
+            out += bias_map
+        out = _ACT_FN[act](out)
     return out
+
+
+def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int, ph: int, pw: int,
+                 with_bias: bool) -> Tuple[Tensor, Optional[Tensor]]:
+    n, h, wd, c0 = x0.shape
+    cout, cin, kh, kw = w.shape
+    dw = torch.empty(cout, cin, kh, kw, device=g.device)
+    db = torch.empty(cout, device=g.device) if with_bias else None
+    g2 = g.view(-1, cout)
+    try:
+        ops.conv_wgrad(g2, x0, x1, dw, db, n, h, wd, kh, kw, s, ph, pw)
+        return dw, db
+    except ScflowError:
+        pass
+    # shapes outside the wgrad kernel (7×7): HIP im2col + one plain GEMM (hipBLASLt)
+    x = x0 if x1 is None else torch.cat([x0, x1], -1)
+    cols = ops.im2col(x.contiguous(), n, h, wd, cin, kh, kw, s, ph, pw)
+    dwm = torch.matmul(g2.t(), cols)  # [cout, kh·kw·cin]
+    dw = dwm.view(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
+    return dw, (g2.sum(0) if with_bias else None)
 
 
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, ph, pw):
-        ctx.save_for_backward(x, w)
-        ctx.stride, ctx.pad, ctx.has_b = stride, (ph, pw), b is not None
-        return _conv_forward(x.contiguous(), w.detach().contiguous(),
-                             None if b is None else b.detach().contiguous(), stride, (ph, pw))
+    def forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act):
+        x0 = x0.contiguous()
+        x1 = None if x1 is None else x1.contiguous()
+        y = _conv_forward(x0, x1, w.detach().contiguous(), None if b is None else b.detach().contiguous(),
+                          stride, (ph, pw), act, None if bias_map is None else bias_map.detach().contiguous())
+        ctx.save_for_backward(x0, x1, w, y if act is not None else None)
+        ctx.stride, ctx.pad, ctx.has_b, ctx.act = stride, (ph, pw), b is not None, act
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x0, x1, w, y = ctx.saved_tensors
         s, (ph, pw) = ctx.stride, ctx.pad
-        dy = dy.contiguous()
-        n, h, wd, cin = x.shape
-        cout, _, kh, kw = w.shape
-        _, oh, ow, _ = dy.shape
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        g = _act_backward(dy.contiguous(), y, ctx.act).contiguous()
+        n, h, wd, c0 = x0.shape
+        cout, cin, kh, kw = w.shape
+        _, oh, ow, _ = g.shape
+        dx0 = dx1 = dw = db = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             if s == 1:
-                z = dy
+                z = g
             else:  # zero-insert onto the input grid: a transposed conv as a 'same' conv
-                z = torch.zeros(n, h, wd, cout, device=dy.device)
-                z[:, 0:(oh - 1) * s + 1:s, 0:(ow - 1) * s + 1:s] = dy
+                z = torch.zeros(n, h, wd, cout, device=g.device)
+                z[:, 0:(oh - 1) * s + 1:s, 0:(ow - 1) * s + 1:s] = g
             qh, qw = kh - 1 - ph, kw - 1 - pw  # dgrad padding
             if s > 1:
                 qh, qw = (kh - 1) // 2, (kw - 1) // 2
                 if (kh - 1 - ph) != qh or (kw - 1 - pw) != qw:
                     raise ScflowError("strided dgrad needs pad == (k-1)/2")
-            dx = _conv_forward(z, _flip_t(w.detach()), None, 1, (qh, qw))
-        if ctx.needs_input_grad[1]:
-            cols = ops.im2col(x.contiguous(), n, h, wd, cin, kh, kw, s, ph, pw)
-            dwm = torch.matmul(dy.view(-1, cout).t(), cols)  # [cout, kh·kw·cin] (hipBLASLt)
-            dw = dwm.view(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy.view(-1, cout).sum(0)
-        return dx, dw, db, None, None, None
+            dx = _conv_forward(z, None, _flip_t(w.detach()), None, 1, (qh, qw))
+            dx0 = dx if x1 is None else dx[..., :c0]
+            dx1 = None if x1 is None else dx[..., c0:]
+        if ctx.needs_input_grad[2] or (ctx.has_b and ctx.needs_input_grad[3]):
+            dw, db = _weight_grad(g, x0, x1, w, s, ph, pw, ctx.has_b and ctx.needs_input_grad[3])
+        dbm = g if ctx.needs_input_grad[4] else None
+        return dx0, dx1, dw, db, dbm, None, None, None, None
 
 
 def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride: int = 1,
-                padding=0) -> Tensor:
-    """nn.Conv2d (cross-correlation) on channels-last tensors, HIP forward and backward."""
+                padding=0, act: Optional[str] = None, x1: Optional[Tensor] = None,
+                bias_map: Optional[Tensor] = None) -> Tensor:
+    """act(nn.Conv2d(cat[x, x1]) + bias_map) (cross-correlation) on channels-last tensors, HIP
+    forward and backward.  ``x1``: optional second input (a channel concat without the copy);
+    ``bias_map``: an [N, OH, OW, cout] tensor added before the activation."""
     ph, pw = (padding, padding) if isinstance(padding, int) else padding
-    return _Conv2dNHWC.apply(x, weight, bias, stride, ph, pw)
+    return _Conv2dNHWC.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act)
 
 
 # ------------------------------------------------------------------------------- correlation

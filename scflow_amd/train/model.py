@@ -36,10 +36,11 @@ def _act(x: Tensor, act) -> Tensor:
     return x
 
 
-def _cm(x: Tensor, m) -> Tensor:
-    """mmcv ConvModule (conv → act; the decoder's ConvModules have no norm)."""
+def _cm(x: Tensor, m, x1: Tensor = None) -> Tensor:
+    """mmcv ConvModule (conv → act, fused; the decoder's ConvModules have no norm); ``x1``: a
+    second input concatenated along channels (read in place)."""
     c = m.conv
-    return _act(conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding), m.act_type)
+    return conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding, act=m.act_type, x1=x1)
 
 
 def _conv(x: Tensor, c) -> Tensor:
@@ -136,9 +137,19 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
     label = label.long()
     outs = ([], [], [], [], [], [], [])
     enc = dec.encoder
-    zr_w = [torch.cat([z.conv.weight, rr.conv.weight], 0) for z, rr in zip(dec.gru.conv_z, dec.gru.conv_r)]
-    zr_b = [torch.cat([z.conv.bias, rr.conv.bias], 0) for z, rr in zip(dec.gru.conv_z, dec.gru.conv_r)]
-    hc = dec.h_channels
+    gru = dec.gru
+    hc, cc = dec.h_channels, dec.cxt_channels
+    # loop-invariant context contribution of every GRU conv, once per forward (its gradient is
+    # the sum over the iterations, so dgrad/wgrad of the context part also run once)
+    it_w, ctx_pre = [], []
+    for zc, rc, qc in zip(gru.conv_z, gru.conv_r, gru.conv_q):
+        z, rr, q = zc.conv, rc.conv, qc.conv
+        wzr = torch.cat([z.weight, rr.weight], 0)
+        bzr = torch.cat([z.bias, rr.bias], 0)
+        ctx_pre.append((conv2d_nhwc(cxt, wzr[:, hc:hc + cc], bzr, 1, q.padding),
+                        conv2d_nhwc(cxt, q.weight[:, hc:hc + cc], q.bias, 1, q.padding)))
+        it_w.append((torch.cat([wzr[:, :hc], wzr[:, hc + cc:]], 1),
+                     torch.cat([q.weight[:, :hc], q.weight[:, hc + cc:]], 1), q.padding))
     for _ in range(iters):
         with torch.no_grad():  # flow is detached every iteration (detach_flow=True)
             f2 = torch.empty(N * hh * ww, 2, device=depth.device, dtype=dt)
@@ -151,18 +162,15 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
         f = f2
         for m in enc.flow_net:
             f = _cm(f, m)
-        out = torch.cat([c, f], -1)
-        for m in enc.out_net:
+        out = _cm(c, enc.out_net[0], x1=f)
+        for m in enc.out_net[1:]:
             out = _cm(out, m)
         motion = torch.cat([out, f2], -1)
-        x = torch.cat([cxt, motion], -1)
-        for s, q in enumerate(dec.gru.conv_q):  # SeqConv: 1×5 then 5×1
-            hx = torch.cat([h, x], -1)
-            zr = torch.sigmoid(conv2d_nhwc(hx, zr_w[s], zr_b[s], 1, q.conv.padding))
+        for (w_zr, w_q, pad), (pre_zr, pre_q) in zip(it_w, ctx_pre):  # SeqConv: 1×5 then 5×1
+            zr = conv2d_nhwc(h, w_zr, None, 1, pad, act="Sigmoid", x1=motion, bias_map=pre_zr)
             z, rg = zr[..., :hc], zr[..., hc:]
-            qq = torch.tanh(conv2d_nhwc(torch.cat([rg * h, x], -1), q.conv.weight, q.conv.bias, 1,
-                                        q.conv.padding))
-            h = (1 - z) * h + z * qq
+            qq = conv2d_nhwc(rg * h, w_q, None, 1, pad, act="Tanh", x1=motion, bias_map=pre_q)
+            h = torch.lerp(h, qq, z)  # (1 − z)·h + z·q
         fh = h
         for m in dec.flow_pred.layers:
             fh = _cm(fh, m)
@@ -170,7 +178,8 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
         mh = h
         for m in dec.mask_pred.layers:
             mh = _cm(mh, m)
-        mask = torch.sigmoid(_conv(mh, dec.mask_pred.predict_layer))
+        pl = dec.mask_pred.predict_layer
+        mask = conv2d_nhwc(mh, pl.weight, pl.bias, 1, pl.padding, act="Sigmoid")
         dff = dflow
         for m in dec.delta_flow_encoder:
             dff = _cm(dff, m)

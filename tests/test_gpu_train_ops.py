@@ -30,6 +30,10 @@ def _close(a, b, rtol, atol, what):
     (2, 64, 64, 64, 96, 1, 2, 0),               # encoder downsample 1×1/2
     (2, 64, 64, 3, 64, 7, 2, 3),                # encoder stem 7×7/2
     (2, 16, 16, 128, 128, 3, 1, 1),             # 16-wide (pose head / 128² encoder)
+    (2, 32, 32, 1, 64, 3, 1, 1),                # mask encoder (cin 1: scalar wgrad staging)
+    (2, 32, 32, 256, 128, (5, 1), 1, (2, 0)),   # GRU 5×1
+    (2, 8, 8, 128, 128, 3, 2, 1),               # pose head conv3 (4×4 output)
+    (3, 128, 128, 64, 64, 3, 1, 1),             # encoder layer1 (wide rows)
 ])
 def test_conv2d_nhwc_forward_backward(case):
     from scflow_amd.train.functions import conv2d_nhwc
@@ -58,6 +62,61 @@ def test_conv2d_nhwc_forward_backward(case):
     _close(xg.grad.permute(0, 3, 1, 2), xr.grad, 1e-5, 1e-5 * np.sqrt(cout * kk[0] * kk[1]), f"{case} dx")
     _close(wg.grad, wr.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), f"{case} dw")
     _close(bg.grad, br.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), f"{case} db")
+
+
+@pytest.mark.parametrize("act,two,bmap", [("Sigmoid", True, True), ("Tanh", True, True),
+                                          ("ReLU", True, False), ("ReLU", False, False)])
+def test_conv2d_nhwc_fused_act_two_sources_bias_map(act, two, bmap):
+    """act(conv(cat[x0, x1]) + bias_map): the GRU's fused form (1×5, h ⊕ motion, hoisted context
+    map) and the motion encoder's cat[c, f] — values and all five gradients vs fp64 autograd."""
+    from scflow_amd.train.functions import conv2d_nhwc
+    g = torch.Generator().manual_seed(11)
+    n, h, w, c0, c1, cout = 2, 32, 32, 128, 128 if two else 0, 256
+    x0 = torch.randn(n, h, w, c0, generator=g)
+    x1 = torch.randn(n, h, w, c1, generator=g) if two else None
+    wt = torch.randn(cout, c0 + c1, 1, 5, generator=g) / np.sqrt((c0 + c1) * 5)
+    b = torch.randn(cout, generator=g) * 0.1 if not bmap else None
+    bm = torch.randn(n, h, w, cout, generator=g) * 0.5 if bmap else None
+    fn = {"Sigmoid": torch.sigmoid, "Tanh": torch.tanh, "ReLU": torch.relu}[act]
+    leaves = [t.double().requires_grad_() if t is not None else None for t in (x0, x1, wt, b, bm)]
+    xr = leaves[0] if not two else torch.cat([leaves[0], leaves[1]], -1)
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), leaves[2], leaves[3], padding=(0, 2)).permute(0, 2, 3, 1)
+    if bmap:
+        yr = yr + leaves[4]
+    yr = fn(yr)
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    (yr * gy).sum().backward()
+    dev = [t.cuda().requires_grad_() if t is not None else None for t in (x0, x1, wt, b, bm)]
+    y = conv2d_nhwc(dev[0], dev[2], dev[3], 1, (0, 2), act=act, x1=dev[1], bias_map=dev[4])
+    (y * gy.float().cuda()).sum().backward()
+    torch.cuda.synchronize()
+    _close(y, yr, 1e-5, 1e-5 * np.sqrt(5 * (c0 + c1)), "y")
+    for name, a, r in zip(("x0", "x1", "w", "b", "bias_map"), dev, leaves):
+        if a is not None:
+            _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), name)
+
+
+def test_conv_wgrad_accumulate_and_split():
+    """scflow_conv_wgrad directly: a Chan slice as the second source, accumulate = 1 adds onto
+    dw / db, and a batch large enough to split the pixel reduction over many workgroups."""
+    from scflow_amd import ops
+    from scflow_amd.ops import Chan
+    g = torch.Generator().manual_seed(12)
+    n, h, w, c0, c1, cout = 8, 64, 64, 64, 32, 96
+    x0 = torch.randn(n, h, w, c0, generator=g)
+    buf = torch.randn(n, h, w, 48, generator=g)  # second source = channels 8..40 of a wider buffer
+    x1 = buf[..., 8:8 + c1]
+    dy = torch.randn(n, h, w, cout, generator=g)
+    ref = torch.nn.grad.conv2d_weight(torch.cat([x0, x1], -1).permute(0, 3, 1, 2).double(),
+                                      (cout, c0 + c1, 3, 3), dy.permute(0, 3, 1, 2).double(), padding=1)
+    dw = torch.ones(cout, c0 + c1, 3, 3).cuda()
+    db = torch.ones(cout).cuda()
+    bufc = buf.cuda()
+    ops.conv_wgrad(dy.cuda().view(-1, cout), x0.cuda(), Chan(bufc.view(-1, 48), 8, c1), dw, db, n, h, w,
+                   3, 3, 1, 1, 1, accumulate=True)
+    torch.cuda.synchronize()
+    _close(dw - 1, ref, 1e-5, 1e-4 * np.sqrt(n * h * w), "dw")
+    _close(db - 1, dy.double().sum((0, 1, 2)), 1e-5, 1e-4 * np.sqrt(n * h * w), "db")
 
 
 def test_corr_pyramid_backward():

@@ -21,8 +21,13 @@ def _patch_torch_ops(monkeypatch):
     from scflow_amd import ops
     from scflow_amd.train import model
 
-    def conv(x, w, b=None, stride=1, padding=0):
-        return F.conv2d(x.permute(0, 3, 1, 2), w, b, stride, padding).permute(0, 2, 3, 1)
+    def conv(x, w, b=None, stride=1, padding=0, act=None, x1=None, bias_map=None):
+        if x1 is not None:
+            x = torch.cat([x, x1], -1)
+        y = F.conv2d(x.permute(0, 3, 1, 2), w, b, stride, padding).permute(0, 2, 3, 1)
+        if bias_map is not None:
+            y = y + bias_map
+        return {None: y, "ReLU": torch.relu(y), "Sigmoid": torch.sigmoid(y), "Tanh": torch.tanh(y)}[act]
 
     def pyramid(f1, f2, L=4):
         return orc.corr_pyramid(f1, f2, L)
