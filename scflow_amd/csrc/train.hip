@@ -145,7 +145,7 @@ constexpr int wg_nx(int kh, int kw, int s) {
   return best;
 }
 
-template <int KH, int KW, int S, bool VEC>
+template <int KH, int KW, int S, bool VEC, bool DB>
 __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgParams P, float* __restrict__ slab,
                                                         float* __restrict__ bslab) {
   constexpr int TAPS = KH * KW;
@@ -153,8 +153,8 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
   constexpr int ND = VEC ? (S == 1 ? 64 : 32) * (WT / 4) / 256 : 1;
   extern __shared__ float smem[];
   const scflow_wgrad_args& a = P.a;
-  float* Ds = smem;                 // [cp][64]   dY chunk
-  float* Xs = smem + P.cp * WT;     // [hr*hc][64] input halo
+  float* Ds = smem;                 // [cp][64] dY chunk, then [hr*hc][64] input halo; ×2 (float4)
+  float* Xs = smem + P.cp * WT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, hh = lane >> 5, wco = wave & 1, wci = wave >> 1;
   const int co_t = blockIdx.x % P.co_tiles, ci_t = blockIdx.x / P.co_tiles;
@@ -212,16 +212,18 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
       rx[j] = v;
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int buf = 0) {
+    float* D = Ds + buf * (P.cp + nh) * WT;
+    float* X = D + P.cp * WT;
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const int idx = tid + 256 * j;
-      if (idx < P.cp * (WT / 4)) *(floatx4*)(Ds + (idx >> 4) * WT + 4 * (idx & 15)) = rd[j];
+      if (idx < P.cp * (WT / 4)) *(floatx4*)(D + (idx >> 4) * WT + 4 * (idx & 15)) = rd[j];
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
       const int idx = tid + 256 * j;
-      if (idx < nh * (WT / 4)) *(floatx4*)(Xs + (idx >> 4) * WT + 4 * (idx & 15)) = rx[j];
+      if (idx < nh * (WT / 4)) *(floatx4*)(X + (idx >> 4) * WT + 4 * (idx & 15)) = rx[j];
     }
   };
   auto stage_scalar = [&](int ch) {  // cin or cout not a multiple of 4: element-wise staging
@@ -245,30 +247,70 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
     }
   };
 
-  const float* Da = Ds + wco * 32 + li;
-  const float* Xb = Xs + wci * 32 + li;
-  if (VEC && c_begin < c_end) gload(c_begin);
+  // float4 path, DB: LDS double buffer — chunk ch+1 is written into the other buffer from the
+  // prefetch registers after this chunk's MFMAs have been issued; one barrier per chunk.
+  // float4 path, !DB: one buffer; the next chunk's global loads are in flight (registers)
+  // during this chunk's MFMAs.  Scalar path: one buffer, staged in place.
+  const int bufsz = (P.cp + nh) * WT;
+  if (VEC && c_begin < c_end) {
+    gload(c_begin);
+    if (DB) {
+      lstore();
+      __syncthreads();
+      if (c_begin + 1 < c_end) gload(c_begin + 1);
+    }
+  }
   for (int ch = c_begin; ch < c_end; ++ch) {
-    __syncthreads();
-    if (VEC) lstore();
-    else stage_scalar(ch);
-    __syncthreads();
-    if (VEC && ch + 1 < c_end) gload(ch + 1);  // in flight under this chunk's MFMAs
-    if (do_bias && tid < WT)
-      for (int p = 0; p < P.cp; ++p) bsum += Ds[p * WT + tid];
-#pragma unroll 2
-    for (int p0 = 0; p0 < P.cp; p0 += 2) {
+    const int cur = (VEC && DB) ? ((ch - c_begin) & 1) : 0;
+    float* Dc = Ds + cur * bufsz;
+    float* Xc = Dc + P.cp * WT;
+    if (!VEC) {
+      __syncthreads();
+      stage_scalar(ch);
+      __syncthreads();
+    } else if (!DB) {
+      __syncthreads();
+      lstore();
+      __syncthreads();
+      if (ch + 1 < c_end) gload(ch + 1);
+    }
+    if (do_bias)  // every thread: one channel (tid & 63), every 4th pixel
+      for (int p = tid >> 6; p < P.cp; p += 4) bsum += Dc[p * WT + (tid & 63)];
+    const float* Da = Dc + wco * 32 + li;
+    const float* Xb = Xc + wci * 32 + li;
+    // software pipeline: the operands of k-step p0+2 are read from LDS before the MFMAs of
+    // k-step p0 issue, so the LDS latency hides under TAPS matrix ops even at 1 wave / SIMD
+    float av, bv[TAPS];
+    auto ldk = [&](int p0, float& a_, float* b_) {
       const int pix = p0 + hh;
       const int r = pix >> P.ltc, c = pix & (P.tc - 1);
-      const float av = Da[pix * WT];
-      const float* xb = Xb + ((r * S) * P.hc + c * S) * WT;
-      float bv[TAPS];
+      a_ = Da[pix * WT];
+      const float* xb = Xb + (r * S * P.hc + c * S) * WT;
 #pragma unroll
       for (int ty = 0; ty < KH; ++ty)
 #pragma unroll
-        for (int tx = 0; tx < KW; ++tx) bv[ty * KW + tx] = xb[(ty * P.hc + tx) * WT];
+        for (int tx = 0; tx < KW; ++tx) b_[ty * KW + tx] = xb[(ty * P.hc + tx) * WT];
+    };
+    // two register sets, two k-steps per trip (cp % 4 == 0): set 1's reads are issued before
+    // set 0's MFMAs and vice versa, with no copies between the sets
+    float a1, b1[TAPS];
+    ldk(0, av, bv);
+    for (int p0 = 0; p0 < P.cp; p0 += 4) {
+      ldk(p0 + 2, a1, b1);
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, TAPS + 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TAPS, 0);
+      ldk(p0 + 4 < P.cp ? p0 + 4 : p0, av, bv);
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1[t], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, TAPS + 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TAPS, 0);
+    }
+    if (VEC && DB && ch + 1 < c_end) {
+      lstore(cur ^ 1);
+      __syncthreads();
+      if (ch + 2 < c_end) gload(ch + 2);
     }
   }
   // partial slab [split][copad][TAPS][cinp]; C/D layout: col = lane&31, row = (r&3)+8(r>>2)+4hh
@@ -281,7 +323,14 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
       const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
       sl[((size_t)co * TAPS + t) * P.cinp + ci] = acc[t][r];
     }
-  if (do_bias && tid < WT) bslab[(size_t)blockIdx.y * P.copad + co0 + tid] = bsum;
+  if (do_bias) {
+    __syncthreads();
+    Ds[tid] = bsum;
+    __syncthreads();
+    if (tid < WT)
+      bslab[(size_t)blockIdx.y * P.copad + co0 + tid] =
+          (Ds[tid] + Ds[tid + 64]) + (Ds[tid + 128] + Ds[tid + 192]);
+  }
 }
 
 // Σ over the splits, fixed order.  Block = one (co, tap) row × 64 ci: 4 groups of 64 threads
@@ -299,13 +348,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   const bool bias_row = db && row < cout && blockIdx.x % cblocks == 0;
   if (row < cout * taps) {
     const float* src = slab + (size_t)row * cinp + ci;
-    float s0 = 0.f, s1 = 0.f;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     int k = grp;
-    for (; k + 4 < splits; k += 8) {
+    for (; k + 12 < splits; k += 16) {  // 4 independent loads in flight per thread
       s0 += src[k * sstride];
       s1 += src[(k + 4) * sstride];
+      s2 += src[(k + 8) * sstride];
+      s3 += src[(k + 12) * sstride];
     }
-    if (k < splits) s0 += src[k * sstride];
+    for (; k < splits; k += 4) s0 += src[k * sstride];
+    s0 = (s0 + s1) + (s2 + s3);
+    s1 = 0.f;
     part[grp][threadIdx.x & 63] = s0 + s1;
   }
   __syncthreads();
@@ -339,7 +392,7 @@ bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   P->tr = cpmax / P->tc < P->oh ? cpmax / P->tc : P->oh;
   if (P->ow % P->tc || P->oh % P->tr) return false;
   P->cp = P->tr * P->tc;
-  if (P->cp & 1) return false;
+  if (P->cp & 3) return false;  // two k-steps (4 pixels) per trip of the MFMA loop
   P->hr = (P->tr - 1) * a.stride + a.kh;
   P->hc = (P->tc - 1) * a.stride + a.kw;
   P->nchunks = a.n * (P->oh / P->tr) * (P->ow / P->tc);
@@ -348,10 +401,11 @@ bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   const int ci_tiles = (cin + WT - 1) / WT;
   P->copad = P->co_tiles * WT;
   P->cinp = ci_tiles * WT;
-  // split the pixel reduction until the grid has ~2 workgroups per CU (the 3×3 kernel's
-  // occupancy), each ≥ 8 chunks (the slab traffic is splits × the weight size)
+  // split the pixel reduction until the grid fills the CUs once at the kernel's occupancy,
+  // each split ≥ 8 chunks (the slab traffic is splits × the weight size)
   const int tiles = P->co_tiles * ci_tiles;
-  int want = (2 * device_cus() + tiles - 1) / tiles;
+  const int occ = a.kh * a.kw >= 9 ? 1 : 2;  // the kernel's resident workgroups per CU
+  int want = (occ * device_cus() + tiles - 1) / tiles;
   int maxs = P->nchunks / 8 > 0 ? P->nchunks / 8 : 1;
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
@@ -390,16 +444,21 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
   const bool vec = a.cout % 4 == 0 && a.sdy % 4 == 0 && aligned16(a.dy) && a.cin0 % 4 == 0 &&
                    a.s0 % 4 == 0 && aligned16(a.src0) &&
                    (a.cin1 == 0 || (a.cin1 % 4 == 0 && a.s1 % 4 == 0 && aligned16(a.src1)));
-  const size_t lds = sizeof(float) * (size_t)(P.cp + P.hr * P.hc) * WT;
+  const size_t lds1 = sizeof(float) * (size_t)(P.cp + P.hr * P.hc) * WT;
+  const int occ = taps >= 9 ? 1 : 2;
+  const bool db2 = vec && 2 * lds1 * occ <= 160 * 1024;  // double-buffer if it keeps occupancy
+  const size_t lds = lds1 * (db2 ? 2 : 1);
   if (lds > 160 * 1024) return SCFLOW_EUNSUPPORTED;
   const dim3 grid((unsigned)(P.co_tiles * (P.cinp / WT)), (unsigned)splits);
   hipStream_t st = (hipStream_t)stream;
 #define SCFLOW_WG(KH_, KW_, S_)                                                                  \
   if (a.kh == KH_ && a.kw == KW_ && a.stride == S_) {                                            \
-    if (vec)                                                                                     \
-      wgrad_kernel<KH_, KW_, S_, true><<<grid, 256, lds, st>>>(P, slab, bslab);                  \
+    if (db2)                                                                                     \
+      wgrad_kernel<KH_, KW_, S_, true, true><<<grid, 256, lds, st>>>(P, slab, bslab);            \
+    else if (vec)                                                                                \
+      wgrad_kernel<KH_, KW_, S_, true, false><<<grid, 256, lds, st>>>(P, slab, bslab);           \
     else                                                                                         \
-      wgrad_kernel<KH_, KW_, S_, false><<<grid, 256, lds, st>>>(P, slab, bslab);                 \
+      wgrad_kernel<KH_, KW_, S_, false, false><<<grid, 256, lds, st>>>(P, slab, bslab);          \
   } else
   SCFLOW_WG(3, 3, 1)
   SCFLOW_WG(1, 1, 1)
