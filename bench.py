@@ -287,7 +287,12 @@ def main():
                "steps": args.e2e_steps, "warmup": 2}
         del ref, rin
 
-    train = bench_train(args, world, rank, dev, feat) if args.train_batch > 0 else None
+    train = None
+    if args.train_batch > 0:
+        try:
+            train = bench_train(args, world, rank, dev, feat)
+        except Exception as e:  # the extra leg must not take the headline line down with it
+            train = {"error": f"{type(e).__name__}: {e}"[:400]}
 
     units = world * args.batch * args.iters * args.steps
     value = units / elapsed

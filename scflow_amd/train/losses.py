@@ -38,12 +38,11 @@ def _pm_terms(pts: Tensor, pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: T
     gt_rot = torch.bmm(pts, gt_r.transpose(1, 2))
     gt_rt = gt_rot + gt_t[:, None]
     pred_rot = torch.bmm(pts, pred_r.transpose(1, 2)) + gt_t[:, None]
-    if bool(sym.any()):
+    if sym is not None:  # symmetric samples: nearest predicted point per GT point (no host sync)
         with torch.no_grad():
-            idx = torch.cdist(gt_rt[sym], pred_rot[sym]).argmin(-1)  # [Bs, P]
-        matched = torch.gather(pred_rot[sym], 1, idx[..., None].expand(-1, -1, 3))
-        pred_rot = pred_rot.clone()
-        pred_rot[sym] = matched
+            idx = torch.cdist(gt_rt, pred_rot).argmin(-1)  # [B, P]
+        matched = torch.gather(pred_rot, 1, idx[..., None].expand(-1, -1, 3))
+        pred_rot = torch.where(sym[:, None, None], matched, pred_rot)
     l_rot = (pred_rot - gt_rt).abs().sum(-1).mean(-1)
     tz = torch.cat([gt_t[:, :2], pred_t[:, 2:]], 1)
     txy = torch.cat([pred_t[:, :2], gt_t[:, 2:]], 1)
@@ -54,21 +53,24 @@ def _pm_terms(pts: Tensor, pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: T
 
 def point_matching_loss(pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tensor, labels: Tensor,
                         points: Sequence[Tensor], diameters: Tensor,
-                        weight: float = POSE_WEIGHT) -> Tensor:
+                        weight: float = POSE_WEIGHT, any_symmetric: bool = True) -> Tensor:
     """DisentanglePointMatchingLoss (point_matching_loss.py:159-218) with loss_type l1,
-    disentangle_z, no xy/depth scaling, reduction mean."""
+    disentangle_z, no xy/depth scaling, reduction mean.  ``any_symmetric=False`` (the caller
+    knows no label is a symmetric class) skips the nearest-neighbour matching."""
     B = pred_r.shape[0]
     labels = labels.long()
-    sym = torch.zeros(B, dtype=torch.bool, device=labels.device)
-    for c in SYMMETRIC_CLASSES:
-        sym |= labels == c
+    sym = None
+    if any_symmetric:
+        for c in SYMMETRIC_CLASSES:
+            sym = (labels == c) if sym is None else (sym | (labels == c))
     diam = diameters[labels]
     if len({int(p.shape[0]) for p in points}) == 1:
         pts = torch.stack(list(points))[labels]
         per = _pm_terms(pts, pred_r, pred_t, gt_r, gt_t, sym)
     else:
         per = torch.cat([_pm_terms(points[int(labels[i])][None], pred_r[i:i + 1], pred_t[i:i + 1],
-                                   gt_r[i:i + 1], gt_t[i:i + 1], sym[i:i + 1]) for i in range(B)])
+                                   gt_r[i:i + 1], gt_t[i:i + 1], None if sym is None else sym[i:i + 1])
+                         for i in range(B)])
     return weight * (per / diam).sum() / B
 
 
@@ -97,9 +99,10 @@ def refine_losses(outs, gt_r: Tensor, gt_t: Tensor, gt_flow: Tensor, render_mask
                   ) -> Tuple[Tensor, Tensor, Tensor]:
     """(loss_pose, loss_flow, loss_mask) from the decoder's 7 lists (scflow_refiner.py:200-242)."""
     _, flow_pred, Rs, ts, masks, _, _ = outs
-    diam = torch.as_tensor(diameters, dtype=gt_r.dtype, device=gt_r.device)
+    diam = diameters if isinstance(diameters, Tensor) else torch.as_tensor(
+        diameters, dtype=gt_r.dtype, device=gt_r.device)
     lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam)
-                        for R, t in zip(Rs, ts)])
+                        for R, t in zip(Rs, ts)])  # (symmetric matching always evaluated: no sync)
     lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow) for f in flow_pred])
     occ = (gt_flow.sum(1) < max_flow).to(gt_flow)
     lm = sequence_loss([mask_l1_loss(m[:, 0], occ) for m in masks])

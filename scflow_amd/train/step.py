@@ -4,11 +4,13 @@ lr 4e-4, betas (0.9, 0.999), eps 1e-8, weight decay 1e-4, clip_grad max_norm 10,
 
 Data parallel = one process per GPU (torch.distributed over RCCL).  Gradients live in a few
 flat fp32 buckets (every ``param.grad`` is a view into one), so the exchange is one all-reduce
-per bucket; each bucket's all-reduce is issued asynchronously from a post-accumulate-grad hook
-as soon as its last gradient is written, overlapping the exchange with the rest of the backward
-pass.  Buckets are filled in reverse registration order (≈ the order backward produces
-gradients), sized for xGMI (default 8 MB, 4 buckets for the 32.7 MB model: large enough that the ring is link-bound, small
-enough that the first buckets start early).  No per-parameter collectives, no DDP wrapper.
+per bucket, sized for xGMI (default 8 MB, 4 buckets for the 32.7 MB model: large enough that
+the ring is link-bound).  By default the buckets are reduced right after the backward pass,
+all issued before the first wait (the 32.7 MB exchange is ≈0.3 ms against a ≈100 ms step, so
+overlapping it buys < 0.5 %); ``overlap=True`` instead issues each bucket's all-reduce from a
+post-accumulate-grad hook as soon as its last gradient is written (buckets filled in reverse
+registration order ≈ the order backward produces gradients).  No per-parameter collectives,
+no DDP wrapper.
 """
 from __future__ import annotations
 
@@ -23,10 +25,11 @@ Tensor = torch.Tensor
 
 
 class GradBuckets:
-    """Flat gradient buckets with overlapped all-reduce (average over the process group)."""
+    """Flat gradient buckets all-reduced (averaged) over the process group, after the backward
+    pass or (``overlap``) from post-accumulate-grad hooks during it."""
 
-    def __init__(self, params: Sequence[torch.nn.Parameter], bucket_bytes: int = 32 << 20,
-                 group=None) -> None:
+    def __init__(self, params: Sequence[torch.nn.Parameter], bucket_bytes: int = 8 << 20,
+                 group=None, overlap: bool = False) -> None:
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -55,7 +58,7 @@ class GradBuckets:
         self._pending = [0] * len(self.members)
         self._work: List[Optional[object]] = [None] * len(self.members)
         self._hooks = []
-        if self.world > 1:
+        if self.world > 1 and overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
@@ -103,14 +106,14 @@ class TrainStep:
     def __init__(self, refiner, model_points: Sequence[Tensor], diameters: Sequence[float],
                  lr: float = 4e-4, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_norm: float = 10.0, bucket_bytes: int = 8 << 20, iters: Optional[int] = None,
-                 group=None) -> None:
+                 group=None, overlap: bool = False) -> None:
         self.refiner = refiner
         self.model_points = list(model_points)
         self.diameters = list(diameters)
         self.max_norm = max_norm
         self.iters = iters
         params = list(dict.fromkeys(refiner.parameters()))  # the shared encoder appears twice
-        self.grads = GradBuckets(params, bucket_bytes, group)
+        self.grads = GradBuckets(params, bucket_bytes, group, overlap)
         self.opt = torch.optim.AdamW(self.grads.params, lr=lr, betas=betas, eps=eps,
                                      weight_decay=weight_decay, foreach=True)
         if dist.is_initialized() and dist.get_world_size(group) > 1:

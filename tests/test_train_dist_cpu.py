@@ -5,6 +5,8 @@ gradients and, after a few optimizer steps, the same weights as one process on t
 import os
 import socket
 
+import pytest
+
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -28,7 +30,7 @@ def _data():
     return torch.randn(8, 3, 8, 8, generator=g), torch.randn(8, 10, generator=g)
 
 
-def _run(rank, world, steps, max_norm):
+def _run(rank, world, steps, max_norm, overlap=True):
     from scflow_amd.train.step import GradBuckets
     m = _model().double()
     x, y = _data()
@@ -36,7 +38,7 @@ def _run(rank, world, steps, max_norm):
     if world > 1:
         n = x.shape[0] // world
         x, y = x[rank * n:(rank + 1) * n], y[rank * n:(rank + 1) * n]
-    gb = GradBuckets(list(m.parameters()), bucket_bytes=8 << 10)  # several buckets
+    gb = GradBuckets(list(m.parameters()), bucket_bytes=8 << 10, overlap=overlap)  # several buckets
     opt = torch.optim.AdamW(gb.params, lr=1e-2, weight_decay=1e-4, foreach=True)
     hooked = []
     for _ in range(steps):
@@ -51,25 +53,26 @@ def _run(rank, world, steps, max_norm):
     return [p.detach().clone() for p in m.parameters()], first_grads, hooked, len(gb.buckets)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.set_num_threads(1)
-        w, g, hooked, nb = _run(rank, world, 3, 0.5)
+        w, g, hooked, nb = _run(rank, world, 3, 0.5, overlap)
         q.put((rank, ([a.numpy() for a in w], [a.numpy() for a in g], hooked, nb)))  # by value
     finally:
         dist.destroy_process_group()
 
 
-def test_bucketed_allreduce_matches_single_process():
+@pytest.mark.parametrize("overlap", [True, False])
+def test_bucketed_allreduce_matches_single_process(overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = dict(q.get(timeout=120) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -77,7 +80,8 @@ def test_bucketed_allreduce_matches_single_process():
     assert nb >= 3
     for rank in (0, 1):
         w, g, hooked, _ = res[rank]
-        assert hooked == [nb] * 3  # every bucket's all-reduce was issued during backward
+        # overlap: every bucket's all-reduce was issued during backward; else all after it
+        assert hooked == ([nb] * 3 if overlap else [0] * 3)
         for a, b in zip(g, ref_g):
             torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-12, atol=1e-14)
         for a, b in zip(w, ref_w):
