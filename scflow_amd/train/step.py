@@ -101,13 +101,25 @@ class GradBuckets:
 
 
 class TrainStep:
-    """forward (HIP) → losses → backward (HIP) → bucketed all-reduce → clip → AdamW."""
+    """forward (HIP) → losses → backward (HIP) → bucketed all-reduce → clip → AdamW.
+
+    ``graph=True`` (experimental, off by default): the forward + backward (≈3000 kernel
+    launches) are captured once into a hipGraph on the third call and replayed on every later
+    call with the batch copied into the captured input buffers; the all-reduce, clipping and the
+    optimizer step stay eager.  The weights are re-packed inside the graph, so optimizer updates
+    are seen by every replay.  One capture on ROCm 7 segfaulted inside the runtime's graph
+    instantiation, so nothing enables it by default."""
 
     def __init__(self, refiner, model_points: Sequence[Tensor], diameters: Sequence[float],
                  lr: float = 4e-4, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_norm: float = 10.0, bucket_bytes: int = 8 << 20, iters: Optional[int] = None,
-                 group=None, overlap: bool = False) -> None:
+                 group=None, overlap: bool = False, graph: bool = False) -> None:
         self.refiner = refiner
+        self.graph = graph
+        self._g = None
+        self._static = None
+        self._out = None
+        self._calls = 0
         self.model_points = list(model_points)
         self.diameters = list(diameters)
         self.max_norm = max_norm
@@ -116,6 +128,8 @@ class TrainStep:
         self.grads = GradBuckets(params, bucket_bytes, group, overlap)
         self.opt = torch.optim.AdamW(self.grads.params, lr=lr, betas=betas, eps=eps,
                                      weight_decay=weight_decay, foreach=True)
+        dev = self.grads.params[0].device
+        self.diam_t = torch.as_tensor(self.diameters, dtype=torch.float32, device=dev)
         if dist.is_initialized() and dist.get_world_size(group) > 1:
             self.broadcast_parameters()
 
@@ -124,11 +138,42 @@ class TrainStep:
         for t in list(self.refiner.parameters()) + list(self.refiner.buffers()):
             dist.broadcast(t.data, src, group=self.grads.group)
 
+    def _fwd_bwd(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        self.grads.zero()
+        out = refiner_train_forward(self.refiner, batch, self.model_points, self.diam_t, self.iters)
+        out["loss"].backward()
+        return out
+
+    def _capture(self, batch: Dict[str, Tensor]) -> None:
+        self._static = {k: v.clone() for k, v in batch.items()}
+        bufs = [b.clone() for b in self.refiner.buffers()]  # the warm-up must not move BN stats
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # allocator warm-up on a side stream (capture recipe)
+            self._fwd_bwd(self._static)
+        torch.cuda.current_stream().wait_stream(side)
+        for b, c in zip(self.refiner.buffers(), bufs):
+            b.copy_(c)
+        self._g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g):
+            self._out = self._fwd_bwd(self._static)
+
     def __call__(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         self.refiner.train()
-        self.grads.zero()
-        out = refiner_train_forward(self.refiner, batch, self.model_points, self.diameters, self.iters)
-        out["loss"].backward()
+        self._calls += 1
+        if self.graph and self._calls > 2:
+            if self._g is None:
+                self._capture(batch)
+            else:
+                for k, v in batch.items():
+                    self._static[k].copy_(v)
+            self._g.replay()
+            # scalars are copied out (the graph overwrites its outputs on the next replay);
+            # the per-iteration lists stay views of the graph's buffers
+            out = {k: (v.detach().clone() if isinstance(v, Tensor) and v.dim() == 0 else v)
+                   for k, v in self._out.items()}
+        else:
+            out = self._fwd_bwd(batch)
         self.grads.finish()
         out["grad_norm"] = self.grads.clip_(self.max_norm)
         self.opt.step()

@@ -19,7 +19,8 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--graph", action="store_true")
     a = ap.parse_args()
     import bench
     from scflow_amd import synthetic
@@ -29,7 +30,7 @@ def main():
     raw = synthetic.make_train_batch(a.batch, a.size, seed=2000)
     batch = {k: torch.from_numpy(v).to(dev) for k, v in raw.items()}
     pts = [torch.from_numpy(p).to(dev) for p in synthetic.make_model_points(1024)]
-    step = TrainStep(ref, pts, synthetic.YCBV_DIAMETERS)
+    step = TrainStep(ref, pts, synthetic.YCBV_DIAMETERS, graph=a.graph)
     for _ in range(a.warmup):
         step(batch)
     torch.cuda.synchronize()
