@@ -278,6 +278,51 @@ int scflow_corr_lookup_backward(const float* dout, int out_layout, int out_strid
                                 int flow_layout, float* dpyr, int n, int h, int w, int num_levels,
                                 int radius, void* stream);
 
+/* §8(f)-3 mesh renderer (replaces pytorch3d's MeshRasterizer + HardPhongShader behind
+ * models/utils/rendering.py:196-248, configured as scflow_ycbv_real.py:261-274).
+ * A batch of n_img images of size×size; image i shows one mesh whose vertices / faces are the
+ * i-th block of the packed arrays (pytorch3d's join_meshes_as_batch packing: faces hold packed
+ * vertex indices; vert_img / face_img give each packed vertex / face its image).  Outputs
+ * (each optional except that images needs normals, colors and the light/material colours):
+ *   images [n][size][size][4] RGBA (background colour, alpha 0 where empty),
+ *   zbuf [n][size][size] (view depth, −1 empty), pix_to_face (packed face, −1 empty),
+ *   bary [n][size][size][3] (perspective-corrected barycentrics, −1 empty).
+ * Light placement (Renderer.forward :209-230): SCFLOW_LIGHT_FIXED = light_location (object
+ * frame; pytorch3d's default (0, 1, 0)); SCFLOW_LIGHT_PER_IMAGE = R_i·(0, 0, max(z_i − 400, 0)),
+ * z_i the image's nearest vertex depth (seperate_lights); SCFLOW_LIGHT_BATCH_ZNEAR =
+ * R_i·(0, 0, znear/4), znear = ⌊min depth over the batch / 100⌋·100.  Vertex depths must be
+ * positive (objects in front of the camera).  workspace: ≥ scflow_render_workspace() bytes. */
+#define SCFLOW_LIGHT_FIXED 0
+#define SCFLOW_LIGHT_PER_IMAGE 1
+#define SCFLOW_LIGHT_BATCH_ZNEAR 2
+typedef struct {
+  const float* verts;    /* [total_verts][3] object frame */
+  const float* normals;  /* [total_verts][3] (pytorch3d verts_normals) */
+  const float* colors;   /* [total_verts][3] vertex colours in [0, 1] */
+  const int* faces;      /* [total_faces][3] packed vertex indices */
+  const int* vert_img;   /* [total_verts] image of each packed vertex */
+  const int* face_img;   /* [total_faces] image of each packed face */
+  const float* R;        /* [n_img][3][3] OpenCV rotation (object → camera) */
+  const float* t;        /* [n_img][3] */
+  const float* K;        /* [n_img][3][3] intrinsics */
+  int n_img, size, total_verts, total_faces;
+  int light_mode;
+  const float* light_location;                  /* [3], SCFLOW_LIGHT_FIXED only */
+  const float* ambient;                         /* [3] light·material ambient */
+  const float* diffuse;                         /* [3] */
+  const float* specular;                        /* [3] */
+  float shininess;
+  const float* background;                      /* [3] */
+  float* images;
+  float* zbuf;
+  int* pix_to_face;
+  float* bary;
+  void* workspace;
+  long long workspace_bytes;
+} scflow_render_args;
+long long scflow_render_workspace(int n_img, int size, int total_verts);
+int scflow_render(const scflow_render_args* args, void* stream);
+
 /* Profiling helper (bench.py roofline timing; no reference equivalent): a one-thread kernel
  * that stores the GPU's constant-rate wall clock (s_memrealtime) into stamps[idx].  Enqueued on
  * the stream of the kernel being timed, before and after it; as an ordinary kernel it is also a

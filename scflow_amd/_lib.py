@@ -71,6 +71,24 @@ class WgradArgs(ctypes.Structure):
     ]
 
 
+class RenderArgs(ctypes.Structure):
+    """Mirror of ``scflow_render_args`` (include/scflow_hip.h)."""
+    _fields_ = [
+        ("verts", c_vp), ("normals", c_vp), ("colors", c_vp), ("faces", c_vp),
+        ("vert_img", c_vp), ("face_img", c_vp),
+        ("R", c_vp), ("t", c_vp), ("K", c_vp),
+        ("n_img", c_int), ("size", c_int), ("total_verts", c_int), ("total_faces", c_int),
+        ("light_mode", c_int),
+        ("light_location", c_vp), ("ambient", c_vp), ("diffuse", c_vp), ("specular", c_vp),
+        ("shininess", c_float),
+        ("background", c_vp),
+        ("images", c_vp), ("zbuf", c_vp), ("pix_to_face", c_vp), ("bary", c_vp),
+        ("workspace", c_vp), ("workspace_bytes", c_ll),
+    ]
+
+
+SCFLOW_LIGHT_FIXED, SCFLOW_LIGHT_PER_IMAGE, SCFLOW_LIGHT_BATCH_ZNEAR = 0, 1, 2
+
 # name -> (restype, argtypes); every function the header declares
 SIGNATURES = {
     "scflow_version": (c_int, []),
@@ -117,6 +135,8 @@ SIGNATURES = {
     "scflow_enc_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "scflow_enc_norm_finalize": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp]),
     "scflow_enc_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_render_workspace": (c_ll, [c_int, c_int, c_int]),
+    "scflow_render": (c_int, [ctypes.POINTER(RenderArgs), c_vp]),
     "scflow_conv_wgrad_workspace": (c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_ll)]),
     "scflow_conv_wgrad": (c_int, [ctypes.POINTER(WgradArgs), c_vp]),
     "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -232,3 +232,33 @@ def make_train_batch(batch: int, size: int, seed: int = 0, labels=None) -> Dict[
     out = {**make_images(batch, size, seed=seed), **scene, **make_train_targets(scene, size, seed=seed)}
     out["label"] = out.pop("labels")
     return out
+
+
+def ellipsoid_mesh(semi_axes, n_lat: int = 24, n_lon: int = 48) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """UV-sphere triangle mesh of the stand-in object (the models_1024 meshes the renderer reads,
+    scflow_ycbv_real.py:262, are absent): verts [V,3] float32 (mm), faces [F,3] int64
+    (outward-consistent winding), vertex colours [V,3] in [0, 1] (a smooth pattern)."""
+    a = np.asarray(semi_axes, np.float64)
+    verts = [[0.0, 0.0, a[2]]]
+    for i in range(1, n_lat):
+        th = math.pi * i / n_lat
+        for j in range(n_lon):
+            ph = 2 * math.pi * j / n_lon
+            verts.append([a[0] * math.sin(th) * math.cos(ph), a[1] * math.sin(th) * math.sin(ph),
+                          a[2] * math.cos(th)])
+    verts.append([0.0, 0.0, -a[2]])
+    verts = np.asarray(verts)
+    faces = []
+    ring = lambda i, j: 1 + (i - 1) * n_lon + (j % n_lon)  # noqa: E731
+    for j in range(n_lon):
+        faces.append([0, ring(1, j), ring(1, j + 1)])
+    for i in range(1, n_lat - 1):
+        for j in range(n_lon):
+            faces.append([ring(i, j), ring(i + 1, j), ring(i + 1, j + 1)])
+            faces.append([ring(i, j), ring(i + 1, j + 1), ring(i, j + 1)])
+    last = len(verts) - 1
+    for j in range(n_lon):
+        faces.append([last, ring(n_lat - 1, j + 1), ring(n_lat - 1, j)])
+    u = verts / a
+    colors = 0.5 + 0.4 * np.stack([u[:, 0], u[:, 1] * u[:, 2], np.cos(3 * u[:, 0])], 1)
+    return verts.astype(np.float32), np.asarray(faces, np.int64), colors.astype(np.float32)

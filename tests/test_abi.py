@@ -56,7 +56,9 @@ def test_host_side_queries_need_no_gpu():
 
 
 @pytest.mark.parametrize("pyname,cname", [("ConvArgs", "scflow_conv_args"),
-                                           ("EncConvArgs", "scflow_enc_conv_args")])
+                                           ("EncConvArgs", "scflow_enc_conv_args"),
+                                           ("WgradArgs", "scflow_wgrad_args"),
+                                           ("RenderArgs", "scflow_render_args")])
 def test_struct_layout_matches_header(tmp_path, pyname, cname):
     """ctypes argument structs have the C compiler's size and field offsets."""
     import shutil
