@@ -4,9 +4,12 @@ Reference: ``models/refiner/scflow_refiner.py`` — ``__init__`` :17-63 (the fea
 shared by the real and rendered images unless ``seperate_encoder``, base_refiner.py:33-40;
 the context encoder is separate), ``extract_feat`` :84-106, ``get_pose`` :108-138.
 
-Only the refinement path is here (SURVEY.md §8 scope): the renderer, data pre-processing,
-losses and the training loop of the reference refiner are out of scope, so the loss / renderer
-configuration arguments are accepted and ignored.
+Also here: the renderer-driven inference loop of ``BaseRefiner`` (base_refiner.py: the render
+step of ``format_data_test`` :106-117, ``update_data`` :239-252, ``forward_multiple_pass``
+:301-312, test cycles from ``test_cfg['cycles']``) as ``render`` / ``refine`` when a
+``renderer`` config is given (the HIP renderer, scflow_amd/renderer.py).  Data loading /
+pre-processing stay the reference's; the loss configuration arguments are accepted and the
+losses live in ``scflow_amd.train``.
 
 ``get_pose`` runs the work MI355X-first rather than call by call:
 
@@ -65,6 +68,57 @@ class SCFlowRefiner(nn.Module):
         self.train_cfg = train_cfg or {}
         self.test_cfg = test_cfg or {}
         self.test_iter_num = self.test_cfg.get("iters", self.decoder.iters)
+        self.test_cycle_num = self.test_cfg.get("cycles", 1)
+        self.renderer = None
+        if renderer is not None:
+            from .renderer import Renderer
+            self.renderer = renderer if isinstance(renderer, Renderer) else Renderer(**renderer)
+
+    def to(self, *args, **kwargs):  # base_refiner.py:69-72: the renderer's meshes move too
+        if self.renderer is not None:
+            dev = args[0] if args else kwargs.get("device")
+            if dev is not None and not isinstance(dev, torch.dtype):
+                self.renderer.to(dev)
+        return super().to(*args, **kwargs)
+
+    def cuda(self, device=None):
+        if self.renderer is not None:
+            self.renderer.to("cuda" if device is None else torch.device("cuda", device))
+        return super().cuda(device)
+
+    # ------------------------------------------------------------------ renderer-driven loop
+    def render(self, rotations: Tensor, translations: Tensor, internel_k: Tensor, labels: Tensor,
+               norm_mean=(0.0, 0.0, 0.0), norm_std=(255.0, 255.0, 255.0)):
+        """format_data_test's render step (base_refiner.py:106-117): rendered images (RGB,
+        normalised with img_norm_cfg /255 — mean 0 / std 255 in the config, i.e. identity),
+        rendered depth (zbuf), rendered masks (depth > 0)."""
+        if self.renderer is None:
+            raise RuntimeError("SCFlowRefiner was built without a renderer config")
+        out = self.renderer(rotations, translations, internel_k, labels)
+        img = out["images"][..., :3].permute(0, 3, 1, 2).contiguous()
+        mean = torch.tensor(norm_mean, device=img.device).view(1, 3, 1, 1) / 255.0
+        std = torch.tensor(norm_std, device=img.device).view(1, 3, 1, 1) / 255.0
+        img = (img - mean) / std
+        depth = out["fragments"].zbuf[..., 0]
+        return img, depth, (depth > 0).float()
+
+    def refine(self, real_images: Tensor, ref_rotations: Tensor, ref_translations: Tensor,
+               internel_k: Tensor, labels: Tensor, cycles: Optional[int] = None):
+        """Test-time refinement (base_refiner.py:301-312 + scflow_refiner.py:142-177): for each
+        cycle render the current pose, run ``get_pose`` with ``test_cfg['iters']`` iterations and
+        take the last pose; returns (rotations, translations, last get_pose outputs)."""
+        cycles = self.test_cycle_num if cycles is None else cycles
+        R, t = ref_rotations, ref_translations
+        iters = self.decoder.iters
+        self.decoder.iters = self.test_iter_num
+        try:
+            for _ in range(cycles):
+                img, depth, _ = self.render(R, t, internel_k, labels)
+                out = self.get_pose(img, real_images, R, t, depth, internel_k, labels)
+                R, t = out[2][-1], out[3][-1]
+        finally:
+            self.decoder.iters = iters
+        return R, t, out
 
     # ------------------------------------------------------------------ reference API
     def extract_feat(self, render_images: Tensor, real_images: Tensor

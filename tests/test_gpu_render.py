@@ -84,3 +84,47 @@ def test_render_depth_matches_closed_form_256():
         both = cov & hit
         rel = np.abs(z[i][both] - zr[both]) / zr[both]
         assert np.median(rel) < 1e-4 and rel.max() < 2e-3
+
+
+def test_refiner_render_and_refine_cycles():
+    """SCFlowRefiner with a renderer config: ``render`` = the Renderer's image / zbuf / mask
+    (format_data_test's render step), and ``refine`` (render → get_pose per cycle) with one
+    cycle equals get_pose on the rendered inputs; two cycles re-render at the refined pose."""
+    from scflow_amd import MODELS, synthetic
+    from tests.test_gpu_decoder import decoder_cfg
+    from tests.test_gpu_encoder import encoder_state_dict  # noqa: F401  (same weights as the e2e tests)
+    from tests.helpers import refiner_state_dict
+    S, B = 256, 2
+    sc = synthetic.make_scene(B, S, seed=21)
+    meshes = {}
+    for lab in set(sc["labels"].tolist()):
+        semi = np.array(synthetic.ELLIPSOID_AXES) * synthetic.YCBV_DIAMETERS[lab]
+        meshes[lab] = synthetic.ellipsoid_mesh(semi, 24, 48)
+    enc = dict(type="RAFTEncoder", in_channels=3, out_channels=256, net_type="Basic", norm_cfg=dict(type="IN"))
+    ctx = dict(type="RAFTEncoder", in_channels=3, out_channels=256, net_type="Basic", norm_cfg=dict(type="BN"))
+    r = MODELS.build(dict(type="SCFlowRefiner", cxt_channels=128, h_channels=128, seperate_encoder=False,
+                          encoder=enc, cxt_encoder=ctx, decoder=dict(type="SCFlowDecoder", **decoder_cfg(2)),
+                          renderer=dict(mesh_dir=None, image_size=(S, S), soft_blending=False,
+                                        render_mask=False, seperate_lights=True, meshes=meshes),
+                          test_cfg=dict(iters=2, cycles=2)))
+    r.load_state_dict({("decoder." + k if not k.startswith(("real_encoder.", "render_encoder.", "context."))
+                        else k): v for k, v in refiner_state_dict().items()}, strict=False)
+    r = r.eval().cuda()
+    R, t, K, lab = (torch.from_numpy(sc[k]).cuda() for k in ("ref_rotation", "ref_translation",
+                                                             "internel_k", "labels"))
+    tgt = synthetic.make_train_targets(sc, S, seed=21)
+    real, _, _ = r.render(torch.from_numpy(tgt["gt_rotation"]).cuda(),
+                          torch.from_numpy(tgt["gt_translation"]).cuda(), K, lab)
+    img, depth, mask = r.render(R, t, K, lab)
+    direct = r.renderer(R, t, K, lab)
+    torch.testing.assert_close(img, direct["images"][..., :3].permute(0, 3, 1, 2))
+    torch.testing.assert_close(depth, direct["fragments"].zbuf[..., 0])
+    assert ((depth > 0) == (mask > 0)).all() and mask.sum() > 1000
+    R1, t1, out1 = r.refine(real, R, t, K, lab, cycles=1)
+    ref_out = r.get_pose(img, real, R, t, depth, K, lab)
+    torch.testing.assert_close(R1, ref_out[2][-1])
+    torch.testing.assert_close(t1, ref_out[3][-1])
+    R2, t2, _ = r.refine(real, R, t, K, lab)  # test_cfg cycles = 2
+    torch.cuda.synchronize()
+    assert torch.isfinite(R2).all() and torch.isfinite(t2).all()
+    assert not torch.equal(R2, R1)
