@@ -278,13 +278,31 @@ def main():
             g2 = GraphedForward(ref, rin, warmup=2, fn=ref.get_pose)
             el2 = time_steps(g2.replay, args.e2e_steps, 0, world, dev)
             del g2
+        render = None
+        try:  # the reference's render step in front of get_pose (format_data_test :106-117)
+            from scflow_amd.renderer import Renderer
+            meshes = {}
+            for lab in range(21):
+                semi = [a * synthetic.YCBV_DIAMETERS[lab] for a in synthetic.ELLIPSOID_AXES]
+                meshes[lab] = synthetic.ellipsoid_mesh(semi, 24, 48)  # 2208 faces
+            rr = Renderer(image_size=(args.size, args.size), soft_blending=False, render_mask=False,
+                          seperate_lights=True, meshes=meshes).to(dev)
+            rargs = (rin["ref_rotation"], rin["ref_translation"], rin["internel_k"], rin["label"])
+            el3 = time_steps(lambda: rr(*rargs), args.e2e_steps, 2, world, dev)
+            render = {"workload": f"HIP renderer (z-buffer + hard Phong, 2208-face meshes), "
+                                  f"{args.e2e_batch} images/GPU at {args.size}x{args.size}",
+                      "ms_per_batch": round(el3 / args.e2e_steps * 1e3, 3),
+                      "images_per_s": round(world * args.e2e_batch * args.e2e_steps / el3, 1)}
+            del rr
+        except Exception as e:  # extra measurement: never take the headline down
+            render = {"error": f"{type(e).__name__}: {e}"[:300]}
         e2e = {"workload": f"SCFlowRefiner.get_pose: images -> shared IN feature encoder (2 images/pair) "
                            f"+ BN context encoder + decoder, {args.e2e_batch} pairs/GPU, "
                            f"{args.size}x{args.size}, {args.iters} iters (BASELINE configs[2], "
                            f"jittered synthetic poses in place of PoseCNN init)",
                "value": round(world * args.e2e_batch * args.iters * args.e2e_steps / el2, 2),
                "unit": "iters/s", "ms_per_step": round(el2 / args.e2e_steps * 1e3, 3),
-               "steps": args.e2e_steps, "warmup": 2}
+               "steps": args.e2e_steps, "warmup": 2, "render": render}
         del ref, rin
 
     train = None
