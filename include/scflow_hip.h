@@ -91,18 +91,29 @@ typedef struct scflow_conv_args {
                                          /* variant): pre-activation += bias_map[pix·sbm + o]; */
                                          /* the decoder passes the loop-invariant context      */
                                          /* contribution of the GRU convs here                 */
-  int bk;                                /* K-stage depth the weights were packed for: 0 or 16 */
-                                         /* (default) or 8 — see scflow_conv_pick_bk           */
+  int bk;                                /* packing format of the weights: K-stage depth 0 or 16 */
+                                         /* (default) or 8, or SCFLOW_CONV_WINO — see           */
+                                         /* scflow_conv_pick_bk                                 */
 } scflow_conv_args;
 
-/* Number of floats of the packed weight buffer (the same for bk 8 and 16); w_oihw is
+/* scflow_conv_args.bk = SCFLOW_CONV_WINO selects the Winograd F(2×2,3×3) kernel (3×3, stride 1,
+ * pad 1, width 32 or 64, height a multiple of 4, SCFLOW_EPI_PLAIN): exact fp32 arithmetic, 2.25×
+ * fewer matrix multiplies than the direct conv; the weights must be packed with the same bk. */
+#define SCFLOW_CONV_WINO 2
+
+/* Number of floats of the packed weight buffer for bk 8 and 16 (the same for both); w_oihw is
  * nn.Conv2d's [cout][c0+c1][kh][kw]. */
 long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, int kw, int stride, int w);
-/* bk: K-stage depth to pack for (0 → 16, or 8); pass the same value in scflow_conv_args.bk. */
+/* The same for any packing format bk (0, 8, 16 or SCFLOW_CONV_WINO). */
+long long scflow_conv_packed_size_bk(int cout, int c0, int c1, int kh, int kw, int stride, int w,
+                                     int bk);
+/* bk: packing format (0 → 16, 8, or SCFLOW_CONV_WINO); pass the same value in
+ * scflow_conv_args.bk. */
 int scflow_conv_pack_weights(const float* w_oihw, float* packed, int cout, int c0, int c1, int kh,
                              int kw, int stride, int w, int bk, void* stream);
-/* Preferred K-stage depth (8 or 16) for this launch shape (batch, sizes, channels, kernel):
- * 8 when the grid needs more resident workgroups than 16-deep stages' LDS allows. */
+/* Preferred packing format for this launch shape (batch, sizes, channels, kernel): Winograd
+ * (SCFLOW_CONV_WINO) for the 3×3 stride-1 convs it covers, else the direct conv's K-stage depth,
+ * 8 when the grid needs more resident workgroups than 16-deep stages' LDS allows, else 16. */
 int scflow_conv_pick_bk(const scflow_conv_args* args);
 int scflow_conv2d(const scflow_conv_args* args, void* stream);
 

@@ -19,6 +19,7 @@ c_int, c_float, c_ll, c_vp = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ct
 
 SCFLOW_ACT = {None: 0, "ReLU": 1, "Sigmoid": 2, "Tanh": 3}
 EPI_PLAIN, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2
+CONV_WINO = 2  # scflow_conv_args.bk: Winograd F(2x2,3x3) packing/kernel (SCFLOW_CONV_WINO)
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 
 
@@ -98,6 +99,7 @@ SIGNATURES = {
     "scflow_corr_lookup": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_vp]),
     "scflow_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "scflow_conv_packed_size_bk": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     "scflow_conv_pack_weights": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_vp]),
     "scflow_conv_pick_bk": (c_int, [ctypes.POINTER(ConvArgs)]),

@@ -627,6 +627,71 @@ __global__ void pack_kernel(const float* __restrict__ w, float* __restrict__ out
   }
 }
 
+#include "conv_wino.h"
+
+// Winograd eligibility (conv_wino.h): 3×3, stride 1, pad 1, whole-row tiles of 32 tiles
+bool wino_shape(int kh, int kw, int stride, int w) {
+  return kh == 3 && kw == 3 && stride == 1 && (w == 32 || w == 64);
+}
+bool wino_launchable(const scflow_conv_args& a) {
+  return wino_shape(a.kh, a.kw, a.stride, a.w) && a.ph == 1 && a.pw == 1 &&
+         a.h % (a.w == 32 ? 4 : 2) == 0 && a.c0 % 4 == 0 && a.c1 % 4 == 0 && a.cout > 4 &&
+         !(a.c0 + a.c1 <= 4 && a.c1 == 0);
+}
+long long wino_packed_size(int cout, int c0, int c1) {
+  const int nst = (round_up(c0, WKC) + round_up(c1, WKC)) / WKC;
+  return (long long)(round_up(cout, 64) / 32) * nst * 16 * 256;
+}
+// 64 output channels per workgroup when that still fills every CU twice, else 32
+int wino_nbw(const scflow_conv_args& a, int cus) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("SCFLOW_WINO_NBW");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced == 1 || forced == 2) return forced;
+  if (a.cout <= 32) return 1;
+  const long long blocks = (long long)a.n * (a.h / (a.w == 32 ? 4 : 2));
+  return blocks * (round_up(a.cout, 64) / 64) >= 2LL * cus ? 2 : 1;
+}
+bool wino_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SCFLOW_CONV_WINO");
+    on = e ? atoi(e) != 0 : 1;
+  }
+  return on;
+}
+
+template <int W, int NBW>
+int launch_wino_w(const WinoParams& p, hipStream_t st) {
+  using G = WinoGeom<W>;
+  const size_t lds = wino_lds_bytes<NBW>(G::HR, G::HC);
+  static bool attr = false;
+  if (lds > 64 * 1024 && !attr) {
+    (void)hipFuncSetAttribute((const void*)conv_wino_kernel<W, NBW>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  dim3 grid(p.a.n * (p.a.h / G::OROWS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
+  conv_wino_kernel<W, NBW><<<grid, 256, lds, st>>>(p);
+  return scflow_launch_status();
+}
+
+int launch_wino(const scflow_conv_args& a, hipStream_t st) {
+  if (!wino_launchable(a) || a.epilogue != SCFLOW_EPI_PLAIN || !a.out) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(a.src0) || (a.s0 & 3) || (a.c1 > 0 && (!aligned16(a.src1) || (a.s1 & 3))) ||
+      !aligned16(a.weight))
+    return SCFLOW_EALIGN;
+  WinoParams p;
+  p.a = a;
+  p.cp0 = round_up(a.c0, WKC);
+  p.nst = (p.cp0 + round_up(a.c1, WKC)) / WKC;
+  const int nbw = wino_nbw(a, device_cus());
+  if (a.w == 32) return nbw == 2 ? launch_wino_w<32, 2>(p, st) : launch_wino_w<32, 1>(p, st);
+  return nbw == 2 ? launch_wino_w<64, 2>(p, st) : launch_wino_w<64, 1>(p, st);
+}
+
 // Workgroup-count heuristic (measured on MI355X, tools/conv_bench.py): 128-pixel tiles when
 // that still gives ≥ 2 workgroups per CU (≥ 512), else 64-pixel tiles (GRU q: 103 vs 94 TF,
 // N=64 convs: 85 vs 54 TF, N=192: 94 vs 91 TF; z|r and the 512-wide heads prefer 128).
@@ -732,10 +797,31 @@ SCFLOW_API long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, i
   return (long long)g.npad * g.ktot;
 }
 
+SCFLOW_API long long scflow_conv_packed_size_bk(int cout, int c0, int c1, int kh, int kw,
+                                                int stride, int w, int bk) {
+  if (bk == SCFLOW_CONV_WINO) {
+    if (cout <= 4 || c0 <= 0 || c1 < 0 || c0 % 4 || c1 % 4 || !wino_shape(kh, kw, stride, w))
+      return SCFLOW_EUNSUPPORTED;
+    return wino_packed_size(cout, c0, c1);
+  }
+  if (bk != 0 && bk != 8 && bk != 16) return SCFLOW_EINVAL;
+  return scflow_conv_packed_size(cout, c0, c1, kh, kw, stride, w);
+}
+
 SCFLOW_API int scflow_conv_pack_weights(const float* w_oihw, float* packed, int cout, int c0,
                                         int c1, int kh, int kw, int stride, int w, int bk,
                                         void* stream) {
   if (!w_oihw || !packed || cout <= 0 || c0 <= 0 || c1 < 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  if (bk == SCFLOW_CONV_WINO) {
+    const long long total = scflow_conv_packed_size_bk(cout, c0, c1, kh, kw, stride, w, bk);
+    if (total < 0) return (int)total;
+    const int cp0 = round_up(c0, WKC);
+    const int nst = (cp0 + round_up(c1, WKC)) / WKC;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    wino_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0, c1, cp0,
+                                                               nst, total);
+    return scflow_launch_status();
+  }
   if (bk == 0) bk = BK;
   if (bk != 8 && bk != 16) return SCFLOW_EINVAL;
   Geometry g = select_variant(cout, c0, c1, kh, kw, stride, w == 64 ? 64 : 32 * 4, w, (kh - 1) / 2,
@@ -753,6 +839,7 @@ SCFLOW_API int scflow_conv_pick_bk(const scflow_conv_args* args) {
   if (!args) return SCFLOW_EINVAL;
   const scflow_conv_args& a = *args;
   if (a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 || a.c1 < 0) return SCFLOW_EINVAL;
+  if (wino_enabled() && a.epilogue == SCFLOW_EPI_PLAIN && wino_launchable(a)) return SCFLOW_CONV_WINO;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
   if (g.variant != V_MFMA) return BK;  // other variants ignore the stage depth
   int tr, hr;
@@ -777,6 +864,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
   } else {
     return SCFLOW_EINVAL;
   }
+  if (a.bk == SCFLOW_CONV_WINO) return launch_wino(a, (hipStream_t)stream);
   if (a.bk != 0 && a.bk != 8 && a.bk != 16) return SCFLOW_EINVAL;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
   if (g.variant == V_NONE) return SCFLOW_EUNSUPPORTED;

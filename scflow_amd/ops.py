@@ -136,14 +136,15 @@ def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: i
 
 # ------------------------------------------------------------------------------- convolutions
 def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1, bk: int = 16) -> Tensor:
-    """Pack an nn.Conv2d weight ``[cout, c0+c1, kh, kw]`` for scflow_conv2d (K-stage depth bk)."""
+    """Pack an nn.Conv2d weight ``[cout, c0+c1, kh, kw]`` for scflow_conv2d (packing format bk:
+    K-stage depth 8/16 of the direct conv, or ``_lib.CONV_WINO`` for the Winograd kernel)."""
     _require(weight, "conv weight", contiguous=False)
     weight = weight.detach().contiguous()
     cout, cin, kh, kw = weight.shape
     if cin != c0 + c1:
         raise ValueError(f"weight has {cin} input channels, expected {c0}+{c1}")
     lib = _lib.load()
-    size = lib.scflow_conv_packed_size(cout, c0, c1, kh, kw, stride, w)
+    size = lib.scflow_conv_packed_size_bk(cout, c0, c1, kh, kw, stride, w, bk)
     if size < 0:
         raise ScflowError(f"no conv kernel for cout={cout} cin={c0}+{c1} k={kh}x{kw} w={w}")
     packed = torch.empty(size, device=weight.device, dtype=torch.float32)
@@ -154,12 +155,13 @@ def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1, 
 
 def conv_pick_bk(n: int, h: int, w: int, c0: int, c1: int, cout: int, kh: int, kw: int, ph: int,
                  pw: int, stride: int = 1) -> int:
-    """The library's preferred K-stage depth (8 or 16) for this launch shape (host-only query)."""
+    """The library's preferred packing format for this launch shape (host-only query): the
+    direct conv's K-stage depth (8 or 16) or ``_lib.CONV_WINO``."""
     a = _lib.ConvArgs()
     a.c0, a.c1, a.n, a.h, a.w = c0, c1, n, h, w
     a.cout, a.kh, a.kw, a.ph, a.pw, a.stride = cout, kh, kw, ph, pw, stride
     bk = _lib.load().scflow_conv_pick_bk(ctypes.byref(a))
-    if bk not in (8, 16):
+    if bk not in (8, 16, _lib.CONV_WINO):
         check(bk if bk < 0 else -2, "scflow_conv_pick_bk")
     return bk
 

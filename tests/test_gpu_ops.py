@@ -153,11 +153,33 @@ def test_conv2d_mfma_stage_depths(ops, case, bk):
     close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"conv {case} bk={bk}")
 
 
-def test_conv_pick_bk_prefers_resident_grids(ops):
-    """Host query: the 3×3 256→192 conv at B=16 (768 workgroups of 64 px) picks 8-deep stages,
-    the GRU z|r conv (512 workgroups of 128 px) 16."""
-    assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == 8
+def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
+    """Host query: 3×3 stride-1 convs take the Winograd kernel; the GRU z|r conv (512 workgroups
+    of 128 px) 16-deep stages of the direct conv."""
+    from scflow_amd._lib import CONV_WINO
+    assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == 16
+    assert ops.conv_pick_bk(2, 20, 20, 64, 0, 64, 3, 3, 1, 1) != CONV_WINO  # width not tileable
+
+
+@pytest.mark.parametrize("case", [
+    # (n, h, w, c0, c1, cout, k, pad, act)
+    (2, 32, 32, 256, 0, 192, 3, 1, "ReLU"),        # corr_net.1
+    (2, 32, 32, 192, 64, 126, 3, 1, "ReLU"),       # out_net: two sources, cout not /32
+    (2, 32, 32, 128, 0, 512, 3, 1, "ReLU"),        # XHead hidden convs (flow ‖ mask)
+    (2, 32, 32, 64, 0, 32, 3, 1, None),            # mask_encoder.1
+    (3, 32, 32, 12, 20, 40, 3, 1, "Tanh"),         # channels not /8 per source, cout 40
+    (1, 64, 64, 128, 0, 64, 3, 1, "ReLU"),         # 512² feature size
+    (2, 64, 64, 36, 4, 100, 3, 1, None),           # W=64, ragged channels
+    (16, 32, 32, 128, 0, 512, 3, 1, "ReLU"),       # B=16 heads: 64-channel workgroups
+])
+def test_conv2d_winograd(ops, case):
+    """Winograd F(2×2,3×3) kernel vs an fp64 direct conv (fp32 tolerance of the direct kernel)."""
+    from scflow_amd._lib import CONV_WINO
+    n, h, w, c0, c1, cout, k, pad, act = case
+    got, ref = _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, bk=CONV_WINO)
+    kk = (c0 + c1) * 9
+    close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"winograd conv {case}")
 
 
 def test_conv_gru_module(ops):
