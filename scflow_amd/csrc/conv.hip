@@ -628,19 +628,35 @@ __global__ void pack_kernel(const float* __restrict__ w, float* __restrict__ out
 }
 
 #include "conv_wino.h"
+#include "conv_wino5.h"
 
-// Winograd eligibility (conv_wino.h): 3×3, stride 1, pad 1, whole-row tiles of 32 tiles
+// Winograd eligibility: F(2×2,3×3) (conv_wino.h) for 3×3, F(4,5) (conv_wino5.h) for 1×5 / 5×1;
+// stride 1, "same" padding, whole-row tiles of 32 tiles
 bool wino_shape(int kh, int kw, int stride, int w) {
-  return kh == 3 && kw == 3 && stride == 1 && (w == 32 || w == 64);
+  const bool k = (kh == 3 && kw == 3) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1);
+  return k && stride == 1 && (w == 32 || w == 64);
 }
 bool wino_launchable(const scflow_conv_args& a) {
-  return wino_shape(a.kh, a.kw, a.stride, a.w) && a.ph == 1 && a.pw == 1 &&
-         a.h % (a.w == 32 ? 4 : 2) == 0 && a.c0 % 4 == 0 && a.c1 % 4 == 0 && a.cout > 4 &&
-         !(a.c0 + a.c1 <= 4 && a.c1 == 0);
+  if (!wino_shape(a.kh, a.kw, a.stride, a.w) || a.c0 % 4 || a.c1 % 4 || a.cout <= 4 ||
+      (a.c0 + a.c1 <= 4 && a.c1 == 0))
+    return false;
+  if (a.kh == 3) return a.ph == 1 && a.pw == 1 && a.h % (a.w == 32 ? 4 : 2) == 0 && a.epilogue == SCFLOW_EPI_PLAIN;
+  if (a.kh == 1) return a.ph == 0 && a.pw == 2 && a.h % (128 / a.w) == 0;
+  return a.ph == 2 && a.pw == 0 && a.h % 4 == 0;
 }
-long long wino_packed_size(int cout, int c0, int c1) {
-  const int nst = (round_up(c0, WKC) + round_up(c1, WKC)) / WKC;
-  return (long long)(round_up(cout, 64) / 32) * nst * 16 * 256;
+long long wino_packed_size(int cout, int c0, int c1, int kh) {
+  if (kh == 3) {
+    const int nst = (round_up(c0, WKC) + round_up(c1, WKC)) / WKC;
+    return (long long)(round_up(cout, 64) / 32) * nst * 16 * 256;
+  }
+  const int nst = (round_up(c0, W5KC) + round_up(c1, W5KC)) / W5KC;
+  return (long long)(round_up(cout, 64) / 32) * nst * 8 * 2 * 256;
+}
+// output rows per workgroup (the grid's x extent is n · h / rows · column blocks)
+long long wino_blocks(const scflow_conv_args& a) {
+  if (a.kh == 3) return (long long)a.n * (a.h / (a.w == 32 ? 4 : 2));
+  if (a.kh == 1) return (long long)a.n * (a.h / (128 / a.w));
+  return (long long)a.n * (a.h / 4) * (a.w / 32);
 }
 // 64 output channels per workgroup when that still fills every CU twice, else 32
 int wino_nbw(const scflow_conv_args& a, int cus) {
@@ -651,16 +667,17 @@ int wino_nbw(const scflow_conv_args& a, int cus) {
   }
   if (forced == 1 || forced == 2) return forced;
   if (a.cout <= 32) return 1;
-  const long long blocks = (long long)a.n * (a.h / (a.w == 32 ? 4 : 2));
-  return blocks * (round_up(a.cout, 64) / 64) >= 2LL * cus ? 2 : 1;
+  return wino_blocks(a) * (round_up(a.cout, 64) / 64) >= 2LL * cus ? 2 : 1;
 }
-bool wino_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("SCFLOW_CONV_WINO");
-    on = e ? atoi(e) != 0 : 1;
+bool wino_enabled(int kh) {
+  static int on3 = -1, on5 = -1;
+  if (on3 < 0) {
+    const char* e = getenv("SCFLOW_CONV_WINO");  // 0: off, 3: 3×3 only, 5: 1×5/5×1 only
+    const int v = e ? atoi(e) : 1;
+    on3 = v == 1 || v == 3;
+    on5 = v == 1 || v == 5;
   }
-  return on;
+  return kh == 3 ? on3 : on5;
 }
 
 template <int W, int NBW>
@@ -678,11 +695,49 @@ int launch_wino_w(const WinoParams& p, hipStream_t st) {
   return scflow_launch_status();
 }
 
+template <int DIR, int W, int NBW, int EPI>
+int launch_wino5_k(const Wino5Params& p, hipStream_t st) {
+  using G = Wino5Geom<DIR, W>;
+  const size_t lds = wino5_lds_bytes<NBW>(G::HR, G::HC);
+  static bool attr = false;
+  if (lds > 64 * 1024 && !attr) {
+    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
+  conv_wino5_kernel<DIR, W, NBW, EPI><<<grid, 256, lds, st>>>(p);
+  return scflow_launch_status();
+}
+
+template <int EPI>
+int launch_wino5_epi(const Wino5Params& p, int nbw, hipStream_t st) {
+  const bool x = p.a.kh == 1;
+  if (p.a.w == 32) {
+    if (x) return nbw == 2 ? launch_wino5_k<0, 32, 2, EPI>(p, st) : launch_wino5_k<0, 32, 1, EPI>(p, st);
+    return nbw == 2 ? launch_wino5_k<1, 32, 2, EPI>(p, st) : launch_wino5_k<1, 32, 1, EPI>(p, st);
+  }
+  if (x) return nbw == 2 ? launch_wino5_k<0, 64, 2, EPI>(p, st) : launch_wino5_k<0, 64, 1, EPI>(p, st);
+  return nbw == 2 ? launch_wino5_k<1, 64, 2, EPI>(p, st) : launch_wino5_k<1, 64, 1, EPI>(p, st);
+}
+
 int launch_wino(const scflow_conv_args& a, hipStream_t st) {
-  if (!wino_launchable(a) || a.epilogue != SCFLOW_EPI_PLAIN || !a.out) return SCFLOW_EUNSUPPORTED;
+  if (!wino_launchable(a)) return SCFLOW_EUNSUPPORTED;
   if (!aligned16(a.src0) || (a.s0 & 3) || (a.c1 > 0 && (!aligned16(a.src1) || (a.s1 & 3))) ||
       !aligned16(a.weight))
     return SCFLOW_EALIGN;
+  if (a.kh != 3) {
+    Wino5Params p;
+    p.a = a;
+    p.cp0 = round_up(a.c0, W5KC);
+    p.nst = (p.cp0 + round_up(a.c1, W5KC)) / W5KC;
+    const int nbw = wino_nbw(a, device_cus());
+    switch (a.epilogue) {
+      case SCFLOW_EPI_GRU_ZR: return launch_wino5_epi<SCFLOW_EPI_GRU_ZR>(p, nbw, st);
+      case SCFLOW_EPI_GRU_Q: return launch_wino5_epi<SCFLOW_EPI_GRU_Q>(p, nbw, st);
+      default: return launch_wino5_epi<SCFLOW_EPI_PLAIN>(p, nbw, st);
+    }
+  }
   WinoParams p;
   p.a = a;
   p.cp0 = round_up(a.c0, WKC);
@@ -802,7 +857,7 @@ SCFLOW_API long long scflow_conv_packed_size_bk(int cout, int c0, int c1, int kh
   if (bk == SCFLOW_CONV_WINO) {
     if (cout <= 4 || c0 <= 0 || c1 < 0 || c0 % 4 || c1 % 4 || !wino_shape(kh, kw, stride, w))
       return SCFLOW_EUNSUPPORTED;
-    return wino_packed_size(cout, c0, c1);
+    return wino_packed_size(cout, c0, c1, kh);
   }
   if (bk != 0 && bk != 8 && bk != 16) return SCFLOW_EINVAL;
   return scflow_conv_packed_size(cout, c0, c1, kh, kw, stride, w);
@@ -815,11 +870,16 @@ SCFLOW_API int scflow_conv_pack_weights(const float* w_oihw, float* packed, int 
   if (bk == SCFLOW_CONV_WINO) {
     const long long total = scflow_conv_packed_size_bk(cout, c0, c1, kh, kw, stride, w, bk);
     if (total < 0) return (int)total;
-    const int cp0 = round_up(c0, WKC);
-    const int nst = (cp0 + round_up(c1, WKC)) / WKC;
+    const int kc = kh == 3 ? WKC : W5KC;
+    const int cp0 = round_up(c0, kc);
+    const int nst = (cp0 + round_up(c1, kc)) / kc;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    wino_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0, c1, cp0,
-                                                               nst, total);
+    if (kh == 3)
+      wino_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0, c1, cp0,
+                                                                 nst, total);
+    else
+      wino5_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0, c1, cp0,
+                                                                  nst, total);
     return scflow_launch_status();
   }
   if (bk == 0) bk = BK;
@@ -839,7 +899,7 @@ SCFLOW_API int scflow_conv_pick_bk(const scflow_conv_args* args) {
   if (!args) return SCFLOW_EINVAL;
   const scflow_conv_args& a = *args;
   if (a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 || a.c1 < 0) return SCFLOW_EINVAL;
-  if (wino_enabled() && a.epilogue == SCFLOW_EPI_PLAIN && wino_launchable(a)) return SCFLOW_CONV_WINO;
+  if (wino_enabled(a.kh) && wino_launchable(a)) return SCFLOW_CONV_WINO;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
   if (g.variant != V_MFMA) return BK;  // other variants ignore the stage depth
   int tr, hr;

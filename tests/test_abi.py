@@ -49,7 +49,10 @@ def test_host_side_queries_need_no_gpu():
     # Winograd packing: 16 transform points × cout padded to 64 × cin padded to 8 per source
     assert lib.scflow_conv_packed_size_bk(192, 256, 0, 3, 3, 1, 32, 2) == 16 * 192 * 256
     assert lib.scflow_conv_packed_size_bk(126, 192, 60, 3, 3, 1, 32, 2) == 16 * 128 * (192 + 64)
-    assert lib.scflow_conv_packed_size_bk(64, 64, 0, 1, 5, 1, 32, 2) < 0  # 3×3 only
+    # F(4,5) packing: 8 transform points × cout padded to 64 × cin padded to 16 per source
+    assert lib.scflow_conv_packed_size_bk(64, 64, 0, 1, 5, 1, 32, 2) == 8 * 64 * 64
+    assert lib.scflow_conv_packed_size_bk(128, 120, 8, 5, 1, 1, 32, 2) == 8 * 128 * (128 + 16)
+    assert lib.scflow_conv_packed_size_bk(64, 64, 0, 1, 1, 1, 32, 2) < 0  # 3×3 / 1×5 / 5×1 only
     assert lib.scflow_conv_packed_size_bk(64, 64, 0, 3, 3, 1, 32, 16) == 64 * 64 * 9
     # argument errors return codes, they do not crash
     assert lib.scflow_corr_pyramid(None, None, None, 1, 1, 8, 8, 4, None) == -1

@@ -154,11 +154,13 @@ def test_conv2d_mfma_stage_depths(ops, case, bk):
 
 
 def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
-    """Host query: 3×3 stride-1 convs take the Winograd kernel; the GRU z|r conv (512 workgroups
-    of 128 px) 16-deep stages of the direct conv."""
+    """Host query: 3×3 / 1×5 / 5×1 stride-1 convs take the Winograd kernels; the 1×1 corr_net.0
+    conv (512 workgroups of 128 px) 16-deep stages of the direct conv."""
     from scflow_amd._lib import CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == CONV_WINO
-    assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == 16
+    assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == CONV_WINO
+    assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 5, 1, 2, 0) == CONV_WINO
+    assert ops.conv_pick_bk(16, 32, 32, 324, 0, 256, 1, 1, 0, 0) == 16
     assert ops.conv_pick_bk(2, 20, 20, 64, 0, 64, 3, 3, 1, 1) != CONV_WINO  # width not tileable
 
 
@@ -172,14 +174,67 @@ def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
     (1, 64, 64, 128, 0, 64, 3, 1, "ReLU"),         # 512² feature size
     (2, 64, 64, 36, 4, 100, 3, 1, None),           # W=64, ragged channels
     (16, 32, 32, 128, 0, 512, 3, 1, "ReLU"),       # B=16 heads: 64-channel workgroups
+    # F(4,5), 1×5 / 5×1
+    (2, 32, 32, 384, 0, 256, (1, 5), (0, 2), "Sigmoid"),    # GRU z|r
+    (2, 32, 32, 128, 256, 128, (5, 1), (2, 0), "Tanh"),     # GRU q, two sources
+    (3, 32, 32, 20, 44, 72, (1, 5), (0, 2), None),          # channels not /16 per source
+    (3, 32, 32, 20, 44, 72, (5, 1), (2, 0), None),
+    (1, 64, 64, 128, 128, 256, (1, 5), (0, 2), "ReLU"),     # 512² feature size
+    (1, 64, 64, 128, 128, 256, (5, 1), (2, 0), "ReLU"),     # two column blocks per row
+    (16, 32, 32, 128, 128, 256, (5, 1), (2, 0), None),      # B=16: 64-channel workgroups
 ])
 def test_conv2d_winograd(ops, case):
-    """Winograd F(2×2,3×3) kernel vs an fp64 direct conv (fp32 tolerance of the direct kernel)."""
+    """Winograd F(2×2,3×3) / F(4,5) kernels vs an fp64 direct conv (fp32 tolerance of the direct
+    kernel; F(4,5)'s fp32 error is ≈2× the direct conv's, within the same bound)."""
     from scflow_amd._lib import CONV_WINO
     n, h, w, c0, c1, cout, k, pad, act = case
     got, ref = _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, bk=CONV_WINO)
-    kk = (c0 + c1) * 9
+    kk = (c0 + c1) * (np.prod(k) if isinstance(k, tuple) else k * k)
     close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"winograd conv {case}")
+
+
+@pytest.mark.parametrize("k,pad", [((1, 5), (0, 2)), ((5, 1), (2, 0))])
+@pytest.mark.parametrize("bk", [16, 2])
+def test_conv_gru_epilogues(ops, k, pad, bk):
+    """GRU z|r and q epilogues (with a bias map) on the direct (bk 16) and F(4,5) Winograd
+    (bk 2) kernels vs fp64: z = σ(.), r·h, then h ← (1−z)h + z·tanh(q)."""
+    from scflow_amd._lib import EPI_GRU_Q, EPI_GRU_ZR
+    from scflow_amd.modules import ConvRunner
+    n, h, w, hc = 2, 32, 32, 128
+    g = torch.Generator().manual_seed(11)
+    hid = torch.tanh(torch.randn(n * h * w, hc, generator=g))
+    x = torch.randn(n * h * w, 128, generator=g)
+    bmap = torch.randn(n * h * w, 3 * hc, generator=g) * 0.3
+    czr = torch.nn.Conv2d(2 * hc, 2 * hc, k, padding=pad)
+    cq = torch.nn.Conv2d(2 * hc, hc, k, padding=pad)
+    for c in (czr, cq):
+        with torch.no_grad():
+            c.weight.copy_(torch.randn(c.weight.shape, generator=g) / np.sqrt(c.weight[0].numel()))
+            c.bias.copy_(torch.randn(c.bias.shape, generator=g) * 0.1)
+
+    def nchw(t):
+        return t.view(n, h, w, -1).permute(0, 3, 1, 2).double()
+    hx = torch.cat([nchw(hid), nchw(x)], 1)
+    pre = F.conv2d(hx, czr.weight.double(), czr.bias.double(), padding=pad) + nchw(bmap[:, :2 * hc])
+    z, r = torch.sigmoid(pre[:, :hc]), torch.sigmoid(pre[:, hc:])
+    q = torch.tanh(F.conv2d(torch.cat([r * nchw(hid), nchw(x)], 1), cq.weight.double(), cq.bias.double(),
+                            padding=pad) + nchw(bmap[:, 2 * hc:]))
+    href = (1 - z) * nchw(hid) + z * q
+
+    dh, dx, db = hid.cuda(), x.cuda(), bmap.cuda()
+    gate = torch.empty(n * h * w, hc, device="cuda")
+    rh = torch.empty(n * h * w, hc, device="cuda")
+    rz, rq = ConvRunner([czr.cuda()], None), ConvRunner([cq.cuda()], None)
+    for r_ in (rz, rq):
+        r_._bk_shape, r_._bk = (n, h, w, hc, 128), bk
+    rz.run(ops.Chan.whole(dh), None, n, h, w, src1=ops.Chan.whole(dx), epilogue=EPI_GRU_ZR,
+           gate=ops.Chan.whole(gate), rh=ops.Chan.whole(rh), hid=ops.Chan.whole(dh),
+           bias_map=ops.Chan(db, 0, 2 * hc))
+    close(ops.chan_to_nchw(ops.Chan.whole(gate), n, h, w), z, 2e-5, 1e-5, "z")
+    close(ops.chan_to_nchw(ops.Chan.whole(rh), n, h, w), r * nchw(hid), 2e-5, 1e-5, "r·h")
+    rq.run(ops.Chan.whole(rh), None, n, h, w, src1=ops.Chan.whole(dx), epilogue=EPI_GRU_Q,
+           gate=ops.Chan.whole(gate), hid=ops.Chan.whole(dh), bias_map=ops.Chan(db, 2 * hc, hc))
+    close(ops.chan_to_nchw(ops.Chan.whole(dh), n, h, w), href, 3e-5, 1e-5, "h")
 
 
 def test_conv_gru_module(ops):
