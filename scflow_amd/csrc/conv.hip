@@ -683,7 +683,7 @@ bool wino_enabled(int kh) {
 template <int W, int NBW>
 int launch_wino_w(const WinoParams& p, hipStream_t st) {
   using G = WinoGeom<W>;
-  const size_t lds = wino_lds_bytes<NBW>(G::HR, G::HC);
+  const size_t lds = wino_lds_bytes<W, NBW>();
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
     (void)hipFuncSetAttribute((const void*)conv_wino_kernel<W, NBW>,
@@ -698,7 +698,7 @@ int launch_wino_w(const WinoParams& p, hipStream_t st) {
 template <int DIR, int W, int NBW, int EPI>
 int launch_wino5_k(const Wino5Params& p, hipStream_t st) {
   using G = Wino5Geom<DIR, W>;
-  const size_t lds = wino5_lds_bytes<NBW>(G::HR, G::HC);
+  const size_t lds = wino5_lds_bytes<DIR, W, NBW>();
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
     (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI>,

@@ -44,11 +44,16 @@ struct WinoGeom {
   static constexpr int HC = W + 2;          // halo columns
   static constexpr int NH4 = HR * HC * 2;   // float4 of one stage's halo (2 per pixel)
   static constexpr int NA = (NH4 + 255) / 256;
+  // LDS halo layout (float4 units): 3 per pixel (8 channels + pad) and one more every 2 pixels,
+  // so the b128 patch reads of 16 consecutive lanes (tiles 2 pixels apart) hit distinct banks
+  static constexpr int ROWP = HC * 3 + HC / 2;
+  static constexpr int BUF4 = HR * ROWP;
+  __device__ static constexpr int addr(int r, int c) { return r * ROWP + c * 3 + (c >> 1); }
 };
 
-template <int NBW>
-constexpr size_t wino_lds_bytes(int hr, int hc) {
-  const size_t halo = (size_t)hr * hc * WLDP;
+template <int W, int NBW>
+constexpr size_t wino_lds_bytes() {
+  const size_t halo = (size_t)2 * WinoGeom<W>::BUF4 * 4;  // double-buffered
   const size_t epi = (size_t)4 * 2 * WTM * 32 * NBW;
   return sizeof(float) * (halo > epi ? halo : epi);
 }
@@ -66,9 +71,10 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   const int img = blockIdx.x / blocks_per_img;
   const int oy0 = (blockIdx.x % blocks_per_img) * G::OROWS;
   const int nst0 = P.cp0 / WKC;
+  const int nst = P.nst;
 
-  // halo addressing (stage-invariant): input pixel or -1 for zero padding
-  int apix[G::NA], acq[G::NA];
+  // halo addressing (stage-invariant): input pixel or -1 for zero padding, LDS slot
+  int apix[G::NA], acq[G::NA], aslot[G::NA];
 #pragma unroll
   for (int j = 0; j < G::NA; ++j) {
     const int idx = tid + 256 * j;
@@ -78,6 +84,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
     const bool ok = idx < G::NH4 && iy >= 0 && iy < a.h && ix >= 0 && ix < W;
     apix[j] = ok ? (img * a.h + iy) * W + ix : -1;
     acq[j] = 4 * (idx & 1);
+    aslot[j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 1) : -1;
   }
   floatx4 ra[G::NA];
   auto hload = [&](int s) {
@@ -94,35 +101,48 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
       ra[j] = v;
     }
   };
-  auto hstore = [&]() {
+  auto hstore = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < G::NA; ++j) {
-      const int idx = tid + 256 * j;
-      if (G::NH4 % 256 == 0 || idx < G::NH4) smem4[(idx >> 1) * (WLDP / 4) + (idx & 1)] = ra[j];
-    }
+    for (int j = 0; j < G::NA; ++j)
+      if (G::NH4 % 256 == 0 || aslot[j] >= 0) smem4[buf * G::BUF4 + aslot[j]] = ra[j];
   };
 
   // transformed weights: [nb32][stage][ξ 16][lane 64][4]; this wave's points are ξ = 4·wave + j
   const int nb0 = blockIdx.y * NBW;
-  auto wptr = [&](int s, int j, int nb) {
-    return a.weight + ((((size_t)(nb0 + nb) * P.nst + s) * 16 + 4 * wave + j) * 64 + lane) * 4;
-  };
   floatx4 ub[4][NBW], un[4][NBW];
   auto uload = [&](floatx4(&u)[4][NBW], int s) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) u[j][nb] = *(const floatx4*)wptr(s, j, nb);
+      for (int nb = 0; nb < NBW; ++nb)
+        u[j][nb] = *(const floatx4*)(a.weight +
+                                     ((((size_t)(nb0 + nb) * nst + s) * 16 + 4 * wave + j) * 64 + lane) * 4);
   };
 
-  // this wave's Bᵀ row: t = c1·d[r1] + c2·d[r2]
+  // this wave's Bᵀ row: t = c1·d[r1] + c2·d[r2]; the lane's tile (MFMA row li) reads the
+  // patch rows r1, r2 of its 4×4 input patch
   const int r1 = wave == 0 ? 0 : 1;
   const int r2 = wave == 0 ? 2 : (wave == 3 ? 3 : 2);
   const float c1 = wave == 2 ? -1.f : 1.f;
   const float c2 = (wave == 0 || wave == 3) ? -1.f : 1.f;
-  // this lane's tile (MFMA row li) and its patch origin in the halo
   const int ttr = li / G::TW, ttc = li % G::TW;
-  const int pbase4 = ((2 * ttr) * G::HC + 2 * ttc) * (WLDP / 4) + hh;  // in float4
+  int off1[4], off2[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    off1[b] = G::addr(2 * ttr + r1, 2 * ttc + b) + hh;
+    off2[b] = G::addr(2 * ttr + r2, 2 * ttc + b) + hh;
+  }
+  // V for this lane's tile, 4 channels (4hh..4hh+3 of the stage) at once
+  auto vcompute = [&](int buf, floatx4(&v)[4]) {
+    const floatx4* hb = smem4 + buf * G::BUF4;
+    floatx4 t[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) t[b] = c1 * hb[off1[b]] + c2 * hb[off2[b]];
+    v[0] = t[0] - t[2];
+    v[1] = t[1] + t[2];
+    v[2] = t[2] - t[1];
+    v[3] = t[1] - t[3];
+  };
 
   floatx16 acc[4][NBW];
 #pragma unroll
@@ -132,45 +152,40 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][nb][e] = 0.f;
 
+  // Software pipeline, one barrier per stage: at stage s the halo of s+1 goes to the other
+  // LDS buffer, the halo of s+2 and the weights of s+1 are loaded into registers, and the
+  // input transform of s+1 runs between the MFMAs of s.  Loads past the last stage re-read it
+  // (no branches in the loop).
   hload(0);
   uload(ub, 0);
   // Drain the prologue loads here: otherwise the compiler's wait-count analysis merges the
   // loop-entry state (ub still in flight) with the steady state and waits for ALL loads — this
   // stage's prefetch included — in front of every stage's first MFMA.
   __builtin_amdgcn_s_waitcnt(0);
-  for (int s = 0; s < P.nst; ++s) {
+  hstore(0);
+  hload(nst > 1 ? 1 : 0);
+  __syncthreads();
+  floatx4 vc[4], vn[4];
+  vcompute(0, vc);
+  for (int s = 0; s < nst; ++s) {
+    const int nbuf = (s + 1) & 1;
+    hstore(nbuf);
     __syncthreads();
-    hstore();
-    __syncthreads();
-    if (s + 1 < P.nst) {
-      hload(s + 1);
-      uload(un, s + 1);
-    }
-    // input transform for this lane's tile, 4 channels (4hh..4hh+3 of the stage) at once
-    floatx4 t[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const floatx4 x1 = smem4[pbase4 + (r1 * G::HC + b) * (WLDP / 4)];
-      const floatx4 x2 = smem4[pbase4 + (r2 * G::HC + b) * (WLDP / 4)];
-      t[b] = c1 * x1 + c2 * x2;
-    }
-    floatx4 v[4];
-    v[0] = t[0] - t[2];
-    v[1] = t[1] + t[2];
-    v[2] = t[2] - t[1];
-    v[3] = t[1] - t[3];
+    hload(s + 2 < nst ? s + 2 : nst - 1);
+    uload(un, s + 1 < nst ? s + 1 : nst - 1);
+    vcompute(nbuf, vn);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb)
-          acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], ub[j][nb][e], acc[j][nb], 0, 0, 0);
-    if (s + 1 < P.nst) {
+          acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[j][e], ub[j][nb][e], acc[j][nb], 0, 0, 0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j) {
+      vc[j] = vn[j];
 #pragma unroll
-        for (int nb = 0; nb < NBW; ++nb) ub[j][nb] = un[j][nb];
+      for (int nb = 0; nb < NBW; ++nb) ub[j][nb] = un[j][nb];
     }
   }
 

@@ -51,11 +51,21 @@ struct Wino5Geom {
   static constexpr int HC = DIR == 0 ? W + 4 : 32;
   static constexpr int NH4 = HR * HC * 4;  // float4 of one stage's halo (4 per pixel)
   static constexpr int NA = (NH4 + 255) / 256;
+  // LDS halo layout (float4 units): 5 per pixel (16 channels + pad); for 1×5 (lanes 4 pixels
+  // apart, 2 or 4 tile rows per 16 lanes) one more float4 every SK pixels plus a row pad, so
+  // the b128 reads of 16 consecutive lanes hit distinct banks (5×1: lanes 1 pixel apart, already
+  // conflict-free)
+  static constexpr int SK = DIR == 1 ? 0 : (W == 32 ? 2 : 4);
+  static constexpr int ROWP = HC * W5P4 + (SK ? HC / SK : 0) + (DIR == 0 && W == 32 ? 1 : 0);
+  static constexpr int BUF4 = HR * ROWP;
+  __device__ static constexpr int addr(int r, int c) {
+    return r * ROWP + c * W5P4 + (SK ? c / SK : 0);
+  }
 };
 
-template <int NBW>
-constexpr size_t wino5_lds_bytes(int hr, int hc) {
-  const size_t halo = (size_t)hr * hc * W5P4 * 4;
+template <int DIR, int W, int NBW>
+constexpr size_t wino5_lds_bytes() {
+  const size_t halo = (size_t)2 * Wino5Geom<DIR, W>::BUF4 * 4;  // double-buffered
   const size_t epi = (size_t)8 * W5TM * 32 * NBW;
   return sizeof(float) * (halo > epi ? halo : epi);
 }
@@ -96,10 +106,11 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   const int rem = blockIdx.x % blocks_per_img;
   const int oy0 = (rem / XB) * G::OROWS, ox0 = (rem % XB) * G::OCOLS;
   const int nst0 = P.cp0 / W5KC;
+  const int nst = P.nst;
   // halo origin in image coordinates
   const int hy0 = DIR == 0 ? oy0 : oy0 - 2, hx0 = DIR == 0 ? -2 : ox0;
 
-  int apix[G::NA], acq[G::NA];
+  int apix[G::NA], acq[G::NA], aslot[G::NA];
 #pragma unroll
   for (int j = 0; j < G::NA; ++j) {
     const int idx = tid + 256 * j;
@@ -109,6 +120,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     const bool ok = idx < G::NH4 && iy >= 0 && iy < a.h && ix >= 0 && ix < W;
     apix[j] = ok ? (img * a.h + iy) * W + ix : -1;
     acq[j] = 4 * (idx & 3);
+    aslot[j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 3) : -1;
   }
   floatx4 ra[G::NA];
   auto hload = [&](int s) {
@@ -125,12 +137,10 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
       ra[j] = v;
     }
   };
-  auto hstore = [&]() {
+  auto hstore = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < G::NA; ++j) {
-      const int idx = tid + 256 * j;
-      if (G::NH4 % 256 == 0 || idx < G::NH4) smem4[(idx >> 2) * W5P4 + (idx & 3)] = ra[j];
-    }
+    for (int j = 0; j < G::NA; ++j)
+      if (G::NH4 % 256 == 0 || aslot[j] >= 0) smem4[buf * G::BUF4 + aslot[j]] = ra[j];
   };
 
   // weights [nb32][stage][ξ 8][q 2][lane 64][4]; this wave's points ξ = 2·wave + x
@@ -144,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb)
           u[q][x][nb] = *(const floatx4*)(a.weight +
-                                          (((((size_t)(nb0 + nb) * P.nst + s) * 8 + 2 * wave + x) * 2 + q) * 64 +
+                                          (((((size_t)(nb0 + nb) * nst + s) * 8 + 2 * wave + x) * 2 + q) * 64 +
                                            lane) * 4);
   };
   // this wave's two Bᵀ rows (wave-uniform)
@@ -153,9 +163,24 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int t = 0; t < 8; ++t) bt[x][t] = kW5BT[2 * wave + x][t];
-  // this lane's tile: the halo pixel of input t is pb + t·tstep
-  const int pb = DIR == 0 ? (li / G::TPR) * G::HC + 4 * (li % G::TPR) : li;
-  constexpr int tstep = DIR == 0 ? 1 : G::HC;
+  // this lane's tile: LDS offsets of its 8 inputs along the conv axis
+  int toff[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    toff[t] = (DIR == 0 ? G::addr(li / G::TPR, 4 * (li % G::TPR) + t) : G::addr(t, li)) + hh;
+  auto vcompute = [&](int buf, floatx4(&v)[2][2]) {  // [q][x]
+    const floatx4* hb = smem4 + buf * G::BUF4;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      v[q][0] = v[q][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const floatx4 d = hb[toff[t] + 2 * q];
+        v[q][0] += bt[0][t] * d;
+        v[q][1] += bt[1][t] * d;
+      }
+    }
+  };
 
   floatx16 acc[2][NBW];
 #pragma unroll
@@ -165,42 +190,40 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[x][nb][e] = 0.f;
 
+  // software pipeline as in conv_wino.h: one barrier per stage, next stage's input transform
+  // between this stage's MFMAs
   hload(0);
   uload(ub, 0);
   __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
-  for (int s = 0; s < P.nst; ++s) {
+  hstore(0);
+  hload(nst > 1 ? 1 : 0);
+  __syncthreads();
+  floatx4 vc[2][2], vn[2][2];
+  vcompute(0, vc);
+  for (int s = 0; s < nst; ++s) {
+    const int nbuf = (s + 1) & 1;
+    hstore(nbuf);
     __syncthreads();
-    hstore();
-    __syncthreads();
-    if (s + 1 < P.nst) {
-      hload(s + 1);
-      uload(un, s + 1);
-    }
+    hload(s + 2 < nst ? s + 2 : nst - 1);
+    uload(un, s + 1 < nst ? s + 1 : nst - 1);
+    vcompute(nbuf, vn);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      floatx4 v[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const floatx4 d = smem4[(pb + t * tstep) * W5P4 + 2 * q + hh];
-        v[0] += bt[0][t] * d;
-        v[1] += bt[1][t] * d;
-      }
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb)
-            acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[x][e], ub[q][x][nb][e], acc[x][nb], 0, 0, 0);
-    }
-    if (s + 1 < P.nst) {
+            acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[q][x][e], ub[q][x][nb][e], acc[x][nb], 0, 0, 0);
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < 2; ++x) {
+        vc[q][x] = vn[q][x];
 #pragma unroll
-          for (int nb = 0; nb < NBW; ++nb) ub[q][x][nb] = un[q][x][nb];
-    }
+        for (int nb = 0; nb < NBW; ++nb) ub[q][x][nb] = un[q][x][nb];
+      }
   }
 
   // epilogue: M[ξ][tile][co] in LDS, then y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ]
