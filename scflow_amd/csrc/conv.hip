@@ -646,11 +646,11 @@ bool wino_launchable(const scflow_conv_args& a) {
 }
 long long wino_packed_size(int cout, int c0, int c1, int kh) {
   if (kh == 3) {
-    const int nst = (round_up(c0, WKC) + round_up(c1, WKC)) / WKC;
-    return (long long)(round_up(cout, 64) / 32) * nst * 16 * 256;
+    const int nsub = (round_up(c0, WSC) + round_up(c1, WSC)) / WKC;
+    return (long long)(round_up(cout, 64) / 32) * nsub * 16 * 256;
   }
-  const int nst = (round_up(c0, W5KC) + round_up(c1, W5KC)) / W5KC;
-  return (long long)(round_up(cout, 64) / 32) * nst * 8 * 2 * 256;
+  const int nsub = (round_up(c0, W5SC) + round_up(c1, W5SC)) / W5KC;
+  return (long long)(round_up(cout, 64) / 32) * nsub * 8 * 2 * 256;
 }
 // output rows per workgroup (the grid's x extent is n · h / rows · column blocks)
 long long wino_blocks(const scflow_conv_args& a) {
@@ -729,8 +729,8 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
   if (a.kh != 3) {
     Wino5Params p;
     p.a = a;
-    p.cp0 = round_up(a.c0, W5KC);
-    p.nst = (p.cp0 + round_up(a.c1, W5KC)) / W5KC;
+    p.cp0 = round_up(a.c0, W5SC);
+    p.nst = (p.cp0 + round_up(a.c1, W5SC)) / W5SC;
     const int nbw = wino_nbw(a, device_cus());
     switch (a.epilogue) {
       case SCFLOW_EPI_GRU_ZR: return launch_wino5_epi<SCFLOW_EPI_GRU_ZR>(p, nbw, st);
@@ -740,8 +740,8 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
   }
   WinoParams p;
   p.a = a;
-  p.cp0 = round_up(a.c0, WKC);
-  p.nst = (p.cp0 + round_up(a.c1, WKC)) / WKC;
+  p.cp0 = round_up(a.c0, WSC);
+  p.nst = (p.cp0 + round_up(a.c1, WSC)) / WSC;
   const int nbw = wino_nbw(a, device_cus());
   if (a.w == 32) return nbw == 2 ? launch_wino_w<32, 2>(p, st) : launch_wino_w<32, 1>(p, st);
   return nbw == 2 ? launch_wino_w<64, 2>(p, st) : launch_wino_w<64, 1>(p, st);
@@ -870,9 +870,10 @@ SCFLOW_API int scflow_conv_pack_weights(const float* w_oihw, float* packed, int 
   if (bk == SCFLOW_CONV_WINO) {
     const long long total = scflow_conv_packed_size_bk(cout, c0, c1, kh, kw, stride, w, bk);
     if (total < 0) return (int)total;
-    const int kc = kh == 3 ? WKC : W5KC;
-    const int cp0 = round_up(c0, kc);
-    const int nst = (cp0 + round_up(c1, kc)) / kc;
+    // channels padded per source to the kernel's stage depth; packed per sub-step
+    const int kc = kh == 3 ? WKC : W5KC, sc = kh == 3 ? WSC : W5SC;
+    const int cp0 = round_up(c0, sc);
+    const int nst = (cp0 + round_up(c1, sc)) / kc;
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     if (kh == 3)
       wino_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0, c1, cp0,

@@ -13,26 +13,64 @@
 //   Aᵀ = [1 1 1 0; 0 1 -1 -1].
 // For each of the 16 transform points ξ = (i, j) the channel contraction is a GEMM
 //   M_ξ[tile][co] = Σ_ci V_ξ[tile][ci] · U_ξ[ci][co],
-// which is where the MFMAs go.
+// which is where the MFMAs go.  Row i = 2 of Bᵀ is stored negated in both V and U (the product
+// is unchanged), so every wave's row transform is one FMA, t = d[r1] + s·d[r2].
 //
 // Workgroup = 32 tiles (128 output pixels: 4 image rows at W = 32, 2 at W = 64) × 32·NBW output
 // channels, 4 waves.  Wave i owns the four points ξ = (i, 0..3): its Bᵀ row picks two patch rows,
-// so the input transform of a wave's A operand is 8 LDS float4 reads and 32 adds per lane per
-// 8-channel stage, computed straight into registers (V never exists in memory).  The transformed
-// weights U are pre-packed in MFMA-lane order, so each wave streams its own points' U slice from
-// L2 as one coalesced 1 KiB load per (ξ, 32 channels), prefetched a stage ahead; nothing of U is
-// shared between waves, so it bypasses LDS.  Only the raw input halo of the stage
-// ((rows + 2) × (W + 2) pixels × 8 channels) is staged in LDS, shared by the 4 waves.  The
-// epilogue applies Aᵀ·A: each wave folds its row of M over j (A), the four rows meet in LDS,
-// and Aᵀ over i gives the 2×2 outputs, written channel-contiguous.
+// so the input transform of a wave's A operand is 8 LDS float4 reads and 16 packed adds per lane
+// per 8-channel sub-step, computed straight into registers (V never exists in memory).  The
+// transformed weights U are pre-packed in MFMA-lane order, so each wave streams its own points'
+// U slice from L2 as one coalesced 1 KiB buffer load per (ξ, 32 channels), each point's slice
+// reloaded for the next sub-step as soon as its MFMAs are issued; nothing of U is shared between
+// waves, so it bypasses LDS.  Only the raw input halo ((rows + 2) × (W + 2) pixels × 32 channels
+// per stage, double-buffered) is staged in LDS, shared by the 4 waves: one barrier per 4
+// sub-steps (128 MFMAs per wave), the next stage's halo loaded and stored in quarters between
+// this stage's sub-steps, the next sub-step's input transform computed between this sub-step's
+// MFMAs.  All global loads are buffer loads (zero padding by the hardware range check, offsets in
+// SGPRs), because every VALU instruction in the loop is paid for in MFMA issue cycles (≈ 6 per
+// v_pk_fma_f32 at 2 waves per SIMD, tools/micro/mfma_mix.hip).  The epilogue applies Aᵀ·A:
+// each wave folds its row of M over j (A), the four rows meet in LDS, and Aᵀ over i gives the
+// 2×2 outputs, written channel-contiguous.
 
-constexpr int WKC = 8;    // input channels per stage
-constexpr int WLDP = 12;  // LDS pitch of one halo pixel (8 channels + 4 pad, 16-B aligned)
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
+// raw buffer resource over [p, p + bytes): loads at offsets ≥ bytes return 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wino_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ floatx4 wino_bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+constexpr int WINO_OOB = 0x7ffffff0;  // voffset of a zero-padding lane (beyond any num_records)
+
+// a + s·b on float4 as two packed FMAs
+__device__ __forceinline__ floatx4 fma_s4(floatx4 b, float s, floatx4 a) {
+  floatx2 lo = __builtin_elementwise_fma(floatx2{b[0], b[1]}, floatx2{s, s}, floatx2{a[0], a[1]});
+  floatx2 hi = __builtin_elementwise_fma(floatx2{b[2], b[3]}, floatx2{s, s}, floatx2{a[2], a[3]});
+  return floatx4{lo[0], lo[1], hi[0], hi[1]};
+}
+
+// float4 a ± b as two packed ops
+__device__ __forceinline__ floatx4 add4(floatx4 a, floatx4 b) {
+  const floatx2 lo = floatx2{a[0], a[1]} + floatx2{b[0], b[1]};
+  const floatx2 hi = floatx2{a[2], a[3]} + floatx2{b[2], b[3]};
+  return floatx4{lo[0], lo[1], hi[0], hi[1]};
+}
+__device__ __forceinline__ floatx4 sub4(floatx4 a, floatx4 b) {
+  const floatx2 lo = floatx2{a[0], a[1]} - floatx2{b[0], b[1]};
+  const floatx2 hi = floatx2{a[2], a[3]} - floatx2{b[2], b[3]};
+  return floatx4{lo[0], lo[1], hi[0], hi[1]};
+}
+
+constexpr int WKC = 8;    // input channels per sub-step (one MFMA k-pass per lane)
+constexpr int WSC = 32;   // input channels per stage (one LDS halo buffer)
+constexpr int WNSUB = WSC / WKC;
 constexpr int WTM = 32;   // tiles per workgroup
 
 struct WinoParams {
   scflow_conv_args a;
-  int cp0, nst;  // padded channels of source 0, stages (8 channels each) over both sources
+  int cp0, nst;  // source 0's channels padded to WSC, stages (WSC channels each) over both
 };
 
 template <int W>
@@ -42,13 +80,13 @@ struct WinoGeom {
   static constexpr int OROWS = 2 * TRW;     // output rows per workgroup
   static constexpr int HR = OROWS + 2;      // halo rows
   static constexpr int HC = W + 2;          // halo columns
-  static constexpr int NH4 = HR * HC * 2;   // float4 of one stage's halo (2 per pixel)
-  static constexpr int NA = (NH4 + 255) / 256;
-  // LDS halo layout (float4 units): 3 per pixel (8 channels + pad) and one more every 2 pixels,
-  // so the b128 patch reads of 16 consecutive lanes (tiles 2 pixels apart) hit distinct banks
-  static constexpr int ROWP = HC * 3 + HC / 2;
+  static constexpr int NH4 = HR * HC * (WSC / 4);  // float4 of one stage's halo
+  static constexpr int NA = (NH4 + 1023) / 1024;   // float4 per thread per quarter stage
+  // LDS halo layout (float4 units): 8 per pixel and one more every 2 pixels, so the b128 patch
+  // reads of 16 consecutive lanes (tiles 2 pixels apart) hit distinct banks
+  static constexpr int ROWP = HC * 8 + HC / 2;
   static constexpr int BUF4 = HR * ROWP;
-  __device__ static constexpr int addr(int r, int c) { return r * ROWP + c * 3 + (c >> 1); }
+  __device__ static constexpr int addr(int r, int c) { return r * ROWP + c * 8 + (c >> 1); }
 };
 
 template <int W, int NBW>
@@ -65,83 +103,93 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   extern __shared__ floatx4 smem4[];  // float4-typed so halo accesses are ds_*_b128
   float* smem = (float*)smem4;
   const scflow_conv_args& a = P.a;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int li = lane & 31, hh = lane >> 5;
   const int blocks_per_img = a.h / G::OROWS;
   const int img = blockIdx.x / blocks_per_img;
   const int oy0 = (blockIdx.x % blocks_per_img) * G::OROWS;
-  const int nst0 = P.cp0 / WKC;
+  const int nst0 = P.cp0 / WSC;
   const int nst = P.nst;
+  const int npix = a.n * a.h * W;
 
-  // halo addressing (stage-invariant): input pixel or -1 for zero padding, LDS slot
-  int apix[G::NA], acq[G::NA], aslot[G::NA];
+  // halo staging: four quarters of NA float4 per thread; slot (part, j) is the (pixel, channel
+  // quad) pair (idx >> 3, idx & 7), idx = tid + 256·(4j + part).  Per slot: the input pixel
+  // (-1 = zero padding) and the LDS float4 index, both stage-invariant.
+  int hpix[4][G::NA], hlds[4][G::NA];
 #pragma unroll
-  for (int j = 0; j < G::NA; ++j) {
-    const int idx = tid + 256 * j;
-    const int pix = idx >> 1;
-    const int hr = pix / G::HC, hcol = pix - hr * G::HC;
-    const int iy = oy0 - 1 + hr, ix = hcol - 1;
-    const bool ok = idx < G::NH4 && iy >= 0 && iy < a.h && ix >= 0 && ix < W;
-    apix[j] = ok ? (img * a.h + iy) * W + ix : -1;
-    acq[j] = 4 * (idx & 1);
-    aslot[j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 1) : -1;
-  }
+  for (int part = 0; part < 4; ++part)
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int idx = tid + 256 * (4 * j + part);
+      const int pix = idx >> 3;
+      const int hr = pix / G::HC, hcol = pix - hr * G::HC;
+      const int iy = oy0 - 1 + hr, ix = hcol - 1;
+      const bool ok = idx < G::NH4 && iy >= 0 && iy < a.h && ix >= 0 && ix < W;
+      hpix[part][j] = ok ? (img * a.h + iy) * W + ix : -1;
+      hlds[part][j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 7) : -1;
+    }
+  const int hq4 = 4 * (tid & 7);  // channel of this thread's quad within the stage (idx & 7 = tid & 7)
   floatx4 ra[G::NA];
-  auto hload = [&](int s) {
+  // stage s's source, as a buffer starting at its first channel
+  __amdgpu_buffer_rsrc_t hsrc;
+  int hss4 = 0, hlim = 0;  // pixel stride in bytes, channels of the stage present in the source
+  auto hsource = [&](int s) {
     const bool s1 = s >= nst0;
     const float* src = s1 ? a.src1 : a.src0;
     const int cs = s1 ? a.c1 : a.c0;
     const int ss = s1 ? a.s1 : a.s0;
-    const int cc = (s1 ? s - nst0 : s) * WKC;
+    const int cc = (s1 ? s - nst0 : s) * WSC;
+    hsrc = wino_rsrc(src + cc, (unsigned)(((long long)(npix - 1) * ss + cs - cc) * 4));
+    hss4 = ss * 4;
+    hlim = cs - cc;
+  };
+  auto hload = [&](int part) {
+    const bool chan_ok = hq4 < hlim;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      const int c = cc + acq[j];
-      if (apix[j] >= 0 && c < cs) v = *(const floatx4*)(src + (size_t)apix[j] * ss + c);
-      ra[j] = v;
+      const int p = hpix[part][j];
+      ra[j] = wino_bload(hsrc, (p >= 0 && chan_ok) ? p * hss4 + hq4 * 4 : WINO_OOB, 0);
     }
   };
-  auto hstore = [&](int buf) {
+  auto hstore = [&](int buf, int part) {
 #pragma unroll
     for (int j = 0; j < G::NA; ++j)
-      if (G::NH4 % 256 == 0 || aslot[j] >= 0) smem4[buf * G::BUF4 + aslot[j]] = ra[j];
+      if (G::NH4 % 1024 == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[j];
   };
 
-  // transformed weights: [nb32][stage][ξ 16][lane 64][4]; this wave's points are ξ = 4·wave + j
-  const int nb0 = blockIdx.y * NBW;
-  floatx4 ub[4][NBW], un[4][NBW];
-  auto uload = [&](floatx4(&u)[4][NBW], int s) {
+  // transformed weights [nb32][sub-step (8 channels)][ξ 16][lane 64][4]; this wave's points are
+  // ξ = 4·wave + j
+  const int nsub = nst * WNSUB;
+  const __amdgpu_buffer_rsrc_t wsrc =
+      wino_rsrc(a.weight + (size_t)blockIdx.y * NBW * nsub * 16 * 256, (unsigned)(NBW * nsub * 16 * 1024));
+  auto uload1 = [&](floatx4(&u)[NBW], int t, int j) {  // point j of sub-step t (clamped)
+    const int tt = t < nsub ? t : nsub - 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int nb = 0; nb < NBW; ++nb)
-        u[j][nb] = *(const floatx4*)(a.weight +
-                                     ((((size_t)(nb0 + nb) * nst + s) * 16 + 4 * wave + j) * 64 + lane) * 4);
+    for (int nb = 0; nb < NBW; ++nb)
+      u[nb] = wino_bload(wsrc, lane * 16, (((nb * nsub + tt) * 16 + 4 * wave + j) * 1024));
   };
 
-  // this wave's Bᵀ row: t = c1·d[r1] + c2·d[r2]; the lane's tile (MFMA row li) reads the
-  // patch rows r1, r2 of its 4×4 input patch
+  // this wave's Bᵀ row (row 2 negated): t = d[r1] + sgn·d[r2]; the lane's tile (MFMA row li)
+  // reads the patch rows r1, r2 of its 4×4 input patch
   const int r1 = wave == 0 ? 0 : 1;
   const int r2 = wave == 0 ? 2 : (wave == 3 ? 3 : 2);
-  const float c1 = wave == 2 ? -1.f : 1.f;
-  const float c2 = (wave == 0 || wave == 3) ? -1.f : 1.f;
+  const float sgn = wave == 1 ? 1.f : -1.f;
   const int ttr = li / G::TW, ttc = li % G::TW;
-  int off1[4], off2[4];
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    off1[b] = G::addr(2 * ttr + r1, 2 * ttc + b) + hh;
-    off2[b] = G::addr(2 * ttr + r2, 2 * ttc + b) + hh;
-  }
-  // V for this lane's tile, 4 channels (4hh..4hh+3 of the stage) at once
-  auto vcompute = [&](int buf, floatx4(&v)[4]) {
-    const floatx4* hb = smem4 + buf * G::BUF4;
+  const int o1 = G::addr(2 * ttr + r1, 2 * ttc) + hh, o2 = G::addr(2 * ttr + r2, 2 * ttc) + hh;
+  // column b of the patch: +8b float4 plus the skew (patches start at even columns)
+  auto vcompute = [&](int buf, int k, floatx4(&v)[4]) {
+    const floatx4* hb = smem4 + buf * G::BUF4 + 2 * k;
     floatx4 t[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) t[b] = c1 * hb[off1[b]] + c2 * hb[off2[b]];
-    v[0] = t[0] - t[2];
-    v[1] = t[1] + t[2];
-    v[2] = t[2] - t[1];
-    v[3] = t[1] - t[3];
+    for (int b = 0; b < 4; ++b) {
+      const int cb = b * 8 + (b >> 1);
+      t[b] = fma_s4(hb[o2 + cb], sgn, hb[o1 + cb]);
+    }
+    v[0] = sub4(t[0], t[2]);
+    v[1] = add4(t[1], t[2]);
+    v[2] = sub4(t[2], t[1]);
+    v[3] = sub4(t[1], t[3]);
   };
 
   floatx16 acc[4][NBW];
@@ -152,41 +200,56 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][nb][e] = 0.f;
 
-  // Software pipeline, one barrier per stage: at stage s the halo of s+1 goes to the other
-  // LDS buffer, the halo of s+2 and the weights of s+1 are loaded into registers, and the
-  // input transform of s+1 runs between the MFMAs of s.  Loads past the last stage re-read it
-  // (no branches in the loop).
-  hload(0);
-  uload(ub, 0);
-  // Drain the prologue loads here: otherwise the compiler's wait-count analysis merges the
-  // loop-entry state (ub still in flight) with the steady state and waits for ALL loads — this
-  // stage's prefetch included — in front of every stage's first MFMA.
-  __builtin_amdgcn_s_waitcnt(0);
-  hstore(0);
-  hload(nst > 1 ? 1 : 0);
-  __syncthreads();
-  floatx4 vc[4], vn[4];
-  vcompute(0, vc);
-  for (int s = 0; s < nst; ++s) {
-    const int nbuf = (s + 1) & 1;
-    hstore(nbuf);
-    __syncthreads();
-    hload(s + 2 < nst ? s + 2 : nst - 1);
-    uload(un, s + 1 < nst ? s + 1 : nst - 1);
-    vcompute(nbuf, vn);
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int nb = 0; nb < NBW; ++nb)
-          acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[j][e], ub[j][nb][e], acc[j][nb], 0, 0, 0);
+  floatx4 u[4][NBW];
+  // one sub-step: the MFMAs of point j, then point j's weights for sub-step tnext
+  auto substep = [&](const floatx4(&v)[4], int tnext) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      vc[j] = vn[j];
 #pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) ub[j][nb] = un[j][nb];
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb)
+          acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[j][nb][e], acc[j][nb], 0, 0, 0);
+      uload1(u[j], tnext, j);
     }
+  };
+
+  // prologue: stage 0's halo in LDS buffer 0, sub-step 0's weights and transform in registers
+#pragma unroll
+  for (int j = 0; j < 4; ++j) uload1(u[j], 0, j);
+  hsource(0);
+#pragma unroll
+  for (int part = 0; part < 4; ++part) {
+    hload(part);
+    hstore(0, part);
+  }
+  // Drain the prologue loads: otherwise the compiler's wait-count analysis merges the
+  // loop-entry state with the steady state and waits for ALL loads in front of the MFMAs.
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  floatx4 vA[4], vB[4];
+  vcompute(0, 0, vA);
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    const int t0 = s * WNSUB;
+    hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
+    hload(0);
+    vcompute(buf, 1, vB);
+    substep(vA, t0 + 1);
+    hstore(buf ^ 1, 0);
+    hload(1);
+    vcompute(buf, 2, vA);
+    substep(vB, t0 + 2);
+    hstore(buf ^ 1, 1);
+    hload(2);
+    vcompute(buf, 3, vB);
+    substep(vA, t0 + 3);
+    hstore(buf ^ 1, 2);
+    hload(3);
+    substep(vB, t0 + 4);
+    hstore(buf ^ 1, 3);
+    __syncthreads();
+    vcompute(buf ^ 1, 0, vA);
   }
 
   // epilogue.  M row i (this wave) folded over j: s0 = M0+M1+M2, s1 = M1−M2−M3, into
@@ -232,18 +295,19 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q] + bias, a.act);
 }
 
-// U = G g Gᵀ per (co, ci), packed [nb32][stage][ξ][lane][4] with lane = li + 32·hh ↔
-// co = 32·nb32 + li, padded channel kc = 8·stage + 4·hh + e (source 1 starts at cp0).
+// U = G g Gᵀ per (co, ci) (row i = 2 negated), packed [nb32][sub-step][ξ][lane][4] with
+// lane = li + 32·hh ↔ co = 32·nb32 + li, padded channel kc = 8·sub-step + 4·hh + e (source 1
+// starts at cp0).
 __global__ void wino_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,
-                                 int c0, int c1, int cp0, int nst, long long total) {
+                                 int c0, int c1, int cp0, int nsub, long long total) {
   const int cin = c0 + c1;
   for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
     long long r = idx;
     const int e = (int)(r & 3); r >>= 2;
     const int lane = (int)(r & 63); r >>= 6;
     const int xi = (int)(r & 15); r >>= 4;
-    const int s = (int)(r % nst);
-    const int nb = (int)(r / nst);
+    const int s = (int)(r % nsub);
+    const int nb = (int)(r / nsub);
     const int o = nb * 32 + (lane & 31);
     const int kc = s * WKC + 4 * (lane >> 5) + e;
     int ci = -1;
@@ -260,7 +324,7 @@ __global__ void wino_pack_kernel(const float* __restrict__ w, float* __restrict_
       double acc = 0.0;
       for (int p = 0; p < 3; ++p)
         for (int q = 0; q < 3; ++q) acc += Gm[i][p] * (double)g[p * 3 + q] * Gm[j][q];
-      v = (float)acc;
+      v = (float)(i == 2 ? -acc : acc);
     }
     out[idx] = v;
   }

@@ -11,35 +11,37 @@
 //
 // Per transform point ξ the channel contraction is a GEMM M_ξ[tile][co] = Σ_ci V_ξ·U_ξ on
 // v_mfma_f32_32x32x2_f32.  Workgroup = 32 tiles (128 output pixels: 128/W whole rows for 1×5,
-// a 4-row × 32-column block for 5×1) × 32·NBW output channels, 4 waves; wave i owns the points
-// ξ = 2i, 2i+1: it forms its two rows of Bᵀd straight into registers from the stage's input
-// halo in LDS (16 float4 reads, 64 FMAs per lane per 16-channel stage) and streams its points'
-// pre-transformed weights from L2 (lane-ordered, 1 KiB per load, prefetched a stage ahead).
-// The epilogue gathers the 8 points of every (tile, channel) in LDS, applies Aᵀ and runs the
-// same fused epilogues as the direct conv (bias map, bias + activation, GRU z | r·h, GRU
-// h ← (1−z)h + z·tanh(q)).
+// a 4-row × 32-column block for 5×1) × 32·NBW output channels, 4 waves.  The points are paired
+// by the symmetry of Bᵀ: waves 0-2 own (1,2), (3,4), (5,6), whose rows are b ± a with a the odd
+// and b the even taps (7 packed float4 ops per 8 channels for both points), wave 3 owns (0,7).
+// Each wave forms its two rows of Bᵀd straight into registers from the input halo in LDS and
+// streams its points' pre-transformed weights from L2 (lane-ordered, one 1 KiB buffer load per
+// point, 8 channels and 32 output channels, reloaded as soon as its MFMAs are issued).  The halo
+// ((rows + 4 or + 0) × (columns + 4 or + 0) pixels × 32 channels per stage) is double-buffered
+// in LDS: one barrier per stage (64 MFMAs per wave), the next stage's halo loaded and stored in
+// halves between this stage's two 16-channel sub-steps, the next sub-step's input transform
+// computed between this sub-step's MFMAs, every global load a buffer load (see conv_wino.h on
+// why VALU work in the loop matters).  The epilogue gathers the 8 points of every (tile,
+// channel) in LDS, applies Aᵀ and runs the same fused epilogues as the direct conv (bias map,
+// bias + activation, GRU z | r·h, GRU h ← (1−z)h + z·tanh(q)).
 
-constexpr int W5KC = 16;  // input channels per stage
-constexpr int W5P4 = 5;   // LDS pitch of one halo pixel in float4 (16 channels + 4 pad floats)
+constexpr int W5KC = 16;  // input channels per sub-step
+constexpr int W5SC = 32;  // input channels per stage (one LDS halo buffer)
+constexpr int W5NSUB = W5SC / W5KC;
 constexpr int W5TM = 32;  // tiles per workgroup
 
-__constant__ float kW5BT[8][8] = {
-    {-1.0f, 0.0f, 5.25f, 0.0f, -5.25f, 0.0f, 1.0f, 0.0f},
-    {0.0f, 1.0f, 1.0f, -4.25f, -4.25f, 1.0f, 1.0f, 0.0f},
-    {0.0f, -1.0f, 1.0f, 4.25f, -4.25f, -1.0f, 1.0f, 0.0f},
-    {0.0f, 0.5f, 0.25f, -2.5f, -1.25f, 2.0f, 1.0f, 0.0f},
-    {0.0f, -0.5f, 0.25f, 2.5f, -1.25f, -2.0f, 1.0f, 0.0f},
-    {0.0f, 2.0f, 4.0f, -2.5f, -5.0f, 0.5f, 1.0f, 0.0f},
-    {0.0f, -2.0f, 4.0f, 2.5f, -5.0f, -0.5f, 1.0f, 0.0f},
-    {0.0f, -1.0f, 0.0f, 5.25f, 0.0f, -5.25f, 0.0f, 1.0f}};
 constexpr float kW5AT[4][8] = {{1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 0.0f},
                                {0.0f, 1.0f, -1.0f, 2.0f, -2.0f, 0.5f, -0.5f, 0.0f},
                                {0.0f, 1.0f, 1.0f, 4.0f, 4.0f, 0.25f, 0.25f, 0.0f},
                                {0.0f, 1.0f, -1.0f, 8.0f, -8.0f, 0.125f, -0.125f, 1.0f}};
+// the transform point held in slot x (0, 1) of wave w
+__host__ __device__ constexpr int w5_point(int w, int x) {
+  return w == 3 ? (x == 0 ? 0 : 7) : 2 * w + 1 + x;
+}
 
 struct Wino5Params {
   scflow_conv_args a;
-  int cp0, nst;  // padded channels of source 0, stages (16 channels each) over both sources
+  int cp0, nst;  // source 0's channels padded to W5SC, stages (W5SC channels each) over both
 };
 
 template <int DIR, int W>  // DIR 0: 1×5 (along x), 1: 5×1 (along y)
@@ -49,18 +51,14 @@ struct Wino5Geom {
   static constexpr int OCOLS = DIR == 0 ? W : 32;       // output columns per workgroup
   static constexpr int HR = DIR == 0 ? OROWS : OROWS + 4;
   static constexpr int HC = DIR == 0 ? W + 4 : 32;
-  static constexpr int NH4 = HR * HC * 4;  // float4 of one stage's halo (4 per pixel)
-  static constexpr int NA = (NH4 + 255) / 256;
-  // LDS halo layout (float4 units): 5 per pixel (16 channels + pad); for 1×5 (lanes 4 pixels
-  // apart, 2 or 4 tile rows per 16 lanes) one more float4 every SK pixels plus a row pad, so
-  // the b128 reads of 16 consecutive lanes hit distinct banks (5×1: lanes 1 pixel apart, already
-  // conflict-free)
-  static constexpr int SK = DIR == 1 ? 0 : (W == 32 ? 2 : 4);
-  static constexpr int ROWP = HC * W5P4 + (SK ? HC / SK : 0) + (DIR == 0 && W == 32 ? 1 : 0);
+  static constexpr int NH4 = HR * HC * (W5SC / 4);  // float4 of one stage's halo
+  static constexpr int NA = (NH4 + 511) / 512;      // float4 per thread per half stage
+  // LDS halo layout (float4 units): 8 per pixel, one more every SK pixels and a row pad, chosen
+  // (exhaustive bank model) so the b128 tap reads of 16 consecutive lanes hit distinct banks
+  static constexpr int SK = DIR == 0 && W == 64 ? 4 : 2;
+  static constexpr int ROWP = HC * 8 + HC / SK + (DIR == 0 && W == 32 ? 1 : 0);
   static constexpr int BUF4 = HR * ROWP;
-  __device__ static constexpr int addr(int r, int c) {
-    return r * ROWP + c * W5P4 + (SK ? c / SK : 0);
-  }
+  __device__ static constexpr int addr(int r, int c) { return r * ROWP + c * 8 + c / SK; }
 };
 
 template <int DIR, int W, int NBW>
@@ -98,86 +96,106 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   extern __shared__ floatx4 smem4[];
   float* smem = (float*)smem4;
   const scflow_conv_args& a = P.a;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int li = lane & 31, hh = lane >> 5;
   constexpr int XB = W / G::OCOLS;  // column blocks per image (1, or 2 for 5×1 at W = 64)
   const int blocks_per_img = (a.h / G::OROWS) * XB;
   const int img = blockIdx.x / blocks_per_img;
   const int rem = blockIdx.x % blocks_per_img;
   const int oy0 = (rem / XB) * G::OROWS, ox0 = (rem % XB) * G::OCOLS;
-  const int nst0 = P.cp0 / W5KC;
+  const int nst0 = P.cp0 / W5SC;
   const int nst = P.nst;
+  const int npix = a.n * a.h * W;
   // halo origin in image coordinates
   const int hy0 = DIR == 0 ? oy0 : oy0 - 2, hx0 = DIR == 0 ? -2 : ox0;
 
-  int apix[G::NA], acq[G::NA], aslot[G::NA];
+  // halo staging in two halves of NA float4 per thread: slot (part, j) is the (pixel, channel
+  // quad) pair (idx >> 3, idx & 7), idx = tid + 256·(2j + part)
+  int hpix[2][G::NA], hlds[2][G::NA];
 #pragma unroll
-  for (int j = 0; j < G::NA; ++j) {
-    const int idx = tid + 256 * j;
-    const int pix = idx >> 2;
-    const int hr = pix / G::HC, hcol = pix - hr * G::HC;
-    const int iy = hy0 + hr, ix = hx0 + hcol;
-    const bool ok = idx < G::NH4 && iy >= 0 && iy < a.h && ix >= 0 && ix < W;
-    apix[j] = ok ? (img * a.h + iy) * W + ix : -1;
-    acq[j] = 4 * (idx & 3);
-    aslot[j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 3) : -1;
-  }
+  for (int part = 0; part < 2; ++part)
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int idx = tid + 256 * (2 * j + part);
+      const int pix = idx >> 3;
+      const int hr = pix / G::HC, hcol = pix - hr * G::HC;
+      const int iy = hy0 + hr, ix = hx0 + hcol;
+      const bool ok = idx < G::NH4 && iy >= 0 && iy < a.h && ix >= 0 && ix < W;
+      hpix[part][j] = ok ? (img * a.h + iy) * W + ix : -1;
+      hlds[part][j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 7) : -1;
+    }
+  const int hq4 = 4 * (tid & 7);
   floatx4 ra[G::NA];
-  auto hload = [&](int s) {
+  __amdgpu_buffer_rsrc_t hsrc;
+  int hss4 = 0, hlim = 0;
+  auto hsource = [&](int s) {
     const bool s1 = s >= nst0;
     const float* src = s1 ? a.src1 : a.src0;
     const int cs = s1 ? a.c1 : a.c0;
     const int ss = s1 ? a.s1 : a.s0;
-    const int cc = (s1 ? s - nst0 : s) * W5KC;
+    const int cc = (s1 ? s - nst0 : s) * W5SC;
+    hsrc = wino_rsrc(src + cc, (unsigned)(((long long)(npix - 1) * ss + cs - cc) * 4));
+    hss4 = ss * 4;
+    hlim = cs - cc;
+  };
+  auto hload = [&](int part) {
+    const bool chan_ok = hq4 < hlim;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      const int c = cc + acq[j];
-      if (apix[j] >= 0 && c < cs) v = *(const floatx4*)(src + (size_t)apix[j] * ss + c);
-      ra[j] = v;
+      const int p = hpix[part][j];
+      ra[j] = wino_bload(hsrc, (p >= 0 && chan_ok) ? p * hss4 + hq4 * 4 : WINO_OOB, 0);
     }
   };
-  auto hstore = [&](int buf) {
+  auto hstore = [&](int buf, int part) {
 #pragma unroll
     for (int j = 0; j < G::NA; ++j)
-      if (G::NH4 % 256 == 0 || aslot[j] >= 0) smem4[buf * G::BUF4 + aslot[j]] = ra[j];
+      if (G::NH4 % 512 == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[j];
   };
 
-  // weights [nb32][stage][ξ 8][q 2][lane 64][4]; this wave's points ξ = 2·wave + x
-  const int nb0 = blockIdx.y * NBW;
-  floatx4 ub[2][2][NBW], un[2][2][NBW];  // [q][x][nb]
-  auto uload = [&](floatx4(&u)[2][2][NBW], int s) {
+  // weights [nb32][sub-step (16 channels)][slot 8][q 2][lane 64][4]; slot 2·wave + x holds
+  // point w5_point(wave, x)
+  const int nsub = nst * W5NSUB;
+  const __amdgpu_buffer_rsrc_t wsrc =
+      wino_rsrc(a.weight + (size_t)blockIdx.y * NBW * nsub * 16 * 256, (unsigned)(NBW * nsub * 16 * 1024));
+  floatx4 u[2][2][NBW];  // [q][x][nb]
+  auto uload1 = [&](int t, int q) {
+    const int tt = t < nsub ? t : nsub - 1;
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int x = 0; x < 2; ++x)
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int nb = 0; nb < NBW; ++nb)
-          u[q][x][nb] = *(const floatx4*)(a.weight +
-                                          (((((size_t)(nb0 + nb) * nst + s) * 8 + 2 * wave + x) * 2 + q) * 64 +
-                                           lane) * 4);
+      for (int nb = 0; nb < NBW; ++nb)
+        u[q][x][nb] = wino_bload(wsrc, lane * 16, ((((nb * nsub + tt) * 8 + 2 * wave + x) * 2 + q) * 1024));
   };
-  // this wave's two Bᵀ rows (wave-uniform)
-  float bt[2][8];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int t = 0; t < 8; ++t) bt[x][t] = kW5BT[2 * wave + x][t];
-  // this lane's tile: LDS offsets of its 8 inputs along the conv axis
-  int toff[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-    toff[t] = (DIR == 0 ? G::addr(li / G::TPR, 4 * (li % G::TPR) + t) : G::addr(t, li)) + hh;
-  auto vcompute = [&](int buf, floatx4(&v)[2][2]) {  // [q][x]
-    const floatx4* hb = smem4 + buf * G::BUF4;
+
+  // Bᵀ rows of this wave: waves 0-2 → V = b ± a (odd taps a = c1·d1 + c3·d3 + c5·d5, even taps
+  // b = c2·d2 + c4·d4 + d6); wave 3 → V0 = (d6 − d0) + 5.25(d2 − d4), V7 = (d7 − d1) + 5.25(d3 − d5)
+  const float c1 = wave == 0 ? 1.f : (wave == 1 ? 0.5f : 2.f);
+  const float c3 = wave == 0 ? -4.25f : -2.5f;
+  const float c5 = wave == 0 ? 1.f : (wave == 1 ? 2.f : 0.5f);
+  const float c2 = wave == 0 ? 1.f : (wave == 1 ? 0.25f : 4.f);
+  const float c4 = wave == 0 ? -4.25f : (wave == 1 ? -1.25f : -5.f);
+  // the lane's tile: LDS float4 index of its input 0 along the conv axis (+ the channel half hh)
+  const int tb = (DIR == 0 ? G::addr(li / G::TPR, 4 * (li % G::TPR)) : G::addr(0, li)) + hh;
+  auto tapoff = [](int t) {  // LDS float4 offset of input t from input 0 (tiles start at c ≡ 0 mod 4)
+    return DIR == 0 ? t * 8 + t / G::SK : t * G::ROWP;
+  };
+  auto vcompute = [&](int buf, int k, floatx4(&v)[2][2]) {  // [q][x]
+    const floatx4* hb = smem4 + buf * G::BUF4 + tb + 4 * k;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      v[q][0] = v[q][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      floatx4 d[8];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const floatx4 d = hb[toff[t] + 2 * q];
-        v[q][0] += bt[0][t] * d;
-        v[q][1] += bt[1][t] * d;
+      for (int t = 0; t < 8; ++t) d[t] = hb[tapoff(t) + 2 * q];
+      if (wave < 3) {
+        const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+        const floatx4 av = fma_s4(d[5], c5, fma_s4(d[3], c3, fma_s4(d[1], c1, zero)));
+        const floatx4 bv = fma_s4(d[4], c4, fma_s4(d[2], c2, d[6]));
+        v[q][0] = add4(bv, av);
+        v[q][1] = sub4(bv, av);
+      } else {
+        v[q][0] = fma_s4(sub4(d[2], d[4]), 5.25f, sub4(d[6], d[0]));
+        v[q][1] = fma_s4(sub4(d[3], d[5]), 5.25f, sub4(d[7], d[1]));
       }
     }
   };
@@ -190,40 +208,45 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[x][nb][e] = 0.f;
 
-  // software pipeline as in conv_wino.h: one barrier per stage, next stage's input transform
-  // between this stage's MFMAs
-  hload(0);
-  uload(ub, 0);
-  __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
-  hstore(0);
-  hload(nst > 1 ? 1 : 0);
-  __syncthreads();
-  floatx4 vc[2][2], vn[2][2];
-  vcompute(0, vc);
-  for (int s = 0; s < nst; ++s) {
-    const int nbuf = (s + 1) & 1;
-    hstore(nbuf);
-    __syncthreads();
-    hload(s + 2 < nst ? s + 2 : nst - 1);
-    uload(un, s + 1 < nst ? s + 1 : nst - 1);
-    vcompute(nbuf, vn);
+  // one 16-channel sub-step: per 8-channel half q, its MFMAs then its weights for tnext
+  auto substep = [&](const floatx4(&v)[2][2], int tnext) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2; ++q) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb)
-            acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(vc[q][x][e], ub[q][x][nb][e], acc[x][nb], 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        vc[q][x] = vn[q][x];
-#pragma unroll
-        for (int nb = 0; nb < NBW; ++nb) ub[q][x][nb] = un[q][x][nb];
-      }
+            acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[q][x][e], u[q][x][nb][e], acc[x][nb], 0, 0, 0);
+      uload1(tnext, q);
+    }
+  };
+
+  uload1(0, 0);
+  uload1(0, 1);
+  hsource(0);
+  hload(0);
+  hstore(0, 0);
+  hload(1);
+  hstore(0, 1);
+  __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
+  __syncthreads();
+  floatx4 vA[2][2], vB[2][2];
+  vcompute(0, 0, vA);
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    const int t0 = s * W5NSUB;
+    hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
+    hload(0);
+    vcompute(buf, 1, vB);
+    substep(vA, t0 + 1);
+    hstore(buf ^ 1, 0);
+    hload(1);
+    substep(vB, t0 + 2);
+    hstore(buf ^ 1, 1);
+    __syncthreads();
+    vcompute(buf ^ 1, 0, vA);
   }
 
   // epilogue: M[ξ][tile][co] in LDS, then y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ]
@@ -236,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = (r & 3) + 8 * (r >> 2) + 4 * hh;
-        S[((2 * wave + x) * W5TM + m) * BNW + nb * 32 + li] = acc[x][nb][r];
+        S[(w5_point(wave, x) * W5TM + m) * BNW + nb * 32 + li] = acc[x][nb][r];
       }
   __syncthreads();
   const int co = tid % BNW;
@@ -273,8 +296,8 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   }
 }
 
-// U_ξ = Σ_j G[ξ][j]·g[j] (fp64) per (co, ci), packed [nb32][stage][ξ][q][lane][4] with
-// lane = li + 32·hh ↔ co = 32·nb32 + li, padded channel kc = 16·stage + 8·q + 4·hh + e.
+// U_ξ = Σ_j G[ξ][j]·g[j] (fp64) per (co, ci), packed [nb32][sub-step][slot][q][lane][4] with
+// lane = li + 32·hh ↔ co = 32·nb32 + li, padded channel kc = 16·sub-step + 8·q + 4·hh + e.
 __global__ void wino5_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,
                                   int c0, int c1, int cp0, int nst, long long total) {
   const double Gm[8][5] = {{-1.0, 0.0, 0.0, 0.0, 0.0},
@@ -291,7 +314,8 @@ __global__ void wino5_pack_kernel(const float* __restrict__ w, float* __restrict
     const int e = (int)(r & 3); r >>= 2;
     const int lane = (int)(r & 63); r >>= 6;
     const int q = (int)(r & 1); r >>= 1;
-    const int xi = (int)(r & 7); r >>= 3;
+    const int slot = (int)(r & 7); r >>= 3;
+    const int xi = w5_point(slot >> 1, slot & 1);
     const int s = (int)(r % nst);
     const int nb = (int)(r / nst);
     const int o = nb * 32 + (lane & 31);

@@ -7,7 +7,10 @@ from scflow_amd.ops import Chan
 
 n, h, w = 16, 32, 32
 M = n * h * w
-for k, pad in [((1, 5), (0, 2)), ((5, 1), (2, 0)), ((3, 3), (1, 1))]:
+KS = [((1, 5), (0, 2)), ((5, 1), (2, 0)), ((3, 3), (1, 1))]
+if len(sys.argv) > 1:
+    KS = [kp for kp in KS if f"{kp[0][0]}x{kp[0][1]}" in sys.argv[1].split(",")]
+for k, pad in KS:
     for cout in (128, 256, 512):
         for cin in (128, 256, 512, 1024):
             conv = torch.nn.Conv2d(cin, cout, k, padding=pad).cuda()
