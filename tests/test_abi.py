@@ -46,12 +46,12 @@ def test_host_side_queries_need_no_gpu():
     # cin 324 is padded to 336 per tap; cout 126 to 128
     assert lib.scflow_conv_packed_size(126, 324, 0, 1, 1, 1, 32) == 128 * 336
     assert lib.scflow_conv_packed_size(64, 64, 0, 3, 3, 1, 20) < 0  # width not tileable → unsupported
-    # Winograd packing: 16 transform points × cout padded to 64 × cin padded to 8 per source
+    # Winograd packing: 16 transform points × cout padded to 64 × cin padded to 32 per source
     assert lib.scflow_conv_packed_size_bk(192, 256, 0, 3, 3, 1, 32, 2) == 16 * 192 * 256
     assert lib.scflow_conv_packed_size_bk(126, 192, 60, 3, 3, 1, 32, 2) == 16 * 128 * (192 + 64)
-    # F(4,5) packing: 8 transform points × cout padded to 64 × cin padded to 16 per source
+    # F(4,5) packing: 8 transform points × cout padded to 64 × cin padded to 32 per source
     assert lib.scflow_conv_packed_size_bk(64, 64, 0, 1, 5, 1, 32, 2) == 8 * 64 * 64
-    assert lib.scflow_conv_packed_size_bk(128, 120, 8, 5, 1, 1, 32, 2) == 8 * 128 * (128 + 16)
+    assert lib.scflow_conv_packed_size_bk(128, 120, 8, 5, 1, 1, 32, 2) == 8 * 128 * (128 + 32)
     assert lib.scflow_conv_packed_size_bk(64, 64, 0, 1, 1, 1, 32, 2) < 0  # 3×3 / 1×5 / 5×1 only
     assert lib.scflow_conv_packed_size_bk(64, 64, 0, 3, 3, 1, 32, 16) == 64 * 64 * 9
     # argument errors return codes, they do not crash
