@@ -12,11 +12,14 @@ SURVEY.md §8(e)); ``value`` = all pairs·iterations of all ranks ÷ the slowest
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Extra JSON fields:
-* ``roofline``: the dominant kernel, ``conv_mfma_kernel<GRU_ZR>`` (the fused z|r SepConvGRU
-  convolution: 2 launches per iteration; with the loop-invariant context contribution hoisted
-  out of the loop it contracts h and the motion features, 2·M·256·5·256 = 10.7 GFLOP per launch
-  at B=16), timed live with HIP events around each of its launches in the timed region;
-  bound = fp32 MFMA, peak 157.3 TFLOP/s.
+* ``roofline``: the dominant kernel, the fused z|r SepConvGRU convolution (2 launches per
+  iteration; with the loop-invariant context contribution hoisted out of the loop it contracts
+  h and the motion features, 2·M·256·5·256 = 10.7 GFLOP of algorithmic work per launch at
+  B=16), on the F(4,5) Winograd kernel ``conv_wino5_kernel<GRU_ZR>`` (2.5× fewer matrix
+  multiplies), timed live with HIP events around each of its launches in the timed region;
+  bound = fp32 MFMA, peak 157.3 TFLOP/s.  ``achieved``/``frac`` use the algorithmic FLOPs (so
+  they can exceed the peak), ``mfma_achieved``/``mfma_frac`` the FLOPs the matrix cores
+  execute.
 * ``cpu_baseline``: the CPU oracle (oracle/scflow_oracle.py, a parity-pinned PyTorch-CPU
   restatement of the reference decoder) on a bounded sample, rank 0 at N=1 only.
 """
@@ -315,9 +318,16 @@ def main():
     units = world * args.batch * args.iters * args.steps
     value = units / elapsed
     zr_ms = timer.mean_ms()
-    flops = dec.gru.zr_flops(args.batch * (args.size // 8) ** 2,
-                             dec.cxt_channels if dec.hoist_context else 0)
+    m_px = args.batch * (args.size // 8) ** 2
+    cxt = dec.cxt_channels if dec.hoist_context else 0
+    zr = dec.gru.zr_runner(cxt)
+    flops = zr.flops(m_px)
     achieved = flops / (zr_ms * 1e-3) / 1e12
+    hc = dec.h_channels
+    mfma_flops = zr.mfma_flops(m_px, hc, zr.cin - hc)
+    mfma_achieved = mfma_flops / (zr_ms * 1e-3) / 1e12
+    zr_kernel = ("conv_wino5_kernel<GRU_ZR> (SepConvGRU z|r conv, Winograd F(4,5) on fp32 MFMA)"
+                 if zr.winograd else "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r conv, direct)")
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -348,12 +358,17 @@ def main():
                        "global_batch": args.batch * world, "image": args.size, "iters": args.iters,
                        "launch": "hipGraph replay" if args.graph else "eager",
                        "parallelism": f"dp{world}"},
-            "roofline": {"kernel": "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r conv)",
+            "roofline": {"kernel": zr_kernel,
                          "bound": "mfma", "achieved": round(achieved, 2),
                          "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                          "avg_launch_ms": round(zr_ms, 4), "launches": timer.count(),
-                         "flops_per_launch": flops},
+                         "flops_per_launch": flops,
+                         # achieved/frac count the direct conv's (algorithmic) FLOPs; Winograd
+                         # executes fewer: these are the matrix cores' own FLOPs and busy share
+                         "mfma_flops_per_launch": mfma_flops,
+                         "mfma_achieved": round(mfma_achieved, 2),
+                         "mfma_frac": round(mfma_achieved / FP32_MFMA_PEAK_TFLOPS, 4)},
         }
         res["rooflines_secondary"] = secondary_rooflines(timers, args.batch, args.size)
         if e2e is not None:

@@ -28,7 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import _lib, ops
 from ._lib import EPI_GRU_Q, EPI_GRU_ZR, EPI_PLAIN
 from .ops import Chan
 from .registry import MODELS
@@ -173,6 +173,23 @@ class ConvRunner:
     def flops(self, m: int) -> float:
         """Algorithmic FLOPs of one launch over m output pixels (2·m·cout·taps·cin)."""
         return 2.0 * m * self.cout * self.kh * self.kw * self.cin
+
+    @property
+    def winograd(self) -> bool:
+        """True once a launch picked the Winograd kernel (F(2×2,3×3) or F(4,5))."""
+        return getattr(self, "_bk", None) == _lib.CONV_WINO
+
+    def mfma_flops(self, m: int, c0: int, c1: int = 0) -> float:
+        """FLOPs the matrix cores execute for one launch over m output pixels with the inputs
+        split c0 + c1: the Winograd kernels multiply per transform point (16 per 2×2 tile for
+        3×3, 8 per 4-pixel tile for 1×5 / 5×1) over channels padded to 32 per source and output
+        channels padded to 32; the direct kernel does the algorithmic work on padded channels."""
+        ru = lambda v, q: (v + q - 1) // q * q  # noqa: E731
+        kpad, npad = ru(c0, 32) + ru(c1, 32), ru(self.cout, 32)
+        if self.winograd:
+            pts, tile = (16, 4) if self.kh * self.kw == 9 else (8, 4)
+            return 2.0 * pts * (m / tile) * kpad * npad
+        return 2.0 * m * npad * self.kh * self.kw * (ru(c0, 16) + ru(c1, 16))
 
 
 # ---------------------------------------------------------------------------------- a1 / a2
@@ -389,11 +406,14 @@ class ConvGRU(nn.Module):
             if hq:
                 hq(False)
 
+    def zr_runner(self, cxt_channels: int = 0) -> "ConvRunner":
+        """The first SeqConv stage's fused z|r conv (context hoisted if cxt_channels > 0)."""
+        return self._ctx_runners(cxt_channels)[0][0] if cxt_channels else self.runners()[0][0]
+
     def zr_flops(self, m: int, cxt_channels: int = 0) -> float:
         """Algorithmic FLOPs of one z|r launch over m pixels (with the context hoisted if
         cxt_channels > 0)."""
-        runners = self._ctx_runners(cxt_channels)[0][0] if cxt_channels else self.runners()[0][0]
-        return runners.flops(m)
+        return self.zr_runner(cxt_channels).flops(m)
 
     def forward(self, h: Tensor, x: Tensor) -> Tensor:
         n, hc, hh, ww = h.shape
