@@ -241,8 +241,14 @@ def main():
     dec = dec.to(dev).eval()
     inp = make_inputs(args.batch, args.size, seed=rank, device=dev)
 
-    timers = {name: (KernelTimer() if args.graph else EventTimer())
-              for name in ("gru_zr", "corr_lookup", "pose_flow", "corr_pyramid")}
+    # launches per step of each bracketed kernel: 2 SeqConv stages per iteration for the z|r
+    # conv, one lookup / pose-flow per iteration, one pyramid per forward.  Eager runs bracket
+    # one launch per step (stride = per-step launches + 1 walks the sampled position through
+    # the iterations), so the timing events cost ≈ 2 queue packets per step, not 2 per launch.
+    per_step = {"gru_zr": 2 * args.iters, "corr_lookup": args.iters, "pose_flow": args.iters,
+                "corr_pyramid": 1}
+    timers = {name: (KernelTimer() if args.graph else EventTimer(stride=n + 1 if n > 1 else 1))
+              for name, n in per_step.items()}
     timer = timers["gru_zr"]
     for t in timers.values():
         t.enabled = False

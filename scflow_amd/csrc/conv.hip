@@ -658,7 +658,9 @@ long long wino_blocks(const scflow_conv_args& a) {
   if (a.kh == 1) return (long long)a.n * (a.h / (128 / a.w));
   return (long long)a.n * (a.h / 4) * (a.w / 32);
 }
-// 64 output channels per workgroup when that still fills every CU twice, else 32
+// 64 output channels per workgroup when that still gives ≥ 1.5 workgroups per CU, else 32
+// (measured per decoder shape at B = 16, tools/conv_bench.py: 3×3 256→192 85 vs 95 µs at 384
+// workgroups; 256→126, 128→64 and the GRU q convs at 256 or fewer prefer 32)
 int wino_nbw(const scflow_conv_args& a, int cus) {
   static int forced = -1;
   if (forced < 0) {
@@ -667,7 +669,7 @@ int wino_nbw(const scflow_conv_args& a, int cus) {
   }
   if (forced == 1 || forced == 2) return forced;
   if (a.cout <= 32) return 1;
-  return wino_blocks(a) * (round_up(a.cout, 64) / 64) >= 2LL * cus ? 2 : 1;
+  return 2 * wino_blocks(a) * (round_up(a.cout, 64) / 64) >= 3LL * cus ? 2 : 1;
 }
 bool wino_enabled(int kh) {
   static int on3 = -1, on5 = -1;

@@ -60,13 +60,22 @@ class EventTimer:
     """Eager-mode alternative: torch (HIP) timing events on the current stream — queue packets
     rather than kernel dispatches, so cheaper, but not usable inside a hipGraph capture."""
 
-    def __init__(self) -> None:
+    def __init__(self, stride: int = 1) -> None:
+        """``stride`` > 1 brackets only every stride-th launch (an event pair costs a few µs of
+        queue time between dependent kernels); with stride = launches per step + 1 the bracketed
+        launch moves one position every step, so K steps sample K different launch positions."""
         self.pairs = []
         self._start = None
         self.enabled = True
+        self.stride = max(1, stride)
+        self._calls = 0
 
     def __call__(self, start: bool) -> None:
         if not self.enabled:
+            return
+        if start:
+            self._calls += 1
+        if (self._calls - 1) % self.stride:
             return
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
@@ -77,6 +86,7 @@ class EventTimer:
 
     def reset(self) -> None:
         self.pairs = []
+        self._calls = 0
 
     def mean_ms(self) -> float:
         if not self.pairs:
