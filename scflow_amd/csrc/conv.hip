@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
   const int hc = P.hc, ow = P.ow;
   float* As = smem;                             // [hr*hc][LDA]
   float* Bs = smem + (size_t)P.hr * hc * LDA;   // [TAPS][BN][LDA]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
   const int tiles_per_img = P.oh / P.tr;
   const int img = blockIdx.x / tiles_per_img;
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void conv_smallcin_kernel(scflow_conv_args a, 
     if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) v = a.src0[((size_t)(img * a.h + iy) * a.w + ix) * a.s0 + c];
     halo[row][col][c] = v;
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int G = npad / 64;               // channel groups (1, 2 or 4)
   const int grp = wave % G;
   const int pshare = 4 / G;              // waves per channel group
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void conv_smallcin_mfma_kernel(scflow_conv_arg
     if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) v = a.src0[((size_t)(img * a.h + iy) * a.w + ix) * a.s0 + c];
     halo[i] = v;
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
   // B fragments: k = 2·kp + hh, column = wn·NBW·32 + nb·32 + li
   float bw[NBW][KP];
@@ -486,6 +486,16 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
       ra[j] = v;
     }
   };
+  // all weights in LDS once, [tap][ci][o] (packed global layout is [o][tap][ci]): the compute
+  // loop reads them as wave-wide broadcasts instead of per-lane global loads
+  float* wl = halo + (size_t)(tr + KH - 1) * hcols * THIN_LD;
+  {
+    const int nw = KH * KW * cin * COUT;
+    for (int i = threadIdx.x; i < nw; i += 256) {
+      const int o = i % COUT, k = i / COUT;  // k = tap·cin + ci
+      wl[i] = a.weight[(size_t)o * KH * KW * cin + k];
+    }
+  }
   float acc[COUT];
 #pragma unroll
   for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
@@ -508,13 +518,18 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
           const float* hp = halo + ((py + ty) * hcols + px + tx) * THIN_LD + c0;
           const floatx4 v0 = *(const floatx4*)(hp);
           const floatx4 v1 = *(const floatx4*)(hp + 4);
-          const float* wp = a.weight + (size_t)(ty * KW + tx) * cin + cc + c0;
+          float w[8 * COUT];  // [ci][o] for this tap's 8 channels
+          const float* wp = wl + ((size_t)(ty * KW + tx) * cin + cc + c0) * COUT;
 #pragma unroll
-          for (int o = 0; o < COUT; ++o) {
-            const float* w = wp + (size_t)o * KH * KW * cin;
-            acc[o] += v0[0] * w[0] + v0[1] * w[1] + v0[2] * w[2] + v0[3] * w[3] +
-                      v1[0] * w[4] + v1[1] * w[5] + v1[2] * w[6] + v1[3] * w[7];
+          for (int i = 0; i < 2 * COUT; ++i) {
+            const floatx4 t = *(const floatx4*)(wp + 4 * i);
+            w[4 * i] = t[0]; w[4 * i + 1] = t[1]; w[4 * i + 2] = t[2]; w[4 * i + 3] = t[3];
           }
+#pragma unroll
+          for (int o = 0; o < COUT; ++o)
+            acc[o] += v0[0] * w[0 * COUT + o] + v0[1] * w[1 * COUT + o] + v0[2] * w[2 * COUT + o] +
+                      v0[3] * w[3 * COUT + o] + v1[0] * w[4 * COUT + o] + v1[1] * w[5 * COUT + o] +
+                      v1[2] * w[6 * COUT + o] + v1[3] * w[7 * COUT + o];
         }
     }
   }
@@ -1010,6 +1025,10 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
   if (a.cout == CO && a.kh == KH_ && a.kw == KW_) {                                             \
     size_t lds = sizeof(float) * (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * THIN_LD;           \
     if (lds < sizeof(float) * 4 * CO * 64) lds = sizeof(float) * 4 * CO * 64;                    \
+    lds += sizeof(float) * (size_t)KH_ * KW_ * (a.c0 + a.c1) * CO; /* weights */                \
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)conv_thin_kernel<CO, KH_, KW_>,  \
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                                                  160 * 1024);                                   \
     conv_thin_kernel<CO, KH_, KW_><<<blocks, 256, lds, st>>>(a, g.oh, g.ow);                    \
     return scflow_launch_status();                                                              \
   }

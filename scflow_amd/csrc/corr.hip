@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(const float* __restri
                                                            int tiles_q, float sqrt_c) {
   __shared__ float As[TK][TM];
   __shared__ float Bs[TK][TN];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
   const int n = blockIdx.y;
   const int tp = blockIdx.x / tiles_q, tq = blockIdx.x % tiles_q;

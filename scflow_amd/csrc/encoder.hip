@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
   const int hc = P.hc, ow = P.ow, tc = P.tc;
   float* As = smem;                            // [hr*hc][ELDA]
   float* Bs = smem + (size_t)P.hr * hc * ELDA;  // [TAPS][EBN][ELDA]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
   const int tiles_x = ow / tc;
   const int tiles_per_img = (P.oh / P.tr) * tiles_x;
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void enc_stem_kernel(const float* __restrict__
     if (iy >= 0 && iy < h && ix >= 0 && ix < w) v = img_in[(((size_t)img * CIN + c) * h + iy) * w + ix];
     halo[row][col][c] = v;
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int G = npad / 64;
   const int grp = wave % G;
   const int pw_ = 32 / (4 / G);

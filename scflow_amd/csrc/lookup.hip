@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void corr_lookup_lds_kernel(
   constexpr int SLOTS = 4 * LK_PPW;  // pixels per workgroup
   __shared__ float win[SLOTS][LK_MAXL][WIN][WIN];
   __shared__ float crd[SLOTS][LK_MAXL][2][D];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int slot = wave * LK_PPW + lane / LK_GL;  // this lane's pixel slot
   const int gl = lane % LK_GL;                     // lane within the pixel's group
   const int P = H * W;

@@ -68,7 +68,7 @@ constexpr int PH_BATCH = SCFLOW_PH_BATCH;  // K chunks whose loads a wave issues
 
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
   __shared__ float red[PH_WAVES / 2][32][33];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 31, hh = lane >> 5;
   const int M = a.n * a.oh * a.ow;
   const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
@@ -223,7 +223,7 @@ template <int FC_RT>  // row tiles of 16 per pass
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
   constexpr int FB = FC_RT == 1 ? PH_BATCH : 2;  // K groups whose loads are issued together
   __shared__ float red[PH_WAVES / 2][FC_RT][64][5];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, kq = lane >> 4;
   const int i0 = blockIdx.x * 16;
   // weight row of this lane's neuron

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
   const scflow_wgrad_args& a = P.a;
   float* Ds = smem;                 // [cp][64] dY chunk, then [hr*hc][64] input halo; ×2 (float4)
   float* Xs = smem + P.cp * WT;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, hh = lane >> 5, wco = wave & 1, wci = wave >> 1;
   const int co_t = blockIdx.x % P.co_tiles, ci_t = blockIdx.x / P.co_tiles;
   const int co0 = co_t * WT, ci0 = ci_t * WT;
