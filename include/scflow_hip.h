@@ -175,6 +175,12 @@ int scflow_ph_conv(const float* src0, int c0, int s0, const float* src1, int c1,
                    const float* scale, const float* shift, const float* packed, const float* bias,
                    float* out, int n, int h, int w, int cout, int kh, int kw, int stride, int pad,
                    void* stream);
+/* scflow_ph_conv with the K chunks split over ksplit workgroup slices: out = ksplit partial slabs
+ *   [ksplit][n·oh·ow][cout] (bias must be NULL), summed by scflow_ph_gn_reduce. */
+int scflow_ph_conv_split(const float* src0, int c0, int s0, const float* src1, int c1, int s1,
+                         const float* scale, const float* shift, const float* packed,
+                         const float* bias, float* out, int n, int h, int w, int cout, int kh,
+                         int kw, int stride, int pad, int ksplit, void* stream);
 int scflow_ph_gn_stats(const float* x, int n, int hw, int c, int groups, const float* gamma,
                        const float* beta, float eps, float* scale, float* shift, void* stream);
 /* scflow_ph_gn_reduce: y = Σ_z parts[z] (nsplit slabs, split_stride floats apart; y written when
@@ -185,6 +191,14 @@ int scflow_ph_gn_reduce(const float* parts, int nsplit, long long split_stride, 
 int scflow_ph_fc_permute(const float* W, float* Wp, int n, int c, int hw, void* stream);
 int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias, float* y,
                  int n, int relu, int gn_c, const float* scale, const float* shift, void* stream);
+/* scflow_ph_fc with K split over ksplit workgroup slices (m ≤ 32): parts [ksplit][m][n] = partial
+ *   x·Wᵀ sums (no bias / activation); gn_c/scale/shift as in scflow_ph_fc.
+ * scflow_ph_fc_sum: y [m][n] = act(x' · Wᵀ + b) with x' = relu(Σ_z parts[z] + xbias), the input
+ *   being the previous layer's split partial sums [nsplit][m][k] (its bias xbias, then ReLU). */
+int scflow_ph_fc_split(const float* x, int ldx, int m, int k, const float* W, float* parts, int n,
+                       int ksplit, int gn_c, const float* scale, const float* shift, void* stream);
+int scflow_ph_fc_sum(const float* parts, int nsplit, int m, int k, const float* xbias,
+                     const float* W, const float* bias, float* y, int n, int relu, void* stream);
 int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* br, int rch,
                     const float* Wt, const float* bt, const long long* label, int num_class,
                     float* drot, float* dt, void* stream);

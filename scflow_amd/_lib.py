@@ -118,6 +118,13 @@ SIGNATURES = {
     "scflow_ph_conv_pack": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
     "scflow_ph_conv": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_ph_conv_split": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_int, c_vp]),
+    "scflow_ph_fc_split": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp,
+                                   c_vp, c_vp]),
+    "scflow_ph_fc_sum": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
+                                 c_vp]),
     "scflow_ph_gn_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_vp,
                                    c_vp]),
     "scflow_ph_gn_reduce": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp,

@@ -36,8 +36,9 @@ struct PhConvArgs {
   const float* shift;   // [n][c0+c1]
   const float* weight;  // packed [cout][taps][cinp], cinp = roundup(c0+c1, 16)
   const float* bias;    // [cout] or NULL
-  float* out;           // [n][oh][ow][cout]
+  float* out;           // [n][oh][ow][cout], or [ksplit][n][oh][ow][cout] partial slabs
   int n, h, w, oh, ow, cout, kh, kw, stride, pad, cinp;
+  int ksplit;           // K chunks split over grid.z (partial slab z = out + z·M·cout)
 };
 
 __device__ __forceinline__ floatx4 ph_load_a(const PhConvArgs& a, int img, int iy, int ix, int c) {
@@ -82,11 +83,14 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
   const bool nvalid = col < a.cout;
   const int taps = a.kh * a.kw;
   const int cchunks = a.cinp / PH_K;
-  const int nchunks = taps * cchunks;
+  const int nall = taps * cchunks;
+  // this workgroup's K range (grid.z splits the chunks; partial slab z)
+  const int klo = (int)((long long)nall * blockIdx.z / a.ksplit);
+  const int nchunks = (int)((long long)nall * (blockIdx.z + 1) / a.ksplit);
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (int base = wave; base < nchunks; base += PH_WAVES * PH_BATCH) {
+  for (int base = klo + wave; base < nchunks; base += PH_WAVES * PH_BATCH) {
     floatx4 A0[PH_BATCH], A1[PH_BATCH], B0[PH_BATCH], B1[PH_BATCH];
 #pragma unroll
     for (int c = 0; c < PH_BATCH; ++c) {  // issue every load of the batch first
@@ -131,10 +135,11 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
   }
   if (wave == 0 && nvalid) {
     const float b = a.bias ? a.bias[col] : 0.f;
+    float* out = a.out + (size_t)blockIdx.z * M * a.cout;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      if (mm < M) a.out[(size_t)mm * a.cout + col] = acc[r] + b;
+      if (mm < M) out[(size_t)mm * a.cout + col] = acc[r] + b;
     }
   }
 }
@@ -217,6 +222,9 @@ struct FcArgs {
   const float* W; const float* bias; float* y; int n; int relu;
   int gn_c; const float* scale; const float* shift;
   const float* Wt; const float* bt; const long long* label; int num_class; int rch; float* dt;
+  int ksplit;                            // >1: grid.y splits K, y + z·m·n gets partial sums
+  int xsplit; long long xstride;         // >0: X = relu(Σ_z x[z·xstride] + xbias) (split producer)
+  const float* xbias;
 };
 
 template <int FC_RT>  // row tiles of 16 per pass
@@ -237,12 +245,15 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
   } else if (ni < f.n) {
     wrow = f.W + (size_t)ni * f.k;
   }
-  const int groups = f.k / 16;
+  const int gall = f.k / 16;
+  const int glo = f.ksplit > 1 ? (int)((long long)gall * blockIdx.y / f.ksplit) : 0;
+  const int groups = f.ksplit > 1 ? (int)((long long)gall * (blockIdx.y + 1) / f.ksplit) : gall;
+  float* yout = f.y + (f.ksplit > 1 ? (size_t)blockIdx.y * f.m * f.n : 0);
   for (int r0 = 0; r0 < f.m; r0 += 16 * FC_RT) {
     floatx4 acc[FC_RT];
 #pragma unroll
     for (int t = 0; t < FC_RT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-    for (int base = wave; base < groups; base += PH_WAVES * FB) {
+    for (int base = glo + wave; base < groups; base += PH_WAVES * FB) {
       floatx4 wv[FB], xv[FB][FC_RT];
 #pragma unroll
       for (int c = 0; c < FB; ++c) {
@@ -256,6 +267,12 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
           floatx4 v = z;
           if (g < groups && row < f.m) {
             v = *(const floatx4*)(f.x + (size_t)row * f.ldx + kk);
+            if (f.xsplit > 0) {
+              for (int z = 1; z < f.xsplit; ++z) v += *(const floatx4*)(f.x + z * f.xstride + (size_t)row * f.ldx + kk);
+              const floatx4 xb = *(const floatx4*)(f.xbias + kk);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] + xb[e], 0.f);
+            }
             if (f.gn_c > 0) {
               const int ch = kk % f.gn_c;
               const floatx4 sc = *(const floatx4*)(f.scale + (size_t)row * f.gn_c + ch);
@@ -309,9 +326,11 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
             else if (i < f.rch + 3)
               f.dt[(size_t)row * 3 + (i - f.rch)] = v + f.bt[cls * 3 + (i - f.rch)];
           } else if (i < f.n) {
-            v += f.bias ? f.bias[i] : 0.f;
-            if (f.relu) v = fmaxf(v, 0.f);
-            f.y[(size_t)row * f.n + i] = v;
+            if (f.ksplit <= 1) {
+              v += f.bias ? f.bias[i] : 0.f;
+              if (f.relu) v = fmaxf(v, 0.f);
+            }
+            yout[(size_t)row * f.n + i] = v;
           }
         }
       }
@@ -363,8 +382,18 @@ SCFLOW_API int scflow_ph_conv(const float* src0, int c0, int s0, const float* sr
                               const float* scale, const float* shift, const float* packed,
                               const float* bias, float* out, int n, int h, int w, int cout, int kh,
                               int kw, int stride, int pad, void* stream) {
+  return scflow_ph_conv_split(src0, c0, s0, src1, c1, s1, scale, shift, packed, bias, out, n, h, w,
+                              cout, kh, kw, stride, pad, 1, stream);
+}
+
+SCFLOW_API int scflow_ph_conv_split(const float* src0, int c0, int s0, const float* src1, int c1,
+                                    int s1, const float* scale, const float* shift,
+                                    const float* packed, const float* bias, float* out, int n, int h,
+                                    int w, int cout, int kh, int kw, int stride, int pad, int ksplit,
+                                    void* stream) {
   if (!src0 || !packed || !out || n <= 0 || h <= 0 || w <= 0 || cout <= 0 || c0 <= 0 || c1 < 0 ||
-      (c1 > 0 && !src1) || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 || (scale && !shift))
+      (c1 > 0 && !src1) || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 || (scale && !shift) ||
+      ksplit <= 0 || (ksplit > 1 && bias))
     return SCFLOW_EINVAL;
   if ((c0 & 3) || (c1 & 3) || (s0 & 3) || (c1 && (s1 & 3)) || !aligned16(src0) ||
       (c1 && !aligned16(src1)) || !aligned16(packed))
@@ -380,8 +409,9 @@ SCFLOW_API int scflow_ph_conv(const float* src0, int c0, int s0, const float* sr
   if (a.oh <= 0 || a.ow <= 0) return SCFLOW_EINVAL;
   a.cout = cout; a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad;
   a.cinp = (c0 + c1 + PH_K - 1) / PH_K * PH_K;
+  a.ksplit = ksplit;
   const long long M = (long long)n * a.oh * a.ow;
-  dim3 grid((unsigned)((M + 31) / 32), (unsigned)((cout + 31) / 32));
+  dim3 grid((unsigned)((M + 31) / 32), (unsigned)((cout + 31) / 32), (unsigned)ksplit);
   ph_conv_kernel<<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(a);
   return scflow_launch_status();
 }
@@ -426,6 +456,40 @@ SCFLOW_API int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* 
   FcArgs f{};
   f.x = x; f.ldx = ldx; f.m = m; f.k = k; f.W = W; f.bias = bias; f.y = y; f.n = n; f.relu = relu;
   f.gn_c = gn_c; f.scale = scale; f.shift = shift;
+  if (m <= 16)
+    ph_fc_kernel<1><<<(n + 15) / 16, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  else
+    ph_fc_kernel<2><<<(n + 15) / 16, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_fc_split(const float* x, int ldx, int m, int k, const float* W,
+                                  float* parts, int n, int ksplit, int gn_c, const float* scale,
+                                  const float* shift, void* stream) {
+  if (!x || !W || !parts || m <= 0 || m > 32 || k <= 0 || n <= 0 || (k & 15) || (ldx & 3) ||
+      ksplit <= 0 || ksplit > k / 16 || !aligned16(W) || !aligned16(x) ||
+      (gn_c > 0 && (!scale || !shift || (gn_c & 3))))
+    return SCFLOW_EINVAL;
+  FcArgs f{};
+  f.x = x; f.ldx = ldx; f.m = m; f.k = k; f.W = W; f.y = parts; f.n = n;
+  f.gn_c = gn_c; f.scale = scale; f.shift = shift; f.ksplit = ksplit;
+  dim3 grid((unsigned)((n + 15) / 16), (unsigned)ksplit);
+  if (m <= 16)
+    ph_fc_kernel<1><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  else
+    ph_fc_kernel<2><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_fc_sum(const float* parts, int nsplit, int m, int k, const float* xbias,
+                                const float* W, const float* bias, float* y, int n, int relu,
+                                void* stream) {
+  if (!parts || !xbias || !W || !y || nsplit <= 0 || m <= 0 || k <= 0 || n <= 0 || (k & 15) ||
+      !aligned16(W) || !aligned16(parts) || !aligned16(xbias))
+    return SCFLOW_EINVAL;
+  FcArgs f{};
+  f.x = parts; f.ldx = k; f.m = m; f.k = k; f.W = W; f.bias = bias; f.y = y; f.n = n; f.relu = relu;
+  f.xsplit = nsplit; f.xstride = (long long)m * k; f.xbias = xbias;
   if (m <= 16)
     ph_fc_kernel<1><<<(n + 15) / 16, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
   else

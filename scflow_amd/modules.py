@@ -151,6 +151,31 @@ class ConvRunner:
             self._key = key
         return self._packed, self._bias
 
+    def bind(self, src0: Chan, out: Optional[Chan], n: int, h: int, w: int,
+             src1: Optional[Chan] = None, epilogue: int = EPI_PLAIN, gate: Optional[Chan] = None,
+             rh: Optional[Chan] = None, hid: Optional[Chan] = None,
+             bias_map: Optional[Chan] = None) -> "ops.BoundLaunch":
+        """``run``'s launch with its arguments fixed (weights packed now, buffers persistent):
+        calling the result launches it on the current stream.  Re-bind after the weights or
+        buffers change."""
+        c1 = 0 if src1 is None else src1.c
+        if src0.c + c1 != self.cin:
+            raise ValueError(f"conv expects {self.cin} input channels, got {src0.c}+{c1}")
+        shape = (n, h, w, src0.c, c1)
+        if ConvRunner.force_bk:
+            self._bk_shape, self._bk = shape, ConvRunner.force_bk
+        if getattr(self, "_bk_shape", None) != shape:
+            self._bk = ops.conv_pick_bk(n, h, w, src0.c, c1, self.cout, self.kh, self.kw, self.ph,
+                                        self.pw, self.stride)
+            self._bk_shape = shape
+        packed, bias = self.packed(src0.c, c1, w, self._bk)
+        args = ops.conv2d_args(src0, packed, bias, n, h, w, self.cout, self.kh, self.kw, self.ph,
+                               self.pw, self.act, out=out, src1=src1, epilogue=epilogue, gate=gate,
+                               rh=rh, hid=hid, stride=self.stride, bias_map=bias_map, bk=self._bk)
+        bl = ops.BoundLaunch(_lib.load().scflow_conv2d, args, src0.buf.device.index, "scflow_conv2d")
+        bl.keep = (packed, bias)  # the launch holds the packed weights alive
+        return bl
+
     def run(self, src0: Chan, out: Optional[Chan], n: int, h: int, w: int,
             src1: Optional[Chan] = None, epilogue: int = EPI_PLAIN, gate: Optional[Chan] = None,
             rh: Optional[Chan] = None, hid: Optional[Chan] = None,
@@ -288,6 +313,17 @@ class MotionEncoder(nn.Module):
         return ops.chan_to_nchw(Chan.whole(out), n, h, w)
 
 
+def bind_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int, w: int,
+               scratch: List[Tensor]) -> List["ops.BoundLaunch"]:
+    """run_chain's launches bound once (see ConvRunner.bind)."""
+    out_l, cur = [], src
+    for i, m in enumerate(layers):
+        out = dst if i == len(layers) - 1 else Chan.whole(scratch[i])
+        out_l.append(ConvRunner.of(m.conv, m.act_type).bind(cur, out, n, h, w))
+        cur = out
+    return out_l
+
+
 def run_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int, w: int,
               scratch: Optional[List[Tensor]] = None) -> None:
     """Run a Sequential of stride-1 ConvModules channels-last; the last one writes ``dst``."""
@@ -368,6 +404,45 @@ class ConvGRU(nn.Module):
         for i, (_, _, rc) in enumerate(runners):
             rc.run(cxt, Chan(bm, i * 3 * hc, 3 * hc), n, h, w)
         return bm
+
+    def bind_step(self, hx: Chan, z: Chan, rh: Chan, n: int, h: int, w: int,
+                  ctx_map: Optional[Tensor] = None, cxt_channels: int = 0):
+        """``step``'s launches bound once; returns step(hooks=None) replaying them."""
+        hc = self.h_channels
+        hid = Chan(hx.buf, hx.off, hc)
+        x = Chan(hx.buf, hx.off + hc, hx.c - hc)
+        launches = []
+        if ctx_map is not None:
+            mot = Chan(hx.buf, hx.off + hc + cxt_channels, hx.c - hc - cxt_channels)
+            for i, (rzr, rq, _) in enumerate(self._ctx_runners(cxt_channels)):
+                bzr = Chan(ctx_map, i * 3 * hc, 2 * hc)
+                bq = Chan(ctx_map, i * 3 * hc + 2 * hc, hc)
+                launches.append((rzr.bind(hid, None, n, h, w, src1=mot, epilogue=EPI_GRU_ZR, gate=z,
+                                          rh=rh, hid=hid, bias_map=bzr),
+                                 rq.bind(rh, None, n, h, w, src1=mot, epilogue=EPI_GRU_Q, gate=z,
+                                         hid=hid, bias_map=bq)))
+        else:
+            for rzr, rq in self.runners():
+                launches.append((rzr.bind(hx, None, n, h, w, epilogue=EPI_GRU_ZR, gate=z, rh=rh,
+                                          hid=hid),
+                                 rq.bind(rh, None, n, h, w, src1=x, epilogue=EPI_GRU_Q, gate=z,
+                                         hid=hid)))
+
+        def step(hooks=None) -> None:
+            hzr = hooks.get("gru_zr") if hooks else None
+            hq = hooks.get("gru_q") if hooks else None
+            for lzr, lq in launches:
+                if hzr:
+                    hzr(True)
+                lzr()
+                if hzr:
+                    hzr(False)
+                if hq:
+                    hq(True)
+                lq()
+                if hq:
+                    hq(False)
+        return step
 
     def step(self, hx: Chan, z: Chan, rh: Chan, n: int, h: int, w: int, hooks=None,
              ctx_map: Optional[Tensor] = None, cxt_channels: int = 0) -> None:
@@ -526,7 +601,7 @@ class MultiClassPoseHead(nn.Module):
         return self._packed, self._fc1_perm
 
     def _conv_mfma(self, i: int, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                   scale: Optional[Tensor], shift: Optional[Tensor]):
+                   scale: Optional[Tensor], shift: Optional[Tensor], keep: Optional[list] = None):
         """conv_layers[i] on the MFMA halo conv (scflow_enc_conv; the previous GroupNorm + ReLU
         applied on load) with a K split over grid.z so that ≥ 512 workgroups run, when the shape
         allows it: returns (partial slabs [ksplit·n·oh·ow, cout], ksplit) or None."""
@@ -552,13 +627,26 @@ class MultiClassPoseHead(nn.Module):
         nst = (src0.c + c1) // 16
         ksplit = max(1, min(nst, -(-512 // tiles)))
         parts = torch.empty(ksplit * n * oh * ow, conv.out_channels, device=src0.buf.device)
+        if keep is not None:
+            keep.append(parts)
         ops.enc_conv(src0, packs[i][1], None, n, h, w, src0.c, conv.out_channels, 3, s, 1, parts,
                      src1=src1, ksplit=ksplit, in_scale=scale, in_shift=shift)
         return parts, ksplit
 
     def forward_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
                     label: Tensor) -> Tuple[Tensor, Tensor]:
-        """Channels-last input cat[src0, src1] of n samples at h×w → (Δrot, Δt).
+        """Channels-last input cat[src0, src1] of n samples at h×w → (Δrot, Δt)."""
+        dev = src0.buf.device
+        x = self.trunk_hip(src0, src1, n, h, w)
+        drot = torch.empty(n, self.rotation_out_channels, device=dev)
+        dt = torch.empty(n, 3, device=dev)
+        self.heads_hip(x, label, drot, dt)
+        return drot, dt
+
+    def trunk_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
+                  ws: Optional[list] = None) -> Tensor:
+        """Convs + FCs of forward_hip → the last FC's output [n, 256].  Every buffer it allocates
+        is appended to ``ws`` (the decoder keeps them alive while replaying these launches).
 
         Each conv runs on the MFMA halo conv with a K split into partial slabs when its shape
         allows (conv1 and conv2 at SCFlow's sizes; summed by the GroupNorm-statistics kernel),
@@ -566,6 +654,12 @@ class MultiClassPoseHead(nn.Module):
         if any(m.norm_type != "GN" or m.act_type != "ReLU" for m in self.conv_layers):
             raise NotImplementedError("HIP pose head: conv + GroupNorm + ReLU layers only")
         dev = src0.buf.device
+        keep = ws if ws is not None else []
+
+        def empty(*shape):
+            t = torch.empty(*shape, device=dev)
+            keep.append(t)
+            return t
         hl, wl = h, w
         for m in self.conv_layers:
             k, st, p = m.conv.kernel_size[0], m.conv.stride[0], m.conv.padding[0]
@@ -578,13 +672,23 @@ class MultiClassPoseHead(nn.Module):
             k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
             oh, ow = (hh + 2 * p - k) // s + 1, (ww + 2 * p - k) // s + 1
             cout = conv.out_channels
-            y = torch.empty(n * oh * ow, cout, device=dev)
-            split = self._conv_mfma(i, cur0, cur1, n, hh, ww, scale, shift)
-            if split is None:
+            y = empty(n * oh * ow, cout)
+            split = self._conv_mfma(i, cur0, cur1, n, hh, ww, scale, shift, keep)
+            if split is None and conv.bias is None:
+                # gather conv with its K split over enough slices to fill the CUs (conv3 at B=16:
+                # 32 output tiles → 8 slices), summed by the GroupNorm-statistics kernel
+                tiles = -(-n * oh * ow // 32) * -(-cout // 32)
+                nk = k * k * -(-(cur0.c + (0 if cur1 is None else cur1.c)) // 16)
+                ks = max(1, min(nk // 16, -(-256 // tiles)))
+                parts = empty(ks * n * oh * ow, cout)
+                ops.ph_conv(cur0, cur1, packs[i], None, n, hh, ww, cout, k, s, p, parts, scale, shift,
+                            ksplit=ks)
+                split = (parts, ks)
+            elif split is None:
                 ops.ph_conv(cur0, cur1, packs[i], None if conv.bias is None else conv.bias.detach(), n,
                             hh, ww, cout, k, s, p, y, scale, shift)
-            scale = torch.empty(n, cout, device=dev)
-            shift = torch.empty(n, cout, device=dev)
+            scale = empty(n, cout)
+            shift = empty(n, cout)
             if split is not None:
                 ops.ph_gn_reduce(split[0], split[1], y, n, oh * ow, cout, m.gn.num_groups,
                                  m.gn.weight.detach(), m.gn.bias.detach(), m.gn.eps, scale, shift)
@@ -595,23 +699,38 @@ class MultiClassPoseHead(nn.Module):
         c = cur0.c
         x = cur0.buf
         k_in = c * hh * ww
+        # FC1 (K = 2048) with K split over 4 slices (64 → 256 workgroups); FC2 sums the slices,
+        # adds FC1's bias and applies its ReLU on load
+        ks1 = 4 if n <= 32 and len(self.fc_layers) >= 2 and (k_in // 16) >= 4 else 1
         for i, fc in enumerate(self.fc_layers):
             lin = fc[0]
-            y = torch.empty(n, lin.out_features, device=dev)
+            if i == 0 and ks1 > 1:
+                y = empty(ks1, n, lin.out_features)
+                ops.ph_fc_split(x, k_in, n, k_in, fc1_w, y, lin.out_features, ks1, gn_c=c, scale=scale,
+                                shift=shift)
+                x = y
+                continue
+            y = empty(n, lin.out_features)
             if i == 0:
                 ops.ph_fc(x, k_in, n, k_in, fc1_w, lin.bias.detach(), y, lin.out_features, True,
                           gn_c=c, scale=scale, shift=shift)
+            elif i == 1 and ks1 > 1:
+                prev = self.fc_layers[0][0]
+                ops.ph_fc_sum(x, ks1, n, prev.out_features, prev.bias.detach(), lin.weight.detach(),
+                              lin.bias.detach(), y, lin.out_features, True)
             else:
                 ops.ph_fc(x, x.shape[1], n, x.shape[1], lin.weight.detach(), lin.bias.detach(), y,
                           lin.out_features, True)
             x = y
-        drot = torch.empty(n, self.rotation_out_channels, device=dev)
-        dt = torch.empty(n, 3, device=dev)
+        return x
+
+    def heads_hip(self, x: Tensor, label: Tensor, drot: Tensor, dt: Tensor) -> None:
+        """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt."""
+        n = x.shape[0]
         ops.ph_heads(x, n, x.shape[1], self.rotation_pred.weight.detach(),
                      self.rotation_pred.bias.detach(), self.rotation_out_channels,
                      self.translation_pred.weight.detach(), self.translation_pred.bias.detach(),
                      label.long(), self.num_class, drot, dt)
-        return drot, dt
 
     def forward(self, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
         """Reference API (NCHW in).  Runs the HIP kernels (inference; no autograd graph)."""

@@ -23,8 +23,66 @@ from ._lib import ScflowError, check
 Tensor = torch.Tensor
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(t: Tensor) -> int:
+    """The current HIP stream of t's device as a raw handle (the C entry points take it)."""
+    if _raw_stream is not None:
+        return _raw_stream(t.device.index)
     return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class BoundCall:
+    """A recorded C-ABI launch: its arguments (device pointers of persistent buffers, sizes)
+    fixed, the stream taken at call time.  See ``binding``."""
+    __slots__ = ("fn", "args", "dev", "name")
+
+    def __init__(self, fn, args, dev: int, name: str) -> None:
+        self.fn, self.args, self.dev, self.name = fn, args, dev, name
+
+    def __call__(self) -> None:
+        rc = self.fn(*self.args, raw_stream(self.dev))
+        if rc:
+            check(rc, self.name)
+
+
+_BINDING: Optional[list] = None
+
+
+class binding:
+    """``with ops.binding(calls):`` — the wrappers below record their launch as a ``BoundCall``
+    into ``calls`` and ALSO run it (so the first pass computes; later passes replay ``calls``,
+    costing one ctypes call per launch instead of the wrapper's Python)."""
+
+    def __init__(self, calls: list) -> None:
+        self.calls = calls
+
+    def __enter__(self):
+        global _BINDING
+        self._prev, _BINDING = _BINDING, self.calls
+        return self.calls
+
+    def __exit__(self, *exc):
+        global _BINDING
+        _BINDING = self._prev
+
+
+def _launch(name: str, dev_tensor: Tensor, *args) -> None:
+    fn = getattr(_lib.load(), name)
+    if _BINDING is not None:
+        bc = BoundCall(fn, args, dev_tensor.device.index, name)
+        _BINDING.append(bc)
+        bc()
+        return
+    check(fn(*args, _stream(dev_tensor)), name)
+
+
+def raw_stream(device_index: int) -> int:
+    """Current HIP stream of a device by index (no Stream object; for per-launch hot paths)."""
+    if _raw_stream is not None:
+        return _raw_stream(device_index)
+    return torch.cuda.current_stream(device_index).cuda_stream
 
 
 def _require(t: Tensor, name: str, dtype=torch.float32, contiguous=True) -> None:
@@ -129,8 +187,8 @@ def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: i
     else:
         res = out.buf
         ptr, olay, ostride = out.ptr, _lib.LAYOUT_NHWC, out.stride
-    check(_lib.load().scflow_corr_lookup(_p(pyr), _p(flow), lay, ptr, olay, ostride, n, h, w,
-                                         num_levels, radius, _stream(flow)), "scflow_corr_lookup")
+    _launch("scflow_corr_lookup", flow,_p(pyr), _p(flow), lay, ptr, olay, ostride, n, h, w,
+                                         num_levels, radius)
     return res
 
 
@@ -171,6 +229,34 @@ def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w
            src1: Optional[Chan] = None, epilogue: int = _lib.EPI_PLAIN, gate: Optional[Chan] = None,
            rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1,
            bias_map: Optional[Chan] = None, bk: int = 16) -> None:
+    a = conv2d_args(src0, packed, bias, n, h, w, cout, kh, kw, ph, pw, act, out, src1, epilogue,
+                    gate, rh, hid, stride, bias_map, bk)
+    _launch("scflow_conv2d", src0.buf,ctypes.byref(a))
+
+
+class BoundLaunch:
+    """A C-ABI launch whose argument struct is built once (pointers of persistent buffers):
+    calling it costs one ctypes call on the caller's current stream.  The decoder binds every
+    convolution of its refinement loop once per forward and replays them every iteration."""
+    __slots__ = ("fn", "args", "ref", "dev", "name", "keep")
+
+    def __init__(self, fn, args, dev: int, name: str) -> None:
+        self.fn, self.args, self.dev, self.name = fn, args, dev, name
+        self.ref = ctypes.byref(args)
+
+    def __call__(self) -> None:
+        rc = self.fn(self.ref, raw_stream(self.dev))
+        if rc:
+            check(rc, self.name)
+
+
+def conv2d_args(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int,
+                cout: int, kh: int, kw: int, ph: int, pw: int, act: Optional[str] = None,
+                out: Optional[Chan] = None, src1: Optional[Chan] = None,
+                epilogue: int = _lib.EPI_PLAIN, gate: Optional[Chan] = None,
+                rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1,
+                bias_map: Optional[Chan] = None, bk: int = 16) -> "_lib.ConvArgs":
+    """The validated scflow_conv_args of one launch (see conv2d)."""
     for nm, ch in (("src0", src0), ("src1", src1), ("out", out), ("gate", gate), ("rh", rh),
                    ("hid", hid), ("bias_map", bias_map)):
         if ch is not None:
@@ -199,7 +285,7 @@ def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w
     if bias_map is not None:
         a.bias_map, a.sbm = bias_map.ptr, bias_map.stride
     a.bk = bk
-    check(_lib.load().scflow_conv2d(ctypes.byref(a), _stream(src0.buf)), "scflow_conv2d")
+    return a
 
 
 # ------------------------------------------------------------------------------- pose
@@ -209,8 +295,7 @@ def lift_points(depth: Tensor, K: Tensor, R: Tensor, t: Tensor) -> Tensor:
         _require(x, nm)
     n, h, w = depth.shape
     pts = torch.empty(n, h, w, 4, device=depth.device, dtype=torch.float32)
-    check(_lib.load().scflow_lift_points(_p(depth), _p(K), _p(R), _p(t), _p(pts), n, h, w,
-                                         _stream(depth)), "scflow_lift_points")
+    _launch("scflow_lift_points", depth,_p(depth), _p(K), _p(R), _p(t), _p(pts), n, h, w)
     return pts
 
 
@@ -222,9 +307,8 @@ def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 
         raise NotImplementedError("only ortho6d delta rotations are on the SCFlow path")
     n = drot.shape[0]
     Ro, to = torch.empty_like(R), torch.empty_like(t)
-    check(_lib.load().scflow_pose_update(_p(drot), _p(dt), _p(R), _p(t), _p(Ro), _p(to), n,
-                                         float(weight), 0 if depth_transform == "exp" else 1,
-                                         _stream(drot)), "scflow_pose_update")
+    _launch("scflow_pose_update", drot,_p(drot), _p(dt), _p(R), _p(t), _p(Ro), _p(to), n,
+                                         float(weight), 0 if depth_transform == "exp" else 1)
     return Ro, to
 
 
@@ -234,8 +318,8 @@ def pose_flow(R: Tensor, t: Tensor, K: Tensor, points: Tensor, invalid_num: floa
         _require(x, nm)
     n, h, w, _ = points.shape
     flow = out if out is not None else torch.empty(n, 2, h, w, device=R.device, dtype=torch.float32)
-    check(_lib.load().scflow_pose_flow(_p(R), _p(t), _p(K), _p(points), _p(flow), n, h, w,
-                                       float(invalid_num), _stream(R)), "scflow_pose_flow")
+    _launch("scflow_pose_flow", R,_p(R), _p(t), _p(K), _p(points), _p(flow), n, h, w,
+                                       float(invalid_num))
     return flow
 
 
@@ -246,10 +330,9 @@ def pose_update_flow(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, 
                   ("R_out", R_out), ("t_out", t_out), ("flow_out", flow_out)):
         _require(x, nm)
     n, h, w, _ = points.shape
-    check(_lib.load().scflow_pose_update_flow(
+    _launch("scflow_pose_update_flow", drot,
         _p(drot), _p(dt), _p(R), _p(t), _p(K), _p(points), _p(R_out), _p(t_out), _p(flow_out), n, h,
-        w, float(weight), 0 if depth_transform == "exp" else 1, float(invalid_num), _stream(drot)),
-        "scflow_pose_update_flow")
+        w, float(weight), 0 if depth_transform == "exp" else 1, float(invalid_num))
 
 
 # ------------------------------------------------------------------------------- resampling
@@ -257,19 +340,17 @@ def flow_downsample(flow: Tensor, out0: Chan, h: int, w: int, value_scale: float
                     out1: Optional[Chan] = None) -> None:
     _require(flow, "flow")
     n, _, H, W = flow.shape
-    check(_lib.load().scflow_flow_downsample(
+    _launch("scflow_flow_downsample", flow,
         _p(flow), out0.ptr, out0.stride, None if out1 is None else out1.ptr,
-        0 if out1 is None else out1.stride, n, H, W, h, w, float(value_scale), _stream(flow)),
-        "scflow_flow_downsample")
+        0 if out1 is None else out1.stride, n, H, W, h, w, float(value_scale))
 
 
 def flow_upsample(lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], n: int, h: int,
                   w: int, H: int, W: int, value_scale: float, flow_out: Tensor,
                   mask_out: Optional[Tensor]) -> None:
     _require(lr, "lr flow")
-    check(_lib.load().scflow_flow_upsample(_p(lr), _p(delta), _p(mask), _p(flow_out), _p(mask_out),
-                                           n, h, w, H, W, float(value_scale), _stream(lr)),
-          "scflow_flow_upsample")
+    _launch("scflow_flow_upsample", lr,_p(lr), _p(delta), _p(mask), _p(flow_out), _p(mask_out),
+                                           n, h, w, H, W, float(value_scale))
 
 
 # ------------------------------------------------------------------------------- layout
@@ -280,16 +361,16 @@ def nchw_into(x: Tensor, dst: Chan) -> None:
     if c != dst.c:
         raise ValueError(f"channel mismatch {c} vs {dst.c}")
     st = dst.stride
-    check(_lib.load().scflow_transpose(_p(x), dst.ptr, n, c, h * w, c * h * w, h * w,
-                                       h * w * st, st, _stream(x)), "scflow_transpose")
+    _launch("scflow_transpose", x,_p(x), dst.ptr, n, c, h * w, c * h * w, h * w,
+                                       h * w * st, st)
 
 
 def chan_to_nchw(src: Chan, n: int, h: int, w: int, out: Optional[Tensor] = None) -> Tensor:
     res = out if out is not None else torch.empty(n, src.c, h, w, device=src.buf.device,
                                                    dtype=torch.float32)
     st = src.stride
-    check(_lib.load().scflow_transpose(src.ptr, _p(res), n, h * w, src.c, h * w * st, st,
-                                       src.c * h * w, h * w, _stream(src.buf)), "scflow_transpose")
+    _launch("scflow_transpose", src.buf,src.ptr, _p(res), n, h * w, src.c, h * w * st, st,
+                                       src.c * h * w, h * w)
     return res
 
 
@@ -307,26 +388,25 @@ def ph_conv_pack(weight: Tensor) -> Tensor:
 
 def ph_conv(src0: Chan, src1: Optional[Chan], packed: Tensor, bias: Optional[Tensor], n: int, h: int,
             w: int, cout: int, k: int, stride: int, pad: int, out: Tensor,
-            scale: Optional[Tensor] = None, shift: Optional[Tensor] = None) -> None:
-    check(_lib.load().scflow_ph_conv(
+            scale: Optional[Tensor] = None, shift: Optional[Tensor] = None, ksplit: int = 1) -> None:
+    """ksplit > 1: ``out`` holds ksplit partial slabs [ksplit, n·oh·ow, cout] (bias None)."""
+    _launch("scflow_ph_conv_split", out,
         src0.ptr, src0.c, src0.stride, None if src1 is None else src1.ptr,
         0 if src1 is None else src1.c, 0 if src1 is None else src1.stride, _p(scale), _p(shift),
-        _p(packed), _p(bias), _p(out), n, h, w, cout, k, k, stride, pad, _stream(out)),
-        "scflow_ph_conv")
+        _p(packed), _p(bias), _p(out), n, h, w, cout, k, k, stride, pad, ksplit)
 
 
 def ph_gn_stats(x: Tensor, n: int, hw: int, c: int, groups: int, gamma: Tensor, beta: Tensor,
                 eps: float, scale: Tensor, shift: Tensor) -> None:
-    check(_lib.load().scflow_ph_gn_stats(_p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps),
-                                         _p(scale), _p(shift), _stream(x)), "scflow_ph_gn_stats")
+    _launch("scflow_ph_gn_stats", x,_p(x), n, hw, c, groups, _p(gamma), _p(beta), float(eps),
+                                         _p(scale), _p(shift))
 
 
 def ph_gn_reduce(parts: Tensor, nsplit: int, y: Tensor, n: int, hw: int, c: int, groups: int,
                  gamma: Tensor, beta: Tensor, eps: float, scale: Tensor, shift: Tensor) -> None:
     """y = sum of the nsplit partial slabs of ``parts`` [nsplit, n·hw, c]; GN scale/shift of y."""
-    check(_lib.load().scflow_ph_gn_reduce(_p(parts), nsplit, n * hw * c, _p(y), n, hw, c, groups,
-                                          _p(gamma), _p(beta), float(eps), _p(scale), _p(shift),
-                                          _stream(parts)), "scflow_ph_gn_reduce")
+    _launch("scflow_ph_gn_reduce", parts,_p(parts), nsplit, n * hw * c, _p(y), n, hw, c, groups,
+                                          _p(gamma), _p(beta), float(eps), _p(scale), _p(shift))
 
 
 def ph_fc_permute(W: Tensor, c: int, hw: int) -> Tensor:
@@ -334,24 +414,37 @@ def ph_fc_permute(W: Tensor, c: int, hw: int) -> Tensor:
     _require(W, "fc weight", contiguous=False)
     W = W.detach().contiguous().float()
     Wp = torch.empty_like(W)
-    check(_lib.load().scflow_ph_fc_permute(_p(W), _p(Wp), W.shape[0], c, hw, _stream(W)),
-          "scflow_ph_fc_permute")
+    _launch("scflow_ph_fc_permute", W,_p(W), _p(Wp), W.shape[0], c, hw)
     return Wp
 
 
 def ph_fc(x: Tensor, ldx: int, m: int, k: int, W: Tensor, bias: Optional[Tensor], y: Tensor, n: int,
           relu: bool, gn_c: int = 0, scale: Optional[Tensor] = None,
           shift: Optional[Tensor] = None) -> None:
-    check(_lib.load().scflow_ph_fc(_p(x), ldx, m, k, _p(W), _p(bias), _p(y), n, int(relu), gn_c,
-                                   _p(scale), _p(shift), _stream(x)), "scflow_ph_fc")
+    _launch("scflow_ph_fc", x,_p(x), ldx, m, k, _p(W), _p(bias), _p(y), n, int(relu), gn_c,
+                                   _p(scale), _p(shift))
+
+
+def ph_fc_split(x: Tensor, ldx: int, m: int, k: int, W: Tensor, parts: Tensor, n: int, ksplit: int,
+                gn_c: int = 0, scale: Optional[Tensor] = None, shift: Optional[Tensor] = None) -> None:
+    """parts [ksplit, m, n] = K-split partial sums of x·Wᵀ (no bias / activation)."""
+    _launch("scflow_ph_fc_split", x,_p(x), ldx, m, k, _p(W), _p(parts), n, ksplit, gn_c,
+                                         _p(scale), _p(shift))
+
+
+def ph_fc_sum(parts: Tensor, nsplit: int, m: int, k: int, xbias: Tensor, W: Tensor,
+              bias: Optional[Tensor], y: Tensor, n: int, relu: bool) -> None:
+    """y = act(relu(Σ parts + xbias)·Wᵀ + bias)."""
+    _launch("scflow_ph_fc_sum", parts,_p(parts), nsplit, m, k, _p(xbias), _p(W), _p(bias), _p(y), n,
+                                       int(relu))
 
 
 def ph_heads(x: Tensor, m: int, k: int, Wr: Tensor, br: Tensor, rch: int, Wt: Tensor, bt: Tensor,
              label: Tensor, num_class: int, drot: Tensor, dt: Tensor) -> None:
     if label.dtype != torch.int64 or label.device != x.device:
         raise TypeError("label must be an int64 tensor on the same device")
-    check(_lib.load().scflow_ph_heads(_p(x), m, k, _p(Wr), _p(br), rch, _p(Wt), _p(bt), _p(label),
-                                      num_class, _p(drot), _p(dt), _stream(x)), "scflow_ph_heads")
+    _launch("scflow_ph_heads", x,_p(x), m, k, _p(Wr), _p(br), rch, _p(Wt), _p(bt), _p(label),
+                                      num_class, _p(drot), _p(dt))
 
 
 # ------------------------------------------------------------------------------- §8(f)-1 encoder
@@ -410,7 +503,7 @@ def enc_conv(src, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int
     a.act = _lib.SCFLOW_ACT[act]
     a.act2 = _lib.SCFLOW_ACT[act2 if act2 is not None else act]
     a.act_split = cout if act_split is None else act_split
-    check(_lib.load().scflow_enc_conv(ctypes.byref(a), _stream(out)), "scflow_enc_conv")
+    _launch("scflow_enc_conv", out,ctypes.byref(a))
 
 
 def enc_stem(img: Tensor, packed: Tensor, bias: Optional[Tensor], cout: int, k: int, stride: int,
@@ -418,9 +511,9 @@ def enc_stem(img: Tensor, packed: Tensor, bias: Optional[Tensor], cout: int, k: 
              out_shift: Optional[Tensor] = None, act: Optional[str] = None) -> None:
     _require(img, "image")
     n, cin, h, w = img.shape
-    check(_lib.load().scflow_enc_stem(_p(img), _p(packed), _p(bias), _p(out_scale), _p(out_shift),
+    _launch("scflow_enc_stem", img,_p(img), _p(packed), _p(bias), _p(out_scale), _p(out_shift),
                                       _p(out), n, cin, h, w, cout, k, k, stride, pad,
-                                      _lib.SCFLOW_ACT[act], _stream(img)), "scflow_enc_stem")
+                                      _lib.SCFLOW_ACT[act])
 
 
 def enc_instance_norm_stats(x: Tensor, n: int, hw: int, c: int, scale: Tensor, shift: Tensor,
@@ -439,9 +532,8 @@ def enc_instance_norm_stats(x: Tensor, n: int, hw: int, c: int, scale: Tensor, s
 def enc_apply(x: Tensor, scale: Tensor, shift: Tensor, out: Tensor, n: int, hw: int, c: int,
               id: Optional[Tensor] = None, id_scale: Optional[Tensor] = None,
               id_shift: Optional[Tensor] = None) -> None:
-    check(_lib.load().scflow_enc_apply(_p(x), _p(scale), _p(shift), _p(id), _p(id_scale),
-                                       _p(id_shift), _p(out), n, hw, c, _stream(x)),
-          "scflow_enc_apply")
+    _launch("scflow_enc_apply", x,_p(x), _p(scale), _p(shift), _p(id), _p(id_scale),
+                                       _p(id_shift), _p(out), n, hw, c)
 
 
 # ------------------------------------------------------------------------------- §8(f)-2 training
@@ -503,7 +595,6 @@ def corr_lookup_backward(dout: Tensor, flow: Tensor, dpyr: Tensor, n: int, h: in
         _require(t, nm)
     lay = {"nchw": _lib.LAYOUT_NCHW, "nhwc": _lib.LAYOUT_NHWC}
     stride = dout.shape[-1] if out_layout == "nhwc" else 0
-    check(_lib.load().scflow_corr_lookup_backward(_p(dout), lay[out_layout], stride, _p(flow),
+    _launch("scflow_corr_lookup_backward", dout,_p(dout), lay[out_layout], stride, _p(flow),
                                                   lay[flow_layout], _p(dpyr), n, h, w, num_levels,
-                                                  radius, _stream(dout)),
-          "scflow_corr_lookup_backward")
+                                                  radius)
