@@ -192,13 +192,20 @@ int scflow_ph_fc_permute(const float* W, float* Wp, int n, int c, int hw, void* 
 int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias, float* y,
                  int n, int relu, int gn_c, const float* scale, const float* shift, void* stream);
 /* scflow_ph_fc with K split over ksplit workgroup slices (m ≤ 32): parts [ksplit][m][n] = partial
- *   x·Wᵀ sums (no bias / activation); gn_c/scale/shift as in scflow_ph_fc.
+ *   x·Wᵀ sums (no bias / activation); gn_c/scale/shift as in scflow_ph_fc, or xsplit > 0: x is
+ *   the previous layer's split partial sums [xsplit][m][ldx] read as relu(Σ + xbias).
  * scflow_ph_fc_sum: y [m][n] = act(x' · Wᵀ + b) with x' = relu(Σ_z parts[z] + xbias), the input
- *   being the previous layer's split partial sums [nsplit][m][k] (its bias xbias, then ReLU). */
+ *   being the previous layer's split partial sums [nsplit][m][k] (its bias xbias, then ReLU).
+ * scflow_ph_heads_sum: scflow_ph_heads on such a split input (xsplit = 0: plain x). */
 int scflow_ph_fc_split(const float* x, int ldx, int m, int k, const float* W, float* parts, int n,
-                       int ksplit, int gn_c, const float* scale, const float* shift, void* stream);
+                       int ksplit, int gn_c, const float* scale, const float* shift, int xsplit,
+                       const float* xbias, void* stream);
 int scflow_ph_fc_sum(const float* parts, int nsplit, int m, int k, const float* xbias,
                      const float* W, const float* bias, float* y, int n, int relu, void* stream);
+int scflow_ph_heads_sum(const float* x, int xsplit, const float* xbias, int m, int k,
+                        const float* Wr, const float* br, int rch, const float* Wt, const float* bt,
+                        const long long* label, int num_class, float* drot, float* dt,
+                        void* stream);
 int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* br, int rch,
                     const float* Wt, const float* bt, const long long* label, int num_class,
                     float* drot, float* dt, void* stream);

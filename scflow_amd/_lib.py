@@ -122,7 +122,9 @@ SIGNATURES = {
                                      c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, c_vp]),
     "scflow_ph_fc_split": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp,
-                                   c_vp, c_vp]),
+                                   c_vp, c_int, c_vp, c_vp]),
+    "scflow_ph_heads_sum": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp,
+                                    c_vp, c_int, c_vp, c_vp, c_vp]),
     "scflow_ph_fc_sum": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int,
                                  c_vp]),
     "scflow_ph_gn_stats": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_float, c_vp, c_vp,

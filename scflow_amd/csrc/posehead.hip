@@ -465,14 +465,17 @@ SCFLOW_API int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* 
 
 SCFLOW_API int scflow_ph_fc_split(const float* x, int ldx, int m, int k, const float* W,
                                   float* parts, int n, int ksplit, int gn_c, const float* scale,
-                                  const float* shift, void* stream) {
+                                  const float* shift, int xsplit, const float* xbias,
+                                  void* stream) {
   if (!x || !W || !parts || m <= 0 || m > 32 || k <= 0 || n <= 0 || (k & 15) || (ldx & 3) ||
       ksplit <= 0 || ksplit > k / 16 || !aligned16(W) || !aligned16(x) ||
-      (gn_c > 0 && (!scale || !shift || (gn_c & 3))))
+      (gn_c > 0 && (!scale || !shift || (gn_c & 3))) || xsplit < 0 || (xsplit > 0 && !xbias) ||
+      (xsplit > 0 && gn_c > 0))
     return SCFLOW_EINVAL;
   FcArgs f{};
   f.x = x; f.ldx = ldx; f.m = m; f.k = k; f.W = W; f.y = parts; f.n = n;
   f.gn_c = gn_c; f.scale = scale; f.shift = shift; f.ksplit = ksplit;
+  f.xsplit = xsplit; f.xstride = (long long)m * ldx; f.xbias = xbias;
   dim3 grid((unsigned)((n + 15) / 16), (unsigned)ksplit);
   if (m <= 16)
     ph_fc_kernel<1><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
@@ -500,12 +503,22 @@ SCFLOW_API int scflow_ph_fc_sum(const float* parts, int nsplit, int m, int k, co
 SCFLOW_API int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* br,
                                int rch, const float* Wt, const float* bt, const long long* label,
                                int num_class, float* drot, float* dt, void* stream) {
+  return scflow_ph_heads_sum(x, 0, nullptr, m, k, Wr, br, rch, Wt, bt, label, num_class, drot, dt,
+                             stream);
+}
+
+SCFLOW_API int scflow_ph_heads_sum(const float* x, int xsplit, const float* xbias, int m, int k,
+                                   const float* Wr, const float* br, int rch, const float* Wt,
+                                   const float* bt, const long long* label, int num_class,
+                                   float* drot, float* dt, void* stream) {
+  if (xsplit < 0 || (xsplit > 0 && (!xbias || !aligned16(xbias)))) return SCFLOW_EINVAL;
   if (!x || !Wr || !br || !Wt || !bt || !label || !drot || !dt || m <= 0 || k <= 0 || (k & 15) ||
       rch <= 0 || rch + 3 > 16 || num_class <= 0 || !aligned16(x) || !aligned16(Wr) || !aligned16(Wt))
     return SCFLOW_EINVAL;
   FcArgs f{};
   f.x = x; f.ldx = k; f.m = m; f.k = k; f.W = Wr; f.bias = br; f.y = drot; f.n = rch + 3;
   f.Wt = Wt; f.bt = bt; f.label = label; f.num_class = num_class; f.rch = rch; f.dt = dt;
+  f.xsplit = xsplit; f.xstride = (long long)m * k; f.xbias = xbias;
   if (m <= 16)
     ph_fc_kernel<1><<<1, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
   else

@@ -699,33 +699,46 @@ class MultiClassPoseHead(nn.Module):
         c = cur0.c
         x = cur0.buf
         k_in = c * hh * ww
-        # FC1 (K = 2048) with K split over 4 slices (64 → 256 workgroups); FC2 sums the slices,
-        # adds FC1's bias and applies its ReLU on load
-        ks1 = 4 if n <= 32 and len(self.fc_layers) >= 2 and (k_in // 16) >= 4 else 1
+        # The FCs (M = n ≤ 32 rows) are weight-streaming: each runs with its K split over 4
+        # workgroup slices (FC1 64 → 256 workgroups) into partial sums that the next layer adds,
+        # biases and ReLUs on load; the trunk returns (partials, split, bias) for the heads.
+        self._split_fc = n <= 32 and all(fc[0].in_features % 64 == 0 for fc in self.fc_layers)
+        if not self._split_fc:
+            for i, fc in enumerate(self.fc_layers):
+                lin = fc[0]
+                y = empty(n, lin.out_features)
+                if i == 0:
+                    ops.ph_fc(x, k_in, n, k_in, fc1_w, lin.bias.detach(), y, lin.out_features, True,
+                              gn_c=c, scale=scale, shift=shift)
+                else:
+                    ops.ph_fc(x, x.shape[1], n, x.shape[1], lin.weight.detach(), lin.bias.detach(),
+                              y, lin.out_features, True)
+                x = y
+            return x
+        ks, xsplit, xbias, ldx = 4, 0, None, k_in
         for i, fc in enumerate(self.fc_layers):
             lin = fc[0]
-            if i == 0 and ks1 > 1:
-                y = empty(ks1, n, lin.out_features)
-                ops.ph_fc_split(x, k_in, n, k_in, fc1_w, y, lin.out_features, ks1, gn_c=c, scale=scale,
-                                shift=shift)
-                x = y
-                continue
-            y = empty(n, lin.out_features)
+            y = empty(ks, n, lin.out_features)
             if i == 0:
-                ops.ph_fc(x, k_in, n, k_in, fc1_w, lin.bias.detach(), y, lin.out_features, True,
-                          gn_c=c, scale=scale, shift=shift)
-            elif i == 1 and ks1 > 1:
-                prev = self.fc_layers[0][0]
-                ops.ph_fc_sum(x, ks1, n, prev.out_features, prev.bias.detach(), lin.weight.detach(),
-                              lin.bias.detach(), y, lin.out_features, True)
+                ops.ph_fc_split(x, k_in, n, k_in, fc1_w, y, lin.out_features, ks, gn_c=c, scale=scale,
+                                shift=shift)
             else:
-                ops.ph_fc(x, x.shape[1], n, x.shape[1], lin.weight.detach(), lin.bias.detach(), y,
-                          lin.out_features, True)
-            x = y
+                ops.ph_fc_split(x, ldx, n, ldx, lin.weight.detach(), y, lin.out_features, ks,
+                                xsplit=xsplit, xbias=xbias)
+            x, xsplit, xbias, ldx = y, ks, lin.bias.detach(), lin.out_features
         return x
 
     def heads_hip(self, x: Tensor, label: Tensor, drot: Tensor, dt: Tensor) -> None:
-        """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt."""
+        """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt
+        (x: [n, 256], or the last FC's split partial sums [split, n, 256])."""
+        if x.dim() == 3:
+            n, k = x.shape[1], x.shape[2]
+            ops.ph_heads(x, n, k, self.rotation_pred.weight.detach(),
+                         self.rotation_pred.bias.detach(), self.rotation_out_channels,
+                         self.translation_pred.weight.detach(), self.translation_pred.bias.detach(),
+                         label.long(), self.num_class, drot, dt, xsplit=x.shape[0],
+                         xbias=self.fc_layers[-1][0].bias.detach())
+            return
         n = x.shape[0]
         ops.ph_heads(x, n, x.shape[1], self.rotation_pred.weight.detach(),
                      self.rotation_pred.bias.detach(), self.rotation_out_channels,

@@ -426,10 +426,12 @@ def ph_fc(x: Tensor, ldx: int, m: int, k: int, W: Tensor, bias: Optional[Tensor]
 
 
 def ph_fc_split(x: Tensor, ldx: int, m: int, k: int, W: Tensor, parts: Tensor, n: int, ksplit: int,
-                gn_c: int = 0, scale: Optional[Tensor] = None, shift: Optional[Tensor] = None) -> None:
-    """parts [ksplit, m, n] = K-split partial sums of x·Wᵀ (no bias / activation)."""
-    _launch("scflow_ph_fc_split", x,_p(x), ldx, m, k, _p(W), _p(parts), n, ksplit, gn_c,
-                                         _p(scale), _p(shift))
+                gn_c: int = 0, scale: Optional[Tensor] = None, shift: Optional[Tensor] = None,
+                xsplit: int = 0, xbias: Optional[Tensor] = None) -> None:
+    """parts [ksplit, m, n] = K-split partial sums of x·Wᵀ (no bias / activation); xsplit > 0:
+    x is [xsplit, m, ldx] partial sums read as relu(Σ + xbias)."""
+    _launch("scflow_ph_fc_split", x, _p(x), ldx, m, k, _p(W), _p(parts), n, ksplit, gn_c,
+            _p(scale), _p(shift), xsplit, _p(xbias))
 
 
 def ph_fc_sum(parts: Tensor, nsplit: int, m: int, k: int, xbias: Tensor, W: Tensor,
@@ -440,11 +442,13 @@ def ph_fc_sum(parts: Tensor, nsplit: int, m: int, k: int, xbias: Tensor, W: Tens
 
 
 def ph_heads(x: Tensor, m: int, k: int, Wr: Tensor, br: Tensor, rch: int, Wt: Tensor, bt: Tensor,
-             label: Tensor, num_class: int, drot: Tensor, dt: Tensor) -> None:
+             label: Tensor, num_class: int, drot: Tensor, dt: Tensor, xsplit: int = 0,
+             xbias: Optional[Tensor] = None) -> None:
+    """xsplit > 0: x is [xsplit, m, k] partial sums of the previous FC, read as relu(Σ + xbias)."""
     if label.dtype != torch.int64 or label.device != x.device:
         raise TypeError("label must be an int64 tensor on the same device")
-    _launch("scflow_ph_heads", x,_p(x), m, k, _p(Wr), _p(br), rch, _p(Wt), _p(bt), _p(label),
-                                      num_class, _p(drot), _p(dt))
+    _launch("scflow_ph_heads_sum", x, _p(x), xsplit, _p(xbias), m, k, _p(Wr), _p(br), rch, _p(Wt),
+            _p(bt), _p(label), num_class, _p(drot), _p(dt))
 
 
 # ------------------------------------------------------------------------------- §8(f)-1 encoder
