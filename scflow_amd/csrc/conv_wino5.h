@@ -68,27 +68,6 @@ constexpr size_t wino5_lds_bytes() {
   return sizeof(float) * (halo > epi ? halo : epi);
 }
 
-// the fused epilogues of one output element (shared with the direct conv's semantics)
-template <int EPI>
-__device__ __forceinline__ void conv_epilogue_store(const scflow_conv_args& a, size_t pix, int col,
-                                                   float v) {
-  if constexpr (EPI == SCFLOW_EPI_PLAIN) {
-    a.out[pix * a.so + col] = act_apply(v, a.act);
-  } else if constexpr (EPI == SCFLOW_EPI_GRU_ZR) {
-    const int hcn = a.cout >> 1;
-    if (col < hcn) {
-      a.gate[pix * a.sg + col] = sigmoidf_(v);
-    } else {
-      const int c = col - hcn;
-      a.rh[pix * a.srh + c] = sigmoidf_(v) * a.hid[pix * a.sh + c];
-    }
-  } else {  // GRU_Q
-    const float z = a.gate[pix * a.sg + col];
-    const float h = a.hid[pix * a.sh + col];
-    a.hid[pix * a.sh + col] = (1.f - z) * h + z * tanhf(v);
-  }
-}
-
 template <int DIR, int W, int NBW, int EPI>
 __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   using G = Wino5Geom<DIR, W>;
@@ -268,31 +247,73 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   const float bias = a.bias ? a.bias[col] : 0.f;
   constexpr int GROUPS = 256 / BNW;
   constexpr int NT = W5TM / GROUPS;  // tiles per thread
+  // Every global read of the epilogue (bias map, h, z) is issued before any store: the stores
+  // may alias them as far as the compiler knows, so interleaving would serialise NT·4 round
+  // trips through memory.
+  float y[NT][4];
+  int pix[NT][4];  // output pixel (n·h·w < 2^31)
 #pragma unroll
   for (int k = 0; k < NT; ++k) {
     const int m = tid / BNW + GROUPS * k;
     float mv[8];
 #pragma unroll
     for (int xi = 0; xi < 8; ++xi) mv[xi] = S[(xi * W5TM + m) * BNW + co];
-    float y[4];
-    size_t pix[4];
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
       float v = 0.f;
 #pragma unroll
       for (int xi = 0; xi < 8; ++xi)
         if (kW5AT[o][xi] != 0.f) v += kW5AT[o][xi] * mv[xi];
-      y[o] = v + bias;
+      y[k][o] = v + bias;
       const int oy = DIR == 0 ? oy0 + m / G::TPR : oy0 + o;
       const int ox = DIR == 0 ? 4 * (m % G::TPR) + o : ox0 + m;
-      pix[o] = ((size_t)img * a.h + oy) * W + ox;
+      pix[k][o] = (img * a.h + oy) * W + ox;
     }
-    if (a.bias_map) {
+  }
+  if (a.bias_map) {
 #pragma unroll
-      for (int o = 0; o < 4; ++o) y[o] += a.bias_map[pix[o] * a.sbm + col];
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) y[k][o] += a.bias_map[(size_t)pix[k][o] * a.sbm + col];
+  }
+  if constexpr (EPI == SCFLOW_EPI_PLAIN) {
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) a.out[(size_t)pix[k][o] * a.so + col] = act_apply(y[k][o], a.act);
+  } else if constexpr (EPI == SCFLOW_EPI_GRU_ZR) {
+    const int hcn = a.cout >> 1;
+    if (col < hcn) {
+#pragma unroll
+      for (int k = 0; k < NT; ++k)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) a.gate[(size_t)pix[k][o] * a.sg + col] = sigmoidf_(y[k][o]);
+    } else {
+      const int c = col - hcn;
+      float hv[NT][4];
+#pragma unroll
+      for (int k = 0; k < NT; ++k)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) hv[k][o] = a.hid[(size_t)pix[k][o] * a.sh + c];
+#pragma unroll
+      for (int k = 0; k < NT; ++k)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) a.rh[(size_t)pix[k][o] * a.srh + c] = sigmoidf_(y[k][o]) * hv[k][o];
     }
+  } else {  // GRU_Q
+    float zv[NT][4], hv[NT][4];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) conv_epilogue_store<EPI>(a, pix[o], col, y[o]);
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        zv[k][o] = a.gate[(size_t)pix[k][o] * a.sg + col];
+        hv[k][o] = a.hid[(size_t)pix[k][o] * a.sh + col];
+      }
+#pragma unroll
+    for (int k = 0; k < NT; ++k)
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+        a.hid[(size_t)pix[k][o] * a.sh + col] = (1.f - zv[k][o]) * hv[k][o] + zv[k][o] * tanhf(y[k][o]);
   }
 }
 
