@@ -180,17 +180,30 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
   const float osh = a.out_scale ? a.out_shift[col] : 0.f;
   const int act = col < a.act_split ? a.act : a.act2;
   float* outz = a.out + (size_t)z * ((size_t)a.n * P.oh * P.ow * a.s_out);
+  // every residual read is issued before any store (the stores may alias them as far as the
+  // compiler knows; interleaved, each read's latency would be serialised)
+  int pixv[RB][16];
 #pragma unroll
-  for (int rr = 0; rr < RB; ++rr) {
+  for (int rr = 0; rr < RB; ++rr)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = wm * (TILE_M / 2) + rr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
       const int oy = oy0 + m / tc, ox = ox0 + m % tc;
-      const size_t pix = ((size_t)img * P.oh + oy) * ow + ox;
+      pixv[rr][r] = (img * P.oh + oy) * ow + ox;
+    }
+  float resv[RB][16];
+#pragma unroll
+  for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) resv[rr][r] = a.res ? a.res[(size_t)pixv[rr][r] * a.s_res + col] : 0.f;
+#pragma unroll
+  for (int rr = 0; rr < RB; ++rr) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
       float v = acc[rr][r] + bias;
       if (a.out_scale) v = v * osc + osh;
-      if (a.res) v += a.res[pix * a.s_res + col];
-      outz[pix * a.s_out + col] = act_apply(v, act);
+      v += resv[rr][r];
+      outz[(size_t)pixv[rr][r] * a.s_out + col] = act_apply(v, act);
     }
   }
 }
