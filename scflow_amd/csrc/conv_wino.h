@@ -201,17 +201,37 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
       for (int e = 0; e < 16; ++e) acc[j][nb][e] = 0.f;
 
   floatx4 u[4][NBW];
-  // one sub-step: the MFMAs of point j, then point j's weights for sub-step tnext
+  // the MFMAs of point j, then point j's weights for sub-step tnext
+  auto point = [&](const floatx4(&v)[4], int j, int tnext) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb)
+        acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[j][nb][e], acc[j][nb], 0, 0, 0);
+    uload1(u[j], tnext, j);
+  };
   auto substep = [&](const floatx4(&v)[4], int tnext) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int nb = 0; nb < NBW; ++nb)
-          acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[j][nb][e], acc[j][nb], 0, 0, 0);
-      uload1(u[j], tnext, j);
-    }
+    for (int j = 0; j < 4; ++j) point(v, j, tnext);
+  };
+  // a sub-step with the NEXT sub-step's input transform (from LDS buffer buf, channels 8k..)
+  // woven between its point groups in program order — the compiler issues in order, so the LDS
+  // latency and the VALU sit under this sub-step's MFMAs instead of in front of them
+  auto substep_next = [&](const floatx4(&v)[4], int tnext, int buf, int k, floatx4(&vn)[4]) {
+    const floatx4* hb = smem4 + buf * G::BUF4 + 2 * k;
+    constexpr int cb1 = 8, cb2 = 16 + 1, cb3 = 24 + 1;  // column b of the patch (+ skew)
+    const floatx4 a0 = hb[o1], b0 = hb[o2], a2 = hb[o1 + cb2], b2 = hb[o2 + cb2];
+    point(v, 0, tnext);
+    const floatx4 t0 = fma_s4(b0, sgn, a0), t2 = fma_s4(b2, sgn, a2);
+    vn[0] = sub4(t0, t2);
+    const floatx4 a1 = hb[o1 + cb1], b1 = hb[o2 + cb1], a3 = hb[o1 + cb3], b3 = hb[o2 + cb3];
+    point(v, 1, tnext);
+    const floatx4 t1 = fma_s4(b1, sgn, a1), t3 = fma_s4(b3, sgn, a3);
+    vn[1] = add4(t1, t2);
+    vn[2] = sub4(t2, t1);
+    vn[3] = sub4(t1, t3);
+    point(v, 2, tnext);
+    point(v, 3, tnext);
   };
 
   // prologue: stage 0's halo in LDS buffer 0, sub-step 0's weights and transform in registers
@@ -234,16 +254,13 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
     const int t0 = s * WNSUB;
     hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
     hload(0);
-    vcompute(buf, 1, vB);
-    substep(vA, t0 + 1);
+    substep_next(vA, t0 + 1, buf, 1, vB);
     hstore(buf ^ 1, 0);
     hload(1);
-    vcompute(buf, 2, vA);
-    substep(vB, t0 + 2);
+    substep_next(vB, t0 + 2, buf, 2, vA);
     hstore(buf ^ 1, 1);
     hload(2);
-    vcompute(buf, 3, vB);
-    substep(vA, t0 + 3);
+    substep_next(vA, t0 + 3, buf, 3, vB);
     hstore(buf ^ 1, 2);
     hload(3);
     substep(vB, t0 + 4);

@@ -159,23 +159,24 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   auto tapoff = [](int t) {  // LDS float4 offset of input t from input 0 (tiles start at c ≡ 0 mod 4)
     return DIR == 0 ? t * 8 + t / G::SK : t * G::ROWP;
   };
-  auto vcompute = [&](int buf, int k, floatx4(&v)[2][2]) {  // [q][x]
-    const floatx4* hb = smem4 + buf * G::BUF4 + tb + 4 * k;
+  // input transform of one 8-channel half q of sub-step k from LDS buffer buf: the taps this
+  // wave needs (1..6, and 0, 7 for wave 3), then its two rows of Bᵀd
+  auto vload = [&](int buf, int k, int q, floatx4(&d)[8], auto w3) {
+    const floatx4* hb = smem4 + buf * G::BUF4 + tb + 4 * k + 2 * q;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      floatx4 d[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) d[t] = hb[tapoff(t) + 2 * q];
-      if (wave < 3) {
-        const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-        const floatx4 av = fma_s4(d[5], c5, fma_s4(d[3], c3, fma_s4(d[1], c1, zero)));
-        const floatx4 bv = fma_s4(d[4], c4, fma_s4(d[2], c2, d[6]));
-        v[q][0] = add4(bv, av);
-        v[q][1] = sub4(bv, av);
-      } else {
-        v[q][0] = fma_s4(sub4(d[2], d[4]), 5.25f, sub4(d[6], d[0]));
-        v[q][1] = fma_s4(sub4(d[3], d[5]), 5.25f, sub4(d[7], d[1]));
-      }
+    for (int t = 0; t < 8; ++t)
+      if (decltype(w3)::value || (t > 0 && t < 7)) d[t] = hb[tapoff(t)];
+  };
+  auto vmath = [&](const floatx4(&d)[8], floatx4(&v)[2], auto w3) {
+    if constexpr (!decltype(w3)::value) {
+      const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+      const floatx4 av = fma_s4(d[5], c5, fma_s4(d[3], c3, fma_s4(d[1], c1, zero)));
+      const floatx4 bv = fma_s4(d[4], c4, fma_s4(d[2], c2, d[6]));
+      v[0] = add4(bv, av);
+      v[1] = sub4(bv, av);
+    } else {
+      v[0] = fma_s4(sub4(d[2], d[4]), 5.25f, sub4(d[6], d[0]));
+      v[1] = fma_s4(sub4(d[3], d[5]), 5.25f, sub4(d[7], d[1]));
     }
   };
 
@@ -187,46 +188,65 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[x][nb][e] = 0.f;
 
-  // one 16-channel sub-step: per 8-channel half q, its MFMAs then its weights for tnext
-  auto substep = [&](const floatx4(&v)[2][2], int tnext) {
+  // the MFMAs of 8-channel half q, then its weights for sub-step tnext
+  auto half = [&](const floatx4(&v)[2][2], int q, int tnext) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int x = 0; x < 2; ++x)
 #pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-          for (int nb = 0; nb < NBW; ++nb)
-            acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[q][x][e], u[q][x][nb][e], acc[x][nb], 0, 0, 0);
-      uload1(tnext, q);
-    }
+        for (int nb = 0; nb < NBW; ++nb)
+          acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[q][x][e], u[q][x][nb][e], acc[x][nb], 0, 0, 0);
+    uload1(tnext, q);
   };
 
-  uload1(0, 0);
-  uload1(0, 1);
-  hsource(0);
-  hload(0);
-  hstore(0, 0);
-  hload(1);
-  hstore(0, 1);
-  __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
-  __syncthreads();
-  floatx4 vA[2][2], vB[2][2];
-  vcompute(0, 0, vA);
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
-    const int t0 = s * W5NSUB;
-    hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
+  // The main loop is instantiated per transform shape (waves 0-2 / wave 3; the wave index is
+  // uniform), so its body has no branches and the next sub-step's transform can be woven
+  // between this sub-step's MFMAs in program order (the compiler issues in order: the LDS
+  // latency and the VALU then sit under the MFMAs instead of in front of them).
+  auto mainloop = [&](auto w3) {
+    floatx4 d[8];
+    uload1(0, 0);
+    uload1(0, 1);
+    hsource(0);
     hload(0);
-    vcompute(buf, 1, vB);
-    substep(vA, t0 + 1);
-    hstore(buf ^ 1, 0);
+    hstore(0, 0);
     hload(1);
-    substep(vB, t0 + 2);
-    hstore(buf ^ 1, 1);
+    hstore(0, 1);
+    __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
     __syncthreads();
-    vcompute(buf ^ 1, 0, vA);
-  }
+    floatx4 vA[2][2], vB[2][2];
+    vload(0, 0, 0, d, w3);
+    vmath(d, vA[0], w3);
+    vload(0, 0, 1, d, w3);
+    vmath(d, vA[1], w3);
+    for (int s = 0; s < nst; ++s) {
+      const int buf = s & 1;
+      const int t0 = s * W5NSUB;
+      hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
+      hload(0);
+      vload(buf, 1, 0, d, w3);
+      half(vA, 0, t0 + 1);
+      vmath(d, vB[0], w3);
+      vload(buf, 1, 1, d, w3);
+      half(vA, 1, t0 + 1);
+      vmath(d, vB[1], w3);
+      hstore(buf ^ 1, 0);
+      hload(1);
+      half(vB, 0, t0 + 2);
+      half(vB, 1, t0 + 2);
+      hstore(buf ^ 1, 1);
+      __syncthreads();
+      vload(buf ^ 1, 0, 0, d, w3);
+      vmath(d, vA[0], w3);
+      vload(buf ^ 1, 0, 1, d, w3);
+      vmath(d, vA[1], w3);
+    }
+  };
+  if (wave == 3)
+    mainloop(std::true_type{});
+  else
+    mainloop(std::false_type{});
 
   // epilogue: M[ξ][tile][co] in LDS, then y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ]
   __syncthreads();
