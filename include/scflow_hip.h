@@ -94,11 +94,19 @@ typedef struct scflow_conv_args {
   int bk;                                /* packing format of the weights: K-stage depth 0 or 16 */
                                          /* (default) or 8, or SCFLOW_CONV_WINO — see           */
                                          /* scflow_conv_pick_bk                                 */
+  /* Winograd 3×3 only (NULL elsewhere) — the RAFT encoder's fused normalisation:              */
+  const float* in_scale;                 /* src0 ← relu(src0·in_scale[n][c0] + in_shift[n][c0]) */
+  const float* in_shift;                 /* on load (InstanceNorm + ReLU of the producer; c1=0) */
+  const float* out_scale;                /* v ← (conv + bias)·out_scale[o] + out_shift[o]       */
+  const float* out_shift;                /* (eval BatchNorm)                                    */
+  const float* res; int sres;            /* v += res[pix·sres + o] before the activation        */
 } scflow_conv_args;
 
-/* scflow_conv_args.bk = SCFLOW_CONV_WINO selects the Winograd F(2×2,3×3) kernel (3×3, stride 1,
- * pad 1, width 32 or 64, height a multiple of 4, SCFLOW_EPI_PLAIN): exact fp32 arithmetic, 2.25×
- * fewer matrix multiplies than the direct conv; the weights must be packed with the same bk. */
+/* scflow_conv_args.bk = SCFLOW_CONV_WINO selects the Winograd kernels: F(2×2,3×3) for 3×3, stride
+ * 1, pad 1, width 32, 64 or 128 (height a multiple of 4 at 32, of 2 otherwise), SCFLOW_EPI_PLAIN;
+ * F(4,5) for 1×5 (pad 0,2) / 5×1 (pad 2,0), width 32 or 64, every epilogue.  Exact fp32
+ * arithmetic, 2.25× / 2.5× fewer matrix multiplies than the direct conv; the weights must be
+ * packed with the same bk. */
 #define SCFLOW_CONV_WINO 2
 
 /* Number of floats of the packed weight buffer for bk 8 and 16 (the same for both); w_oihw is

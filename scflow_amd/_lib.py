@@ -38,6 +38,9 @@ class ConvArgs(ctypes.Structure):
         ("hid", c_vp), ("sh", c_int),
         ("bias_map", c_vp), ("sbm", c_int),
         ("bk", c_int),
+        ("in_scale", c_vp), ("in_shift", c_vp),
+        ("out_scale", c_vp), ("out_shift", c_vp),
+        ("res", c_vp), ("sres", c_int),
     ]
 
 

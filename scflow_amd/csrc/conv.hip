@@ -648,14 +648,23 @@ __global__ void pack_kernel(const float* __restrict__ w, float* __restrict__ out
 // Winograd eligibility: F(2×2,3×3) (conv_wino.h) for 3×3, F(4,5) (conv_wino5.h) for 1×5 / 5×1;
 // stride 1, "same" padding, whole-row tiles of 32 tiles
 bool wino_shape(int kh, int kw, int stride, int w) {
-  const bool k = (kh == 3 && kw == 3) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1);
+  if (kh == 3 && kw == 3) return stride == 1 && (w == 32 || w == 64 || w == 128);
+  const bool k = (kh == 1 && kw == 5) || (kh == 5 && kw == 1);
   return k && stride == 1 && (w == 32 || w == 64);
+}
+bool has_fused_norm(const scflow_conv_args& a) {
+  return a.in_scale || a.in_shift || a.out_scale || a.out_shift || a.res;
 }
 bool wino_launchable(const scflow_conv_args& a) {
   if (!wino_shape(a.kh, a.kw, a.stride, a.w) || a.c0 % 4 || a.c1 % 4 || a.cout <= 4 ||
       (a.c0 + a.c1 <= 4 && a.c1 == 0))
     return false;
-  if (a.kh == 3) return a.ph == 1 && a.pw == 1 && a.h % (a.w == 32 ? 4 : 2) == 0 && a.epilogue == SCFLOW_EPI_PLAIN;
+  if (a.kh == 3)
+    return a.ph == 1 && a.pw == 1 && a.h % (a.w == 32 ? 4 : 2) == 0 &&
+           a.epilogue == SCFLOW_EPI_PLAIN &&
+           (!(a.in_scale || a.in_shift) || (a.in_scale && a.in_shift && a.c1 == 0)) &&
+           (!a.out_scale) == (!a.out_shift);
+  if (has_fused_norm(a)) return false;
   if (a.kh == 1) return a.ph == 0 && a.pw == 2 && a.h % (128 / a.w) == 0;
   return a.ph == 2 && a.pw == 0 && a.h % 4 == 0;
 }
@@ -669,7 +678,7 @@ long long wino_packed_size(int cout, int c0, int c1, int kh) {
 }
 // output rows per workgroup (the grid's x extent is n · h / rows · column blocks)
 long long wino_blocks(const scflow_conv_args& a) {
-  if (a.kh == 3) return (long long)a.n * (a.h / (a.w == 32 ? 4 : 2));
+  if (a.kh == 3) return (long long)a.n * (a.h / (a.w == 32 ? 4 : 2)) * (a.w == 128 ? 2 : 1);
   if (a.kh == 1) return (long long)a.n * (a.h / (128 / a.w));
   return (long long)a.n * (a.h / 4) * (a.w / 32);
 }
@@ -707,7 +716,7 @@ int launch_wino_w(const WinoParams& p, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  dim3 grid(p.a.n * (p.a.h / G::OROWS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
+  dim3 grid(p.a.n * (p.a.h / G::OROWS) * G::XB, round_up(p.a.cout, 32 * NBW) / (32 * NBW));
   conv_wino_kernel<W, NBW><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }
@@ -761,6 +770,7 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
   p.nst = (p.cp0 + round_up(a.c1, WSC)) / WSC;
   const int nbw = wino_nbw(a, device_cus());
   if (a.w == 32) return nbw == 2 ? launch_wino_w<32, 2>(p, st) : launch_wino_w<32, 1>(p, st);
+  if (a.w == 128) return nbw == 2 ? launch_wino_w<128, 2>(p, st) : launch_wino_w<128, 1>(p, st);
   return nbw == 2 ? launch_wino_w<64, 2>(p, st) : launch_wino_w<64, 1>(p, st);
 }
 
@@ -943,6 +953,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     return SCFLOW_EINVAL;
   }
   if (a.bk == SCFLOW_CONV_WINO) return launch_wino(a, (hipStream_t)stream);
+  if (has_fused_norm(a)) return SCFLOW_EUNSUPPORTED;  // Winograd 3×3 only
   if (a.bk != 0 && a.bk != 8 && a.bk != 16) return SCFLOW_EINVAL;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
   if (g.variant == V_NONE) return SCFLOW_EUNSUPPORTED;

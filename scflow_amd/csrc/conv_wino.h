@@ -75,11 +75,13 @@ struct WinoParams {
 
 template <int W>
 struct WinoGeom {
-  static constexpr int TW = W / 2;          // tiles per tile row
+  static constexpr int OCOLS = W < 64 ? W : 64;  // output columns per workgroup
+  static constexpr int XB = W / OCOLS;           // column blocks per image row (2 at W = 128)
+  static constexpr int TW = OCOLS / 2;      // tiles per tile row of the block
   static constexpr int TRW = WTM / TW;      // tile rows per workgroup
   static constexpr int OROWS = 2 * TRW;     // output rows per workgroup
   static constexpr int HR = OROWS + 2;      // halo rows
-  static constexpr int HC = W + 2;          // halo columns
+  static constexpr int HC = OCOLS + 2;      // halo columns
   static constexpr int NH4 = HR * HC * (WSC / 4);  // float4 of one stage's halo
   static constexpr int NA = (NH4 + 1023) / 1024;   // float4 per thread per quarter stage
   // LDS halo layout (float4 units): 8 per pixel and one more every 2 pixels, so the b128 patch
@@ -106,9 +108,10 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int li = lane & 31, hh = lane >> 5;
-  const int blocks_per_img = a.h / G::OROWS;
+  const int blocks_per_img = (a.h / G::OROWS) * G::XB;
   const int img = blockIdx.x / blocks_per_img;
-  const int oy0 = (blockIdx.x % blocks_per_img) * G::OROWS;
+  const int brem = blockIdx.x % blocks_per_img;
+  const int oy0 = (brem / G::XB) * G::OROWS, ox0 = (brem % G::XB) * G::OCOLS;
   const int nst0 = P.cp0 / WSC;
   const int nst = P.nst;
   const int npix = a.n * a.h * W;
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
       const int idx = tid + 256 * (4 * j + part);
       const int pix = idx >> 3;
       const int hr = pix / G::HC, hcol = pix - hr * G::HC;
-      const int iy = oy0 - 1 + hr, ix = hcol - 1;
+      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hcol;
       const bool ok = idx < G::NH4 && iy >= 0 && iy < a.h && ix >= 0 && ix < W;
       hpix[part][j] = ok ? (img * a.h + iy) * W + ix : -1;
       hlds[part][j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 7) : -1;
@@ -134,6 +137,8 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   // stage s's source, as a buffer starting at its first channel
   __amdgpu_buffer_rsrc_t hsrc;
   int hss4 = 0, hlim = 0;  // pixel stride in bytes, channels of the stage present in the source
+  floatx4 isc = {1.f, 1.f, 1.f, 1.f}, ish = {0.f, 0.f, 0.f, 0.f};  // input affine (encoder IN)
+  const bool in_aff = a.in_scale != nullptr;
   auto hsource = [&](int s) {
     const bool s1 = s >= nst0;
     const float* src = s1 ? a.src1 : a.src0;
@@ -143,13 +148,23 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
     hsrc = wino_rsrc(src + cc, (unsigned)(((long long)(npix - 1) * ss + cs - cc) * 4));
     hss4 = ss * 4;
     hlim = cs - cc;
+    if (in_aff && hq4 < hlim) {  // this thread's 4 channels of the stage, for its image
+      isc = *(const floatx4*)(a.in_scale + (size_t)img * a.c0 + cc + hq4);
+      ish = *(const floatx4*)(a.in_shift + (size_t)img * a.c0 + cc + hq4);
+    }
   };
   auto hload = [&](int part) {
     const bool chan_ok = hq4 < hlim;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       const int p = hpix[part][j];
-      ra[j] = wino_bload(hsrc, (p >= 0 && chan_ok) ? p * hss4 + hq4 * 4 : WINO_OOB, 0);
+      const bool ok = p >= 0 && chan_ok;
+      floatx4 v = wino_bload(hsrc, ok ? p * hss4 + hq4 * 4 : WINO_OOB, 0);
+      if (in_aff && ok) {  // zero padding stays zero (it pads the normalised activation)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * isc[e] + ish[e], 0.f);
+      }
+      ra[j] = v;
     }
   };
   auto hstore = [&](int buf, int part) {
@@ -289,6 +304,8 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   const int col = blockIdx.y * BNW + co;
   if (col >= a.cout) return;
   const float bias = a.bias ? a.bias[col] : 0.f;
+  const float osc = a.out_scale ? a.out_scale[col] : 1.f;
+  const float osh = a.out_scale ? a.out_shift[col] : 0.f;
   constexpr int GROUPS = 256 / BNW;
   constexpr int NPX = WTM * 4 / GROUPS;  // output pixels per thread
   size_t pix[NPX];
@@ -301,15 +318,21 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
     const float s0 = Sb[0 * 2 * WTM * BNW], s1 = Sb[1 * 2 * WTM * BNW];
     const float s2 = Sb[2 * 2 * WTM * BNW], s3 = Sb[3 * 2 * WTM * BNW];
     val[q] = ar == 0 ? s0 + s1 + s2 : s1 - s2 - s3;
-    const int y = oy0 + 2 * (m / G::TW) + ar, x = 2 * (m % G::TW) + bc;
+    const int y = oy0 + 2 * (m / G::TW) + ar, x = ox0 + 2 * (m % G::TW) + bc;
     pix[q] = ((size_t)img * a.h + y) * W + x;
+    val[q] = (val[q] + bias) * osc + osh;
   }
+  // all global reads (bias map, residual) before any store
   if (a.bias_map) {
 #pragma unroll
     for (int q = 0; q < NPX; ++q) val[q] += a.bias_map[pix[q] * a.sbm + col];
   }
+  if (a.res) {
 #pragma unroll
-  for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q] + bias, a.act);
+    for (int q = 0; q < NPX; ++q) val[q] += a.res[pix[q] * a.sres + col];
+  }
+#pragma unroll
+  for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q], a.act);
 }
 
 // U = G g Gᵀ per (co, ci) (row i = 2 negated), packed [nb32][sub-step][ξ][lane][4] with

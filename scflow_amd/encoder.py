@@ -28,7 +28,7 @@ from typing import Optional, Sequence, Tuple, Union
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 from .registry import MODELS
 
 Tensor = torch.Tensor
@@ -123,6 +123,31 @@ def _packed(conv: nn.Conv2d, stem: bool = False) -> Tensor:
         conv._scflow_enc_packed = ops.enc_stem_pack(w) if stem else ops.enc_conv_pack(w)
         conv._scflow_enc_key = key
     return conv._scflow_enc_packed
+
+
+def _wino_ok(conv: nn.Conv2d, h: int, w: int, cin: int) -> bool:
+    """3×3 stride-1 pad-1 convs at widths 32/64/128 run on the Winograd F(2×2,3×3) kernel with
+    the block's normalisation fused (scflow_conv2d, SCFLOW_CONV_WINO)."""
+    return (conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1) and
+            w in (32, 64, 128) and h % (4 if w == 32 else 2) == 0 and cin % 4 == 0 and
+            conv.groups == 1 and conv.dilation == (1, 1))
+
+
+def _wino_conv(conv: nn.Conv2d, x: Tensor, out: Tensor, n: int, h: int, w: int, cin: int,
+               in_scale: Optional[Tensor] = None, in_shift: Optional[Tensor] = None,
+               out_scale: Optional[Tensor] = None, out_shift: Optional[Tensor] = None,
+               res: Optional[Tensor] = None, act: Optional[str] = None) -> None:
+    wt = conv.weight
+    key = (wt.data_ptr(), wt._version, cin, w)
+    cache = getattr(conv, "_scflow_wino", None)
+    if cache is None or cache[0] != key:
+        cache = (key, ops.pack_conv_weight(wt.detach().float(), cin, 0, w, 1, _lib.CONV_WINO))
+        conv._scflow_wino = cache
+    cout = conv.out_channels
+    ops.conv2d(ops.Chan.whole(x.view(-1, cin)), cache[1], _bias(conv), n, h, w, cout, 3, 3, 1, 1,
+               act, out=ops.Chan.whole(out.view(-1, cout)), bk=_lib.CONV_WINO, in_scale=in_scale,
+               in_shift=in_shift, out_scale=out_scale, out_shift=out_shift,
+               res=None if res is None else ops.Chan.whole(res.view(-1, res.shape[-1])))
 
 
 def _bias(conv: nn.Conv2d) -> Optional[Tensor]:
@@ -255,11 +280,18 @@ class RAFTEncoder(nn.Module):
         ds = blk.downsample
         if IN:
             sc1, sh1, sc2, sh2 = (torch.empty(n, planes, device=dev) for _ in range(4))
-            ops.enc_conv(x, _packed(blk.conv1), _bias(blk.conv1), n, h, w, cin, planes, 3, st, 1, y1)
+            if st == 1 and _wino_ok(blk.conv1, h, w, cin):
+                _wino_conv(blk.conv1, x, y1, n, h, w, cin)
+            else:
+                ops.enc_conv(x, _packed(blk.conv1), _bias(blk.conv1), n, h, w, cin, planes, 3, st, 1,
+                             y1)
             ops.enc_instance_norm_stats(y1, n, oh * ow, planes, sc1, sh1, eps=blk.norm1.eps)
             y2 = torch.empty_like(y1)
-            ops.enc_conv(y1, _packed(blk.conv2), _bias(blk.conv2), n, oh, ow, planes, planes, 3, 1, 1,
-                         y2, in_scale=sc1, in_shift=sh1)
+            if _wino_ok(blk.conv2, oh, ow, planes):
+                _wino_conv(blk.conv2, y1, y2, n, oh, ow, planes, in_scale=sc1, in_shift=sh1)
+            else:
+                ops.enc_conv(y1, _packed(blk.conv2), _bias(blk.conv2), n, oh, ow, planes, planes, 3,
+                             1, 1, y2, in_scale=sc1, in_shift=sh1)
             ops.enc_instance_norm_stats(y2, n, oh * ow, planes, sc2, sh2, eps=blk.norm2.eps)
             if ds is not None:
                 d = torch.empty_like(y1)
@@ -271,16 +303,24 @@ class RAFTEncoder(nn.Module):
                 ops.enc_apply(y2, sc2, sh2, out, n, oh * ow, planes, id=x)
         else:
             b1, b2 = _bn_affine(blk.norm1), _bn_affine(blk.norm2)
-            ops.enc_conv(x, _packed(blk.conv1), _bias(blk.conv1), n, h, w, cin, planes, 3, st, 1, y1,
-                         out_scale=b1[0], out_shift=b1[1], act="ReLU")
+            if st == 1 and _wino_ok(blk.conv1, h, w, cin):
+                _wino_conv(blk.conv1, x, y1, n, h, w, cin, out_scale=b1[0], out_shift=b1[1],
+                           act="ReLU")
+            else:
+                ops.enc_conv(x, _packed(blk.conv1), _bias(blk.conv1), n, h, w, cin, planes, 3, st, 1,
+                             y1, out_scale=b1[0], out_shift=b1[1], act="ReLU")
             res = x
             if ds is not None:
                 res = torch.empty_like(y1)
                 bd = _bn_affine(ds[1])
                 ops.enc_conv(x, _packed(ds[0]), _bias(ds[0]), n, h, w, cin, planes, 1, st, 0, res,
                              out_scale=bd[0], out_shift=bd[1])
-            ops.enc_conv(y1, _packed(blk.conv2), _bias(blk.conv2), n, oh, ow, planes, planes, 3, 1, 1,
-                         out, out_scale=b2[0], out_shift=b2[1], res=res, act="ReLU")
+            if _wino_ok(blk.conv2, oh, ow, planes):
+                _wino_conv(blk.conv2, y1, out, n, oh, ow, planes, out_scale=b2[0], out_shift=b2[1],
+                           res=res, act="ReLU")
+            else:
+                ops.enc_conv(y1, _packed(blk.conv2), _bias(blk.conv2), n, oh, ow, planes, planes, 3,
+                             1, 1, out, out_scale=b2[0], out_shift=b2[1], res=res, act="ReLU")
         return out, oh, ow, planes
 
     def forward(self, x: Tensor, return_middle_result: bool = False) -> Tensor:

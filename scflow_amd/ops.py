@@ -228,9 +228,11 @@ def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w
            kh: int, kw: int, ph: int, pw: int, act: Optional[str] = None, out: Optional[Chan] = None,
            src1: Optional[Chan] = None, epilogue: int = _lib.EPI_PLAIN, gate: Optional[Chan] = None,
            rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1,
-           bias_map: Optional[Chan] = None, bk: int = 16) -> None:
+           bias_map: Optional[Chan] = None, bk: int = 16, **fused) -> None:
+    """One scflow_conv2d launch; ``fused``: in_scale / in_shift / out_scale / out_shift / res
+    (Winograd 3×3 only, see conv2d_args)."""
     a = conv2d_args(src0, packed, bias, n, h, w, cout, kh, kw, ph, pw, act, out, src1, epilogue,
-                    gate, rh, hid, stride, bias_map, bk)
+                    gate, rh, hid, stride, bias_map, bk, **fused)
     _launch("scflow_conv2d", src0.buf,ctypes.byref(a))
 
 
@@ -255,8 +257,12 @@ def conv2d_args(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: i
                 out: Optional[Chan] = None, src1: Optional[Chan] = None,
                 epilogue: int = _lib.EPI_PLAIN, gate: Optional[Chan] = None,
                 rh: Optional[Chan] = None, hid: Optional[Chan] = None, stride: int = 1,
-                bias_map: Optional[Chan] = None, bk: int = 16) -> "_lib.ConvArgs":
-    """The validated scflow_conv_args of one launch (see conv2d)."""
+                bias_map: Optional[Chan] = None, bk: int = 16, in_scale: Optional[Tensor] = None,
+                in_shift: Optional[Tensor] = None, out_scale: Optional[Tensor] = None,
+                out_shift: Optional[Tensor] = None, res: Optional[Chan] = None) -> "_lib.ConvArgs":
+    """The validated scflow_conv_args of one launch (see conv2d).  in_/out_scale/shift and res
+    (Winograd 3×3 only): relu(x·in_scale + in_shift) on load, (conv + b)·out_scale + out_shift,
+    + res before the activation."""
     for nm, ch in (("src0", src0), ("src1", src1), ("out", out), ("gate", gate), ("rh", rh),
                    ("hid", hid), ("bias_map", bias_map)):
         if ch is not None:
@@ -285,6 +291,14 @@ def conv2d_args(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: i
     if bias_map is not None:
         a.bias_map, a.sbm = bias_map.ptr, bias_map.stride
     a.bk = bk
+    for nm, t in (("in_scale", in_scale), ("in_shift", in_shift), ("out_scale", out_scale),
+                  ("out_shift", out_shift)):
+        if t is not None:
+            _require(t, nm)
+            setattr(a, nm, t.data_ptr())
+    if res is not None:
+        _require(res.buf, "res")
+        a.res, a.sres = res.ptr, res.stride
     return a
 
 
