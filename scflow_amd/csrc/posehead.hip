@@ -149,6 +149,9 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
 // to y.  Grid (n, c/32): a workgroup takes one sample's 32-channel block; thread t holds channel
 // quad t%8 of pixel slot t/8 (32 slots), float4 loads; per-channel sums in fp64 reduced over the
 // slots in a fixed order, then per group (c/groups channels) → mean, biased variance.
+// NS > 0: compile-time slab count; the pixel loop is unrolled PU-fold with every load of a
+// round issued before any add (this kernel is latency-bound: 64 workgroups at B = 16)
+template <int NS>
 __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restrict__ x, int nsplit,
                                                            long long split_stride, float* __restrict__ y,
                                                            int hw, int c, int groups,
@@ -161,7 +164,34 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
   const int img = blockIdx.x, cb = blockIdx.y * 32;
   const int q = threadIdx.x & 7, slot = threadIdx.x >> 3;
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
-  for (int p = slot; p < hw; p += 32) {
+  auto acc = [&](floatx4 v, size_t off) {
+    if (y) *(floatx4*)(y + off) = v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] += (double)v[e];
+      b[e] += (double)v[e] * (double)v[e];
+    }
+  };
+  int p = slot;
+  if constexpr (NS > 0) {
+    constexpr int PU = NS <= 2 ? 4 : (NS <= 4 ? 2 : 1);
+    for (; p + 32 * (PU - 1) < hw; p += 32 * PU) {
+      floatx4 v[PU][NS];
+#pragma unroll
+      for (int u = 0; u < PU; ++u)
+#pragma unroll
+        for (int z = 0; z < NS; ++z)
+          v[u][z] = *(const floatx4*)(x + (size_t)z * split_stride + ((size_t)img * hw + p + 32 * u) * c +
+                                      cb + 4 * q);
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+#pragma unroll
+        for (int z = 1; z < NS; ++z) v[u][0] += v[u][z];
+        acc(v[u][0], ((size_t)img * hw + p + 32 * u) * c + cb + 4 * q);
+      }
+    }
+  }
+  for (; p < hw; p += 32) {
     const size_t off = ((size_t)img * hw + p) * c + cb + 4 * q;
     floatx4 v = *(const floatx4*)(x + off);
     for (int z = 1; z < nsplit; ++z) {
@@ -169,12 +199,7 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += u[e];
     }
-    if (y) *(floatx4*)(y + off) = v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      a[e] += (double)v[e];
-      b[e] += (double)v[e] * (double)v[e];
-    }
+    acc(v, off);
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -434,8 +459,19 @@ SCFLOW_API int scflow_ph_gn_reduce(const float* parts, int nsplit, long long spl
   if (c % 32 || 32 % cpg) return SCFLOW_EUNSUPPORTED;
   if (!aligned16(parts) || (y && !aligned16(y)) || (split_stride & 3)) return SCFLOW_EALIGN;
   dim3 grid(n, c / 32);
-  ph_gn_reduce_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(parts, nsplit, split_stride, y, hw, c,
-                                                             groups, gamma, beta, eps, scale, shift);
+#define SCFLOW_GNR(NS_)                                                                           \
+  ph_gn_reduce_kernel<NS_><<<grid, 256, 0, (hipStream_t)stream>>>(parts, nsplit, split_stride, y, hw, \
+                                                                  c, groups, gamma, beta, eps,       \
+                                                                  scale, shift)
+  switch (nsplit) {
+    case 1: SCFLOW_GNR(1); break;
+    case 2: SCFLOW_GNR(2); break;
+    case 3: SCFLOW_GNR(3); break;
+    case 4: SCFLOW_GNR(4); break;
+    case 8: SCFLOW_GNR(8); break;
+    default: SCFLOW_GNR(0); break;
+  }
+#undef SCFLOW_GNR
   return scflow_launch_status();
 }
 
