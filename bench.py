@@ -360,7 +360,8 @@ def main():
             "data": "synthetic (seeded features, YCB-V-like poses/intrinsics, analytic ellipsoid depth; "
                     "deterministic random-init weights)",
             "config": {"workload": f"SCFlowDecoder forward, {args.batch} pairs/GPU, "
-                                   f"{args.size}x{args.size}, {args.iters} GRU iters (BASELINE configs[1])",
+                                   f"{args.size}x{args.size}, {args.iters} GRU iters (BASELINE "
+                                   f"{'configs[4]' if (args.size, args.iters) == (512, 12) else 'configs[1]' if (args.batch, args.size, args.iters) == (16, 256, 8) else 'custom size'})",
                        "global_batch": args.batch * world, "image": args.size, "iters": args.iters,
                        "launch": "hipGraph replay" if args.graph else "eager",
                        "parallelism": f"dp{world}"},
