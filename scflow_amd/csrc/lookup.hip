@@ -1,15 +1,20 @@
 // a2 — multi-scale pyramid window lookup (CorrLookup, /root/reference/models/utils/corr_lookup.py:102-136).
 //
-// One WAVE per source pixel p (4 per workgroup):
-//  1. 2·L·D lanes compute the sample coordinates of every level once — the reference's own
+// 16 lanes per source pixel p, 16 pixels per workgroup:
+//  1. the pixel's lanes compute the sample coordinates of every level once — the reference's own
 //     arithmetic: centroid (x+flow)/2^l, + window offset, normalise g·2/max(W−1,1)−1 and the
 //     align_corners unnormalise ((g+1)/2)·(W−1), FP contraction off, so each sample's floor()
 //     is grid_sample's;
-//  2. the wave stages, per level, the (D+3)² window around floor(first sample) − 1 in LDS with
-//     zero padding (one-tap margin each side: a rounded sample coordinate can move its floor by
-//     at most one);
-//  3. lanes produce the L·D² outputs (channel k = l·D² + a·D + b samples x+a−r, y+b−r) from LDS
-//     with grid_sample's bilinear weights (nw, ne, sw, se) — contiguous channels-last stores.
+//  2. they stage, per level, a region in LDS with rows of D+3 floats: the whole map with a
+//     zero border when it fits (levels ≥ 2 at SCFlow's 32×32: 10 and 6 rows), else the
+//     (D+3)² window around floor(first sample) − 1 with zero padding (one-tap margin each
+//     side: a rounded sample coordinate can move its floor by at most one) — 480 instead of
+//     576 floats per pixel at r = 4, L = 4, so every pixel of a B=16 batch is resident at once.
+//     The region-relative floor of every (level, axis, index) is computed once here (not
+//     once per sample);
+//  3. the lanes take the L·D (level, column) pairs in turn and produce the D samples of each
+//     (channel k = l·D² + a·D + b samples x+a−r, y+b−r) from LDS with grid_sample's bilinear
+//     weights (nw, ne, sw, se; taps outside the map are zero).
 // The pyramid (≈5.6 MB per pair at 256²) is read through L2 / Infinity Cache.
 // A generic one-thread-per-(p, l, a) kernel remains for L > 4 or r > 6.
 #include "common.h"
@@ -94,23 +99,50 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(
 constexpr int LK_MAXL = 4;
 constexpr int LK_PPW = 4;              // pixels per wave (16 lanes each)
 constexpr int LK_GL = 64 / LK_PPW;     // lanes per pixel
+constexpr int LK_SLOTS = 4 * LK_PPW;   // pixels per workgroup
+
+// LDS region of level l for a pixel, rows of WIN floats: the whole map with a zero border
+// ((h>>l)+2 rows) when it fits in the (D+3)-wide window, else the (D+3)² window.  Returns the
+// floats of one pixel slot (all levels), ≡ 4 mod 8: 16-B aligned slots whose 4 per wave start
+// in different banks.
+__host__ __device__ inline bool lk_whole(int hl, int wl, int win) { return hl + 2 <= win && wl + 2 <= win; }
+__host__ __device__ inline int lk_rows(int hl, int wl, int win) { return lk_whole(hl, wl, win) ? hl + 2 : win; }
+__host__ __device__ inline int lk_slot_floats(int h, int w, int L, int win) {
+  int t = 0;
+  for (int l = 0; l < L; ++l) t += lk_rows(h >> l, w >> l, win) * win;
+  t = (t + 3) & ~3;
+  return (t & 7) ? t : t + 4;
+}
+
+constexpr int LK_OOB = 0x7ffffff0;  // buffer voffset of a zero tap (beyond any num_records)
+
+__device__ __forceinline__ float lk_bload(__amdgpu_buffer_rsrc_t r, int voff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
 
 template <int R>
-__global__ __launch_bounds__(256) void corr_lookup_lds_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void corr_lookup_lds_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
-    float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L) {
+    float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
+    int vec_out) {
 #pragma clang fp contract(off)
   constexpr int D = 2 * R + 1;
   constexpr int WIN = D + 3;
-  constexpr int SLOTS = 4 * LK_PPW;  // pixels per workgroup
-  __shared__ float win[SLOTS][LK_MAXL][WIN][WIN];
-  __shared__ float crd[SLOTS][LK_MAXL][2][D];
+  constexpr int NPR = (LK_MAXL * D + LK_GL - 1) / LK_GL;  // (level, a) pairs per lane
+  extern __shared__ float win[];  // [LK_SLOTS][slot floats]
+  __shared__ float crd[LK_SLOTS][LK_MAXL][2][D];
+  __shared__ int sr[LK_SLOTS][LK_MAXL][2][D];  // region-relative floor of a sample, −1: none
+  __shared__ int org[LK_SLOTS][LK_MAXL][2];    // region origin (map coordinates)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int slot = wave * LK_PPW + lane / LK_GL;  // this lane's pixel slot
-  const int gl = lane % LK_GL;                     // lane within the pixel's group
+  const int ks = lane / LK_GL;                    // pixel slot within the wave
+  const int slot = wave * LK_PPW + ks;
+  const int gl = lane % LK_GL;                    // lane within the pixel's group
   const int P = H * W;
-  const long long gp = (long long)blockIdx.x * SLOTS + slot;  // global pixel n·P + p
-  const bool active = gp < (long long)N * P;
+  const long long NP = (long long)N * P;
+  float* sw = win + slot * lk_slot_floats(H, W, L, WIN);
+  const long long gp0 = (long long)blockIdx.x * LK_SLOTS + wave * LK_PPW;  // wave's first pixel
+  const long long gp = gp0 + ks;                                          // n·P + p
+  const bool active = gp < NP;
   const int n = active ? (int)(gp / P) : 0;
   const int p = active ? (int)(gp % P) : 0;
   const int y = p / W, x = p % W;
@@ -132,80 +164,158 @@ __global__ __launch_bounds__(256) void corr_lookup_lds_kernel(
     crd[slot][l][axis][i] = unnorm_coord(c + (float)(i - R), size);
   }
   __syncthreads();
-  // 2. windows (zero padded), origin = floor(first sample) − 1 per level and axis; every load
-  //    of the pixel's L windows is issued before the LDS writes (one memory latency)
+  // 1b. per (level, axis): the region origin — −1 for a whole map, else floor(first sample) − 1
+  //     (one-tap margin: a rounded sample coordinate moves its floor by at most one), far out
+  //     of the map when the level has no finite samples; per (level, axis, index): the sample's
+  //     region-relative floor
+  for (int t = gl; t < L * 2 * D; t += LK_GL) {
+    const int l = t / (2 * D), axis = (t / D) % 2, i = t % D;
+    const bool whole = lk_whole(H >> l, W >> l, WIN);
+    const float c0x = crd[slot][l][0][0], c0y = crd[slot][l][1][0];
+    const bool fin = isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f && fabsf(c0y) < 1e8f;
+    const float s = crd[slot][l][axis][i];
+    const int o = whole ? -1 : (fin ? (int)floorf(axis == 0 ? c0x : c0y) - 1 : -(1 << 29));
+    sr[slot][l][axis][i] = fin && isfinite(s) ? (int)floorf(s) - o : -1;
+    if (i == 0) org[slot][l][axis] = o;
+  }
+  __syncthreads();
+  // 2. regions (zero padded) through buffer loads (out-of-map taps read as zero, no branches):
+  //    every load of the pixel's L regions is issued before the LDS writes
   constexpr int NW1 = (WIN * WIN + LK_GL - 1) / LK_GL;  // loads per lane per level
   float vals[LK_MAXL][NW1];
-  int oxl[LK_MAXL], oyl[LK_MAXL];
-  bool finl[LK_MAXL];
+  int rn[LK_MAXL], ox[LK_MAXL], oy[LK_MAXL];
+#pragma unroll
+  for (int l = 0; l < LK_MAXL; ++l) {
+    ox[l] = l < L ? org[slot][l][0] : 0;
+    oy[l] = l < L ? org[slot][l][1] : 0;
+  }
   {
     size_t loff = 0;
     int Hl = H, Wl = W;
+    const long long left = NP - gp0;
+    const int npx = left < LK_PPW ? (int)left : LK_PPW;  // pixels of this wave
 #pragma unroll
     for (int l = 0; l < LK_MAXL; ++l) {
       const bool use = l < L;
-      const float* m = pyr + loff + ((size_t)n * P + p) * Hl * Wl;
-      const float c0x = use ? crd[slot][l][0][0] : 0.f, c0y = use ? crd[slot][l][1][0] : 0.f;
-      finl[l] = use && active && isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f &&
-                fabsf(c0y) < 1e8f;
-      oxl[l] = finl[l] ? (int)floorf(c0x) - 1 : 0;
-      oyl[l] = finl[l] ? (int)floorf(c0y) - 1 : 0;
+      const int hw = Hl * Wl;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(pyr + loff + (size_t)gp0 * hw), (short)0, use ? npx * hw * 4 : 0,
+          0x00020000);
+      rn[l] = use ? lk_rows(Hl, Wl, WIN) * WIN : 0;
 #pragma unroll
       for (int j = 0; j < NW1; ++j) {
         const int i = gl + LK_GL * j;
-        const int gx = oxl[l] + i % WIN, gy = oyl[l] + i / WIN;
-        float v = 0.f;
-        if (i < WIN * WIN && finl[l] && gx >= 0 && gx < Wl && gy >= 0 && gy < Hl) v = m[gy * Wl + gx];
-        vals[l][j] = v;
+        const int gx = ox[l] + i % WIN, gy = oy[l] + i / WIN;
+        const bool ok = i < rn[l] && active && gx >= 0 && gx < Wl && gy >= 0 && gy < Hl;
+        vals[l][j] = lk_bload(rs, ok ? (ks * hw + gy * Wl + gx) * 4 : LK_OOB);
       }
-      if (use) loff += (size_t)N * P * Hl * Wl;
+      if (use) loff += (size_t)NP * hw;
       Hl >>= 1;
       Wl >>= 1;
     }
   }
+  {
+    int off = 0;
 #pragma unroll
-  for (int l = 0; l < LK_MAXL; ++l)
+    for (int l = 0; l < LK_MAXL; ++l) {
 #pragma unroll
-    for (int j = 0; j < NW1; ++j) {
-      const int i = gl + LK_GL * j;
-      if (i < WIN * WIN) (&win[slot][l][0][0])[i] = vals[l][j];
+      for (int j = 0; j < NW1; ++j) {
+        const int i = gl + LK_GL * j;
+        if (i < rn[l]) sw[off + i] = vals[l][j];
+      }
+      off += rn[l];
     }
+  }
   __syncthreads();
+  // 3. samples: the pixel's 16 lanes take its L·D (level, a) pairs in turn and produce the D
+  //    samples b of each (channel k = l·D² + a·D + b samples x+a−r, y+b−r); a sample whose
+  //    2×2 taps leave the region is zero (off the map: grid_sample's zero padding).  Every LDS
+  //    read of a pair is issued before its arithmetic (clamped addresses, selects, no branches)
+  int offl[LK_MAXL];
+  {
+    int o = 0;
+#pragma unroll
+    for (int l = 0; l < LK_MAXL; ++l) {
+      offl[l] = o;
+      o += rn[l];
+    }
+  }
+  float res[NPR][D];
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    const int t = gl + LK_GL * q;
+    const bool tv = active && t < L * D;
+    const int l = tv ? t / D : 0, a = tv ? t % D : 0;
+    int off = offl[0], rows = rn[0] / WIN;
+#pragma unroll
+    for (int k = 1; k < LK_MAXL; ++k)
+      if (l == k) { off = offl[k]; rows = rn[k] / WIN; }
+    const int rx = sr[slot][l][0][a];
+    const float ix = crd[slot][l][0][a];
+    int ry[D];
+    float iy[D];
+#pragma unroll
+    for (int b = 0; b < D; ++b) {
+      ry[b] = sr[slot][l][1][b];
+      iy[b] = crd[slot][l][1][b];
+    }
+    const bool okx = tv && rx >= 0 && rx + 1 < WIN;
+    float t00[D], t01[D], t10[D], t11[D];
+    bool ok[D];
+#pragma unroll
+    for (int b = 0; b < D; ++b) {
+      ok[b] = okx && ry[b] >= 0 && ry[b] + 1 < rows;
+      const float* wr = sw + off + (ok[b] ? ry[b] * WIN + rx : 0);
+      t00[b] = wr[0];
+      t01[b] = wr[1];
+      t10[b] = wr[WIN];
+      t11[b] = wr[WIN + 1];
+    }
+    const float ix_w = floorf(ix), ix_e = ix_w + 1.f;
+    const float wxw = ix_e - ix, wxe = ix - ix_w;
+#pragma unroll
+    for (int b = 0; b < D; ++b) {
+      const float iy_n = floorf(iy[b]), iy_s = iy_n + 1.f;
+      const float wyn = iy_s - iy[b], wys = iy[b] - iy_n;
+      float v = 0.f;
+      v += t00[b] * (wxw * wyn);
+      v += t01[b] * (wxe * wyn);
+      v += t10[b] * (wxw * wys);
+      v += t11[b] * (wxe * wys);
+      res[q][b] = ok[b] ? v : 0.f;
+    }
+  }
+  if (vec_out) {
+    // channels-last with a 16-B aligned pixel stride: the pixel's L·D² outputs go through its
+    // own LDS region (only its 16 lanes, one wave, read it) and out as 16-B stores
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const int t = gl + LK_GL * q;
+      if (t < L * D) {
+#pragma unroll
+        for (int b = 0; b < D; ++b) sw[t * D + b] = res[q][b];
+      }
+    }
+    __syncthreads();
+    if (active) {
+      float* o = out + (size_t)gp * out_stride;
+      const int K4 = L * D * D / 4;
+      for (int c = gl; c < K4; c += LK_GL) *(floatx4*)(o + 4 * c) = *(const floatx4*)(sw + 4 * c);
+      for (int c = 4 * K4 + gl; c < L * D * D; c += LK_GL) o[c] = sw[c];
+    }
+    return;
+  }
   if (!active) return;
-  // 3. samples: lane g takes (level, a) pairs g, g+16, …; per pair the x coordinate, x weights
-  //    and window column are computed once for the D samples b of that column
-  const int K = L * D * D;
   float* o = out_layout == SCFLOW_LAYOUT_NHWC ? out + ((size_t)n * P + p) * out_stride
-                                              : out + (size_t)n * K * P + p;
+                                              : out + (size_t)n * L * D * D * P + p;
   const int ostep = out_layout == SCFLOW_LAYOUT_NHWC ? 1 : P;
 #pragma unroll
-  for (int l = 0; l < LK_MAXL; ++l) {
-    if (l >= L) break;
-    for (int a = gl; a < D; a += LK_GL) {
-      const float ix = crd[slot][l][0][a];
-      const bool okx = finl[l] && isfinite(ix);
-      const float ix_w = floorf(ix), ix_e = ix_w + 1.f;
-      const float wxe = ix - ix_w, wxw = ix_e - ix;
-      const int rx = okx ? (int)ix_w - oxl[l] : -1;
-      const bool inx = rx >= 0 && rx + 1 < WIN;
-      float* ol = o + (size_t)(l * D * D + a * D) * ostep;
+  for (int q = 0; q < NPR; ++q) {
+    const int t = gl + LK_GL * q;
+    if (t < L * D) {
 #pragma unroll
-      for (int b = 0; b < D; ++b) {
-        const float iy = crd[slot][l][1][b];
-        float v = 0.f;
-        if (inx && isfinite(iy)) {
-          const float iy_n = floorf(iy), iy_s = iy_n + 1.f;
-          const int ry = (int)iy_n - oyl[l];
-          if (ry >= 0 && ry + 1 < WIN) {
-            const float* wr = &win[slot][l][ry][rx];
-            v += wr[0] * (wxw * (iy_s - iy));
-            v += wr[1] * (wxe * (iy_s - iy));
-            v += wr[WIN] * (wxw * (iy - iy_n));
-            v += wr[WIN + 1] * (wxe * (iy - iy_n));
-          }
-        }
-        ol[(size_t)b * ostep] = v;
-      }
+      for (int b = 0; b < D; ++b) o[(size_t)(t * D + b) * ostep] = res[q][b];
     }
   }
 }
@@ -224,13 +334,21 @@ SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_
   if (out_layout != SCFLOW_LAYOUT_NHWC && out_layout != SCFLOW_LAYOUT_NCHW) return SCFLOW_EINVAL;
   if ((h >> (num_levels - 1)) < 1 || (w >> (num_levels - 1)) < 1) return SCFLOW_EUNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  if (num_levels <= LK_MAXL && radius >= 1 && radius <= 4) {
-    const unsigned blk = (unsigned)(((long long)n * h * w + 4 * LK_PPW - 1) / (4 * LK_PPW));
+  // the LDS kernel addresses one wave's 4 pixel maps of a level through a buffer descriptor
+  // (offsets < 2^31 bytes)
+  if (num_levels <= LK_MAXL && radius >= 1 && radius <= 4 &&
+      (long long)LK_PPW * h * w * 4 < LK_OOB) {
+    const unsigned blk = (unsigned)(((long long)n * h * w + LK_SLOTS - 1) / LK_SLOTS);
+    const int D = 2 * radius + 1;
+    const int sf = lk_slot_floats(h, w, num_levels, D + 3);
+    const size_t lds = sizeof(float) * LK_SLOTS * sf;
+    const int vec = out_layout == SCFLOW_LAYOUT_NHWC && out_stride % 4 == 0 &&
+                    ((uintptr_t)out & 15) == 0 && sf >= num_levels * D * D;
     switch (radius) {
-      case 1: corr_lookup_lds_kernel<1><<<blk, 256, 0, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels); break;
-      case 2: corr_lookup_lds_kernel<2><<<blk, 256, 0, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels); break;
-      case 3: corr_lookup_lds_kernel<3><<<blk, 256, 0, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels); break;
-      default: corr_lookup_lds_kernel<4><<<blk, 256, 0, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels); break;
+      case 1: corr_lookup_lds_kernel<1><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
+      case 2: corr_lookup_lds_kernel<2><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
+      case 3: corr_lookup_lds_kernel<3><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
+      default: corr_lookup_lds_kernel<4><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
     }
     return scflow_launch_status();
   }
