@@ -113,7 +113,7 @@ def time_steps(step, steps, warmup, world, dev):
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
 
-def secondary_rooflines(timers, batch, size):
+def secondary_rooflines(timers, batch, size, fused_tail=True):
     """The other hot-path kernels, timed live like the primary one (same events, same timed
     region): the pyramid lookup and the pose-induced-flow reprojection are HBM/gather-bound
     (algorithmic bytes per launch from SURVEY.md §8(d)), the correlation GEMM is MFMA-bound.
@@ -122,12 +122,15 @@ def secondary_rooflines(timers, batch, size):
     h = w = size // 8
     P = h * w
     lookup_bytes = batch * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
-    flow_bytes = batch * 20 * size * size
+    # pose flow: 16-B point read + 8-B flow write per pixel; the fused tail (pose_step_kernel)
+    # also writes the ×8 flow prediction and mask (12 B per pixel)
+    flow_bytes = batch * (36 if fused_tail else 20) * size * size
     corr_flops = 2.0 * batch * P * P * 256
     out = []
     for name, kernel, bound, amount in (
             ("corr_lookup", "corr_lookup_lds_kernel<4> (a2)", "hbm", lookup_bytes),
-            ("pose_flow", "pose_flow_kernel (a8+a10)", "hbm", flow_bytes),
+            ("pose_flow", "pose_step_kernel (a8+a10+a11)" if fused_tail else "pose_flow_kernel (a8+a10)",
+             "hbm", flow_bytes),
             ("corr_pyramid", "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma", corr_flops)):
         t = timers[name]
         if t.count() == 0:
@@ -377,7 +380,8 @@ def main():
                          "mfma_achieved": round(mfma_achieved, 2),
                          "mfma_frac": round(mfma_achieved / FP32_MFMA_PEAK_TFLOPS, 4)},
         }
-        res["rooflines_secondary"] = secondary_rooflines(timers, args.batch, args.size)
+        res["rooflines_secondary"] = secondary_rooflines(timers, args.batch, args.size,
+                                                       getattr(dec, "fuse_tail", True))
         if e2e is not None:
             res["end_to_end"] = e2e
         if train is not None:

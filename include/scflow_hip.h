@@ -24,6 +24,8 @@
  *   scflow_pose_update_flow  <- the two calls above fused, as used at     scflow_decoder.py:231-244
  *   scflow_flow_downsample   <- 1/8·F.interpolate(flow, 1/8, bilinear, align_corners=True)  scflow_decoder.py:197-198
  *   scflow_flow_upsample     <- 8·F.interpolate(flow+Δflow, ×8) and mask ×8 (same)          scflow_decoder.py:223-228
+ *   scflow_pose_step         <- one iteration's tail fused: pose update + pose flow + the ×8
+ *                               prediction + the next iteration's ↓8 flow   scflow_decoder.py:197-198, 223-244
  *   scflow_transpose         <- layout plumbing (NCHW <-> channels-last slices), no reference equivalent
  *   scflow_ph_*              <- MultiClassPoseHead.forward                models/head/pose_head.py:201-211
  *   scflow_enc_*             <- RAFTEncoder.forward (Basic; IN / BN)      models/encoder/raft_encoder.py:286-314
@@ -157,6 +159,18 @@ int scflow_flow_downsample(const float* flow, float* out0, int s0, float* out1, 
 int scflow_flow_upsample(const float* lr, const float* delta, const float* mask, float* flow_out,
                          float* mask_out, int n, int h, int w, int H, int W, float value_scale,
                          void* stream);
+
+/* One launch = scflow_pose_update_flow(drot6 .. invalid_num; flow is [n][2][H][W]) +
+ * scflow_flow_upsample(lr, delta, mask, flow_up, mask_up, n, h, w, H, W, up_scale) when flow_up
+ * != NULL + scflow_flow_downsample(flow, lr_next, s_next, hx_next, s_hx, n, H, W, h, w,
+ * down_scale) when lr_next != NULL (the ↓8 flow is computed from the new pose directly, bit-
+ * identical to downsampling `flow`).  lr_next must not alias lr. */
+int scflow_pose_step(const float* drot6, const float* dt, const float* R_src, const float* t_src,
+                     const float* K, const float* points, float* R_dst, float* t_dst, float* flow,
+                     int n, int H, int W, float weight, int depth_transform, float invalid_num,
+                     const float* lr, const float* delta, const float* mask, float* flow_up,
+                     float* mask_up, float* lr_next, int s_next, float* hx_next, int s_hx, int h,
+                     int w, float up_scale, float down_scale, void* stream);
 
 /* out[n·ons + b·obs + a] = in[n·ins + a·ias + b] for a < A, b < B (batched 2-D transpose; e.g.
  * NCHW -> a channel slice of an NHWC buffer, or back). */

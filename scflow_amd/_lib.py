@@ -116,6 +116,8 @@ SIGNATURES = {
                                        c_int, c_float, c_vp]),
     "scflow_flow_upsample": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
                                      c_float, c_vp]),
+    "scflow_pose_step": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_float, c_int, c_float] +
+                         [c_vp] * 6 + [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_vp]),
     "scflow_transpose": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_int, c_ll, c_int, c_vp]),
     "scflow_ph_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
     "scflow_ph_conv_pack": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),

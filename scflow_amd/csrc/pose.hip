@@ -112,15 +112,37 @@ __global__ __launch_bounds__(256) void lift_kernel(const float* __restrict__ dep
   }
 }
 
-// flow[n][0/1][p] from pose (R,t) in LDS; `upd` != 0: compute (R,t) from the delta first
-__global__ __launch_bounds__(256) void pose_flow_kernel(
-    const float* __restrict__ drot6, const float* __restrict__ dtv, const float* __restrict__ Rsrc,
-    const float* __restrict__ tsrc, const float* __restrict__ K, const floatx4* __restrict__ pts,
-    float* __restrict__ Rout, float* __restrict__ tout, float* __restrict__ flow, int H, int W,
-    float weight, int depth_transform, float invalid, int upd) {
+// flow of one pixel p (point P = {X, Y, Z, valid}) under the pose in LDS (R[9] t[3] K[9])
+__device__ __forceinline__ void proj_flow(const float* sh, const floatx4 P, int X, int Y,
+                                          float invalid, float& fx, float& fy) {
 #pragma clang fp contract(off)
-  __shared__ float sh[21];  // R[9] t[3] K[9]
-  const int n = blockIdx.y;
+  fx = invalid;
+  fy = invalid;
+  if (P[3] != 0.f) {
+    float c[3], u[3];
+    for (int r = 0; r < 3; ++r) {
+      float s = sh[r * 3 + 0] * P[0];
+      s += sh[r * 3 + 1] * P[1];
+      s += sh[r * 3 + 2] * P[2];
+      c[r] = s + sh[9 + r];
+    }
+    for (int r = 0; r < 3; ++r) {
+      float s = sh[12 + r * 3 + 0] * c[0];
+      s += sh[12 + r * 3 + 1] * c[1];
+      s += sh[12 + r * 3 + 2] * c[2];
+      u[r] = s;
+    }
+    fx = u[0] / u[2] - (float)X;
+    fy = u[1] / u[2] - (float)Y;
+  }
+}
+
+// the pose of image n into LDS (R[9] t[3] K[9]); `upd` != 0: (R,t) from the delta first, and
+// workgroup x == 0 stores it
+__device__ __forceinline__ void pose_prologue(float* sh, int n, const float* drot6, const float* dtv,
+                                              const float* Rsrc, const float* tsrc, const float* K,
+                                              float* Rout, float* tout, float weight,
+                                              int depth_transform, int upd) {
   if (threadIdx.x == 0) {
     if (upd) {
       pose_update_one(drot6 + 6 * n, dtv + 3 * n, Rsrc + 9 * n, tsrc + 3 * n, sh, sh + 9, weight,
@@ -136,27 +158,21 @@ __global__ __launch_bounds__(256) void pose_flow_kernel(
     for (int k = 0; k < 9; ++k) sh[12 + k] = K[9 * n + k];
   }
   __syncthreads();
+}
+
+// flow[n][0/1][p] from pose (R,t) in LDS; `upd` != 0: compute (R,t) from the delta first
+__global__ __launch_bounds__(256) void pose_flow_kernel(
+    const float* __restrict__ drot6, const float* __restrict__ dtv, const float* __restrict__ Rsrc,
+    const float* __restrict__ tsrc, const float* __restrict__ K, const floatx4* __restrict__ pts,
+    float* __restrict__ Rout, float* __restrict__ tout, float* __restrict__ flow, int H, int W,
+    float weight, int depth_transform, float invalid, int upd) {
+  __shared__ float sh[21];  // R[9] t[3] K[9]
+  const int n = blockIdx.y;
+  pose_prologue(sh, n, drot6, dtv, Rsrc, tsrc, K, Rout, tout, weight, depth_transform, upd);
   const int HW = H * W;
   for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
-    const floatx4 P = pts[(size_t)n * HW + p];
-    float fx = invalid, fy = invalid;
-    if (P[3] != 0.f) {
-      float c[3], u[3];
-      for (int r = 0; r < 3; ++r) {
-        float s = sh[r * 3 + 0] * P[0];
-        s += sh[r * 3 + 1] * P[1];
-        s += sh[r * 3 + 2] * P[2];
-        c[r] = s + sh[9 + r];
-      }
-      for (int r = 0; r < 3; ++r) {
-        float s = sh[12 + r * 3 + 0] * c[0];
-        s += sh[12 + r * 3 + 1] * c[1];
-        s += sh[12 + r * 3 + 2] * c[2];
-        u[r] = s;
-      }
-      fx = u[0] / u[2] - (float)(p % W);
-      fy = u[1] / u[2] - (float)(p / W);
-    }
+    float fx, fy;
+    proj_flow(sh, pts[(size_t)n * HW + p], p % W, p / W, invalid, fx, fy);
     flow[((size_t)n * 2 + 0) * HW + p] = fx;
     flow[((size_t)n * 2 + 1) * HW + p] = fy;
   }
@@ -243,6 +259,73 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
   }
   if (mask && mo)
     mo[(size_t)n * H * W + (size_t)Y * W + X] = bilerp(mask[i00], mask[i01], mask[i10], mask[i11], ly, lx);
+}
+
+// One refinement iteration's tail in one launch (decoder a8 + a10 + a11): pose update →
+// pose-induced flow (workgroups x < bf, as pose_flow_kernel), the iteration's 8× upsampled
+// flow/mask prediction of the same full-resolution pixels (as upsample_kernel, from the
+// iteration's low-resolution flow `lr`), and — workgroups x ≥ bf — the NEXT iteration's ↓8 flow
+// (as downsample_kernel) computed straight from the new pose: each low-resolution pixel
+// reprojects the 4 full-resolution points its bilinear tap reads (the same arithmetic as the
+// stored flow), so nothing waits for the full-resolution flow.  lr_next must not alias lr.
+__global__ __launch_bounds__(256) void pose_step_kernel(
+    const float* __restrict__ drot6, const float* __restrict__ dtv, const float* __restrict__ Rsrc,
+    const float* __restrict__ tsrc, const float* __restrict__ K, const floatx4* __restrict__ pts,
+    float* __restrict__ Rout, float* __restrict__ tout, float* __restrict__ flow, int H, int W,
+    float weight, int depth_transform, float invalid, const float* __restrict__ lr,
+    const float* __restrict__ delta, const float* __restrict__ mask, float* __restrict__ fo,
+    float* __restrict__ mo, float* __restrict__ o0, int s0, float* __restrict__ o1, int s1, int h,
+    int w, float up_scale, float down_scale, int bf) {
+#pragma clang fp contract(off)
+  __shared__ float sh[21];
+  const int n = blockIdx.y;
+  pose_prologue(sh, n, drot6, dtv, Rsrc, tsrc, K, Rout, tout, weight, depth_transform, 1);
+  const int HW = H * W;
+  if ((int)blockIdx.x < bf) {
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += bf * 256) {
+      const int X = p % W, Y = p / W;
+      float fx, fy;
+      proj_flow(sh, pts[(size_t)n * HW + p], X, Y, invalid, fx, fy);
+      flow[((size_t)n * 2 + 0) * HW + p] = fx;
+      flow[((size_t)n * 2 + 1) * HW + p] = fy;
+      if (fo) {
+        const Lin ly = lin_src(Y, h, H), lx = lin_src(X, w, W);
+        const size_t b = (size_t)n * h * w;
+        const size_t i00 = b + (size_t)ly.i0 * w + lx.i0, i01 = b + (size_t)ly.i0 * w + lx.i1;
+        const size_t i10 = b + (size_t)ly.i1 * w + lx.i0, i11 = b + (size_t)ly.i1 * w + lx.i1;
+        for (int c = 0; c < 2; ++c) {
+          float v00 = lr[i00 * 2 + c], v01 = lr[i01 * 2 + c], v10 = lr[i10 * 2 + c],
+                v11 = lr[i11 * 2 + c];
+          if (delta) {
+            v00 = v00 + delta[i00 * 2 + c];
+            v01 = v01 + delta[i01 * 2 + c];
+            v10 = v10 + delta[i10 * 2 + c];
+            v11 = v11 + delta[i11 * 2 + c];
+          }
+          fo[((size_t)n * 2 + c) * HW + p] = up_scale * bilerp(v00, v01, v10, v11, ly, lx);
+        }
+        if (mask && mo)
+          mo[(size_t)n * HW + p] = bilerp(mask[i00], mask[i01], mask[i10], mask[i11], ly, lx);
+      }
+    }
+    return;
+  }
+  const int bl = gridDim.x - bf;
+  for (int q = (blockIdx.x - bf) * 256 + threadIdx.x; q < h * w; q += bl * 256) {
+    const int x = q % w, y = q / w;
+    const Lin ly = lin_src(y, H, h), lx = lin_src(x, W, w);
+    float f[4][2];  // [dy·2 + dx][axis]
+    for (int k = 0; k < 4; ++k) {
+      const int cy = (k >> 1) ? ly.i1 : ly.i0, cx = (k & 1) ? lx.i1 : lx.i0;
+      proj_flow(sh, pts[(size_t)n * HW + (size_t)cy * W + cx], cx, cy, invalid, f[k][0], f[k][1]);
+    }
+    const size_t idx = (size_t)n * h * w + q;
+    for (int a = 0; a < 2; ++a) {
+      const float v = down_scale * bilerp(f[0][a], f[1][a], f[2][a], f[3][a], ly, lx);
+      o0[idx * s0 + a] = v;
+      if (o1) o1[idx * s1 + a] = v;
+    }
+  }
 }
 
 // batched 2-D transpose through a padded LDS tile
@@ -334,6 +417,30 @@ SCFLOW_API int scflow_flow_upsample(const float* lr, const float* delta, const f
   const long long total = (long long)n * H * W;
   upsample_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
       lr, delta, mask, flow_out, mask_out, n, h, w, H, W, value_scale);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_pose_step(const float* drot6, const float* dt, const float* R_src,
+                                const float* t_src, const float* K, const float* points,
+                                float* R_dst, float* t_dst, float* flow, int n, int H, int W,
+                                float weight, int depth_transform, float invalid_num,
+                                const float* lr, const float* delta, const float* mask,
+                                float* flow_up, float* mask_up, float* lr_next, int s_next,
+                                float* hx_next, int s_hx, int h, int w, float up_scale,
+                                float down_scale, void* stream) {
+  if (!drot6 || !dt || !R_src || !t_src || !K || !points || !R_dst || !t_dst || !flow || n <= 0 ||
+      H <= 0 || W <= 0 || (depth_transform != 0 && depth_transform != 1))
+    return SCFLOW_EINVAL;
+  if ((flow_up || lr_next) && (h <= 0 || w <= 0)) return SCFLOW_EINVAL;
+  if (flow_up && !lr) return SCFLOW_EINVAL;
+  if (lr_next && (s_next < 2 || (hx_next && s_hx < 2) || lr_next == lr)) return SCFLOW_EINVAL;
+  if (!aligned16(points)) return SCFLOW_EALIGN;
+  const int bf = ceil_div((long long)H * W, 256) < 256 ? ceil_div((long long)H * W, 256) : 256;
+  const int bl = lr_next ? (ceil_div((long long)h * w, 256) < 64 ? ceil_div((long long)h * w, 256) : 64) : 0;
+  pose_step_kernel<<<dim3(bf + bl, n), 256, 0, (hipStream_t)stream>>>(
+      drot6, dt, R_src, t_src, K, (const floatx4*)points, R_dst, t_dst, flow, H, W, weight,
+      depth_transform, invalid_num, lr, delta, mask, flow_up, mask_up, lr_next, s_next, hx_next,
+      s_hx, h, w, up_scale, down_scale, bf);
   return scflow_launch_status();
 }
 

@@ -221,17 +221,20 @@ class SCFlowDecoder(nn.Module):
         # Δflow encoder.  Every buffer is allocated above on the main stream and outlives the
         # forward, and the main stream always waits for the side branch before reusing them.
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev)
+        two = getattr(self, "side_stream", True)
+        side = self._side_stream(dev) if two else main
 
         def fork():
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
+            if two:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
 
         def join():
-            ev = torch.cuda.Event()
-            ev.record(side)
-            main.wait_event(ev)
+            if two:
+                ev = torch.cuda.Event()
+                ev.record(side)
+                main.wait_event(ev)
 
         # Host path: the launches that read and write the same persistent buffers in every
         # iteration are recorded on the first iteration (ops.binding: argument structs built
@@ -256,6 +259,12 @@ class SCFlowDecoder(nn.Module):
                                       ctx_map=ctx_map, cxt_channels=xc)
         o_drot = torch.empty(iters, N, self.pose_pred.rotation_out_channels, device=dev, dtype=f32)
         o_dt = torch.empty(iters, N, 3, device=dev, dtype=f32)
+        # Fused iteration tail (no masking): one launch does the pose update, the pose flow, this
+        # iteration's ×8 prediction (from F2) and the next iteration's ↓8 flow (into the other
+        # F2 buffer, computed from the new pose).  F2 alternates between two buffers, so the
+        # recorded launches that read it (lookup, flow branch) are recorded once per parity.
+        fuse_tail = getattr(self, "fuse_tail", True) and not (self.mask_flow or self.mask_corr)
+        F2s = [F2, torch.empty_like(F2)] if fuse_tail else [F2, F2]
         flow_in = F2 * mask_lr if self.mask_flow else F2
 
         def seg_flow_branch():
@@ -292,19 +301,25 @@ class SCFlowDecoder(nn.Module):
             pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep))
 
         for it in range(iters):
-            # a11 ↓: flow at feature resolution → F2 (and the motion-feature flow channels)
-            ops.flow_downsample(flow_full, Chan.whole(F2), h, w, 1.0 / scale,
-                                out1=None if self.mask_flow else hx_flow)
+            par = f"{it % 2}" if fuse_tail else ""
+            F2 = F2s[it % 2]
+            if not self.mask_flow:
+                flow_in = F2
+            # a11 ↓: flow at feature resolution → F2 (and the motion-feature flow channels); the
+            # fused tail of the previous iteration already wrote it
+            if not fuse_tail or it == 0:
+                ops.flow_downsample(flow_full, Chan.whole(F2), h, w, 1.0 / scale,
+                                    out1=None if self.mask_flow else hx_flow)
             if self.mask_flow:
                 torch.mul(F2, mask_lr, out=flow_in)
                 HX[:, hx_c - 2:].copy_(flow_in)
             # a3 (flow branch) on the side stream
             fork()
             with torch.cuda.stream(side):
-                segment("flow_branch", seg_flow_branch)
+                segment("flow_branch" + par, seg_flow_branch)
             # a2 + a3 (correlation branch)
             self._hook("corr_lookup", True)
-            segment("lookup", seg_lookup)
+            segment("lookup" + par, seg_lookup)
             self._hook("corr_lookup", False)
             if self.mask_corr:
                 CORR.mul_(mask_lr)
@@ -328,13 +343,26 @@ class SCFlowDecoder(nn.Module):
             segment("pose_trunk", seg_pose_trunk)
             drot, dtr = o_drot[it], o_dt[it]
             self.pose_pred.heads_hip(pose_x[0], label, drot, dtr)
-            # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
-            ops.flow_upsample(F2, D2, MASK, N, h, w, H, W, float(scale), o_flow_pred[it], o_mask[it])
-            # a8 + a10: pose update + pose-induced flow (one launch)
-            self._hook("pose_flow", True)
-            ops.pose_update_flow(drot, dtr, R_prev, t_prev, K, points, o_R[it], o_t[it],
-                                 o_flow_pose[it], invalid, depth_transform=self.depth_transform)
-            self._hook("pose_flow", False)
+            if fuse_tail:
+                # a8 + a10 + a11 ↑ (+ the next iteration's a11 ↓): one launch
+                last = it == iters - 1
+                self._hook("pose_flow", True)
+                ops.pose_step(drot, dtr, R_prev, t_prev, K, points, o_R[it], o_t[it],
+                              o_flow_pose[it], invalid, F2, D2, MASK, o_flow_pred[it], o_mask[it],
+                              h, w, float(scale),
+                              lr_next=None if last else Chan.whole(F2s[(it + 1) % 2]),
+                              hx_next=None if last else hx_flow,
+                              depth_transform=self.depth_transform)
+                self._hook("pose_flow", False)
+            else:
+                # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
+                ops.flow_upsample(F2, D2, MASK, N, h, w, H, W, float(scale), o_flow_pred[it],
+                                  o_mask[it])
+                # a8 + a10: pose update + pose-induced flow (one launch)
+                self._hook("pose_flow", True)
+                ops.pose_update_flow(drot, dtr, R_prev, t_prev, K, points, o_R[it], o_t[it],
+                                     o_flow_pose[it], invalid, depth_transform=self.depth_transform)
+                self._hook("pose_flow", False)
             R_prev, t_prev = o_R[it], o_t[it]
             flow_full = o_flow_pose[it]
             drots.append(drot)

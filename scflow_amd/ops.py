@@ -349,6 +349,31 @@ def pose_update_flow(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, 
         w, float(weight), 0 if depth_transform == "exp" else 1, float(invalid_num))
 
 
+def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points: Tensor,
+              R_out: Tensor, t_out: Tensor, flow_out: Tensor, invalid_num: float,
+              lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], flow_up: Tensor,
+              mask_up: Optional[Tensor], h: int, w: int, up_scale: float,
+              lr_next: Optional[Chan] = None, hx_next: Optional[Chan] = None,
+              weight: float = 10.0, depth_transform: str = "exp") -> None:
+    """One launch: ``pose_update_flow`` + ``flow_upsample(lr, delta, mask → flow_up, mask_up)``
+    + (if ``lr_next``) the next iteration's ``flow_downsample`` of the new pose flow into
+    ``lr_next`` / ``hx_next``, computed from the pose directly (scflow_pose_step)."""
+    for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t), ("K", K), ("points", points),
+                  ("R_out", R_out), ("t_out", t_out), ("flow_out", flow_out), ("lr", lr),
+                  ("flow_up", flow_up)):
+        _require(x, nm)
+    n, H, W, _ = points.shape
+    if lr_next is not None and lr_next.buf.data_ptr() == lr.data_ptr():
+        raise ValueError("pose_step: lr_next must not alias lr")
+    _launch("scflow_pose_step", drot,
+        _p(drot), _p(dt), _p(R), _p(t), _p(K), _p(points), _p(R_out), _p(t_out), _p(flow_out), n,
+        H, W, float(weight), 0 if depth_transform == "exp" else 1, float(invalid_num), _p(lr),
+        _p(delta), _p(mask), _p(flow_up), _p(mask_up),
+        None if lr_next is None else lr_next.ptr, 0 if lr_next is None else lr_next.stride,
+        None if hx_next is None else hx_next.ptr, 0 if hx_next is None else hx_next.stride,
+        h, w, float(up_scale), 1.0 / float(up_scale))
+
+
 # ------------------------------------------------------------------------------- resampling
 def flow_downsample(flow: Tensor, out0: Chan, h: int, w: int, value_scale: float,
                     out1: Optional[Chan] = None) -> None:

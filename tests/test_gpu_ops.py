@@ -301,6 +301,53 @@ def test_pose_full_res_vs_oracle(ops):
     assert ((fl.cpu() == 0) == ~valid[:, None].expand(-1, 2, -1, -1)).all()
 
 
+@pytest.mark.parametrize("S,s,nxt", [(256, 32, True), (256, 32, False), (128, 16, True)])
+def test_pose_step_matches_separate_launches(ops, S, s, nxt):
+    """scflow_pose_step (the decoder's fused iteration tail) is bit-identical to
+    pose_update_flow + flow_upsample + flow_downsample of the new flow."""
+    from scflow_amd import synthetic
+    n = 3
+    sc = synthetic.make_scene(n, S, seed=5)
+    R0, t0, K, depth = (t(sc[k]).cuda() for k in ("ref_rotation", "ref_translation", "internel_k",
+                                                   "depth"))
+    g = torch.Generator().manual_seed(8)
+    drot = (torch.tensor([[1.0, 0, 0, 0, 1.0, 0]]).repeat(n, 1) +
+            0.03 * torch.randn(n, 6, generator=g)).cuda()
+    dt = (0.05 * torch.randn(n, 3, generator=g)).cuda()
+    pts = ops.lift_points(depth, K, R0, t0)
+    lr = torch.randn(n * s * s, 2, generator=g).cuda()
+    delta = torch.randn(n * s * s, 2, generator=g).cuda()
+    mask = torch.rand(n * s * s, 1, generator=g).cuda()
+    scale = S // s
+    # separate launches
+    Ra, ta = torch.empty(n, 3, 3, device="cuda"), torch.empty(n, 3, device="cuda")
+    fa = torch.empty(n, 2, S, S, device="cuda")
+    ops.pose_update_flow(drot, dt, R0, t0, K, pts, Ra, ta, fa, 400.0)
+    upa, ma = torch.empty(n, 2, S, S, device="cuda"), torch.empty(n, 1, S, S, device="cuda")
+    ops.flow_upsample(lr, delta, mask, n, s, s, S, S, float(scale), upa, ma)
+    nxa, hxa = torch.empty(n * s * s, 2, device="cuda"), torch.zeros(n * s * s, 6, device="cuda")
+    ops.flow_downsample(fa, ops.Chan.whole(nxa), s, s, 1.0 / scale, out1=ops.Chan(hxa, 4, 2))
+    # one launch
+    Rb, tb = torch.empty_like(Ra), torch.empty_like(ta)
+    fb, upb, mb = torch.empty_like(fa), torch.empty_like(upa), torch.empty_like(ma)
+    nxb, hxb = torch.full_like(nxa, 7.0), torch.zeros_like(hxa)
+    ops.pose_step(drot, dt, R0, t0, K, pts, Rb, tb, fb, 400.0, lr, delta, mask, upb, mb, s, s,
+                  float(scale), lr_next=ops.Chan.whole(nxb) if nxt else None,
+                  hx_next=ops.Chan(hxb, 4, 2) if nxt else None)
+    torch.cuda.synchronize()
+    for a, b, nm in ((Ra, Rb, "R"), (ta, tb, "t"), (fa, fb, "flow"), (upa, upb, "flow ×8"),
+                     (ma, mb, "mask ×8")):
+        assert torch.equal(a, b), nm
+    if nxt:
+        assert torch.equal(nxa, nxb), "next ↓8 flow"
+        assert torch.equal(hxa, hxb), "next ↓8 flow (second output)"
+    else:
+        assert (nxb == 7.0).all()
+    with pytest.raises(ValueError):
+        ops.pose_step(drot, dt, R0, t0, K, pts, Rb, tb, fb, 400.0, lr, delta, mask, upb, mb, s, s,
+                      float(scale), lr_next=ops.Chan.whole(lr))
+
+
 @pytest.mark.parametrize("S,s", [(256, 32), (512, 64), (100, 13)])
 def test_flow_resampling(ops, S, s):
     g = torch.Generator().manual_seed(4)

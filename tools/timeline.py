@@ -1,7 +1,7 @@
 """Per-iteration kernel timeline from a rocprofv3 kernel-trace db (both streams).
 
 usage: python tools/timeline.py DB [--skip-forwards K] [--iteration I]
-Finds SCFlowDecoder iterations by the pose_flow kernel (last launch of an iteration) and
+Finds SCFlowDecoder iterations by the pose_flow / pose_step kernel (last launch of an iteration) and
 prints, for one iteration, every kernel: start offset, duration, stream, gap to the previous
 kernel on any stream; then the iteration's wall time, busy time (union of kernel intervals)
 and idle gaps.
@@ -24,7 +24,7 @@ def main():
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     rows = list(con.execute("select name, start, end, stream_id, queue_id from kernels order by start"))
-    ends = [i for i, r in enumerate(rows) if "pose_flow_kernel" in r[0]]
+    ends = [i for i, r in enumerate(rows) if "pose_flow_kernel" in r[0] or "pose_step_kernel" in r[0]]
     it = a.iteration
     lo, hi = ends[it - 1] + 1, ends[it] + 1
     seg = rows[lo:hi]
