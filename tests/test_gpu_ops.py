@@ -83,6 +83,29 @@ def test_corr_lookup_random(ops, n, h, w):
     assert (wide[:, :4] == 7).all() and (wide[:, 4 + K:] == 7).all()
 
 
+@pytest.mark.parametrize("levels,radius,h,w", [(3, 2, 24, 40), (2, 3, 16, 16), (4, 1, 32, 48),
+                                               (1, 4, 12, 12)])
+def test_corr_lookup_levels_radii(ops, levels, radius, h, w):
+    """Other pyramid depths / radii: whole-map LDS regions (maps narrower than the window) next
+    to windowed ones, and channel counts L·(2r+1)² that are not a multiple of 4 (the 16-B store
+    path's scalar tail), channels-last into a wider buffer."""
+    g = torch.Generator().manual_seed(11)
+    n = 2
+    f1 = torch.randn(n, 8, h, w, generator=g)
+    f2 = torch.randn(n, 8, h, w, generator=g)
+    flow = (torch.rand(n, 2, h, w, generator=g) - 0.5) * 1.5 * h
+    buf, lv = ops.corr_pyramid(f1.cuda(), f2.cuda(), levels)
+    ref = orc.corr_lookup([x.cpu() for x in lv], flow, radius)
+    K = levels * (2 * radius + 1) ** 2
+    for off in (0, 4):
+        wide = torch.full((n * h * w, (K + 15) // 4 * 4), 7.0, device="cuda")  # 16-B pixel stride
+        ops.corr_lookup(buf, flow.permute(0, 2, 3, 1).contiguous().cuda(), n, h, w, levels, radius,
+                        out=ops.Chan(wide, off, K), flow_layout="nhwc")
+        got = wide[:, off:off + K].view(n, h, w, K).permute(0, 3, 1, 2)
+        close(got, ref, 1e-5, 1e-5, f"lookup L={levels} r={radius} off={off}")
+        assert (wide[:, :off] == 7).all() and (wide[:, off + K:] == 7).all()
+
+
 # ------------------------------------------------------------------------------ convs
 def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0, bk=None):
     from scflow_amd.modules import ConvRunner
