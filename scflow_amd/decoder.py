@@ -224,17 +224,18 @@ class SCFlowDecoder(nn.Module):
         two = getattr(self, "side_stream", True)
         side = self._side_stream(dev) if two else main
 
+        # two events reused every iteration (a wait captures the event's state when issued)
+        ev_fork, ev_join = (torch.cuda.Event(), torch.cuda.Event()) if two else (None, None)
+
         def fork():
             if two:
-                ev = torch.cuda.Event()
-                ev.record(main)
-                side.wait_event(ev)
+                ev_fork.record(main)
+                side.wait_event(ev_fork)
 
         def join():
             if two:
-                ev = torch.cuda.Event()
-                ev.record(side)
-                main.wait_event(ev)
+                ev_join.record(side)
+                main.wait_event(ev_join)
 
         # Host path: the launches that read and write the same persistent buffers in every
         # iteration are recorded on the first iteration (ops.binding: argument structs built
@@ -296,6 +297,7 @@ class SCFlowDecoder(nn.Module):
             run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe)
 
         pose_x = []
+        tail_calls = None  # fused tail: per-iteration (heads, pose_step) launches, built once
 
         def seg_pose_trunk():
             pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep))
@@ -342,19 +344,37 @@ class SCFlowDecoder(nn.Module):
             # a7 pose head on cat[h, Δflow feat, mask feat] (two channel sources, no concat)
             segment("pose_trunk", seg_pose_trunk)
             drot, dtr = o_drot[it], o_dt[it]
-            self.pose_pred.heads_hip(pose_x[0], label, drot, dtr)
             if fuse_tail:
-                # a8 + a10 + a11 ↑ (+ the next iteration's a11 ↓): one launch
-                last = it == iters - 1
+                # a8 + a10 + a11 ↑ (+ the next iteration's a11 ↓): one launch.  The heads and
+                # this launch take per-iteration pointers; their argument lists for every
+                # iteration are built once (after the trunk's first pass) and replayed as one
+                # ctypes call each, like the recorded segments
+                if tail_calls is None:
+                    tail_calls = []
+                    Rp, tp = R_prev, t_prev
+                    for j in range(iters):
+                        last = j == iters - 1
+                        hc, pc = [], []
+                        with ops.binding(hc, run=False):
+                            self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
+                        with ops.binding(pc, run=False):
+                            ops.pose_step(o_drot[j], o_dt[j], Rp, tp, K, points, o_R[j], o_t[j],
+                                          o_flow_pose[j], invalid, F2s[j % 2], D2, MASK,
+                                          o_flow_pred[j], o_mask[j], h, w, float(scale),
+                                          lr_next=None if last else Chan.whole(F2s[(j + 1) % 2]),
+                                          hx_next=None if last else hx_flow,
+                                          depth_transform=self.depth_transform)
+                        tail_calls.append((hc, pc))
+                        Rp, tp = o_R[j], o_t[j]
+                hc, pc = tail_calls[it]
+                for c in hc:
+                    c()
                 self._hook("pose_flow", True)
-                ops.pose_step(drot, dtr, R_prev, t_prev, K, points, o_R[it], o_t[it],
-                              o_flow_pose[it], invalid, F2, D2, MASK, o_flow_pred[it], o_mask[it],
-                              h, w, float(scale),
-                              lr_next=None if last else Chan.whole(F2s[(it + 1) % 2]),
-                              hx_next=None if last else hx_flow,
-                              depth_transform=self.depth_transform)
+                for c in pc:
+                    c()
                 self._hook("pose_flow", False)
             else:
+                self.pose_pred.heads_hip(pose_x[0], label, drot, dtr)
                 # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
                 ops.flow_upsample(F2, D2, MASK, N, h, w, H, W, float(scale), o_flow_pred[it],
                                   o_mask[it])

@@ -48,24 +48,27 @@ class BoundCall:
 
 
 _BINDING: Optional[list] = None
+_BINDING_RUN = True
 
 
 class binding:
     """``with ops.binding(calls):`` — the wrappers below record their launch as a ``BoundCall``
     into ``calls`` and ALSO run it (so the first pass computes; later passes replay ``calls``,
-    costing one ctypes call per launch instead of the wrapper's Python)."""
+    costing one ctypes call per launch instead of the wrapper's Python).  ``run=False`` only
+    records (the launches are replayed later; their buffers must outlive the replay)."""
 
-    def __init__(self, calls: list) -> None:
-        self.calls = calls
+    def __init__(self, calls: list, run: bool = True) -> None:
+        self.calls, self.run = calls, run
 
     def __enter__(self):
-        global _BINDING
+        global _BINDING, _BINDING_RUN
         self._prev, _BINDING = _BINDING, self.calls
+        self._prev_run, _BINDING_RUN = _BINDING_RUN, self.run
         return self.calls
 
     def __exit__(self, *exc):
-        global _BINDING
-        _BINDING = self._prev
+        global _BINDING, _BINDING_RUN
+        _BINDING, _BINDING_RUN = self._prev, self._prev_run
 
 
 def _launch(name: str, dev_tensor: Tensor, *args) -> None:
@@ -73,7 +76,8 @@ def _launch(name: str, dev_tensor: Tensor, *args) -> None:
     if _BINDING is not None:
         bc = BoundCall(fn, args, dev_tensor.device.index, name)
         _BINDING.append(bc)
-        bc()
+        if _BINDING_RUN:
+            bc()
         return
     check(fn(*args, _stream(dev_tensor)), name)
 
