@@ -89,6 +89,11 @@ class SCFlowDecoder(nn.Module):
         self.kernel_hooks: Dict[str, object] = {}
         # compute the context features' (loop-invariant) GRU contribution once per forward
         self.hoist_context = True
+        # independent branches on a second HIP stream (else everything on the current stream)
+        self.side_stream = True
+        # the iteration's tail (pose update, pose flow, ×8 prediction, next ↓8 flow) as one
+        # launch (scflow_pose_step); only without flow/correlation masking
+        self.fuse_tail = True
 
     # ------------------------------------------------------------------ helpers
     def _hidden_heads(self):
@@ -221,7 +226,7 @@ class SCFlowDecoder(nn.Module):
         # Δflow encoder.  Every buffer is allocated above on the main stream and outlives the
         # forward, and the main stream always waits for the side branch before reusing them.
         main = torch.cuda.current_stream(dev)
-        two = getattr(self, "side_stream", True)
+        two = self.side_stream
         side = self._side_stream(dev) if two else main
 
         # two events reused every iteration (a wait captures the event's state when issued)
@@ -264,7 +269,7 @@ class SCFlowDecoder(nn.Module):
         # iteration's ×8 prediction (from F2) and the next iteration's ↓8 flow (into the other
         # F2 buffer, computed from the new pose).  F2 alternates between two buffers, so the
         # recorded launches that read it (lookup, flow branch) are recorded once per parity.
-        fuse_tail = getattr(self, "fuse_tail", True) and not (self.mask_flow or self.mask_corr)
+        fuse_tail = self.fuse_tail and not (self.mask_flow or self.mask_corr)
         F2s = [F2, torch.empty_like(F2)] if fuse_tail else [F2, F2]
         flow_in = F2 * mask_lr if self.mask_flow else F2
 
