@@ -172,6 +172,14 @@ int scflow_pose_step(const float* drot6, const float* dt, const float* R_src, co
                      float* mask_up, float* lr_next, int s_next, float* hx_next, int s_hx, int h,
                      int w, float up_scale, float down_scale, void* stream);
 
+/* Cross-stream ordering on one device (the decoder's side stream): events without timing and
+ * with a device-scope release (hipEventDisableSystemFence) — a default event's system-scope
+ * release writes back the GPU caches on every record.  No reference equivalent (plumbing). */
+int scflow_sync_event_create(void** event);
+int scflow_sync_event_destroy(void* event);
+int scflow_sync_event_record(void* event, void* stream);
+int scflow_stream_wait_event(void* stream, void* event);
+
 /* out[n·ons + b·obs + a] = in[n·ins + a·ias + b] for a < A, b < B (batched 2-D transpose; e.g.
  * NCHW -> a channel slice of an NHWC buffer, or back). */
 int scflow_transpose(const float* in, float* out, int n, int A, int B, long long ins, int ias,

@@ -118,6 +118,10 @@ SIGNATURES = {
                                      c_float, c_vp]),
     "scflow_pose_step": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_float, c_int, c_float] +
                          [c_vp] * 6 + [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_vp]),
+    "scflow_sync_event_create": (c_int, [ctypes.POINTER(c_vp)]),
+    "scflow_sync_event_destroy": (c_int, [c_vp]),
+    "scflow_sync_event_record": (c_int, [c_vp, c_vp]),
+    "scflow_stream_wait_event": (c_int, [c_vp, c_vp]),
     "scflow_transpose": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_int, c_ll, c_int, c_vp]),
     "scflow_ph_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
     "scflow_ph_conv_pack": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),

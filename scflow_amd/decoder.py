@@ -91,6 +91,8 @@ class SCFlowDecoder(nn.Module):
         self.hoist_context = True
         # independent branches on a second HIP stream (else everything on the current stream)
         self.side_stream = True
+        # fork / join with device-scope events (no system-scope cache writeback per record)
+        self.device_scope_events = True
         # the iteration's tail (pose update, pose flow, ×8 prediction, next ↓8 flow) as one
         # launch (scflow_pose_step); only without flow/correlation masking
         self.fuse_tail = True
@@ -110,6 +112,13 @@ class SCFlowDecoder(nn.Module):
     def hx_channels(self) -> int:
         """Channels of the channels-last GRU working buffer: [h | cxt | motion | flow]."""
         return self.h_channels + self.cxt_channels + self.encoder.out_channels[0] + 2
+
+    def _sync_events(self):
+        """The fork / join events of the side stream (created once)."""
+        evs = getattr(self, "_sync_evs", None)
+        if evs is None:
+            evs = self._sync_evs = (ops.SyncEvent(), ops.SyncEvent())
+        return evs
 
     def _side_stream(self, dev) -> torch.cuda.Stream:
         """A second HIP stream for the decoder's independent branches (created once per device)."""
@@ -229,18 +238,31 @@ class SCFlowDecoder(nn.Module):
         two = self.side_stream
         side = self._side_stream(dev) if two else main
 
-        # two events reused every iteration (a wait captures the event's state when issued)
-        ev_fork, ev_join = (torch.cuda.Event(), torch.cuda.Event()) if two else (None, None)
+        # two events reused every iteration (a wait captures the event's state when issued);
+        # device-scope ones (ops.SyncEvent) unless self.device_scope_events is False
+        if two and self.device_scope_events:
+            ev_fork, ev_join = self._sync_events()
+            h_main, h_side = main.cuda_stream, side.cuda_stream
 
-        def fork():
-            if two:
-                ev_fork.record(main)
-                side.wait_event(ev_fork)
+            def fork():
+                ev_fork.record(h_main)
+                ev_fork.wait(h_side)
 
-        def join():
-            if two:
-                ev_join.record(side)
-                main.wait_event(ev_join)
+            def join():
+                ev_join.record(h_side)
+                ev_join.wait(h_main)
+        else:
+            ev_fork, ev_join = (torch.cuda.Event(), torch.cuda.Event()) if two else (None, None)
+
+            def fork():
+                if two:
+                    ev_fork.record(main)
+                    side.wait_event(ev_fork)
+
+            def join():
+                if two:
+                    ev_join.record(side)
+                    main.wait_event(ev_join)
 
         # Host path: the launches that read and write the same persistent buffers in every
         # iteration are recorded on the first iteration (ops.binding: argument structs built

@@ -256,6 +256,36 @@ class BoundLaunch:
             check(rc, self.name)
 
 
+class SyncEvent:
+    """A device-scope cross-stream event (scflow_sync_event_*): ``record(stream)`` then
+    ``wait(stream)`` orders the second stream after the first without the system-scope cache
+    writeback of a default HIP event."""
+
+    def __init__(self) -> None:
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(lib.scflow_sync_event_create(ctypes.byref(h)), "scflow_sync_event_create")
+        self._h, self._lib = h, lib
+
+    def record(self, stream: int) -> None:
+        rc = self._lib.scflow_sync_event_record(self._h, stream)
+        if rc:
+            check(rc, "scflow_sync_event_record")
+
+    def wait(self, stream: int) -> None:
+        rc = self._lib.scflow_stream_wait_event(stream, self._h)
+        if rc:
+            check(rc, "scflow_stream_wait_event")
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self._lib.scflow_sync_event_destroy(h)
+            except Exception:
+                pass
+
+
 def conv2d_args(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w: int,
                 cout: int, kh: int, kw: int, ph: int, pw: int, act: Optional[str] = None,
                 out: Optional[Chan] = None, src1: Optional[Chan] = None,

@@ -91,18 +91,20 @@ def test_decoder_matches_oracle_b4_8iters(hoist):
 @pytest.mark.gpu
 def test_decoder_schedules_bit_identical():
     """The launch schedule does not change the arithmetic: the fused iteration tail
-    (scflow_pose_step, double-buffered ↓8 flow) vs separate launches, and the side stream vs one
-    stream, give bit-identical outputs (every one of the 7 lists, every iteration)."""
+    (scflow_pose_step, double-buffered ↓8 flow) vs separate launches, the side stream vs one
+    stream, device-scope vs default events give bit-identical outputs (every one of the 7
+    lists, every iteration)."""
     inp = decoder_inputs(2, 256, seed=13)
     dec = build_decoder(3, seed=4)
     base = run_gpu(dec, inp)
-    for fuse, side in ((False, True), (True, False), (False, False)):
-        dec.fuse_tail, dec.side_stream = fuse, side
+    for fuse, side, dse in ((False, True, True), (True, False, True), (False, False, True),
+                            (True, True, False)):
+        dec.fuse_tail, dec.side_stream, dec.device_scope_events = fuse, side, dse
         out = run_gpu(dec, inp)
         for a, b in zip(base, out):
             for x, y in zip(a, b):
-                assert torch.equal(x, y), (fuse, side)
-    dec.fuse_tail, dec.side_stream = True, True
+                assert torch.equal(x, y), (fuse, side, dse)
+    dec.fuse_tail, dec.side_stream, dec.device_scope_events = True, True, True
 
 
 @pytest.mark.gpu
