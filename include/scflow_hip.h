@@ -179,6 +179,10 @@ int scflow_sync_event_create(void** event);
 int scflow_sync_event_destroy(void* event);
 int scflow_sync_event_record(void* event, void* stream);
 int scflow_stream_wait_event(void* stream, void* event);
+/* Timing events (device-scope release; destroy with scflow_sync_event_destroy, record with
+ * scflow_sync_event_record); *ms = end − start after waiting for end. */
+int scflow_timing_event_create(void** event);
+int scflow_event_elapsed_ms(void* start, void* end, float* ms);
 
 /* out[n·ons + b·obs + a] = in[n·ins + a·ias + b] for a < A, b < B (batched 2-D transpose; e.g.
  * NCHW -> a channel slice of an NHWC buffer, or back). */

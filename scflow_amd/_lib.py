@@ -122,6 +122,8 @@ SIGNATURES = {
     "scflow_sync_event_destroy": (c_int, [c_vp]),
     "scflow_sync_event_record": (c_int, [c_vp, c_vp]),
     "scflow_stream_wait_event": (c_int, [c_vp, c_vp]),
+    "scflow_timing_event_create": (c_int, [ctypes.POINTER(c_vp)]),
+    "scflow_event_elapsed_ms": (c_int, [c_vp, c_vp, ctypes.POINTER(c_float)]),
     "scflow_transpose": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_int, c_ll, c_int, c_vp]),
     "scflow_ph_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
     "scflow_ph_conv_pack": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),

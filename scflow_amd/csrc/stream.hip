@@ -30,3 +30,21 @@ SCFLOW_API int scflow_stream_wait_event(void* stream, void* event) {
   if (!event) return SCFLOW_EINVAL;
   return (int)hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0);
 }
+
+// Timing events for the bench's live kernel timing: timing enabled, device-scope release, so
+// an event pair brackets the kernel without a system-scope cache writeback inside the bracket.
+SCFLOW_API int scflow_timing_event_create(void** event) {
+  if (!event) return SCFLOW_EINVAL;
+  hipEvent_t e = nullptr;
+  const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  if (r != hipSuccess) return (int)r;
+  *event = (void*)e;
+  return SCFLOW_OK;
+}
+
+SCFLOW_API int scflow_event_elapsed_ms(void* start, void* end, float* ms) {
+  if (!start || !end || !ms) return SCFLOW_EINVAL;
+  const hipError_t r = hipEventSynchronize((hipEvent_t)end);
+  if (r != hipSuccess) return (int)r;
+  return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end);
+}

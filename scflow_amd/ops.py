@@ -259,13 +259,23 @@ class BoundLaunch:
 class SyncEvent:
     """A device-scope cross-stream event (scflow_sync_event_*): ``record(stream)`` then
     ``wait(stream)`` orders the second stream after the first without the system-scope cache
-    writeback of a default HIP event."""
+    writeback of a default HIP event.  ``timing=True``: a timing event (``elapsed_ms``)."""
 
-    def __init__(self) -> None:
+    def __init__(self, timing: bool = False) -> None:
         lib = _lib.load()
         h = ctypes.c_void_p()
-        check(lib.scflow_sync_event_create(ctypes.byref(h)), "scflow_sync_event_create")
+        if timing:
+            check(lib.scflow_timing_event_create(ctypes.byref(h)), "scflow_timing_event_create")
+        else:
+            check(lib.scflow_sync_event_create(ctypes.byref(h)), "scflow_sync_event_create")
         self._h, self._lib = h, lib
+
+    def elapsed_ms(self, end: "SyncEvent") -> float:
+        """Milliseconds from this (timing) event to ``end`` (waits for ``end``)."""
+        ms = ctypes.c_float()
+        check(self._lib.scflow_event_elapsed_ms(self._h, end._h, ctypes.byref(ms)),
+              "scflow_event_elapsed_ms")
+        return float(ms.value)
 
     def record(self, stream: int) -> None:
         rc = self._lib.scflow_sync_event_record(self._h, stream)

@@ -69,6 +69,9 @@ class EventTimer:
         self.enabled = True
         self.stride = max(1, stride)
         self._calls = 0
+        # device-scope timing events (scflow_timing_event_create): no system-scope cache
+        # writeback inside the bracket
+        self.device_scope = True
 
     def __call__(self, start: bool) -> None:
         if not self.enabled:
@@ -77,8 +80,13 @@ class EventTimer:
             self._calls += 1
         if (self._calls - 1) % self.stride:
             return
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
+        if self.device_scope:
+            from . import ops
+            ev = ops.SyncEvent(timing=True)
+            ev.record(ops.raw_stream(torch.cuda.current_device()))
+        else:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
         if start:
             self._start = ev
         else:
@@ -92,6 +100,8 @@ class EventTimer:
         if not self.pairs:
             return float("nan")
         torch.cuda.synchronize()
+        if self.device_scope:
+            return sum(a.elapsed_ms(b) for a, b in self.pairs) / len(self.pairs)
         return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
 
     def count(self) -> int:
