@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp
 B="--steps 10 --warmup 3 --no-cpu-baseline --e2e-batch 0 --train-batch 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run -- python3 $R/bench.py $B > $OUT/bench_kt.json 2> $OUT/kt.err || exit $?
 python3 $R/tools/stats_file.py $(find $OUT/kt -name "*.db" | head -1) "python bench.py $B" > $OUT/stats.txt
-python3 $R/tools/prof_summary.py $(find $OUT/kt -name "*.db" | head -1) 13 > $OUT/per_forward.txt
+python3 $R/tools/prof_summary.py $(find $OUT/kt -name "*.db" | head -1) 24 > $OUT/per_forward.txt  # 3 warmup + 10 timed + 1 + 10 secondary-timer forwards
 python3 $R/tools/timeline.py $(find $OUT/kt -name "*.db" | head -1) --iteration 60 > $OUT/timeline.txt 2>&1
 rm -rf $OUT/kt
 P="--steps 2 --warmup 1 --no-cpu-baseline --e2e-batch 0 --train-batch 0 --no-kernel-timer"
