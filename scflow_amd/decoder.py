@@ -113,12 +113,15 @@ class SCFlowDecoder(nn.Module):
         """Channels of the channels-last GRU working buffer: [h | cxt | motion | flow]."""
         return self.h_channels + self.cxt_channels + self.encoder.out_channels[0] + 2
 
-    def _sync_events(self):
-        """The fork / join events of the side stream (created once)."""
+    def _sync_events(self, dev):
+        """The fork / join events of the side stream (created once per device, on it)."""
         evs = getattr(self, "_sync_evs", None)
         if evs is None:
-            evs = self._sync_evs = (ops.SyncEvent(), ops.SyncEvent())
-        return evs
+            evs = self._sync_evs = {}
+        if dev not in evs:
+            with torch.cuda.device(dev):
+                evs[dev] = (ops.SyncEvent(), ops.SyncEvent())
+        return evs[dev]
 
     def _side_stream(self, dev) -> torch.cuda.Stream:
         """A second HIP stream for the decoder's independent branches (created once per device)."""
@@ -241,7 +244,7 @@ class SCFlowDecoder(nn.Module):
         # two events reused every iteration (a wait captures the event's state when issued);
         # device-scope ones (ops.SyncEvent) unless self.device_scope_events is False
         if two and self.device_scope_events:
-            ev_fork, ev_join = self._sync_events()
+            ev_fork, ev_join = self._sync_events(dev)
             h_main, h_side = main.cuda_stream, side.cuda_stream
 
             def fork():
