@@ -150,7 +150,8 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
 // quad t%8 of pixel slot t/8 (32 slots), float4 loads; per-channel sums in fp64 reduced over the
 // slots in a fixed order, then per group (c/groups channels) → mean, biased variance.
 // NS > 0: compile-time slab count; the pixel loop is unrolled PU-fold with every load of a
-// round issued before any add (this kernel is latency-bound: 64 workgroups at B = 16)
+// round issued before any add (this kernel is latency-bound: 64 workgroups at B = 16; at the
+// pose head's first conv every slot's 8 pixels × 4 slabs are one round)
 template <int NS>
 __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restrict__ x, int nsplit,
                                                            long long split_stride, float* __restrict__ y,
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
   };
   int p = slot;
   if constexpr (NS > 0) {
-    constexpr int PU = NS <= 2 ? 4 : (NS <= 4 ? 2 : 1);
+    constexpr int PU = NS <= 4 ? 8 : 1;  // ≤ 32 float4 loads in flight
     for (; p + 32 * (PU - 1) < hw; p += 32 * PU) {
       floatx4 v[PU][NS];
 #pragma unroll
@@ -194,10 +195,18 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
   for (; p < hw; p += 32) {
     const size_t off = ((size_t)img * hw + p) * c + cb + 4 * q;
     floatx4 v = *(const floatx4*)(x + off);
-    for (int z = 1; z < nsplit; ++z) {
-      const floatx4 u = *(const floatx4*)(x + (size_t)z * split_stride + off);
+    if constexpr (NS > 0) {
+      floatx4 u[NS > 1 ? NS : 1];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += u[e];
+      for (int z = 1; z < NS; ++z) u[z] = *(const floatx4*)(x + (size_t)z * split_stride + off);
+#pragma unroll
+      for (int z = 1; z < NS; ++z) v += u[z];
+    } else {
+      for (int z = 1; z < nsplit; ++z) {
+        const floatx4 u = *(const floatx4*)(x + (size_t)z * split_stride + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += u[e];
+      }
     }
     acc(v, off);
   }
