@@ -12,20 +12,23 @@ SURVEY.md §8(e)); ``value`` = all pairs·iterations of all ranks ÷ the slowest
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Extra JSON fields:
-* ``roofline``: the dominant kernel, the fused z|r SepConvGRU convolution (2 launches per
-  iteration; with the loop-invariant context contribution hoisted out of the loop it contracts
-  h and the motion features, 2·M·256·5·256 = 10.7 GFLOP of algorithmic work per launch at
-  B=16), on the F(4,5) Winograd kernel ``conv_wino5_kernel<GRU_ZR>`` (2.5× fewer matrix
-  multiplies), timed live with HIP events around one of its launches per step in the timed
-  region;
-  bound = fp32 MFMA, peak 157.3 TFLOP/s.  ``achieved``/``frac`` use the algorithmic FLOPs (so
-  they can exceed the peak), ``mfma_achieved``/``mfma_frac`` the FLOPs the matrix cores
-  execute.
-* ``rooflines_secondary``: lookup, fused iteration tail, correlation pyramid — the same events
-  in a short untimed pass after the timed region (same workload), so the headline carries only
-  the roofline kernel's event pair per step.
+* ``roofline``: the kernel with the most GPU time in the step, ``conv_wino_kernel<32,2>`` — the
+  F(2×2,3×3) Winograd convolution on fp32 MFMA with 64-channel workgroups, which runs the XHead
+  hidden convs (128→512, both heads in one launch) and corr_net.1 (256→192) once per iteration
+  each.  Both launches are bracketed live with HIP events inside the timed region (one of each
+  per step).  ``achieved``/``frac`` count the FLOPs the matrix cores EXECUTE (Winograd: 16
+  transform points per 2×2 tile, 2.25× fewer multiplies than a direct conv), so ``frac`` ≤ 1 is
+  a true roofline fraction; ``direct_conv_flops_per_launch`` / ``direct_equiv_tflops`` give the
+  direct-conv count for comparison.  ``traffic`` = memory-side bytes per launch from the
+  rocprofv3 FETCH_SIZE / WRITE_SIZE passes in ``profiles/traffic_*.json``.
+* ``rooflines_secondary``: the SepConvGRU z|r conv (F(4,5) Winograd, same FLOP basis), the
+  pyramid lookup (HBM/gather), the fused iteration tail ``pose_step_kernel`` and the
+  correlation pyramid — the same events in a short untimed pass after the timed region.
 * ``cpu_baseline``: the CPU oracle (oracle/scflow_oracle.py, a parity-pinned PyTorch-CPU
-  restatement of the reference decoder) on a bounded sample, rank 0 at N=1 only.
+  restatement of the reference decoder) on the same B=16 × 8-iteration workload, rank 0 at N=1.
+
+``--gpus N`` without a launcher: the parent starts ``torch.distributed.run`` with N ranks as a
+child process (before touching the GPU) and relays its output; rank 0 prints the JSON line.
 """
 from __future__ import annotations
 
@@ -117,12 +120,53 @@ def time_steps(step, steps, warmup, world, dev):
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
 
-def secondary_rooflines(timers, batch, size, fused_tail=True):
-    """The other hot-path kernels, timed with the same events in an untimed pass after the timed
-    region: the pyramid lookup and the pose-induced-flow reprojection are HBM/gather-bound
-    (algorithmic bytes per launch from SURVEY.md §8(d)), the correlation GEMM is MFMA-bound.
+def load_traffic(path):
+    """{group: bytes per launch} from tools/traffic_json.py's output (None if absent)."""
+    if not path or not os.path.exists(path):
+        return None, None
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    return tj, {k: v.get("hbm_bytes_per_launch") for k, v in tj.get("kernels", {}).items()}
+
+
+def conv_roofline(kernel, parts, timers, m_px, traffic=None, alg_bytes=None):
+    """Roofline entry of a conv kernel symbol covering one or more launch shapes.
+
+    ``parts`` = [(timer name, ConvRunner, c0, c1)]: achieved = Σ executed FLOPs ÷ Σ mean launch
+    times, i.e. the kernel's executed rate over one launch of each shape; avg_launch_ms is the
+    mean over the shapes (what rocprofv3's per-symbol average shows, one launch of each per
+    iteration)."""
+    ms = [timers[n].mean_ms() for n, *_ in parts]
+    ex = [r.mfma_flops(m_px, c0, c1) for _, r, c0, c1 in parts]
+    di = [r.flops(m_px) for _, r, _, _ in parts]
+    t = sum(ms) * 1e-3
+    ach = sum(ex) / t / 1e12
+    out = {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2),
+           "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+           "traffic": traffic,
+           "flop_basis": "executed on the matrix cores (Winograd transform-domain products, "
+                         "channels padded to 32)",
+           "avg_launch_ms": round(sum(ms) / len(ms), 4),
+           "launches": sum(timers[n].count() for n, *_ in parts),
+           "launch_ms": {n: round(v, 4) for (n, *_), v in zip(parts, ms)},
+           "flops_per_launch": sum(ex) / len(ex),
+           "direct_conv_flops_per_launch": sum(di) / len(di),
+           "direct_equiv_tflops": round(sum(di) / t / 1e12, 2)}
+    if alg_bytes is not None:
+        out["algorithmic_bytes_per_launch"] = alg_bytes
+        if traffic:
+            out["traffic_over_algorithmic"] = round(traffic / alg_bytes, 3)
+    return out
+
+
+def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True):
+    """The HBM/gather-bound kernels and the correlation GEMM, timed with the same events in an
+    untimed pass after the timed region (algorithmic bytes per launch from SURVEY.md §8(d)).
     At B=16, 256² the 86 MB pyramid is Infinity-Cache resident, so the lookup's GB/s is an
-    on-die rate; --size 512 --batch 32 (configs[4]) puts it in HBM."""
+    on-die rate; --size 512 --batch 32 --iters 12 (configs[4]) puts it in HBM."""
     h = w = size // 8
     P = h * w
     lookup_bytes = batch * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
@@ -130,12 +174,13 @@ def secondary_rooflines(timers, batch, size, fused_tail=True):
     # also writes the ×8 flow prediction and mask (12 B per pixel)
     flow_bytes = batch * (36 if fused_tail else 20) * size * size
     corr_flops = 2.0 * batch * P * P * 256
+    traffic = traffic or {}
     out = []
-    for name, kernel, bound, amount in (
-            ("corr_lookup", "corr_lookup_lds_kernel<4> (a2)", "hbm", lookup_bytes),
-            ("pose_flow", "pose_step_kernel (a8+a10+a11)" if fused_tail else "pose_flow_kernel (a8+a10)",
-             "hbm", flow_bytes),
-            ("corr_pyramid", "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma", corr_flops)):
+    for name, tkey, kernel, bound, amount in (
+            ("corr_lookup", "corr_lookup", "corr_lookup_lds_kernel<4> (a2)", "hbm", lookup_bytes),
+            ("pose_flow", "pose_step", "pose_step_kernel (a8+a10+a11)" if fused_tail
+             else "pose_flow_kernel (a8+a10)", "hbm", flow_bytes),
+            ("corr_pyramid", None, "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma", corr_flops)):
         t = timers[name]
         if t.count() == 0:
             continue
@@ -144,17 +189,24 @@ def secondary_rooflines(timers, batch, size, fused_tail=True):
             ach, peak, unit = amount / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
         else:
             ach, peak, unit = amount / (ms * 1e-3) / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
-        out.append({"kernel": kernel, "bound": bound, "achieved": round(ach, 2), "peak": peak,
-                    "unit": unit, "frac": round(ach / peak, 4), "avg_launch_ms": round(ms, 4),
-                    "launches": t.count(),
-                    ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): amount})
+        e = {"kernel": kernel, "bound": bound, "achieved": round(ach, 2), "peak": peak,
+             "unit": unit, "frac": round(ach / peak, 4), "avg_launch_ms": round(ms, 4),
+             "launches": t.count(),
+             ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): amount}
+        if bound == "hbm":
+            tr = traffic.get(tkey)
+            e["traffic"] = tr
+            if tr:
+                e["traffic_over_algorithmic"] = round(tr / amount, 3)
+                e["traffic_gbs"] = round(tr / (ms * 1e-3) / 1e9, 1)
+        out.append(e)
     return out
 
 
 def bench_train(args, world, rank, dev, feat):
     """BASELINE configs[3]: the training step — SCFlowRefiner.loss forward on the HIP kernels,
-    backward through the HIP adjoint kernels, bucketed gradient all-reduce over RCCL (world > 1,
-    overlapped with the backward pass), clip 10, AdamW — `train_batch` pairs per GPU."""
+    backward through the HIP adjoint kernels, bucketed gradient all-reduce over RCCL (world > 1),
+    clip 10, AdamW — `train_batch` pairs per GPU (configs[3] = 16/GPU × 8 GPUs = 128)."""
     from scflow_amd import synthetic
     from scflow_amd.train.step import TrainStep
     ref = build_refiner(args.iters, dev, feat).train()
@@ -168,12 +220,16 @@ def bench_train(args, world, rank, dev, feat):
         losses.append(step(batch)["loss"].detach())
     el = time_steps(one, args.train_steps, 2, world, dev)
     nparam = sum(p.numel() for p in step.grads.params)
-    out = {"workload": f"training step (SCFlowRefiner.loss fwd+bwd, 3 losses, grad all-reduce, clip, "
-                       f"AdamW), {args.train_batch} pairs/GPU, {args.size}x{args.size}, {args.iters} "
-                       f"iters (BASELINE configs[3] at N=8: global batch {8 * args.train_batch})",
-           "value": round(world * args.train_batch * args.iters * args.train_steps / el, 2),
+    gb = world * args.train_batch
+    which = ("BASELINE configs[3]" if (world, args.train_batch, args.size, args.iters) == (8, 16, 256, 8)
+             else f"configs[3]'s per-GPU shard at N={world} (configs[3] itself is N=8, global batch 128)")
+    out = {"workload": f"training step (SCFlowRefiner.loss fwd+bwd, 3 losses, grad all-reduce over "
+                       f"{'RCCL' if world > 1 else 'nothing (1 rank)'}, clip, AdamW), "
+                       f"{args.train_batch} pairs/GPU x {world} GPU(s) = global batch {gb}, "
+                       f"{args.size}x{args.size}, {args.iters} iters — {which}",
+           "value": round(gb * args.iters * args.train_steps / el, 2),
            "unit": "iters/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
-           "steps": args.train_steps, "warmup": 2, "global_batch": world * args.train_batch,
+           "steps": args.train_steps, "warmup": 2, "global_batch": gb, "n_gpus": world,
            "allreduce_bytes": 4 * nparam if world > 1 else 0,
            "buckets": len(step.grads.buckets),
            "loss_first_last": [round(float(losses[0]), 4), round(float(losses[-1]), 4)]}
@@ -181,15 +237,17 @@ def bench_train(args, world, rank, dev, feat):
     return out
 
 
-def cpu_baseline(seconds: float, iters: int, size: int):
-    """Time the CPU oracle on a bounded sample: B=2 pairs, `iters` iterations, repeated."""
+def cpu_baseline(seconds: float, batch: int, iters: int, size: int):
+    """Time the CPU oracle on the bench's own workload (``batch`` pairs × ``iters`` at ``size``²),
+    repeated until ``seconds`` have passed (at least one forward)."""
     from oracle import scflow_oracle as orc
     from scflow_amd import MODELS, synthetic
     threads = torch.get_num_threads()
-    dec = MODELS.build(decoder_cfg(iters))
+    feat = (size // 8, size // 8) if size != 256 else None
+    dec = MODELS.build(decoder_cfg(iters, feat))
     synthetic.fill_module_(dec)
     sd = {k: v.detach() for k, v in dec.state_dict().items()}
-    inp = make_inputs(2, size, 100, "cpu")
+    inp = make_inputs(batch, size, 100, "cpu")
     orc.decoder_forward(sd, **inp, iters=1)  # warm up allocator / threads
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -198,10 +256,25 @@ def cpu_baseline(seconds: float, iters: int, size: int):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": round(reps * 2 * iters / el, 3), "unit": "iters/s", "cores": threads,
+    return {"value": round(reps * batch * iters / el, 3), "unit": "iters/s", "cores": threads,
             "kind": "port",
-            "sample": f"oracle decoder (PyTorch CPU fp32), B=2 pairs x {iters} iters at {size}x{size}, "
-                      f"{reps} reps in {el:.1f}s, torch threads={threads}"}
+            "sample": f"oracle decoder (PyTorch CPU fp32), B={batch} pairs x {iters} iters at "
+                      f"{size}x{size} (the bench's own workload), {reps} forward(s) in {el:.1f}s, "
+                      f"torch threads={threads}"}
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` run directly: start torch.distributed.run with N ranks as a CHILD process (this
+    process has not touched the GPU and never execs) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=dict(os.environ))
 
 
 def main():
@@ -223,23 +296,30 @@ def main():
                          "0 disables it")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-kernel-timer", action="store_true",
-                    help="do not bracket the roofline kernel (throughput without timer overhead)")
+                    help="do not bracket the roofline kernels (throughput without timer overhead)")
     ap.add_argument("--graph", action="store_true",
-                    help="replay a captured hipGraph per step instead of launching kernel by kernel "
-                         "(measured slower on MI355X/ROCm 7: 14.38k vs 14.66k iters/s)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_gru_zr.json"),
-                    help="HBM bytes per launch of the dominant kernel from a rocprofv3 PMC pass")
+                    help="replay a captured hipGraph per step instead of launching kernel by kernel")
+    ap.add_argument("--traffic-json", default=None,
+                    help="memory-side bytes per launch from rocprofv3 PMC passes "
+                         "(default profiles/traffic_b{batch}_s{size}.json)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting {world}",
+              file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
     from scflow_amd import MODELS, synthetic
+    from scflow_amd.modules import ConvRunner
     from scflow_amd.profiling import EventTimer, KernelTimer
 
     feat = (args.size // 8, args.size // 8) if args.size != 256 else None
@@ -249,14 +329,15 @@ def main():
     inp = make_inputs(args.batch, args.size, seed=rank, device=dev)
 
     # launches per step of each bracketed kernel: 2 SeqConv stages per iteration for the z|r
-    # conv, one lookup / pose-flow per iteration, one pyramid per forward.  Eager runs bracket
-    # one launch per step (stride = per-step launches + 1 walks the sampled position through
-    # the iterations), so the timing events cost ≈ 2 queue packets per step, not 2 per launch.
-    per_step = {"gru_zr": 2 * args.iters, "corr_lookup": args.iters, "pose_flow": args.iters,
-                "corr_pyramid": 1}
+    # conv, one heads / corr_net.1 / lookup / pose-flow per iteration, one pyramid per forward.
+    # Eager runs bracket one launch per step per timer (stride = per-step launches + 1 walks the
+    # sampled position through the iterations), so an event pair costs ≈ 2 queue packets per
+    # step, not 2 per launch.
+    per_step = {"heads": args.iters, "corr_net1": args.iters, "gru_zr": 2 * args.iters,
+                "corr_lookup": args.iters, "pose_flow": args.iters, "corr_pyramid": 1}
+    live = ("heads", "corr_net1")  # the headline kernel's launches: bracketed in the timed region
     timers = {name: (KernelTimer() if args.graph else EventTimer(stride=n + 1 if n > 1 else 1))
               for name, n in per_step.items()}
-    timer = timers["gru_zr"]
     for t in timers.values():
         t.enabled = False
     if not args.no_kernel_timer:
@@ -266,9 +347,8 @@ def main():
             return dec(**inp, invalid_flow_num=0.0)
         for _ in range(args.warmup):
             step()
-        # the timed region brackets the roofline kernel only; the secondary kernels' events are
-        # recorded in a separate untimed pass afterwards (an event pair costs queue time)
-        timer.enabled = True
+        for n in live:
+            timers[n].enabled = True
     else:
         # one hipGraph per forward: captured after `warmup` eager passes, replayed per step
         from scflow_amd.graph import GraphedForward
@@ -285,7 +365,7 @@ def main():
     if not args.graph and not args.no_kernel_timer:
         step()  # the queue refilled past the timed region's final synchronize
         for name, t in timers.items():
-            t.enabled = name != "gru_zr"
+            t.enabled = name not in live
         for _ in range(min(args.steps, 10)):
             step()
         torch.cuda.synchronize()
@@ -340,28 +420,40 @@ def main():
 
     units = world * args.batch * args.iters * args.steps
     value = units / elapsed
-    zr_ms = timer.mean_ms()
-    m_px = args.batch * (args.size // 8) ** 2
-    cxt = dec.cxt_channels if dec.hoist_context else 0
-    zr = dec.gru.zr_runner(cxt)
-    flops = zr.flops(m_px)
-    achieved = flops / (zr_ms * 1e-3) / 1e12
-    hc = dec.h_channels
-    mfma_flops = zr.mfma_flops(m_px, hc, zr.cin - hc)
-    mfma_achieved = mfma_flops / (zr_ms * 1e-3) / 1e12
-    zr_kernel = ("conv_wino5_kernel<GRU_ZR> (SepConvGRU z|r conv, Winograd F(4,5) on fp32 MFMA)"
-                 if zr.winograd else "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r conv, direct)")
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("batch") == args.batch and tj.get("size") == args.size:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    h8 = args.size // 8
+    m_px = args.batch * h8 * h8
+    hc, xc = dec.h_channels, dec.cxt_channels
+    tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_b{args.batch}_s{args.size}.json")
+    tj, traffic = load_traffic(tpath)
+    traffic = traffic or {}
+    alg = {k: v.get("algorithmic_bytes_per_launch") for k, v in (tj or {}).get("kernels", {}).items()}
+
+    heads_r = dec._hidden_heads()
+    c1 = dec.encoder.corr_net[-1].conv
+    corr1_r = ConvRunner.of(c1, dec.encoder.corr_net[-1].act_type)
+    headline = conv_roofline(
+        "conv_wino_kernel<32,2> (F(2x2,3x3) Winograd on fp32 MFMA, 64-channel workgroups): "
+        "XHead hidden convs 128->512 + corr_net.1 256->192",
+        [("heads", heads_r, hc, 0), ("corr_net1", corr1_r, c1.in_channels, 0)], timers, m_px,
+        traffic.get("conv_wino_kernel<32,2>"), alg.get("conv_wino_kernel<32,2>"))
+    if not (heads_r.winograd and corr1_r.winograd):
+        headline["kernel"] = "direct conv_mfma_kernel (Winograd off): XHead hidden + corr_net.1"
+
+    secondary = []
+    if timers["gru_zr"].count():
+        cxt = xc if dec.hoist_context else 0
+        zr = dec.gru.zr_runner(cxt)
+        secondary.append(conv_roofline(
+            "conv_wino5_kernel<·,32,2,GRU_ZR> (SepConvGRU z|r, Winograd F(4,5) on fp32 MFMA)"
+            if zr.winograd else "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r, direct)",
+            [("gru_zr", zr, hc, zr.cin - hc)], timers, m_px, traffic.get("gru_zr"), alg.get("gru_zr")))
+    secondary += secondary_rooflines(timers, args.batch, args.size, traffic,
+                                     getattr(dec, "fuse_tail", True))
 
     if rank == 0:
+        cfg_name = ("configs[4]" if (args.batch, args.size, args.iters) == (32, 512, 12)
+                    else "configs[1]" if (args.batch, args.size, args.iters) == (16, 256, 8)
+                    else "custom size")
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -377,31 +469,20 @@ def main():
             "data": "synthetic (seeded features, YCB-V-like poses/intrinsics, analytic ellipsoid depth; "
                     "deterministic random-init weights)",
             "config": {"workload": f"SCFlowDecoder forward, {args.batch} pairs/GPU, "
-                                   f"{args.size}x{args.size}, {args.iters} GRU iters (BASELINE "
-                                   f"{'configs[4]' if (args.size, args.iters) == (512, 12) else 'configs[1]' if (args.batch, args.size, args.iters) == (16, 256, 8) else 'custom size'})",
+                                   f"{args.size}x{args.size}, {args.iters} GRU iters (BASELINE {cfg_name})",
                        "global_batch": args.batch * world, "image": args.size, "iters": args.iters,
                        "launch": "hipGraph replay" if args.graph else "eager",
                        "parallelism": f"dp{world}"},
-            "roofline": {"kernel": zr_kernel,
-                         "bound": "mfma", "achieved": round(achieved, 2),
-                         "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                         "avg_launch_ms": round(zr_ms, 4), "launches": timer.count(),
-                         "flops_per_launch": flops,
-                         # achieved/frac count the direct conv's (algorithmic) FLOPs; Winograd
-                         # executes fewer: these are the matrix cores' own FLOPs and busy share
-                         "mfma_flops_per_launch": mfma_flops,
-                         "mfma_achieved": round(mfma_achieved, 2),
-                         "mfma_frac": round(mfma_achieved / FP32_MFMA_PEAK_TFLOPS, 4)},
+            "roofline": headline,
+            "rooflines_secondary": secondary,
+            "traffic_source": os.path.relpath(tpath, ROOT) if tj else None,
         }
-        res["rooflines_secondary"] = secondary_rooflines(timers, args.batch, args.size,
-                                                       getattr(dec, "fuse_tail", True))
         if e2e is not None:
             res["end_to_end"] = e2e
         if train is not None:
             res["training_step"] = train
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.iters, args.size)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.batch, args.iters, args.size)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

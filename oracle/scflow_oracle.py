@@ -300,8 +300,11 @@ def decoder_forward(sd: StateDict, feat_render: Tensor, feat_real: Tensor, h_fea
                     invalid_flow_num: float = 0.0, iters: int = 8, num_levels: int = 4,
                     radius: int = 4, act: str | None = "ReLU", gru_type: str = "SeqConv",
                     num_class: int = 21, depth_transform: str = "exp", mask_flow: bool = False,
-                    mask_corr: bool = False, hooks: dict | None = None, train: bool = False):
-    """Returns the reference's 7 lists (scflow_decoder.py:252).  ``train``: apply the configured
+                    mask_corr: bool = False, hooks: dict | None = None, train: bool = False,
+                    head_label: Tensor | None = None):
+    """Returns the reference's 7 lists (scflow_decoder.py:252).  ``head_label``: the labels
+    whose first entry picks the pose head's class (default ``label``; the reference's label[0]
+    quirk, pose_head.py:208-209) — a data-parallel shard passes the global batch's label[:1].  ``train``: apply the configured
     detaches for autograd (detach_flow / detach_pose / detach_depth_for_xy = True,
     scflow_decoder.py:193-196,231-236; config scflow_ycbv_real.py:211-214) — values unchanged."""
     dt = feat_render.dtype
@@ -334,7 +337,8 @@ def decoder_forward(sd: StateDict, feat_render: Tensor, feat_real: Tensor, h_fea
                           "delta_flow_encoder.1", act, padding=1)
         mf = conv_module(conv_module(mask, sd, "mask_encoder.0", act, padding=1), sd,
                          "mask_encoder.1", act, padding=1)
-        drot, dtr = pose_head(sd, torch.cat([h, dff, mf], 1), label, num_class)
+        drot, dtr = pose_head(sd, torch.cat([h, dff, mf], 1),
+                              label if head_label is None else head_label, num_class)
         flow_pred = scale * upsample(flow + dflow, scale)
         up_mask = upsample(mask, scale)
         if train:

@@ -140,17 +140,22 @@ class SCFlowDecoder(nn.Module):
     # ------------------------------------------------------------------ forward
     def forward(self, feat_render: Tensor, feat_real: Tensor, h_feat: Tensor, cxt_feat: Tensor,
                 ref_rotation: Tensor, ref_translation: Tensor, depth: Tensor, internel_k: Tensor,
-                label: Tensor, init_flow: Tensor, invalid_flow_num: float):
+                label: Tensor, init_flow: Tensor, invalid_flow_num: float,
+                head_label: Optional[Tensor] = None):
+        """``head_label`` (extension, default None = ``label``): the labels whose first entry
+        picks the pose head's class for the whole batch (the reference's ``label[0]`` quirk,
+        ``pose_head.py:208-209``).  A data-parallel shard passes the GLOBAL batch's ``label[:1]``
+        so that sharded output equals the unsharded forward (``dist.shard_batch``)."""
         if feat_render.device.type != "cuda":
             raise ScflowError("SCFlowDecoder runs on the gfx950 HIP kernels only; move inputs to a "
                               "ROCm device (there is no CPU fallback)")
         with torch.no_grad():
             return self._forward(feat_render, feat_real, h_feat, cxt_feat, ref_rotation,
                                  ref_translation, depth, internel_k, label, init_flow,
-                                 float(invalid_flow_num))
+                                 float(invalid_flow_num), head_label=head_label)
 
     def _forward(self, feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label, init_flow,
-                 invalid, hx: Optional[Tensor] = None):
+                 invalid, hx: Optional[Tensor] = None, head_label: Optional[Tensor] = None):
         """``hx``: optional channels-last [N·h·w, ≥ hc+xc+co+2] buffer whose first hc+xc channels
         already hold tanh(h) | relu(cxt) (SCFlowRefiner writes the context encoder's output
         there directly); h_feat / cxt_feat are then ignored."""
@@ -225,7 +230,7 @@ class SCFlowDecoder(nn.Module):
         head_runner = self._hidden_heads()
         flow_pred_r = ConvRunner.of(self.flow_pred.predict_layer, None)
         mask_pred_r = ConvRunner.of(self.mask_pred.predict_layer, "Sigmoid")
-        label = label.to(dev).long()
+        label = (label if head_label is None else head_label).to(dev).long()
         mask_lr = None
         if self.mask_corr or self.mask_flow:
             mask_lr = torch.ones(M, 1, device=dev, dtype=f32)  # interpolate(ones, 1/8) == ones
@@ -305,8 +310,16 @@ class SCFlowDecoder(nn.Module):
             ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
                             flow_layout="nhwc")
 
-        def seg_corr_out():
-            run_chain(self.encoder.corr_net, Chan.whole(CORR), Chan(MF, 0, cc), N, h, w, s_corr)
+        corr_net = self.encoder.corr_net
+
+        def seg_corr_hidden():  # corr_net.0 (1×1 324→256)
+            if len(corr_net) > 1:
+                run_chain(corr_net[:-1], Chan.whole(CORR), Chan.whole(s_corr[-1]), N, h, w,
+                          s_corr[:-1])
+
+        def seg_corr_last():  # corr_net.1 (3×3 256→192), bracketed by the "corr_net1" hook
+            src = Chan.whole(s_corr[-1]) if len(corr_net) > 1 else Chan.whole(CORR)
+            ConvRunner.of(corr_net[-1].conv, corr_net[-1].act_type).run(src, Chan(MF, 0, cc), N, h, w)
 
         def seg_out():
             run_chain(self.encoder.out_net, Chan.whole(MF), hx_motion, N, h, w, s_out)
@@ -355,13 +368,18 @@ class SCFlowDecoder(nn.Module):
             self._hook("corr_lookup", False)
             if self.mask_corr:
                 CORR.mul_(mask_lr)
-            segment("corr_out", seg_corr_out)
+            segment("corr_hidden", seg_corr_hidden)
+            self._hook("corr_net1", True)
+            segment("corr_last", seg_corr_last)
+            self._hook("corr_net1", False)
             join()
             segment("out", seg_out)
             # a4 GRU (in place on HX[:, :hc])
             gru_step(self.kernel_hooks)
             # a5 heads
+            self._hook("heads", True)
             segment("heads", seg_heads)
+            self._hook("heads", False)
             # mask predictor + mask encoder (a5, a6) on the side stream
             fork()
             with torch.cuda.stream(side):

@@ -10,7 +10,7 @@ gather runs over xGMI; the CPU tests use gloo.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -27,15 +27,29 @@ def shard_range(batch: int, rank: int, world: int) -> Tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
-def shard_batch(batch: Dict[str, Tensor], rank: int, world: int, batch_dim: int = 0) -> Dict[str, Tensor]:
-    """Slice every per-pair tensor of a decoder input dict to this rank's shard."""
+def shard_batch(batch: Dict[str, Tensor], rank: int, world: int, batch_dim: int = 0,
+                head_label_key: Optional[str] = "label") -> Dict[str, Tensor]:
+    """Slice every per-pair tensor of a decoder input dict to this rank's shard.
+
+    The reference's pose head picks the class head of ``label[0]`` for the WHOLE batch
+    (``pose_head.py:208-209``), so a shard whose first label differs from the global batch's
+    would pick a different head than the unsharded forward.  With ``head_label_key`` set (the
+    default, ``"label"``) the shard also carries ``head_label`` = the global ``label[:1]``,
+    which ``SCFlowDecoder.forward`` / ``SCFlowRefiner.get_pose`` / the training step take as
+    the pose head's label: sharded output then equals unsharded output for multi-class
+    batches.  (The reference's own DDP runs — ``train.py:42-45``, ``tools/eval.py`` — shard
+    through the data loader, so there every rank uses its local ``label[0]``; pass
+    ``head_label_key=None`` for that behaviour.)"""
     sizes = {v.shape[batch_dim] for v in batch.values() if isinstance(v, Tensor) and v.dim() > 0}
     if len(sizes) != 1:
         raise ValueError(f"inconsistent batch sizes {sizes}")
     b = sizes.pop()
     s, e = shard_range(b, rank, world)
-    return {k: (v.narrow(batch_dim, s, e - s) if isinstance(v, Tensor) and v.dim() > 0 else v)
-            for k, v in batch.items()}
+    out = {k: (v.narrow(batch_dim, s, e - s) if isinstance(v, Tensor) and v.dim() > 0 else v)
+           for k, v in batch.items()}
+    if head_label_key is not None and head_label_key in batch and "head_label" not in batch:
+        out["head_label"] = batch[head_label_key].narrow(batch_dim, 0, 1)
+    return out
 
 
 def gather_shards(x: Tensor, group=None) -> Tensor:

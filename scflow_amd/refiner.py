@@ -136,19 +136,20 @@ class SCFlowRefiner(nn.Module):
 
     def get_pose(self, render_images: Tensor, real_images: Tensor, ref_rotation: Tensor,
                  ref_translation: Tensor, depth: Tensor, internel_k: Tensor, label: Tensor,
-                 init_flow: Optional[Tensor] = None):
+                 init_flow: Optional[Tensor] = None, head_label: Optional[Tensor] = None):
         """scflow_refiner.py:108-138 — images → encoders → SCFlowDecoder outputs (7 lists)."""
         if render_images.device.type != "cuda":
             raise ScflowError("SCFlowRefiner runs on the gfx950 HIP kernels only (no CPU fallback)")
         with torch.no_grad():
             return self._get_pose(render_images.contiguous().float(), real_images.contiguous().float(),
-                                  ref_rotation, ref_translation, depth, internel_k, label, init_flow)
+                                  ref_rotation, ref_translation, depth, internel_k, label, init_flow,
+                                  head_label)
 
     def forward(self, *args, **kwargs):
         return self.get_pose(*args, **kwargs)
 
     # ------------------------------------------------------------------ fused path
-    def _get_pose(self, render, real, R, t, depth, K, label, init_flow):
+    def _get_pose(self, render, real, R, t, depth, K, label, init_flow, head_label=None):
         N, _, H, W = real.shape
         dev = real.device
         dec = self.decoder
@@ -170,4 +171,4 @@ class SCFlowRefiner(nn.Module):
         if init_flow is None:
             init_flow = torch.zeros(N, 2, H, W, device=dev)
         return dec._forward(render_feat.contiguous(), real_feat.contiguous(), None, None, R, t, depth,
-                            K, label, init_flow, 0.0, hx=hx)
+                            K, label, init_flow, 0.0, hx=hx, head_label=head_label)

@@ -208,7 +208,8 @@ def refiner_train_forward(refiner, batch: Dict[str, Tensor], model_points: Seque
                           diameters: Sequence[float], iters: int = None) -> Dict[str, Tensor]:
     """Images → losses (SCFlowRefiner.loss), autograd graph attached.  ``batch`` keys:
     render_images, real_images [N,3,S,S]; ref_rotation, ref_translation, gt_rotation,
-    gt_translation, internel_k, depth, label."""
+    gt_translation, internel_k, depth, label; optional head_label (the pose head's class label,
+    default label — a data-parallel shard passes the global batch's label[:1], dist.shard_batch)."""
     dec = refiner.decoder
     iters = int(dec.iters if iters is None else iters)
     real = batch["real_images"].permute(0, 2, 3, 1).contiguous()
@@ -225,8 +226,8 @@ def refiner_train_forward(refiner, batch: Dict[str, Tensor], model_points: Seque
     hc = refiner.h_channels
     h, cxt = torch.tanh(cx[..., :hc]), torch.relu(cx[..., hc:])
     outs = decoder_train(dec, feat_render, feat_real, h, cxt, batch["ref_rotation"],
-                         batch["ref_translation"], batch["depth"], batch["internel_k"], batch["label"],
-                         iters)
+                         batch["ref_translation"], batch["depth"], batch["internel_k"],
+                         batch.get("head_label", batch["label"]), iters)
     with torch.no_grad():  # GT flow: lift with the reference pose, project with the GT pose
         depth = batch["depth"].contiguous().to(dt)
         K = batch["internel_k"].contiguous().to(dt)

@@ -1,5 +1,5 @@
 """CPU, world_size 2 over gloo: batch sharding + end-of-run gather reproduce the single-process
-result exactly (the per-rank compute is the CPU oracle standing in for the GPU decoder, which
+result on a MULTI-CLASS batch (each shard carries the global label[0] for the pose head) (the per-rank compute is the CPU oracle standing in for the GPU decoder, which
 has no CPU path)."""
 import os
 import socket
@@ -36,8 +36,9 @@ def _worker(rank, world, port, q):
         from oracle import scflow_oracle as orc
         from tests.helpers import decoder_inputs, oracle_state_dict
         inp = decoder_inputs(3, 256, seed=4)           # B=3: uneven 2 / 1 split
-        inp["label"] = torch.full_like(inp["label"], 5)  # see DESIGN.md: pose head uses label[0]
+        inp["label"] = torch.tensor([5, 11, 2])          # mixed classes: rank 1's label[0] != 5
         mine = shard_batch(inp, rank, world)
+        assert mine["head_label"].tolist() == [5]        # the global batch's label[0]
         sd = oracle_state_dict()
         out = orc.decoder_forward(sd, **mine, iters=2)
         flow, pred, R, t = gather_results(out)
@@ -63,7 +64,7 @@ def test_sharded_decode_equals_single_process():
     from oracle import scflow_oracle as orc
     from tests.helpers import decoder_inputs, oracle_state_dict
     inp = decoder_inputs(3, 256, seed=4)
-    inp["label"] = torch.full_like(inp["label"], 5)
+    inp["label"] = torch.tensor([5, 11, 2])
     ref = orc.decoder_forward(oracle_state_dict(), **inp, iters=2)
     # CPU conv summation order depends on batch size / threads: equal to fp32 rounding, not bitwise
     assert float(orc.cal_epe_mean(ref[0][-1], flow).max()) < 1e-4

@@ -218,12 +218,15 @@ def test_conv2d_winograd(ops, case):
 
 @pytest.mark.parametrize("k,pad", [((1, 5), (0, 2)), ((5, 1), (2, 0))])
 @pytest.mark.parametrize("bk", [16, 2])
-def test_conv_gru_epilogues(ops, k, pad, bk):
+@pytest.mark.parametrize("n", [2, 16])
+def test_conv_gru_epilogues(ops, k, pad, bk, n):
     """GRU z|r and q epilogues (with a bias map) on the direct (bk 16) and F(4,5) Winograd
-    (bk 2) kernels vs fp64: z = σ(.), r·h, then h ← (1−z)h + z·tanh(q)."""
+    (bk 2) kernels vs fp64: z = σ(.), r·h, then h ← (1−z)h + z·tanh(q).  n=16 is BASELINE
+    configs[1]'s batch: the Winograd launch there takes 64-channel workgroups
+    (conv_wino5_kernel<·,32,2,GRU_ZR/GRU_Q>, the instantiation bench.py times)."""
     from scflow_amd._lib import EPI_GRU_Q, EPI_GRU_ZR
     from scflow_amd.modules import ConvRunner
-    n, h, w, hc = 2, 32, 32, 128
+    h, w, hc = 32, 32, 128
     g = torch.Generator().manual_seed(11)
     hid = torch.tanh(torch.randn(n * h * w, hc, generator=g))
     x = torch.randn(n * h * w, 128, generator=g)

@@ -1,16 +1,41 @@
-"""Per-launch HBM-side traffic of the bench's roofline kernel from two rocprofv3 PMC passes.
+"""Per-launch memory-side traffic of the bench's roofline kernels from two rocprofv3 PMC passes.
 
-usage: python tools/traffic_json.py FETCH_DIR WRITE_DIR SUBSTRING [SUBSTRING ...] > profiles/traffic_gru_zr.json
+usage: python tools/traffic_json.py FETCH_DIR WRITE_DIR --batch B --size S [--iters I]
+           > profiles/traffic_<tag>.json
 
-Kernels whose name contains any SUBSTRING (e.g. the 1×5 and 5×1 z|r launches) are averaged.
+For every kernel group below (kernel-name substrings), the counters of its launches are averaged:
 FETCH_SIZE is doubled per MI355X_MICROARCH.md's gfx950 note (16-B-per-lane reads are tallied at
-64 B per 128-B request); WRITE_SIZE is taken as is; both are KiB, memory side of L2.
+64 B per 128-B request); WRITE_SIZE is taken as is; both are KiB on the memory side of L2
+(Infinity-Cache hits included).  Each group also carries its ALGORITHMIC bytes per launch
+(compulsory reads + writes) and the ratio counter / algorithmic — well above 1
+means re-reads.
 """
+import argparse
 import collections
 import csv
 import glob
 import json
-import sys
+
+
+def groups(B, S):
+    h = w = S // 8
+    M = B * h * w
+    P = h * w
+    f = 4
+    heads = f * (M * 128 + M * 512 + 512 * 128 * 9)            # XHead hidden convs 128→512
+    corr1 = f * (M * 256 + M * 192 + 192 * 256 * 9)            # corr_net.1 256→192
+    zr = f * M * (256 + 256 + 128 + 256) + f * 256 * 256 * 5   # h|motion, bias map, h, z|rh, W
+    lookup = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
+    pose_step = B * 36 * S * S
+    return {
+        "conv_wino_kernel<32,2>": (["conv_wino_kernel<32, 2>"], (heads + corr1) / 2,
+                                   "XHead hidden 128→512 + corr_net.1 256→192 (launches averaged)"),
+        "gru_zr": (["conv_wino5_kernel<0, 32, 2, 1>", "conv_wino5_kernel<1, 32, 2, 1>",
+                    "conv_wino5_kernel<0, 32, 1, 1>", "conv_wino5_kernel<1, 32, 1, 1>"], zr,
+                   "SepConvGRU z|r 1×5 + 5×1 (context hoisted)"),
+        "corr_lookup": (["corr_lookup_lds_kernel"], lookup, "pyramid lookup r=4, 4 levels"),
+        "pose_step": (["pose_step_kernel"], pose_step, "pose update + pose flow + ×8 flow/mask"),
+    }
 
 
 def per_kernel(d, counter):
@@ -23,24 +48,31 @@ def per_kernel(d, counter):
 
 
 def main():
-    fdir, wdir, subs = sys.argv[1], sys.argv[2], sys.argv[3:]
-    fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
-    pick = lambda d: {k: v for k, v in d.items() if any(s in k for s in subs)}  # noqa: E731
-    f, w = pick(fetch), pick(write)
-    fk = {k[:70]: sum(v) / len(v) for k, v in f.items()}
-    wk = {k[:70]: sum(v) / len(v) for k, v in w.items()}
-    favg = sum(sum(v) for v in f.values()) / sum(len(v) for v in f.values())
-    wavg = sum(sum(v) for v in w.values()) / sum(len(v) for v in w.values())
-    m = 16 * 32 * 32
-    alg = 4 * m * (256 + 256 + 128 + 256) + 4 * 256 * 256 * 5  # in h|motion, bias map, h, z|rh out, W
-    print(json.dumps({
-        "kernel": " + ".join(subs) + " (launches averaged)", "batch": 16, "size": 256,
-        "hbm_bytes_per_launch": int((2 * favg + wavg) * 1024),
-        "fetch_size_kb_raw": fk, "write_size_kb": wk,
-        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py "
-                  "--steps 2 --warmup 1 (decoder only); FETCH_SIZE doubled per the gfx950 note; "
-                  "WRITE_SIZE as is; memory-side (L2->fabric) bytes, Infinity-Cache hits included",
-        "algorithmic_bytes_per_launch": alg}, indent=1))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=8)
+    a = ap.parse_args()
+    fetch, write = per_kernel(a.fetch_dir, "FETCH_SIZE"), per_kernel(a.write_dir, "WRITE_SIZE")
+    out = {"batch": a.batch, "size": a.size, "iters": a.iters,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                     "bench.py (decoder leg only); FETCH_SIZE doubled per the gfx950 note; "
+                     "WRITE_SIZE as is; memory-side (L2->fabric) bytes, Infinity-Cache hits included",
+           "kernels": {}}
+    for name, (subs, alg, what) in groups(a.batch, a.size).items():
+        f = [v for k, vs in fetch.items() if any(s in k for s in subs) for v in vs]
+        w = [v for k, vs in write.items() if any(s in k for s in subs) for v in vs]
+        if not f or not w:
+            continue
+        hbm = (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024
+        out["kernels"][name] = {
+            "what": what, "match": subs, "launches_fetch": len(f), "launches_write": len(w),
+            "hbm_bytes_per_launch": int(hbm),
+            "fetch_kb_raw_avg": round(sum(f) / len(f), 1), "write_kb_avg": round(sum(w) / len(w), 1),
+            "algorithmic_bytes_per_launch": int(alg), "ratio_to_algorithmic": round(hbm / alg, 3)}
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
