@@ -29,6 +29,8 @@
  *   scflow_transpose         <- layout plumbing (NCHW <-> channels-last slices), no reference equivalent
  *   scflow_ph_*              <- MultiClassPoseHead.forward                models/head/pose_head.py:201-211
  *   scflow_enc_*             <- RAFTEncoder.forward (Basic; IN / BN)      models/encoder/raft_encoder.py:286-314
+ *   scflow_gemm_f32          <- torch.matmul / F.linear in the training step's adjoints (raft_decoder.py:35-58,
+ *                               pose_head.py:201-211)
  */
 #ifndef SCFLOW_HIP_H
 #define SCFLOW_HIP_H
@@ -338,6 +340,23 @@ typedef struct {
   int n, h, w, cout, kh, kw, stride, ph, pw;
   int accumulate;
 } scflow_wgrad_args;
+/* scflow_gemm_f32: batched strided fp32 GEMM on the matrix cores (training-step contractions:
+ * the correlation volume's backward, the 7x7 convs' dY^T.cols weight gradient, the pose head's
+ * fully connected layers forward/backward; replaces torch.matmul / F.linear there,
+ * raft_decoder.py:35-58 and pose_head.py:201-211 adjoints):
+ *   C[b][m][n] = alpha * sum_k A[b][m][k] * B[b][k][n] (+ beta * C[b][m][n]) (+ bias)
+ * with element strides: A (b, m, k) at b*sab + m*sam + k*sak, B (b, k, n) at b*sbb + k*sbk + n*sbn,
+ * C (b, m, n) at b*scb + m*scm + n*scn.  bias_mode 0: none, 1: bias[n], 2: bias[m].  Any strides
+ * work; float4 loads are used along a unit-stride dimension when the base and outer strides are
+ * 16-byte aligned.  splits > 1 splits K over the grid: workspace holds splits*batch*M*N floats
+ * and a second launch sums the splits in order (deterministic); scflow_gemm_f32_splits() gives
+ * the split count this build picks for a shape (1 = no workspace needed). */
+int scflow_gemm_f32_splits(int batch, int M, int N, int K);
+int scflow_gemm_f32(const float* A, const float* B, float* C, const float* bias, int batch, int M,
+                    int N, int K, long long sab, long long sam, long long sak, long long sbb,
+                    long long sbk, long long sbn, long long scb, long long scm, long long scn,
+                    float alpha, float beta, int bias_mode, int splits, float* workspace,
+                    void* stream);
 int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats);
 int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream);
 int scflow_corr_lookup_backward(const float* dout, int out_layout, int out_stride, const float* flow,

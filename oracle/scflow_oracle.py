@@ -426,7 +426,7 @@ def extract_feat(sd: StateDict, render_images: Tensor, real_images: Tensor,
 # the SCFlowRefiner.loss composition scflow_refiner.py:182-256; weights from
 # configs/refine_models/scflow_ycbv_real.py:231-262)
 # ---------------------------------------------------------------------------------------------
-SYMMETRIC_CLASSES = (12, 15, 18)  # 0-based labels of 'cls_13', 'cls_16', 'cls_19' (config :34-38)
+SYMMETRIC_CLASSES = (12, 15, 18, 19, 20)  # 0-based labels of cls_13, cls_16, cls_19, cls_20, cls_21 (config :34-40)
 
 
 def raft_loss(pred: Tensor, gt: Tensor, valid: Tensor, weight: float = 0.1, max_flow: float = 400.,

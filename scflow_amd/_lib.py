@@ -165,6 +165,9 @@ SIGNATURES = {
                               c_int, c_vp]),
     "scflow_corr_lookup_backward": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int,
                                             c_int, c_int, c_vp]),
+    "scflow_gemm_f32_splits": (c_int, [c_int, c_int, c_int, c_int]),
+    "scflow_gemm_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int] + [c_ll] * 9 +
+                        [c_float, c_float, c_int, c_int, c_vp, c_vp]),
     "scflow_timestamp": (c_int, [c_vp, c_int, c_vp]),
     "scflow_wallclock_khz": (c_ll, []),
 }

@@ -685,3 +685,43 @@ def corr_lookup_backward(dout: Tensor, flow: Tensor, dpyr: Tensor, n: int, h: in
     _launch("scflow_corr_lookup_backward", dout,_p(dout), lay[out_layout], stride, _p(flow),
                                                   lay[flow_layout], _p(dpyr), n, h, w, num_levels,
                                                   radius)
+
+
+def gemm(a: Tensor, b: Tensor, out: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0,
+         bias: Optional[Tensor] = None, bias_dim: str = "n") -> Tensor:
+    """``alpha·(a @ b) [+ beta·out] [+ bias]`` on the HIP fp32 MFMA GEMM (scflow_gemm_f32).
+    ``a`` [M, K] or [Bt, M, K], ``b`` [K, N] or [Bt, K, N] — any strides (transposed views are
+    free); ``out`` [M, N] / [Bt, M, N] (any strides; allocated contiguous if None; read when
+    beta ≠ 0).  ``bias`` [N] (bias_dim "n") or [M] ("m")."""
+    for t, nm in ((a, "a"), (b, "b")):
+        _require(t, nm, contiguous=False)
+    batched = a.dim() == 3
+    if a.dim() != b.dim() or a.dim() not in (2, 3):
+        raise ValueError(f"gemm: a {tuple(a.shape)} and b {tuple(b.shape)} must both be 2-D or 3-D")
+    A = a if batched else a.unsqueeze(0)
+    B = b if batched else b.unsqueeze(0)
+    bt, M, K = A.shape
+    if B.shape[0] != bt or B.shape[1] != K:
+        raise ValueError(f"gemm: shapes {tuple(a.shape)} x {tuple(b.shape)} do not contract")
+    N = B.shape[2]
+    if out is None:
+        if beta != 0.0:
+            raise ValueError("gemm: beta != 0 needs out")
+        out = torch.empty((bt, M, N) if batched else (M, N), device=a.device)
+    _require(out, "out", contiguous=False)
+    C = out if batched else out.unsqueeze(0)
+    if tuple(C.shape) != (bt, M, N):
+        raise ValueError(f"gemm: out {tuple(out.shape)} is not {(bt, M, N)}")
+    mode = 0
+    if bias is not None:
+        _require(bias, "bias")
+        mode = 1 if bias_dim == "n" else 2
+        if bias.numel() != (N if mode == 1 else M):
+            raise ValueError("gemm: bias size")
+    sa, sb, sc = A.stride(), B.stride(), C.stride()
+    splits = int(_lib.load().scflow_gemm_f32_splits(bt, M, N, K))
+    ws = torch.empty(splits * bt * M * N, device=a.device) if splits > 1 else None
+    _launch("scflow_gemm_f32", a, _p(a), _p(b), _p(out), _p(bias), bt, M, N, K,
+            sa[0], sa[1], sa[2], sb[0], sb[1], sb[2], sc[0], sc[1], sc[2], float(alpha), float(beta), mode,
+            splits, _p(ws))
+    return out

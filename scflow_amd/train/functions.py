@@ -9,11 +9,16 @@ Activations are channels-last [N, H, W, C] contiguous fp32 tensors on the ROCm d
   from the saved output; dX = the same HIP conv of the output gradient with the flipped,
   in/out-transposed weights (for stride s > 1 over the gradient zero-inserted to the input
   grid — a transposed conv as a 'same' convolution); dW and db = ``scflow_conv_wgrad`` (MFMA
-  implicit GEMM over the pixels, no im2col matrix); 7×7 kernels fall back to HIP im2col + one
-  plain GEMM dYᵀ·cols (hipBLASLt via ``torch.matmul``).
+  implicit GEMM over the pixels, no im2col matrix); 7×7 kernels use HIP im2col + one
+  ``scflow_gemm_f32`` dYᵀ·cols.
 * ``corr_pyramid`` — forward ``scflow_corr_pyramid``; backward: average-pool adjoints (¼ to each
-  of the 4 children) down to level 0, then dF1 = dC·F2ᵀ/√C, dF2 = dCᵀ·F1/√C as batched GEMMs
-  (hipBLASLt).  (raft_decoder.py:35-58)
+  of the 4 children) down to level 0, then dF1 = dC·F2ᵀ/√C, dF2 = dCᵀ·F1/√C as batched
+  ``scflow_gemm_f32`` launches.  (raft_decoder.py:35-58)
+* ``linear`` — F.linear with the forward and both backward products on ``scflow_gemm_f32``
+  (the pose head's FC layers, pose_head.py:201-211).
+
+No vendor BLAS kernel runs in the training step, so the whole forward + backward can be captured
+into one hipGraph (the vendor GEMM's kernels could not be instantiated in a captured graph).
 * ``corr_lookup`` — forward ``scflow_corr_lookup``; backward ``scflow_corr_lookup_backward``
   (scatter-add into the pyramid gradient; the flow input is detached in SCFlow,
   scflow_decoder.py:193-194).
@@ -132,10 +137,10 @@ def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int,
         return dw, db
     except ScflowError:
         pass
-    # shapes outside the wgrad kernel (7×7): HIP im2col + one plain GEMM (hipBLASLt)
+    # shapes outside the wgrad kernel (7×7): HIP im2col + one HIP GEMM
     x = x0 if x1 is None else torch.cat([x0, x1], -1)
     cols = ops.im2col(x.contiguous(), n, h, wd, cin, kh, kw, s, ph, pw)
-    dwm = torch.matmul(g2.t(), cols)  # [cout, kh·kw·cin]
+    dwm = ops.gemm(g2.t(), cols)  # [cout, kh·kw·cin]
     dw = dwm.view(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
     return dw, (g2.sum(0) if with_bias else None)
 
@@ -217,8 +222,8 @@ class _CorrPyramid(torch.autograd.Function):
         dC = g.view(n, P, P) / (c ** 0.5)                 # dC[n][p][q]
         F1 = f1.view(n, c, P)
         F2 = f2.view(n, c, P)
-        df1 = torch.bmm(F2, dC.transpose(1, 2))            # [n][c][p] = Σ_q F2[c][q] dC[p][q]
-        df2 = torch.bmm(F1, dC)                           # [n][c][q] = Σ_p F1[c][p] dC[p][q]
+        df1 = ops.gemm(F2, dC.transpose(1, 2))  # [n][c][p] = Σ_q F2[c][q] dC[p][q]
+        df2 = ops.gemm(F1, dC)                  # [n][c][q] = Σ_p F1[c][p] dC[p][q]
         return df1.view_as(f1), df2.view_as(f2), None
 
 
@@ -250,3 +255,27 @@ def corr_lookup(pyr: Tensor, flow_nhwc: Tensor, n: int, h: int, w: int, num_leve
                 radius: int = 4) -> Tensor:
     """[n, h, w, L·(2r+1)²] channels-last lookup; differentiable w.r.t. the pyramid only."""
     return _CorrLookup.apply(pyr, flow_nhwc.detach(), n, h, w, num_levels, radius)
+
+
+# ------------------------------------------------------------------------------- linear
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x = x.contiguous()
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return ops.gemm(x, w.detach().t(), bias=None if b is None else b.detach().contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = ops.gemm(dy, w.detach()) if ctx.needs_input_grad[0] else None
+        dw = ops.gemm(dy.t(), x) if ctx.needs_input_grad[1] else None
+        db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None) -> Tensor:
+    """F.linear(x, weight, bias) for 2-D x on the HIP GEMM, forward and backward."""
+    return _Linear.apply(x, weight, bias)

@@ -5,7 +5,8 @@ configs/refine_models/scflow_ycbv_real.py:231-262), batched over the samples.
 The point-matching loss runs all B samples at once when every class's model-point set has the
 same size (one [B, P, 3] gather + batched matmuls); ragged point sets fall back to a per-sample
 loop.  Symmetric classes (SYMMETRIC_CLASSES) replace pytorch3d ``knn_points(K=1)`` by a
-brute-force nearest neighbour (cdist + argmin; indices carry no gradient, as with knn_points).
+brute-force nearest neighbour (squared distances + argmin; indices carry no gradient, as with
+knn_points).
 """
 from __future__ import annotations
 
@@ -16,7 +17,7 @@ import torch.nn.functional as F
 
 Tensor = torch.Tensor
 
-SYMMETRIC_CLASSES = (12, 15, 18)  # 0-based labels of cls_13, cls_16, cls_19 (config :34-38)
+SYMMETRIC_CLASSES = (12, 15, 18, 19, 20)  # 0-based labels of cls_13, cls_16, cls_19, cls_20, cls_21 (config :34-40)
 POSE_WEIGHT, FLOW_WEIGHT, MASK_WEIGHT, GAMMA = 10.0, 0.1, 10.0, 0.8
 
 
@@ -32,15 +33,22 @@ def mask_l1_loss(pred: Tensor, gt: Tensor, weight: float = MASK_WEIGHT) -> Tenso
     return weight * (pred - gt).abs().mean()
 
 
+def matmul3(a: Tensor, b: Tensor) -> Tensor:
+    """Batched a @ b for a tiny inner dimension (3×3 rotations, [B, P, 3] point sets) as
+    broadcast multiply-adds: no vendor GEMM kernel in the training step (it must stay
+    capturable into one hipGraph)."""
+    return (a[..., :, :, None] * b[..., None, :, :]).sum(-2)
+
+
 def _pm_terms(pts: Tensor, pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tensor,
               sym: Tensor) -> Tensor:
     """[B] per-sample (l_rot + l_z + l_xy), l1 norms, disentangle_z."""
-    gt_rot = torch.bmm(pts, gt_r.transpose(1, 2))
+    gt_rot = matmul3(pts, gt_r.transpose(1, 2))
     gt_rt = gt_rot + gt_t[:, None]
-    pred_rot = torch.bmm(pts, pred_r.transpose(1, 2)) + gt_t[:, None]
+    pred_rot = matmul3(pts, pred_r.transpose(1, 2)) + gt_t[:, None]
     if sym is not None:  # symmetric samples: nearest predicted point per GT point (no host sync)
-        with torch.no_grad():
-            idx = torch.cdist(gt_rt, pred_rot).argmin(-1)  # [B, P]
+        with torch.no_grad():  # squared distances by broadcasting (knn_points' metric, no GEMM)
+            idx = ((gt_rt[:, :, None] - pred_rot[:, None]) ** 2).sum(-1).argmin(-1)  # [B, P]
         matched = torch.gather(pred_rot, 1, idx[..., None].expand(-1, -1, 3))
         pred_rot = torch.where(sym[:, None, None], matched, pred_rot)
     l_rot = (pred_rot - gt_rt).abs().sum(-1).mean(-1)

@@ -20,8 +20,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import conv2d_nhwc, corr_lookup, corr_pyramid
-from .losses import filter_flow_by_mask, refine_losses
+from .functions import conv2d_nhwc, corr_lookup, corr_pyramid, linear
+from .losses import filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
 
@@ -84,10 +84,10 @@ def pose_head_train(head, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
         x = torch.relu(y).permute(0, 2, 3, 1)
     v = x.permute(0, 3, 1, 2).reshape(x.shape[0], -1)  # nn.Flatten of NCHW
     for fc in head.fc_layers:
-        v = torch.relu(F.linear(v, fc[0].weight, fc[0].bias))
+        v = torch.relu(linear(v, fc[0].weight, fc[0].bias))
     n = v.shape[0]
-    t = F.linear(v, head.translation_pred.weight, head.translation_pred.bias).view(n, head.num_class, 3)
-    r = F.linear(v, head.rotation_pred.weight, head.rotation_pred.bias).view(
+    t = linear(v, head.translation_pred.weight, head.translation_pred.bias).view(n, head.num_class, 3)
+    r = linear(v, head.rotation_pred.weight, head.rotation_pred.bias).view(
         n, head.num_class, head.rotation_out_channels)
     t = torch.index_select(t, 1, label)[:, 0]
     r = torch.index_select(r, 1, label)[:, 0]
@@ -105,7 +105,7 @@ def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 
     x = _normalize(drot[:, 0:3])
     z = _normalize(torch.cross(x, drot[:, 3:6], dim=1))
     y = torch.cross(z, x, dim=1)
-    Rd = torch.bmm(torch.stack([x, y, z], dim=2), R)
+    Rd = matmul3(torch.stack([x, y, z], dim=2), R)
     vz = t[:, 2] / torch.exp(dt[:, 2]) if depth_transform == "exp" else t[:, 2] * (dt[:, 2] + 1)
     vzxy = vz.detach() if detach_depth_for_xy else vz
     vx = vzxy * (dt[:, 0] / weight + t[:, 0] / t[:, 2])

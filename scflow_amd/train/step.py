@@ -103,12 +103,12 @@ class GradBuckets:
 class TrainStep:
     """forward (HIP) → losses → backward (HIP) → bucketed all-reduce → clip → AdamW.
 
-    ``graph=True`` (experimental, off by default): the forward + backward (≈3000 kernel
+    ``graph=True`` (off by default): the forward + backward (≈3000 kernel
     launches) are captured once into a hipGraph on the third call and replayed on every later
     call with the batch copied into the captured input buffers; the all-reduce, clipping and the
     optimizer step stay eager.  The weights are re-packed inside the graph, so optimizer updates
-    are seen by every replay.  One capture on ROCm 7 segfaulted inside the runtime's graph
-    instantiation, so nothing enables it by default."""
+    are seen by every replay.  Every kernel of the forward + backward is one of ours (no vendor
+    GEMM: see functions.py), and eager steps and the capture run on the step's own stream."""
 
     def __init__(self, refiner, model_points: Sequence[Tensor], diameters: Sequence[float],
                  lr: float = 4e-4, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
@@ -129,6 +129,7 @@ class TrainStep:
         self.opt = torch.optim.AdamW(self.grads.params, lr=lr, betas=betas, eps=eps,
                                      weight_decay=weight_decay, foreach=True)
         dev = self.grads.params[0].device
+        self.stream = torch.cuda.Stream(device=dev)
         self.diam_t = torch.as_tensor(self.diameters, dtype=torch.float32, device=dev)
         if dist.is_initialized() and dist.get_world_size(group) > 1:
             self.broadcast_parameters()
@@ -142,25 +143,21 @@ class TrainStep:
         self.grads.zero()
         out = refiner_train_forward(self.refiner, batch, self.model_points, self.diam_t, self.iters)
         out["loss"].backward()
-        return out
+        # detached: a returned tensor must not keep this step's autograd graph (and its
+        # AccumulateGrad nodes) alive into the next step or a capture
+        return {k: _detach(v) for k, v in out.items()}
 
     def _capture(self, batch: Dict[str, Tensor]) -> None:
         self._static = {k: v.clone() for k, v in batch.items()}
         bufs = [b.clone() for b in self.refiner.buffers()]  # the warm-up must not move BN stats
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):  # allocator warm-up on a side stream (capture recipe)
-            self._fwd_bwd(self._static)
-        torch.cuda.current_stream().wait_stream(side)
+        self._fwd_bwd(self._static)  # allocator warm-up on the step's stream (capture recipe)
         for b, c in zip(self.refiner.buffers(), bufs):
             b.copy_(c)
         self._g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g):
+        with torch.cuda.graph(self._g, stream=self.stream):
             self._out = self._fwd_bwd(self._static)
 
-    def __call__(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
-        self.refiner.train()
-        self._calls += 1
+    def _step(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         if self.graph and self._calls > 2:
             if self._g is None:
                 self._capture(batch)
@@ -170,7 +167,7 @@ class TrainStep:
             self._g.replay()
             # scalars are copied out (the graph overwrites its outputs on the next replay);
             # the per-iteration lists stay views of the graph's buffers
-            out = {k: (v.detach().clone() if isinstance(v, Tensor) and v.dim() == 0 else v)
+            out = {k: (v.clone() if isinstance(v, Tensor) and v.dim() == 0 else v)
                    for k, v in self._out.items()}
         else:
             out = self._fwd_bwd(batch)
@@ -178,3 +175,24 @@ class TrainStep:
         out["grad_norm"] = self.grads.clip_(self.max_norm)
         self.opt.step()
         return out
+
+    def __call__(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        """One step, enqueued on the step's own stream (eager steps and the captured graph see
+        the same stream, so autograd's gradient accumulation never crosses streams), ordered
+        after and before the caller's current stream."""
+        self.refiner.train()
+        self._calls += 1
+        cur = torch.cuda.current_stream(self.stream.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            out = self._step(batch)
+        cur.wait_stream(self.stream)
+        return out
+
+
+def _detach(v):
+    if isinstance(v, Tensor):
+        return v.detach()
+    if isinstance(v, (list, tuple)):
+        return type(v)(_detach(x) for x in v)
+    return v

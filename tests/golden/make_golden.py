@@ -341,9 +341,117 @@ def gen_refine(ref, out, B=2, S=256, iters=4):
     out["meta"] = np.array([B, S, iters, 13])
 
 
+def _knn_points_standin(p1, p2, K=1, **kw):
+    """pytorch3d.ops.knn_points restated for K=1 (absent here): for every point of p1[b] the
+    index of its nearest point of p2[b] by squared Euclidean distance.  Only the symmetric-class
+    fixture exercises it."""
+    assert K == 1
+    d = torch.cdist(p1, p2)
+    dist, idx = d.min(dim=2)
+    return types.SimpleNamespace(dists=(dist ** 2)[..., None], idx=idx[..., None], knn=None)
+
+
+def load_losses(ref, mesh_points):
+    """The reference's loss modules (models/loss/sequence_loss.py, point_matching_loss.py) and
+    models/utils/flow.py.  Test-only stand-ins: ``trimesh.load`` returns the synthetic model
+    points of the class whose file it is asked for (the reference's own ``_load_mesh`` globs and
+    sorts the files); ``pytorch3d.ops.knn_points`` is the brute-force K=1 search above."""
+    import tempfile
+    mesh_dir = tempfile.mkdtemp(prefix="scflow_meshes_")
+    for c in range(len(mesh_points)):
+        open(os.path.join(mesh_dir, f"obj_{c + 1:06d}.obj"), "w").close()
+
+    def _trimesh_load(path):
+        c = int(os.path.basename(path)[4:10]) - 1
+        return types.SimpleNamespace(vertices=np.asarray(mesh_points[c]))
+    _stub("trimesh", load=_trimesh_load)
+    _stub("pytorch3d")
+    _stub("pytorch3d.ops", knn_points=_knn_points_standin)
+    _pkg("models.loss", os.path.join(REF, "models/loss"))
+    seq = _load("models.loss.sequence_loss", "models/loss/sequence_loss.py")
+    pm = _load("models.loss.point_matching_loss", "models/loss/point_matching_loss.py")
+    _load("models.utils.warp", "models/utils/warp.py")
+    flow = _load("models.utils.flow", "models/utils/flow.py")
+    return types.SimpleNamespace(seq=seq, pm=pm, flow=flow, mesh_dir=mesh_dir)
+
+
+# configs/refine_models/scflow_ycbv_real.py:19-21 (mesh_diameter), :34-40 (symmetry_types)
+YCBV_SYMMETRY = {"cls_13": {"z": 0}, "cls_16": {"x": 180, "y": 180, "z": 90}, "cls_19": {"y": 180},
+                 "cls_20": {"x": 180}, "cls_21": {"x": 180, "y": 90, "z": 180}}
+
+
+def gen_train(ref, out, labels, B=2, S=256, iters=2, seed=5):
+    """One training-step slice (SURVEY §8(c) fixture 6): SCFlowRefiner.loss's data flow
+    (scflow_refiner.py:182-242) on the reference's modules in train mode — shared IN feature
+    encoder (seed 1), BN context encoder (seed 2, batch statistics), decoder (seed 0) — the GT
+    flow from pose.get_flow_from_delta_pose_and_depth + flow.filter_flow_by_mask, and the three
+    configured SequenceLosses (config :231-262).  Stores the losses, the per-iteration loss
+    lists and the gradient norm of every parameter (the shared encoder's gradient sums both
+    passes, as it does for the reference's shared module)."""
+    pts = synthetic.make_model_points(256)
+    L = load_losses(ref, pts)
+    raw = synthetic.make_train_batch(B, S, seed=seed, labels=list(labels))
+    t = {k: t32(v) for k, v in raw.items()}
+    enc, ctx = build_encoder(ref, "IN", 1).train(), build_encoder(ref, "BN", 2).train()
+    dec = ref.MODELS.build(dict(type=ref.scflow.SCFlowDecoder, **decoder_cfg(ref, iters)))
+    synthetic.fill_module_(dec, seed=0)
+    dec.train()
+    real_feat = enc(t["real_images"])
+    render_feat = enc(t["render_images"])
+    cxt = ctx(t["render_images"])
+    h_feat, cxt_feat = torch.split(cxt, [128, 128], dim=1)
+    h_feat, cxt_feat = torch.tanh(h_feat), torch.relu(cxt_feat)
+    depth = t["depth"]
+    res = dec(render_feat, real_feat, h_feat, cxt_feat, t["ref_rotation"], t["ref_translation"],
+              depth, t["internel_k"], init_flow=torch.zeros(B, 2, S, S), label=t["label"],
+              invalid_flow_num=0.)
+    flow_pose, flow_pred, Rs, ts, masks, _, _ = res
+    max_flow = 400.
+    gt_flow = ref.pose.get_flow_from_delta_pose_and_depth(
+        t["ref_rotation"], t["ref_translation"], t["gt_rotation"], t["gt_translation"], depth,
+        t["internel_k"], invalid_num=max_flow)
+    gt_flow = L.flow.filter_flow_by_mask(gt_flow, t["gt_masks"], invalid_num=max_flow)
+    rendered_masks = (depth > 0).to(torch.float32)  # base_refiner.py:191
+    pose_loss = L.seq.SequenceLoss(gamma=0.8, loss_func_cfg=dict(
+        type=L.pm.DisentanglePointMatchingLoss, symmetry_types=YCBV_SYMMETRY,
+        mesh_diameter=list(synthetic.YCBV_DIAMETERS), mesh_path=L.mesh_dir, loss_type="l1",
+        disentangle_z=True, loss_weight=10.0))
+    flow_loss = L.seq.SequenceLoss(gamma=0.8, loss_func_cfg=dict(type=L.seq.RAFTLoss, loss_weight=.1,
+                                                                 max_flow=400.))
+    mask_loss = L.seq.SequenceLoss(gamma=0.8, loss_func_cfg=dict(type=L.seq.L1Loss, loss_weight=10.))
+    lp, lp_seq = pose_loss(Rs, ts, gt_r=t["gt_rotation"], gt_t=t["gt_translation"], labels=t["label"],
+                           scale_factors=None)
+    lf, lf_seq = flow_loss(flow_pred, gt_flow=gt_flow, valid=rendered_masks)
+    occ = (torch.sum(gt_flow, dim=1, keepdim=False) < max_flow).to(torch.float32)
+    lm, lm_seq = mask_loss([m.squeeze(dim=1) for m in masks], gt_mask=occ, valid=rendered_masks)
+    loss = lp + lf + lm
+    loss.backward()
+    out["losses"] = np.array([loss.item(), lp.item(), lf.item(), lm.item()])
+    out["seq_losses"] = np.array([[x.item() for x in s] for s in (lp_seq, lf_seq, lm_seq)])
+    out["gt_flow_stats"] = np.array([gt_flow.double().sum().item(), (gt_flow >= max_flow).sum().item(),
+                                     gt_flow[gt_flow < max_flow].double().abs().sum().item()])
+    out["R"] = torch.stack(Rs).detach().numpy()
+    out["t"] = torch.stack(ts).detach().numpy()
+    names, norms = [], []
+    for prefix, mod in (("encoder.", enc), ("context.", ctx), ("decoder.", dec)):
+        for n, p in mod.named_parameters():
+            names.append(prefix + n)
+            norms.append(np.nan if p.grad is None else p.grad.double().norm().item())
+    out["grad_names"] = np.array(names)
+    out["grad_norms"] = np.array(norms)
+    out["meta"] = np.array([B, S, iters, seed, *labels])
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = load_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "train":  # only the training fixtures
+        for tag, labels in (("", (4, 9)), ("_sym", (15, 20))):
+            tr = {}
+            gen_train(ref, tr, labels)
+            np.savez_compressed(os.path.join(HERE, f"golden_train_b2_s256_it2{tag}.npz"), **tr)
+            print(tag, tr["losses"], tr["seq_losses"])
+        return
     ops = {}
     gen_ops(ref, ops)
     np.savez_compressed(os.path.join(HERE, "golden_ops.npz"), **ops)

@@ -164,3 +164,34 @@ def test_corr_lookup_backward(radius):
     torch.cuda.synchronize()
     ref = torch.cat([lv.grad.float().reshape(-1) for lv in levels])
     _close(pyr.grad, ref, 1e-5, 1e-5, "lookup backward")
+
+
+@pytest.mark.parametrize("bt,M,N,K,ta,tb", [
+    (1, 16, 1024, 2048, False, True),     # pose head FC forward: x · Wᵀ
+    (1, 1024, 2048, 16, True, False),     # FC weight grad: dYᵀ · x
+    (4, 256, 1024, 1024, False, True),    # corr backward dF1 = F2 · dCᵀ
+    (4, 256, 1024, 1024, False, False),   # corr backward dF2 = F1 · dC
+    (1, 128, 6272, 4096, True, False),    # 7×7 wgrad dYᵀ · cols
+    (1, 64, 147, 32768, True, False),     # stem wgrad: deep K, split over the grid
+    (2, 64, 98, 8192, True, False),       # batched + split
+    (3, 77, 45, 19, False, False),        # ragged edges, unaligned
+    (2, 130, 129, 33, True, True),
+])
+def test_gemm_f32_strided(bt, M, N, K, ta, tb):
+    """scflow_gemm_f32 vs fp64 torch on transposed / batched views (bias, alpha, beta)."""
+    from scflow_amd import ops
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(bt, K, M, generator=g).transpose(1, 2) if ta else torch.randn(bt, M, K, generator=g)
+    B = torch.randn(bt, N, K, generator=g).transpose(1, 2) if tb else torch.randn(bt, K, N, generator=g)
+    C0 = torch.randn(bt, M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = 0.5 * torch.matmul(A.double(), B.double()) + 2.0 * C0.double() + bias.double()
+    out = C0.cuda()
+    ops.gemm(A.cuda(), B.cuda(), out=out, alpha=0.5, beta=2.0, bias=bias.cuda())
+    scale = float(ref.abs().max())
+    err = float((out.cpu().double() - ref).abs().max())
+    assert err <= 2e-6 * scale * max(1.0, K / 256) ** 0.5, err
+    if bt == 1:  # 2-D call, fresh output, no bias
+        o2 = ops.gemm(A[0].cuda(), B[0].cuda())
+        torch.testing.assert_close(o2.cpu().double(), torch.matmul(A[0].double(), B[0].double()),
+                                   rtol=1e-5, atol=1e-4 * max(1.0, K / 256) ** 0.5)

@@ -51,6 +51,7 @@ def _patch_torch_ops(monkeypatch):
         out0.buf.view(-1, out0.buf.shape[-1])[:, out0.off:out0.off + 2] = f.permute(0, 2, 3, 1).reshape(-1, 2)
 
     monkeypatch.setattr(model, "conv2d_nhwc", conv)
+    monkeypatch.setattr(model, "linear", F.linear)
     monkeypatch.setattr(model, "corr_pyramid", pyramid)
     monkeypatch.setattr(model, "corr_lookup", lookup)
     monkeypatch.setattr(ops, "lift_points", lift)
