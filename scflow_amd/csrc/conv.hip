@@ -706,8 +706,26 @@ bool wino_enabled(int kh) {
   return kh == 3 ? on3 : on5;
 }
 
+// XCD-aware block order for a (R row blocks) × (C column blocks) Winograd grid: the number of
+// column parts across the 8 XCDs (wino_block), 0 when the grid does not divide.
+// SCFLOW_WINO_SWZ=c forces c column parts (tuning); default WINO_SWZ_DEFAULT.
+#ifndef WINO_SWZ_DEFAULT
+#define WINO_SWZ_DEFAULT 0
+#endif
+int wino_swz(int R, int C) {
+  static int forced = -2;
+  if (forced == -2) {
+    const char* e = getenv("SCFLOW_WINO_SWZ");
+    forced = e ? atoi(e) : -1;
+  }
+  int c = forced >= 0 ? forced : WINO_SWZ_DEFAULT;
+  while (c > 1 && (C % c || 8 % c)) c >>= 1;  // largest usable power of two ≤ c
+  if (c <= 0 || R % (8 / c)) return 0;
+  return c;
+}
+
 template <int W, int NBW>
-int launch_wino_w(const WinoParams& p, hipStream_t st) {
+int launch_wino_w(WinoParams p, hipStream_t st) {
   using G = WinoGeom<W>;
   const size_t lds = wino_lds_bytes<W, NBW>();
   static bool attr = false;
@@ -717,12 +735,13 @@ int launch_wino_w(const WinoParams& p, hipStream_t st) {
     attr = true;
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * G::XB, round_up(p.a.cout, 32 * NBW) / (32 * NBW));
+  p.swz_c = wino_swz(grid.x, grid.y);
   conv_wino_kernel<W, NBW><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }
 
 template <int DIR, int W, int NBW, int EPI>
-int launch_wino5_k(const Wino5Params& p, hipStream_t st) {
+int launch_wino5_k(Wino5Params p, hipStream_t st) {
   using G = Wino5Geom<DIR, W>;
   const size_t lds = wino5_lds_bytes<DIR, W, NBW>();
   static bool attr = false;
@@ -732,6 +751,7 @@ int launch_wino5_k(const Wino5Params& p, hipStream_t st) {
     attr = true;
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
+  p.swz_c = wino_swz(grid.x, grid.y);
   conv_wino5_kernel<DIR, W, NBW, EPI><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }

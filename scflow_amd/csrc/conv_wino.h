@@ -44,6 +44,7 @@ __device__ __forceinline__ floatx4 wino_bload(__amdgpu_buffer_rsrc_t r, int voff
 }
 constexpr int WINO_OOB = 0x7ffffff0;  // voffset of a zero-padding lane (beyond any num_records)
 
+#ifndef WX_SCALAR_VALU
 // a + s·b on float4 as two packed FMAs
 __device__ __forceinline__ floatx4 fma_s4(floatx4 b, float s, floatx4 a) {
   floatx2 lo = __builtin_elementwise_fma(floatx2{b[0], b[1]}, floatx2{s, s}, floatx2{a[0], a[1]});
@@ -62,6 +63,20 @@ __device__ __forceinline__ floatx4 sub4(floatx4 a, floatx4 b) {
   const floatx2 hi = floatx2{a[2], a[3]} - floatx2{b[2], b[3]};
   return floatx4{lo[0], lo[1], hi[0], hi[1]};
 }
+#else
+// scalar forms (v_fma_f32 / v_add_f32 issue beside MFMAs without the packed-op penalty);
+// build with -fno-slp-vectorize so they stay scalar
+__device__ __forceinline__ floatx4 fma_s4(floatx4 b, float s, floatx4 a) {
+  return floatx4{__builtin_fmaf(b[0], s, a[0]), __builtin_fmaf(b[1], s, a[1]),
+                 __builtin_fmaf(b[2], s, a[2]), __builtin_fmaf(b[3], s, a[3])};
+}
+__device__ __forceinline__ floatx4 add4(floatx4 a, floatx4 b) {
+  return floatx4{a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]};
+}
+__device__ __forceinline__ floatx4 sub4(floatx4 a, floatx4 b) {
+  return floatx4{a[0] - b[0], a[1] - b[1], a[2] - b[2], a[3] - b[3]};
+}
+#endif
 
 constexpr int WKC = 8;    // input channels per sub-step (one MFMA k-pass per lane)
 constexpr int WSC = 32;   // input channels per stage (one LDS halo buffer)
@@ -71,7 +86,25 @@ constexpr int WTM = 32;   // tiles per workgroup
 struct WinoParams {
   scflow_conv_args a;
   int cp0, nst;  // source 0's channels padded to WSC, stages (WSC channels each) over both
+  int swz_c;     // XCD-aware block order (wino_block): column parts across the 8 XCDs, 0 = off
 };
+
+// (tile block, output-channel block) of this workgroup.  Workgroups are dispatched round-robin
+// over the 8 XCDs (each with its own L2) in linear block order; with swz_c > 0 the grid is cut
+// into an (8/swz_c) × swz_c arrangement of row × column parts, one per XCD, so an XCD's
+// workgroups share their transformed-weight slices (column part) and input halos (row part) in
+// its L2 instead of every XCD touching every column's weights.  Host guarantees divisibility.
+__device__ __forceinline__ void wino_block(int swz_c, int& bx, int& by) {
+  bx = blockIdx.x;
+  by = blockIdx.y;
+  if (swz_c <= 0) return;
+  const int R = gridDim.x, C = gridDim.y;
+  const int id = blockIdx.y * R + blockIdx.x;
+  const int xcd = id & 7, slot = id >> 3;
+  const int rows = R / (8 / swz_c), cols = C / swz_c;
+  by = (xcd % swz_c) * cols + slot % cols;
+  bx = (xcd / swz_c) * rows + slot / cols;
+}
 
 template <int W>
 struct WinoGeom {
@@ -94,7 +127,7 @@ struct WinoGeom {
 template <int W, int NBW>
 constexpr size_t wino_lds_bytes() {
   const size_t halo = (size_t)2 * WinoGeom<W>::BUF4 * 4;  // double-buffered
-  const size_t epi = (size_t)4 * 2 * WTM * 32 * NBW;
+  const size_t epi = (size_t)4 * 2 * (WTM + 4) * 32 * NBW;
   return sizeof(float) * (halo > epi ? halo : epi);
 }
 
@@ -108,9 +141,11 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int li = lane & 31, hh = lane >> 5;
+  int bx, by;
+  wino_block(P.swz_c, bx, by);
   const int blocks_per_img = (a.h / G::OROWS) * G::XB;
-  const int img = blockIdx.x / blocks_per_img;
-  const int brem = blockIdx.x % blocks_per_img;
+  const int img = bx / blocks_per_img;
+  const int brem = bx % blocks_per_img;
   const int oy0 = (brem / G::XB) * G::OROWS, ox0 = (brem % G::XB) * G::OCOLS;
   const int nst0 = P.cp0 / WSC;
   const int nst = P.nst;
@@ -119,6 +154,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   // halo staging: four quarters of NA float4 per thread; slot (part, j) is the (pixel, channel
   // quad) pair (idx >> 3, idx & 7), idx = tid + 256·(4j + part).  Per slot: the input pixel
   // (-1 = zero padding) and the LDS float4 index, both stage-invariant.
+  bool inloop = false;  // tuning experiments (WX_NO_*): prologue loads still happen
   int hpix[4][G::NA], hlds[4][G::NA];
 #pragma unroll
   for (int part = 0; part < 4; ++part)
@@ -154,6 +190,9 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
     }
   };
   auto hload = [&](int part) {
+#ifdef WX_NO_HALO
+    if (inloop) return;
+#endif
     const bool chan_ok = hq4 < hlim;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
@@ -168,6 +207,9 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
     }
   };
   auto hstore = [&](int buf, int part) {
+#ifdef WX_NO_HALO
+    if (inloop) return;
+#endif
 #pragma unroll
     for (int j = 0; j < G::NA; ++j)
       if (G::NH4 % 1024 == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[j];
@@ -177,8 +219,11 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   // ξ = 4·wave + j
   const int nsub = nst * WNSUB;
   const __amdgpu_buffer_rsrc_t wsrc =
-      wino_rsrc(a.weight + (size_t)blockIdx.y * NBW * nsub * 16 * 256, (unsigned)(NBW * nsub * 16 * 1024));
+      wino_rsrc(a.weight + (size_t)by * NBW * nsub * 16 * 256, (unsigned)(NBW * nsub * 16 * 1024));
   auto uload1 = [&](floatx4(&u)[NBW], int t, int j) {  // point j of sub-step t (clamped)
+#ifdef WX_NO_U
+    if (inloop) return;
+#endif
     const int tt = t < nsub ? t : nsub - 1;
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb)
@@ -233,6 +278,11 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   // woven between its point groups in program order — the compiler issues in order, so the LDS
   // latency and the VALU sit under this sub-step's MFMAs instead of in front of them
   auto substep_next = [&](const floatx4(&v)[4], int tnext, int buf, int k, floatx4(&vn)[4]) {
+#ifdef WX_NO_V
+    substep(v, tnext);
+    for (int j = 0; j < 4; ++j) vn[j] = v[j];
+    return;
+#endif
     const floatx4* hb = smem4 + buf * G::BUF4 + 2 * k;
     constexpr int cb1 = 8, cb2 = 16 + 1, cb3 = 24 + 1;  // column b of the patch (+ skew)
     const floatx4 a0 = hb[o1], b0 = hb[o2], a2 = hb[o1 + cb2], b2 = hb[o2 + cb2];
@@ -264,6 +314,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   __syncthreads();
   floatx4 vA[4], vB[4];
   vcompute(0, 0, vA);
+  inloop = true;
   for (int s = 0; s < nst; ++s) {
     const int buf = s & 1;
     const int t0 = s * WNSUB;
@@ -280,47 +331,81 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
     hload(3);
     substep(vB, t0 + 4);
     hstore(buf ^ 1, 3);
+#ifndef WX_NO_SYNC
     __syncthreads();
+#endif
+#ifndef WX_NO_V
     vcompute(buf ^ 1, 0, vA);
+#endif
   }
 
+#ifdef WX_NO_EPI
+  {
+    float t = 0.f;
+    for (int j = 0; j < 4; ++j)
+      for (int nb = 0; nb < NBW; ++nb)
+        for (int e = 0; e < 16; ++e) t += acc[j][nb][e];
+    if (t == 12345.678f) a.out[tid] = t;
+    return;
+  }
+#endif
   // epilogue.  M row i (this wave) folded over j: s0 = M0+M1+M2, s1 = M1−M2−M3, into
-  // S[i][b][tile][co]; then out[a][b] = Σ_i Aᵀ[a][i]·S[i][b].
-  // C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).
+  // S[i][b][co][tile] (tiles contiguous, WEP-float rows: a lane's 4 accumulator rows r..r+3 of
+  // a 32×32 block are 4 consecutive tiles, so each goes out as one 16-B store); then every
+  // thread owns one output position (a, b) of its channel co over a run of tiles and reads the
+  // four rows i of 4 tiles at a time (16-B loads): out[a][b] = Σ_i Aᵀ[a][i]·S[i][b].
+  // C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).  Row stride WEP = 36 floats
+  // keeps both the b128 stores (8-lane groups) and the b128 loads (16-lane groups) conflict-free.
+  constexpr int WEP = WTM + 4;
   __syncthreads();
   float* S = smem;
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = (r & 3) + 8 * (r >> 2) + 4 * hh;
+    for (int q4 = 0; q4 < 4; ++q4) {
       const int co = nb * 32 + li;
-      const float y0 = acc[0][nb][r], y1 = acc[1][nb][r], y2 = acc[2][nb][r], y3 = acc[3][nb][r];
-      S[((wave * 2 + 0) * WTM + m) * BNW + co] = y0 + y1 + y2;
-      S[((wave * 2 + 1) * WTM + m) * BNW + co] = y1 - y2 - y3;
+      floatx4 s0v, s1v;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = 4 * q4 + rr;
+        const float y0 = acc[0][nb][r], y1 = acc[1][nb][r], y2 = acc[2][nb][r], y3 = acc[3][nb][r];
+        s0v[rr] = y0 + y1 + y2;
+        s1v[rr] = y1 - y2 - y3;
+      }
+      const int m0 = 8 * q4 + 4 * hh;
+      *(floatx4*)&S[((wave * 2 + 0) * BNW + co) * WEP + m0] = s0v;
+      *(floatx4*)&S[((wave * 2 + 1) * BNW + co) * WEP + m0] = s1v;
     }
   __syncthreads();
   const int co = tid % BNW;
-  const int col = blockIdx.y * BNW + co;
+  const int col = by * BNW + co;
   if (col >= a.cout) return;
   const float bias = a.bias ? a.bias[col] : 0.f;
   const float osc = a.out_scale ? a.out_scale[col] : 1.f;
   const float osh = a.out_scale ? a.out_shift[col] : 0.f;
-  constexpr int GROUPS = 256 / BNW;
-  constexpr int NPX = WTM * 4 / GROUPS;  // output pixels per thread
+  constexpr int GROUPS = 256 / BNW;            // 4 (BNW 64) or 8 (BNW 32)
+  constexpr int NPX = WTM * 4 / GROUPS;        // output pixels per thread
+  const int g = tid / BNW;
+  const int ar = (g >> 1) & 1, bc = g & 1;      // this thread's output position in the 2×2 tile
+  const int mbase = (g >> 2) * NPX;             // its run of NPX tiles
   size_t pix[NPX];
   float val[NPX];
 #pragma unroll
-  for (int q = 0; q < NPX; ++q) {
-    const int p = tid / BNW + GROUPS * q;  // 0..127: tile m = p>>2, a = (p>>1)&1, b = p&1
-    const int m = p >> 2, ar = (p >> 1) & 1, bc = p & 1;
-    const float* Sb = S + (size_t)bc * WTM * BNW + m * BNW + co;
-    const float s0 = Sb[0 * 2 * WTM * BNW], s1 = Sb[1 * 2 * WTM * BNW];
-    const float s2 = Sb[2 * 2 * WTM * BNW], s3 = Sb[3 * 2 * WTM * BNW];
-    val[q] = ar == 0 ? s0 + s1 + s2 : s1 - s2 - s3;
-    const int y = oy0 + 2 * (m / G::TW) + ar, x = ox0 + 2 * (m % G::TW) + bc;
-    pix[q] = ((size_t)img * a.h + y) * W + x;
-    val[q] = (val[q] + bias) * osc + osh;
+  for (int q4 = 0; q4 < NPX / 4; ++q4) {
+    const int m0 = mbase + 4 * q4;
+    const float* Sb = S + ((size_t)bc * BNW + co) * WEP + m0;
+    const floatx4 s0 = *(const floatx4*)(Sb + 0 * 2 * BNW * WEP);
+    const floatx4 s1 = *(const floatx4*)(Sb + 1 * 2 * BNW * WEP);
+    const floatx4 s2 = *(const floatx4*)(Sb + 2 * 2 * BNW * WEP);
+    const floatx4 s3 = *(const floatx4*)(Sb + 3 * 2 * BNW * WEP);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = 4 * q4 + e, m = m0 + e;
+      const float v = ar == 0 ? s0[e] + s1[e] + s2[e] : s1[e] - s2[e] - s3[e];
+      const int y = oy0 + 2 * (m / G::TW) + ar, x = ox0 + 2 * (m % G::TW) + bc;
+      pix[q] = ((size_t)img * a.h + y) * W + x;
+      val[q] = (v + bias) * osc + osh;
+    }
   }
   // all global reads (bias map, residual) before any store
   if (a.bias_map) {

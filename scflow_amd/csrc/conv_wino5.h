@@ -42,6 +42,7 @@ __host__ __device__ constexpr int w5_point(int w, int x) {
 struct Wino5Params {
   scflow_conv_args a;
   int cp0, nst;  // source 0's channels padded to W5SC, stages (W5SC channels each) over both
+  int swz_c;     // XCD-aware block order (wino_block, conv_wino.h), 0 = off
 };
 
 template <int DIR, int W>  // DIR 0: 1×5 (along x), 1: 5×1 (along y)
@@ -64,7 +65,7 @@ struct Wino5Geom {
 template <int DIR, int W, int NBW>
 constexpr size_t wino5_lds_bytes() {
   const size_t halo = (size_t)2 * Wino5Geom<DIR, W>::BUF4 * 4;  // double-buffered
-  const size_t epi = (size_t)8 * W5TM * 32 * NBW;
+  const size_t epi = (size_t)8 * (W5TM + 4) * 32 * NBW;
   return sizeof(float) * (halo > epi ? halo : epi);
 }
 
@@ -79,9 +80,11 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int li = lane & 31, hh = lane >> 5;
   constexpr int XB = W / G::OCOLS;  // column blocks per image (1, or 2 for 5×1 at W = 64)
+  int bx, by;
+  wino_block(P.swz_c, bx, by);
   const int blocks_per_img = (a.h / G::OROWS) * XB;
-  const int img = blockIdx.x / blocks_per_img;
-  const int rem = blockIdx.x % blocks_per_img;
+  const int img = bx / blocks_per_img;
+  const int rem = bx % blocks_per_img;
   const int oy0 = (rem / XB) * G::OROWS, ox0 = (rem % XB) * G::OCOLS;
   const int nst0 = P.cp0 / W5SC;
   const int nst = P.nst;
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   // point w5_point(wave, x)
   const int nsub = nst * W5NSUB;
   const __amdgpu_buffer_rsrc_t wsrc =
-      wino_rsrc(a.weight + (size_t)blockIdx.y * NBW * nsub * 16 * 256, (unsigned)(NBW * nsub * 16 * 1024));
+      wino_rsrc(a.weight + (size_t)by * NBW * nsub * 16 * 256, (unsigned)(NBW * nsub * 16 * 1024));
   floatx4 u[2][2][NBW];  // [q][x][nb]
   auto uload1 = [&](int t, int q) {
     const int tt = t < nsub ? t : nsub - 1;
@@ -248,7 +251,21 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   else
     mainloop(std::false_type{});
 
-  // epilogue: M[ξ][tile][co] in LDS, then y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ]
+#ifdef WX_NO_EPI
+  {
+    float t = 0.f;
+    for (int x = 0; x < 2; ++x)
+      for (int nb = 0; nb < NBW; ++nb)
+        for (int e = 0; e < 16; ++e) t += acc[x][nb][e];
+    if (t == 12345.678f) a.out[tid] = t;
+    return;
+  }
+#endif
+  // epilogue: M[ξ][co][tile] in LDS (tiles contiguous, WEP-float rows: a lane's accumulator
+  // rows r..r+3 are 4 consecutive tiles → one 16-B store; conflict-free for the b128 stores and
+  // loads, see conv_wino.h), then every thread takes a run of NT tiles of its channel, 4 tiles
+  // per 16-B load of each point, and y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ]
+  constexpr int WEP = W5TM + 4;
   __syncthreads();
   float* S = smem;
 #pragma unroll
@@ -256,38 +273,44 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = (r & 3) + 8 * (r >> 2) + 4 * hh;
-        S[(w5_point(wave, x) * W5TM + m) * BNW + nb * 32 + li] = acc[x][nb][r];
+      for (int q4 = 0; q4 < 4; ++q4) {
+        floatx4 v;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) v[rr] = acc[x][nb][4 * q4 + rr];
+        *(floatx4*)&S[(w5_point(wave, x) * BNW + nb * 32 + li) * WEP + 8 * q4 + 4 * hh] = v;
       }
   __syncthreads();
   const int co = tid % BNW;
-  const int col = blockIdx.y * BNW + co;
+  const int col = by * BNW + co;
   if (col >= a.cout) return;
   const float bias = a.bias ? a.bias[col] : 0.f;
   constexpr int GROUPS = 256 / BNW;
   constexpr int NT = W5TM / GROUPS;  // tiles per thread
+  const int mbase = (tid / BNW) * NT;
   // Every global read of the epilogue (bias map, h, z) is issued before any store: the stores
   // may alias them as far as the compiler knows, so interleaving would serialise NT·4 round
   // trips through memory.
   float y[NT][4];
   int pix[NT][4];  // output pixel (n·h·w < 2^31)
 #pragma unroll
-  for (int k = 0; k < NT; ++k) {
-    const int m = tid / BNW + GROUPS * k;
-    float mv[8];
+  for (int k4 = 0; k4 < NT / 4; ++k4) {
+    floatx4 mv[8];
 #pragma unroll
-    for (int xi = 0; xi < 8; ++xi) mv[xi] = S[(xi * W5TM + m) * BNW + co];
+    for (int xi = 0; xi < 8; ++xi) mv[xi] = *(const floatx4*)&S[(xi * BNW + co) * WEP + mbase + 4 * k4];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      float v = 0.f;
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * k4 + e, m = mbase + k;
 #pragma unroll
-      for (int xi = 0; xi < 8; ++xi)
-        if (kW5AT[o][xi] != 0.f) v += kW5AT[o][xi] * mv[xi];
-      y[k][o] = v + bias;
-      const int oy = DIR == 0 ? oy0 + m / G::TPR : oy0 + o;
-      const int ox = DIR == 0 ? 4 * (m % G::TPR) + o : ox0 + m;
-      pix[k][o] = (img * a.h + oy) * W + ox;
+      for (int o = 0; o < 4; ++o) {
+        float v = 0.f;
+#pragma unroll
+        for (int xi = 0; xi < 8; ++xi)
+          if (kW5AT[o][xi] != 0.f) v += kW5AT[o][xi] * mv[xi][e];
+        y[k][o] = v + bias;
+        const int oy = DIR == 0 ? oy0 + m / G::TPR : oy0 + o;
+        const int ox = DIR == 0 ? 4 * (m % G::TPR) + o : ox0 + m;
+        pix[k][o] = (img * a.h + oy) * W + ox;
+      }
     }
   }
   if (a.bias_map) {

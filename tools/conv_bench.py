@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--size", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="comma-separated substrings of the shapes to run")
+    ap.add_argument("--no-extras", action="store_true", help="skip the pyramid / lookup timings")
     a = ap.parse_args()
     n, h, w = a.batch, a.size, a.size
     M = n * h * w
@@ -54,6 +56,8 @@ def main():
     res = []
     tot_us = 0.0
     for name, c0, c1, cout, k, pad, act, epi in SHAPES:
+        if a.only and not any(t in name for t in a.only.split(",")):
+            continue
         conv = torch.nn.Conv2d(c0 + c1, cout, k, padding=pad).to(dev)
         x0 = torch.randn(M, c0, device=dev)
         x1 = torch.randn(M, c1, device=dev) if c1 else None
@@ -95,6 +99,8 @@ def main():
         res.append(dict(name=name, us=round(us, 2), tflops=round(tf, 2)))
         print(f"{name:28s} {us:9.2f} us  {tf:7.2f} TFLOP/s", flush=True)
     print(f"{'sum (one of each)':28s} {tot_us:9.2f} us")
+    if a.no_extras:
+        return
     # a1 pyramid + a2 lookup (algorithmic bytes: SURVEY.md §8(d))
     C, P = 256, h * w
     f1 = torch.randn(n, C, h, w, device=dev)
