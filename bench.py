@@ -297,6 +297,8 @@ def main():
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="do not bracket the roofline kernels (throughput without timer overhead)")
+    ap.add_argument("--pingpong", action="store_true",
+                    help="run the batch as two interleaved halves (SCFlowDecoder.pingpong)")
     ap.add_argument("--graph", action="store_true",
                     help="replay a captured hipGraph per step instead of launching kernel by kernel")
     ap.add_argument("--traffic-json", default=None,
@@ -326,6 +328,7 @@ def main():
     dec = MODELS.build(decoder_cfg(args.iters, feat))
     synthetic.fill_module_(dec)
     dec = dec.to(dev).eval()
+    dec.pingpong = args.pingpong
     inp = make_inputs(args.batch, args.size, seed=rank, device=dev)
 
     # launches per step of each bracketed kernel: 2 SeqConv stages per iteration for the z|r
@@ -421,9 +424,10 @@ def main():
     units = world * args.batch * args.iters * args.steps
     value = units / elapsed
     h8 = args.size // 8
-    m_px = args.batch * h8 * h8
+    hb = dec.hook_batch or args.batch  # pairs per bracketed launch (a ping-pong half: batch / 2)
+    m_px = hb * h8 * h8
     hc, xc = dec.h_channels, dec.cxt_channels
-    tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_b{args.batch}_s{args.size}.json")
+    tpath = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_b{hb}_s{args.size}.json")
     tj, traffic = load_traffic(tpath)
     traffic = traffic or {}
     alg = {k: v.get("algorithmic_bytes_per_launch") for k, v in (tj or {}).get("kernels", {}).items()}
@@ -447,7 +451,7 @@ def main():
             "conv_wino5_kernel<·,32,2,GRU_ZR> (SepConvGRU z|r, Winograd F(4,5) on fp32 MFMA)"
             if zr.winograd else "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r, direct)",
             [("gru_zr", zr, hc, zr.cin - hc)], timers, m_px, traffic.get("gru_zr"), alg.get("gru_zr")))
-    secondary += secondary_rooflines(timers, args.batch, args.size, traffic,
+    secondary += secondary_rooflines(timers, hb, args.size, traffic,
                                      getattr(dec, "fuse_tail", True))
 
     if rank == 0:
@@ -472,6 +476,8 @@ def main():
                                    f"{args.size}x{args.size}, {args.iters} GRU iters (BASELINE {cfg_name})",
                        "global_batch": args.batch * world, "image": args.size, "iters": args.iters,
                        "launch": "hipGraph replay" if args.graph else "eager",
+                       "schedule": (f"two interleaved halves of {args.batch - hb} + {hb} pairs "
+                                    f"(ping-pong)" if hb != args.batch else "whole batch"),
                        "parallelism": f"dp{world}"},
             "roofline": headline,
             "rooflines_secondary": secondary,

@@ -96,6 +96,13 @@ class SCFlowDecoder(nn.Module):
         # the iteration's tail (pose update, pose flow, ×8 prediction, next ↓8 flow) as one
         # launch (scflow_pose_step); only without flow/correlation masking
         self.fuse_tail = True
+        # a batch of ≥ 2·pingpong_min pairs runs as two interleaved halves (_forward_pingpong).
+        # Off: measured slower at B=16 (5.76 vs 5.33 ms/step) — a half's tail kernels do not get
+        # CUs while the other half's convolutions hold every CU's LDS, so they serialise anyway
+        self.pingpong = False
+        self.pingpong_min = 4
+        self._hooks_on = True
+        self.hook_batch = 0
 
     # ------------------------------------------------------------------ helpers
     def _hidden_heads(self):
@@ -113,26 +120,33 @@ class SCFlowDecoder(nn.Module):
         """Channels of the channels-last GRU working buffer: [h | cxt | motion | flow]."""
         return self.h_channels + self.cxt_channels + self.encoder.out_channels[0] + 2
 
-    def _sync_events(self, dev):
-        """The fork / join events of the side stream (created once per device, on it)."""
+    def _sync_events(self, dev, slot=0):
+        """The fork / join events of a side stream (created once per device and slot, on it)."""
         evs = getattr(self, "_sync_evs", None)
         if evs is None:
             evs = self._sync_evs = {}
-        if dev not in evs:
+        if (dev, slot) not in evs:
             with torch.cuda.device(dev):
-                evs[dev] = (ops.SyncEvent(), ops.SyncEvent())
-        return evs[dev]
+                evs[(dev, slot)] = (ops.SyncEvent(), ops.SyncEvent())
+        return evs[(dev, slot)]
 
-    def _side_stream(self, dev) -> torch.cuda.Stream:
-        """A second HIP stream for the decoder's independent branches (created once per device)."""
+    def _pp_events(self, dev):
+        """The two ping-pong events of _forward_pingpong (device scope, once per device)."""
+        return self._sync_events(dev, "pingpong")
+
+    def _side_stream(self, dev, slot=0) -> torch.cuda.Stream:
+        """An extra HIP stream (created once per device and slot): slot 0 / 1 the side branches
+        of each ping-pong half, "main1" the second half's main stream."""
         ss = getattr(self, "_streams", None)
         if ss is None:
             ss = self._streams = {}
-        if dev not in ss:
-            ss[dev] = torch.cuda.Stream(device=dev)
-        return ss[dev]
+        if (dev, slot) not in ss:
+            ss[(dev, slot)] = torch.cuda.Stream(device=dev)
+        return ss[(dev, slot)]
 
     def _hook(self, name: str, start: bool) -> None:
+        if not self._hooks_on:
+            return
         h = self.kernel_hooks.get(name)
         if h is not None:
             h(start)
@@ -158,8 +172,105 @@ class SCFlowDecoder(nn.Module):
                  invalid, hx: Optional[Tensor] = None, head_label: Optional[Tensor] = None):
         """``hx``: optional channels-last [N·h·w, ≥ hc+xc+co+2] buffer whose first hc+xc channels
         already hold tanh(h) | relu(cxt) (SCFlowRefiner writes the context encoder's output
-        there directly); h_feat / cxt_feat are then ignored."""
+        there directly); h_feat / cxt_feat are then ignored.
+
+        With ``self.pingpong`` and a batch of ≥ 2·``pingpong_min`` pairs the batch runs as two
+        halves interleaved on two stream pairs (``_forward_pingpong``); else as one."""
+        N = feat_render.shape[0]
+        if self.pingpong and hx is None and N >= 2 * self.pingpong_min:
+            return self._forward_pingpong(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K,
+                                          label, init_flow, invalid, head_label)
+        gen = self._forward_steps(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label,
+                                  init_flow, invalid, hx=hx, head_label=head_label)
+        while True:
+            try:
+                next(gen)
+            except StopIteration as e:
+                return e.value
+
+    def _forward_pingpong(self, feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label,
+                          init_flow, invalid, head_label):
+        """The batch as two halves A | B, each a complete forward on its own (main, side) stream
+        pair, with their iterations interleaved so that one half's latency-bound iteration tail
+        (Δflow / mask encoders, pose head, pose update: many small launches that leave most CUs
+        idle) runs while the other half's convolutions fill the chip.  Two device-scope events
+        keep the halves' convolution phases ("heavy": lookup → motion encoder → GRU → heads) in
+        strict alternation: A.heavy(i) → B.heavy(i) → A.heavy(i+1) → …, each half's tail
+        overlapping the other's heavy phase.  Every sample is independent except the pose head's
+        class, which both halves take from the whole batch's label[0] (pose_head.py:208-209), so
+        the result equals the unsplit forward.  Outputs are written straight into the full-batch
+        tensors (per-half views)."""
         dev = feat_render.device
+        N = feat_render.shape[0]
+        n0 = N // 2
+        iters = int(self.iters)
+        _, H, W = depth.shape
+        f32 = torch.float32
+        outs = dict(flow_pose=torch.empty(iters, N, 2, H, W, device=dev, dtype=f32),
+                    flow_pred=torch.empty(iters, N, 2, H, W, device=dev, dtype=f32),
+                    mask=torch.empty(iters, N, 1, H, W, device=dev, dtype=f32),
+                    R=torch.empty(iters, N, 3, 3, device=dev, dtype=f32),
+                    t=torch.empty(iters, N, 3, device=dev, dtype=f32),
+                    drot=torch.empty(iters, N, self.pose_pred.rotation_out_channels, device=dev,
+                                     dtype=f32),
+                    dt=torch.empty(iters, N, 3, device=dev, dtype=f32))
+        gl = (label if head_label is None else head_label).to(dev).long()[:1]
+        cur = torch.cuda.current_stream(dev)
+        mains = [cur, self._side_stream(dev, "main1")]
+        ev = self._pp_events(dev)  # (A heavy done, B heavy done)
+        h_main = [m.cuda_stream for m in mains]
+        mains[1].wait_stream(cur)  # inputs produced on the caller's stream
+        halves = [slice(0, n0), slice(n0, N)]
+
+        def pp(k):
+            def before(it):
+                if k == 1:
+                    ev[0].wait(h_main[1])      # B.heavy(i) after A.heavy(i)
+                elif it > 0:
+                    ev[1].wait(h_main[0])      # A.heavy(i) after B.heavy(i−1)
+
+            def after(it):
+                ev[k].record(h_main[k])
+            return before, after
+
+        gens = []
+        for k, sl in enumerate(halves):
+            sub = dict(flow_pose=outs["flow_pose"][:, sl], flow_pred=outs["flow_pred"][:, sl],
+                       mask=outs["mask"][:, sl], R=outs["R"][:, sl], t=outs["t"][:, sl],
+                       drot=outs["drot"][:, sl], dt=outs["dt"][:, sl])
+            with torch.cuda.stream(mains[k]):
+                gens.append(self._forward_steps(
+                    feat_render[sl], feat_real[sl], h_feat[sl], cxt_feat[sl], R0[sl], t0[sl],
+                    depth[sl], K[sl], label[sl], init_flow[sl], invalid, head_label=gl, outs=sub,
+                    slot=k, pp=pp(k), hooks=k == 0))
+        # host issue order: A.heavy(i), B.heavy(i), A.tail(i), B.tail(i), … (each generator step
+        # runs up to its next yield on its own main stream)
+        live = [True, True]
+        while any(live):
+            for k in (0, 1):
+                if live[k]:
+                    with torch.cuda.stream(mains[k]):
+                        try:
+                            next(gens[k])
+                        except StopIteration:
+                            live[k] = False
+        cur.wait_stream(mains[1])
+        return (list(outs["flow_pose"].unbind(0)), list(outs["flow_pred"].unbind(0)),
+                list(outs["R"].unbind(0)), list(outs["t"].unbind(0)), list(outs["mask"].unbind(0)),
+                list(outs["drot"].unbind(0)), list(outs["dt"].unbind(0)))
+
+    def _forward_steps(self, feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label,
+                       init_flow, invalid, hx: Optional[Tensor] = None,
+                       head_label: Optional[Tensor] = None, outs: Optional[dict] = None,
+                       slot: int = 0, pp=None, hooks: bool = True):
+        """The forward as a generator on the CURRENT stream (+ this slot's side stream): yields
+        after each iteration's heavy phase (through the heads) and after its tail; returns the
+        7 lists.  ``outs``: preallocated output tensors (``_forward_pingpong``'s views);
+        ``pp``: (before_heavy(it), after_heavy(it)) callables ordering this half against the
+        other; ``hooks``: whether the bench's kernel timers bracket this forward's launches."""
+        dev = feat_render.device
+        self._hooks_on = hooks
+        self.hook_batch = feat_render.shape[0]  # pairs per bracketed launch (bench roofline)
         f32 = torch.float32
         feat_render = feat_render.contiguous().float()
         feat_real = feat_real.contiguous().float()
@@ -220,11 +331,15 @@ class SCFlowDecoder(nn.Module):
         s_me = scratch(self.mask_encoder)
 
         # outputs (stacked; the lists returned are views)
-        o_flow_pose = torch.empty(iters, N, 2, H, W, device=dev, dtype=f32)
-        o_flow_pred = torch.empty(iters, N, 2, H, W, device=dev, dtype=f32)
-        o_mask = torch.empty(iters, N, 1, H, W, device=dev, dtype=f32)
-        o_R = torch.empty(iters, N, 3, 3, device=dev, dtype=f32)
-        o_t = torch.empty(iters, N, 3, device=dev, dtype=f32)
+        if outs is not None:
+            o_flow_pose, o_flow_pred, o_mask = outs["flow_pose"], outs["flow_pred"], outs["mask"]
+            o_R, o_t = outs["R"], outs["t"]
+        else:
+            o_flow_pose = torch.empty(iters, N, 2, H, W, device=dev, dtype=f32)
+            o_flow_pred = torch.empty(iters, N, 2, H, W, device=dev, dtype=f32)
+            o_mask = torch.empty(iters, N, 1, H, W, device=dev, dtype=f32)
+            o_R = torch.empty(iters, N, 3, 3, device=dev, dtype=f32)
+            o_t = torch.empty(iters, N, 3, device=dev, dtype=f32)
         drots, dts = [], []
 
         head_runner = self._hidden_heads()
@@ -244,12 +359,12 @@ class SCFlowDecoder(nn.Module):
         # forward, and the main stream always waits for the side branch before reusing them.
         main = torch.cuda.current_stream(dev)
         two = self.side_stream
-        side = self._side_stream(dev) if two else main
+        side = self._side_stream(dev, slot) if two else main
 
         # two events reused every iteration (a wait captures the event's state when issued);
         # device-scope ones (ops.SyncEvent) unless self.device_scope_events is False
         if two and self.device_scope_events:
-            ev_fork, ev_join = self._sync_events(dev)
+            ev_fork, ev_join = self._sync_events(dev, slot)
             h_main, h_side = main.cuda_stream, side.cuda_stream
 
             def fork():
@@ -293,8 +408,12 @@ class SCFlowDecoder(nn.Module):
 
         gru_step = self.gru.bind_step(Chan.whole(HX), Chan.whole(Z), Chan.whole(RH), N, h, w,
                                       ctx_map=ctx_map, cxt_channels=xc)
-        o_drot = torch.empty(iters, N, self.pose_pred.rotation_out_channels, device=dev, dtype=f32)
-        o_dt = torch.empty(iters, N, 3, device=dev, dtype=f32)
+        if outs is not None:
+            o_drot, o_dt = outs["drot"], outs["dt"]
+        else:
+            o_drot = torch.empty(iters, N, self.pose_pred.rotation_out_channels, device=dev,
+                                 dtype=f32)
+            o_dt = torch.empty(iters, N, 3, device=dev, dtype=f32)
         # Fused iteration tail (no masking): one launch does the pose update, the pose flow, this
         # iteration's ×8 prediction (from F2) and the next iteration's ↓8 flow (into the other
         # F2 buffer, computed from the new pose).  F2 alternates between two buffers, so the
@@ -358,6 +477,8 @@ class SCFlowDecoder(nn.Module):
             if self.mask_flow:
                 torch.mul(F2, mask_lr, out=flow_in)
                 HX[:, hx_c - 2:].copy_(flow_in)
+            if pp is not None:
+                pp[0](it)
             # a3 (flow branch) on the side stream
             fork()
             with torch.cuda.stream(side):
@@ -380,6 +501,9 @@ class SCFlowDecoder(nn.Module):
             self._hook("heads", True)
             segment("heads", seg_heads)
             self._hook("heads", False)
+            if pp is not None:
+                pp[1](it)
+            yield "heavy"
             # mask predictor + mask encoder (a5, a6) on the side stream
             fork()
             with torch.cuda.stream(side):
@@ -435,6 +559,7 @@ class SCFlowDecoder(nn.Module):
             flow_full = o_flow_pose[it]
             drots.append(drot)
             dts.append(dtr)
+            yield "tail"
 
         return (list(o_flow_pose.unbind(0)), list(o_flow_pred.unbind(0)), list(o_R.unbind(0)),
                 list(o_t.unbind(0)), list(o_mask.unbind(0)), drots, dts)

@@ -108,6 +108,30 @@ def test_decoder_schedules_bit_identical():
 
 
 @pytest.mark.gpu
+def test_decoder_pingpong_halves_equal_whole_batch():
+    """_forward_pingpong (two interleaved halves on two stream pairs, both taking the whole
+    batch's label[0] for the pose head) against the single-schedule forward of the same
+    multi-class batch: every list, every iteration.  Not bit-identical — a half-batch launch may
+    pick other K splits (pose-head GroupNorm partials) — so EPE ≤ 1e-4 px and rotations /
+    translations to fp32 rounding."""
+    inp = decoder_inputs(8, 256, seed=17)
+    inp["label"] = torch.tensor([3, 11, 0, 7, 20, 3, 15, 9])
+    dec = build_decoder(4, seed=8)
+    dec.pingpong = False
+    whole = run_gpu(dec, inp)
+    dec.pingpong, dec.pingpong_min = True, 4
+    halves = run_gpu(dec, inp)
+    for k in (0, 1):
+        for a, b in zip(whole[k], halves[k]):
+            assert float(orc.cal_epe_mean(a, b).max()) <= 1e-4
+    for k in (2, 3, 5, 6):
+        for a, b in zip(whole[k], halves[k]):
+            torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-5)
+    for a, b in zip(whole[4], halves[4]):
+        torch.testing.assert_close(b, a, rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_decoder_512_feat64():
     inp = decoder_inputs(1, 512, seed=5)
     dec = build_decoder(2, feat_size=(64, 64), seed=2)
