@@ -53,6 +53,11 @@ extern "C" {
 #define SCFLOW_EPI_GRU_ZR 1 /* cout = 2·hc: z = σ(.) -> gate[:, :hc];  r = σ(.), rh = r·h -> rh   */
 #define SCFLOW_EPI_GRU_Q 2  /* cout = hc:   q = tanh(.);  hid <- (1-z)·hid + z·q  (z from gate)     */
 
+/* pose-update mode word (the depth_transform argument of scflow_pose_update / _update_flow /
+ * _step): bit 0 = depth transform (0 'exp', 1 linear); | SCFLOW_POSE_QUAT_XYZW = the delta
+ * rotation is a quaternion (x, y, z, w) [n][4] (pose.py:132-133) instead of ortho6d [n][6]. */
+#define SCFLOW_POSE_QUAT_XYZW 16
+
 #define SCFLOW_LAYOUT_NCHW 0 /* [N][C][H][W] */
 #define SCFLOW_LAYOUT_NHWC 1 /* [N][H][W][stride], channels contiguous */
 
@@ -67,13 +72,19 @@ long long scflow_corr_pyramid_size(int n, int h, int w, int num_levels);
 int scflow_corr_pyramid(const float* f1, const float* f2, float* pyr, int n, int c, int h, int w,
                         int num_levels, void* stream);
 
-/* a2: multi-scale (2r+1)² bilinear window lookup, align_corners=True, zero padding.
+/* a2: multi-scale (2r+1)² bilinear window lookup, align_corners=True (SCFlow's config), zero padding.
  * flow: [n][2][h][w] (flow_layout NCHW) or [n·h·w][2] (NHWC).  out channel
  * k = lvl·(2r+1)² + a·(2r+1) + b samples x+Δx=a−r, y+Δy=b−r.  out: NCHW [n][L(2r+1)²][h][w]
  * or NHWC with pixel stride out_stride (>= L(2r+1)²). */
 int scflow_corr_lookup(const float* pyr, const float* flow, int flow_layout, float* out,
                        int out_layout, int out_stride, int n, int h, int w, int num_levels,
                        int radius, void* stream);
+/* The same with grid_sample's align_corners chosen: 1 = the call above; 0 = CorrLookup(align_corners=
+ * False) (bilinear_sample's own default, corr_lookup.py:35): sample (g+1)·size/2 − 1/2 after the same
+ * g = s·2/max(size−1,1) − 1 normalisation (corr_lookup.py:63-64). */
+int scflow_corr_lookup_ex(const float* pyr, const float* flow, int flow_layout, float* out,
+                          int out_layout, int out_stride, int n, int h, int w, int num_levels,
+                          int radius, int align_corners, void* stream);
 
 /* Channels-last convolution (cross-correlation, like nn.Conv2d) with fused bias/activation and
  * optional ConvGRU gate epilogues.  Input channels = c0 (src0) ++ c1 (src1, may be 0).

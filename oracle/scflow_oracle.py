@@ -81,8 +81,11 @@ def _sample_zero_pad(img: Tensor, ix: Tensor, iy: Tensor) -> Tensor:
     return out
 
 
-def corr_lookup(pyramid: Sequence[Tensor], flow: Tensor, radius: int = 4) -> Tensor:
-    """``CorrLookup.forward`` (corr_lookup.py:102-136), ``align_corners=True``, zeros padding.
+def corr_lookup(pyramid: Sequence[Tensor], flow: Tensor, radius: int = 4,
+                align_corners: bool = True) -> Tensor:
+    """``CorrLookup.forward`` (corr_lookup.py:102-136), zeros padding; ``align_corners`` True
+    (SCFlow's config) or False (bilinear_sample's default, corr_lookup.py:35: grid_sample maps back with
+    ``((g+1)·W − 1)/2``).
 
     * grid = pixel coords (x, y) + flow (coords_grid, :11-28; :114-115);
     * level i: centroid = grid / 2**i, window point = centroid + (dy[i'], dx[j']) where
@@ -110,8 +113,12 @@ def corr_lookup(pyramid: Sequence[Tensor], flow: Tensor, radius: int = 4) -> Ten
         sy = gy / 2 ** lvl + off_y
         nx = sx * 2.0 / max(Wl - 1, 1) - 1.0
         ny = sy * 2.0 / max(Hl - 1, 1) - 1.0
-        ix = (nx + 1) / 2 * (Wl - 1)
-        iy = (ny + 1) / 2 * (Hl - 1)
+        if align_corners:
+            ix = (nx + 1) / 2 * (Wl - 1)
+            iy = (ny + 1) / 2 * (Hl - 1)
+        else:
+            ix = ((nx + 1) * Wl - 1) / 2
+            iy = ((ny + 1) * Hl - 1) / 2
         outs.append(_sample_zero_pad(corr.reshape(-1, Hl, Wl), ix, iy).reshape(B, H, W, n * n))
     out = torch.cat(outs, dim=-1)
     return out.permute(0, 3, 1, 2).contiguous()
@@ -199,6 +206,7 @@ def pose_head(sd: StateDict, x: Tensor, label: Tensor, num_class: int = 21,
     r = F.linear(x, sd[f"{prefix}.rotation_pred.weight"].to(x.dtype),
                  sd[f"{prefix}.rotation_pred.bias"].to(x.dtype))
     t = t.view(-1, num_class, 3)
+    rot_ch = sd[f"{prefix}.rotation_pred.bias"].numel() // num_class  # 6 ortho6d / 4 quaternion
     r = r.view(-1, num_class, rot_ch)
     idx = label.long()
     ar = torch.arange(x.shape[0])
@@ -221,12 +229,30 @@ def rotation_from_ortho6d(o6: Tensor) -> Tensor:
     return torch.stack([x, y, z], dim=2)  # columns x, y, z (pose.py:163-169)
 
 
+def rotation_from_quaternion_xyzw(q: Tensor) -> Tensor:
+    """kornia.geometry.conversions.quaternion_to_rotation_matrix (pose.py:132-133; kornia is
+    unpinned in requirements.txt and absent here — PARITY UNPINNED: restated from kornia's
+    published implementation): q normalised (F.normalize, eps 1e-12), then the unit-quaternion
+    matrix.  Coefficient order x, y, z, w: kornia ≤ 0.6's default, and the order the pose
+    head's identity bias [0, 0, 0, 1] assumes (pose_head.py:192-194)."""
+    q = _normalize(q)
+    x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    tx, ty, tz = 2.0 * x, 2.0 * y, 2.0 * z
+    twx, twy, twz = tx * w, ty * w, tz * w
+    txx, txy, txz = tx * x, ty * x, tz * x
+    tyy, tyz, tzz = ty * y, tz * y, tz * z
+    one = torch.ones_like(x)
+    return torch.stack([one - (tyy + tzz), txy - twz, txz + twy,
+                        txy + twz, one - (txx + tzz), tyz - twx,
+                        txz - twy, tyz + twx, one - (txx + tyy)], dim=-1).view(-1, 3, 3)
+
+
 def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 10.0,
                 depth_transform: str = "exp", detach_depth_for_xy: bool = False) -> Tuple[Tensor, Tensor]:
-    """get_pose_from_delta_pose (pose.py:124-149); detach_depth_for_xy only changes gradients."""
-    if drot.shape[1] != 6:
-        raise NotImplementedError("quaternion delta rotation (kornia) is not on the configured path")
-    Rd = torch.bmm(rotation_from_ortho6d(drot), R)
+    """get_pose_from_delta_pose (pose.py:124-149); detach_depth_for_xy only changes gradients.
+    ``drot`` [n, 6] ortho6d or [n, 4] quaternion (x, y, z, w)."""
+    dR = rotation_from_quaternion_xyzw(drot) if drot.shape[1] == 4 else rotation_from_ortho6d(drot)
+    Rd = torch.bmm(dR, R)
     if depth_transform == "exp":
         vz = t[:, 2] / torch.exp(dt[:, 2])
     else:

@@ -21,10 +21,12 @@
 
 namespace {
 
-__device__ __forceinline__ float unnorm_coord(float s, int size) {
+// bilinear_sample's normalisation g = s·2/max(size−1, 1) − 1 (corr_lookup.py:63-64), then
+// grid_sample's unnormalisation: align_corners ((g+1)/2)·(size−1), else ((g+1)·size − 1)/2
+__device__ __forceinline__ float unnorm_coord(float s, int size, int ac) {
 #pragma clang fp contract(off)
   const float g = (s * 2.f) / (float)(size - 1 > 1 ? size - 1 : 1) - 1.f;
-  return ((g + 1.f) / 2.f) * (float)(size - 1);
+  return ac ? ((g + 1.f) / 2.f) * (float)(size - 1) : ((g + 1.f) * (float)size - 1.f) / 2.f;
 }
 
 __device__ __forceinline__ float tap(const float* __restrict__ m, int x, int y, int Wl, int Hl) {
@@ -35,7 +37,7 @@ template <int R>
 __global__ __launch_bounds__(256) void corr_lookup_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
     float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
-    long long total) {
+    long long total, int ac) {
 #pragma clang fp contract(off)
   constexpr int r = R;
   constexpr int D = 2 * R + 1;
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(
   const float scale = (float)(1 << lvl);
   const float cx = ((float)x + fx) / scale;
   const float cy = ((float)y + fy) / scale;
-  const float ix = unnorm_coord(cx + (float)(a - r), Wl);
+  const float ix = unnorm_coord(cx + (float)(a - r), Wl, ac);
   const float ix_w = floorf(ix);
   const float ix_e = ix_w + 1.f;
   const int xw = (int)ix_w, xe = xw + 1;
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(256) void corr_lookup_kernel(
   const int ostep = out_layout == SCFLOW_LAYOUT_NHWC ? 1 : P;
 #pragma unroll
   for (int b = 0; b < D; ++b) {
-    const float iy = unnorm_coord(cy + (float)(b - r), Hl);
+    const float iy = unnorm_coord(cy + (float)(b - r), Hl, ac);
     const float iy_n = floorf(iy);
     const float iy_s = iy_n + 1.f;
     const int yn = (int)iy_n, ys = yn + 1;
@@ -124,7 +126,7 @@ template <int R>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void corr_lookup_lds_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
     float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
-    int vec_out) {
+    int vec_out, int ac) {
 #pragma clang fp contract(off)
   constexpr int D = 2 * R + 1;
   constexpr int WIN = D + 3;
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     const int l = t / (2 * D), axis = (t / D) % 2, i = t % D;
     const int size = axis == 0 ? (W >> l) : (H >> l);
     const float c = ((float)(axis == 0 ? x : y) + (axis == 0 ? fx : fy)) / (float)(1 << l);
-    crd[slot][l][axis][i] = unnorm_coord(c + (float)(i - R), size);
+    crd[slot][l][axis][i] = unnorm_coord(c + (float)(i - R), size, ac);
   }
   __syncthreads();
   // 1b. per (level, axis): the region origin — −1 for a whole map, else floor(first sample) − 1
@@ -322,9 +324,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 
 }  // namespace
 
-SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_layout, float* out,
-                                  int out_layout, int out_stride, int n, int h, int w,
-                                  int num_levels, int radius, void* stream) {
+SCFLOW_API int scflow_corr_lookup_ex(const float* pyr, const float* flow, int flow_layout, float* out,
+                                     int out_layout, int out_stride, int n, int h, int w,
+                                     int num_levels, int radius, int align_corners, void* stream) {
+  const int ac = align_corners ? 1 : 0;
   if (!pyr || !flow || !out || n <= 0 || h <= 0 || w <= 0 || num_levels < 1 || num_levels > 8 ||
       radius < 0)
     return SCFLOW_EINVAL;
@@ -336,8 +339,17 @@ SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_
   hipStream_t st = (hipStream_t)stream;
   // the LDS kernel addresses one wave's 4 pixel maps of a level through a buffer descriptor
   // (offsets < 2^31 bytes)
-  if (num_levels <= LK_MAXL && radius >= 1 && radius <= 4 &&
-      (long long)LK_PPW * h * w * 4 < LK_OOB) {
+  // LDS kernel: a level's window holds D + 3 columns; without align_corners the samples are
+  // size/(size−1) apart, which fits when every windowed level is ≥ 2r+1 wide and tall
+  bool lds_ok = num_levels <= LK_MAXL && radius >= 1 && radius <= 4 &&
+                (long long)LK_PPW * h * w * 4 < LK_OOB;
+  if (lds_ok && !ac) {
+    for (int l = 0; l < num_levels; ++l) {
+      const int hl = h >> l, wl = w >> l;
+      if (!lk_whole(hl, wl, 2 * radius + 4) && (hl < 2 * radius + 1 || wl < 2 * radius + 1)) lds_ok = false;
+    }
+  }
+  if (lds_ok) {
     const unsigned blk = (unsigned)(((long long)n * h * w + LK_SLOTS - 1) / LK_SLOTS);
     const int D = 2 * radius + 1;
     const int sf = lk_slot_floats(h, w, num_levels, D + 3);
@@ -345,10 +357,10 @@ SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_
     const int vec = out_layout == SCFLOW_LAYOUT_NHWC && out_stride % 4 == 0 &&
                     ((uintptr_t)out & 15) == 0 && sf >= num_levels * D * D;
     switch (radius) {
-      case 1: corr_lookup_lds_kernel<1><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
-      case 2: corr_lookup_lds_kernel<2><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
-      case 3: corr_lookup_lds_kernel<3><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
-      default: corr_lookup_lds_kernel<4><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec); break;
+      case 1: corr_lookup_lds_kernel<1><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
+      case 2: corr_lookup_lds_kernel<2><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
+      case 3: corr_lookup_lds_kernel<3><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
+      default: corr_lookup_lds_kernel<4><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
     }
     return scflow_launch_status();
   }
@@ -357,7 +369,7 @@ SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_
 #define SCFLOW_LK(RR)                                                                            \
   case RR:                                                                                       \
     corr_lookup_kernel<RR><<<blocks, 256, 0, st>>>(pyr, flow, flow_layout, out, out_layout,      \
-                                                   out_stride, n, h, w, num_levels, total);      \
+                                                   out_stride, n, h, w, num_levels, total, ac); \
     break;
   switch (radius) {
     SCFLOW_LK(0) SCFLOW_LK(1) SCFLOW_LK(2) SCFLOW_LK(3) SCFLOW_LK(4) SCFLOW_LK(5) SCFLOW_LK(6)
@@ -365,4 +377,11 @@ SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_
   }
 #undef SCFLOW_LK
   return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_layout, float* out,
+                                  int out_layout, int out_stride, int n, int h, int w,
+                                  int num_levels, int radius, void* stream) {
+  return scflow_corr_lookup_ex(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w,
+                               num_levels, radius, 1, stream);
 }

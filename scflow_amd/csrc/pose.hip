@@ -35,11 +35,36 @@ __device__ void inv3x3(const float* m, float* o) {
   o[8] = (float)((a * e - b * d) * id);
 }
 
-// ortho6d → R (columns x, y, z), then R_dst = ΔR·R_src, and the translation update
-__device__ void pose_update_one(const float* d6, const float* dt, const float* Rs, const float* ts,
-                                float* Rd, float* td, float weight, int depth_transform) {
+// Pose-update mode word (scflow_pose_update / _flow / _step): bit 0 the depth transform
+// (0 exp, 1 linear), SCFLOW_POSE_QUAT_XYZW (16) a 4-value quaternion delta rotation instead of
+// ortho6d.
+__host__ __device__ inline int pose_rot_dim(int mode) { return (mode & SCFLOW_POSE_QUAT_XYZW) ? 4 : 6; }
+__host__ inline bool pose_mode_ok(int mode) { return (mode & ~(SCFLOW_POSE_QUAT_XYZW | 1)) == 0; }
+
+// ΔR from the head's rotation output:
+//  ortho6d (pose.py:153-169): x = normalize(o[0:3]), z = normalize(x × o[3:6]), y = z × x,
+//    columns (x, y, z);
+//  quaternion (pose.py:132-133, kornia.geometry.conversions.quaternion_to_rotation_matrix with
+//    the x, y, z, w coefficient order that the head's identity bias [0, 0, 0, 1] implies,
+//    pose_head.py:192-194): q = q / max(‖q‖, 1e-12), then the standard unit-quaternion matrix.
+__device__ void delta_rotation(const float* d, int quat, float* D) {
 #pragma clang fp contract(off)
-  float x[3] = {d6[0], d6[1], d6[2]}, yr[3] = {d6[3], d6[4], d6[5]};
+  if (quat) {
+    float q[4] = {d[0], d[1], d[2], d[3]};
+    float nq = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    nq = fmaxf(nq, 1e-12f);
+    for (int k = 0; k < 4; ++k) q[k] = q[k] / nq;
+    const float x = q[0], y = q[1], z = q[2], w = q[3];
+    const float tx = 2.f * x, ty = 2.f * y, tz = 2.f * z;
+    const float twx = tx * w, twy = ty * w, twz = tz * w;
+    const float txx = tx * x, txy = ty * x, txz = tz * x;
+    const float tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    D[0] = 1.f - (tyy + tzz); D[1] = txy - twz;         D[2] = txz + twy;
+    D[3] = txy + twz;         D[4] = 1.f - (txx + tzz); D[5] = tyz - twx;
+    D[6] = txz - twy;         D[7] = tyz + twx;         D[8] = 1.f - (txx + tyy);
+    return;
+  }
+  float x[3] = {d[0], d[1], d[2]}, yr[3] = {d[3], d[4], d[5]};
   float nx = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
   nx = fmaxf(nx, 1e-12f);
   for (int k = 0; k < 3; ++k) x[k] = x[k] / nx;
@@ -48,7 +73,19 @@ __device__ void pose_update_one(const float* d6, const float* dt, const float* R
   nz = fmaxf(nz, 1e-12f);
   for (int k = 0; k < 3; ++k) z[k] = z[k] / nz;
   float y[3] = {z[1] * x[2] - z[2] * x[1], z[2] * x[0] - z[0] * x[2], z[0] * x[1] - z[1] * x[0]};
-  float D[9] = {x[0], y[0], z[0], x[1], y[1], z[1], x[2], y[2], z[2]};
+  D[0] = x[0]; D[1] = y[0]; D[2] = z[0];
+  D[3] = x[1]; D[4] = y[1]; D[5] = z[1];
+  D[6] = x[2]; D[7] = y[2]; D[8] = z[2];
+}
+
+// ΔR (ortho6d or quaternion), then R_dst = ΔR·R_src, and the translation update
+// (get_pose_from_delta_pose, pose.py:124-149)
+__device__ void pose_update_one(const float* d6, const float* dt, const float* Rs, const float* ts,
+                                float* Rd, float* td, float weight, int mode) {
+#pragma clang fp contract(off)
+  const int depth_transform = mode & 1;
+  float D[9];
+  delta_rotation(d6, (mode & SCFLOW_POSE_QUAT_XYZW) != 0, D);
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 3; ++c) {
       float s = D[r * 3 + 0] * Rs[0 * 3 + c];
@@ -67,8 +104,8 @@ __global__ void pose_update_kernel(const float* drot6, const float* dt, const fl
                                    int depth_transform) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  pose_update_one(drot6 + 6 * i, dt + 3 * i, Rs + 9 * i, ts + 3 * i, Rd + 9 * i, td + 3 * i, weight,
-                  depth_transform);
+  pose_update_one(drot6 + pose_rot_dim(depth_transform) * i, dt + 3 * i, Rs + 9 * i, ts + 3 * i,
+                  Rd + 9 * i, td + 3 * i, weight, depth_transform);
 }
 
 __global__ __launch_bounds__(256) void lift_kernel(const float* __restrict__ depth,
@@ -145,8 +182,8 @@ __device__ __forceinline__ void pose_prologue(float* sh, int n, const float* dro
                                               int depth_transform, int upd) {
   if (threadIdx.x == 0) {
     if (upd) {
-      pose_update_one(drot6 + 6 * n, dtv + 3 * n, Rsrc + 9 * n, tsrc + 3 * n, sh, sh + 9, weight,
-                      depth_transform);
+      pose_update_one(drot6 + pose_rot_dim(depth_transform) * n, dtv + 3 * n, Rsrc + 9 * n,
+                      tsrc + 3 * n, sh, sh + 9, weight, depth_transform);
       if (blockIdx.x == 0) {
         for (int k = 0; k < 9; ++k) Rout[9 * n + k] = sh[k];
         for (int k = 0; k < 3; ++k) tout[3 * n + k] = sh[9 + k];
@@ -354,7 +391,7 @@ SCFLOW_API int scflow_pose_update(const float* drot6, const float* dt, const flo
                                   const float* t_src, float* R_dst, float* t_dst, int n,
                                   float weight, int depth_transform, void* stream) {
   if (!drot6 || !dt || !R_src || !t_src || !R_dst || !t_dst || n <= 0 ||
-      (depth_transform != 0 && depth_transform != 1))
+      !pose_mode_ok(depth_transform))
     return SCFLOW_EINVAL;
   pose_update_kernel<<<(n + 63) / 64, 64, 0, (hipStream_t)stream>>>(drot6, dt, R_src, t_src, R_dst,
                                                                    t_dst, n, weight, depth_transform);
@@ -389,7 +426,7 @@ SCFLOW_API int scflow_pose_update_flow(const float* drot6, const float* dt, cons
                                        int w, float weight, int depth_transform,
                                        float invalid_num, void* stream) {
   if (!drot6 || !dt || !R_src || !t_src || !K || !points || !R_dst || !t_dst || !flow || n <= 0 ||
-      h <= 0 || w <= 0 || (depth_transform != 0 && depth_transform != 1))
+      h <= 0 || w <= 0 || !pose_mode_ok(depth_transform))
     return SCFLOW_EINVAL;
   if (!aligned16(points)) return SCFLOW_EALIGN;
   const int bx = ceil_div((long long)h * w, 256) < 256 ? ceil_div((long long)h * w, 256) : 256;
@@ -429,7 +466,7 @@ SCFLOW_API int scflow_pose_step(const float* drot6, const float* dt, const float
                                 float* hx_next, int s_hx, int h, int w, float up_scale,
                                 float down_scale, void* stream) {
   if (!drot6 || !dt || !R_src || !t_src || !K || !points || !R_dst || !t_dst || !flow || n <= 0 ||
-      H <= 0 || W <= 0 || (depth_transform != 0 && depth_transform != 1))
+      H <= 0 || W <= 0 || !pose_mode_ok(depth_transform))
     return SCFLOW_EINVAL;
   if ((flow_up || lr_next) && (h <= 0 || w <= 0)) return SCFLOW_EINVAL;
   if (flow_up && !lr) return SCFLOW_EINVAL;

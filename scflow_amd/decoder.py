@@ -427,7 +427,7 @@ class SCFlowDecoder(nn.Module):
 
         def seg_lookup():
             ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
-                            flow_layout="nhwc")
+                            flow_layout="nhwc", align_corners=self.corr_lookup.align_corners)
 
         corr_net = self.encoder.corr_net
 

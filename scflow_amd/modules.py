@@ -231,14 +231,14 @@ class CorrelationPyramid(nn.Module):
 
 
 class CorrLookup(nn.Module):
-    """corr_lookup.py:71-136.  Only the configuration SCFlow uses exists as a kernel:
-    bilinear, zero padding, align_corners=True."""
+    """corr_lookup.py:71-136: bilinear, zero padding, align_corners True (SCFlow's config) or
+    False (bilinear_sample's default, corr_lookup.py:35)."""
 
     def __init__(self, radius: int = 4, mode: str = "bilinear", padding_mode: str = "zeros",
                  align_corners: bool = True) -> None:
         super().__init__()
-        if mode != "bilinear" or padding_mode != "zeros" or not align_corners:
-            raise NotImplementedError("CorrLookup kernel: bilinear / zeros / align_corners=True only")
+        if mode != "bilinear" or padding_mode != "zeros":
+            raise NotImplementedError("CorrLookup kernel: bilinear sampling with zero padding only")
         self.r = radius
         self.mode = mode
         self.padding_mode = padding_mode
@@ -247,7 +247,8 @@ class CorrLookup(nn.Module):
     def forward(self, corr_pyramid: Sequence[Tensor], flow: Tensor) -> Tensor:
         B, _, H, W = flow.shape
         buf = ops.pyramid_buffer(corr_pyramid, B, H, W)
-        return ops.corr_lookup(buf, flow.contiguous().float(), B, H, W, len(corr_pyramid), self.r)
+        return ops.corr_lookup(buf, flow.contiguous().float(), B, H, W, len(corr_pyramid), self.r,
+                               align_corners=self.align_corners)
 
 
 # ---------------------------------------------------------------------------------- a3

@@ -178,9 +178,11 @@ def pyramid_buffer(levels: Sequence[Tensor], n: int, h: int, w: int) -> Tensor:
 
 # ------------------------------------------------------------------------------- a2 lookup
 def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: int, radius: int,
-                out: Optional[Chan] = None, flow_layout: str = "nchw") -> Tensor:
+                out: Optional[Chan] = None, flow_layout: str = "nchw",
+                align_corners: bool = True) -> Tensor:
     """Window lookup.  ``out=None`` → NCHW ``[n, L(2r+1)², h, w]`` (the reference's layout,
-    corr_lookup.py:135-136); otherwise written channels-last into ``out``."""
+    corr_lookup.py:135-136); otherwise written channels-last into ``out``.  ``align_corners``:
+    grid_sample's (SCFlow's config True; False: bilinear_sample's default, corr_lookup.py:35)."""
     _require(pyr, "pyramid")
     _require(flow, "flow")
     K = num_levels * (2 * radius + 1) ** 2
@@ -191,8 +193,12 @@ def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: i
     else:
         res = out.buf
         ptr, olay, ostride = out.ptr, _lib.LAYOUT_NHWC, out.stride
-    _launch("scflow_corr_lookup", flow,_p(pyr), _p(flow), lay, ptr, olay, ostride, n, h, w,
-                                         num_levels, radius)
+    if align_corners:
+        _launch("scflow_corr_lookup", flow, _p(pyr), _p(flow), lay, ptr, olay, ostride, n, h, w,
+                num_levels, radius)
+    else:
+        _launch("scflow_corr_lookup_ex", flow, _p(pyr), _p(flow), lay, ptr, olay, ostride, n, h, w,
+                num_levels, radius, 0)
     return res
 
 
@@ -357,16 +363,27 @@ def lift_points(depth: Tensor, K: Tensor, R: Tensor, t: Tensor) -> Tensor:
     return pts
 
 
+POSE_QUAT_XYZW = 16  # SCFLOW_POSE_QUAT_XYZW
+
+
+def pose_mode(drot: Tensor, depth_transform: str) -> int:
+    """The C-ABI pose-update mode word: depth transform bit | quaternion flag (drot [n, 4])."""
+    if drot.dim() != 2 or drot.shape[1] not in (4, 6):
+        raise ValueError(f"delta rotation must be [n, 6] (ortho6d) or [n, 4] (quaternion x, y, z, w), "
+                         f"got {tuple(drot.shape)}")
+    return (0 if depth_transform == "exp" else 1) | (POSE_QUAT_XYZW if drot.shape[1] == 4 else 0)
+
+
 def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 10.0,
                 depth_transform: str = "exp") -> Tuple[Tensor, Tensor]:
+    """get_pose_from_delta_pose (pose.py:124-149): drot ortho6d [n, 6] or quaternion [n, 4]."""
     for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t)):
         _require(x, nm)
-    if drot.shape[1] != 6:
-        raise NotImplementedError("only ortho6d delta rotations are on the SCFlow path")
+    mode = pose_mode(drot, depth_transform)
     n = drot.shape[0]
     Ro, to = torch.empty_like(R), torch.empty_like(t)
-    _launch("scflow_pose_update", drot,_p(drot), _p(dt), _p(R), _p(t), _p(Ro), _p(to), n,
-                                         float(weight), 0 if depth_transform == "exp" else 1)
+    _launch("scflow_pose_update", drot, _p(drot), _p(dt), _p(R), _p(t), _p(Ro), _p(to), n,
+            float(weight), mode)
     return Ro, to
 
 
@@ -390,7 +407,7 @@ def pose_update_flow(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, 
     n, h, w, _ = points.shape
     _launch("scflow_pose_update_flow", drot,
         _p(drot), _p(dt), _p(R), _p(t), _p(K), _p(points), _p(R_out), _p(t_out), _p(flow_out), n, h,
-        w, float(weight), 0 if depth_transform == "exp" else 1, float(invalid_num))
+        w, float(weight), pose_mode(drot, depth_transform), float(invalid_num))
 
 
 def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points: Tensor,
@@ -411,7 +428,7 @@ def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points:
         raise ValueError("pose_step: lr_next must not alias lr")
     _launch("scflow_pose_step", drot,
         _p(drot), _p(dt), _p(R), _p(t), _p(K), _p(points), _p(R_out), _p(t_out), _p(flow_out), n,
-        H, W, float(weight), 0 if depth_transform == "exp" else 1, float(invalid_num), _p(lr),
+        H, W, float(weight), pose_mode(drot, depth_transform), float(invalid_num), _p(lr),
         _p(delta), _p(mask), _p(flow_up), _p(mask_up),
         None if lr_next is None else lr_next.ptr, 0 if lr_next is None else lr_next.stride,
         None if hx_next is None else hx_next.ptr, 0 if hx_next is None else hx_next.stride,

@@ -101,11 +101,23 @@ def _normalize(v: Tensor) -> Tensor:
 
 def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 10.0,
                 depth_transform: str = "exp", detach_depth_for_xy: bool = True) -> Tuple[Tensor, Tensor]:
-    """get_pose_from_delta_pose + get_rotation_matrix_from_ortho6d (pose.py:124-169)."""
-    x = _normalize(drot[:, 0:3])
-    z = _normalize(torch.cross(x, drot[:, 3:6], dim=1))
-    y = torch.cross(z, x, dim=1)
-    Rd = matmul3(torch.stack([x, y, z], dim=2), R)
+    """get_pose_from_delta_pose + get_rotation_matrix_from_ortho6d (pose.py:124-169); a [n, 4]
+    drot is a quaternion (x, y, z, w; pose.py:132-133, see oracle.rotation_from_quaternion_xyzw)."""
+    if drot.shape[1] == 4:
+        q = drot / drot.norm(dim=1, keepdim=True).clamp_min(1e-12)
+        qx, qy, qz, qw = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+        tx, ty, tz = 2.0 * qx, 2.0 * qy, 2.0 * qz
+        one = torch.ones_like(qx)
+        D = torch.stack([one - (ty * qy + tz * qz), ty * qx - tz * qw, tz * qx + ty * qw,
+                         ty * qx + tz * qw, one - (tx * qx + tz * qz), tz * qy - tx * qw,
+                         tz * qx - ty * qw, tz * qy + tx * qw, one - (tx * qx + ty * qy)],
+                        dim=-1).view(-1, 3, 3)
+        Rd = matmul3(D, R)
+    else:
+        x = _normalize(drot[:, 0:3])
+        z = _normalize(torch.cross(x, drot[:, 3:6], dim=1))
+        y = torch.cross(z, x, dim=1)
+        Rd = matmul3(torch.stack([x, y, z], dim=2), R)
     vz = t[:, 2] / torch.exp(dt[:, 2]) if depth_transform == "exp" else t[:, 2] * (dt[:, 2] + 1)
     vzxy = vz.detach() if detach_depth_for_xy else vz
     vx = vzxy * (dt[:, 0] / weight + t[:, 0] / t[:, 2])

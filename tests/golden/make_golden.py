@@ -208,6 +208,9 @@ def gen_ops(ref, out):
     for r in (4, 1):
         lk = ref.corr_lookup.CorrLookup(radius=r, align_corners=True)
         out[f"lk_r{r}"] = lk([p.clone() for p in pyr], t32(flow)).numpy()
+    # align_corners=False (bilinear_sample's default, corr_lookup.py:35; a CorrLookup option)
+    lk = ref.corr_lookup.CorrLookup(radius=4, align_corners=False)
+    out["lk_r4_ac0"] = lk([p.clone() for p in pyr], t32(flow)).numpy()
     # (3) one SeqConv GRU step, h/x at 2×8×8 (h 8 ch, x 16 ch)
     gru = ref.raft.ConvGRU(8, 16, net_type="SeqConv")
     synthetic.fill_module_(gru, seed=3)
@@ -445,6 +448,11 @@ def gen_train(ref, out, labels, B=2, S=256, iters=2, seed=5):
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = load_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == "ops":  # only golden_ops.npz
+        ops = {}
+        gen_ops(ref, ops)
+        np.savez_compressed(os.path.join(HERE, "golden_ops.npz"), **ops)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "train":  # only the training fixtures
         for tag, labels in (("", (4, 9)), ("_sym", (15, 20))):
             tr = {}

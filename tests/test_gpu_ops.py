@@ -62,6 +62,27 @@ def test_corr_lookup_golden(ops, radius):
     close(out, t(gd[f"lk_r{radius}"]), 2e-5, 2e-5, "lookup vs reference fixture")
 
 
+def test_corr_lookup_align_corners_false(ops):
+    """CorrLookup(align_corners=False) (bilinear_sample's default, corr_lookup.py:35): the fixture from
+    the reference's own module, then random flows on the LDS kernel (windowed and whole-map
+    levels, 32² and 64²) and on the generic kernel (a windowed level narrower than 2r+1)."""
+    from scflow_amd.modules import CorrLookup
+    gd = golden("ops")
+    _, lv = ops.corr_pyramid(t(gd["pyr_f1"]).cuda(), t(gd["pyr_f2"]).cuda(), 4)
+    out = CorrLookup(radius=4, align_corners=False)(lv, t(gd["lk_flow"]).cuda())
+    close(out, t(gd["lk_r4_ac0"]), 2e-5, 2e-5, "lookup align_corners=False vs reference fixture")
+    g = torch.Generator().manual_seed(23)
+    for n, h, w, L, r in ((2, 32, 32, 4, 4), (1, 64, 64, 4, 4), (2, 24, 20, 3, 4), (2, 16, 16, 2, 3)):
+        f1 = torch.randn(n, 8, h, w, generator=g)
+        f2 = torch.randn(n, 8, h, w, generator=g)
+        flow = (torch.rand(n, 2, h, w, generator=g) - 0.5) * h
+        flow[:, :, 0, 0] = torch.tensor([0.5, -0.5])
+        buf, lv = ops.corr_pyramid(f1.cuda(), f2.cuda(), L)
+        ref = orc.corr_lookup([x.cpu() for x in lv], flow, r, align_corners=False)
+        got = ops.corr_lookup(buf, flow.cuda(), n, h, w, L, r, align_corners=False)
+        close(got, ref, 1e-5, 1e-5, f"lookup align_corners=False {n}x{h}x{w} L{L} r{r}")
+
+
 @pytest.mark.parametrize("n,h,w", [(2, 32, 32), (1, 64, 64), (3, 20, 28)])
 def test_corr_lookup_random(ops, n, h, w):
     g = torch.Generator().manual_seed(2)
@@ -325,6 +346,31 @@ def test_pose_full_res_vs_oracle(ops):
     close(Ro, Rr, 2e-6, 0, "R")
     close(fl, ref, 5e-3, 1e-5, "flow")
     assert ((fl.cpu() == 0) == ~valid[:, None].expand(-1, 2, -1, -1)).all()
+
+
+def test_pose_update_quaternion(ops):
+    """Quaternion (x, y, z, w) delta rotations through pose_update, pose_update_flow and the
+    fused pose_step, against the oracle (pose.py:132-133; kornia absent → parity unpinned
+    against the reference, the oracle's convention is checked against scipy)."""
+    from scflow_amd import synthetic
+    sc = synthetic.make_scene(3, 64, seed=4)
+    R0, t0, K, depth = (t(sc[k]).cuda() for k in ("ref_rotation", "ref_translation", "internel_k", "depth"))
+    g = torch.Generator().manual_seed(8)
+    q = torch.tensor([[0.0, 0, 0, 1.0]]).repeat(3, 1) + 0.1 * torch.randn(3, 4, generator=g)
+    q[2] *= 3.0  # un-normalised
+    dt = 0.05 * torch.randn(3, 3, generator=g)
+    Rr, tr = orc.pose_update(q.double(), dt.double(), R0.cpu().double(), t0.cpu().double())
+    Ro, to = ops.pose_update(q.cuda(), dt.cuda(), R0, t0)
+    close(Ro, Rr, 2e-6, 0, "R quaternion")
+    close(to, tr, 1e-5, 1e-6, "t quaternion")
+    pts = ops.lift_points(depth, K, R0, t0)
+    Rf, tf = torch.empty_like(Ro), torch.empty_like(to)
+    fl = torch.empty(3, 2, 64, 64, device="cuda")
+    ops.pose_update_flow(q.cuda(), dt.cuda(), R0, t0, K, pts, Rf, tf, fl, 0.0)
+    close(Rf, Ro, 0, 0, "fused R quaternion")
+    pts_r, valid = orc.lift_points(depth.cpu().double(), K.cpu().double(), R0.cpu().double(),
+                                   t0.cpu().double())
+    close(fl, orc.pose_flow(Rr, tr, K.cpu().double(), pts_r, valid, 0.0), 5e-3, 1e-5, "flow quaternion")
 
 
 @pytest.mark.parametrize("S,s,nxt", [(256, 32, True), (256, 32, False), (128, 16, True)])

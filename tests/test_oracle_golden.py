@@ -27,6 +27,15 @@ def test_corr_lookup_matches_reference(radius):
     np.testing.assert_allclose(out.numpy(), g[f"lk_r{radius}"], rtol=1e-5, atol=1e-6)
 
 
+def test_corr_lookup_align_corners_false_matches_reference():
+    """CorrLookup(align_corners=False) (grid_sample's other convention; bilinear_sample's own
+    default, corr_lookup.py:35)."""
+    g = golden("ops")
+    pyr = [t(g[f"pyr_l{i}"]) for i in range(4)]
+    out = orc.corr_lookup(pyr, t(g["lk_flow"]), 4, align_corners=False)
+    np.testing.assert_allclose(out.numpy(), g["lk_r4_ac0"], rtol=1e-5, atol=1e-6)
+
+
 def test_conv_gru_matches_reference():
     g = golden("ops")
     from scflow_amd import synthetic
@@ -113,3 +122,29 @@ def test_refine_e2e_matches_reference():
     assert float(orc.cal_epe_mean(t(g["flow_pose_last"]), fp[-1]).max()) <= 1e-3
     assert float(orc.cal_epe_mean(t(g["flow_pred_last"]), fpred[-1]).max()) <= 1e-3
     np.testing.assert_allclose(torch.stack(ts).numpy(), g["t"], rtol=1e-5, atol=1e-3)
+
+
+def test_quaternion_delta_rotation_convention():
+    """The quaternion branch of get_pose_from_delta_pose (pose.py:132-133) goes through kornia,
+    which is absent and unpinned (PARITY UNPINNED against the reference): the oracle's
+    restatement is checked against scipy's independent x, y, z, w (scalar-last) rotation, the
+    order the pose head's identity bias [0, 0, 0, 1] assumes (pose_head.py:192-194), and the
+    identity bias must give ΔR = I."""
+    from scipy.spatial.transform import Rotation
+    g = torch.Generator().manual_seed(3)
+    q = torch.randn(64, 4, generator=g, dtype=torch.float64) * torch.rand(64, 1, generator=g,
+                                                                          dtype=torch.float64) * 3
+    got = orc.rotation_from_quaternion_xyzw(q)
+    ref = torch.from_numpy(Rotation.from_quat(q.numpy()).as_matrix())
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), atol=1e-12)
+    eye = orc.rotation_from_quaternion_xyzw(torch.tensor([[0.0, 0.0, 0.0, 1.0]], dtype=torch.float64))
+    np.testing.assert_allclose(eye[0].numpy(), np.eye(3), atol=0)
+    # the update with a quaternion delta equals the ortho6d update with ΔR's first two columns
+    R0 = torch.from_numpy(Rotation.random(64, random_state=1).as_matrix())
+    t0 = torch.tensor([[10.0, -20.0, 900.0]], dtype=torch.float64).repeat(64, 1)
+    dt = torch.randn(64, 3, generator=g, dtype=torch.float64) * 0.1
+    Rq, tq = orc.pose_update(q, dt, R0, t0)
+    o6 = torch.cat([ref[:, :, 0], ref[:, :, 1]], 1)
+    R6, t6 = orc.pose_update(o6, dt, R0, t0)
+    np.testing.assert_allclose(Rq.numpy(), R6.numpy(), atol=1e-12)
+    np.testing.assert_allclose(tq.numpy(), t6.numpy(), atol=0)
