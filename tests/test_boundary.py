@@ -41,8 +41,9 @@ def test_load_state_dict_strict_roundtrip():
 def test_module_surface_matches_reference():
     from scflow_amd.modules import ConvGRU, CorrLookup, CorrelationPyramid, MotionEncoder, XHead
     assert CorrLookup(radius=4).r == 4
+    assert CorrLookup(radius=4, align_corners=False).align_corners is False
     with pytest.raises(NotImplementedError):
-        CorrLookup(radius=4, align_corners=False)
+        CorrLookup(radius=4, mode="nearest")
     assert CorrelationPyramid(num_levels=4).num_levels == 4
     me = MotionEncoder(num_levels=4, radius=4, net_type="Basic", act_cfg=dict(type="ReLU"))
     assert me.out_channels == [126]
