@@ -22,8 +22,8 @@ Extra JSON fields:
   direct-conv count for comparison.  ``traffic`` = memory-side bytes per launch from the
   rocprofv3 FETCH_SIZE / WRITE_SIZE passes in ``profiles/traffic_*.json``.
 * ``rooflines_secondary``: the SepConvGRU z|r conv (F(4,5) Winograd, same FLOP basis), the
-  pyramid lookup (HBM/gather), the fused iteration tail ``pose_step_kernel`` and the
-  correlation pyramid — the same events in a short untimed pass after the timed region.
+  pyramid lookup (HBM/gather), the persistent pose-head + pose-step tail ``ph_tail_kernel``
+  (or, unfused, ``pose_step_kernel``) and the correlation pyramid — the same events in a short untimed pass after the timed region.
 * ``cpu_baseline``: the CPU oracle (oracle/scflow_oracle.py, a parity-pinned PyTorch-CPU
   restatement of the reference decoder) on the same B=16 × 8-iteration workload, rank 0 at N=1.
 
@@ -162,7 +162,7 @@ def conv_roofline(kernel, parts, timers, m_px, traffic=None, alg_bytes=None):
     return out
 
 
-def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True):
+def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail_weight_bytes=0):
     """The HBM/gather-bound kernels and the correlation GEMM, timed with the same events in an
     untimed pass after the timed region (algorithmic bytes per launch from SURVEY.md §8(d)).
     At B=16, 256² the 86 MB pyramid is Infinity-Cache resident, so the lookup's GB/s is an
@@ -180,6 +180,11 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True):
             ("corr_lookup", "corr_lookup", "corr_lookup_lds_kernel<4> (a2)", "hbm", lookup_bytes),
             ("pose_flow", "pose_step", "pose_step_kernel (a8+a10+a11)" if fused_tail
              else "pose_flow_kernel (a8+a10)", "hbm", flow_bytes),
+            # the persistent pose-head tail (GN 1 → convs 2-3 → FCs → heads) + the pose step:
+            # bytes = the pose step's 36 B/pixel + the pose head's weights after conv 1 (read once)
+            ("pose_tail", "ph_tail", "ph_tail_kernel (a7 after conv 1 + a8+a10+a11, one persistent "
+             "launch; latency-bound phases, bytes dominated by the pose step)", "hbm",
+             flow_bytes + tail_weight_bytes),
             ("corr_pyramid", None, "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma", corr_flops)):
         t = timers[name]
         if t.count() == 0:
@@ -337,7 +342,8 @@ def main():
     # sampled position through the iterations), so an event pair costs ≈ 2 queue packets per
     # step, not 2 per launch.
     per_step = {"heads": args.iters, "corr_net1": args.iters, "gru_zr": 2 * args.iters,
-                "corr_lookup": args.iters, "pose_flow": args.iters, "corr_pyramid": 1}
+                "corr_lookup": args.iters, "pose_flow": args.iters, "pose_tail": args.iters,
+                "corr_pyramid": 1}
     live = ("heads", "corr_net1")  # the headline kernel's launches: bracketed in the timed region
     timers = {name: (KernelTimer() if args.graph else EventTimer(stride=n + 1 if n > 1 else 1))
               for name, n in per_step.items()}
@@ -451,8 +457,11 @@ def main():
             "conv_wino5_kernel<·,32,2,GRU_ZR> (SepConvGRU z|r, Winograd F(4,5) on fp32 MFMA)"
             if zr.winograd else "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r, direct)",
             [("gru_zr", zr, hc, zr.cin - hc)], timers, m_px, traffic.get("gru_zr"), alg.get("gru_zr")))
+    ph = dec.pose_pred
+    tail_w = 4 * sum(p.numel() for m in (ph.conv_layers[1:], ph.fc_layers) for p in m.parameters())
+    tail_w += 4 * (ph.rotation_out_channels + 3) * ph.fc_layers[-1][0].out_features  # label[0] rows
     secondary += secondary_rooflines(timers, hb, args.size, traffic,
-                                     getattr(dec, "fuse_tail", True))
+                                     getattr(dec, "fuse_tail", True), tail_w)
 
     if rank == 0:
         cfg_name = ("configs[4]" if (args.batch, args.size, args.iters) == (32, 512, 12)

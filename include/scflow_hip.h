@@ -257,6 +257,60 @@ int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* 
                     const float* Wt, const float* bt, const long long* label, int num_class,
                     float* drot, float* dt, void* stream);
 
+/* scflow_pose_step's arguments as a struct (stream aside) — used by scflow_ph_tail. */
+typedef struct scflow_pose_step_args {
+  const float* drot6; const float* dt; const float* R_src; const float* t_src; const float* K;
+  const float* points; float* R_dst; float* t_dst; float* flow;
+  int n, H, W; float weight; int depth_transform; float invalid_num;
+  const float* lr; const float* delta; const float* mask; float* flow_up; float* mask_up;
+  float* lr_next; int s_next; float* hx_next; int s_hx; int h, w; float up_scale, down_scale;
+} scflow_pose_step_args;
+
+/* scflow_ph_tail: MultiClassPoseHead after its first conv (pose_head.py:201-211) — GroupNorm 1,
+ * conv 2 → GN 2, conv 3 → GN 3, FC1, FC2, the label[0] heads — and optionally the iteration's
+ * tail (scflow_pose_step, scflow_decoder.py:223-244), as ONE persistent launch instead of 8–9.
+ * Workgroups take work items from an atomic ticket in dependency order (every item only waits
+ * for items with smaller tickets, which are already running: no deadlock whatever the residency)
+ * and wait per sample where the data flow allows (conv 2 of sample i starts once GN 1 of sample
+ * i is done).  The arithmetic per item is that of the unfused kernels: same results as
+ * scflow_ph_gn_reduce / scflow_ph_conv_split / scflow_ph_fc_split / scflow_ph_heads_sum /
+ * scflow_pose_step up to the GroupNorm statistics' fp64 summation order.
+ *   Layer l = 0, 1, 2 is conv l+1 → GroupNorm(groups, eps[l]) → ReLU with c output channels
+ *   (c % 32 == 0), output h[l]×w[l] per sample.  Conv 1 runs before (scflow_enc_conv or
+ *   scflow_ph_conv_split with K split into conv1_split raw partial slabs [split][n·h0·w0][c]);
+ *   y[l] receive the summed raw conv outputs, scale/shift[l] [n][c] the GroupNorm affine
+ *   (the consumer applies relu(y·scale + shift) on load).  Conv 2 and 3: kh×kh, stride, pad,
+ *   weights packed by scflow_ph_conv_pack, K split conv_split[j] (partial slabs conv_parts[j]).
+ *   FC1 (weights permuted by scflow_ph_fc_permute, k = c·h[2]·w[2]) and FC2 with K split into
+ *   partial slabs fc*_parts [split][n][fc*_n]; heads as scflow_ph_heads_sum → drot, dt.
+ *   n ≤ 32.  sync: scflow_ph_tail_sync_ints(n) ints of workspace (16-B aligned), zeroed by the
+ *   call (an async memset ahead of the launch); after the launch sync[2] ≠ 0 means a dependency
+ *   wait gave up (bounded at 50 ms by the GPU's real-time clock) and the results are invalid —
+ *   sync[9..13] then hold the first give-up's ticket, counter index, value, target and phase + 1.
+ *   Concurrent launches need separate sync arrays. */
+typedef struct scflow_ph_tail_args {
+  int n, c, groups;
+  float eps[3];
+  int h[3], w[3];
+  const float* conv1_parts; int conv1_split;
+  const float* gamma[3]; const float* beta[3];
+  float* y[3]; float* scale[3]; float* shift[3];
+  const float* conv_w[2]; int kh, stride, pad;
+  int conv_split[2]; float* conv_parts[2];
+  const float* fc1_w; const float* fc1_b; int fc1_n, fc1_split; float* fc1_parts;
+  const float* fc2_w; const float* fc2_b; int fc2_n, fc2_split; float* fc2_parts;
+  const float* rot_w; const float* rot_b; int rch;
+  const float* trans_w; const float* trans_b;
+  const long long* label; int num_class;
+  float* drot; float* dt;
+  const scflow_pose_step_args* pose;      /* NULL: stop after the heads */
+  int* sync;
+  void* stamps;                           /* NULL, or (profiling) 4 u64 real-time-clock stamps per
+                                             work item: start, dependencies met, body done, signalled */
+} scflow_ph_tail_args;
+int scflow_ph_tail_sync_ints(int n);
+int scflow_ph_tail(const scflow_ph_tail_args* args, void* stream);
+
 /* §8(f)-1: RAFTEncoder (Basic) — feature encoder (InstanceNorm) and context encoder (BatchNorm,
  * eval statistics), models/encoder/raft_encoder.py:286-314, BasicBlock models/backbone/resnet.py:
  * 12-92, ResLayer resnet.py:676-771, called from SCFlowRefiner.extract_feat

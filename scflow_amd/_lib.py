@@ -75,6 +75,35 @@ class WgradArgs(ctypes.Structure):
     ]
 
 
+class PoseStepArgs(ctypes.Structure):
+    """Mirror of ``scflow_pose_step_args`` (include/scflow_hip.h)."""
+    _fields_ = [
+        ("drot6", c_vp), ("dt", c_vp), ("R_src", c_vp), ("t_src", c_vp), ("K", c_vp),
+        ("points", c_vp), ("R_dst", c_vp), ("t_dst", c_vp), ("flow", c_vp),
+        ("n", c_int), ("H", c_int), ("W", c_int), ("weight", c_float), ("depth_transform", c_int),
+        ("invalid_num", c_float),
+        ("lr", c_vp), ("delta", c_vp), ("mask", c_vp), ("flow_up", c_vp), ("mask_up", c_vp),
+        ("lr_next", c_vp), ("s_next", c_int), ("hx_next", c_vp), ("s_hx", c_int), ("h", c_int),
+        ("w", c_int), ("up_scale", c_float), ("down_scale", c_float),
+    ]
+
+
+class PhTailArgs(ctypes.Structure):
+    """Mirror of ``scflow_ph_tail_args`` (include/scflow_hip.h)."""
+    _fields_ = [
+        ("n", c_int), ("c", c_int), ("groups", c_int), ("eps", c_float * 3), ("h", c_int * 3),
+        ("w", c_int * 3), ("conv1_parts", c_vp), ("conv1_split", c_int),
+        ("gamma", c_vp * 3), ("beta", c_vp * 3), ("y", c_vp * 3), ("scale", c_vp * 3),
+        ("shift", c_vp * 3), ("conv_w", c_vp * 2), ("kh", c_int), ("stride", c_int), ("pad", c_int),
+        ("conv_split", c_int * 2), ("conv_parts", c_vp * 2),
+        ("fc1_w", c_vp), ("fc1_b", c_vp), ("fc1_n", c_int), ("fc1_split", c_int), ("fc1_parts", c_vp),
+        ("fc2_w", c_vp), ("fc2_b", c_vp), ("fc2_n", c_int), ("fc2_split", c_int), ("fc2_parts", c_vp),
+        ("rot_w", c_vp), ("rot_b", c_vp), ("rch", c_int), ("trans_w", c_vp), ("trans_b", c_vp),
+        ("label", c_vp), ("num_class", c_int), ("drot", c_vp), ("dt", c_vp),
+        ("pose", ctypes.POINTER(PoseStepArgs)), ("sync", c_vp), ("stamps", c_vp),
+    ]
+
+
 class RenderArgs(ctypes.Structure):
     """Mirror of ``scflow_render_args`` (include/scflow_hip.h)."""
     _fields_ = [
@@ -120,6 +149,8 @@ SIGNATURES = {
                                      c_float, c_vp]),
     "scflow_pose_step": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_float, c_int, c_float] +
                          [c_vp] * 6 + [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_vp]),
+    "scflow_ph_tail": (c_int, [ctypes.POINTER(PhTailArgs), c_vp]),
+    "scflow_ph_tail_sync_ints": (c_int, [c_int]),
     "scflow_sync_event_create": (c_int, [ctypes.POINTER(c_vp)]),
     "scflow_sync_event_destroy": (c_int, [c_vp]),
     "scflow_sync_event_record": (c_int, [c_vp, c_vp]),

@@ -24,6 +24,9 @@
 //    gather of the input (FC1 reads conv3's raw output).
 //  * scflow_ph_heads — the label[0] class's 6 rotation and 3 translation rows only.
 #include "common.h"
+#include "pose_dev.h"
+
+#include <stdlib.h>
 
 namespace {
 
@@ -67,12 +70,15 @@ __device__ __forceinline__ floatx4 ph_load_a(const PhConvArgs& a, int img, int i
 constexpr int PH_WAVES = SCFLOW_PH_WAVES;  // waves per workgroup; they split K
 constexpr int PH_BATCH = SCFLOW_PH_BATCH;  // K chunks whose loads a wave issues together
 
-__global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
-  __shared__ float red[PH_WAVES / 2][32][33];
+// one 32×32 output tile (bx, by) of K slice bz; NW waves (threads ≥ NW·64 must not call);
+// red: (NW/2)·32·33 floats of LDS
+template <int NW>
+__device__ __forceinline__ void ph_conv_body(const PhConvArgs& a, int bx, int by, int bz,
+                                             float* red) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 31, hh = lane >> 5;
   const int M = a.n * a.oh * a.ow;
-  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  const int m0 = bx * 32, n0 = by * 32;
   // this lane's A row (output pixel) and B column (output channel)
   const int m = m0 + li;
   const bool mvalid = m < M;
@@ -85,18 +91,18 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
   const int cchunks = a.cinp / PH_K;
   const int nall = taps * cchunks;
   // this workgroup's K range (grid.z splits the chunks; partial slab z)
-  const int klo = (int)((long long)nall * blockIdx.z / a.ksplit);
-  const int nchunks = (int)((long long)nall * (blockIdx.z + 1) / a.ksplit);
+  const int klo = (int)((long long)nall * bz / a.ksplit);
+  const int nchunks = (int)((long long)nall * (bz + 1) / a.ksplit);
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (int base = klo + wave; base < nchunks; base += PH_WAVES * PH_BATCH) {
+  for (int base = klo + wave; base < nchunks; base += NW * PH_BATCH) {
     floatx4 A0[PH_BATCH], A1[PH_BATCH], B0[PH_BATCH], B1[PH_BATCH];
 #pragma unroll
     for (int c = 0; c < PH_BATCH; ++c) {  // issue every load of the batch first
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
       A0[c] = A1[c] = B0[c] = B1[c] = z;
-      const int kc = base + c * PH_WAVES;
+      const int kc = base + c * NW;
       if (kc < nchunks) {
         const int tap = kc / cchunks, c0 = (kc % cchunks) * PH_K;
         const int ty = tap / a.kw, tx = tap % a.kw;
@@ -121,27 +127,32 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
     }
   }
   // deterministic tree reduction of the waves' partial tiles
-  for (int half = PH_WAVES / 2; half >= 1; half >>= 1) {
+  for (int half = NW / 2; half >= 1; half >>= 1) {
     if (wave >= half && wave < 2 * half) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[wave - half][(r & 3) + 8 * (r >> 2) + 4 * hh][li] = acc[r];
+      for (int r = 0; r < 16; ++r) red[((wave - half) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * 33 + li] = acc[r];
     }
     __syncthreads();
     if (wave < half) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] += red[wave][(r & 3) + 8 * (r >> 2) + 4 * hh][li];
+      for (int r = 0; r < 16; ++r) acc[r] += red[(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * 33 + li];
     }
     __syncthreads();
   }
   if (wave == 0 && nvalid) {
     const float b = a.bias ? a.bias[col] : 0.f;
-    float* out = a.out + (size_t)blockIdx.z * M * a.cout;
+    float* out = a.out + (size_t)bz * M * a.cout;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
       if (mm < M) out[(size_t)mm * a.cout + col] = acc[r] + b;
     }
   }
+}
+
+__global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
+  __shared__ float red[PH_WAVES / 2 * 32 * 33];
+  ph_conv_body<PH_WAVES>(a, blockIdx.x, blockIdx.y, blockIdx.z, red);
 }
 
 // GroupNorm statistics of x [n][hw][c] → per-channel scale/shift for y = relu(x·scale + shift),
@@ -261,13 +272,13 @@ struct FcArgs {
   const float* xbias;
 };
 
-template <int FC_RT>  // row tiles of 16 per pass
-__global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
+// one 16-neuron tile bx of K slice by; NW waves; red: (NW/2)·FC_RT·64·5 floats of LDS
+template <int NW, int FC_RT>  // row tiles of 16 per pass
+__device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, float* red) {
   constexpr int FB = FC_RT == 1 ? PH_BATCH : 2;  // K groups whose loads are issued together
-  __shared__ float red[PH_WAVES / 2][FC_RT][64][5];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, kq = lane >> 4;
-  const int i0 = blockIdx.x * 16;
+  const int i0 = bx * 16;
   // weight row of this lane's neuron
   const int ni = i0 + li;
   const float* wrow = nullptr;
@@ -280,18 +291,18 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
     wrow = f.W + (size_t)ni * f.k;
   }
   const int gall = f.k / 16;
-  const int glo = f.ksplit > 1 ? (int)((long long)gall * blockIdx.y / f.ksplit) : 0;
-  const int groups = f.ksplit > 1 ? (int)((long long)gall * (blockIdx.y + 1) / f.ksplit) : gall;
-  float* yout = f.y + (f.ksplit > 1 ? (size_t)blockIdx.y * f.m * f.n : 0);
+  const int glo = f.ksplit > 1 ? (int)((long long)gall * by / f.ksplit) : 0;
+  const int groups = f.ksplit > 1 ? (int)((long long)gall * (by + 1) / f.ksplit) : gall;
+  float* yout = f.y + (f.ksplit > 1 ? (size_t)by * f.m * f.n : 0);
   for (int r0 = 0; r0 < f.m; r0 += 16 * FC_RT) {
     floatx4 acc[FC_RT];
 #pragma unroll
     for (int t = 0; t < FC_RT; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-    for (int base = glo + wave; base < groups; base += PH_WAVES * FB) {
+    for (int base = glo + wave; base < groups; base += NW * FB) {
       floatx4 wv[FB], xv[FB][FC_RT];
 #pragma unroll
       for (int c = 0; c < FB; ++c) {
-        const int g = base + c * PH_WAVES;
+        const int g = base + c * NW;
         const int kk = g * 16 + 4 * kq;
         const floatx4 z = {0.f, 0.f, 0.f, 0.f};
         wv[c] = (g < groups && wrow) ? *(const floatx4*)(wrow + kk) : z;
@@ -326,19 +337,19 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
           for (int e = 0; e < 4; ++e)
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[c][e], xv[c][t][e], acc[t], 0, 0, 0);
     }
-    for (int half = PH_WAVES / 2; half >= 1; half >>= 1) {
+    for (int half = NW / 2; half >= 1; half >>= 1) {
       if (wave >= half && wave < 2 * half) {
 #pragma unroll
         for (int t = 0; t < FC_RT; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) red[wave - half][t][lane][r] = acc[t][r];
+          for (int r = 0; r < 4; ++r) red[(((wave - half) * FC_RT + t) * 64 + lane) * 5 + r] = acc[t][r];
       }
       __syncthreads();
       if (wave < half) {
 #pragma unroll
         for (int t = 0; t < FC_RT; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[t][r] += red[wave][t][lane][r];
+          for (int r = 0; r < 4; ++r) acc[t][r] += red[((wave * FC_RT + t) * 64 + lane) * 5 + r];
       }
       __syncthreads();
     }
@@ -372,6 +383,12 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
   }
 }
 
+template <int FC_RT>
+__global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
+  __shared__ float red[PH_WAVES / 2 * FC_RT * 64 * 5];
+  ph_fc_body<PH_WAVES, FC_RT>(f, blockIdx.x, blockIdx.y, red);
+}
+
 // W [n][c·hw] with columns in NCHW-flatten order (c·hw + p) → Wp [n][hw·c] channels-last order
 __global__ void ph_fc_permute_kernel(const float* __restrict__ W, float* __restrict__ Wp, int n,
                                      int c, int hw) {
@@ -395,6 +412,304 @@ __global__ void ph_pack_kernel(const float* __restrict__ w, float* __restrict__ 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// scflow_ph_tail: GN 1 → conv 2 → GN 2 → conv 3 → GN 3 → FC1 → FC2 → heads (→ pose step) as one
+// persistent launch.  Work items are numbered phase by phase (off[]); a workgroup takes the next
+// ticket from sync[0], waits (one lane: relaxed sc1 polls + s_sleep, then ONE agent acquire) until
+// the items it reads from have signalled, runs the item with the unfused kernels' bodies, and
+// signals (every storing wave drains its stores, the workgroup joins, one lane releases at agent
+// scope — the L2s of the 8 XCDs are not coherent with each other — and adds to the counter).  An
+// item only waits for smaller tickets, all held by running workgroups, so the launch drains
+// whatever the residency; every wait is bounded by the real-time clock (PHT_WAIT_TICKS) and a
+// give-up sets the error word and lets every later wait fall through, so a protocol fault ends the
+// launch instead of hanging it.  The host zeroes the sync words before every launch.
+//   sync (ints): [0] ticket  [2] error  [3] GN-3 items done  [4] FC1 done  [5] FC2 done
+//     [6] heads done  [8..12] first give-up: 1 + phase, ticket, counter index, value seen, target
+//     [16 + i] GN 1 of sample i, [16 + n + i] conv 2 items over sample i, [16 + 2n + i] GN 2,
+//     [16 + 3n + i] conv 3;  [16 + 4n + b] the last ticket workgroup b started (diagnostics)
+
+struct PhGn {
+  const float* x; int nsplit; long long sstride; float* y;
+  int hw, c, groups; const float* gamma; const float* beta; float eps; float* scale; float* shift;
+};
+
+struct PhTail {
+  int n;
+  PhGn gn[3];
+  PhConvArgs conv[2];
+  FcArgs fc1, fc2, heads;
+  int fc1_split, fc2_split;
+  PoseStepArgs ps;
+  int pose;
+  int* sync;
+  int off[10];  // first ticket of phase p; off[9] = total
+  int dbg;      // debugging (SCFLOW_PHT_DBG): bit 0 skips the item bodies, bit 1 the publishes
+  unsigned long long* stamps;  // debugging: per ticket 4 real-time stamps (start, waited, body, out)
+};
+
+enum { PHT_GN0, PHT_CONV2, PHT_GN1, PHT_CONV3, PHT_GN2, PHT_FC1, PHT_FC2, PHT_HEADS, PHT_POSE };
+constexpr int PHT_CTR = 16;                          // first per-sample counter
+constexpr unsigned long long PHT_WAIT_TICKS = 5000000;  // 50 ms of the 100 MHz real-time clock
+
+__device__ __forceinline__ int pht_poll(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// thread 0: until S[idx] ≥ target, then one agent acquire.  false: gave up (error set)
+__device__ bool pht_wait(int* S, int idx, int target, int ticket, int ph) {
+  int v = pht_poll(S + idx);
+  if (v < target) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      __builtin_amdgcn_s_sleep(2);
+      v = pht_poll(S + idx);
+      if (v >= target) break;
+      if (pht_poll(S + 2) || __builtin_amdgcn_s_memrealtime() - t0 > PHT_WAIT_TICKS) {
+        if (__hip_atomic_fetch_add(S + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+          __hip_atomic_store(S + 9, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(S + 10, idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(S + 11, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(S + 12, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(S + 13, 1 + ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __hip_atomic_fetch_or(S + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
+// after a thread-0 wait: the acquire's invalidate completes before any wave loads
+__device__ __forceinline__ void pht_join_after_wait() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// GroupNorm of one (sample img, 32-channel block cb) with NW·64 threads: sums the K-split
+// partial slabs (writes y when nsplit > 1, same order as ph_gn_reduce_kernel), fp64 moments —
+// per wave by shuffles, then over the waves in a fixed order — then scale/shift per channel.
+// red: NW·64 + 128 doubles of LDS.
+template <int NW>
+__device__ void ph_gn_body(const PhGn& g, int img, int cb, double* red) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = tid & 7, slot = tid >> 3;
+  constexpr int SL = NW * 8;
+  double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+  for (int p = slot; p < g.hw; p += SL) {
+    const size_t off = ((size_t)img * g.hw + p) * g.c + cb + 4 * q;
+    floatx4 u[4];
+    u[0] = *(const floatx4*)(g.x + off);
+#pragma unroll
+    for (int z = 1; z < 4; ++z)
+      if (z < g.nsplit) u[z] = *(const floatx4*)(g.x + z * g.sstride + off);
+    floatx4 v = u[0];
+#pragma unroll
+    for (int z = 1; z < 4; ++z)
+      if (z < g.nsplit) v += u[z];
+    for (int z = 4; z < g.nsplit; z += 4) {  // the next ≤ 4 slabs' loads issued together
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (z + k < g.nsplit) u[k] = *(const floatx4*)(g.x + (z + k) * g.sstride + off);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (z + k < g.nsplit) v += u[k];
+    }
+    if (g.nsplit > 1) *(floatx4*)(g.y + off) = v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] += (double)v[e];
+      b[e] += (double)v[e] * (double)v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+#pragma unroll
+    for (int m = 8; m < 64; m <<= 1) {
+      a[e] += __shfl_xor(a[e], m);
+      b[e] += __shfl_xor(b[e], m);
+    }
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[(wave * 2 + 0) * 32 + 4 * lane + e] = a[e];
+      red[(wave * 2 + 1) * 32 + 4 * lane + e] = b[e];
+    }
+  }
+  __syncthreads();
+  double* ch = red + NW * 64;  // [2][32] per-channel sums
+  if (tid < 64) {
+    const int k = tid >> 5, cc = tid & 31;
+    double s = 0;
+    for (int w = 0; w < NW; ++w) s += red[(w * 2 + k) * 32 + cc];
+    ch[k * 32 + cc] = s;
+  }
+  __syncthreads();
+  const int cpg = g.c / g.groups, ng = 32 / cpg;
+  double* gs = ch + 64;  // [2][≤32] group mean, rstd
+  if (tid < ng) {
+    double A = 0, B = 0;
+    for (int k = 0; k < cpg; ++k) {
+      A += ch[tid * cpg + k];
+      B += ch[32 + tid * cpg + k];
+    }
+    const double cnt = (double)g.hw * cpg;
+    const double mean = A / cnt;
+    double var = B / cnt - mean * mean;
+    if (var < 0) var = 0;
+    gs[tid] = mean;
+    gs[32 + tid] = 1.0 / sqrt(var + (double)g.eps);
+  }
+  __syncthreads();
+  if (tid < 32) {
+    const int c = cb + tid, gi = tid / cpg;
+    const float sc = g.gamma[c] * (float)gs[32 + gi];
+    g.scale[(size_t)img * g.c + c] = sc;
+    g.shift[(size_t)img * g.c + c] = g.beta[c] - (float)gs[gi] * sc;
+  }
+}
+
+constexpr int PHT_WAVES = 16;
+constexpr int PHT_SMEM = PHT_WAVES / 2 * 32 * 33;  // floats: the largest body's LDS (conv)
+static_assert(PHT_SMEM * 4 >= (PHT_WAVES * 64 + 192) * 8, "GN body LDS");
+static_assert(PHT_SMEM >= PHT_WAVES / 2 * 2 * 64 * 5, "FC body LDS");
+
+// the counters item (ph, i) waits for: [wait0, wait0 + wait_count), each up to `target`; and
+// the ones it adds 1 to when done: [sig0, sig0 + sig_count)
+struct PhtDeps {
+  int wait0, wait_count, target;
+  int sig0, sig_count;
+};
+
+// The kernel's arguments are read from the kernarg segment through a pointer made opaque once per
+// item (asm): the compiler cannot hoist the ~1.2 KB of argument fields out of the ticket loop into
+// registers (that spilled hundreds of SGPRs), it reloads what an item needs (scalar loads) into
+// item-local copies.
+typedef const PhTail __attribute__((address_space(4)))* PhTailK;
+
+// an item-local copy of an argument sub-struct (word by word: scalar loads from the kernarg
+// segment; a struct copy cannot bind an address-space-4 reference)
+template <class T>
+__device__ __forceinline__ T pht_kcopy(const T __attribute__((address_space(4)))* p) {
+  static_assert(sizeof(T) % 4 == 0, "word copy");
+  T v;
+  const int __attribute__((address_space(4)))* src = (const int __attribute__((address_space(4)))*)p;
+  int* dst = (int*)&v;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); ++k) dst[k] = src[k];
+  return v;
+}
+
+__device__ __forceinline__ PhtDeps pht_deps_k(PhTailK K, int ph, int i) {
+  const int n = K->n;
+  PhtDeps d{0, 0, 0, 0, 0};
+  if (ph == PHT_GN0 || ph == PHT_GN1 || ph == PHT_GN2) {
+    const int L = ph == PHT_GN0 ? 0 : ph == PHT_GN1 ? 1 : 2;
+    const int img = i / (K->gn[L].c / 32);
+    if (L > 0) {  // every conv item over this sample
+      const int oh = K->conv[L - 1].oh, ow = K->conv[L - 1].ow;
+      const int nt = (K->conv[L - 1].cout + 31) / 32, ks = K->conv[L - 1].ksplit;
+      const int P = oh * ow;
+      const int tiles = ((img + 1) * P - 1) / 32 - img * P / 32 + 1;
+      d.wait0 = PHT_CTR + (L == 1 ? n : 3 * n) + img;
+      d.wait_count = 1;
+      d.target = tiles * nt * ks;
+    }
+    d.sig0 = L == 0 ? PHT_CTR + img : L == 1 ? PHT_CTR + 2 * n + img : 3;
+    d.sig_count = 1;
+  } else if (ph == PHT_CONV2 || ph == PHT_CONV3) {
+    const int j = ph == PHT_CONV2 ? 0 : 1;
+    const int nt = (K->conv[j].cout + 31) / 32, ks = K->conv[j].ksplit;
+    const int bx = i / (ks * nt);
+    const int P = K->conv[j].oh * K->conv[j].ow, M = n * P;
+    const int lo = bx * 32 / P, hi = min(bx * 32 + 31, M - 1) / P;
+    d.wait0 = PHT_CTR + (j == 0 ? 0 : 2 * n) + lo;
+    d.wait_count = hi - lo + 1;
+    d.target = K->gn[j].c / 32;
+    d.sig0 = PHT_CTR + (j == 0 ? n : 3 * n) + lo;
+    d.sig_count = hi - lo + 1;
+  } else if (ph == PHT_FC1) {
+    d.wait0 = 3; d.wait_count = 1; d.target = n * (K->gn[2].c / 32);
+    d.sig0 = 4; d.sig_count = 1;
+  } else if (ph == PHT_FC2) {
+    d.wait0 = 4; d.wait_count = 1; d.target = K->off[PHT_FC1 + 1] - K->off[PHT_FC1];
+    d.sig0 = 5; d.sig_count = 1;
+  } else if (ph == PHT_HEADS) {
+    d.wait0 = 5; d.wait_count = 1; d.target = K->off[PHT_FC2 + 1] - K->off[PHT_FC2];
+    d.sig0 = 6; d.sig_count = 1;
+  } else {
+    d.wait0 = 6; d.wait_count = 1; d.target = 1;
+  }
+  return d;
+}
+
+template <int RT>
+__global__ __launch_bounds__(PHT_WAVES * 64) void ph_tail_kernel(PhTail A) {
+  __shared__ __attribute__((aligned(16))) float smem[PHT_SMEM];
+  __shared__ int s_item;
+  const int tid = threadIdx.x;
+  PhTailK K = (PhTailK)__builtin_amdgcn_kernarg_segment_ptr();
+  for (;;) {
+    asm volatile("" : "+s"(K));
+    int* const S = K->sync;
+    if (tid == 0) s_item = __hip_atomic_fetch_add(S, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane(s_item);
+    __syncthreads();
+    if (t >= K->off[9]) break;
+    int ph = 0;
+    while (t >= K->off[ph + 1]) ++ph;
+    const int i = t - K->off[ph];
+    const PhtDeps d = pht_deps_k(K, ph, i);
+    unsigned long long* const st = K->stamps;
+    if (st && tid == 0) st[4 * t] = __builtin_amdgcn_s_memrealtime();
+    if (d.wait_count > 0) {
+      if (tid == 0)
+        for (int k = 0; k < d.wait_count; ++k) pht_wait(S, d.wait0 + k, d.target, t, ph);
+      pht_join_after_wait();
+    }
+    const int dbg = K->dbg;
+    if (st && tid == 0) st[4 * t + 1] = __builtin_amdgcn_s_memrealtime();
+    if (!(dbg & 1)) {
+      if (ph == PHT_GN0 || ph == PHT_GN1 || ph == PHT_GN2) {
+        const int L = ph == PHT_GN0 ? 0 : ph == PHT_GN1 ? 1 : 2;
+        const PhGn g = pht_kcopy(&K->gn[L]);
+        const int ncb = g.c / 32;
+        ph_gn_body<PHT_WAVES>(g, i / ncb, (i % ncb) * 32, (double*)smem);
+      } else if (ph == PHT_CONV2 || ph == PHT_CONV3) {
+        const PhConvArgs cv = pht_kcopy(&K->conv[ph == PHT_CONV2 ? 0 : 1]);
+        const int nt = (cv.cout + 31) / 32;
+        ph_conv_body<PHT_WAVES>(cv, i / (cv.ksplit * nt), (i / cv.ksplit) % nt, i % cv.ksplit, smem);
+      } else if (ph == PHT_FC1 || ph == PHT_FC2 || ph == PHT_HEADS) {
+        const FcArgs f = pht_kcopy(ph == PHT_FC1 ? &K->fc1 : ph == PHT_FC2 ? &K->fc2 : &K->heads);
+        const int split = ph == PHT_FC1 ? K->fc1_split : ph == PHT_FC2 ? K->fc2_split : 1;
+        ph_fc_body<PHT_WAVES, RT>(f, i / split, i % split, smem);
+      } else {
+        const PoseStepArgs ps = pht_kcopy(&K->ps);
+        const int nb = ps.bf + ps.bl;
+        pose_step_body(ps, smem, i % nb, i / nb, tid, PHT_WAVES * 64, true);
+      }
+    }
+    if (st) {
+      __syncthreads();
+      if (tid == 0) st[4 * t + 2] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (d.sig_count > 0 && !(dbg & 2)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores drained
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int k = 0; k < d.sig_count; ++k)
+          __hip_atomic_fetch_add(S + d.sig0 + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (st && tid == 0) st[4 * t + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
 }  // namespace
 
 SCFLOW_API long long scflow_ph_conv_packed_size(int cout, int cin, int kh, int kw) {
@@ -568,5 +883,137 @@ SCFLOW_API int scflow_ph_heads_sum(const float* x, int xsplit, const float* xbia
     ph_fc_kernel<1><<<1, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
   else
     ph_fc_kernel<2><<<1, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_tail_sync_ints(int n) {
+  if (n <= 0 || n > 32) return SCFLOW_EINVAL;
+  return (PHT_CTR + 4 * n + 512 + 3) / 4 * 4;  // counters + per-workgroup diagnostics, 16-B multiple
+}
+
+SCFLOW_API int scflow_ph_tail(const scflow_ph_tail_args* p, void* stream) {
+  if (!p) return SCFLOW_EINVAL;
+  const int n = p->n, c = p->c;
+  if (n <= 0 || n > 32 || c <= 0 || c % 32 || p->groups <= 0 || c % p->groups ||
+      32 % (c / p->groups) || !p->conv1_parts || p->conv1_split <= 0 || !p->sync || !p->label ||
+      !p->drot || !p->dt || p->kh <= 0 || p->stride <= 0 || p->pad < 0 || p->rch <= 0 ||
+      p->rch + 3 > 16 || p->num_class <= 0)
+    return SCFLOW_EINVAL;
+  for (int l = 0; l < 3; ++l) {
+    if (p->h[l] <= 0 || p->w[l] <= 0 || !p->gamma[l] || !p->beta[l] || !p->scale[l] ||
+        !p->shift[l] || !p->y[l])
+      return SCFLOW_EINVAL;
+    if (l > 0 && (p->h[l] != (p->h[l - 1] + 2 * p->pad - p->kh) / p->stride + 1 ||
+                  p->w[l] != (p->w[l - 1] + 2 * p->pad - p->kh) / p->stride + 1))
+      return SCFLOW_EINVAL;
+  }
+  const int cinp = (c + PH_K - 1) / PH_K * PH_K;
+  const int nchunks = p->kh * p->kh * (cinp / PH_K);
+  for (int j = 0; j < 2; ++j)
+    if (!p->conv_w[j] || !p->conv_parts[j] || p->conv_split[j] <= 0 || p->conv_split[j] > nchunks)
+      return SCFLOW_EINVAL;
+  const int k1 = c * p->h[2] * p->w[2];
+  if (!p->fc1_w || !p->fc1_b || !p->fc1_parts || !p->fc2_w || !p->fc2_b || !p->fc2_parts ||
+      !p->rot_w || !p->rot_b || !p->trans_w || !p->trans_b || p->fc1_n <= 0 || p->fc2_n <= 0 ||
+      (k1 & 15) || (p->fc1_n & 15) || (p->fc2_n & 15) || p->fc1_split <= 0 ||
+      p->fc1_split > k1 / 16 || p->fc2_split <= 0 || p->fc2_split > p->fc1_n / 16)
+    return SCFLOW_EINVAL;
+  if (!aligned16(p->conv1_parts) || !aligned16(p->fc1_w) || !aligned16(p->fc2_w) ||
+      !aligned16(p->rot_w) || !aligned16(p->trans_w) || !aligned16(p->fc1_parts) ||
+      !aligned16(p->fc2_parts) || !aligned16(p->fc1_b) || !aligned16(p->fc2_b))
+    return SCFLOW_EALIGN;
+  for (int l = 0; l < 3; ++l)
+    if (!aligned16(p->y[l]) || !aligned16(p->scale[l]) || !aligned16(p->shift[l])) return SCFLOW_EALIGN;
+  for (int j = 0; j < 2; ++j)
+    if (!aligned16(p->conv_w[j]) || !aligned16(p->conv_parts[j])) return SCFLOW_EALIGN;
+
+  PhTail A{};
+  A.n = n;
+  A.sync = p->sync;
+  const float* gx[3] = {p->conv1_parts, p->conv_parts[0], p->conv_parts[1]};
+  const int gs[3] = {p->conv1_split, p->conv_split[0], p->conv_split[1]};
+  const float* gout[3];  // what the next consumer reads: the summed output (or the only slab)
+  for (int l = 0; l < 3; ++l) {
+    PhGn& g = A.gn[l];
+    g.x = gx[l]; g.nsplit = gs[l]; g.hw = p->h[l] * p->w[l];
+    g.sstride = (long long)n * g.hw * c; g.y = p->y[l];
+    g.c = c; g.groups = p->groups; g.gamma = p->gamma[l]; g.beta = p->beta[l]; g.eps = p->eps[l];
+    g.scale = p->scale[l]; g.shift = p->shift[l];
+    gout[l] = gs[l] > 1 ? p->y[l] : gx[l];
+  }
+  for (int j = 0; j < 2; ++j) {
+    PhConvArgs& a = A.conv[j];
+    a.src0 = gout[j]; a.c0 = c; a.s0 = c;
+    a.src1 = nullptr; a.c1 = 0; a.s1 = 0;
+    a.scale = p->scale[j]; a.shift = p->shift[j];
+    a.weight = p->conv_w[j]; a.bias = nullptr; a.out = p->conv_parts[j];
+    a.n = n; a.h = p->h[j]; a.w = p->w[j]; a.oh = p->h[j + 1]; a.ow = p->w[j + 1];
+    a.cout = c; a.kh = p->kh; a.kw = p->kh; a.stride = p->stride; a.pad = p->pad;
+    a.cinp = cinp; a.ksplit = p->conv_split[j];
+  }
+  FcArgs& f1 = A.fc1;
+  f1.x = gout[2]; f1.ldx = k1; f1.m = n; f1.k = k1; f1.W = p->fc1_w; f1.y = p->fc1_parts;
+  f1.n = p->fc1_n; f1.gn_c = c; f1.scale = p->scale[2]; f1.shift = p->shift[2];
+  f1.ksplit = p->fc1_split;
+  FcArgs& f2 = A.fc2;
+  f2.x = p->fc1_parts; f2.ldx = p->fc1_n; f2.m = n; f2.k = p->fc1_n; f2.W = p->fc2_w;
+  f2.y = p->fc2_parts; f2.n = p->fc2_n; f2.ksplit = p->fc2_split; f2.xsplit = p->fc1_split;
+  f2.xstride = (long long)n * p->fc1_n; f2.xbias = p->fc1_b;
+  FcArgs& hd = A.heads;
+  hd.x = p->fc2_parts; hd.ldx = p->fc2_n; hd.m = n; hd.k = p->fc2_n; hd.W = p->rot_w;
+  hd.bias = p->rot_b; hd.y = p->drot; hd.n = p->rch + 3; hd.Wt = p->trans_w; hd.bt = p->trans_b;
+  hd.label = p->label; hd.num_class = p->num_class; hd.rch = p->rch; hd.dt = p->dt;
+  hd.xsplit = p->fc2_split; hd.xstride = (long long)n * p->fc2_n; hd.xbias = p->fc2_b;
+  hd.ksplit = 1;
+  A.fc1_split = p->fc1_split;
+  A.fc2_split = p->fc2_split;
+  int pose_items = 0;
+  if (p->pose) {
+    const scflow_pose_step_args* s = p->pose;
+    if (s->n != n || s->drot6 != p->drot || s->dt != p->dt) return SCFLOW_EINVAL;
+    const int st = pose_step_args(&A.ps, s->drot6, s->dt, s->R_src, s->t_src, s->K, s->points,
+                                  s->R_dst, s->t_dst, s->flow, s->n, s->H, s->W, s->weight,
+                                  s->depth_transform, s->invalid_num, s->lr, s->delta, s->mask,
+                                  s->flow_up, s->mask_up, s->lr_next, s->s_next, s->hx_next,
+                                  s->s_hx, s->h, s->w, s->up_scale, s->down_scale, PHT_WAVES * 64);
+    if (st != SCFLOW_OK) return st;
+    A.pose = 1;
+    pose_items = (A.ps.bf + A.ps.bl) * n;
+  }
+  const int ncb = c / 32;
+  const int items[9] = {
+      n * ncb,
+      ceil_div((long long)n * p->h[1] * p->w[1], 32) * ncb * p->conv_split[0],
+      n * ncb,
+      ceil_div((long long)n * p->h[2] * p->w[2], 32) * ncb * p->conv_split[1],
+      n * ncb,
+      ceil_div(p->fc1_n, 16) * p->fc1_split,
+      ceil_div(p->fc2_n, 16) * p->fc2_split,
+      1,
+      pose_items};
+  A.off[0] = 0;
+  for (int k = 0; k < 9; ++k) A.off[k + 1] = A.off[k] + items[k];
+  if (const char* e = getenv("SCFLOW_PHT_DBG")) A.dbg = atoi(e);
+  A.stamps = (unsigned long long*)p->stamps;
+  if (const char* e = getenv("SCFLOW_PHT_PHASES")) {  // debugging: run only the first k phases
+    const int k = atoi(e);
+    if (k >= 0 && k < 9) A.off[9] = A.off[k];
+  }
+  static int resident[2] = {0, 0};  // ≤ 512 (the diagnostics words)
+  const int ri = n <= 16 ? 0 : 1;
+  if (!resident[ri]) {
+    int per_cu = 0;
+    hipError_t e = ri == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ph_tail_kernel<1>, PHT_WAVES * 64, 0)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ph_tail_kernel<2>, PHT_WAVES * 64, 0);
+    if (e != hipSuccess || per_cu <= 0) per_cu = 1;
+    resident[ri] = per_cu * device_cus() < 512 ? per_cu * device_cus() : 512;
+  }
+  const int grid = A.off[9] < 1 ? 1 : A.off[9] < resident[ri] ? A.off[9] : resident[ri];
+  hipError_t me = hipMemsetAsync(p->sync, 0, scflow_ph_tail_sync_ints(n) * sizeof(int), (hipStream_t)stream);
+  if (me != hipSuccess) return (int)me;
+  if (ri == 0)
+    ph_tail_kernel<1><<<grid, PHT_WAVES * 64, 0, (hipStream_t)stream>>>(A);
+  else
+    ph_tail_kernel<2><<<grid, PHT_WAVES * 64, 0, (hipStream_t)stream>>>(A);
   return scflow_launch_status();
 }

@@ -101,6 +101,13 @@ class SCFlowDecoder(nn.Module):
         # CUs while the other half's convolutions hold every CU's LDS, so they serialise anyway
         self.pingpong = False
         self.pingpong_min = 4
+        # with fuse_tail: the pose head after its first conv (GroupNorms, convs 2-3, FCs, heads)
+        # and the pose step as ONE persistent launch (scflow_ph_tail) instead of 9.  Off: measured
+        # slower (tools/dbg/ph_tail_check.py: 151 vs 127 µs per pose head at B=16) — its phases
+        # are a dependency chain of latency-bound items, each paying cross-XCD hand-off latency
+        # (agent release + acquire + L2 misses on the producer's lines) that a kernel boundary
+        # (≈2 µs) does not
+        self.fuse_posehead = False
         self._hooks_on = True
         self.hook_batch = 0
 
@@ -464,6 +471,13 @@ class SCFlowDecoder(nn.Module):
         def seg_pose_trunk():
             pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep))
 
+        fuse_ph = fuse_tail and self.fuse_posehead and \
+            self.pose_pred.tail_supported(hid, Chan.whole(FM), N, h, w)
+        ph_ctx = []
+
+        def seg_pose_conv1():
+            ph_ctx.append(self.pose_pred.tail_conv1(hid, Chan.whole(FM), N, h, w, ws=keep))
+
         for it in range(iters):
             par = f"{it % 2}" if fuse_tail else ""
             F2 = F2s[it % 2]
@@ -514,7 +528,10 @@ class SCFlowDecoder(nn.Module):
             if mask_lr is not None:
                 mask_lr = MASK
             # a7 pose head on cat[h, Δflow feat, mask feat] (two channel sources, no concat)
-            segment("pose_trunk", seg_pose_trunk)
+            if fuse_ph:
+                segment("pose_conv1", seg_pose_conv1)
+            else:
+                segment("pose_trunk", seg_pose_trunk)
             drot, dtr = o_drot[it], o_dt[it]
             if fuse_tail:
                 # a8 + a10 + a11 ↑ (+ the next iteration's a11 ↓): one launch.  The heads and
@@ -527,24 +544,33 @@ class SCFlowDecoder(nn.Module):
                     for j in range(iters):
                         last = j == iters - 1
                         hc, pc = [], []
-                        with ops.binding(hc, run=False):
-                            self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
-                        with ops.binding(pc, run=False):
-                            ops.pose_step(o_drot[j], o_dt[j], Rp, tp, K, points, o_R[j], o_t[j],
-                                          o_flow_pose[j], invalid, F2s[j % 2], D2, MASK,
-                                          o_flow_pred[j], o_mask[j], h, w, float(scale),
-                                          lr_next=None if last else Chan.whole(F2s[(j + 1) % 2]),
-                                          hx_next=None if last else hx_flow,
-                                          depth_transform=self.depth_transform)
+                        step = (o_drot[j], o_dt[j], Rp, tp, K, points, o_R[j], o_t[j],
+                                o_flow_pose[j], invalid, F2s[j % 2], D2, MASK, o_flow_pred[j],
+                                o_mask[j], h, w, float(scale))
+                        nxt = dict(lr_next=None if last else Chan.whole(F2s[(j + 1) % 2]),
+                                   hx_next=None if last else hx_flow,
+                                   depth_transform=self.depth_transform)
+                        if fuse_ph:  # GN 1 → … → heads → pose step: one launch
+                            ps = ops.pose_step_struct(*step, **nxt)
+                            args = self.pose_pred.tail_args(ph_ctx[0], label, o_drot[j], o_dt[j],
+                                                            pose=ps)
+                            with ops.binding(pc, run=False):
+                                ops.ph_tail(args, o_drot[j])
+                        else:
+                            with ops.binding(hc, run=False):
+                                self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
+                            with ops.binding(pc, run=False):
+                                ops.pose_step(*step, **nxt)
                         tail_calls.append((hc, pc))
                         Rp, tp = o_R[j], o_t[j]
                 hc, pc = tail_calls[it]
                 for c in hc:
                     c()
-                self._hook("pose_flow", True)
+                hook = "pose_tail" if fuse_ph else "pose_flow"
+                self._hook(hook, True)
                 for c in pc:
                     c()
-                self._hook("pose_flow", False)
+                self._hook(hook, False)
             else:
                 self.pose_pred.heads_hip(pose_x[0], label, drot, dtr)
                 # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑

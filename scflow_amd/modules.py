@@ -22,6 +22,7 @@ and calls the kernels directly (``ConvRunner``), so no NCHW round trips happen i
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Optional, Sequence, Tuple, Union
 
 import torch
@@ -745,6 +746,139 @@ class MultiClassPoseHead(nn.Module):
                      self.rotation_pred.bias.detach(), self.rotation_out_channels,
                      self.translation_pred.weight.detach(), self.translation_pred.bias.detach(),
                      label.long(), self.num_class, drot, dt)
+
+    # ---------------------------------------------------- fused tail (scflow_ph_tail)
+    #: work items per convolution phase of the fused tail (its K split is chosen to reach this)
+    tail_conv_items = 256
+    tail_fc_split = (4, 4)
+
+    def tail_supported(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int) -> bool:
+        """Whether ``tail_conv1`` + ``tail_args`` (one persistent launch after the first conv)
+        cover this head: three equal-width conv + GroupNorm + ReLU layers with the same square
+        kernel / stride / padding after the first, two FC layers, n ≤ 32."""
+        convs = [m.conv for m in self.conv_layers]
+        if len(convs) != 3 or len(self.fc_layers) != 2 or not 1 <= n <= 32:
+            return False
+        if any(m.norm_type != "GN" or m.act_type != "ReLU" or m.conv.bias is not None
+               for m in self.conv_layers):
+            return False
+        c = convs[0].out_channels
+        if c % 32 or any(cv.out_channels != c for cv in convs) or \
+                len({m.gn.num_groups for m in self.conv_layers}) != 1:
+            return False
+        cpg = c // self.conv_layers[0].gn.num_groups
+        if c % self.conv_layers[0].gn.num_groups or 32 % cpg:
+            return False
+        k2 = convs[1].kernel_size
+        if k2[0] != k2[1] or any(cv.kernel_size != k2 or cv.stride != convs[1].stride or
+                                 cv.padding != convs[1].padding or cv.stride[0] != cv.stride[1] or
+                                 cv.padding[0] != cv.padding[1] for cv in convs[1:]):
+            return False
+        if any(fc[0].in_features % 16 or fc[0].out_features % 16 for fc in self.fc_layers):
+            return False
+        if self.rotation_out_channels + 3 > 16:
+            return False
+        c1 = 0 if src1 is None else src1.c
+        k, s, p = convs[0].kernel_size[0], convs[0].stride[0], convs[0].padding[0]
+        return convs[0].kernel_size == (3, 3) and p == 1 and s in (1, 2) and \
+            src0.c % 16 == 0 and c1 % 16 == 0 and (h - 1) // s + 1 >= 8
+
+    def tail_conv1(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
+                   ws: Optional[list] = None) -> dict:
+        """The first conv on the MFMA halo conv with its K split into partial slabs (GroupNorm
+        and everything after it run in ``tail_args``' launch); returns the context
+        ``tail_args`` needs.  Buffers are appended to ``ws``."""
+        keep = ws if ws is not None else []
+        split = self._conv_mfma(0, src0, src1, n, h, w, None, None, keep)
+        if split is None:
+            raise NotImplementedError("tail_conv1: the first conv's shape has no K-split MFMA kernel")
+        return dict(parts=split[0], split=split[1], n=n, h=h, w=w, dev=src0.buf.device, keep=keep)
+
+    def tail_args(self, ctx: dict, label: Tensor, drot: Tensor, dt: Tensor,
+                  pose=None) -> "_lib.PhTailArgs":
+        """``scflow_ph_tail_args`` for GN 1 → … → heads (→ ``pose``, an
+        ``ops.pose_step_struct`` whose drot/dt are these) over ``tail_conv1``'s output.  The
+        workspace (summed conv outputs, GroupNorm affines, partial slabs, the counters) is
+        allocated once per context and shared by every call made with it (their launches must
+        run one after the other)."""
+        n, dev = ctx["n"], ctx["dev"]
+        convs = [m.conv for m in self.conv_layers]
+        c = convs[0].out_channels
+        hs, wsz = [], []
+        hh, ww = ctx["h"], ctx["w"]
+        for cv in convs:
+            k, s, p = cv.kernel_size[0], cv.stride[0], cv.padding[0]
+            hh, ww = (hh + 2 * p - k) // s + 1, (ww + 2 * p - k) // s + 1
+            hs.append(hh)
+            wsz.append(ww)
+        packs, fc1_w = self._packs(c, hs[2] * wsz[2])
+        if "tail_ws" not in ctx:
+            keep = ctx["keep"]
+
+            def empty(*shape, dtype=torch.float32):
+                t = torch.empty(*shape, device=dev, dtype=dtype)
+                keep.append(t)
+                return t
+            k2 = convs[1].kernel_size[0]
+            nchunks = k2 * k2 * (-(-c // 16))
+            splits = []
+            for j in (1, 2):
+                tiles = -(-n * hs[j] * wsz[j] // 32) * (c // 32)
+                splits.append(max(1, min(nchunks, -(-self.tail_conv_items // tiles))))
+            f1, f2 = (fc[0].out_features for fc in self.fc_layers)
+            sync = torch.zeros(_lib.load().scflow_ph_tail_sync_ints(n), device=dev,
+                               dtype=torch.int32)
+            keep.append(sync)
+            ctx["tail_ws"] = dict(
+                y=[empty(n * hs[l] * wsz[l], c) for l in range(3)],
+                scale=[empty(n, c) for _ in range(3)], shift=[empty(n, c) for _ in range(3)],
+                splits=splits,
+                conv_parts=[empty(splits[j] * n * hs[j + 1] * wsz[j + 1], c) for j in range(2)],
+                fc1_parts=empty(self.tail_fc_split[0], n, f1),
+                fc2_parts=empty(self.tail_fc_split[1], n, f2), sync=sync)
+        t = ctx["tail_ws"]
+        a = _lib.PhTailArgs()
+        a.n, a.c, a.groups = n, c, self.conv_layers[0].gn.num_groups
+        for l, m in enumerate(self.conv_layers):
+            a.eps[l] = float(m.gn.eps)
+            a.h[l], a.w[l] = hs[l], wsz[l]
+            a.gamma[l], a.beta[l] = m.gn.weight.data_ptr(), m.gn.bias.data_ptr()
+            a.y[l], a.scale[l], a.shift[l] = (t["y"][l].data_ptr(), t["scale"][l].data_ptr(),
+                                              t["shift"][l].data_ptr())
+        a.conv1_parts, a.conv1_split = ctx["parts"].data_ptr(), ctx["split"]
+        a.conv_w[0], a.conv_w[1] = packs[1].data_ptr(), packs[2].data_ptr()
+        a.kh, a.stride, a.pad = convs[1].kernel_size[0], convs[1].stride[0], convs[1].padding[0]
+        for j in range(2):
+            a.conv_split[j] = t["splits"][j]
+            a.conv_parts[j] = t["conv_parts"][j].data_ptr()
+        l1, l2 = self.fc_layers[0][0], self.fc_layers[1][0]
+        a.fc1_w, a.fc1_b, a.fc1_n = fc1_w.data_ptr(), l1.bias.data_ptr(), l1.out_features
+        a.fc1_split, a.fc1_parts = self.tail_fc_split[0], t["fc1_parts"].data_ptr()
+        a.fc2_w, a.fc2_b, a.fc2_n = l2.weight.data_ptr(), l2.bias.data_ptr(), l2.out_features
+        a.fc2_split, a.fc2_parts = self.tail_fc_split[1], t["fc2_parts"].data_ptr()
+        a.rot_w, a.rot_b = self.rotation_pred.weight.data_ptr(), self.rotation_pred.bias.data_ptr()
+        a.rch = self.rotation_out_channels
+        a.trans_w = self.translation_pred.weight.data_ptr()
+        a.trans_b = self.translation_pred.bias.data_ptr()
+        label = label.long()
+        ctx["keep"].append(label)
+        a.label, a.num_class = label.data_ptr(), self.num_class
+        a.drot, a.dt = drot.data_ptr(), dt.data_ptr()
+        if pose is not None:
+            a.pose = ctypes.pointer(pose)
+        a.sync = t["sync"].data_ptr()
+        return a
+
+    def forward_fused(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
+                      label: Tensor) -> Tuple[Tensor, Tensor]:
+        """``forward_hip`` as two launches (the first conv, then scflow_ph_tail)."""
+        dev = src0.buf.device
+        ctx = self.tail_conv1(src0, src1, n, h, w)
+        drot = torch.empty(n, self.rotation_out_channels, device=dev)
+        dt = torch.empty(n, 3, device=dev)
+        ops.ph_tail(self.tail_args(ctx, label.to(dev), drot, dt), drot)
+        ctx["result"] = (drot, dt)
+        return drot, dt
 
     def forward(self, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
         """Reference API (NCHW in).  Runs the HIP kernels (inference; no autograd graph)."""

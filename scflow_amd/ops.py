@@ -435,6 +435,41 @@ def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points:
         h, w, float(up_scale), 1.0 / float(up_scale))
 
 
+def pose_step_struct(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points: Tensor,
+                     R_out: Tensor, t_out: Tensor, flow_out: Tensor, invalid_num: float,
+                     lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], flow_up: Tensor,
+                     mask_up: Optional[Tensor], h: int, w: int, up_scale: float,
+                     lr_next: Optional[Chan] = None, hx_next: Optional[Chan] = None,
+                     weight: float = 10.0, depth_transform: str = "exp") -> "_lib.PoseStepArgs":
+    """``pose_step``'s arguments as a ``scflow_pose_step_args`` struct (for ``ph_tail``)."""
+    for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t), ("K", K), ("points", points),
+                  ("R_out", R_out), ("t_out", t_out), ("flow_out", flow_out), ("lr", lr),
+                  ("flow_up", flow_up)):
+        _require(x, nm)
+    n, H, W, _ = points.shape
+    if lr_next is not None and lr_next.buf.data_ptr() == lr.data_ptr():
+        raise ValueError("pose_step: lr_next must not alias lr")
+    s = _lib.PoseStepArgs()
+    s.drot6, s.dt, s.R_src, s.t_src, s.K = _p(drot), _p(dt), _p(R), _p(t), _p(K)
+    s.points, s.R_dst, s.t_dst, s.flow = _p(points), _p(R_out), _p(t_out), _p(flow_out)
+    s.n, s.H, s.W, s.weight = n, H, W, float(weight)
+    s.depth_transform, s.invalid_num = pose_mode(drot, depth_transform), float(invalid_num)
+    s.lr, s.delta, s.mask, s.flow_up, s.mask_up = _p(lr), _p(delta), _p(mask), _p(flow_up), _p(mask_up)
+    s.lr_next = None if lr_next is None else lr_next.ptr
+    s.s_next = 0 if lr_next is None else lr_next.stride
+    s.hx_next = None if hx_next is None else hx_next.ptr
+    s.s_hx = 0 if hx_next is None else hx_next.stride
+    s.h, s.w, s.up_scale, s.down_scale = h, w, float(up_scale), 1.0 / float(up_scale)
+    return s
+
+
+def ph_tail(args: "_lib.PhTailArgs", dev_tensor: Tensor) -> None:
+    """The fused pose-head tail (scflow_ph_tail; arguments built by
+    ``MultiClassPoseHead.tail_args``) on ``dev_tensor``'s device."""
+    _require(dev_tensor, "device tensor", contiguous=False)
+    _launch("scflow_ph_tail", dev_tensor, ctypes.byref(args))
+
+
 # ------------------------------------------------------------------------------- resampling
 def flow_downsample(flow: Tensor, out0: Chan, h: int, w: int, value_scale: float,
                     out1: Optional[Chan] = None) -> None:

@@ -488,6 +488,22 @@ def test_pose_head_hip_vs_oracle(ops, n, feat):
     # NCHW module API
     r2, t2 = head(x.cuda(), label.cuda())
     close(r2, r, 1e-6, 1e-6, "pose head NCHW api")
+    # fused tail (first conv + ONE persistent launch: scflow_ph_tail), twice (the second launch
+    # reuses the sync words); its error word must stay clear
+    src0, src1 = ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf)
+    assert head.tail_supported(src0, src1, n, feat, feat)
+    for rep in range(2):
+        ctx = head.tail_conv1(src0, src1, n, feat, feat)
+        r3 = torch.empty(n, 6, device="cuda")
+        t3 = torch.empty(n, 3, device="cuda")
+        ops.ph_tail(head.tail_args(ctx, label.cuda(), r3, t3), r3)
+        torch.cuda.synchronize()
+        sync = ctx["tail_ws"]["sync"].cpu()
+        assert int(sync[2]) == 0, ("fused pose-head tail: a dependency wait gave up "
+                                   f"(ticket, counter, value, target, phase+1) = {sync[9:14].tolist()}")
+        close(r3, r_ref, 2e-5, 1e-5, "fused pose head rotation")
+        close(t3, t_ref, 2e-5, 1e-5, "fused pose head translation")
+        close(r3, r, 1e-5, 1e-6, "fused vs unfused pose head rotation")
 
 
 def test_corr_lookup_far_out_of_bounds(ops):
