@@ -162,7 +162,8 @@ def conv_roofline(kernel, parts, timers, m_px, traffic=None, alg_bytes=None):
     return out
 
 
-def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail_weight_bytes=0):
+def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail_weight_bytes=0,
+                        tiled=True):
     """The HBM/gather-bound kernels and the correlation GEMM, timed with the same events in an
     untimed pass after the timed region (algorithmic bytes per launch from SURVEY.md §8(d)).
     At B=16, 256² the 86 MB pyramid is Infinity-Cache resident, so the lookup's GB/s is an
@@ -177,7 +178,9 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
     traffic = traffic or {}
     out = []
     for name, tkey, kernel, bound, amount in (
-            ("corr_lookup", "corr_lookup", "corr_lookup_lds_kernel<4> (a2)", "hbm", lookup_bytes),
+            ("corr_lookup", "corr_lookup", "corr_lookup_lds_kernel<4> (a2%s)" % (", tiled pyramid"
+                                                                              if tiled else ""),
+             "hbm", lookup_bytes),
             ("pose_flow", "pose_step", "pose_step_kernel (a8+a10+a11)" if fused_tail
              else "pose_flow_kernel (a8+a10)", "hbm", flow_bytes),
             # the persistent pose-head tail (GN 1 → convs 2-3 → FCs → heads) + the pose step:
@@ -185,7 +188,9 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
             ("pose_tail", "ph_tail", "ph_tail_kernel (a7 after conv 1 + a8+a10+a11, one persistent "
              "launch; latency-bound phases, bytes dominated by the pose step)", "hbm",
              flow_bytes + tail_weight_bytes),
-            ("corr_pyramid", None, "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma", corr_flops)):
+            ("corr_pyramid", None, "corr_gemm_pyr_kernel (a1: level 0 + pooled levels 1-3 in one "
+             "launch, tiled layout)" if tiled else "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma",
+             corr_flops)):
         t = timers[name]
         if t.count() == 0:
             continue
@@ -304,6 +309,8 @@ def main():
                     help="do not bracket the roofline kernels (throughput without timer overhead)")
     ap.add_argument("--pingpong", action="store_true",
                     help="run the batch as two interleaved halves (SCFlowDecoder.pingpong)")
+    ap.add_argument("--no-tiled-pyramid", action="store_true",
+                    help="row-major pyramid + separate pooling launches (SCFlowDecoder.tiled_pyramid off)")
     ap.add_argument("--graph", action="store_true",
                     help="replay a captured hipGraph per step instead of launching kernel by kernel")
     ap.add_argument("--traffic-json", default=None,
@@ -334,6 +341,7 @@ def main():
     synthetic.fill_module_(dec)
     dec = dec.to(dev).eval()
     dec.pingpong = args.pingpong
+    dec.tiled_pyramid = not args.no_tiled_pyramid
     inp = make_inputs(args.batch, args.size, seed=rank, device=dev)
 
     # launches per step of each bracketed kernel: 2 SeqConv stages per iteration for the z|r
@@ -461,7 +469,7 @@ def main():
     tail_w = 4 * sum(p.numel() for m in (ph.conv_layers[1:], ph.fc_layers) for p in m.parameters())
     tail_w += 4 * (ph.rotation_out_channels + 3) * ph.fc_layers[-1][0].out_features  # label[0] rows
     secondary += secondary_rooflines(timers, hb, args.size, traffic,
-                                     getattr(dec, "fuse_tail", True), tail_w)
+                                     getattr(dec, "fuse_tail", True), tail_w, dec.tiled_pyramid)
 
     if rank == 0:
         cfg_name = ("configs[4]" if (args.batch, args.size, args.iters) == (32, 512, 12)

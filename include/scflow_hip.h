@@ -86,6 +86,19 @@ int scflow_corr_lookup_ex(const float* pyr, const float* flow, int flow_layout, 
                           int out_layout, int out_stride, int n, int h, int w, int num_levels,
                           int radius, int align_corners, void* stream);
 
+/* a1 + a2 with the pyramid in TILED layout: level l of query pixel m is an (h>>l)×(w>>l) map
+ * stored in 4×4 tiles of 16 contiguous floats, tiles row-major — element (y, x) at
+ * ((y>>2)·((w>>l)>>2) + (x>>2))·16 + (y&3)·4 + (x&3) from the map's start (same map sizes and
+ * level offsets as scflow_corr_pyramid).  scflow_corr_pyramid_tiled computes level 0 and pools
+ * levels 1..L−1 inside the GEMM epilogue (one launch; values bit-identical to
+ * scflow_corr_pyramid's); needs L ≤ 4, h and w multiples of 8 and of 4·2^(L−1), f1/f2 16-B
+ * aligned.  scflow_corr_lookup_tiled = scflow_corr_lookup_ex on such a pyramid (same outputs). */
+int scflow_corr_pyramid_tiled(const float* f1, const float* f2, float* pyr, int n, int c, int h,
+                              int w, int num_levels, void* stream);
+int scflow_corr_lookup_tiled(const float* pyr, const float* flow, int flow_layout, float* out,
+                             int out_layout, int out_stride, int n, int h, int w, int num_levels,
+                             int radius, int align_corners, void* stream);
+
 /* Channels-last convolution (cross-correlation, like nn.Conv2d) with fused bias/activation and
  * optional ConvGRU gate epilogues.  Input channels = c0 (src0) ++ c1 (src1, may be 0).
  * Weights must be packed by scflow_conv_pack_weights for the same shape. */

@@ -98,6 +98,163 @@ __global__ __launch_bounds__(256, 2) void corr_gemm_kernel(const float* __restri
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tiled pyramid (scflow_corr_pyramid_tiled): every level's map of a query pixel stored in 4×4
+// tiles of 16 floats (64 B, tiles row-major): element (y, x) of an hl×wl map at
+// ((y>>2)·(wl>>2) + (x>>2))·16 + (y&3)·4 + (x&3).  A lookup window of (2r+2)² taps then touches
+// ≈ 3.3² whole 64-B sectors instead of 2r+2 row segments that straddle them.
+//
+// The GEMM's N dimension runs over the target pixels q in 8×8-block order (block-major, then
+// row-major inside the 8×8 block), so each wave's 64 accumulator columns are one 8×8 block of the
+// map: the epilogue writes level 0 (each 32-lane half-row pair is one contiguous 128-B run: two
+// adjacent tiles), then pools level 1 (the block's 4×4 = one tile), 2 (2×2) and 3 (1×1) from the
+// registers with lane shuffles — the same sums in the same order as AvgPool2d's reference kernel
+// (s00 + s01 + s10 + s11, then /4), so the levels are bit-identical to the row-major path's.
+// Needs h, w multiples of 8 and each level ≥ 4 wide/tall (h, w multiples of 4·2^(L−1)).
+__device__ __forceinline__ size_t tiled_off(int y, int x, int wl) {
+  return (size_t)(((y >> 2) * (wl >> 2) + (x >> 2)) * 16 + (y & 3) * 4 + (x & 3));
+}
+
+__global__ __launch_bounds__(256, 2) void corr_gemm_pyr_kernel(const float* __restrict__ f1,
+                                                               const float* __restrict__ f2,
+                                                               float* __restrict__ pyr, int C, int H,
+                                                               int W, int tiles_q, int L,
+                                                               long long NP, float sqrt_c) {
+  __shared__ float As[TK][TM];
+  __shared__ float Bs[TK][TN];
+  const int P = H * W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
+  const int n = blockIdx.y;
+  const int tp = blockIdx.x / tiles_q, tq = blockIdx.x % tiles_q;
+  const int p0 = tp * TM, q0 = tq * TN;
+  const float* A = f1 + (size_t)n * C * P;
+  const float* B = f2 + (size_t)n * C * P;
+  const int bw = W / 8;  // 8×8 blocks per map row
+  const int lr = tid >> 5, lc = (tid & 31) * 4;
+  // this thread's B columns: block-order index q' = q0 + lc (4 consecutive x of one block row)
+  int qb;
+  {
+    const int qq = q0 + lc, blk = qq >> 6, in = qq & 63;
+    qb = ((blk / bw) * 8 + (in >> 3)) * W + (blk % bw) * 8 + (in & 7);
+  }
+  floatx4 ra[2], rb[2];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = k0 + lr + 8 * j;
+      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+      ra[j] = (k < C && p0 + lc < P) ? *(const floatx4*)(A + (size_t)k * P + p0 + lc) : z;
+      rb[j] = (k < C && q0 + lc < P) ? *(const floatx4*)(B + (size_t)k * P + qb) : z;
+    }
+  };
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  gload(0);
+  for (int k0 = 0; k0 < C; k0 += TK) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      *(floatx4*)&As[lr + 8 * j][lc] = ra[j];
+      *(floatx4*)&Bs[lr + 8 * j][lc] = rb[j];
+    }
+    __syncthreads();
+    if (k0 + TK < C) gload(k0 + TK);
+#pragma unroll
+    for (int kk = 0; kk < TK; kk += 2) {
+      float av[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) av[a] = As[kk + hh][wm * 64 + a * 32 + li];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bv[b] = Bs[kk + hh][wn * 64 + b * 32 + li];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+  }
+  // epilogue: this wave's columns are the 8×8 block blk of the map; lane li of accumulator
+  // column block b holds (ly, lx) = (4b + li/8, li%8).  C/D rows: p = … + (r&3) + 8(r>>2) + 4hh
+  const int blk = (q0 + wn * 64) >> 6;
+  if (q0 + wn * 64 >= P) return;
+  const int by0 = (blk / bw) * 8, bx0 = (blk % bw) * 8;
+  const int lx = li & 7, lyq = li >> 3;  // ly = 4b + lyq
+  size_t loff[4];  // level bases
+  {
+    size_t o = 0;
+    int hl = H, wl = W;
+    for (int l = 0; l < 4; ++l) {
+      loff[l] = o;
+      o += (size_t)NP * hl * wl;
+      hl >>= 1;
+      wl >>= 1;
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int p = p0 + wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const bool pv = p < P;
+      const size_t m = (size_t)n * P + p;  // query pixel (map index)
+      float v0[2], v1[2], v2[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float v = acc[a][b][r] / sqrt_c;
+        v0[b] = v;
+        const int y = by0 + 4 * b + lyq, x = bx0 + lx;
+        if (pv) pyr[loff[0] + m * P + tiled_off(y, x, W)] = v;
+      }
+      if (L < 2) continue;
+      // level 1: lanes with even (lx, ly) sum their 2×2 (x+1: lane+1, y+1: lane+8)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float s01 = __shfl(v0[b], lane + 1), s10 = __shfl(v0[b], lane + 8),
+                    s11 = __shfl(v0[b], lane + 9);
+        float v = v0[b];
+        v += s01;
+        v += s10;
+        v += s11;
+        v1[b] = v / 4.f;
+        const int y1 = (by0 + 4 * b + lyq) >> 1, x1 = (bx0 + lx) >> 1;
+        if (pv && !(lx & 1) && !(lyq & 1)) pyr[loff[1] + m * (P / 4) + tiled_off(y1, x1, W / 2)] = v1[b];
+      }
+      if (L < 3) continue;
+      // level 2: level-1 cells at lanes with lx%4 == 0, lyq even; x+1 → lane+2, y+1 → lane+16
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float s01 = __shfl(v1[b], lane + 2), s10 = __shfl(v1[b], lane + 16),
+                    s11 = __shfl(v1[b], lane + 18);
+        float v = v1[b];
+        v += s01;
+        v += s10;
+        v += s11;
+        v2[b] = v / 4.f;
+        const int y2 = (by0 + 4 * b) >> 2, x2 = (bx0 + lx) >> 2;
+        if (pv && !(lx & 3) && lyq == 0) pyr[loff[2] + m * (P / 16) + tiled_off(y2, x2, W / 4)] = v2[b];
+      }
+      if (L < 4) continue;
+      // level 3: level-2 cells (b, lx/4): x+1 → lane+4, y+1 → the b = 1 value of the same lane
+      {
+        const float s01 = __shfl(v2[0], lane + 4), s11 = __shfl(v2[1], lane + 4);
+        float v = v2[0];
+        v += s01;
+        v += v2[1];
+        v += s11;
+        v = v / 4.f;
+        if (pv && lx == 0 && lyq == 0)
+          pyr[loff[3] + m * (P / 64) + tiled_off(by0 >> 3, bx0 >> 3, W / 8)] = v;
+      }
+    }
+  }
+}
+
 // one pyramid level: out[m][y][x] = (in[2y][2x] + in[2y][2x+1] + in[2y+1][2x] + in[2y+1][2x+1])/4
 __global__ void avgpool2_kernel(const float* __restrict__ in, float* __restrict__ out, long long M,
                                 int Hi, int Wi, int Ho, int Wo) {
@@ -156,4 +313,20 @@ SCFLOW_API int scflow_corr_pyramid(const float* f1, const float* f2, float* pyr,
     Wi = Wo;
   }
   return SCFLOW_OK;
+}
+
+SCFLOW_API int scflow_corr_pyramid_tiled(const float* f1, const float* f2, float* pyr, int n, int c,
+                                         int h, int w, int num_levels, void* stream) {
+  if (!f1 || !f2 || !pyr || n <= 0 || c <= 0 || h <= 0 || w <= 0 || num_levels < 1 ||
+      num_levels > 4)
+    return SCFLOW_EINVAL;
+  const int g = 4 << (num_levels - 1);  // every level's map a whole number of 4×4 tiles
+  if (h % 8 || w % 8 || h % g || w % g) return SCFLOW_EUNSUPPORTED;
+  if (((uintptr_t)f1 & 15) || ((uintptr_t)f2 & 15)) return SCFLOW_EALIGN;
+  const int P = h * w;
+  const int tp = ceil_div(P, TM), tq = ceil_div(P, TN);
+  dim3 grid(tp * tq, n);
+  corr_gemm_pyr_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(f1, f2, pyr, c, h, w, tq, num_levels,
+                                                            (long long)n * P, sqrtf((float)c));
+  return scflow_launch_status();
 }

@@ -17,6 +17,10 @@
 //     weights (nw, ne, sw, se; taps outside the map are zero).
 // The pyramid (≈5.6 MB per pair at 256²) is read through L2 / Infinity Cache.
 // A generic one-thread-per-(p, l, a) kernel remains for L > 4 or r > 6.
+// scflow_corr_lookup_tiled reads a pyramid whose maps are stored in 4×4 tiles of 16 floats
+// (scflow_corr_pyramid_tiled): the same loads, addressed into the tiles, so a wave's window
+// loads coalesce into ≈ 3.3² whole 64-B sectors per level instead of 12 row segments that
+// straddle sector boundaries (the configs[4] over-fetch, profiles/traffic_b32_s512.json).
 #include "common.h"
 
 namespace {
@@ -122,7 +126,8 @@ __device__ __forceinline__ float lk_bload(__amdgpu_buffer_rsrc_t r, int voff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
 }
 
-template <int R>
+// TILED: the pyramid's maps are in 4×4 tiles of 16 floats (scflow_corr_pyramid_tiled)
+template <int R, bool TILED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void corr_lookup_lds_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
     float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
@@ -209,7 +214,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
         const int i = gl + LK_GL * j;
         const int gx = ox[l] + i % WIN, gy = oy[l] + i / WIN;
         const bool ok = i < rn[l] && active && gx >= 0 && gx < Wl && gy >= 0 && gy < Hl;
-        vals[l][j] = lk_bload(rs, ok ? (ks * hw + gy * Wl + gx) * 4 : LK_OOB);
+        const int e = TILED ? ((gy >> 2) * (Wl >> 2) + (gx >> 2)) * 16 + (gy & 3) * 4 + (gx & 3)
+                            : gy * Wl + gx;
+        vals[l][j] = lk_bload(rs, ok ? (ks * hw + e) * 4 : LK_OOB);
       }
       if (use) loff += (size_t)NP * hw;
       Hl >>= 1;
@@ -324,9 +331,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 
 }  // namespace
 
-SCFLOW_API int scflow_corr_lookup_ex(const float* pyr, const float* flow, int flow_layout, float* out,
-                                     int out_layout, int out_stride, int n, int h, int w,
-                                     int num_levels, int radius, int align_corners, void* stream) {
+static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layout, float* out,
+                              int out_layout, int out_stride, int n, int h, int w, int num_levels,
+                              int radius, int align_corners, bool tiled, void* stream) {
   const int ac = align_corners ? 1 : 0;
   if (!pyr || !flow || !out || n <= 0 || h <= 0 || w <= 0 || num_levels < 1 || num_levels > 8 ||
       radius < 0)
@@ -349,6 +356,8 @@ SCFLOW_API int scflow_corr_lookup_ex(const float* pyr, const float* flow, int fl
       if (!lk_whole(hl, wl, 2 * radius + 4) && (hl < 2 * radius + 1 || wl < 2 * radius + 1)) lds_ok = false;
     }
   }
+  if (tiled && (!lds_ok || (h >> (num_levels - 1)) % 4 || (w >> (num_levels - 1)) % 4))
+    return SCFLOW_EUNSUPPORTED;
   if (lds_ok) {
     const unsigned blk = (unsigned)(((long long)n * h * w + LK_SLOTS - 1) / LK_SLOTS);
     const int D = 2 * radius + 1;
@@ -356,12 +365,20 @@ SCFLOW_API int scflow_corr_lookup_ex(const float* pyr, const float* flow, int fl
     const size_t lds = sizeof(float) * LK_SLOTS * sf;
     const int vec = out_layout == SCFLOW_LAYOUT_NHWC && out_stride % 4 == 0 &&
                     ((uintptr_t)out & 15) == 0 && sf >= num_levels * D * D;
-    switch (radius) {
-      case 1: corr_lookup_lds_kernel<1><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
-      case 2: corr_lookup_lds_kernel<2><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
-      case 3: corr_lookup_lds_kernel<3><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
-      default: corr_lookup_lds_kernel<4><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac); break;
+#define SCFLOW_LKL(RR, TT)                                                                          \
+  corr_lookup_lds_kernel<RR, TT><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout,      \
+                                                        out_stride, n, h, w, num_levels, vec, ac)
+    switch (radius * 2 + (tiled ? 1 : 0)) {
+      case 2: SCFLOW_LKL(1, false); break;
+      case 3: SCFLOW_LKL(1, true); break;
+      case 4: SCFLOW_LKL(2, false); break;
+      case 5: SCFLOW_LKL(2, true); break;
+      case 6: SCFLOW_LKL(3, false); break;
+      case 7: SCFLOW_LKL(3, true); break;
+      case 9: SCFLOW_LKL(4, true); break;
+      default: SCFLOW_LKL(4, false); break;
     }
+#undef SCFLOW_LKL
     return scflow_launch_status();
   }
   const long long total = (long long)n * h * w * num_levels * (2 * radius + 1);
@@ -377,6 +394,21 @@ SCFLOW_API int scflow_corr_lookup_ex(const float* pyr, const float* flow, int fl
   }
 #undef SCFLOW_LK
   return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_corr_lookup_ex(const float* pyr, const float* flow, int flow_layout, float* out,
+                                     int out_layout, int out_stride, int n, int h, int w,
+                                     int num_levels, int radius, int align_corners, void* stream) {
+  return corr_lookup_launch(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels,
+                            radius, align_corners, false, stream);
+}
+
+SCFLOW_API int scflow_corr_lookup_tiled(const float* pyr, const float* flow, int flow_layout,
+                                        float* out, int out_layout, int out_stride, int n, int h,
+                                        int w, int num_levels, int radius, int align_corners,
+                                        void* stream) {
+  return corr_lookup_launch(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels,
+                            radius, align_corners, true, stream);
 }
 
 SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_layout, float* out,

@@ -108,6 +108,9 @@ class SCFlowDecoder(nn.Module):
         # (agent release + acquire + L2 misses on the producer's lines) that a kernel boundary
         # (≈2 µs) does not
         self.fuse_posehead = False
+        # correlation pyramid in the tiled layout (4×4 tiles of 16 floats per map, pooling fused
+        # into the GEMM epilogue; ops.corr_pyramid_tiled) when the geometry allows it
+        self.tiled_pyramid = True
         self._hooks_on = True
         self.hook_batch = 0
 
@@ -291,8 +294,13 @@ class SCFlowDecoder(nn.Module):
         iters = int(self.iters)
 
         # a1 + a9 (once per forward)
+        tiled = self.tiled_pyramid and ops.tiled_lookup_ok(h, w, self.num_levels, self.radius,
+                                                           self.corr_lookup.align_corners)
         self._hook("corr_pyramid", True)
-        pyr, _ = ops.corr_pyramid(feat_render, feat_real, self.num_levels)
+        if tiled:
+            pyr = ops.corr_pyramid_tiled(feat_render, feat_real, self.num_levels)
+        else:
+            pyr, _ = ops.corr_pyramid(feat_render, feat_real, self.num_levels)
         self._hook("corr_pyramid", False)
         depth = depth.contiguous().float()
         K = K.contiguous().float()
@@ -434,7 +442,8 @@ class SCFlowDecoder(nn.Module):
 
         def seg_lookup():
             ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
-                            flow_layout="nhwc", align_corners=self.corr_lookup.align_corners)
+                            flow_layout="nhwc", align_corners=self.corr_lookup.align_corners,
+                            tiled=tiled)
 
         corr_net = self.encoder.corr_net
 

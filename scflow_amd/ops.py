@@ -148,6 +148,57 @@ def corr_pyramid(feat1: Tensor, feat2: Tensor, num_levels: int = 4) -> Tuple[Ten
     return buf, pyramid_views(buf, n, h, w, num_levels)
 
 
+def tiled_pyramid_ok(h: int, w: int, num_levels: int) -> bool:
+    """Whether scflow_corr_pyramid_tiled supports this geometry."""
+    g = 4 << (num_levels - 1)
+    return 1 <= num_levels <= 4 and h % 8 == 0 and w % 8 == 0 and h % g == 0 and w % g == 0
+
+
+def tiled_lookup_ok(h: int, w: int, num_levels: int, radius: int, align_corners: bool) -> bool:
+    """Whether scflow_corr_lookup_tiled supports this geometry (its LDS kernel: r in 1..4, and
+    without align_corners every windowed level at least 2r+1 wide and tall)."""
+    if not tiled_pyramid_ok(h, w, num_levels) or not 1 <= radius <= 4:
+        return False
+    if not align_corners:
+        win = 2 * radius + 4
+        for l in range(num_levels):
+            hl, wl = h >> l, w >> l
+            whole = hl + 2 <= win and wl + 2 <= win
+            if not whole and (hl < 2 * radius + 1 or wl < 2 * radius + 1):
+                return False
+    return True
+
+
+def corr_pyramid_tiled(feat1: Tensor, feat2: Tensor, num_levels: int = 4) -> Tensor:
+    """The pyramid in the TILED layout (scflow_corr_pyramid_tiled: every map in 4×4 tiles of 16
+    floats, pooling fused into the GEMM epilogue) as one flat buffer — for ``corr_lookup(...,
+    tiled=True)``; ``untile_pyramid`` turns it back into the reference's level views."""
+    _require(feat1, "feat1")
+    _require(feat2, "feat2")
+    if feat1.shape != feat2.shape or feat1.dim() != 4:
+        raise ValueError(f"feature shapes differ or are not 4-D: {feat1.shape} {feat2.shape}")
+    n, c, h, w = feat1.shape
+    if not tiled_pyramid_ok(h, w, num_levels):
+        raise ScflowError(f"tiled pyramid needs L <= 4 and h, w multiples of 8 and 4*2^(L-1): "
+                          f"h={h} w={w} L={num_levels}")
+    lib = _lib.load()
+    buf = torch.empty(lib.scflow_corr_pyramid_size(n, h, w, num_levels), device=feat1.device,
+                      dtype=torch.float32)
+    _launch("scflow_corr_pyramid_tiled", feat1, _p(feat1), _p(feat2), _p(buf), n, c, h, w,
+            num_levels)
+    return buf
+
+
+def untile_pyramid(buf: Tensor, n: int, h: int, w: int, num_levels: int) -> List[Tensor]:
+    """Level views ``[N·H·W, 1, H_l, W_l]`` (row-major copies) of a tiled pyramid buffer."""
+    out, off, P = [], 0, h * w
+    for hl, wl in pyramid_level_shapes(h, w, num_levels):
+        t = buf[off: off + n * P * hl * wl].view(n * P, hl // 4, wl // 4, 4, 4)
+        out.append(t.permute(0, 1, 3, 2, 4).reshape(n * P, 1, hl, wl))
+        off += n * P * hl * wl
+    return out
+
+
 def pyramid_views(buf: Tensor, n: int, h: int, w: int, num_levels: int) -> List[Tensor]:
     views, off, P = [], 0, h * w
     for hl, wl in pyramid_level_shapes(h, w, num_levels):
@@ -179,10 +230,11 @@ def pyramid_buffer(levels: Sequence[Tensor], n: int, h: int, w: int) -> Tensor:
 # ------------------------------------------------------------------------------- a2 lookup
 def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: int, radius: int,
                 out: Optional[Chan] = None, flow_layout: str = "nchw",
-                align_corners: bool = True) -> Tensor:
+                align_corners: bool = True, tiled: bool = False) -> Tensor:
     """Window lookup.  ``out=None`` → NCHW ``[n, L(2r+1)², h, w]`` (the reference's layout,
     corr_lookup.py:135-136); otherwise written channels-last into ``out``.  ``align_corners``:
-    grid_sample's (SCFlow's config True; False: bilinear_sample's default, corr_lookup.py:35)."""
+    grid_sample's (SCFlow's config True; False: bilinear_sample's default, corr_lookup.py:35).
+    ``tiled``: ``pyr`` is a ``corr_pyramid_tiled`` buffer."""
     _require(pyr, "pyramid")
     _require(flow, "flow")
     K = num_levels * (2 * radius + 1) ** 2
@@ -193,7 +245,10 @@ def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: i
     else:
         res = out.buf
         ptr, olay, ostride = out.ptr, _lib.LAYOUT_NHWC, out.stride
-    if align_corners:
+    if tiled:
+        _launch("scflow_corr_lookup_tiled", flow, _p(pyr), _p(flow), lay, ptr, olay, ostride, n, h,
+                w, num_levels, radius, int(bool(align_corners)))
+    elif align_corners:
         _launch("scflow_corr_lookup", flow, _p(pyr), _p(flow), lay, ptr, olay, ostride, n, h, w,
                 num_levels, radius)
     else:

@@ -45,6 +45,30 @@ def test_corr_pyramid(ops, shape):
         close(a, b, 2e-5, 2e-5, f"level {i}")
 
 
+@pytest.mark.parametrize("n,c,h,w,L", [(2, 256, 32, 32, 4), (1, 64, 64, 64, 4), (3, 16, 16, 24, 2),
+                                       (2, 32, 32, 48, 3), (1, 8, 8, 8, 1)])
+def test_corr_pyramid_tiled_bit_identical(ops, n, c, h, w, L):
+    """The tiled pyramid (4×4 tiles per map, pooling in the GEMM epilogue) holds exactly the
+    row-major pyramid's values — the same GEMM sums and AvgPool2d's sum order — at every level,
+    and the tiled lookup gives exactly the row-major lookup's output (both align_corners)."""
+    g = torch.Generator().manual_seed(5)
+    f1 = torch.randn(n, c, h, w, generator=g).cuda()
+    f2 = torch.randn(n, c, h, w, generator=g).cuda()
+    _, lv = ops.corr_pyramid(f1, f2, L)
+    tb = ops.corr_pyramid_tiled(f1, f2, L)
+    for i, (a, b) in enumerate(zip(lv, ops.untile_pyramid(tb, n, h, w, L))):
+        assert torch.equal(a, b), f"level {i}: max diff {(a - b).abs().max().item():.3e}"
+    flow = ((torch.rand(n, 2, h, w, generator=g) - 0.5) * 1.5 * h).cuda()
+    flow[:, :, 0, 0] = torch.tensor([0.5, -0.5])
+    buf = ops.pyramid_buffer(lv, n, h, w)
+    for ac in (True, False):
+        if not ops.tiled_lookup_ok(h, w, L, 4, ac):
+            continue
+        ref = ops.corr_lookup(buf, flow, n, h, w, L, 4, align_corners=ac)
+        got = ops.corr_lookup(tb, flow, n, h, w, L, 4, align_corners=ac, tiled=True)
+        assert torch.equal(ref, got), f"tiled lookup ac={ac}: {(ref - got).abs().max().item():.3e}"
+
+
 def test_corr_pyramid_golden(ops):
     gd = golden("ops")
     _, lv = ops.corr_pyramid(t(gd["pyr_f1"]).cuda(), t(gd["pyr_f2"]).cuda(), 4)
