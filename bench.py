@@ -12,10 +12,10 @@ SURVEY.md §8(e)); ``value`` = all pairs·iterations of all ranks ÷ the slowest
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Extra JSON fields:
-* ``roofline``: the kernel with the most GPU time in the step, ``conv_wino_kernel<32,2>`` — the
-  F(2×2,3×3) Winograd convolution on fp32 MFMA with 64-channel workgroups, which runs the XHead
-  hidden convs (128→512, both heads in one launch) and corr_net.1 (256→192) once per iteration
-  each.  Both launches are bracketed live with HIP events inside the timed region (one of each
+* ``roofline``: the kernel with the most GPU time in the step, ``conv_wino_kernel`` — the
+  F(2×2,3×3) Winograd convolution on fp32 MFMA — on its two largest launch shapes, the XHead
+  hidden convs (128→512, both heads in one launch, 64-channel workgroups) and corr_net.1
+  (256→192, 96-channel workgroups), once per iteration each.  Both launches are bracketed live with HIP events inside the timed region (one of each
   per step).  ``achieved``/``frac`` count the FLOPs the matrix cores EXECUTE (Winograd: 16
   transform points per 2×2 tile, 2.25× fewer multiplies than a direct conv), so ``frac`` ≤ 1 is
   a true roofline fraction; ``direct_conv_flops_per_launch`` / ``direct_equiv_tflops`` give the
@@ -450,10 +450,12 @@ def main():
     c1 = dec.encoder.corr_net[-1].conv
     corr1_r = ConvRunner.of(c1, dec.encoder.corr_net[-1].act_type)
     headline = conv_roofline(
-        "conv_wino_kernel<32,2> (F(2x2,3x3) Winograd on fp32 MFMA, 64-channel workgroups): "
-        "XHead hidden convs 128->512 + corr_net.1 256->192",
+        "conv_wino_kernel (F(2x2,3x3) Winograd on fp32 MFMA): XHead hidden convs 128->512 "
+        "(<32,2>: 64-channel workgroups) + corr_net.1 256->192 (<32,3>: 96-channel workgroups, one "
+        "per CU)",
         [("heads", heads_r, hc, 0), ("corr_net1", corr1_r, c1.in_channels, 0)], timers, m_px,
-        traffic.get("conv_wino_kernel<32,2>"), alg.get("conv_wino_kernel<32,2>"))
+        traffic.get("conv_wino_kernel", traffic.get("conv_wino_kernel<32,2>")),
+        alg.get("conv_wino_kernel", alg.get("conv_wino_kernel<32,2>")))
     if not (heads_r.winograd and corr1_r.winograd):
         headline["kernel"] = "direct conv_mfma_kernel (Winograd off): XHead hidden + corr_net.1"
 

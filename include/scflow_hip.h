@@ -98,6 +98,12 @@ int scflow_corr_pyramid_tiled(const float* f1, const float* f2, float* pyr, int 
 int scflow_corr_lookup_tiled(const float* pyr, const float* flow, int flow_layout, float* out,
                              int out_layout, int out_stride, int n, int h, int w, int num_levels,
                              int radius, int align_corners, void* stream);
+/* Profiling only: later LDS-kernel lookups (scflow_corr_lookup*) write 6 u64 real-time-clock
+ * stamps per workgroup of 16 query pixels to `stamps` (phase boundaries; NULL turns it off). */
+int scflow_debug_lookup_stamps(void* stamps);
+/* Profiling only: later F(2×2,3×3) Winograd conv launches write 4 u64 real-time-clock stamps per
+ * workgroup (start, prologue done, main loop done, epilogue done), NULL turns it off. */
+int scflow_debug_conv_stamps(void* stamps);
 
 /* Channels-last convolution (cross-correlation, like nn.Conv2d) with fused bias/activation and
  * optional ConvGRU gate epilogues.  Input channels = c0 (src0) ++ c1 (src1, may be 0).

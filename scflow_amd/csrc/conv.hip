@@ -682,7 +682,8 @@ long long wino_blocks(const scflow_conv_args& a) {
   if (a.kh == 1) return (long long)a.n * (a.h / (128 / a.w));
   return (long long)a.n * (a.h / 4) * (a.w / 32);
 }
-// 64 output channels per workgroup when that still gives ≥ 1.5 workgroups per CU, else 32
+// 64 output channels per workgroup when that still gives ≥ 1.5 workgroups per CU, else 32;
+// SCFLOW_WINO_NBW=1|2 forces one, =4 disables the 96-channel choice (tuning only)
 // (measured per decoder shape at B = 16, tools/conv_bench.py: 3×3 256→192 85 vs 95 µs at 384
 // workgroups; 256→126, 128→64 and the GRU q convs at 256 or fewer prefer 32)
 int wino_nbw(const scflow_conv_args& a, int cus) {
@@ -693,6 +694,10 @@ int wino_nbw(const scflow_conv_args& a, int cus) {
   }
   if (forced == 1 || forced == 2) return forced;
   if (a.cout <= 32) return 1;
+  // 96 channels when that is exactly one workgroup per CU where 64 would leave 1.5 (3×3, W = 32)
+  if (forced != 4 && a.kh == 3 && a.w == 32 && a.cout % 96 == 0 &&
+      wino_blocks(a) * (a.cout / 96) == cus && (2 * wino_blocks(a) * (a.cout / 64)) % (2LL * cus))
+    return 3;
   return 2 * wino_blocks(a) * (round_up(a.cout, 64) / 64) >= 3LL * cus ? 2 : 1;
 }
 bool wino_enabled(int kh) {
@@ -724,6 +729,9 @@ int wino_swz(int R, int C) {
   return c;
 }
 
+// profiling: where the next F(2×2,3×3) Winograd launches write their per-workgroup stamps
+static unsigned long long* g_wino_stamps = nullptr;
+
 template <int W, int NBW>
 int launch_wino_w(WinoParams p, hipStream_t st) {
   using G = WinoGeom<W>;
@@ -736,6 +744,7 @@ int launch_wino_w(WinoParams p, hipStream_t st) {
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * G::XB, round_up(p.a.cout, 32 * NBW) / (32 * NBW));
   p.swz_c = wino_swz(grid.x, grid.y);
+  p.stamps = g_wino_stamps;
   conv_wino_kernel<W, NBW><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }
@@ -789,7 +798,9 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
   p.cp0 = round_up(a.c0, WSC);
   p.nst = (p.cp0 + round_up(a.c1, WSC)) / WSC;
   const int nbw = wino_nbw(a, device_cus());
-  if (a.w == 32) return nbw == 2 ? launch_wino_w<32, 2>(p, st) : launch_wino_w<32, 1>(p, st);
+  if (a.w == 32)
+    return nbw == 3 ? launch_wino_w<32, 3>(p, st)
+                    : nbw == 2 ? launch_wino_w<32, 2>(p, st) : launch_wino_w<32, 1>(p, st);
   if (a.w == 128) return nbw == 2 ? launch_wino_w<128, 2>(p, st) : launch_wino_w<128, 1>(p, st);
   return nbw == 2 ? launch_wino_w<64, 2>(p, st) : launch_wino_w<64, 1>(p, st);
 }
@@ -1078,4 +1089,11 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     default: return SCFLOW_EUNSUPPORTED;
   }
   return scflow_launch_status();
+}
+
+// Profiling only: later F(2×2,3×3) Winograd launches write 4 u64 real-time-clock stamps per
+// workgroup (start, prologue done, main loop done, epilogue done) to `stamps`, or stop (NULL).
+SCFLOW_API int scflow_debug_conv_stamps(void* stamps) {
+  g_wino_stamps = (unsigned long long*)stamps;
+  return SCFLOW_OK;
 }

@@ -87,7 +87,15 @@ struct WinoParams {
   scflow_conv_args a;
   int cp0, nst;  // source 0's channels padded to WSC, stages (WSC channels each) over both
   int swz_c;     // XCD-aware block order (wino_block): column parts across the 8 XCDs, 0 = off
+  unsigned long long* stamps;  // profiling (scflow_debug_conv_stamps): 4 per workgroup, or NULL
 };
+
+// profiling: thread 0's real-time-clock stamp k (0 start, 1 prologue done, 2 main loop done,
+// 3 epilogue done) of this workgroup
+__device__ __forceinline__ void wino_stamp(unsigned long long* st, int k) {
+  if (st && threadIdx.x == 0)
+    st[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // (tile block, output-channel block) of this workgroup.  Workgroups are dispatched round-robin
 // over the 8 XCDs (each with its own L2) in linear block order; with swz_c > 0 the grid is cut
@@ -131,8 +139,10 @@ constexpr size_t wino_lds_bytes() {
   return sizeof(float) * (halo > epi ? halo : epi);
 }
 
+// NBW = 3 (96 output channels, one workgroup per CU: 192 accumulator registers per lane) balances
+// grids whose 64-channel version would leave 1.5 workgroups per CU (corr_net.1 at B = 16).
 template <int W, int NBW>
-__global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
+__global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoParams P) {
   using G = WinoGeom<W>;
   constexpr int BNW = 32 * NBW;  // output channels per workgroup
   extern __shared__ floatx4 smem4[];  // float4-typed so halo accesses are ds_*_b128
@@ -143,6 +153,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   const int li = lane & 31, hh = lane >> 5;
   int bx, by;
   wino_block(P.swz_c, bx, by);
+  wino_stamp(P.stamps, 0);
   const int blocks_per_img = (a.h / G::OROWS) * G::XB;
   const int img = bx / blocks_per_img;
   const int brem = bx % blocks_per_img;
@@ -312,6 +323,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   // loop-entry state with the steady state and waits for ALL loads in front of the MFMAs.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  wino_stamp(P.stamps, 1);
   floatx4 vA[4], vB[4];
   vcompute(0, 0, vA);
   inloop = true;
@@ -358,6 +370,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
   // keeps both the b128 stores (8-lane groups) and the b128 loads (16-lane groups) conflict-free.
   constexpr int WEP = WTM + 4;
   __syncthreads();
+  wino_stamp(P.stamps, 2);
   float* S = smem;
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb)
@@ -377,47 +390,95 @@ __global__ __launch_bounds__(256, 2) void conv_wino_kernel(WinoParams P) {
       *(floatx4*)&S[((wave * 2 + 1) * BNW + co) * WEP + m0] = s1v;
     }
   __syncthreads();
-  const int co = tid % BNW;
-  const int col = by * BNW + co;
-  if (col >= a.cout) return;
-  const float bias = a.bias ? a.bias[col] : 0.f;
-  const float osc = a.out_scale ? a.out_scale[col] : 1.f;
-  const float osh = a.out_scale ? a.out_shift[col] : 0.f;
-  constexpr int GROUPS = 256 / BNW;            // 4 (BNW 64) or 8 (BNW 32)
-  constexpr int NPX = WTM * 4 / GROUPS;        // output pixels per thread
-  const int g = tid / BNW;
-  const int ar = (g >> 1) & 1, bc = g & 1;      // this thread's output position in the 2×2 tile
-  const int mbase = (g >> 2) * NPX;             // its run of NPX tiles
-  size_t pix[NPX];
-  float val[NPX];
+  if constexpr (256 % BNW == 0) {
+    const int co = tid % BNW;
+    const int col = by * BNW + co;
+    if (col >= a.cout) return;
+    const float bias = a.bias ? a.bias[col] : 0.f;
+    const float osc = a.out_scale ? a.out_scale[col] : 1.f;
+    const float osh = a.out_scale ? a.out_shift[col] : 0.f;
+    constexpr int GROUPS = 256 / BNW;            // 4 (BNW 64) or 8 (BNW 32)
+    constexpr int NPX = WTM * 4 / GROUPS;        // output pixels per thread
+    const int g = tid / BNW;
+    const int ar = (g >> 1) & 1, bc = g & 1;      // this thread's output position in the 2×2 tile
+    const int mbase = (g >> 2) * NPX;             // its run of NPX tiles
+    size_t pix[NPX];
+    float val[NPX];
+  #pragma unroll
+    for (int q4 = 0; q4 < NPX / 4; ++q4) {
+      const int m0 = mbase + 4 * q4;
+      const float* Sb = S + ((size_t)bc * BNW + co) * WEP + m0;
+      const floatx4 s0 = *(const floatx4*)(Sb + 0 * 2 * BNW * WEP);
+      const floatx4 s1 = *(const floatx4*)(Sb + 1 * 2 * BNW * WEP);
+      const floatx4 s2 = *(const floatx4*)(Sb + 2 * 2 * BNW * WEP);
+      const floatx4 s3 = *(const floatx4*)(Sb + 3 * 2 * BNW * WEP);
+  #pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int q = 4 * q4 + e, m = m0 + e;
+        const float v = ar == 0 ? s0[e] + s1[e] + s2[e] : s1[e] - s2[e] - s3[e];
+        const int y = oy0 + 2 * (m / G::TW) + ar, x = ox0 + 2 * (m % G::TW) + bc;
+        pix[q] = ((size_t)img * a.h + y) * W + x;
+        val[q] = (v + bias) * osc + osh;
+      }
+    }
+    // all global reads (bias map, residual) before any store
+    if (a.bias_map) {
+  #pragma unroll
+      for (int q = 0; q < NPX; ++q) val[q] += a.bias_map[pix[q] * a.sbm + col];
+    }
+    if (a.res) {
+  #pragma unroll
+      for (int q = 0; q < NPX; ++q) val[q] += a.res[pix[q] * a.sres + col];
+    }
+  #pragma unroll
+    for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q], a.act);
+
+  } else {
+    // BNW does not divide the 256 threads: (output position, channel) pairs dealt round robin,
+    // each pair over all WTM tiles (same arithmetic as above)
+    for (int pi = tid; pi < 4 * BNW; pi += 256) {
+      const int co = pi % BNW, g = pi / BNW;
+      const int col = by * BNW + co;
+      if (col >= a.cout) continue;
+      const float bias = a.bias ? a.bias[col] : 0.f;
+      const float osc = a.out_scale ? a.out_scale[col] : 1.f;
+      const float osh = a.out_scale ? a.out_shift[col] : 0.f;
+      const int ar = (g >> 1) & 1, bc = g & 1;
+#pragma unroll 2
+      for (int q4 = 0; q4 < WTM / 4; ++q4) {
+        const int m0 = 4 * q4;
+        const float* Sb = S + ((size_t)bc * BNW + co) * WEP + m0;
+        const floatx4 s0 = *(const floatx4*)(Sb + 0 * 2 * BNW * WEP);
+        const floatx4 s1 = *(const floatx4*)(Sb + 1 * 2 * BNW * WEP);
+        const floatx4 s2 = *(const floatx4*)(Sb + 2 * 2 * BNW * WEP);
+        const floatx4 s3 = *(const floatx4*)(Sb + 3 * 2 * BNW * WEP);
+        size_t pix[4];
+        float val[4];
 #pragma unroll
-  for (int q4 = 0; q4 < NPX / 4; ++q4) {
-    const int m0 = mbase + 4 * q4;
-    const float* Sb = S + ((size_t)bc * BNW + co) * WEP + m0;
-    const floatx4 s0 = *(const floatx4*)(Sb + 0 * 2 * BNW * WEP);
-    const floatx4 s1 = *(const floatx4*)(Sb + 1 * 2 * BNW * WEP);
-    const floatx4 s2 = *(const floatx4*)(Sb + 2 * 2 * BNW * WEP);
-    const floatx4 s3 = *(const floatx4*)(Sb + 3 * 2 * BNW * WEP);
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + e;
+          const float v = ar == 0 ? s0[e] + s1[e] + s2[e] : s1[e] - s2[e] - s3[e];
+          const int y = oy0 + 2 * (m / G::TW) + ar, x = ox0 + 2 * (m % G::TW) + bc;
+          pix[e] = ((size_t)img * a.h + y) * W + x;
+          val[e] = (v + bias) * osc + osh;
+        }
+        if (a.bias_map) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = 4 * q4 + e, m = m0 + e;
-      const float v = ar == 0 ? s0[e] + s1[e] + s2[e] : s1[e] - s2[e] - s3[e];
-      const int y = oy0 + 2 * (m / G::TW) + ar, x = ox0 + 2 * (m % G::TW) + bc;
-      pix[q] = ((size_t)img * a.h + y) * W + x;
-      val[q] = (v + bias) * osc + osh;
+          for (int e = 0; e < 4; ++e) val[e] += a.bias_map[pix[e] * a.sbm + col];
+        }
+        if (a.res) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) val[e] += a.res[pix[e] * a.sres + col];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a.out[pix[e] * a.so + col] = act_apply(val[e], a.act);
+      }
     }
   }
-  // all global reads (bias map, residual) before any store
-  if (a.bias_map) {
-#pragma unroll
-    for (int q = 0; q < NPX; ++q) val[q] += a.bias_map[pix[q] * a.sbm + col];
+  if (P.stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    wino_stamp(P.stamps, 3);
   }
-  if (a.res) {
-#pragma unroll
-    for (int q = 0; q < NPX; ++q) val[q] += a.res[pix[q] * a.sres + col];
-  }
-#pragma unroll
-  for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q], a.act);
 }
 
 // U = G g Gᵀ per (co, ci) (row i = 2 negated), packed [nb32][sub-step][ξ][lane][4] with

@@ -131,10 +131,16 @@ template <int R, bool TILED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void corr_lookup_lds_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
     float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
-    int vec_out, int ac) {
+    int vec_out, int ac, unsigned long long* stamps) {
 #pragma clang fp contract(off)
   constexpr int D = 2 * R + 1;
   constexpr int WIN = D + 3;
+  // profiling (scflow_debug_lookup_stamps): thread 0's real-time-clock stamps at the phase
+  // boundaries, 6 per workgroup
+  auto stamp = [&](int k) {
+    if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 6 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   constexpr int NPR = (LK_MAXL * D + LK_GL - 1) / LK_GL;  // (level, a) pairs per lane
   extern __shared__ float win[];  // [LK_SLOTS][slot floats]
   __shared__ float crd[LK_SLOTS][LK_MAXL][2][D];
@@ -171,6 +177,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     crd[slot][l][axis][i] = unnorm_coord(c + (float)(i - R), size, ac);
   }
   __syncthreads();
+  stamp(1);
   // 1b. per (level, axis): the region origin — −1 for a whole map, else floor(first sample) − 1
   //     (one-tap margin: a rounded sample coordinate moves its floor by at most one), far out
   //     of the map when the level has no finite samples; per (level, axis, index): the sample's
@@ -223,6 +230,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
       Wl >>= 1;
     }
   }
+  stamp(2);
   {
     int off = 0;
 #pragma unroll
@@ -236,6 +244,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     }
   }
   __syncthreads();
+  stamp(3);
   // 3. samples: the pixel's 16 lanes take its L·D (level, a) pairs in turn and produce the D
   //    samples b of each (channel k = l·D² + a·D + b samples x+a−r, y+b−r); a sample whose
   //    2×2 taps leave the region is zero (off the map: grid_sample's zero padding).  Every LDS
@@ -298,6 +307,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     // channels-last with a 16-B aligned pixel stride: the pixel's L·D² outputs go through its
     // own LDS region (only its 16 lanes, one wave, read it) and out as 16-B stores
     __syncthreads();
+    stamp(4);
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
       const int t = gl + LK_GL * q;
@@ -312,6 +322,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
       const int K4 = L * D * D / 4;
       for (int c = gl; c < K4; c += LK_GL) *(floatx4*)(o + 4 * c) = *(const floatx4*)(sw + 4 * c);
       for (int c = 4 * K4 + gl; c < L * D * D; c += LK_GL) o[c] = sw[c];
+    }
+    if (stamps) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      stamp(5);
     }
     return;
   }
@@ -330,6 +345,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 }
 
 }  // namespace
+
+// profiling: where the next LDS-kernel launches write their phase stamps (NULL: off)
+static unsigned long long* g_lk_stamps = nullptr;
 
 static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layout, float* out,
                               int out_layout, int out_stride, int n, int h, int w, int num_levels,
@@ -367,7 +385,8 @@ static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layo
                     ((uintptr_t)out & 15) == 0 && sf >= num_levels * D * D;
 #define SCFLOW_LKL(RR, TT)                                                                          \
   corr_lookup_lds_kernel<RR, TT><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout,      \
-                                                        out_stride, n, h, w, num_levels, vec, ac)
+                                                        out_stride, n, h, w, num_levels, vec, ac,  \
+                                                        g_lk_stamps)
     switch (radius * 2 + (tiled ? 1 : 0)) {
       case 2: SCFLOW_LKL(1, false); break;
       case 3: SCFLOW_LKL(1, true); break;
@@ -416,4 +435,12 @@ SCFLOW_API int scflow_corr_lookup(const float* pyr, const float* flow, int flow_
                                   int num_levels, int radius, void* stream) {
   return scflow_corr_lookup_ex(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w,
                                num_levels, radius, 1, stream);
+}
+
+// Profiling only: later LDS-kernel lookups write, per workgroup, 6 real-time-clock stamps
+// (100 MHz) to `stamps` — start, coordinates done, window loads returned, windows in LDS,
+// samples done, outputs stored (the last two with vec_out) — or stop (NULL).
+SCFLOW_API int scflow_debug_lookup_stamps(void* stamps) {
+  g_lk_stamps = (unsigned long long*)stamps;
+  return SCFLOW_OK;
 }

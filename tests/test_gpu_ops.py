@@ -242,6 +242,7 @@ def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
     (1, 64, 64, 128, 0, 64, 3, 1, "ReLU"),         # 512² feature size
     (2, 64, 64, 36, 4, 100, 3, 1, None),           # W=64, ragged channels
     (16, 32, 32, 128, 0, 512, 3, 1, "ReLU"),       # B=16 heads: 64-channel workgroups
+    (16, 32, 32, 256, 0, 192, 3, 1, "ReLU"),       # B=16 corr_net.1: 96-channel workgroups
     # F(4,5), 1×5 / 5×1
     (2, 32, 32, 384, 0, 256, (1, 5), (0, 2), "Sigmoid"),    # GRU z|r
     (2, 32, 32, 128, 256, 128, (5, 1), (2, 0), "Tanh"),     # GRU q, two sources

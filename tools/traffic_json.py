@@ -28,8 +28,9 @@ def groups(B, S):
     lookup = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
     pose_step = B * 36 * S * S
     return {
-        "conv_wino_kernel<32,2>": (["conv_wino_kernel<32, 2>"], (heads + corr1) / 2,
-                                   "XHead hidden 128→512 + corr_net.1 256→192 (launches averaged)"),
+        "conv_wino_kernel": (["conv_wino_kernel<32, 2>", "conv_wino_kernel<32, 3>"], (heads + corr1) / 2,
+                             "F(2x2,3x3) Winograd: XHead hidden 128→512 <32,2> + corr_net.1 256→192 "
+                             "<32,3> (launches averaged)"),
         "gru_zr": (["conv_wino5_kernel<0, 32, 2, 1>", "conv_wino5_kernel<1, 32, 2, 1>",
                     "conv_wino5_kernel<0, 32, 1, 1>", "conv_wino5_kernel<1, 32, 1, 1>"], zr,
                    "SepConvGRU z|r 1×5 + 5×1 (context hoisted)"),
