@@ -67,6 +67,17 @@ def test_corr_pyramid_tiled_bit_identical(ops, n, c, h, w, L):
         ref = ops.corr_lookup(buf, flow, n, h, w, L, 4, align_corners=ac)
         got = ops.corr_lookup(tb, flow, n, h, w, L, 4, align_corners=ac, tiled=True)
         assert torch.equal(ref, got), f"tiled lookup ac={ac}: {(ref - got).abs().max().item():.3e}"
+        # channels-last flow and 16-B aligned channels-last output: the persistent pipelined
+        # kernel (corr_lookup_pipe_kernel), both layouts, against the per-batch kernel's NCHW
+        K = L * 81
+        nhwc = flow.permute(0, 2, 3, 1).contiguous()
+        for pyr_buf, til in ((buf, False), (tb, True)):
+            o = torch.full((n * h * w, K + 4), 7.0, device="cuda")
+            ops.corr_lookup(pyr_buf, nhwc, n, h, w, L, 4, out=ops.Chan(o, 4, K), flow_layout="nhwc",
+                            align_corners=ac, tiled=til)
+            o2 = o[:, 4:].reshape(n, h, w, K).permute(0, 3, 1, 2)
+            assert torch.equal(ref, o2), f"pipelined lookup tiled={til} ac={ac}"
+            assert (o[:, :4] == 7).all()
 
 
 def test_corr_pyramid_golden(ops):
