@@ -424,6 +424,17 @@ typedef struct {
   int n, h, w, cout, kh, kw, stride, ph, pw;
   int accumulate;
 } scflow_wgrad_args;
+/* Training: InstanceNorm2d(affine=False) (+ ReLU) of channels-last x [n][hw][c] (c % 4 == 0,
+ * c ≤ 256 for the backward), the feature encoder's norms (resnet.py BasicBlock).  Statistics from
+ * scflow_enc_stats + scflow_enc_norm_finalize (scale = rstd, shift = −mean·rstd);
+ * scflow_in_apply: y = act(x·scale + shift);  scflow_in_backward: dx = rstd·(g − mean(g) −
+ * x̂·mean(g·x̂)), g = dy masked by x̂ > 0 when relu — workspace partial: n·chunks·2·c doubles,
+ * mm: n·2·c floats. */
+int scflow_in_apply(const float* x, const float* scale, const float* shift, float* y, int n, int hw,
+                    int c, int relu, void* stream);
+int scflow_in_backward(const float* dy, const float* x, const float* scale, const float* shift,
+                       float* dx, double* partial, float* mm, int n, int hw, int c, int chunks,
+                       int relu, void* stream);
 /* scflow_gemm_f32: batched strided fp32 GEMM on the matrix cores (training-step contractions:
  * the correlation volume's backward, the 7x7 convs' dY^T.cols weight gradient, the pose head's
  * fully connected layers forward/backward; replaces torch.matmul / F.linear there,

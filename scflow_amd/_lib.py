@@ -135,6 +135,9 @@ SIGNATURES = {
     "scflow_corr_pyramid_tiled": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "scflow_corr_lookup_tiled": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_vp]),
+    "scflow_in_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_in_backward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
+                                   c_int, c_int, c_vp]),
     "scflow_debug_lookup_stamps": (c_int, [c_vp]),
     "scflow_debug_conv_stamps": (c_int, [c_vp]),
     "scflow_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),

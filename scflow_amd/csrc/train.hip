@@ -414,6 +414,122 @@ bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   return true;
 }
 
+// ---------------------------------------------------------------------------------------------
+// InstanceNorm2d(affine=False) (+ ReLU) forward / backward for the training step's feature
+// encoder (raft_encoder.py / resnet.py BasicBlock norms), channels-last x [n][hw][c], c % 4 == 0.
+// Statistics: scflow_enc_stats + scflow_enc_norm_finalize (fp64 partials) → scale = rstd,
+// shift = −mean·rstd, so x̂ = x·scale + shift.  Backward, with g = dy·[x̂ > 0 if relu]:
+//   dx = rstd · (g − mean_hw(g) − x̂ · mean_hw(g·x̂))
+// in three launches: fp64 partial sums of g and g·x̂ per (image, pixel chunk) in a fixed order,
+// their finalisation per (image, channel), and the elementwise dx.
+
+__global__ void in_apply_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                                const float* __restrict__ sh, float* __restrict__ y, int hw, int c,
+                                int relu, long long total4) {
+  const int c4 = c / 4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const int cq = (int)(i % c4) * 4;
+    const int img = (int)(i / c4 / hw);
+    const size_t so = (size_t)img * c + cq;
+    const floatx4 v = ((const floatx4*)x)[i];
+    const floatx4 a = *(const floatx4*)(sc + so), b = *(const floatx4*)(sh + so);
+    floatx4 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      r[e] = v[e] * a[e] + b[e];
+      if (relu) r[e] = fmaxf(r[e], 0.f);
+    }
+    ((floatx4*)y)[i] = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void in_bwd_stats_kernel(const float* __restrict__ dy,
+                                                           const float* __restrict__ x,
+                                                           const float* __restrict__ sc,
+                                                           const float* __restrict__ sh, int hw,
+                                                           int c, int chunks, int relu,
+                                                           double* __restrict__ partial) {
+  __shared__ double red[2][256][4];
+  const int img = blockIdx.y, ch = blockIdx.x;
+  const int tpp = c / 4, ppp = 256 / tpp;
+  const int q = threadIdx.x % tpp, ps = threadIdx.x / tpp;
+  const int p_begin = (int)((long long)hw * ch / chunks), p_end = (int)((long long)hw * (ch + 1) / chunks);
+  double s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (ps < ppp) {
+    const size_t so = (size_t)img * c + 4 * q;
+    const floatx4 a = *(const floatx4*)(sc + so), b = *(const floatx4*)(sh + so);
+    const size_t base = (size_t)img * hw * c + 4 * q;
+    for (int p = p_begin + ps; p < p_end; p += ppp) {
+      const floatx4 g = *(const floatx4*)(dy + base + (size_t)p * c);
+      const floatx4 v = *(const floatx4*)(x + base + (size_t)p * c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = v[e] * a[e] + b[e];
+        const float gg = relu && !(xh > 0.f) ? 0.f : g[e];
+        s[e] += (double)gg;
+        s2[e] += (double)gg * (double)xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][threadIdx.x][e] = s[e];
+    red[1][threadIdx.x][e] = s2[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < c) {
+    const int qq = threadIdx.x / 4, e = threadIdx.x % 4;
+    double a0 = 0, a1 = 0;
+    for (int k = 0; k < ppp; ++k) {
+      a0 += red[0][k * tpp + qq][e];
+      a1 += red[1][k * tpp + qq][e];
+    }
+    double* o = partial + (((size_t)img * chunks + ch) * 2) * c;
+    o[threadIdx.x] = a0;
+    o[c + threadIdx.x] = a1;
+  }
+}
+
+// m1 = mean(g), m2 = mean(g·x̂) per (image, channel), as floats into mm [n][2][c]
+__global__ void in_bwd_finalize_kernel(const double* __restrict__ partial, int n, int chunks, int c,
+                                       int hw, float* __restrict__ mm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * c) return;
+  const int img = i / c, ch = i % c;
+  double s = 0, s2 = 0;
+  for (int k = 0; k < chunks; ++k) {
+    const double* o = partial + (((size_t)img * chunks + k) * 2) * c;
+    s += o[ch];
+    s2 += o[c + ch];
+  }
+  mm[(size_t)img * 2 * c + ch] = (float)(s / hw);
+  mm[(size_t)img * 2 * c + c + ch] = (float)(s2 / hw);
+}
+
+__global__ void in_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                    const float* __restrict__ sc, const float* __restrict__ sh,
+                                    const float* __restrict__ mm, float* __restrict__ dx, int hw,
+                                    int c, int relu, long long total4) {
+  const int c4 = c / 4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const int cq = (int)(i % c4) * 4;
+    const int img = (int)(i / c4 / hw);
+    const size_t so = (size_t)img * c + cq;
+    const floatx4 g = ((const floatx4*)dy)[i], v = ((const floatx4*)x)[i];
+    const floatx4 a = *(const floatx4*)(sc + so), b = *(const floatx4*)(sh + so);
+    const floatx4 m1 = *(const floatx4*)(mm + (size_t)img * 2 * c + cq);
+    const floatx4 m2 = *(const floatx4*)(mm + (size_t)img * 2 * c + c + cq);
+    floatx4 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = v[e] * a[e] + b[e];
+      const float gg = relu && !(xh > 0.f) ? 0.f : g[e];
+      r[e] = a[e] * (gg - m1[e] - xh * m2[e]);
+    }
+    ((floatx4*)dx)[i] = r;
+  }
+}
+
 }  // namespace
 
 SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats) {
@@ -520,5 +636,36 @@ SCFLOW_API int scflow_corr_lookup_backward(const float* dout, int out_layout, in
     default:
       return SCFLOW_EUNSUPPORTED;
   }
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_in_apply(const float* x, const float* scale, const float* shift, float* y,
+                               int n, int hw, int c, int relu, void* stream) {
+  if (!x || !scale || !shift || !y || n <= 0 || hw <= 0 || c <= 0) return SCFLOW_EINVAL;
+  if (c % 4) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(x) || !aligned16(y) || !aligned16(scale) || !aligned16(shift)) return SCFLOW_EALIGN;
+  const long long total4 = (long long)n * hw * c / 4;
+  const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
+  in_apply_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, scale, shift, y, hw, c, relu ? 1 : 0, total4);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_in_backward(const float* dy, const float* x, const float* scale,
+                                  const float* shift, float* dx, double* partial, float* mm, int n,
+                                  int hw, int c, int chunks, int relu, void* stream) {
+  if (!dy || !x || !scale || !shift || !dx || !partial || !mm || n <= 0 || hw <= 0 || c <= 0 ||
+      chunks <= 0)
+    return SCFLOW_EINVAL;
+  if (c % 4 || c > 256) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(dy) || !aligned16(x) || !aligned16(dx) || !aligned16(scale) || !aligned16(shift) ||
+      !aligned16(mm))
+    return SCFLOW_EALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  in_bwd_stats_kernel<<<dim3(chunks, n), 256, 0, st>>>(dy, x, scale, shift, hw, c, chunks, relu ? 1 : 0,
+                                                       partial);
+  in_bwd_finalize_kernel<<<ceil_div((long long)n * c, 256), 256, 0, st>>>(partial, n, chunks, c, hw, mm);
+  const long long total4 = (long long)n * hw * c / 4;
+  const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
+  in_bwd_apply_kernel<<<blocks, 256, 0, st>>>(dy, x, scale, shift, mm, dx, hw, c, relu ? 1 : 0, total4);
   return scflow_launch_status();
 }

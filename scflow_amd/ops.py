@@ -723,6 +723,23 @@ def enc_instance_norm_stats(x: Tensor, n: int, hw: int, c: int, scale: Tensor, s
                                        _p(shift), _stream(x)), "scflow_enc_norm_finalize")
 
 
+def in_apply(x: Tensor, scale: Tensor, shift: Tensor, y: Tensor, n: int, hw: int, c: int,
+             relu: bool) -> None:
+    """y = act(x·scale + shift) per (image, channel) of channels-last x (scflow_in_apply)."""
+    _launch("scflow_in_apply", x, _p(x), _p(scale), _p(shift), _p(y), n, hw, c, int(bool(relu)))
+
+
+def in_backward(dy: Tensor, x: Tensor, scale: Tensor, shift: Tensor, dx: Tensor, n: int, hw: int,
+                c: int, relu: bool) -> None:
+    """InstanceNorm(+ReLU) backward (scflow_in_backward): dx from dy, the input x and its
+    scale/shift (rstd, −mean·rstd)."""
+    chunks = max(1, min(64, hw // 256))
+    partial = torch.empty(n * chunks * 2 * c, dtype=torch.float64, device=x.device)
+    mm = torch.empty(n * 2 * c, device=x.device)
+    _launch("scflow_in_backward", x, _p(dy), _p(x), _p(scale), _p(shift), _p(dx), _p(partial),
+            _p(mm), n, hw, c, chunks, int(bool(relu)))
+
+
 def enc_apply(x: Tensor, scale: Tensor, shift: Tensor, out: Tensor, n: int, hw: int, c: int,
               id: Optional[Tensor] = None, id_scale: Optional[Tensor] = None,
               id_shift: Optional[Tensor] = None) -> None:

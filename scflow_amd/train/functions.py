@@ -40,9 +40,33 @@ Tensor = torch.Tensor
 
 
 # ------------------------------------------------------------------------------- conv dispatch
+def _cached(w: Tensor, key: tuple, make):
+    """A form derived from weight ``w`` (packed for a kernel, flipped for dX), made once per
+    version of ``w`` and kept on the tensor object: a decoder weight is used in every refinement
+    iteration (8 forward and 8 dX launches per step) but changes only at the optimizer step (its
+    version counter moves).  Tensors made per step (the GRU's concatenated weights) carry their
+    cache with them and drop it when they die.  Not while a hipGraph is being captured: the
+    captured step must re-derive every form on replay (the weights move between replays)."""
+    if not w.is_cuda or torch.cuda.is_current_stream_capturing():
+        return make()
+    ver = w._version
+    cache = getattr(w, "_scflow_cache", None)
+    if cache is None or cache[0] != ver:
+        cache = (ver, {})
+        try:
+            w._scflow_cache = cache
+        except (AttributeError, RuntimeError):
+            return make()
+    v = cache[1].get(key)
+    if v is None:
+        v = cache[1][key] = make()
+    return v
+
+
 def _flip_t(w: Tensor) -> Tensor:
-    """[cout, cin, kh, kw] → [cin, cout, kh, kw] flipped in space (the dgrad weights)."""
-    return w.flip(2, 3).transpose(0, 1).contiguous()
+    """[cout, cin, kh, kw] → [cin, cout, kh, kw] flipped in space (the dgrad weights), cached per
+    version of ``w``."""
+    return _cached(w, ("flip_t",), lambda: w.detach().flip(2, 3).transpose(0, 1).contiguous())
 
 
 _ACT_FN = {None: lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Tanh": torch.tanh}
@@ -63,10 +87,12 @@ def _act_backward(dy: Tensor, y: Tensor, act: Optional[str]) -> Tensor:
 
 def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tensor], stride: int,
                   pad: Tuple[int, int], act: Optional[str] = None,
-                  bias_map: Optional[Tensor] = None) -> Tensor:
+                  bias_map: Optional[Tensor] = None, wkey: Optional[Tensor] = None) -> Tensor:
     """act(conv(cat[x0, x1]) + b + bias_map) of channels-last inputs on the HIP conv variant
     that supports the shape; act and bias_map are fused into the epilogue where the variant has
-    one, applied after it otherwise."""
+    one, applied after it otherwise.  ``wkey``: the weight tensor object whose version keys the
+    cached packed forms (default ``w``)."""
+    wkey = w if wkey is None else wkey
     n, h, wd, c0 = x0.shape
     c1 = 0 if x1 is None else x1.shape[-1]
     cin = c0 + c1
@@ -82,7 +108,8 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
     if lib_ok:
         bk = ops.conv_pick_bk(n, h, wd, c0, c1, cout, kh, kw, ph, pw, 1)
         try:
-            packed = ops.pack_conv_weight(w.float(), c0, c1, wd, 1, bk)
+            packed = _cached(wkey, ("conv", c0, c1, wd, bk),
+                             lambda: ops.pack_conv_weight(w.float(), c0, c1, wd, 1, bk))
             ops.conv2d(Chan.whole(x0.view(-1, c0)), packed, b, n, h, wd, cout, kh, kw, ph, pw, act,
                        out=Chan.whole(out.view(-1, cout)), bk=bk,
                        src1=None if x1 is None else Chan.whole(x1.view(-1, c1)),
@@ -95,7 +122,8 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
             and stride in (1, 2)):
         try:
             fuse = bias_map is None
-            ops.enc_conv(Chan.whole(x0.view(-1, c0)), ops.enc_conv_pack(w), b, n, h, wd, c0, cout, kh,
+            ops.enc_conv(Chan.whole(x0.view(-1, c0)), _cached(wkey, ("enc",), lambda: ops.enc_conv_pack(w)),
+                         b, n, h, wd, c0, cout, kh,
                          stride, ph, out, act=act if fuse else None,
                          src1=None if x1 is None else Chan.whole(x1.view(-1, c1)))
             post = not fuse
@@ -108,15 +136,17 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
             raise ScflowError(f"no HIP conv for kernel {kh}x{kw} pad {pad} stride {stride}")
         if cin == 3 and kh == 7 and stride in (1, 2) and cout <= 256 and cout != 192:
             # the encoder stem kernel (NCHW image in, channels-last out)
-            ops.enc_stem(x.permute(0, 3, 1, 2).contiguous(), ops.enc_stem_pack(w), b, cout, 7, stride,
+            ops.enc_stem(x.permute(0, 3, 1, 2).contiguous(),
+                         _cached(wkey, ("stem",), lambda: ops.enc_stem_pack(w)), b, cout, 7, stride,
                          ph, out)
         else:
-            if cin % 4:  # the gather conv reads float4 channel groups: zero-pad the channels
-                pad4 = 4 - cin % 4
+            pad4 = (4 - cin % 4) % 4
+            if pad4:  # the gather conv reads float4 channel groups: zero-pad the channels
                 x = F.pad(x, (0, pad4))
-                w = F.pad(w, (0, 0, 0, 0, 0, pad4))
                 cin += pad4
-            ops.ph_conv(Chan.whole(x.reshape(-1, cin)), None, ops.ph_conv_pack(w.contiguous()), b, n, h,
+            packed = _cached(wkey, ("ph", pad4), lambda: ops.ph_conv_pack(
+                (F.pad(w, (0, 0, 0, 0, 0, pad4)) if pad4 else w).contiguous()))
+            ops.ph_conv(Chan.whole(x.reshape(-1, cin)), None, packed, b, n, h,
                         wd, cout, kh, stride, ph, out.view(-1, cout))
     if post:
         if bias_map is not None:
@@ -151,38 +181,75 @@ class _Conv2dNHWC(torch.autograd.Function):
         x0 = x0.contiguous()
         x1 = None if x1 is None else x1.contiguous()
         y = _conv_forward(x0, x1, w.detach().contiguous(), None if b is None else b.detach().contiguous(),
-                          stride, (ph, pw), act, None if bias_map is None else bias_map.detach().contiguous())
+                          stride, (ph, pw), act, None if bias_map is None else bias_map.detach().contiguous(),
+                          wkey=w)
         ctx.save_for_backward(x0, x1, w, y if act is not None else None)
         ctx.stride, ctx.pad, ctx.has_b, ctx.act = stride, (ph, pw), b is not None, act
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x0, x1, w, y = ctx.saved_tensors
-        s, (ph, pw) = ctx.stride, ctx.pad
-        g = _act_backward(dy.contiguous(), y, ctx.act).contiguous()
-        n, h, wd, c0 = x0.shape
-        cout, cin, kh, kw = w.shape
-        _, oh, ow, _ = g.shape
-        dx0 = dx1 = dw = db = None
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-            if s == 1:
-                z = g
-            else:  # zero-insert onto the input grid: a transposed conv as a 'same' conv
-                z = torch.zeros(n, h, wd, cout, device=g.device)
-                z[:, 0:(oh - 1) * s + 1:s, 0:(ow - 1) * s + 1:s] = g
-            qh, qw = kh - 1 - ph, kw - 1 - pw  # dgrad padding
-            if s > 1:
-                qh, qw = (kh - 1) // 2, (kw - 1) // 2
-                if (kh - 1 - ph) != qh or (kw - 1 - pw) != qw:
-                    raise ScflowError("strided dgrad needs pad == (k-1)/2")
-            dx = _conv_forward(z, None, _flip_t(w.detach()), None, 1, (qh, qw))
-            dx0 = dx if x1 is None else dx[..., :c0]
-            dx1 = None if x1 is None else dx[..., c0:]
-        if ctx.needs_input_grad[2] or (ctx.has_b and ctx.needs_input_grad[3]):
-            dw, db = _weight_grad(g, x0, x1, w, s, ph, pw, ctx.has_b and ctx.needs_input_grad[3])
-        dbm = g if ctx.needs_input_grad[4] else None
-        return dx0, dx1, dw, db, dbm, None, None, None, None
+        return _conv_backward(ctx, dy)
+
+
+class _Conv2dNHWCSplit(torch.autograd.Function):
+    """``_Conv2dNHWC`` whose output channels come back as two tensors [..., :split], [..., split:]
+    (the GRU's z | r): their gradients are concatenated once in backward, instead of autograd
+    zero-filling a full-width buffer per slice and adding the two."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act, split):
+        y = _Conv2dNHWC.forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act)
+        ctx.split = split
+        ctx.cout = y.shape[-1]
+        return y[..., :split], y[..., split:]
+
+    @staticmethod
+    def backward(ctx, da, db_):
+        shape = list((da if da is not None else db_).shape)
+        parts = []
+        for g, c in ((da, ctx.split), (db_, ctx.cout - ctx.split)):
+            shape[-1] = c
+            parts.append(g.contiguous() if g is not None else
+                         torch.zeros(shape, device=(da if da is not None else db_).device))
+        return _conv_backward(ctx, torch.cat(parts, -1)) + (None,)
+
+
+def _conv_backward(ctx, dy):
+    """dX (the forward kernels on the flipped weights), dW / db (wgrad) and the bias-map gradient."""
+    x0, x1, w, y = ctx.saved_tensors
+    s, (ph, pw) = ctx.stride, ctx.pad
+    g = _act_backward(dy.contiguous(), y, ctx.act).contiguous()
+    n, h, wd, c0 = x0.shape
+    cout, cin, kh, kw = w.shape
+    _, oh, ow, _ = g.shape
+    dx0 = dx1 = dw = db = None
+    if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+        if s == 1:
+            z = g
+        else:  # zero-insert onto the input grid: a transposed conv as a 'same' conv
+            z = torch.zeros(n, h, wd, cout, device=g.device)
+            z[:, 0:(oh - 1) * s + 1:s, 0:(ow - 1) * s + 1:s] = g
+        qh, qw = kh - 1 - ph, kw - 1 - pw  # dgrad padding
+        if s > 1:
+            qh, qw = (kh - 1) // 2, (kw - 1) // 2
+            if (kh - 1 - ph) != qh or (kw - 1 - pw) != qw:
+                raise ScflowError("strided dgrad needs pad == (k-1)/2")
+        dx = _conv_forward(z, None, _flip_t(w), None, 1, (qh, qw))
+        dx0 = dx if x1 is None else dx[..., :c0]
+        dx1 = None if x1 is None else dx[..., c0:]
+    if ctx.needs_input_grad[2] or (ctx.has_b and ctx.needs_input_grad[3]):
+        dw, db = _weight_grad(g, x0, x1, w, s, ph, pw, ctx.has_b and ctx.needs_input_grad[3])
+    dbm = g if ctx.needs_input_grad[4] else None
+    return dx0, dx1, dw, db, dbm, None, None, None, None
+
+
+def conv2d_nhwc_split(x: Tensor, weight: Tensor, split: int, bias: Optional[Tensor] = None,
+                      stride: int = 1, padding=0, act: Optional[str] = None,
+                      x1: Optional[Tensor] = None, bias_map: Optional[Tensor] = None):
+    """``conv2d_nhwc`` returning (out[..., :split], out[..., split:])."""
+    ph, pw = (padding, padding) if isinstance(padding, int) else padding
+    return _Conv2dNHWCSplit.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act, split)
 
 
 def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride: int = 1,
@@ -193,6 +260,41 @@ def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride
     ``bias_map``: an [N, OH, OW, cout] tensor added before the activation."""
     ph, pw = (padding, padding) if isinstance(padding, int) else padding
     return _Conv2dNHWC.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act)
+
+
+# ------------------------------------------------------------------------------- norms
+class _InstanceNormNHWC(torch.autograd.Function):
+    """InstanceNorm2d(affine=False) (+ ReLU) of a channels-last [N, H, W, C] tensor on HIP kernels:
+    fp64 statistics (scflow_enc_stats), one apply pass, and a three-launch backward
+    (scflow_in_backward) — instead of torch's strided mean / var reductions and their autograd
+    graph over the channels-last layout."""
+
+    @staticmethod
+    def forward(ctx, x, eps, relu):
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        scale = torch.empty(n, c, device=x.device)
+        shift = torch.empty(n, c, device=x.device)
+        ops.enc_instance_norm_stats(x, n, h * w, c, scale, shift, eps)
+        y = torch.empty_like(x)
+        ops.in_apply(x, scale, shift, y, n, h * w, c, relu)
+        ctx.save_for_backward(x, scale, shift)
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, scale, shift = ctx.saved_tensors
+        n, h, w, c = x.shape
+        dx = torch.empty_like(x)
+        ops.in_backward(dy.contiguous(), x, scale, shift, dx, n, h * w, c, ctx.relu)
+        return dx, None, None
+
+
+def instance_norm_nhwc(x: Tensor, eps: float = 1e-5, relu: bool = False) -> Tensor:
+    """InstanceNorm2d(affine=False) (then ReLU if ``relu``) of channels-last x, HIP fwd + bwd
+    (channels a multiple of 4, at most 256)."""
+    return _InstanceNormNHWC.apply(x, float(eps), bool(relu))
 
 
 # ------------------------------------------------------------------------------- correlation

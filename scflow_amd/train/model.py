@@ -20,7 +20,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import conv2d_nhwc, corr_lookup, corr_pyramid, linear
+from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid,
+                        instance_norm_nhwc, linear)
 from .losses import filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
@@ -48,26 +49,31 @@ def _conv(x: Tensor, c) -> Tensor:
 
 
 # ------------------------------------------------------------------------------- encoders
-def _norm(x: Tensor, mod) -> Tensor:
-    """InstanceNorm2d (affine=False) or BatchNorm2d (train mode: batch statistics, running-stat
-    update) on a channels-last tensor."""
+def _norm(x: Tensor, mod, relu: bool = False) -> Tensor:
+    """InstanceNorm2d (affine=False; HIP statistics / apply / backward, the ReLU fused) or
+    BatchNorm2d (train mode: batch statistics, running-stat update) on a channels-last tensor."""
     if isinstance(mod, torch.nn.InstanceNorm2d):
+        c = x.shape[-1]
+        if x.is_cuda and c % 4 == 0 and c <= 256 and not mod.affine:
+            return instance_norm_nhwc(x, mod.eps, relu)
         m = x.mean(dim=(1, 2), keepdim=True)
         v = x.var(dim=(1, 2), unbiased=False, keepdim=True)
-        return (x - m) / torch.sqrt(v + mod.eps)
+        y = (x - m) / torch.sqrt(v + mod.eps)
+        return torch.relu(y) if relu else y
     y = F.batch_norm(x.permute(0, 3, 1, 2), mod.running_mean, mod.running_var, mod.weight, mod.bias,
                      training=mod.training, momentum=mod.momentum, eps=mod.eps)
     if mod.training and mod.num_batches_tracked is not None:
         mod.num_batches_tracked.add_(1)
-    return y.permute(0, 2, 3, 1)
+    y = y.permute(0, 2, 3, 1)
+    return torch.relu(y) if relu else y
 
 
 def encoder_train(enc, x_nhwc: Tensor) -> Tensor:
     """RAFTEncoder.forward (raft_encoder.py:286-314) with autograd; channels-last in and out."""
-    x = torch.relu(_norm(_conv(x_nhwc, enc.conv1), enc.norm1))
+    x = _norm(_conv(x_nhwc, enc.conv1), enc.norm1, relu=True)
     for name in enc.res_layers:
         for blk in getattr(enc, name):
-            out = torch.relu(_norm(_conv(x, blk.conv1), blk.norm1))
+            out = _norm(_conv(x, blk.conv1), blk.norm1, relu=True)
             out = _norm(_conv(out, blk.conv2), blk.norm2)
             ident = x if blk.downsample is None else _norm(_conv(x, blk.downsample[0]), blk.downsample[1])
             x = torch.relu(out + ident)
@@ -179,8 +185,8 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
             out = _cm(out, m)
         motion = torch.cat([out, f2], -1)
         for (w_zr, w_q, pad), (pre_zr, pre_q) in zip(it_w, ctx_pre):  # SeqConv: 1×5 then 5×1
-            zr = conv2d_nhwc(h, w_zr, None, 1, pad, act="Sigmoid", x1=motion, bias_map=pre_zr)
-            z, rg = zr[..., :hc], zr[..., hc:]
+            z, rg = conv2d_nhwc_split(h, w_zr, hc, None, 1, pad, act="Sigmoid", x1=motion,
+                                      bias_map=pre_zr)
             qq = conv2d_nhwc(rg * h, w_q, None, 1, pad, act="Tanh", x1=motion, bias_map=pre_q)
             h = torch.lerp(h, qq, z)  # (1 − z)·h + z·q
         fh = h

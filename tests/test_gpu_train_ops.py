@@ -1,6 +1,7 @@
 """GPU: training-step autograd Functions (HIP forward + backward) against CPU autograd of the
 plain torch ops (fp64) — convolution (every variant the path uses, strides 1 and 2), the
-correlation pyramid and the pyramid lookup (adjoint of CorrLookup, corr_lookup.py:102-136)."""
+correlation pyramid, the pyramid lookup (adjoint of CorrLookup, corr_lookup.py:102-136), the
+feature encoder's InstanceNorm (+ ReLU) and the GRU's split-output z | r conv."""
 import numpy as np
 import pytest
 import torch
@@ -195,3 +196,48 @@ def test_gemm_f32_strided(bt, M, N, K, ta, tb):
         o2 = ops.gemm(A[0].cuda(), B[0].cuda())
         torch.testing.assert_close(o2.cpu().double(), torch.matmul(A[0].double(), B[0].double()),
                                    rtol=1e-5, atol=1e-4 * max(1.0, K / 256) ** 0.5)
+
+
+@pytest.mark.parametrize("n,h,w,c,relu", [(4, 64, 64, 64, True), (3, 32, 32, 96, False),
+                                          (2, 16, 16, 128, True), (2, 8, 12, 4, False)])
+def test_instance_norm_nhwc_forward_backward(n, h, w, c, relu):
+    """HIP InstanceNorm2d(affine=False) (+ ReLU): output and input gradient against fp64 autograd
+    of F.instance_norm on the same channels-last data."""
+    from scflow_amd.train.functions import instance_norm_nhwc
+    g = torch.Generator().manual_seed(31)
+    x = (torch.randn(n, h, w, c, generator=g) * 2 + 0.5)
+    dy = torch.randn(n, h, w, c, generator=g)
+    xr = x.double().requires_grad_(True)
+    yr = F.instance_norm(xr.permute(0, 3, 1, 2), eps=1e-5).permute(0, 2, 3, 1)
+    if relu:
+        yr = torch.relu(yr)
+    (yr * dy.double()).sum().backward()
+    xg = x.cuda().requires_grad_(True)
+    y = instance_norm_nhwc(xg, 1e-5, relu)
+    (y * dy.cuda()).sum().backward()
+    _close(y, yr, 1e-5, 1e-5, "instance norm forward")
+    _close(xg.grad, xr.grad, 1e-4, 1e-5, "instance norm input gradient")
+
+
+def test_conv2d_nhwc_split_matches_whole():
+    """The split-output conv (GRU z | r) gives the whole conv's outputs and the same gradients,
+    including when one half receives no gradient."""
+    from scflow_amd.train.functions import conv2d_nhwc, conv2d_nhwc_split
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(2, 32, 32, 128, generator=g).cuda()
+    x1 = torch.randn(2, 32, 32, 128, generator=g).cuda()
+    w = (torch.randn(256, 256, 1, 5, generator=g) * 0.05).cuda()
+    for use_r in (True, False):
+        ws = w.clone().requires_grad_(True)
+        wc = w.clone().requires_grad_(True)
+        xs = x.clone().requires_grad_(True)
+        xc = x.clone().requires_grad_(True)
+        z, r = conv2d_nhwc_split(xs, ws, 128, None, 1, (0, 2), act="Sigmoid", x1=x1)
+        y = conv2d_nhwc(xc, wc, None, 1, (0, 2), act="Sigmoid", x1=x1)
+        assert torch.equal(z, y[..., :128]) and torch.equal(r, y[..., 128:])
+        loss_s = (z * 1.5).sum() + ((r * r).sum() if use_r else 0)
+        loss_c = (y[..., :128] * 1.5).sum() + ((y[..., 128:] ** 2).sum() if use_r else 0)
+        loss_s.backward()
+        loss_c.backward()
+        _close(xs.grad, xc.grad, 1e-6, 1e-7, "split conv dX")
+        _close(ws.grad, wc.grad, 1e-6, 1e-7, "split conv dW")

@@ -29,6 +29,10 @@ def _patch_torch_ops(monkeypatch):
             y = y + bias_map
         return {None: y, "ReLU": torch.relu(y), "Sigmoid": torch.sigmoid(y), "Tanh": torch.tanh(y)}[act]
 
+    def conv_split(x, w, split, b=None, stride=1, padding=0, act=None, x1=None, bias_map=None):
+        y = conv(x, w, b, stride, padding, act, x1, bias_map)
+        return y[..., :split], y[..., split:]
+
     def pyramid(f1, f2, L=4):
         return orc.corr_pyramid(f1, f2, L)
 
@@ -51,6 +55,7 @@ def _patch_torch_ops(monkeypatch):
         out0.buf.view(-1, out0.buf.shape[-1])[:, out0.off:out0.off + 2] = f.permute(0, 2, 3, 1).reshape(-1, 2)
 
     monkeypatch.setattr(model, "conv2d_nhwc", conv)
+    monkeypatch.setattr(model, "conv2d_nhwc_split", conv_split)
     monkeypatch.setattr(model, "linear", F.linear)
     monkeypatch.setattr(model, "corr_pyramid", pyramid)
     monkeypatch.setattr(model, "corr_lookup", lookup)
