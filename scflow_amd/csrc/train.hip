@@ -333,45 +333,58 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
   }
 }
 
-// Σ over the splits, fixed order.  Block = one (co, tap) row × 64 ci: 4 groups of 64 threads
-// each sum every 4th split (independent loads in flight), then an LDS reduction of the 4.
+// Σ over the splits, fixed order.  Workgroup = 256/G consecutive slab entries (a run of one
+// (co, tap) row's ci) × G lanes of partial sums (G = 2^lg ≤ 16 ≈ splits/4: lane k sums splits
+// k, k+G, …, two loads in flight), then the G partials in order through LDS.  The bias slab
+// rides along as the last, row-less workgroups.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
     const float* __restrict__ slab, const float* __restrict__ bslab, float* __restrict__ dw,
     float* __restrict__ db, int splits, int cout, int cin, int taps, int copad, int cinp,
-    int accumulate) {
-  __shared__ float part[4][64];
-  const int cblocks = cinp / 64;
-  const int row = blockIdx.x / cblocks;            // co * taps + t
-  const int ci = (blockIdx.x % cblocks) * 64 + (threadIdx.x & 63);
-  const int grp = threadIdx.x >> 6;
+    int accumulate, int lg) {
+  __shared__ float part[256];
+  const int G = 1 << lg, OPB = 256 >> lg;
+  const int o = threadIdx.x & (OPB - 1), k = threadIdx.x >> (8 - lg);
+  const long long wtot = (long long)cout * taps * cinp;
+  const long long nw = (wtot + OPB - 1) / OPB;  // weight blocks; then bias blocks
+  const bool wblk = blockIdx.x < nw;
   const size_t sstride = (size_t)copad * taps * cinp;
-  const bool bias_row = db && row < cout && blockIdx.x % cblocks == 0;
-  if (row < cout * taps) {
-    const float* src = slab + (size_t)row * cinp + ci;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int k = grp;
-    for (; k + 12 < splits; k += 16) {  // 4 independent loads in flight per thread
-      s0 += src[k * sstride];
-      s1 += src[(k + 4) * sstride];
-      s2 += src[(k + 8) * sstride];
-      s3 += src[(k + 12) * sstride];
+  long long i;
+  const float* src;
+  size_t step;
+  bool valid;
+  if (wblk) {
+    i = (long long)blockIdx.x * OPB + o;  // = row·cinp + ci
+    src = slab + i;
+    step = sstride;
+    valid = i < wtot && (int)(i % cinp) < cin;
+  } else {
+    i = (long long)(blockIdx.x - nw) * OPB + o;  // channel
+    src = bslab + i;
+    step = (size_t)copad;
+    valid = i < cout;
+  }
+  float s0 = 0.f, s1 = 0.f;
+  if (valid) {
+    int b = k;
+    for (; b + G < splits; b += 2 * G) {
+      s0 += src[b * step];
+      s1 += src[(b + G) * step];
     }
-    for (; k < splits; k += 4) s0 += src[k * sstride];
-    s0 = (s0 + s1) + (s2 + s3);
-    s1 = 0.f;
-    part[grp][threadIdx.x & 63] = s0 + s1;
+    if (b < splits) s0 += src[b * step];
   }
+  part[threadIdx.x] = s0 + s1;
   __syncthreads();
-  if (grp == 0 && row < cout * taps && ci < cin) {
-    const float s = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
-    const int co = row / taps, t = row % taps;
-    float* d = dw + ((size_t)co * cin + ci) * taps + t;
-    *d = accumulate ? *d + s : s;
-  }
-  if (bias_row && threadIdx.x == 64) {  // bias of channel `row` (rows < cout exist as taps ≥ 1)
+  if (k == 0 && valid) {
     float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += bslab[(size_t)k * copad + row];
-    db[row] = accumulate ? db[row] + s : s;
+    for (int j = 0; j < G; ++j) s += part[j * OPB + o];
+    if (wblk) {
+      const int row = (int)(i / cinp), ci = (int)(i % cinp);
+      const int co = row / taps, t = row % taps;
+      float* d = dw + ((size_t)co * cin + ci) * taps + t;
+      *d = accumulate ? *d + s : s;
+    } else {
+      db[i] = accumulate ? db[i] + s : s;
+    }
   }
 }
 
@@ -401,17 +414,243 @@ bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   const int ci_tiles = (cin + WT - 1) / WT;
   P->copad = P->co_tiles * WT;
   P->cinp = ci_tiles * WT;
-  // split the pixel reduction until the grid fills the CUs once at the kernel's occupancy,
-  // each split ≥ 8 chunks (the slab traffic is splits × the weight size)
+  // split the pixel reduction until the grid fills the CUs once at the kernel's occupancy
   const int tiles = P->co_tiles * ci_tiles;
   const int occ = a.kh * a.kw >= 9 ? 1 : 2;  // the kernel's resident workgroups per CU
   int want = (occ * device_cus() + tiles - 1) / tiles;
-  int maxs = P->nchunks / 8 > 0 ? P->nchunks / 8 : 1;
-  if (want > maxs) want = maxs;
+  // ≥ 8 chunks per split, unless that leaves CUs idle: then down to one chunk per split until
+  // every CU has a workgroup, while the partial slabs (splits × the padded weight size, written
+  // and read once more by the reduction) stay under 8 Mi floats
+  long long maxs = P->nchunks / 8 > 0 ? P->nchunks / 8 : 1;
+  if ((long long)tiles * maxs < device_cus()) {
+    const long long per_split = (long long)P->copad * a.kh * a.kw * P->cinp;
+    long long m = (device_cus() + tiles - 1) / tiles;
+    if (m > P->nchunks) m = P->nchunks;
+    if (m > (8ll << 20) / per_split) m = (8ll << 20) / per_split;
+    if (m > maxs) maxs = m;
+  }
+  if (want > maxs) want = (int)maxs;
   if (want < 1) want = 1;
   P->cps = (P->nchunks + want - 1) / want;
   *splits = (P->nchunks + P->cps - 1) / P->cps;
   return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Thin weight gradients: one side of the conv at most 4 channels (the flow / mask predictors'
+// 256→2 / 256→1, the mask encoder's 1→64 input; kernels up to 5×5).  On the 64×64 MFMA
+// tile such a shape wastes ≥ 16/17 of every matrix op and its grid is a handful of workgroups;
+// here it is a plain fp32 reduction over the pixels.  The WIDE side (C ≤ 256 channels, C % 4
+// == 0) is spread over the lanes as float4 groups g; the lanes that share a group are pixel
+// streams st.  A workgroup owns a run of ppb output pixels and one kernel row ty (grid.y), and
+// keeps T (thin channels) × KW (taps of the row) × 4 (the float4) fp32 accumulators per lane:
+//   THIN_CO (cout ≤ T): acc[co][tx][e] += dy[p][co]       · x[p + (ty, tx)][4g + e]
+//   !THIN_CO (cin ≤ T): acc[ci][tx][e] += dy[p][4g + e]   · x[p + (ty, tx)][ci]
+// The streams are summed through LDS in a fixed order and each workgroup writes its partial
+// dw (torch layout) to a slab row; wthin_reduce_kernel sums the rows in a fixed order.
+struct WtParams {
+  scflow_wgrad_args a;
+  int oh, ow, cin, C, G, lg2, ppb, nbp, thin_co;
+};
+
+bool wthin_geometry(const scflow_wgrad_args& a, WtParams* P) {
+  static const bool off = [] {
+    const char* e = getenv("SCFLOW_WGRAD_THIN");
+    return e && e[0] == '0';
+  }();
+  if (off) return false;
+  const int cin = a.cin0 + a.cin1;
+  // 7×7 (the stem, the flow encoders' 2→128) stays on im2col + GEMM: measured faster there
+  if (a.kw != 1 && a.kw != 3 && a.kw != 5) return false;
+  if (a.kh < 1 || a.kh > 5 || a.stride < 1 || a.stride > 2) return false;
+  const bool thin_co = a.cout <= 4 && cin % 4 == 0 && a.cin0 % 4 == 0 && cin <= 256 &&
+                       a.s0 % 4 == 0 && aligned16(a.src0) &&
+                       (a.cin1 == 0 || (a.s1 % 4 == 0 && aligned16(a.src1)));
+  const bool thin_ci = !thin_co && cin <= 4 && a.cin1 == 0 && a.cout % 4 == 0 && a.cout <= 256 &&
+                       a.sdy % 4 == 0 && aligned16(a.dy);
+  if (!thin_co && !thin_ci) return false;
+  P->a = a;
+  P->cin = cin;
+  P->oh = (a.h + 2 * a.ph - a.kh) / a.stride + 1;
+  P->ow = (a.w + 2 * a.pw - a.kw) / a.stride + 1;
+  if (P->oh <= 0 || P->ow <= 0) return false;
+  P->thin_co = thin_co;
+  P->C = thin_co ? cin : a.cout;
+  P->G = P->C / 4;
+  P->lg2 = 0;
+  while ((1 << P->lg2) < P->G) ++P->lg2;
+  const long long pix = (long long)a.n * P->oh * P->ow;
+  // ≥ 64 pixels per workgroup, at most 512 workgroups per kernel row (the slab rows)
+  long long ppb = (pix + 511) / 512;
+  if (ppb < 64) ppb = 64;
+  P->ppb = (int)ppb;
+  P->nbp = (int)((pix + ppb - 1) / ppb);
+  return true;
+}
+
+template <int T, int KW, bool THIN_CO>
+__global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __restrict__ slab,
+                                                         float* __restrict__ bslab) {
+  constexpr int NA = T * KW * 4 + 4;  // accumulators + 4 bias partials
+  __shared__ float red[256][17];
+  const scflow_wgrad_args& a = P.a;
+  const int tid = threadIdx.x;
+  const int G2 = 1 << P.lg2, S = 256 >> P.lg2;
+  const int g = tid & (G2 - 1), st = tid >> P.lg2;
+  const bool act = g < P.G;
+  const int ty = blockIdx.y;
+  const long long ohw = (long long)P.oh * P.ow;
+  const long long pix = a.n * ohw;
+  const long long pb0 = (long long)blockIdx.x * P.ppb;
+  const long long pb1 = pb0 + P.ppb < pix ? pb0 + P.ppb : pix;
+  const int tn = THIN_CO ? a.cout : P.cin;  // thin channels actually present
+  float acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = 0.f;
+  const int c4 = 4 * g;
+  if (act) {
+#pragma unroll 2
+    for (long long p = pb0 + st; p < pb1; p += S) {
+      const int img = (int)(p / ohw);
+      const int rem = (int)(p - img * ohw);
+      const int oy = rem / P.ow, ox = rem - oy * P.ow;
+      const int iy = oy * a.stride - a.ph + ty;
+      const bool rok = iy >= 0 && iy < a.h;
+      const size_t rowpix = ((size_t)img * a.h + iy) * a.w;
+      if (THIN_CO) {
+        float d[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) d[t] = t < tn ? a.dy[p * a.sdy + t] : 0.f;
+#pragma unroll
+        for (int t = 0; t < T; ++t) acc[T * KW * 4 + t] += d[t];
+#pragma unroll
+        for (int tx = 0; tx < KW; ++tx) {
+          const int ix = ox * a.stride - a.pw + tx;
+          floatx4 v = {0.f, 0.f, 0.f, 0.f};
+          if (rok && ix >= 0 && ix < a.w) {
+            const size_t q = rowpix + ix;
+            v = c4 < a.cin0 ? *(const floatx4*)(a.src0 + q * a.s0 + c4)
+                            : *(const floatx4*)(a.src1 + q * a.s1 + (c4 - a.cin0));
+          }
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[(t * KW + tx) * 4 + e] += d[t] * v[e];
+        }
+      } else {
+        const floatx4 d = *(const floatx4*)(a.dy + p * a.sdy + c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[T * KW * 4 + e] += d[e];
+#pragma unroll
+        for (int tx = 0; tx < KW; ++tx) {
+          const int ix = ox * a.stride - a.pw + tx;
+          const bool ok = rok && ix >= 0 && ix < a.w;
+          const size_t q = rowpix + ix;
+#pragma unroll
+          for (int t = 0; t < T; ++t) {
+            const float xv = ok && t < tn ? a.src0[q * a.s0 + t] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[(t * KW + tx) * 4 + e] += d[e] * xv;
+          }
+        }
+      }
+    }
+  }
+  // Σ over the streams (fixed order), 16 accumulators per round; lanes st == 0 write the row
+  const int taps = a.kh * a.kw;
+  float* row = slab + (size_t)blockIdx.x * a.cout * P.cin * taps;
+#pragma unroll
+  for (int r0 = 0; r0 < NA; r0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (r0 + j < NA) red[tid][j] = acc[r0 + j];
+    __syncthreads();
+    if (st == 0 && act) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int i = r0 + j;
+        if (i >= NA) break;
+        float s = 0.f;
+        for (int k = 0; k < S; ++k) s += red[k * G2 + g][j];
+        if (i < T * KW * 4) {
+          const int e = i & 3, tx = (i >> 2) % KW, t = (i >> 2) / KW;
+          if (t < tn) {
+            const int co = THIN_CO ? t : c4 + e, ci = THIN_CO ? c4 + e : t;
+            row[((size_t)co * P.cin + ci) * taps + ty * a.kw + tx] = s;
+          }
+        } else if (bslab && ty == 0) {
+          const int e = i - T * KW * 4;
+          if (THIN_CO) {
+            if (g == 0 && e < tn) bslab[(size_t)blockIdx.x * a.cout + e] = s;
+          } else {
+            bslab[(size_t)blockIdx.x * a.cout + c4 + e] = s;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dst[i] (+)= Σ_b slab[b][i], b in order: 16 outputs × 16 lanes of partial sums per workgroup
+__global__ __launch_bounds__(256) void wthin_reduce_kernel(const float* __restrict__ slab, int nb,
+                                                           long long total, float* __restrict__ dst,
+                                                           int accumulate) {
+  __shared__ float part[16][17];
+  const int o = threadIdx.x & 15, k = threadIdx.x >> 4;
+  const long long i = (long long)blockIdx.x * 16 + o;
+  float s0 = 0.f, s1 = 0.f;
+  if (i < total) {
+    int b = k;
+    for (; b + 16 < nb; b += 32) {
+      s0 += slab[(size_t)b * total + i];
+      s1 += slab[(size_t)(b + 16) * total + i];
+    }
+    if (b < nb) s0 += slab[(size_t)b * total + i];
+  }
+  part[k][o] = s0 + s1;
+  __syncthreads();
+  if (k == 0 && i < total) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += part[j][o];
+    dst[i] = accumulate ? dst[i] + s : s;
+  }
+}
+
+long long wthin_workspace(const WtParams& P) {
+  const scflow_wgrad_args& a = P.a;
+  return (long long)P.nbp * a.cout * P.cin * a.kh * a.kw + (long long)P.nbp * a.cout;
+}
+
+int wthin_launch(const WtParams& P, hipStream_t st) {
+  const scflow_wgrad_args& a = P.a;
+  const bool thin_co = P.thin_co != 0;
+  const int tn = thin_co ? a.cout : P.cin;
+  float* slab = a.workspace;
+  const long long total = (long long)a.cout * P.cin * a.kh * a.kw;
+  float* bslab = a.db ? a.workspace + (size_t)P.nbp * total : nullptr;
+  const dim3 grid((unsigned)P.nbp, (unsigned)a.kh);
+#define SCFLOW_WT(T_, KW_)                                                                   \
+  if (a.kw == KW_ && tn <= T_) {                                                             \
+    if (thin_co)                                                                             \
+      wgrad_thin_kernel<T_, KW_, true><<<grid, 256, 0, st>>>(P, slab, bslab);                \
+    else                                                                                     \
+      wgrad_thin_kernel<T_, KW_, false><<<grid, 256, 0, st>>>(P, slab, bslab);               \
+  } else
+  SCFLOW_WT(1, 1) SCFLOW_WT(2, 1) SCFLOW_WT(4, 1)
+  SCFLOW_WT(1, 3) SCFLOW_WT(2, 3) SCFLOW_WT(4, 3)
+  SCFLOW_WT(1, 5) SCFLOW_WT(2, 5) SCFLOW_WT(4, 5)
+  return SCFLOW_EUNSUPPORTED;
+#undef SCFLOW_WT
+  int rc = scflow_launch_status();
+  if (rc != SCFLOW_OK) return rc;
+  wthin_reduce_kernel<<<(unsigned)((total + 15) / 16), 256, 0, st>>>(slab, P.nbp, total, a.dw,
+                                                                     a.accumulate);
+  if (a.db)
+    wthin_reduce_kernel<<<(unsigned)((a.cout + 15) / 16), 256, 0, st>>>(bslab, P.nbp, a.cout, a.db,
+                                                                         a.accumulate);
+  return scflow_launch_status();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -534,6 +773,11 @@ __global__ void in_bwd_apply_kernel(const float* __restrict__ dy, const float* _
 
 SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats) {
   if (!args || !floats) return SCFLOW_EINVAL;
+  WtParams Q;
+  if (wthin_geometry(*args, &Q)) {
+    *floats = wthin_workspace(Q);
+    return SCFLOW_OK;
+  }
   WgParams P;
   int splits = 0;
   if (!wgrad_geometry(*args, &P, &splits)) return SCFLOW_EUNSUPPORTED;
@@ -549,6 +793,11 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
       a.cout <= 0 || a.cin0 <= 0 || a.cin1 < 0 || (a.cin1 > 0 && !a.src1) || a.sdy < a.cout ||
       a.s0 < a.cin0 || (a.cin1 > 0 && a.s1 < a.cin1) || a.ph < 0 || a.pw < 0)
     return SCFLOW_EINVAL;
+  WtParams Q;
+  if (wthin_geometry(a, &Q)) {
+    if (a.workspace_floats < wthin_workspace(Q)) return SCFLOW_EINVAL;
+    return wthin_launch(Q, (hipStream_t)stream);
+  }
   WgParams P;
   int splits = 0;
   if (!wgrad_geometry(a, &P, &splits)) return SCFLOW_EUNSUPPORTED;
@@ -586,9 +835,14 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
 #undef SCFLOW_WG
   int rc = scflow_launch_status();
   if (rc != SCFLOW_OK) return rc;
-  const unsigned rblocks = (unsigned)((long long)a.cout * taps * (P.cinp / WT));
+  int lg = 0;  // 2^lg lanes of partial sums per output, ≈ splits / 4 of them, ≤ 16
+  while (lg < 4 && (4 << lg) < splits) ++lg;
+  const int opb = 256 >> lg;
+  const unsigned rblocks = (unsigned)(((long long)a.cout * taps * P.cinp + opb - 1) / opb +
+                                      (a.db ? (a.cout + opb - 1) / opb : 0));
   wgrad_reduce_kernel<<<rblocks, 256, 0, st>>>(slab, bslab, a.dw, a.db, splits, a.cout,
-                                               a.cin0 + a.cin1, taps, P.copad, P.cinp, a.accumulate);
+                                               a.cin0 + a.cin1, taps, P.copad, P.cinp, a.accumulate,
+                                               lg);
   return scflow_launch_status();
 }
 

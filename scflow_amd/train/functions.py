@@ -40,15 +40,43 @@ Tensor = torch.Tensor
 
 
 # ------------------------------------------------------------------------------- conv dispatch
+_CAPTURE_CACHE: Optional[dict] = None
+
+
+class capture_cache:
+    """Scope of a hipGraph capture of the forward + backward: inside it each derived weight form
+    is made once per capture (the first use records the pack kernel, later uses in the same
+    replay read its output), never taken from or left in the eager per-version cache — the
+    weights move between replays, so a form made outside the graph would be stale in it."""
+
+    def __enter__(self):
+        global _CAPTURE_CACHE
+        _CAPTURE_CACHE = {}
+        return self
+
+    def __exit__(self, *exc):
+        global _CAPTURE_CACHE
+        _CAPTURE_CACHE = None
+        return False
+
+
 def _cached(w: Tensor, key: tuple, make):
     """A form derived from weight ``w`` (packed for a kernel, flipped for dX), made once per
     version of ``w`` and kept on the tensor object: a decoder weight is used in every refinement
     iteration (8 forward and 8 dX launches per step) but changes only at the optimizer step (its
     version counter moves).  Tensors made per step (the GRU's concatenated weights) carry their
-    cache with them and drop it when they die.  Not while a hipGraph is being captured: the
-    captured step must re-derive every form on replay (the weights move between replays)."""
-    if not w.is_cuda or torch.cuda.is_current_stream_capturing():
+    cache with them and drop it when they die.  While a hipGraph is being captured the forms
+    live in the capture's own cache (``capture_cache``), or are re-made per use outside one."""
+    if not w.is_cuda:
         return make()
+    if torch.cuda.is_current_stream_capturing():
+        if _CAPTURE_CACHE is None:
+            return make()
+        k = (id(w), w._version) + key
+        hit = _CAPTURE_CACHE.get(k)
+        if hit is None:
+            hit = _CAPTURE_CACHE[k] = (w, make())  # w kept alive so its id stays unique
+        return hit[1]
     ver = w._version
     cache = getattr(w, "_scflow_cache", None)
     if cache is None or cache[0] != ver:
@@ -63,10 +91,45 @@ def _cached(w: Tensor, key: tuple, make):
     return v
 
 
-def _flip_t(w: Tensor) -> Tensor:
-    """[cout, cin, kh, kw] → [cin, cout, kh, kw] flipped in space (the dgrad weights), cached per
-    version of ``w``."""
-    return _cached(w, ("flip_t",), lambda: w.detach().flip(2, 3).transpose(0, 1).contiguous())
+def _flip_t(w: Tensor, pad_co: int = 0) -> Tensor:
+    """[cout, cin, kh, kw] → [cin, cout (+ pad_co zero channels), kh, kw] flipped in space (the
+    dgrad weights), cached per version of ``w``."""
+    def make():
+        f = w.detach().flip(2, 3).transpose(0, 1)
+        return (F.pad(f, (0, 0, 0, 0, 0, pad_co)) if pad_co else f).contiguous()
+    return _cached(w, ("flip_t", pad_co), make)
+
+
+_DIRECT_WGRAD = False
+
+
+class direct_weight_grads:
+    """Scope in which a conv's backward adds its weight / bias gradient straight into the leaf
+    parameters' existing ``.grad`` buffers (scflow_conv_wgrad accumulate = 1) and hands autograd
+    no gradient for them — instead of a fresh dW per use, autograd summing a decoder weight's 8
+    per-iteration gradients and AccumulateGrad adding the sum.  Only for parameters whose
+    ``.grad`` is already allocated (GradBuckets' flat views) and when nothing observes their
+    accumulation (no post-accumulate-grad hooks: TrainStep without ``overlap``)."""
+
+    def __enter__(self):
+        global _DIRECT_WGRAD
+        self._prev, _DIRECT_WGRAD = _DIRECT_WGRAD, True
+        return self
+
+    def __exit__(self, *exc):
+        global _DIRECT_WGRAD
+        _DIRECT_WGRAD = self._prev
+        return False
+
+
+def _grad_sink(t: Optional[Tensor]) -> Optional[Tensor]:
+    """t.grad when gradients of leaf ``t`` may be added into it directly, else None."""
+    if t is None or not _DIRECT_WGRAD or not t.is_leaf or not t.requires_grad:
+        return None
+    gr = t.grad
+    if gr is None or not gr.is_contiguous() or gr.dtype != torch.float32:
+        return None
+    return gr
 
 
 _ACT_FN = {None: lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Tanh": torch.tanh}
@@ -156,17 +219,38 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
 
 
 def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int, ph: int, pw: int,
-                 with_bias: bool) -> Tuple[Tensor, Optional[Tensor]]:
+                 with_bias: bool, dw: Optional[Tensor] = None,
+                 db: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """(dW, db) of the conv; given ``dw`` (and ``db`` when with_bias) the gradients are ADDED
+    into them (and returned)."""
     n, h, wd, c0 = x0.shape
     cout, cin, kh, kw = w.shape
-    dw = torch.empty(cout, cin, kh, kw, device=g.device)
-    db = torch.empty(cout, device=g.device) if with_bias else None
-    g2 = g.view(-1, cout)
+    accumulate = dw is not None
+    if not accumulate:
+        dw = torch.empty(cout, cin, kh, kw, device=g.device)
+        db = torch.empty(cout, device=g.device) if with_bias else None
+    g2 = g.reshape(-1, g.shape[-1])
+    if g.shape[-1] != cout:  # output channels zero-padded to a multiple of 4 (see _conv_backward)
+        dwp = torch.empty(g.shape[-1], cin, kh, kw, device=g.device)
+        dbp = torch.empty(g.shape[-1], device=g.device) if with_bias else None
+        ops.conv_wgrad(g2, x0, x1, dwp, dbp, n, h, wd, kh, kw, s, ph, pw)
+        if accumulate:
+            dw += dwp[:cout]
+            if with_bias:
+                db += dbp[:cout]
+            return dw, db
+        return dwp[:cout], (dbp[:cout] if with_bias else None)
     try:
-        ops.conv_wgrad(g2, x0, x1, dw, db, n, h, wd, kh, kw, s, ph, pw)
+        ops.conv_wgrad(g2, x0, x1, dw, db, n, h, wd, kh, kw, s, ph, pw, accumulate=accumulate)
         return dw, db
     except ScflowError:
         pass
+    if accumulate:
+        gw, gb = _weight_grad(g, x0, x1, w, s, ph, pw, with_bias)
+        dw += gw
+        if with_bias:
+            db += gb
+        return dw, db
     # shapes outside the wgrad kernel (7×7): HIP im2col + one HIP GEMM
     x = x0 if x1 is None else torch.cat([x0, x1], -1)
     cols = ops.im2col(x.contiguous(), n, h, wd, cin, kh, kw, s, ph, pw)
@@ -185,6 +269,7 @@ class _Conv2dNHWC(torch.autograd.Function):
                           wkey=w)
         ctx.save_for_backward(x0, x1, w, y if act is not None else None)
         ctx.stride, ctx.pad, ctx.has_b, ctx.act = stride, (ph, pw), b is not None, act
+        ctx.bias = b  # the leaf itself (direct gradient accumulation), not saved data
         return y
 
     @staticmethod
@@ -224,23 +309,33 @@ def _conv_backward(ctx, dy):
     cout, cin, kh, kw = w.shape
     _, oh, ow, _ = g.shape
     dx0 = dx1 = dw = db = None
+    dbm = g if ctx.needs_input_grad[4] else None
+    # output channels not a multiple of 4 (out_net's 126): zero-pad dY so dgrad reads whole float4
+    # channel groups (the Winograd / MFMA variants) and wgrad stays on its vector path
+    pad_co = (-cout) % 4 if cout > 4 else 0
+    gp = F.pad(g, (0, pad_co)) if pad_co else g
     if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
         if s == 1:
-            z = g
+            z = gp
         else:  # zero-insert onto the input grid: a transposed conv as a 'same' conv
-            z = torch.zeros(n, h, wd, cout, device=g.device)
-            z[:, 0:(oh - 1) * s + 1:s, 0:(ow - 1) * s + 1:s] = g
+            z = torch.zeros(n, h, wd, cout + pad_co, device=g.device)
+            z[:, 0:(oh - 1) * s + 1:s, 0:(ow - 1) * s + 1:s] = gp
         qh, qw = kh - 1 - ph, kw - 1 - pw  # dgrad padding
         if s > 1:
             qh, qw = (kh - 1) // 2, (kw - 1) // 2
             if (kh - 1 - ph) != qh or (kw - 1 - pw) != qw:
                 raise ScflowError("strided dgrad needs pad == (k-1)/2")
-        dx = _conv_forward(z, None, _flip_t(w), None, 1, (qh, qw))
+        dx = _conv_forward(z, None, _flip_t(w, pad_co), None, 1, (qh, qw))
         dx0 = dx if x1 is None else dx[..., :c0]
         dx1 = None if x1 is None else dx[..., c0:]
-    if ctx.needs_input_grad[2] or (ctx.has_b and ctx.needs_input_grad[3]):
-        dw, db = _weight_grad(g, x0, x1, w, s, ph, pw, ctx.has_b and ctx.needs_input_grad[3])
-    dbm = g if ctx.needs_input_grad[4] else None
+    want_b = ctx.has_b and ctx.needs_input_grad[3]
+    if ctx.needs_input_grad[2] or want_b:
+        sw = _grad_sink(w) if ctx.needs_input_grad[2] else None
+        sb = _grad_sink(ctx.bias) if want_b else None
+        if sw is not None and (sb is not None or not want_b):
+            _weight_grad(gp, x0, x1, w, s, ph, pw, want_b, dw=sw, db=sb)  # added in place
+        else:
+            dw, db = _weight_grad(gp, x0, x1, w, s, ph, pw, want_b)
     return dx0, dx1, dw, db, dbm, None, None, None, None
 
 
@@ -366,6 +461,7 @@ class _Linear(torch.autograd.Function):
         x = x.contiguous()
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        ctx.bias = b
         return ops.gemm(x, w.detach().t(), bias=None if b is None else b.detach().contiguous())
 
     @staticmethod
@@ -373,8 +469,19 @@ class _Linear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy = dy.contiguous()
         dx = ops.gemm(dy, w.detach()) if ctx.needs_input_grad[0] else None
-        dw = ops.gemm(dy.t(), x) if ctx.needs_input_grad[1] else None
-        db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            sw = _grad_sink(w)
+            if sw is not None:  # dW added in place: beta = 1 onto the parameter's .grad
+                ops.gemm(dy.t(), x, out=sw, beta=1.0)
+            else:
+                dw = ops.gemm(dy.t(), x)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy.sum(0)
+            sb = _grad_sink(ctx.bias)
+            if sb is not None:
+                sb += db
+                db = None
         return dx, dw, db
 
 

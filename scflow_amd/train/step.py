@@ -19,6 +19,7 @@ from typing import Dict, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from .functions import capture_cache, direct_weight_grads
 from .model import refiner_train_forward
 
 Tensor = torch.Tensor
@@ -142,7 +143,11 @@ class TrainStep:
     def _fwd_bwd(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         self.grads.zero()
         out = refiner_train_forward(self.refiner, batch, self.model_points, self.diam_t, self.iters)
-        out["loss"].backward()
+        if self.grads._hooks:  # per-parameter hooks must see every accumulation
+            out["loss"].backward()
+        else:
+            with direct_weight_grads():
+                out["loss"].backward()
         # detached: a returned tensor must not keep this step's autograd graph (and its
         # AccumulateGrad nodes) alive into the next step or a capture
         return {k: _detach(v) for k, v in out.items()}
@@ -154,7 +159,7 @@ class TrainStep:
         for b, c in zip(self.refiner.buffers(), bufs):
             b.copy_(c)
         self._g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g, stream=self.stream):
+        with torch.cuda.graph(self._g, stream=self.stream), capture_cache():
             self._out = self._fwd_bwd(self._static)
 
     def _step(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:

@@ -35,6 +35,7 @@ def _close(a, b, rtol, atol, what):
     (2, 32, 32, 256, 128, (5, 1), 1, (2, 0)),   # GRU 5×1
     (2, 8, 8, 128, 128, 3, 2, 1),               # pose head conv3 (4×4 output)
     (3, 128, 128, 64, 64, 3, 1, 1),             # encoder layer1 (wide rows)
+    (2, 32, 32, 256, 126, 3, 1, 1),             # out_net (cout not a multiple of 4)
 ])
 def test_conv2d_nhwc_forward_backward(case):
     from scflow_amd.train.functions import conv2d_nhwc
@@ -120,6 +121,41 @@ def test_conv_wgrad_accumulate_and_split():
     torch.cuda.synchronize()
     _close(dw - 1, ref, 1e-5, 1e-4 * np.sqrt(n * h * w), "dw")
     _close(db - 1, dy.double().sum((0, 1, 2)), 1e-5, 1e-4 * np.sqrt(n * h * w), "db")
+
+
+@pytest.mark.parametrize("case", [
+    # (n, h, w, c0, c1, cout, kh, kw, stride)   thin side
+    (16, 32, 32, 128, 128, 2, 3, 3, 1),       # cout 2, two sources (Chan slice), 256 workgroups
+    (16, 32, 32, 256, 0, 1, 1, 1, 1),         # cout 1, 1×1 (mask predictor)
+    (4, 32, 32, 1, 0, 64, 3, 3, 1),           # cin 1 (mask encoder)
+    (2, 33, 31, 3, 0, 64, 3, 3, 2),           # cin 3, 3×3 / 2, odd sizes
+    (2, 32, 32, 2, 0, 128, 5, 1, 1),          # cin 2, 5×1 (rows over grid.y, one tap per row)
+    (2, 16, 16, 64, 0, 4, 1, 5, 2),           # cout 4, 1×5 / 2
+])
+def test_conv_wgrad_thin(case):
+    """The thin-channel weight gradient (one side ≤ 4 channels): fp64 reference, accumulate = 1
+    onto dw / db, a Chan slice as the second source."""
+    from scflow_amd import ops
+    from scflow_amd.ops import Chan
+    n, h, w, c0, c1, cout, kh, kw, s = case
+    g = torch.Generator().manual_seed(sum(case))
+    ph, pw = kh // 2, kw // 2
+    x0 = torch.randn(n, h, w, c0, generator=g)
+    buf = torch.randn(n, h, w, c1 + 8, generator=g)
+    x1 = buf[..., 4:4 + c1]
+    oh, ow = (h + 2 * ph - kh) // s + 1, (w + 2 * pw - kw) // s + 1
+    dy = torch.randn(n, oh, ow, cout, generator=g)
+    xc = torch.cat([x0, x1], -1) if c1 else x0
+    ref = torch.nn.grad.conv2d_weight(xc.permute(0, 3, 1, 2).double(), (cout, c0 + c1, kh, kw),
+                                      dy.permute(0, 3, 1, 2).double(), stride=s, padding=(ph, pw))
+    dw = torch.ones(cout, c0 + c1, kh, kw).cuda()
+    db = torch.ones(cout).cuda()
+    src1 = Chan(buf.cuda().view(-1, c1 + 8), 4, c1) if c1 else None
+    ops.conv_wgrad(dy.cuda().view(-1, cout), x0.cuda(), src1, dw, db, n, h, w, kh, kw, s, ph, pw,
+                   accumulate=True)
+    torch.cuda.synchronize()
+    _close(dw - 1, ref, 1e-5, 1e-4 * np.sqrt(n * oh * ow), "dw")
+    _close(db - 1, dy.double().sum((0, 1, 2)), 1e-5, 1e-4 * np.sqrt(n * oh * ow), "db")
 
 
 def test_corr_pyramid_backward():
