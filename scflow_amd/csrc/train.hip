@@ -418,6 +418,16 @@ bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   const int tiles = P->co_tiles * ci_tiles;
   const int occ = a.kh * a.kw >= 9 ? 1 : 2;  // the kernel's resident workgroups per CU
   int want = (occ * device_cus() + tiles - 1) / tiles;
+  static const int forced = [] {  // SCFLOW_WGRAD_SPLITS=k forces k splits (tuning only)
+    const char* e = getenv("SCFLOW_WGRAD_SPLITS");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) {
+    want = forced < P->nchunks ? forced : P->nchunks;
+    P->cps = (P->nchunks + want - 1) / want;
+    *splits = (P->nchunks + P->cps - 1) / P->cps;
+    return true;
+  }
   // ≥ 8 chunks per split, unless that leaves CUs idle: then down to one chunk per split until
   // every CU has a workgroup, while the partial slabs (splits × the padded weight size, written
   // and read once more by the reduction) stay under 8 Mi floats

@@ -167,7 +167,9 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
     lib_ok = same and (
         (cin <= 4 and x1 is None) or (cout <= 4 and cin % 8 == 0) or
         (c0 % 4 == 0 and c1 % 4 == 0 and wd in (32, 64) and (kh, kw) in ((1, 1), (3, 3), (1, 5), (5, 1))
-         and oh % (128 // wd if wd <= 128 else 1) == 0))
+         and oh % (128 // wd if wd <= 128 else 1) == 0) or
+        # the encoders' 128-wide 3×3 convs (and their dX): Winograd, two output rows per block
+        (c0 % 4 == 0 and c1 % 4 == 0 and wd == 128 and (kh, kw) == (3, 3) and oh % 2 == 0))
     if lib_ok:
         bk = ops.conv_pick_bk(n, h, wd, c0, c1, cout, kh, kw, ph, pw, 1)
         try:

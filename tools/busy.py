@@ -39,6 +39,20 @@ def main():
     tot = sum(fam.values())
     print(f"kernels {len(rows)}  wall {wall / 1e6:.2f} ms  busy {busy / 1e6:.2f} ms  "
           f"({100 * busy / wall:.1f}%)  kernel-time {tot / 1e6:.2f} ms")
+    # idle gaps between consecutive kernels (a start after every earlier kernel's end)
+    edges = [0, 2, 5, 10, 20, 50, 200, 1e12]
+    gc, gs = [0] * (len(edges) - 1), [0.0] * (len(edges) - 1)
+    last_e = rows[0][2]
+    for _, s, e in rows[1:]:
+        if s > last_e:
+            g = (s - last_e) / 1e3
+            i = next(j for j in range(len(edges) - 1) if g < edges[j + 1])
+            gc[i] += 1
+            gs[i] += g
+        last_e = max(last_e, e)
+    print("idle gaps (us bins): " + "  ".join(
+        f"[{edges[i]:g},{edges[i + 1]:g}) n={gc[i]} {gs[i] / 1e3:.2f}ms" for i in range(len(gc))
+        if gc[i]).replace("1e+12", "inf"))
     for k, v in fam.most_common(40):
         print(f"{v / 1e6:10.3f} ms {100 * v / tot:6.2f}% {cnt[k]:7d}  {k[:90]}")
 
