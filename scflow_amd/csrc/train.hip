@@ -127,38 +127,46 @@ __global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(
 // ------------------------------------------------------------------------------ wgrad
 struct WgParams {
   scflow_wgrad_args a;
-  int oh, ow, tr, tc, ltc, hr, hc, cp, nchunks, cps, co_tiles, copad, cinp;
+  int oh, ow, tr, tc, ltc, hr, hc, cp, nchunks, cps, co_tiles, copad, cinp, wco;
 };
 
-constexpr int WT = 64;  // co and ci tile of a workgroup
+constexpr int WT = 64;  // ci tile of a workgroup (and the co tile of the 4-wave variant)
 
-// float4 per thread needed to stage the largest halo a (KH, KW, S) launch can have
-constexpr int wg_nx(int kh, int kw, int s) {
+// float4 per thread needed to stage the largest halo a (KH, KW, S) launch can have (NT threads)
+constexpr int wg_nx(int kh, int kw, int s, int nt) {
   const int cp = s == 1 ? 64 : 32;
   int best = 0;
   for (int tc = 2; tc <= 32; tc *= 2) {
     const int tr = cp / tc;
     const int hr = (tr - 1) * s + kh, hc = (tc - 1) * s + kw;
-    const int v = (hr * hc * (WT / 4) + 255) / 256;
+    const int v = (hr * hc * (WT / 4) + nt - 1) / nt;
     if (v > best) best = v;
   }
   return best;
 }
 
-template <int KH, int KW, int S, bool VEC, bool DB>
-__global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgParams P, float* __restrict__ slab,
-                                                        float* __restrict__ bslab) {
+// WCO = output channels per workgroup (64: 2 co × 2 ci waves of 32×32; 128: 4 co × 2 ci).
+// KS = 2: a second set of waves takes every other pair of k-steps of each chunk (two waves per
+// SIMD, so one wave's LDS reads and chunk barriers hide under the other's MFMAs); the two sets'
+// accumulators are summed through LDS before the slab write.
+template <int KH, int KW, int S, bool VEC, bool DB, int WCO = 64, int KS = 1>
+__global__ __launch_bounds__(WCO * 4 * KS, (KH * KW >= 9 || WCO * KS > 64) ? 1 : 2) void wgrad_kernel(
+    WgParams P, float* __restrict__ slab, float* __restrict__ bslab) {
+  constexpr int NT = WCO * 4 * KS; // threads
+  constexpr int CQ = WCO / 4;      // float4 per dY pixel row of the tile
+  constexpr int NWCO = WCO / 32;   // waves along co
   constexpr int TAPS = KH * KW;
-  constexpr int NX = VEC ? wg_nx(KH, KW, S) : 1;
-  constexpr int ND = VEC ? (S == 1 ? 64 : 32) * (WT / 4) / 256 : 1;
+  constexpr int NX = VEC ? wg_nx(KH, KW, S, NT) : 1;
+  constexpr int ND = VEC ? (S == 1 ? 64 : 32) * CQ / NT : 1;
   extern __shared__ float smem[];
   const scflow_wgrad_args& a = P.a;
-  float* Ds = smem;                 // [cp][64] dY chunk, then [hr*hc][64] input halo; ×2 (float4)
-  float* Xs = smem + P.cp * WT;
+  float* Ds = smem;                 // [cp][WCO] dY chunk, then [hr*hc][64] input halo; ×2 (float4)
+  float* Xs = smem + P.cp * WCO;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int li = lane & 31, hh = lane >> 5, wco = wave & 1, wci = wave >> 1;
+  const int li = lane & 31, hh = lane >> 5, wq = wave % (2 * NWCO);
+  const int wco = wq % NWCO, wci = wq / NWCO, ks = wave / (2 * NWCO);
   const int co_t = blockIdx.x % P.co_tiles, ci_t = blockIdx.x / P.co_tiles;
-  const int co0 = co_t * WT, ci0 = ci_t * WT;
+  const int co0 = co_t * WCO, ci0 = ci_t * WT;
   const int cin = a.cin0 + a.cin1;
   const int c_begin = blockIdx.y * P.cps;
   const int c_end = min(P.nchunks, c_begin + P.cps);
@@ -186,8 +194,8 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
     chunk_origin(ch, &img, &oy0, &ox0);
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
-      const int idx = tid + 256 * j;
-      const int p = idx >> 4, co = co0 + 4 * (idx & 15);
+      const int idx = tid + NT * j;
+      const int p = idx / CQ, co = co0 + 4 * (idx % CQ);
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (p < P.cp && co < a.cout) {
         const size_t m = ((size_t)img * P.oh + oy0 + (p >> P.ltc)) * P.ow + ox0 + (p & (P.tc - 1));
@@ -197,7 +205,7 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const int idx = tid + 256 * j;
+      const int idx = tid + NT * j;
       const int hp = idx >> 4, c = ci0 + 4 * (idx & 15);
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (hp < nh && c < cin) {
@@ -213,28 +221,28 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
     }
   };
   auto lstore = [&](int buf = 0) {
-    float* D = Ds + buf * (P.cp + nh) * WT;
-    float* X = D + P.cp * WT;
+    float* D = Ds + buf * (P.cp * WCO + nh * WT);
+    float* X = D + P.cp * WCO;
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
-      const int idx = tid + 256 * j;
-      if (idx < P.cp * (WT / 4)) *(floatx4*)(D + (idx >> 4) * WT + 4 * (idx & 15)) = rd[j];
+      const int idx = tid + NT * j;
+      if (idx < P.cp * CQ) *(floatx4*)(D + (idx / CQ) * WCO + 4 * (idx % CQ)) = rd[j];
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const int idx = tid + 256 * j;
+      const int idx = tid + NT * j;
       if (idx < nh * (WT / 4)) *(floatx4*)(X + (idx >> 4) * WT + 4 * (idx & 15)) = rx[j];
     }
   };
   auto stage_scalar = [&](int ch) {  // cin or cout not a multiple of 4: element-wise staging
     int img, oy0, ox0;
     chunk_origin(ch, &img, &oy0, &ox0);
-    for (int idx = tid; idx < P.cp * WT; idx += 256) {
-      const int p = idx >> 6, co = co0 + (idx & 63);
+    for (int idx = tid; idx < P.cp * WCO; idx += NT) {
+      const int p = idx / WCO, co = co0 + (idx % WCO);
       const size_t m = ((size_t)img * P.oh + oy0 + (p >> P.ltc)) * P.ow + ox0 + (p & (P.tc - 1));
       Ds[idx] = co < a.cout ? a.dy[m * a.sdy + co] : 0.f;
     }
-    for (int idx = tid; idx < nh * WT; idx += 256) {
+    for (int idx = tid; idx < nh * WT; idx += NT) {
       const int hp = idx >> 6, c = ci0 + (idx & 63);
       const int hy = hp / P.hc, hx = hp - hy * P.hc;
       const int iy = oy0 * S - a.ph + hy, ix = ox0 * S - a.pw + hx;
@@ -251,7 +259,7 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
   // prefetch registers after this chunk's MFMAs have been issued; one barrier per chunk.
   // float4 path, !DB: one buffer; the next chunk's global loads are in flight (registers)
   // during this chunk's MFMAs.  Scalar path: one buffer, staged in place.
-  const int bufsz = (P.cp + nh) * WT;
+  const int bufsz = P.cp * WCO + nh * WT;
   if (VEC && c_begin < c_end) {
     gload(c_begin);
     if (DB) {
@@ -263,7 +271,7 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
   for (int ch = c_begin; ch < c_end; ++ch) {
     const int cur = (VEC && DB) ? ((ch - c_begin) & 1) : 0;
     float* Dc = Ds + cur * bufsz;
-    float* Xc = Dc + P.cp * WT;
+    float* Xc = Dc + P.cp * WCO;
     if (!VEC) {
       __syncthreads();
       stage_scalar(ch);
@@ -274,8 +282,8 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
       __syncthreads();
       if (ch + 1 < c_end) gload(ch + 1);
     }
-    if (do_bias)  // every thread: one channel (tid & 63), every 4th pixel
-      for (int p = tid >> 6; p < P.cp; p += 4) bsum += Dc[p * WT + (tid & 63)];
+    if (do_bias)  // every thread: one channel (tid % WCO), every (NT / WCO)-th pixel
+      for (int p = tid / WCO; p < P.cp; p += NT / WCO) bsum += Dc[p * WCO + (tid % WCO)];
     const float* Da = Dc + wco * 32 + li;
     const float* Xb = Xc + wci * 32 + li;
     // software pipeline: the operands of k-step p0+2 are read from LDS before the MFMAs of
@@ -284,7 +292,7 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
     auto ldk = [&](int p0, float& a_, float* b_) {
       const int pix = p0 + hh;
       const int r = pix >> P.ltc, c = pix & (P.tc - 1);
-      a_ = Da[pix * WT];
+      a_ = Da[pix * WCO];
       const float* xb = Xb + (r * S * P.hc + c * S) * WT;
 #pragma unroll
       for (int ty = 0; ty < KH; ++ty)
@@ -294,14 +302,14 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
     // two register sets, two k-steps per trip (cp % 4 == 0): set 1's reads are issued before
     // set 0's MFMAs and vice versa, with no copies between the sets
     float a1, b1[TAPS];
-    ldk(0, av, bv);
-    for (int p0 = 0; p0 < P.cp; p0 += 4) {
+    ldk(4 * ks, av, bv);
+    for (int p0 = 4 * ks; p0 < P.cp; p0 += 4 * KS) {
       ldk(p0 + 2, a1, b1);
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[t], acc[t], 0, 0, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, TAPS + 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TAPS, 0);
-      ldk(p0 + 4 < P.cp ? p0 + 4 : p0, av, bv);
+      ldk(p0 + 4 * KS < P.cp ? p0 + 4 * KS : p0, av, bv);
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1[t], acc[t], 0, 0, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, TAPS + 1, 0);
@@ -313,23 +321,42 @@ __global__ __launch_bounds__(256, KH * KW >= 9 ? 1 : 2) void wgrad_kernel(WgPara
       if (ch + 2 < c_end) gload(ch + 2);
     }
   }
+  if constexpr (KS == 2) {  // the second wave set's accumulators onto the first's, tap by tap
+    constexpr int HALF = NT / 2;
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) {
+      __syncthreads();
+      if (ks == 1)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) smem[r * HALF + (tid - HALF)] = acc[t][r];
+      __syncthreads();
+      if (ks == 0)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] += smem[r * HALF + tid];
+    }
+  }
   // partial slab [split][copad][TAPS][cinp]; C/D layout: col = lane&31, row = (r&3)+8(r>>2)+4hh
   float* sl = slab + (size_t)blockIdx.y * P.copad * TAPS * P.cinp;
   const int ci = ci0 + wci * 32 + li;
+  if (ks == 0)
 #pragma unroll
-  for (int t = 0; t < TAPS; ++t)
+    for (int t = 0; t < TAPS; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      sl[((size_t)co * TAPS + t) * P.cinp + ci] = acc[t][r];
-    }
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wco * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        sl[((size_t)co * TAPS + t) * P.cinp + ci] = acc[t][r];
+      }
   if (do_bias) {
+    constexpr int NG = NT / WCO;  // partial sums per channel
     __syncthreads();
-    Ds[tid] = bsum;
+    smem[tid] = bsum;
     __syncthreads();
-    if (tid < WT)
-      bslab[(size_t)blockIdx.y * P.copad + co0 + tid] =
-          (Ds[tid] + Ds[tid + 64]) + (Ds[tid + 128] + Ds[tid + 192]);
+    if (tid < WCO) {
+      float b = 0.f;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) b += smem[tid + g * WCO];
+      bslab[(size_t)blockIdx.y * P.copad + co0 + tid] = b;
+    }
   }
 }
 
@@ -826,9 +853,21 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
   if (lds > 160 * 1024) return SCFLOW_EUNSUPPORTED;
   const dim3 grid((unsigned)(P.co_tiles * (P.cinp / WT)), (unsigned)splits);
   hipStream_t st = (hipStream_t)stream;
+  // 3×3 (one workgroup per CU): two wave sets splitting each chunk's k-steps (SCFLOW_WGRAD_KS=1
+  // keeps one set; tuning only)
+  static const int ks_env = [] {
+    const char* e = getenv("SCFLOW_WGRAD_KS");
+    return e ? atoi(e) : 2;
+  }();
+  const bool ks2 = vec && taps >= 9 && ks_env == 2;
 #define SCFLOW_WG(KH_, KW_, S_)                                                                  \
   if (a.kh == KH_ && a.kw == KW_ && a.stride == S_) {                                            \
-    if (db2)                                                                                     \
+    if (KH_ * KW_ >= 9 && ks2) {                                                                 \
+      if (db2)                                                                                   \
+        wgrad_kernel<KH_, KW_, S_, true, true, 64, 2><<<grid, 512, lds, st>>>(P, slab, bslab);   \
+      else                                                                                       \
+        wgrad_kernel<KH_, KW_, S_, true, false, 64, 2><<<grid, 512, lds, st>>>(P, slab, bslab);  \
+    } else if (db2)                                                                              \
       wgrad_kernel<KH_, KW_, S_, true, true><<<grid, 256, lds, st>>>(P, slab, bslab);            \
     else if (vec)                                                                                \
       wgrad_kernel<KH_, KW_, S_, true, false><<<grid, 256, lds, st>>>(P, slab, bslab);           \
