@@ -456,6 +456,55 @@ def corr_lookup(pyr: Tensor, flow_nhwc: Tensor, n: int, h: int, w: int, num_leve
     return _CorrLookup.apply(pyr, flow_nhwc.detach(), n, h, w, num_levels, radius)
 
 
+# ------------------------------------------------------------------------------- upsampling
+_INTERP = {}
+
+
+def _interp_matrix(n_in: int, n_out: int, device) -> Tensor:
+    """[n_out, n_in] bilinear weights of align_corners=True resampling along one axis (source
+    coordinate o·(n_in−1)/(n_out−1), as ATen's upsample_bilinear2d)."""
+    key = (n_in, n_out, str(device))
+    m = _INTERP.get(key)
+    if m is None:
+        scale = (n_in - 1) / (n_out - 1) if n_out > 1 else 0.0
+        src = torch.arange(n_out, dtype=torch.float32) * torch.tensor(scale, dtype=torch.float32)
+        i0 = src.floor().long().clamp(max=n_in - 1)
+        lam = src - i0.float()
+        i1 = (i0 + 1).clamp(max=n_in - 1)
+        m = torch.zeros(n_out, n_in)
+        m.index_put_((torch.arange(n_out), i0), 1.0 - lam, accumulate=True)
+        m.index_put_((torch.arange(n_out), i1), lam, accumulate=True)
+        m = _INTERP[key] = m.to(device)
+    return m
+
+
+class _UpsampleAC(torch.autograd.Function):
+    """F.interpolate(x, scale_factor=s, mode="bilinear", align_corners=True) on NCHW x; the
+    backward is the separable adjoint Ayᵀ·g·Ax as two GEMMs on the HIP fp32 MFMA GEMM instead of
+    ATen's atomic scatter (75 µs per 16×2×256² gradient; the full-resolution flow / mask of
+    every refinement iteration, scflow_decoder.py:223-228)."""
+
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.hw = x.shape[-2:]
+        return F.interpolate(x, scale_factor=(s, s), mode="bilinear", align_corners=True)
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.hw
+        n, c, H, W = g.shape
+        ax = _interp_matrix(w, W, g.device)   # [W, w]
+        ayt = _interp_matrix(h, H, g.device).t()  # [h, H]
+        t = ops.gemm(g.contiguous().view(n * c * H, W), ax)  # [n·c·H, w]
+        dx = ops.gemm(ayt.unsqueeze(0).expand(n * c, h, H), t.view(n * c, H, w))
+        return dx.view(n, c, h, w), None
+
+
+def upsample_bilinear_ac(x: Tensor, scale: int) -> Tensor:
+    """Bilinear ×scale upsampling with align_corners=True of NCHW x (torch forward, GEMM backward)."""
+    return _UpsampleAC.apply(x, scale)
+
+
 # ------------------------------------------------------------------------------- linear
 class _Linear(torch.autograd.Function):
     @staticmethod

@@ -21,10 +21,17 @@ SYMMETRIC_CLASSES = (12, 15, 18, 19, 20)  # 0-based labels of cls_13, cls_16, cl
 POSE_WEIGHT, FLOW_WEIGHT, MASK_WEIGHT, GAMMA = 10.0, 0.1, 10.0, 0.8
 
 
+def flow_valid(gt: Tensor, valid: Tensor, max_flow: float = 400.) -> Tensor:
+    """RAFTLoss's pixel mask (sequence_loss.py:15-23): valid ≥ 0.5 and |gt| < max_flow."""
+    return ((valid >= 0.5) & (gt.pow(2).sum(1).sqrt() < max_flow)).to(gt)
+
+
 def flow_l1_loss(pred: Tensor, gt: Tensor, valid: Tensor, max_flow: float = 400.,
-                 weight: float = FLOW_WEIGHT, eps: float = 1e-10) -> Tensor:
-    """RAFTLoss (sequence_loss.py:15-23): valid-masked L1 of the flow."""
-    v = ((valid >= 0.5) & (gt.pow(2).sum(1).sqrt() < max_flow)).to(gt)
+                 weight: float = FLOW_WEIGHT, eps: float = 1e-10, v: Tensor = None) -> Tensor:
+    """RAFTLoss (sequence_loss.py:15-23): valid-masked L1 of the flow (``v``: the mask from
+    flow_valid, when the caller computes it once for all iterations)."""
+    if v is None:
+        v = flow_valid(gt, valid, max_flow)
     return weight * (v[:, None] * (pred - gt).abs()).sum() / (v.sum() + eps)
 
 
@@ -111,7 +118,8 @@ def refine_losses(outs, gt_r: Tensor, gt_t: Tensor, gt_flow: Tensor, render_mask
         diameters, dtype=gt_r.dtype, device=gt_r.device)
     lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam)
                         for R, t in zip(Rs, ts)])  # (symmetric matching always evaluated: no sync)
-    lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow) for f in flow_pred])
+    v = flow_valid(gt_flow, render_mask, max_flow)  # iteration-invariant
+    lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow, v=v) for f in flow_pred])
     occ = (gt_flow.sum(1) < max_flow).to(gt_flow)
     lm = sequence_loss([mask_l1_loss(m[:, 0], occ) for m in masks])
     return lp, lf, lm

@@ -57,6 +57,8 @@ def _patch_torch_ops(monkeypatch):
     monkeypatch.setattr(model, "conv2d_nhwc", conv)
     monkeypatch.setattr(model, "conv2d_nhwc_split", conv_split)
     monkeypatch.setattr(model, "linear", F.linear)
+    monkeypatch.setattr(model, "upsample_bilinear_ac", lambda x, s: F.interpolate(
+        x, scale_factor=(s, s), mode="bilinear", align_corners=True))
     monkeypatch.setattr(model, "corr_pyramid", pyramid)
     monkeypatch.setattr(model, "corr_lookup", lookup)
     monkeypatch.setattr(ops, "lift_points", lift)
@@ -141,3 +143,22 @@ def test_train_forward_host_matches_oracle(monkeypatch):
     assert checked > 100
     # BN running stats were updated in train mode (SCFlowRefiner.train())
     assert int(r.context.norm1.num_batches_tracked) == 1
+
+
+def test_upsample_adjoint_matches_autograd(monkeypatch):
+    """The training step's ×8 upsampling backward (two GEMMs on the interpolation matrices, here
+    on torch.matmul in place of the HIP GEMM) equals autograd of F.interpolate(align_corners)."""
+    from scflow_amd.train import functions as fn
+    monkeypatch.setattr(fn.ops, "gemm", lambda a, b: torch.matmul(a, b))
+    g = torch.Generator().manual_seed(5)
+    for (h, w, s) in ((32, 32, 8), (7, 5, 4)):
+        x = torch.randn(2, 3, h, w, generator=g, dtype=torch.float64)
+        xr = x.clone().requires_grad_()
+        yr = F.interpolate(xr, scale_factor=(s, s), mode="bilinear", align_corners=True)
+        gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+        (yr * gy).sum().backward()
+        xg = x.float().requires_grad_()
+        y = fn.upsample_bilinear_ac(xg, s)
+        (y * gy.float()).sum().backward()
+        assert torch.allclose(y.double(), yr.detach(), atol=1e-5)
+        assert torch.allclose(xg.grad.double(), xr.grad, rtol=1e-5, atol=1e-4)
