@@ -400,6 +400,13 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
  *   SCFlow (scflow_decoder.py:193-194), so no flow gradient. */
 int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh, int kw,
                   int stride, int ph, int pw, void* stream);
+/* scflow_col2im: the adjoint of scflow_im2col (same geometry; dx has pixel stride sdx ≥ cin):
+ *   dx[n][iy][ix][c] = Σ_{ty,tx: (iy+ph−ty)/s, (ix+pw−tx)/s integral, inside} cols[(n,oy,ox)][(ty·kw+tx)·cin+c]
+ * — a fixed-order gather, written (not accumulated).  With cols = dY·Wmat (Wmat[co][(ty·kw+tx)·cin+ci]
+ * = w[co][ci][ty][tx]) it is a strided conv's input gradient without zero insertion (training:
+ * the stride-2 convs of the encoders and the pose head, resnet.py / pose_head.py:201-211). */
+int scflow_col2im(const float* cols, float* dx, int sdx, int n, int h, int w, int cin, int kh, int kw,
+                  int stride, int ph, int pw, void* stream);
 
 /* scflow_conv_wgrad: weight (and bias) gradient of a channels-last conv without an im2col
  * matrix — dw[co][ci][ty][tx] (+)= Σ_p dy[p][co] · x[n][oy·s − ph + ty][ox·s − pw + tx][ci],

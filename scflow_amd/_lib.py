@@ -204,6 +204,8 @@ SIGNATURES = {
     "scflow_conv_wgrad": (c_int, [ctypes.POINTER(WgradArgs), c_vp]),
     "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_vp]),
+    "scflow_col2im": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_vp]),
     "scflow_corr_lookup_backward": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int,
                                             c_int, c_int, c_vp]),
     "scflow_gemm_f32_splits": (c_int, [c_int, c_int, c_int, c_int]),

@@ -54,6 +54,50 @@ __global__ void im2col_kernel(const float* __restrict__ x, int sx, float* __rest
   }
 }
 
+// col2im: the adjoint of im2col — dx[n][iy][ix][c] = Σ over the taps (ty, tx) whose output pixel
+// oy = (iy + ph − ty)/s, ox = (ix + pw − tx)/s is integral and inside the output grid of
+// cols[(n, oy, ox)][(ty·kw + tx)·cin + c].  A gather (no atomics, fixed order): the strided
+// conv's dX as cols = dY·Wmat (one GEMM with exactly the needed products) + this.
+__global__ void col2im_kernel(const float* __restrict__ cols, float* __restrict__ dx, int sdx,
+                              int h, int w, int cin, int kh, int kw, int stride, int ph, int pw,
+                              int oh, int ow, long long total_vec, int vec) {
+  const int K = kh * kw * cin;
+  const int cv = cin / vec;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total_vec; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % cv) * vec;
+    const long long pix = i / cv;
+    const int ix = (int)(pix % w);
+    const long long t = pix / w;
+    const int iy = (int)(t % h);
+    const int img = (int)(t / h);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int ty = 0; ty < kh; ++ty) {
+      const int ny = iy + ph - ty;
+      if (ny < 0 || ny % stride) continue;
+      const int oy = ny / stride;
+      if (oy >= oh) continue;
+      for (int tx = 0; tx < kw; ++tx) {
+        const int nx = ix + pw - tx;
+        if (nx < 0 || nx % stride) continue;
+        const int ox = nx / stride;
+        if (ox >= ow) continue;
+        const float* src = cols + ((size_t)(img * oh + oy) * ow + ox) * K + (ty * kw + tx) * cin + c;
+        if (vec == 4) {
+          const floatx4 v = *(const floatx4*)src;
+          acc[0] += v[0]; acc[1] += v[1]; acc[2] += v[2]; acc[3] += v[3];
+        } else {
+          acc[0] += *src;
+        }
+      }
+    }
+    float* dst = dx + (size_t)pix * sdx + c;
+    if (vec == 4)
+      *(floatx4*)dst = acc;
+    else
+      *dst = acc[0];
+  }
+}
+
 __device__ __forceinline__ float unnorm_coord_b(float s, int size) {
 #pragma clang fp contract(off)
   const float g = (s * 2.f) / (float)(size - 1 > 1 ? size - 1 : 1) - 1.f;
@@ -907,6 +951,21 @@ SCFLOW_API int scflow_im2col(const float* x, int sx, float* cols, int n, int h, 
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   im2col_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, sx, cols, h, w, cin, kh, kw, stride, ph,
                                                          pw, oh, ow, total, vec);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_col2im(const float* cols, float* dx, int sdx, int n, int h, int w, int cin,
+                             int kh, int kw, int stride, int ph, int pw, void* stream) {
+  if (!cols || !dx || n <= 0 || h <= 0 || w <= 0 || cin <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
+      ph < 0 || pw < 0 || sdx < cin)
+    return SCFLOW_EINVAL;
+  const int oh = (h + 2 * ph - kh) / stride + 1, ow = (w + 2 * pw - kw) / stride + 1;
+  if (oh <= 0 || ow <= 0) return SCFLOW_EINVAL;
+  const int vec = (cin % 4 == 0 && sdx % 4 == 0 && aligned16(dx) && aligned16(cols)) ? 4 : 1;
+  const long long total = (long long)n * h * w * cin / vec;
+  const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  col2im_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(cols, dx, sdx, h, w, cin, kh, kw, stride,
+                                                         ph, pw, oh, ow, total, vec);
   return scflow_launch_status();
 }
 

@@ -798,6 +798,18 @@ def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, p
     return out
 
 
+def col2im(cols: Tensor, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, ph: int,
+           pw: int, out: Optional[Tensor] = None) -> Tensor:
+    """Adjoint of im2col: [n·oh·ow, kh·kw·cin] patch gradients → channels-last [n, h, w, cin]."""
+    _require(cols, "cols")
+    if out is None:
+        out = torch.empty(n, h, w, cin, device=cols.device)
+    _require(out, "out", contiguous=False)
+    _launch("scflow_col2im", cols, _p(cols), _p(out), out.stride(-2), n, h, w, cin, kh, kw, stride,
+            ph, pw)
+    return out
+
+
 def corr_lookup_backward(dout: Tensor, flow: Tensor, dpyr: Tensor, n: int, h: int, w: int,
                          num_levels: int, radius: int, out_layout: str = "nhwc",
                          flow_layout: str = "nhwc") -> None:

@@ -7,8 +7,8 @@ Activations are channels-last [N, H, W, C] contiguous fp32 tensors on the ROCm d
   activation and an optional pre-activation bias map fused into the epilogue, and an optional
   second input source (channel concat without a copy).  Backward: the activation's derivative
   from the saved output; dX = the same HIP conv of the output gradient with the flipped,
-  in/out-transposed weights (for stride s > 1 over the gradient zero-inserted to the input
-  grid — a transposed conv as a 'same' convolution); dW and db = ``scflow_conv_wgrad`` (MFMA
+  in/out-transposed weights (stride s > 1: cols = dY·Wmat on the HIP GEMM + the col2im gather,
+  no zero-inserted grid); dW and db = ``scflow_conv_wgrad`` (MFMA
   implicit GEMM over the pixels, no im2col matrix); 7×7 kernels use HIP im2col + one
   ``scflow_gemm_f32`` dYᵀ·cols.
 * ``corr_pyramid`` — forward ``scflow_corr_pyramid``; backward: average-pool adjoints (¼ to each
@@ -317,17 +317,14 @@ def _conv_backward(ctx, dy):
     pad_co = (-cout) % 4 if cout > 4 else 0
     gp = F.pad(g, (0, pad_co)) if pad_co else g
     if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-        if s == 1:
-            z = gp
-        else:  # zero-insert onto the input grid: a transposed conv as a 'same' conv
-            z = torch.zeros(n, h, wd, cout + pad_co, device=g.device)
-            z[:, 0:(oh - 1) * s + 1:s, 0:(ow - 1) * s + 1:s] = gp
-        qh, qw = kh - 1 - ph, kw - 1 - pw  # dgrad padding
-        if s > 1:
-            qh, qw = (kh - 1) // 2, (kw - 1) // 2
-            if (kh - 1 - ph) != qh or (kw - 1 - pw) != qw:
-                raise ScflowError("strided dgrad needs pad == (k-1)/2")
-        dx = _conv_forward(z, None, _flip_t(w, pad_co), None, 1, (qh, qw))
+        if s == 1:  # a 'same' conv of dY with the flipped, transposed weights
+            dx = _conv_forward(gp, None, _flip_t(w, pad_co), None, 1, (kh - 1 - ph, kw - 1 - pw))
+        else:
+            # strided: cols = dY·Wmat (exactly the products the transposed conv needs, no
+            # zero-inserted grid) and the col2im gather onto the input grid
+            wm = _cached(w, ("wmat",), lambda: w.detach().permute(0, 2, 3, 1).reshape(cout, -1).contiguous())
+            cols = ops.gemm(g.view(-1, cout), wm)
+            dx = ops.col2im(cols, n, h, wd, cin, kh, kw, s, ph, pw)
         dx0 = dx if x1 is None else dx[..., :c0]
         dx1 = None if x1 is None else dx[..., c0:]
     want_b = ctx.has_b and ctx.needs_input_grad[3]

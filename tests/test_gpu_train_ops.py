@@ -36,6 +36,8 @@ def _close(a, b, rtol, atol, what):
     (2, 8, 8, 128, 128, 3, 2, 1),               # pose head conv3 (4×4 output)
     (3, 128, 128, 64, 64, 3, 1, 1),             # encoder layer1 (wide rows)
     (2, 32, 32, 256, 126, 3, 1, 1),             # out_net (cout not a multiple of 4)
+    (2, 33, 31, 16, 40, 3, 2, 1),               # stride 2 on odd sizes (col2im dX)
+    (2, 17, 15, 6, 8, 5, 2, 2),                 # stride 2, 5×5, channels not a multiple of 4
 ])
 def test_conv2d_nhwc_forward_backward(case):
     from scflow_amd.train.functions import conv2d_nhwc
