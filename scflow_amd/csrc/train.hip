@@ -459,6 +459,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   }
 }
 
+#include "wgrad_wino.h"
+
 bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   if (a.stride != 1 && a.stride != 2) return false;
   const bool shape_ok = (a.kh == 1 && a.kw == 1) || (a.kh == 3 && a.kw == 3) ||
@@ -859,6 +861,11 @@ SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long l
     *floats = wthin_workspace(Q);
     return SCFLOW_OK;
   }
+  WwParams R;
+  if (wwino_geometry(*args, &R)) {
+    *floats = wwino_workspace(R);
+    return SCFLOW_OK;
+  }
   WgParams P;
   int splits = 0;
   if (!wgrad_geometry(*args, &P, &splits)) return SCFLOW_EUNSUPPORTED;
@@ -878,6 +885,11 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
   if (wthin_geometry(a, &Q)) {
     if (a.workspace_floats < wthin_workspace(Q)) return SCFLOW_EINVAL;
     return wthin_launch(Q, (hipStream_t)stream);
+  }
+  WwParams R;
+  if (wwino_geometry(a, &R)) {
+    if (a.workspace_floats < wwino_workspace(R)) return SCFLOW_EINVAL;
+    return wwino_launch(R, (hipStream_t)stream);
   }
   WgParams P;
   int splits = 0;
