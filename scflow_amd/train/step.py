@@ -106,9 +106,10 @@ class TrainStep:
 
     ``graph=True`` (off by default): the forward + backward (≈3000 kernel
     launches) are captured once into a hipGraph on the third call and replayed on every later
-    call with the batch copied into the captured input buffers; the all-reduce, clipping and the
-    optimizer step stay eager.  The weights are re-packed inside the graph, so optimizer updates
-    are seen by every replay.  Every kernel of the forward + backward is one of ours (no vendor
+    call with the batch copied into the captured input buffers; the gradient all-reduce stays
+    eager between two replays, and clipping + AdamW (``capturable``: step counts on the device)
+    are a second captured graph.  The weights are re-packed inside the graph, so optimizer
+    updates are seen by every replay.  Every kernel of the forward + backward is one of ours (no vendor
     GEMM: see functions.py), and eager steps and the capture run on the step's own stream."""
 
     def __init__(self, refiner, model_points: Sequence[Tensor], diameters: Sequence[float],
@@ -118,6 +119,8 @@ class TrainStep:
         self.refiner = refiner
         self.graph = graph
         self._g = None
+        self._g_opt = None
+        self._gn = None
         self._static = None
         self._out = None
         self._calls = 0
@@ -128,7 +131,7 @@ class TrainStep:
         params = list(dict.fromkeys(refiner.parameters()))  # the shared encoder appears twice
         self.grads = GradBuckets(params, bucket_bytes, group, overlap)
         self.opt = torch.optim.AdamW(self.grads.params, lr=lr, betas=betas, eps=eps,
-                                     weight_decay=weight_decay, foreach=True)
+                                     weight_decay=weight_decay, foreach=True, capturable=graph)
         dev = self.grads.params[0].device
         self.stream = torch.cuda.Stream(device=dev)
         self.diam_t = torch.as_tensor(self.diameters, dtype=torch.float32, device=dev)
@@ -174,8 +177,16 @@ class TrainStep:
             # the per-iteration lists stay views of the graph's buffers
             out = {k: (v.clone() if isinstance(v, Tensor) and v.dim() == 0 else v)
                    for k, v in self._out.items()}
-        else:
-            out = self._fwd_bwd(batch)
+            self.grads.finish()
+            if self._g_opt is None:  # optimizer state exists (eager calls 1-2): capture clip + AdamW
+                self._g_opt = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g_opt, stream=self.stream):
+                    self._gn = self.grads.clip_(self.max_norm)
+                    self.opt.step()
+            self._g_opt.replay()
+            out["grad_norm"] = self._gn.clone()
+            return out
+        out = self._fwd_bwd(batch)
         self.grads.finish()
         out["grad_norm"] = self.grads.clip_(self.max_norm)
         self.opt.step()
