@@ -146,11 +146,14 @@ class TrainStep:
     def _fwd_bwd(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         self.grads.zero()
         out = refiner_train_forward(self.refiner, batch, self.model_points, self.diam_t, self.iters)
-        if self.grads._hooks:  # per-parameter hooks must see every accumulation
-            out["loss"].backward()
-        else:
-            with direct_weight_grads():
+        # backward on the calling thread: the step's ~2000 autograd nodes are launch-bound host
+        # work, and the device thread's hand-offs cost more than they overlap
+        with torch.autograd.set_multithreading_enabled(False):
+            if self.grads._hooks:  # per-parameter hooks must see every accumulation
                 out["loss"].backward()
+            else:
+                with direct_weight_grads():
+                    out["loss"].backward()
         # detached: a returned tensor must not keep this step's autograd graph (and its
         # AccumulateGrad nodes) alive into the next step or a capture
         return {k: _detach(v) for k, v in out.items()}

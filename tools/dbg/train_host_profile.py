@@ -20,7 +20,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--main-thread-backward", action="store_true",
+                    help="run autograd's backward on the calling thread, so cProfile sees it")
     a = ap.parse_args()
+    if a.main_thread_backward:
+        torch.autograd.set_multithreading_enabled(False)
     import bench
     from scflow_amd import synthetic
     from scflow_amd.train.step import TrainStep
