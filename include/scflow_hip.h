@@ -400,6 +400,20 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
  *   SCFlow (scflow_decoder.py:193-194), so no flow gradient. */
 int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh, int kw,
                   int stride, int ph, int pw, void* stream);
+/* SepConvGRU gate algebra of the training step (raft_decoder.py:235-253), channels-last,
+ * c % 4 == 0, zr = the z | r conv's sigmoid output [npix][2c]:
+ *   scflow_gru_gate_forward mode 0: out = r·h;  mode 1: out = h + z·(q − h)
+ *   scflow_gru_gate_backward_q: dq = dh2·z·(1 − q²); dzr[:, :c] = dh2·(q − h)·z(1 − z);
+ *                               dha = dh2·(1 − z)
+ *   scflow_gru_gate_backward_r: dzr[:, c:] = drh·h·r(1 − r); dh = dha + drh·r (drh pixel stride sdrh) */
+int scflow_gru_gate_forward(const float* zr, const float* h, const float* q, float* out,
+                            long long npix, int c, int mode, void* stream);
+int scflow_gru_gate_backward_q(const float* dh2, const float* zr, const float* h, const float* q,
+                               float* dq, float* dzr, float* dha, long long npix, int c,
+                               void* stream);
+int scflow_gru_gate_backward_r(const float* drh, int sdrh, const float* zr, const float* h,
+                               const float* dha, float* dzr, float* dh, long long npix, int c,
+                               void* stream);
 /* scflow_col2im: the adjoint of scflow_im2col (same geometry; dx has pixel stride sdx ≥ cin):
  *   dx[n][iy][ix][c] = Σ_{ty,tx: (iy+ph−ty)/s, (ix+pw−tx)/s integral, inside} cols[(n,oy,ox)][(ty·kw+tx)·cin+c]
  * — a fixed-order gather, written (not accumulated).  With cols = dY·Wmat (Wmat[co][(ty·kw+tx)·cin+ci]

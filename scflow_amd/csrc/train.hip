@@ -852,7 +852,127 @@ __global__ void in_bwd_apply_kernel(const float* __restrict__ dy, const float* _
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// SepConvGRU gate algebra of the training step (raft_decoder.py:235-253 with the reference's
+// z = σ(convz), r = σ(convr), q = tanh(convq(r·h ⊕ x)), h' = (1 − z)·h + z·q), channels-last,
+// zr = the z | r conv's sigmoid output [p][2c] (z = channels 0..c−1, r = c..2c−1), c % 4 == 0.
+//   rh = r·h;   h' = h + z·(q − h)
+// backward, given dh' and (through the q conv) d(rh):
+//   dq_pre = dh'·z·(1 − q²)            dzr[:, :c] = dh'·(q − h)·z(1 − z)     dh_a = dh'·(1 − z)
+//   dzr[:, c:] = d(rh)·h·r(1 − r)       dh = dh_a + d(rh)·r
+// (the activations' derivatives fused: the convs' backward then runs on pre-activation grads).
+__global__ void gru_fwd_kernel(const float* __restrict__ zr, const float* __restrict__ h,
+                               const float* __restrict__ q, float* __restrict__ out, int c,
+                               long long total4, int mode) {
+  const int c4 = c / 4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const long long p = i / c4;
+    const int cq = (int)(i % c4) * 4;
+    const floatx4 hv = *(const floatx4*)(h + p * c + cq);
+    floatx4 r;
+    if (mode == 0) {  // rh = r·h
+      const floatx4 rv = *(const floatx4*)(zr + p * 2 * c + c + cq);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = rv[e] * hv[e];
+    } else {          // h' = h + z·(q − h)
+      const floatx4 zv = *(const floatx4*)(zr + p * 2 * c + cq);
+      const floatx4 qv = *(const floatx4*)(q + p * c + cq);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = hv[e] + zv[e] * (qv[e] - hv[e]);
+    }
+    *(floatx4*)(out + p * c + cq) = r;
+  }
+}
+
+__global__ void gru_bwd_q_kernel(const float* __restrict__ dh2, const float* __restrict__ zr,
+                                 const float* __restrict__ h, const float* __restrict__ q,
+                                 float* __restrict__ dq, float* __restrict__ dzr,
+                                 float* __restrict__ dha, int c, long long total4) {
+  const int c4 = c / 4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const long long p = i / c4;
+    const int cq = (int)(i % c4) * 4;
+    const floatx4 g = *(const floatx4*)(dh2 + p * c + cq);
+    const floatx4 zv = *(const floatx4*)(zr + p * 2 * c + cq);
+    const floatx4 hv = *(const floatx4*)(h + p * c + cq);
+    const floatx4 qv = *(const floatx4*)(q + p * c + cq);
+    floatx4 a, b, d;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] = g[e] * zv[e] * (1.f - qv[e] * qv[e]);
+      b[e] = g[e] * (qv[e] - hv[e]) * (zv[e] * (1.f - zv[e]));
+      d[e] = g[e] * (1.f - zv[e]);
+    }
+    *(floatx4*)(dq + p * c + cq) = a;
+    *(floatx4*)(dzr + p * 2 * c + cq) = b;
+    *(floatx4*)(dha + p * c + cq) = d;
+  }
+}
+
+__global__ void gru_bwd_r_kernel(const float* __restrict__ drh, int sdrh,
+                                 const float* __restrict__ zr, const float* __restrict__ h,
+                                 const float* __restrict__ dha, float* __restrict__ dzr,
+                                 float* __restrict__ dh, int c, long long total4) {
+  const int c4 = c / 4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const long long p = i / c4;
+    const int cq = (int)(i % c4) * 4;
+    const floatx4 g = *(const floatx4*)(drh + p * sdrh + cq);
+    const floatx4 rv = *(const floatx4*)(zr + p * 2 * c + c + cq);
+    const floatx4 hv = *(const floatx4*)(h + p * c + cq);
+    const floatx4 av = *(const floatx4*)(dha + p * c + cq);
+    floatx4 a, b;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] = g[e] * hv[e] * (rv[e] * (1.f - rv[e]));
+      b[e] = av[e] + g[e] * rv[e];
+    }
+    *(floatx4*)(dzr + p * 2 * c + c + cq) = a;
+    *(floatx4*)(dh + p * c + cq) = b;
+  }
+}
+
+int gru_grid(long long total4) {
+  const long long b = (total4 + 255) / 256;
+  return (int)(b < 8192 ? b : 8192);
+}
+
 }  // namespace
+
+SCFLOW_API int scflow_gru_gate_forward(const float* zr, const float* h, const float* q, float* out,
+                                       long long npix, int c, int mode, void* stream) {
+  if (!zr || !h || !out || npix <= 0 || c <= 0 || (c & 3) || (mode != 0 && mode != 1) ||
+      (mode == 1 && !q) || !aligned16(zr) || !aligned16(h) || !aligned16(out) ||
+      (q && !aligned16(q)))
+    return SCFLOW_EINVAL;
+  const long long t4 = npix * c / 4;
+  gru_fwd_kernel<<<gru_grid(t4), 256, 0, (hipStream_t)stream>>>(zr, h, q, out, c, t4, mode);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_gru_gate_backward_q(const float* dh2, const float* zr, const float* h,
+                                          const float* q, float* dq, float* dzr, float* dha,
+                                          long long npix, int c, void* stream) {
+  if (!dh2 || !zr || !h || !q || !dq || !dzr || !dha || npix <= 0 || c <= 0 || (c & 3) ||
+      !aligned16(dh2) || !aligned16(zr) || !aligned16(h) || !aligned16(q) || !aligned16(dq) ||
+      !aligned16(dzr) || !aligned16(dha))
+    return SCFLOW_EINVAL;
+  const long long t4 = npix * c / 4;
+  gru_bwd_q_kernel<<<gru_grid(t4), 256, 0, (hipStream_t)stream>>>(dh2, zr, h, q, dq, dzr, dha, c, t4);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_gru_gate_backward_r(const float* drh, int sdrh, const float* zr,
+                                          const float* h, const float* dha, float* dzr, float* dh,
+                                          long long npix, int c, void* stream) {
+  if (!drh || !zr || !h || !dha || !dzr || !dh || npix <= 0 || c <= 0 || (c & 3) || sdrh < c ||
+      (sdrh & 3) || !aligned16(drh) || !aligned16(zr) || !aligned16(h) || !aligned16(dha) ||
+      !aligned16(dzr) || !aligned16(dh))
+    return SCFLOW_EINVAL;
+  const long long t4 = npix * c / 4;
+  gru_bwd_r_kernel<<<gru_grid(t4), 256, 0, (hipStream_t)stream>>>(drh, sdrh, zr, h, dha, dzr, dh, c, t4);
+  return scflow_launch_status();
+}
 
 SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats) {
   if (!args || !floats) return SCFLOW_EINVAL;

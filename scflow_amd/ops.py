@@ -798,6 +798,39 @@ def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, p
     return out
 
 
+def gru_gate_forward(zr: Tensor, h: Tensor, out: Tensor, q: Optional[Tensor] = None) -> Tensor:
+    """SepConvGRU gate (training): out = r·h (q None) or h + z·(q − h); zr [..., 2c], h / q / out
+    [..., c], channels-last contiguous."""
+    for nm, t in (("zr", zr), ("h", h), ("out", out)) + ((("q", q),) if q is not None else ()):
+        _require(t, nm)
+    c = h.shape[-1]
+    _launch("scflow_gru_gate_forward", h, _p(zr), _p(h), _p(q), _p(out), h.numel() // c, c,
+            0 if q is None else 1)
+    return out
+
+
+def gru_gate_backward_q(dh2: Tensor, zr: Tensor, h: Tensor, q: Tensor, dq: Tensor, dzr: Tensor,
+                        dha: Tensor) -> None:
+    """dq = dh2·z·(1 − q²), dzr[..., :c] = dh2·(q − h)·z(1 − z), dha = dh2·(1 − z)."""
+    for nm, t in (("dh2", dh2), ("zr", zr), ("h", h), ("q", q), ("dq", dq), ("dzr", dzr), ("dha", dha)):
+        _require(t, nm)
+    c = h.shape[-1]
+    _launch("scflow_gru_gate_backward_q", h, _p(dh2), _p(zr), _p(h), _p(q), _p(dq), _p(dzr), _p(dha),
+            h.numel() // c, c)
+
+
+def gru_gate_backward_r(drh: Tensor, zr: Tensor, h: Tensor, dha: Tensor, dzr: Tensor,
+                        dh: Tensor) -> None:
+    """dzr[..., c:] = drh·h·r(1 − r), dh = dha + drh·r; drh may be a channel slice (pixel stride
+    ≥ c)."""
+    for nm, t in (("zr", zr), ("h", h), ("dha", dha), ("dzr", dzr), ("dh", dh)):
+        _require(t, nm)
+    _require(drh, "drh", contiguous=False)
+    c = h.shape[-1]
+    _launch("scflow_gru_gate_backward_r", h, _p(drh), drh.stride(-2), _p(zr), _p(h), _p(dha),
+            _p(dzr), _p(dh), h.numel() // c, c)
+
+
 def col2im(cols: Tensor, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, ph: int,
            pw: int, out: Optional[Tensor] = None) -> Tensor:
     """Adjoint of im2col: [n·oh·ow, kh·kw·cin] patch gradients → channels-last [n, h, w, cin]."""

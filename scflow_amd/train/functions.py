@@ -356,6 +356,60 @@ def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride
     return _Conv2dNHWC.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act)
 
 
+# ------------------------------------------------------------------------------- ConvGRU step
+class _GruStep(torch.autograd.Function):
+    """One SepConvGRU direction (raft_decoder.py:235-253) as one autograd node:
+        zr = σ(conv([h, x]; w_zr) + pre_zr)      (z | r from one launch)
+        q  = tanh(conv([r·h, x]; w_q) + pre_q)
+        h' = h + z·(q − h)
+    forward: the two HIP convs (activation and the hoisted context map fused) and two HIP gate
+    kernels; backward: the gate / activation derivatives in two HIP kernels, the two convs' dX
+    and dW, and one add each for dh and dx — instead of ~17 separate autograd kernels
+    (lerp, mul, the activation backwards, slice concatenation, gradient accumulation)."""
+
+    @staticmethod
+    def forward(ctx, h, x, w_zr, w_q, pre_zr, pre_q, pad):
+        h = h.contiguous()
+        x = x.contiguous()
+        zr = _conv_forward(h, x, w_zr.detach(), None, 1, pad, "Sigmoid", pre_zr.detach().contiguous(),
+                           wkey=w_zr)
+        rh = ops.gru_gate_forward(zr, h, torch.empty_like(h))
+        q = _conv_forward(rh, x, w_q.detach(), None, 1, pad, "Tanh", pre_q.detach().contiguous(),
+                          wkey=w_q)
+        h2 = ops.gru_gate_forward(zr, h, torch.empty_like(h), q=q)
+        ctx.save_for_backward(h, x, zr, rh, q, w_zr, w_q)
+        ctx.pad = pad
+        return h2
+
+    @staticmethod
+    def backward(ctx, dh2):
+        h, x, zr, rh, q, w_zr, w_q = ctx.saved_tensors
+        ph, pw = ctx.pad
+        c = h.shape[-1]
+        _, _, kh, kw = w_q.shape
+        dq = torch.empty_like(h)
+        dzr = torch.empty_like(zr)
+        dha = torch.empty_like(h)
+        ops.gru_gate_backward_q(dh2.contiguous(), zr, h, q, dq, dzr, dha)
+        dxq = _conv_forward(dq, None, _flip_t(w_q), None, 1, (kh - 1 - ph, kw - 1 - pw))
+        dw_q, _ = _weight_grad(dq, rh, x, w_q, 1, ph, pw, False)
+        dh = torch.empty_like(h)
+        ops.gru_gate_backward_r(dxq[..., :c], zr, h, dha, dzr, dh)
+        dxz = _conv_forward(dzr, None, _flip_t(w_zr), None, 1, (kh - 1 - ph, kw - 1 - pw))
+        dw_zr, _ = _weight_grad(dzr, h, x, w_zr, 1, ph, pw, False)
+        dh += dxz[..., :c]
+        dx = dxq[..., c:] + dxz[..., c:]
+        return dh, dx, dw_zr, dw_q, dzr, dq, None
+
+
+def gru_step(h: Tensor, x: Tensor, w_zr: Tensor, w_q: Tensor, pre_zr: Tensor, pre_q: Tensor,
+             padding) -> Tensor:
+    """h' of one SepConvGRU direction; channels-last h [.., c], x [.., cx]; w_zr [2c, c + cx, ..],
+    w_q [c, c + cx, ..]; pre_zr / pre_q: the pre-activation maps added before σ / tanh."""
+    pad = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    return _GruStep.apply(h, x, w_zr, w_q, pre_zr, pre_q, pad)
+
+
 # ------------------------------------------------------------------------------- norms
 class _InstanceNormNHWC(torch.autograd.Function):
     """InstanceNorm2d(affine=False) (+ ReLU) of a channels-last [N, H, W, C] tensor on HIP kernels:

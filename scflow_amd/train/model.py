@@ -20,8 +20,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid,
-                        instance_norm_nhwc, linear, upsample_bilinear_ac)
+from .functions import (conv2d_nhwc, corr_lookup, corr_pyramid, gru_step, instance_norm_nhwc,
+                        linear, upsample_bilinear_ac)
 from .losses import filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
@@ -188,10 +188,7 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
             out = _cm(out, m)
         motion = torch.cat([out, f2], -1)
         for (w_zr, w_q, pad), (pre_zr, pre_q) in zip(it_w, ctx_pre):  # SeqConv: 1×5 then 5×1
-            z, rg = conv2d_nhwc_split(h, w_zr, hc, None, 1, pad, act="Sigmoid", x1=motion,
-                                      bias_map=pre_zr)
-            qq = conv2d_nhwc(rg * h, w_q, None, 1, pad, act="Tanh", x1=motion, bias_map=pre_q)
-            h = torch.lerp(h, qq, z)  # (1 − z)·h + z·q
+            h = gru_step(h, motion, w_zr, w_q, pre_zr, pre_q, pad)  # (1 − z)·h + z·q
         fh = h
         for m in dec.flow_pred.layers:
             fh = _cm(fh, m)

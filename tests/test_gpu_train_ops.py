@@ -279,3 +279,38 @@ def test_conv2d_nhwc_split_matches_whole():
         loss_c.backward()
         _close(xs.grad, xc.grad, 1e-6, 1e-7, "split conv dX")
         _close(ws.grad, wc.grad, 1e-6, 1e-7, "split conv dW")
+
+
+@pytest.mark.parametrize("k,pad", [((1, 5), (0, 2)), ((5, 1), (2, 0))])
+def test_gru_step_forward_backward(k, pad):
+    """One SepConvGRU direction as one autograd node (HIP convs + fused gate kernels) against
+    fp64 CPU autograd of the reference's formulation (raft_decoder.py:235-253): h', and the
+    gradients of h, x, both weights and both pre-activation maps."""
+    from scflow_amd.train.functions import gru_step
+    g = torch.Generator().manual_seed(21)
+    n, hh, ww, c, cx = 2, 32, 32, 128, 128
+    h = torch.tanh(torch.randn(n, hh, ww, c, generator=g))
+    x = torch.randn(n, hh, ww, cx, generator=g)
+    wzr = torch.randn(2 * c, c + cx, *k, generator=g) / np.sqrt((c + cx) * 5)
+    wq = torch.randn(c, c + cx, *k, generator=g) / np.sqrt((c + cx) * 5)
+    pzr = torch.randn(n, hh, ww, 2 * c, generator=g) * 0.5
+    pq = torch.randn(n, hh, ww, c, generator=g) * 0.5
+    leaves = [t.double().requires_grad_() for t in (h, x, wzr, wq, pzr, pq)]
+    hr, xr, wzrr, wqr, pzrr, pqr = leaves
+
+    def conv(a, b, w, m):
+        y = F.conv2d(torch.cat([a, b], -1).permute(0, 3, 1, 2), w, padding=pad).permute(0, 2, 3, 1)
+        return y + m
+    zr = torch.sigmoid(conv(hr, xr, wzrr, pzrr))
+    z, r = zr[..., :c], zr[..., c:]
+    q = torch.tanh(conv(r * hr, xr, wqr, pqr))
+    yr = (1 - z) * hr + z * q
+    gy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    (yr * gy).sum().backward()
+    dev = [t.cuda().requires_grad_() for t in (h, x, wzr, wq, pzr, pq)]
+    y = gru_step(*dev, pad)
+    (y * gy.float().cuda()).sum().backward()
+    torch.cuda.synchronize()
+    _close(y, yr.detach(), 1e-5, 1e-5 * np.sqrt(5 * (c + cx)), "h'")
+    for name, a_, r_ in zip(("h", "x", "w_zr", "w_q", "pre_zr", "pre_q"), dev, leaves):
+        _close(a_.grad, r_.grad, 1e-5, 1e-4 * np.sqrt(n * hh * ww), name)

@@ -55,7 +55,14 @@ def _patch_torch_ops(monkeypatch):
         out0.buf.view(-1, out0.buf.shape[-1])[:, out0.off:out0.off + 2] = f.permute(0, 2, 3, 1).reshape(-1, 2)
 
     monkeypatch.setattr(model, "conv2d_nhwc", conv)
-    monkeypatch.setattr(model, "conv2d_nhwc_split", conv_split)
+    def gru(h, x, w_zr, w_q, pre_zr, pre_q, pad):
+        c = h.shape[-1]
+        zr = conv(h, w_zr, None, 1, pad, "Sigmoid", x, pre_zr)
+        z, r = zr[..., :c], zr[..., c:]
+        q = conv(r * h, w_q, None, 1, pad, "Tanh", x, pre_q)
+        return torch.lerp(h, q, z)
+
+    monkeypatch.setattr(model, "gru_step", gru)
     monkeypatch.setattr(model, "linear", F.linear)
     monkeypatch.setattr(model, "upsample_bilinear_ac", lambda x, s: F.interpolate(
         x, scale_factor=(s, s), mode="bilinear", align_corners=True))
