@@ -482,10 +482,24 @@ def corr_pyramid(f1: Tensor, f2: Tensor, num_levels: int = 4) -> Tensor:
 
 
 class _CorrLookup(torch.autograd.Function):
+    """The pyramid is looked up once per refinement iteration; every iteration's backward
+    scatters into ONE gradient buffer shared through the pyramid tensor (zeroed once per step):
+    the first backward call hands that buffer to autograd, the later ones add into it in place
+    and hand over nothing — autograd runs the pyramid's backward only after all of them, so it
+    sees the complete sum, without a zeroed buffer and a full-size add per iteration."""
+
     @staticmethod
     def forward(ctx, pyr, flow_nhwc, n, h, w, num_levels, radius):
         flow_nhwc = flow_nhwc.contiguous()
         ctx.save_for_backward(flow_nhwc)
+        holder = getattr(pyr, "_scflow_dpyr", None)
+        if holder is None:
+            holder = {"buf": None}
+            try:
+                pyr._scflow_dpyr = holder
+            except (AttributeError, RuntimeError):
+                pass
+        ctx.holder = holder
         ctx.dims = (n, h, w, num_levels, radius, pyr.numel())
         out = torch.empty(n * h * w, num_levels * (2 * radius + 1) ** 2, device=pyr.device)
         ops.corr_lookup(pyr, flow_nhwc, n, h, w, num_levels, radius, out=Chan.whole(out),
@@ -496,9 +510,12 @@ class _CorrLookup(torch.autograd.Function):
     def backward(ctx, dout):
         (flow,) = ctx.saved_tensors
         n, h, w, L, r, size = ctx.dims
-        dpyr = torch.zeros(size, device=dout.device)
+        first = ctx.holder["buf"] is None
+        if first:
+            ctx.holder["buf"] = torch.zeros(size, device=dout.device)
+        dpyr = ctx.holder["buf"]
         ops.corr_lookup_backward(dout.contiguous().view(n * h * w, -1), flow, dpyr, n, h, w, L, r)
-        return dpyr, None, None, None, None, None, None
+        return (dpyr if first else None), None, None, None, None, None, None
 
 
 def corr_lookup(pyr: Tensor, flow_nhwc: Tensor, n: int, h: int, w: int, num_levels: int = 4,
