@@ -357,6 +357,27 @@ def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride
 
 
 # ------------------------------------------------------------------------------- ConvGRU step
+def _shared_grad_holder(w: Tensor) -> dict:
+    """A gradient accumulator shared by every use of the per-step tensor ``w`` (the GRU's
+    concatenated weights, used by all 8 iterations)."""
+    holder = getattr(w, "_scflow_gacc", None)
+    if holder is None:
+        holder = {"buf": None}
+        w._scflow_gacc = holder
+    return holder
+
+
+def _shared_wgrad(holder: dict, w: Tensor, add) -> Optional[Tensor]:
+    """Add this use's weight gradient into the shared buffer (``add(buf)``); the first backward
+    call hands the buffer to autograd, the later ones nothing — autograd runs the backward of
+    ``w``'s producer only after every use, so it receives the complete sum with no per-use adds."""
+    first = holder["buf"] is None
+    if first:
+        holder["buf"] = torch.zeros_like(w)
+    add(holder["buf"])
+    return holder["buf"] if first else None
+
+
 class _GruStep(torch.autograd.Function):
     """One SepConvGRU direction (raft_decoder.py:235-253) as one autograd node:
         zr = σ(conv([h, x]; w_zr) + pre_zr)      (z | r from one launch)
@@ -379,6 +400,7 @@ class _GruStep(torch.autograd.Function):
         h2 = ops.gru_gate_forward(zr, h, torch.empty_like(h), q=q)
         ctx.save_for_backward(h, x, zr, rh, q, w_zr, w_q)
         ctx.pad = pad
+        ctx.acc = (_shared_grad_holder(w_zr), _shared_grad_holder(w_q))
         return h2
 
     @staticmethod
@@ -392,11 +414,11 @@ class _GruStep(torch.autograd.Function):
         dha = torch.empty_like(h)
         ops.gru_gate_backward_q(dh2.contiguous(), zr, h, q, dq, dzr, dha)
         dxq = _conv_forward(dq, None, _flip_t(w_q), None, 1, (kh - 1 - ph, kw - 1 - pw))
-        dw_q, _ = _weight_grad(dq, rh, x, w_q, 1, ph, pw, False)
+        dw_q = _shared_wgrad(ctx.acc[1], w_q, lambda buf: _weight_grad(dq, rh, x, w_q, 1, ph, pw, False, dw=buf))
         dh = torch.empty_like(h)
         ops.gru_gate_backward_r(dxq[..., :c], zr, h, dha, dzr, dh)
         dxz = _conv_forward(dzr, None, _flip_t(w_zr), None, 1, (kh - 1 - ph, kw - 1 - pw))
-        dw_zr, _ = _weight_grad(dzr, h, x, w_zr, 1, ph, pw, False)
+        dw_zr = _shared_wgrad(ctx.acc[0], w_zr, lambda buf: _weight_grad(dzr, h, x, w_zr, 1, ph, pw, False, dw=buf))
         dh += dxz[..., :c]
         dx = dxq[..., c:] + dxz[..., c:]
         return dh, dx, dw_zr, dw_q, dzr, dq, None
