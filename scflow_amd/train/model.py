@@ -13,6 +13,7 @@ per-sample); FCs are plain library GEMMs.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Sequence, Tuple
 
 import torch
@@ -20,11 +21,12 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import (conv2d_nhwc, corr_lookup, corr_pyramid, gru_step, instance_norm_nhwc,
-                        linear, upsample_bilinear_ac)
+from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid, gru_step,
+                        instance_norm_nhwc, linear, upsample_bilinear_ac)
 from .losses import filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
+_GRU_FUSED = os.environ.get("SCFLOW_TRAIN_GRU_FUSED", "1") != "0"  # A/B switch (tuning)
 
 
 def _act(x: Tensor, act) -> Tensor:
@@ -188,7 +190,13 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
             out = _cm(out, m)
         motion = torch.cat([out, f2], -1)
         for (w_zr, w_q, pad), (pre_zr, pre_q) in zip(it_w, ctx_pre):  # SeqConv: 1×5 then 5×1
-            h = gru_step(h, motion, w_zr, w_q, pre_zr, pre_q, pad)  # (1 − z)·h + z·q
+            if _GRU_FUSED:
+                h = gru_step(h, motion, w_zr, w_q, pre_zr, pre_q, pad)  # (1 − z)·h + z·q
+            else:  # the same step as separate autograd ops (A/B reference)
+                z, rg = conv2d_nhwc_split(h, w_zr, hc, None, 1, pad, act="Sigmoid", x1=motion,
+                                          bias_map=pre_zr)
+                qq = conv2d_nhwc(rg * h, w_q, None, 1, pad, act="Tanh", x1=motion, bias_map=pre_q)
+                h = torch.lerp(h, qq, z)
         fh = h
         for m in dec.flow_pred.layers:
             fh = _cm(fh, m)

@@ -14,6 +14,7 @@ no DDP wrapper.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -23,6 +24,7 @@ from .functions import capture_cache, direct_weight_grads
 from .model import refiner_train_forward
 
 Tensor = torch.Tensor
+_MT_BACKWARD = os.environ.get("SCFLOW_TRAIN_MT_BACKWARD", "1") == "1"  # A/B switch (tuning)
 
 
 class GradBuckets:
@@ -146,9 +148,8 @@ class TrainStep:
     def _fwd_bwd(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         self.grads.zero()
         out = refiner_train_forward(self.refiner, batch, self.model_points, self.diam_t, self.iters)
-        # backward on the calling thread: the step's ~2000 autograd nodes are launch-bound host
-        # work, and the device thread's hand-offs cost more than they overlap
-        with torch.autograd.set_multithreading_enabled(False):
+        # SCFLOW_TRAIN_MT_BACKWARD=0 runs backward on the calling thread (measured equal)
+        with torch.autograd.set_multithreading_enabled(_MT_BACKWARD):
             if self.grads._hooks:  # per-parameter hooks must see every accumulation
                 out["loss"].backward()
             else:
