@@ -400,6 +400,11 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
  *   SCFlow (scflow_decoder.py:193-194), so no flow gradient. */
 int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh, int kw,
                   int stride, int ph, int pw, void* stream);
+/* scflow_knn1: idx[b][i] = argmin_j |gt[b][i] − pred[b][j]|² over [batch][P][3] / [batch][Q][3]
+ * point sets (first minimum in index order) — pytorch3d knn_points(K=1) in the symmetric-class
+ * point-matching loss (point_matching_loss.py:183-186; pytorch3d is absent, torch.argmin's rule). */
+int scflow_knn1(const float* gt, const float* pred, long long* idx, int batch, int P, int Q,
+                void* stream);
 /* SepConvGRU gate algebra of the training step (raft_decoder.py:235-253), channels-last,
  * c % 4 == 0, zr = the z | r conv's sigmoid output [npix][2c]:
  *   scflow_gru_gate_forward mode 0: out = r·h;  mode 1: out = h + z·(q − h)

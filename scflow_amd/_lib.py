@@ -204,6 +204,7 @@ SIGNATURES = {
     "scflow_conv_wgrad": (c_int, [ctypes.POINTER(WgradArgs), c_vp]),
     "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_vp]),
+    "scflow_knn1": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_gru_gate_forward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp]),
     "scflow_gru_gate_backward_q": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,
                                            c_int, c_vp]),

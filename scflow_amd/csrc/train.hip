@@ -932,12 +932,58 @@ __global__ void gru_bwd_r_kernel(const float* __restrict__ drh, int sdrh,
   }
 }
 
+// Nearest predicted point of every GT point (pytorch3d knn_points K=1 in the symmetric-class
+// point-matching loss, point_matching_loss.py:183-186): idx[b][i] = argmin_j Σ_d (g[b][i][d] −
+// q[b][j][d])², the first minimum in index order (torch.argmin's tie rule), the squared
+// distance summed d = 0, 1, 2 in order.  Workgroup = 256 GT points of one sample; the sample's
+// predicted points staged in LDS in chunks of 1024.
+__global__ __launch_bounds__(256) void knn1_kernel(const float* __restrict__ g,
+                                                   const float* __restrict__ q,
+                                                   long long* __restrict__ idx, int P, int Q) {
+#pragma clang fp contract(off)
+  __shared__ float qs[1024 * 3];
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  float gx = 0.f, gy = 0.f, gz = 0.f;
+  if (i < P) {
+    const float* gp = g + ((size_t)b * P + i) * 3;
+    gx = gp[0];
+    gy = gp[1];
+    gz = gp[2];
+  }
+  float best = 0.f;
+  int bi = -1;
+  for (int j0 = 0; j0 < Q; j0 += 1024) {
+    const int nq = Q - j0 < 1024 ? Q - j0 : 1024;
+    __syncthreads();
+    for (int t = threadIdx.x; t < nq * 3; t += 256) qs[t] = q[((size_t)b * Q + j0) * 3 + t];
+    __syncthreads();
+    for (int j = 0; j < nq; ++j) {
+      const float dx = gx - qs[3 * j], dy = gy - qs[3 * j + 1], dz = gz - qs[3 * j + 2];
+      const float d = dx * dx + dy * dy + dz * dz;
+      if (bi < 0 || d < best) {
+        best = d;
+        bi = j0 + j;
+      }
+    }
+  }
+  if (i < P) idx[(size_t)b * P + i] = bi;
+}
+
 int gru_grid(long long total4) {
   const long long b = (total4 + 255) / 256;
   return (int)(b < 8192 ? b : 8192);
 }
 
 }  // namespace
+
+SCFLOW_API int scflow_knn1(const float* gt, const float* pred, long long* idx, int batch, int P,
+                           int Q, void* stream) {
+  if (!gt || !pred || !idx || batch <= 0 || P <= 0 || Q <= 0) return SCFLOW_EINVAL;
+  const dim3 grid((unsigned)((P + 255) / 256), (unsigned)batch);
+  knn1_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(gt, pred, idx, P, Q);
+  return scflow_launch_status();
+}
 
 SCFLOW_API int scflow_gru_gate_forward(const float* zr, const float* h, const float* q, float* out,
                                        long long npix, int c, int mode, void* stream) {

@@ -798,6 +798,16 @@ def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, p
     return out
 
 
+def knn1(gt: Tensor, pred: Tensor) -> Tensor:
+    """[B, P] int64 index of the nearest ``pred`` point ([B, Q, 3]) of every ``gt`` point ([B, P, 3])."""
+    _require(gt, "gt")
+    _require(pred, "pred")
+    B, P, _ = gt.shape
+    idx = torch.empty(B, P, dtype=torch.int64, device=gt.device)
+    _launch("scflow_knn1", gt, _p(gt), _p(pred), _p(idx), B, P, pred.shape[1])
+    return idx
+
+
 def gru_gate_forward(zr: Tensor, h: Tensor, out: Tensor, q: Optional[Tensor] = None) -> Tensor:
     """SepConvGRU gate (training): out = r·h (q None) or h + z·(q − h); zr [..., 2c], h / q / out
     [..., c], channels-last contiguous."""

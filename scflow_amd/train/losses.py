@@ -15,6 +15,8 @@ from typing import Sequence, Tuple
 import torch
 import torch.nn.functional as F
 
+from .. import ops
+
 Tensor = torch.Tensor
 
 SYMMETRIC_CLASSES = (12, 15, 18, 19, 20)  # 0-based labels of cls_13, cls_16, cls_19, cls_20, cls_21 (config :34-40)
@@ -54,8 +56,11 @@ def _pm_terms(pts: Tensor, pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: T
     gt_rt = gt_rot + gt_t[:, None]
     pred_rot = matmul3(pts, pred_r.transpose(1, 2)) + gt_t[:, None]
     if sym is not None:  # symmetric samples: nearest predicted point per GT point (no host sync)
-        with torch.no_grad():  # squared distances by broadcasting (knn_points' metric, no GEMM)
-            idx = ((gt_rt[:, :, None] - pred_rot[:, None]) ** 2).sum(-1).argmin(-1)  # [B, P]
+        with torch.no_grad():  # knn_points' squared distance; HIP kernel on the device
+            if gt_rt.is_cuda:
+                idx = ops.knn1(gt_rt.float().contiguous(), pred_rot.float().contiguous())
+            else:
+                idx = ((gt_rt[:, :, None] - pred_rot[:, None]) ** 2).sum(-1).argmin(-1)  # [B, P]
         matched = torch.gather(pred_rot, 1, idx[..., None].expand(-1, -1, 3))
         pred_rot = torch.where(sym[:, None, None], matched, pred_rot)
     l_rot = (pred_rot - gt_rt).abs().sum(-1).mean(-1)

@@ -314,3 +314,18 @@ def test_gru_step_forward_backward(k, pad):
     _close(y, yr.detach(), 1e-5, 1e-5 * np.sqrt(5 * (c + cx)), "h'")
     for name, a_, r_ in zip(("h", "x", "w_zr", "w_q", "pre_zr", "pre_q"), dev, leaves):
         _close(a_.grad, r_.grad, 1e-5, 1e-4 * np.sqrt(n * hh * ww), name)
+
+
+def test_knn1_matches_argmin():
+    """scflow_knn1 (symmetric-class point matching) equals torch's broadcast distances + argmin,
+    ties included (duplicated predicted points: the first index wins), Q over one LDS chunk."""
+    from scflow_amd import ops
+    g = torch.Generator().manual_seed(31)
+    B, P, Q = 3, 700, 1500
+    gt = torch.randn(B, P, 3, generator=g) * 50
+    pred = torch.randn(B, Q, 3, generator=g) * 50
+    pred[:, 1100:1200] = pred[:, 100:200]  # exact duplicates later in index order
+    gt[:, :50] = pred[:, 150:200]          # exact hits on duplicated points
+    ref = ((gt[:, :, None] - pred[:, None]) ** 2).sum(-1).argmin(-1)
+    idx = ops.knn1(gt.cuda(), pred.cuda()).cpu()
+    assert torch.equal(idx, ref)
