@@ -10,6 +10,7 @@ knn_points).
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence, Tuple
 
 import torch
@@ -21,6 +22,7 @@ Tensor = torch.Tensor
 
 SYMMETRIC_CLASSES = (12, 15, 18, 19, 20)  # 0-based labels of cls_13, cls_16, cls_19, cls_20, cls_21 (config :34-40)
 POSE_WEIGHT, FLOW_WEIGHT, MASK_WEIGHT, GAMMA = 10.0, 0.1, 10.0, 0.8
+_KNN_TORCH = os.environ.get("SCFLOW_TRAIN_KNN_TORCH", "0") == "1"  # A/B switch (tuning)
 
 
 def flow_valid(gt: Tensor, valid: Tensor, max_flow: float = 400.) -> Tensor:
@@ -57,7 +59,7 @@ def _pm_terms(pts: Tensor, pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: T
     pred_rot = matmul3(pts, pred_r.transpose(1, 2)) + gt_t[:, None]
     if sym is not None:  # symmetric samples: nearest predicted point per GT point (no host sync)
         with torch.no_grad():  # knn_points' squared distance; HIP kernel on the device
-            if gt_rt.is_cuda:
+            if gt_rt.is_cuda and not _KNN_TORCH:
                 idx = ops.knn1(gt_rt.float().contiguous(), pred_rot.float().contiguous())
             else:
                 idx = ((gt_rt[:, :, None] - pred_rot[:, None]) ** 2).sum(-1).argmin(-1)  # [B, P]
