@@ -400,6 +400,14 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
  *   SCFlow (scflow_decoder.py:193-194), so no flow gradient. */
 int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh, int kw,
                   int stride, int ph, int pw, void* stream);
+/* scflow_pose_update6_train: the training step's pose update for an ortho6d Δrotation
+ * (pose.py:124-169), forward (backward = 0: o0 = Rn [n][3][3], o1 = tn [n][3]) or its gradient
+ * (backward = 1, given gRn, gtn: o0 = g drot [n][6], o1 = g dt [n][3], o2 = g R, o3 = g t);
+ * depth_exp: depth_transform 'exp' (else 'linear'); detach_xy: detach_depth_for_xy. */
+int scflow_pose_update6_train(const float* drot, const float* dt, const float* R, const float* t,
+                              const float* gRn, const float* gtn, float* o0, float* o1, float* o2,
+                              float* o3, int n, float weight, int depth_exp, int detach_xy,
+                              int backward, void* stream);
 /* scflow_knn1: idx[b][i] = argmin_j |gt[b][i] − pred[b][j]|² over [batch][P][3] / [batch][Q][3]
  * point sets (first minimum in index order) — pytorch3d knn_points(K=1) in the symmetric-class
  * point-matching loss (point_matching_loss.py:183-186; pytorch3d is absent, torch.argmin's rule). */

@@ -204,6 +204,8 @@ SIGNATURES = {
     "scflow_conv_wgrad": (c_int, [ctypes.POINTER(WgradArgs), c_vp]),
     "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_vp]),
+    "scflow_pose_update6_train": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                          c_int, c_float, c_int, c_int, c_int, c_vp]),
     "scflow_knn1": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_gru_gate_forward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp]),
     "scflow_gru_gate_backward_q": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,

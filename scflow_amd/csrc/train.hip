@@ -970,12 +970,121 @@ __global__ __launch_bounds__(256) void knn1_kernel(const float* __restrict__ g,
   if (i < P) idx[(size_t)b * P + i] = bi;
 }
 
+// Training-step pose update for the ortho6d Δrotation (pose.py:124-169 — get_pose_from_delta_pose
+// with get_rotation_matrix_from_ortho6d; what train/model.py:pose_update computes with ~30 tiny
+// torch ops forward and ~60 backward), one thread per sample:
+//   x = a/|a|, z = (x × b)/|x × b|, y = z × x (|·| clamped at 1e-12), Rn = [x y z]·R,
+//   vz = t2·e^(−dt2) ('exp') or t2·(dt2 + 1), v_xy = vz'·(dt_xy/weight + t_xy/t2) (vz' = vz, its
+//   gradient cut when detach_xy), tn = (vx, vy, vz).
+// The backward recomputes the forward and applies the chain rule by hand (normalise:
+// g_v = (g_u − u·(u·g_u))/|v|; cross c = p × q: g_p = q × g_c, g_q = g_c × p).
+struct Vec3 { float x, y, z; };
+__device__ __forceinline__ Vec3 v3(const float* p) { return {p[0], p[1], p[2]}; }
+__device__ __forceinline__ Vec3 cross3(Vec3 a, Vec3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ float dot3(Vec3 a, Vec3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float norm3(Vec3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ Vec3 scale3(Vec3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ Vec3 add3(Vec3 a, Vec3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ Vec3 div3(Vec3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ float comp(Vec3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+// gradient of u = v / max(|v|, 1e-12) given g_u
+__device__ __forceinline__ Vec3 norm_back(Vec3 u, float nv, Vec3 gu) {
+  if (nv < 1e-12f) return div3(gu, 1e-12f);
+  const float d = dot3(u, gu);
+  return div3({gu.x - u.x * d, gu.y - u.y * d, gu.z - u.z * d}, nv);
+}
+
+__global__ void pose_update6_kernel(const float* __restrict__ drot, const float* __restrict__ dt,
+                                    const float* __restrict__ R, const float* __restrict__ t,
+                                    const float* __restrict__ gRn, const float* __restrict__ gtn,
+                                    float* __restrict__ o0, float* __restrict__ o1,
+                                    float* __restrict__ o2, float* __restrict__ o3, int n,
+                                    float weight, int depth_exp, int detach_xy, int backward) {
+#pragma clang fp contract(off)
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const Vec3 a = v3(drot + s * 6), b = v3(drot + s * 6 + 3);
+  const float na = norm3(a), nac = na < 1e-12f ? 1e-12f : na;
+  const Vec3 x = div3(a, nac);
+  const Vec3 c = cross3(x, b);
+  const float nc = norm3(c), ncc = nc < 1e-12f ? 1e-12f : nc;
+  const Vec3 z = div3(c, ncc);
+  const Vec3 y = cross3(z, x);
+  const float* Rs = R + s * 9;
+  const float* ts = t + s * 3;
+  const float* ds = dt + s * 3;
+  const float e = depth_exp ? expf(ds[2]) : 0.f;
+  const float vz = depth_exp ? ts[2] / e : ts[2] * (ds[2] + 1.f);
+  const float fx = ds[0] / weight + ts[0] / ts[2], fy = ds[1] / weight + ts[1] / ts[2];
+  if (!backward) {  // o0 = Rn [3][3], o1 = tn [3]
+    for (int i = 0; i < 3; ++i) {
+      const float m0 = comp(x, i), m1 = comp(y, i), m2 = comp(z, i);
+      for (int k = 0; k < 3; ++k) o0[s * 9 + i * 3 + k] = (m0 * Rs[k] + m1 * Rs[3 + k]) + m2 * Rs[6 + k];
+    }
+    o1[s * 3 + 0] = vz * fx;
+    o1[s * 3 + 1] = vz * fy;
+    o1[s * 3 + 2] = vz;
+    return;
+  }
+  // backward: o0 = g drot [6], o1 = g dt [3], o2 = g R [3][3], o3 = g t [3]
+  const float* G = gRn + s * 9;
+  Vec3 gx, gy, gz;  // g M[:, j] = Σ_k gRn[i][k]·R[j][k]
+  float gm[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      gm[i][j] = (G[i * 3 + 0] * Rs[j * 3 + 0] + G[i * 3 + 1] * Rs[j * 3 + 1]) + G[i * 3 + 2] * Rs[j * 3 + 2];
+  gx = {gm[0][0], gm[1][0], gm[2][0]};
+  gy = {gm[0][1], gm[1][1], gm[2][1]};
+  gz = {gm[0][2], gm[1][2], gm[2][2]};
+  for (int j = 0; j < 3; ++j)  // g R[j][k] = Σ_i M[i][j]·gRn[i][k]
+    for (int k = 0; k < 3; ++k) {
+      const Vec3 col = j == 0 ? x : (j == 1 ? y : z);
+      o2[s * 9 + j * 3 + k] = (col.x * G[0 * 3 + k] + col.y * G[1 * 3 + k]) + col.z * G[2 * 3 + k];
+    }
+  gz = add3(gz, cross3(x, gy));  // y = z × x
+  gx = add3(gx, cross3(gy, z));
+  const Vec3 gc = norm_back(z, nc, gz);  // z = c / |c|
+  gx = add3(gx, cross3(b, gc));  // c = x × b
+  const Vec3 gb = cross3(gc, x);
+  const Vec3 ga = norm_back(x, na, gx);  // x = a / |a|
+  float* gd = o0 + s * 6;
+  gd[0] = ga.x; gd[1] = ga.y; gd[2] = ga.z; gd[3] = gb.x; gd[4] = gb.y; gd[5] = gb.z;
+  const float gvx = gtn[s * 3 + 0], gvy = gtn[s * 3 + 1], gvz = gtn[s * 3 + 2];
+  float gt0 = gvx * vz / ts[2], gt1 = gvy * vz / ts[2];
+  float gt2 = gvx * vz * (-ts[0] / (ts[2] * ts[2])) + gvy * vz * (-ts[1] / (ts[2] * ts[2]));
+  const float gvz_all = gvz + (detach_xy ? 0.f : gvx * fx + gvy * fy);
+  const float dvz_ddt = depth_exp ? -vz : ts[2];
+  const float dvz_dt2 = depth_exp ? 1.f / e : ds[2] + 1.f;
+  o1[s * 3 + 0] = gvx * vz / weight;
+  o1[s * 3 + 1] = gvy * vz / weight;
+  o1[s * 3 + 2] = gvz_all * dvz_ddt;
+  gt2 += gvz_all * dvz_dt2;
+  o3[s * 3 + 0] = gt0;
+  o3[s * 3 + 1] = gt1;
+  o3[s * 3 + 2] = gt2;
+}
+
 int gru_grid(long long total4) {
   const long long b = (total4 + 255) / 256;
   return (int)(b < 8192 ? b : 8192);
 }
 
 }  // namespace
+
+SCFLOW_API int scflow_pose_update6_train(const float* drot, const float* dt, const float* R,
+                                         const float* t, const float* gRn, const float* gtn,
+                                         float* o0, float* o1, float* o2, float* o3, int n,
+                                         float weight, int depth_exp, int detach_xy, int backward,
+                                         void* stream) {
+  if (!drot || !dt || !R || !t || !o0 || !o1 || n <= 0 || weight == 0.f ||
+      (backward && (!gRn || !gtn || !o2 || !o3)))
+    return SCFLOW_EINVAL;
+  pose_update6_kernel<<<(n + 63) / 64, 64, 0, (hipStream_t)stream>>>(
+      drot, dt, R, t, gRn, gtn, o0, o1, o2, o3, n, weight, depth_exp, detach_xy, backward);
+  return scflow_launch_status();
+}
 
 SCFLOW_API int scflow_knn1(const float* gt, const float* pred, long long* idx, int batch, int P,
                            int Q, void* stream) {

@@ -798,6 +798,27 @@ def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, p
     return out
 
 
+def pose_update6_train(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float, depth_exp: bool,
+                       detach_xy: bool, grads: Optional[Tuple[Tensor, Tensor]] = None):
+    """Forward (Rn, tn) or, given grads = (gRn, gtn), the backward (g drot, g dt, g R, g t) of the
+    training step's ortho6d pose update (scflow_pose_update6_train)."""
+    for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t)):
+        _require(x, nm)
+    n = drot.shape[0]
+    if grads is None:
+        Rn = torch.empty(n, 3, 3, device=drot.device)
+        tn = torch.empty(n, 3, device=drot.device)
+        _launch("scflow_pose_update6_train", drot, _p(drot), _p(dt), _p(R), _p(t), None, None, _p(Rn),
+                _p(tn), None, None, n, float(weight), int(depth_exp), int(detach_xy), 0)
+        return Rn, tn
+    gRn, gtn = grads
+    out = [torch.empty(n, 6, device=drot.device), torch.empty(n, 3, device=drot.device),
+           torch.empty(n, 3, 3, device=drot.device), torch.empty(n, 3, device=drot.device)]
+    _launch("scflow_pose_update6_train", drot, _p(drot), _p(dt), _p(R), _p(t), _p(gRn), _p(gtn),
+            *[_p(o) for o in out], n, float(weight), int(depth_exp), int(detach_xy), 1)
+    return tuple(out)
+
+
 def knn1(gt: Tensor, pred: Tensor) -> Tensor:
     """[B, P] int64 index of the nearest ``pred`` point ([B, Q, 3]) of every ``gt`` point ([B, P, 3])."""
     _require(gt, "gt")

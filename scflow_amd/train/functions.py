@@ -432,6 +432,33 @@ def gru_step(h: Tensor, x: Tensor, w_zr: Tensor, w_q: Tensor, pre_zr: Tensor, pr
     return _GruStep.apply(h, x, w_zr, w_q, pre_zr, pre_q, pad)
 
 
+# ------------------------------------------------------------------------------- pose update
+class _PoseUpdate6(torch.autograd.Function):
+    """get_pose_from_delta_pose with the ortho6d rotation (pose.py:124-169) as one HIP kernel
+    forward and one backward (chain rule by hand) instead of ~90 tiny autograd kernels."""
+
+    @staticmethod
+    def forward(ctx, drot, dt, R, t, weight, depth_exp, detach_xy):
+        drot, dt, R, t = (v.contiguous().float() for v in (drot, dt, R, t))
+        ctx.save_for_backward(drot, dt, R, t)
+        ctx.cfg = (weight, depth_exp, detach_xy)
+        return ops.pose_update6_train(drot, dt, R, t, weight, depth_exp, detach_xy)
+
+    @staticmethod
+    def backward(ctx, gRn, gtn):
+        drot, dt, R, t = ctx.saved_tensors
+        gRn = torch.zeros_like(R) if gRn is None else gRn.contiguous()
+        gtn = torch.zeros_like(t) if gtn is None else gtn.contiguous()
+        gd, gdt, gR, gt = ops.pose_update6_train(drot, dt, R, t, *ctx.cfg, grads=(gRn, gtn))
+        return gd, gdt, gR, gt, None, None, None
+
+
+def pose_update6(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 10.0,
+                 depth_exp: bool = True, detach_xy: bool = True):
+    """(R_new [n,3,3], t_new [n,3]) from an ortho6d Δrotation [n,6] and Δt [n,3] (HIP fwd + bwd)."""
+    return _PoseUpdate6.apply(drot, dt, R, t, float(weight), bool(depth_exp), bool(detach_xy))
+
+
 # ------------------------------------------------------------------------------- norms
 class _InstanceNormNHWC(torch.autograd.Function):
     """InstanceNorm2d(affine=False) (+ ReLU) of a channels-last [N, H, W, C] tensor on HIP kernels:

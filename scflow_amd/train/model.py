@@ -22,7 +22,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import Chan
 from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid, gru_step,
-                        instance_norm_nhwc, linear, upsample_bilinear_ac)
+                        instance_norm_nhwc, linear, pose_update6, upsample_bilinear_ac)
 from .losses import filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
@@ -114,6 +114,8 @@ def pose_update(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: float = 
                 depth_transform: str = "exp", detach_depth_for_xy: bool = True) -> Tuple[Tensor, Tensor]:
     """get_pose_from_delta_pose + get_rotation_matrix_from_ortho6d (pose.py:124-169); a [n, 4]
     drot is a quaternion (x, y, z, w; pose.py:132-133, see oracle.rotation_from_quaternion_xyzw)."""
+    if drot.shape[1] == 6 and drot.is_cuda and depth_transform in ("exp", "linear"):
+        return pose_update6(drot, dt, R, t, weight, depth_transform == "exp", detach_depth_for_xy)
     if drot.shape[1] == 4:
         q = drot / drot.norm(dim=1, keepdim=True).clamp_min(1e-12)
         qx, qy, qz, qw = q[:, 0], q[:, 1], q[:, 2], q[:, 3]

@@ -329,3 +329,32 @@ def test_knn1_matches_argmin():
     ref = ((gt[:, :, None] - pred[:, None]) ** 2).sum(-1).argmin(-1)
     idx = ops.knn1(gt.cuda(), pred.cuda()).cpu()
     assert torch.equal(idx, ref)
+
+
+@pytest.mark.parametrize("depth,detach_xy", [("exp", True), ("linear", False)])
+def test_pose_update6_forward_backward(depth, detach_xy):
+    """The HIP ortho6d pose update (forward + hand-written backward) against fp64 autograd of
+    the torch formulation (train/model.py:pose_update, pose.py:124-169), gradients of Δrot, Δt,
+    R and t."""
+    from scflow_amd.train import model as tm
+    from scflow_amd.train.functions import pose_update6
+    g = torch.Generator().manual_seed(41)
+    n = 16
+    drot = torch.randn(n, 6, generator=g)
+    dt = torch.randn(n, 3, generator=g) * 0.1
+    q, _ = torch.linalg.qr(torch.randn(n, 3, 3, generator=g))
+    R = q
+    t = torch.cat([torch.randn(n, 2, generator=g) * 50, 500 + 200 * torch.rand(n, 1, generator=g)], 1)
+    leaves = [v.double().requires_grad_() for v in (drot, dt, R, t)]
+    Rr, tr = tm.pose_update(*leaves, depth_transform=depth, detach_depth_for_xy=detach_xy)
+    gR = torch.randn(n, 3, 3, generator=g, dtype=torch.float64)
+    gt = torch.randn(n, 3, generator=g, dtype=torch.float64)
+    ((Rr * gR).sum() + (tr * gt).sum()).backward()
+    dev = [v.cuda().requires_grad_() for v in (drot, dt, R, t)]
+    Rn, tn = pose_update6(*dev, 10.0, depth == "exp", detach_xy)
+    ((Rn * gR.float().cuda()).sum() + (tn * gt.float().cuda()).sum()).backward()
+    torch.cuda.synchronize()
+    _close(Rn, Rr.detach(), 1e-5, 1e-5, "R_new")
+    _close(tn, tr.detach(), 1e-5, 1e-4, "t_new")
+    for name, a_, r_ in zip(("drot", "dt", "R", "t"), dev, leaves):
+        _close(a_.grad, r_.grad, 1e-4, 1e-5, name)
