@@ -408,6 +408,22 @@ int scflow_pose_update6_train(const float* drot, const float* dt, const float* R
                               const float* gRn, const float* gtn, float* o0, float* o1, float* o2,
                               float* o3, int n, float weight, int depth_exp, int detach_xy,
                               int backward, void* stream);
+/* scflow_pm_loss / scflow_pm_loss_backward: one refinement iteration's disentangled L1
+ * point-matching loss (point_matching_loss.py:159-218, disentangle_z, mean) fused — model points
+ * pts [B][P][3] (each sample's class's set), rotations [B][3][3], translations [B][3], sym [B]
+ * (1.0 = symmetric class: nearest-point matching as scflow_knn1; NULL = none), diam [B];
+ * workspace gt_rt, pred_rot [B][P][3], idx [B][P]; loss = weight·Σ_b l_b/diam_b/B (one float).
+ * The backward takes the loss gradient (one float, device) and the forward's workspace and
+ * writes g_pred_r [B][3][3], g_pred_t [B][3]. */
+int scflow_pm_loss(const float* pts, const float* gt_r, const float* gt_t, const float* pred_r,
+                   const float* pred_t, const float* sym, const float* diam, float* gt_rt,
+                   float* pred_rot, long long* idx, float* loss, int B, int P, float weight,
+                   void* stream);
+int scflow_pm_loss_backward(const float* gloss, const float* pts, const float* gt_rt,
+                            const float* pred_rot, const long long* idx, const float* sym,
+                            const float* pred_t, const float* gt_t, const float* diam,
+                            float* g_pred_r, float* g_pred_t, int B, int P, float weight,
+                            void* stream);
 /* scflow_knn1: idx[b][i] = argmin_j |gt[b][i] − pred[b][j]|² over [batch][P][3] / [batch][Q][3]
  * point sets (first minimum in index order) — pytorch3d knn_points(K=1) in the symmetric-class
  * point-matching loss (point_matching_loss.py:183-186; pytorch3d is absent, torch.argmin's rule). */

@@ -206,6 +206,10 @@ SIGNATURES = {
                               c_int, c_vp]),
     "scflow_pose_update6_train": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           c_int, c_float, c_int, c_int, c_int, c_vp]),
+    "scflow_pm_loss": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_int, c_int, c_float, c_vp]),
+    "scflow_pm_loss_backward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp, c_int, c_int, c_float, c_vp]),
     "scflow_knn1": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_gru_gate_forward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp]),
     "scflow_gru_gate_backward_q": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,

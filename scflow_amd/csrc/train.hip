@@ -1066,6 +1066,110 @@ __global__ void pose_update6_kernel(const float* __restrict__ drot, const float*
   o3[s * 3 + 2] = gt2;
 }
 
+// Disentangled point-matching loss of one refinement iteration (DisentanglePointMatchingLoss,
+// point_matching_loss.py:159-218: l1, disentangle_z, reduction mean), fused:
+//   pm_points: gt_rt[b][p] = R_gt·x + t_gt, pred_rot[b][p] = R_pred·x + t_gt (x = the sample's model
+//              point; rotation by the torch matmul3 order Σ_j in j order);
+//   pm_loss:   l_rot = mean_p Σ_d |pred_rot[m] − gt_rt[p]| (m = the nearest predicted point of p
+//              for symmetric samples, else p), l_z = |t_pred,z − t_gt,z|, l_xy = Σ_{x,y} |…|,
+//              loss = weight · Σ_b (l_rot + l_z + l_xy)/diam_b / B — one workgroup, fixed order;
+//   pm_grad:   g R_pred[b] = c_b/P · Σ_p sgn(pred_rot[m] − gt_rt[p]) ⊗ x[m], g t_pred = c_b·sgn(Δt)
+//              with c_b = g_loss · weight / (B · diam_b) (sgn 0 = 0, as torch's abs backward).
+__global__ void pm_points_kernel(const float* __restrict__ pts, const float* __restrict__ gr,
+                                 const float* __restrict__ gtt, const float* __restrict__ pr,
+                                 float* __restrict__ gt_rt, float* __restrict__ pred_rot, int B,
+                                 int P) {
+#pragma clang fp contract(off)
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= (long long)B * P) return;
+  const int b = (int)(i / P);
+  const float* x = pts + i * 3;
+  const float* G = gr + b * 9;
+  const float* Q = pr + b * 9;
+  const float* tg = gtt + b * 3;
+  for (int k = 0; k < 3; ++k) {
+    const float gk = (x[0] * G[k * 3 + 0] + x[1] * G[k * 3 + 1]) + x[2] * G[k * 3 + 2];
+    const float pk = (x[0] * Q[k * 3 + 0] + x[1] * Q[k * 3 + 1]) + x[2] * Q[k * 3 + 2];
+    gt_rt[i * 3 + k] = gk + tg[k];
+    pred_rot[i * 3 + k] = pk + tg[k];
+  }
+}
+
+__device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
+
+__global__ __launch_bounds__(256) void pm_loss_kernel(
+    const float* __restrict__ gt_rt, const float* __restrict__ pred_rot,
+    const long long* __restrict__ idx, const float* __restrict__ sym, const float* __restrict__ pt,
+    const float* __restrict__ gtt, const float* __restrict__ diam, float* __restrict__ loss, int B,
+    int P, float weight) {
+#pragma clang fp contract(off)
+  __shared__ float red[256];
+  float total = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const bool s = sym && sym[b] != 0.f;
+    float acc = 0.f;
+    for (int p = threadIdx.x; p < P; p += 256) {
+      const long long m = s ? idx[(size_t)b * P + p] : p;
+      const float* a = pred_rot + ((size_t)b * P + m) * 3;
+      const float* g = gt_rt + ((size_t)b * P + p) * 3;
+      acc += (fabsf(a[0] - g[0]) + fabsf(a[1] - g[1])) + fabsf(a[2] - g[2]);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const float lrot = red[0] / (float)P;
+      const float lz = fabsf(pt[b * 3 + 2] - gtt[b * 3 + 2]);
+      const float lxy = fabsf(pt[b * 3 + 0] - gtt[b * 3 + 0]) + fabsf(pt[b * 3 + 1] - gtt[b * 3 + 1]);
+      total += ((lrot + lz) + lxy) / diam[b];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = weight * total / (float)B;
+}
+
+__global__ __launch_bounds__(256) void pm_grad_kernel(
+    const float* __restrict__ gloss, const float* __restrict__ pts, const float* __restrict__ gt_rt,
+    const float* __restrict__ pred_rot, const long long* __restrict__ idx,
+    const float* __restrict__ sym, const float* __restrict__ pt, const float* __restrict__ gtt,
+    const float* __restrict__ diam, float* __restrict__ gR, float* __restrict__ gT, int B, int P,
+    float weight) {
+#pragma clang fp contract(off)
+  __shared__ float red[9][256];
+  const int b = blockIdx.x;
+  const bool s = sym && sym[b] != 0.f;
+  const float cb = gloss[0] * weight / ((float)B * diam[b]);
+  float acc[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) acc[q] = 0.f;
+  for (int p = threadIdx.x; p < P; p += 256) {
+    const long long m = s ? idx[(size_t)b * P + p] : p;
+    const float* a = pred_rot + ((size_t)b * P + m) * 3;
+    const float* g = gt_rt + ((size_t)b * P + p) * 3;
+    const float* x = pts + ((size_t)b * P + m) * 3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float sg = sgnf(a[i] - g[i]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[i * 3 + j] += sg * x[j];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+#pragma unroll
+      for (int q = 0; q < 9; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 9) gR[b * 9 + threadIdx.x] = cb / (float)P * red[threadIdx.x][0];
+  if (threadIdx.x < 3) gT[b * 3 + threadIdx.x] = cb * sgnf(pt[b * 3 + threadIdx.x] - gtt[b * 3 + threadIdx.x]);
+}
+
 int gru_grid(long long total4) {
   const long long b = (total4 + 255) / 256;
   return (int)(b < 8192 ? b : 8192);
@@ -1083,6 +1187,39 @@ SCFLOW_API int scflow_pose_update6_train(const float* drot, const float* dt, con
     return SCFLOW_EINVAL;
   pose_update6_kernel<<<(n + 63) / 64, 64, 0, (hipStream_t)stream>>>(
       drot, dt, R, t, gRn, gtn, o0, o1, o2, o3, n, weight, depth_exp, detach_xy, backward);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_pm_loss(const float* pts, const float* gt_r, const float* gt_t,
+                              const float* pred_r, const float* pred_t, const float* sym,
+                              const float* diam, float* gt_rt, float* pred_rot, long long* idx,
+                              float* loss, int B, int P, float weight, void* stream) {
+  if (!pts || !gt_r || !gt_t || !pred_r || !pred_t || !diam || !gt_rt || !pred_rot || !loss ||
+      (sym && !idx) || B <= 0 || P <= 0)
+    return SCFLOW_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = (long long)B * P;
+  pm_points_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(pts, gt_r, gt_t, pred_r, gt_rt,
+                                                                pred_rot, B, P);
+  if (sym) {
+    const dim3 grid((unsigned)((P + 255) / 256), (unsigned)B);
+    knn1_kernel<<<grid, 256, 0, st>>>(gt_rt, pred_rot, idx, P, P);
+  }
+  pm_loss_kernel<<<1, 256, 0, st>>>(gt_rt, pred_rot, idx, sym, pred_t, gt_t, diam, loss, B, P,
+                                    weight);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_pm_loss_backward(const float* gloss, const float* pts, const float* gt_rt,
+                                       const float* pred_rot, const long long* idx,
+                                       const float* sym, const float* pred_t, const float* gt_t,
+                                       const float* diam, float* g_pred_r, float* g_pred_t, int B,
+                                       int P, float weight, void* stream) {
+  if (!gloss || !pts || !gt_rt || !pred_rot || (sym && !idx) || !pred_t || !gt_t || !diam ||
+      !g_pred_r || !g_pred_t || B <= 0 || P <= 0)
+    return SCFLOW_EINVAL;
+  pm_grad_kernel<<<B, 256, 0, (hipStream_t)stream>>>(gloss, pts, gt_rt, pred_rot, idx, sym, pred_t,
+                                                     gt_t, diam, g_pred_r, g_pred_t, B, P, weight);
   return scflow_launch_status();
 }
 

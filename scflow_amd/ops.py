@@ -819,6 +819,34 @@ def pose_update6_train(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, weight: f
     return tuple(out)
 
 
+def pm_loss(pts: Tensor, gt_r: Tensor, gt_t: Tensor, pred_r: Tensor, pred_t: Tensor,
+            sym: Optional[Tensor], diam: Tensor, weight: float):
+    """Fused point-matching loss of one iteration (scflow_pm_loss): (loss [1], workspace) where
+    workspace = (gt_rt, pred_rot, idx) feeds pm_loss_backward."""
+    B, P, _ = pts.shape
+    for nm, x in (("pts", pts), ("gt_r", gt_r), ("gt_t", gt_t), ("pred_r", pred_r), ("pred_t", pred_t),
+                  ("diam", diam)):
+        _require(x, nm)
+    gt_rt = torch.empty(B, P, 3, device=pts.device)
+    pred_rot = torch.empty(B, P, 3, device=pts.device)
+    idx = torch.empty(B, P, dtype=torch.int64, device=pts.device) if sym is not None else None
+    loss = torch.empty(1, device=pts.device)
+    _launch("scflow_pm_loss", pts, _p(pts), _p(gt_r), _p(gt_t), _p(pred_r), _p(pred_t), _p(sym), _p(diam),
+            _p(gt_rt), _p(pred_rot), _p(idx), _p(loss), B, P, float(weight))
+    return loss, (gt_rt, pred_rot, idx)
+
+
+def pm_loss_backward(gloss: Tensor, pts: Tensor, ws, sym: Optional[Tensor], pred_t: Tensor,
+                     gt_t: Tensor, diam: Tensor, weight: float) -> Tuple[Tensor, Tensor]:
+    gt_rt, pred_rot, idx = ws
+    B, P, _ = pts.shape
+    g_r = torch.empty(B, 3, 3, device=pts.device)
+    g_t = torch.empty(B, 3, device=pts.device)
+    _launch("scflow_pm_loss_backward", pts, _p(gloss), _p(pts), _p(gt_rt), _p(pred_rot), _p(idx), _p(sym),
+            _p(pred_t), _p(gt_t), _p(diam), _p(g_r), _p(g_t), B, P, float(weight))
+    return g_r, g_t
+
+
 def knn1(gt: Tensor, pred: Tensor) -> Tensor:
     """[B, P] int64 index of the nearest ``pred`` point ([B, Q, 3]) of every ``gt`` point ([B, P, 3])."""
     _require(gt, "gt")

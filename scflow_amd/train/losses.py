@@ -23,6 +23,7 @@ Tensor = torch.Tensor
 SYMMETRIC_CLASSES = (12, 15, 18, 19, 20)  # 0-based labels of cls_13, cls_16, cls_19, cls_20, cls_21 (config :34-40)
 POSE_WEIGHT, FLOW_WEIGHT, MASK_WEIGHT, GAMMA = 10.0, 0.1, 10.0, 0.8
 _KNN_TORCH = os.environ.get("SCFLOW_TRAIN_KNN_TORCH", "0") == "1"  # A/B switch (tuning)
+_PM_TORCH = os.environ.get("SCFLOW_TRAIN_PM_TORCH", "0") == "1"    # A/B switch (tuning)
 
 
 def flow_valid(gt: Tensor, valid: Tensor, max_flow: float = 400.) -> Tensor:
@@ -73,9 +74,35 @@ def _pm_terms(pts: Tensor, pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: T
     return l_rot + l_z + l_xy
 
 
+class _PointMatchingLoss(torch.autograd.Function):
+    """The disentangled L1 point-matching loss of one iteration as three HIP launches forward
+    (points, nearest-point matching, loss) and one backward (scflow_pm_loss), instead of ~25
+    torch kernels forward and ~40 backward; gradients w.r.t. the predicted rotation and
+    translation (the GT pose and the model points carry none)."""
+
+    @staticmethod
+    def forward(ctx, pred_r, pred_t, gt_r, gt_t, pts, sym, diam, weight):
+        pred_r, pred_t = pred_r.contiguous().float(), pred_t.contiguous().float()
+        loss, ws = ops.pm_loss(pts, gt_r, gt_t, pred_r, pred_t, sym, diam, weight)
+        ctx.save_for_backward(pts, pred_t, gt_t, diam, *[w for w in ws if w is not None])
+        ctx.has_sym = sym is not None
+        ctx.sym = sym
+        ctx.weight = weight
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        pts, pred_t, gt_t, diam, gt_rt, pred_rot, *rest = ctx.saved_tensors
+        idx = rest[0] if ctx.has_sym else None
+        g_r, g_t = ops.pm_loss_backward(g.reshape(1).contiguous().float(), pts, (gt_rt, pred_rot, idx),
+                                        ctx.sym, pred_t, gt_t, diam, ctx.weight)
+        return g_r, g_t, None, None, None, None, None, None
+
+
 def point_matching_loss(pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tensor, labels: Tensor,
                         points: Sequence[Tensor], diameters: Tensor,
-                        weight: float = POSE_WEIGHT, any_symmetric: bool = True) -> Tensor:
+                        weight: float = POSE_WEIGHT, any_symmetric: bool = True,
+                        pts: Tensor = None) -> Tensor:
     """DisentanglePointMatchingLoss (point_matching_loss.py:159-218) with loss_type l1,
     disentangle_z, no xy/depth scaling, reduction mean.  ``any_symmetric=False`` (the caller
     knows no label is a symmetric class) skips the nearest-neighbour matching."""
@@ -87,7 +114,13 @@ def point_matching_loss(pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tens
             sym = (labels == c) if sym is None else (sym | (labels == c))
     diam = diameters[labels]
     if len({int(p.shape[0]) for p in points}) == 1:
-        pts = torch.stack(list(points))[labels]
+        if pts is None:
+            pts = torch.stack(list(points))[labels]
+        if pred_r.is_cuda and not _PM_TORCH:
+            return _PointMatchingLoss.apply(
+                pred_r, pred_t, gt_r.contiguous().float(), gt_t.contiguous().float(),
+                pts.contiguous().float(), None if sym is None else sym.float().contiguous(),
+                diam.contiguous().float(), float(weight))
         per = _pm_terms(pts, pred_r, pred_t, gt_r, gt_t, sym)
     else:
         per = torch.cat([_pm_terms(points[int(labels[i])][None], pred_r[i:i + 1], pred_t[i:i + 1],
@@ -123,7 +156,8 @@ def refine_losses(outs, gt_r: Tensor, gt_t: Tensor, gt_flow: Tensor, render_mask
     _, flow_pred, Rs, ts, masks, _, _ = outs
     diam = diameters if isinstance(diameters, Tensor) else torch.as_tensor(
         diameters, dtype=gt_r.dtype, device=gt_r.device)
-    lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam)
+    pts = torch.stack(list(points))[labels.long()] if len({int(p.shape[0]) for p in points}) == 1 else None
+    lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam, pts=pts)
                         for R, t in zip(Rs, ts)])  # (symmetric matching always evaluated: no sync)
     v = flow_valid(gt_flow, render_mask, max_flow)  # iteration-invariant
     lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow, v=v) for f in flow_pred])

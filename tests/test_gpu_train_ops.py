@@ -358,3 +358,31 @@ def test_pose_update6_forward_backward(depth, detach_xy):
     _close(tn, tr.detach(), 1e-5, 1e-4, "t_new")
     for name, a_, r_ in zip(("drot", "dt", "R", "t"), dev, leaves):
         _close(a_.grad, r_.grad, 1e-4, 1e-5, name)
+
+
+def test_point_matching_loss_fused():
+    """The fused HIP point-matching loss (scflow_pm_loss, symmetric classes matched to the
+    nearest predicted point) against the torch formulation in fp64 on the CPU: the loss and its
+    gradients w.r.t. the predicted rotation and translation."""
+    from scflow_amd.train import losses
+    g = torch.Generator().manual_seed(51)
+    B, P, C = 8, 1024, 21
+    points = [torch.randn(P, 3, generator=g) * 40 for _ in range(C)]
+    diam = torch.rand(C, generator=g) * 100 + 50
+    labels = torch.tensor([0, 12, 3, 15, 7, 18, 1, 20])
+    qr = lambda: torch.linalg.qr(torch.randn(B, 3, 3, generator=g))[0]  # noqa: E731
+    gt_r, pr = qr(), qr()
+    gt_t = torch.cat([torch.randn(B, 2, generator=g) * 30, 600 + torch.rand(B, 1, generator=g) * 100], 1)
+    pt = gt_t + torch.randn(B, 3, generator=g) * 5
+    ref_leaves = [pr.double().requires_grad_(), pt.double().requires_grad_()]
+    lr = losses.point_matching_loss(ref_leaves[0], ref_leaves[1], gt_r.double(), gt_t.double(), labels,
+                                    [p.double() for p in points], diam.double())
+    lr.backward()
+    dev = [pr.cuda().requires_grad_(), pt.cuda().requires_grad_()]
+    l = losses.point_matching_loss(dev[0], dev[1], gt_r.cuda(), gt_t.cuda(), labels.cuda(),
+                                   [p.cuda() for p in points], diam.cuda())
+    l.backward()
+    torch.cuda.synchronize()
+    _close(l, lr.detach(), 1e-5, 1e-6, "loss")
+    _close(dev[0].grad, ref_leaves[0].grad, 1e-4, 1e-6, "g_pred_r")
+    _close(dev[1].grad, ref_leaves[1].grad, 1e-5, 1e-6, "g_pred_t")
