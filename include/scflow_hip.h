@@ -424,6 +424,15 @@ int scflow_pm_loss_backward(const float* gloss, const float* pts, const float* g
                             const float* pred_t, const float* gt_t, const float* diam,
                             float* g_pred_r, float* g_pred_t, int B, int P, float weight,
                             void* stream);
+/* scflow_up_l1_loss: a full-resolution L1 loss of the sequence loss on the ×(H/h) bilinear
+ * (align_corners) upsampling of the channels-last low-resolution prediction f [N][h][w][C]:
+ * loss = weight·Σ v·|sval·up(f) − target| / denom (target NCHW [N][C][H][W], v = vmask [N][H][W]
+ * or 1, denom = *denom (device) or cdenom), RAFTLoss / L1Loss of sequence_loss.py:15-36 after
+ * scflow_decoder.py:223-228.  Writes sgn = v·sgn(sval·up − target) [N][C][H][W] for the backward
+ * (the upsampling adjoint) and uses partial[ceil(N·H·W/256)] as workspace. */
+int scflow_up_l1_loss(const float* f, int C, int h, int w, const float* target, const float* vmask,
+                      int N, int H, int W, float sval, const float* denom, float cdenom,
+                      float weight, float* sgn, float* partial, float* loss, void* stream);
 /* scflow_knn1: idx[b][i] = argmin_j |gt[b][i] − pred[b][j]|² over [batch][P][3] / [batch][Q][3]
  * point sets (first minimum in index order) — pytorch3d knn_points(K=1) in the symmetric-class
  * point-matching loss (point_matching_loss.py:183-186; pytorch3d is absent, torch.argmin's rule). */

@@ -1170,6 +1170,70 @@ __global__ __launch_bounds__(256) void pm_grad_kernel(
   if (threadIdx.x < 3) gT[b * 3 + threadIdx.x] = cb * sgnf(pt[b * 3 + threadIdx.x] - gtt[b * 3 + threadIdx.x]);
 }
 
+// Full-resolution L1 losses of the sequence loss (RAFTLoss / L1Loss, sequence_loss.py:15-36)
+// on the ×s upsampled prediction (F.interpolate bilinear, align_corners=True — ATen's source
+// index scale·dst and its two-level weighting order), fused with the upsampling:
+//   partial[block] = Σ_{pixels, c} v·|s_val·up(f)_c − target_c|,  sgn_out = v·sgn(s_val·up − t)
+// (v = the valid mask or 1); up_l1_finish sums the partials in order: loss = weight·Σ/denom.
+// f is channels-last [N][h][w][C] (the decoder's low-resolution flow / mask), target and sgn
+// NCHW [N][C][H][W]; the backward is the GEMM adjoint of the upsampling applied to sgn_out.
+__global__ __launch_bounds__(256) void up_l1_kernel(
+    const float* __restrict__ f, int C, int h, int w, const float* __restrict__ tgt,
+    const float* __restrict__ vmask, int N, int H, int W, float sval, float* __restrict__ sgn,
+    float* __restrict__ partial) {
+#pragma clang fp contract(off)
+  __shared__ float red[256];
+  const long long HW = (long long)H * W;
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  float acc = 0.f;
+  if (i < N * HW) {
+    const int n = (int)(i / HW);
+    const int rem = (int)(i - n * HW);
+    const int Y = rem / W, X = rem - Y * W;
+    const float sy = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+    const float sx = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+    const float ry = sy * (float)Y, rx = sx * (float)X;
+    const int y0 = (int)ry, x0 = (int)rx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly1 = ry - (float)y0, lx1 = rx - (float)x0;
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float v = vmask ? vmask[i] : 1.f;
+    const float* f00 = f + (((size_t)n * h + y0) * w + x0) * C;
+    const float* f01 = f + (((size_t)n * h + y0) * w + x1) * C;
+    const float* f10 = f + (((size_t)n * h + y1) * w + x0) * C;
+    const float* f11 = f + (((size_t)n * h + y1) * w + x1) * C;
+    for (int c = 0; c < C; ++c) {
+      const float up = ly0 * (lx0 * f00[c] + lx1 * f01[c]) + ly1 * (lx0 * f10[c] + lx1 * f11[c]);
+      const size_t o = ((size_t)n * C + c) * HW + rem;
+      const float d = sval * up - tgt[o];
+      acc += v * fabsf(d);
+      sgn[o] = v * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void up_l1_finish(const float* __restrict__ partial, int nb,
+                                                    const float* __restrict__ denom, float cdenom,
+                                                    float weight, float* __restrict__ loss) {
+  __shared__ float red[256];
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < nb; b += 256) acc += partial[b];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = weight * red[0] / (denom ? denom[0] : cdenom);
+}
+
 int gru_grid(long long total4) {
   const long long b = (total4 + 255) / 256;
   return (int)(b < 8192 ? b : 8192);
@@ -1220,6 +1284,21 @@ SCFLOW_API int scflow_pm_loss_backward(const float* gloss, const float* pts, con
     return SCFLOW_EINVAL;
   pm_grad_kernel<<<B, 256, 0, (hipStream_t)stream>>>(gloss, pts, gt_rt, pred_rot, idx, sym, pred_t,
                                                      gt_t, diam, g_pred_r, g_pred_t, B, P, weight);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_up_l1_loss(const float* f, int C, int h, int w, const float* target,
+                                 const float* vmask, int N, int H, int W, float sval,
+                                 const float* denom, float cdenom, float weight, float* sgn,
+                                 float* partial, float* loss, void* stream) {
+  if (!f || !target || !sgn || !partial || !loss || C <= 0 || h <= 0 || w <= 0 || N <= 0 ||
+      H <= 0 || W <= 0 || (!denom && cdenom == 0.f))
+    return SCFLOW_EINVAL;
+  const long long n = (long long)N * H * W;
+  const int nb = (int)((n + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  up_l1_kernel<<<nb, 256, 0, st>>>(f, C, h, w, target, vmask, N, H, W, sval, sgn, partial);
+  up_l1_finish<<<1, 256, 0, st>>>(partial, nb, denom, cdenom, weight, loss);
   return scflow_launch_status();
 }
 

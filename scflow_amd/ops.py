@@ -847,6 +847,21 @@ def pm_loss_backward(gloss: Tensor, pts: Tensor, ws, sym: Optional[Tensor], pred
     return g_r, g_t
 
 
+def up_l1_loss(f: Tensor, target: Tensor, vmask: Optional[Tensor], sval: float,
+               denom: Optional[Tensor], cdenom: float, weight: float) -> Tuple[Tensor, Tensor]:
+    """(loss [1], sgn [N, C, H, W]) of scflow_up_l1_loss; f channels-last [N, h, w, C]."""
+    _require(f, "f")
+    _require(target, "target")
+    N, h, w, C = f.shape
+    H, W = target.shape[-2:]
+    sgn = torch.empty(N, C, H, W, device=f.device)
+    partial = torch.empty((N * H * W + 255) // 256, device=f.device)
+    loss = torch.empty(1, device=f.device)
+    _launch("scflow_up_l1_loss", f, _p(f), C, h, w, _p(target), _p(vmask), N, H, W, float(sval),
+            _p(denom), float(cdenom), float(weight), _p(sgn), _p(partial), _p(loss))
+    return loss, sgn
+
+
 def knn1(gt: Tensor, pred: Tensor) -> Tensor:
     """[B, P] int64 index of the nearest ``pred`` point ([B, Q, 3]) of every ``gt`` point ([B, P, 3])."""
     _require(gt, "gt")

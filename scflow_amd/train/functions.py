@@ -617,6 +617,40 @@ class _UpsampleAC(torch.autograd.Function):
         return dx.view(n, c, h, w), None
 
 
+class _UpL1Loss(torch.autograd.Function):
+    """weight·Σ v·|sval·up(f) − target| / denom with the ×(H/h) align_corners upsampling of the
+    channels-last low-resolution f fused into the loss (scflow_up_l1_loss: one pass over the
+    full-resolution target, no upsampled tensor); backward = the upsampling's GEMM adjoint of
+    the saved v·sgn map, scaled by g·weight·sval/denom."""
+
+    @staticmethod
+    def forward(ctx, f, target, vmask, sval, denom, cdenom, weight):
+        f = f.contiguous()
+        loss, sgn = ops.up_l1_loss(f, target.contiguous(), None if vmask is None else vmask.contiguous(),
+                                   sval, denom, cdenom, weight)
+        ctx.save_for_backward(sgn, denom if denom is not None else torch.empty(0))
+        ctx.cfg = (f.shape, sval, cdenom, weight, denom is not None)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        sgn, denom = ctx.saved_tensors
+        (n, h, w, c), sval, cdenom, weight, has_denom = ctx.cfg
+        H, W = sgn.shape[-2:]
+        ax = _interp_matrix(w, W, sgn.device)
+        ayt = _interp_matrix(h, H, sgn.device).t()
+        t = ops.gemm(sgn.view(n * c * H, W), ax)
+        dx = ops.gemm(ayt.unsqueeze(0).expand(n * c, h, H), t.view(n * c, H, w)).view(n, c, h, w)
+        coef = g * (weight * sval) / (denom[0] if has_denom else cdenom)
+        return (dx * coef).permute(0, 2, 3, 1), None, None, None, None, None, None
+
+
+def up_l1_loss(f_nhwc: Tensor, target: Tensor, vmask: Optional[Tensor], sval: float,
+               denom: Optional[Tensor], cdenom: float, weight: float) -> Tensor:
+    """Fused upsample + masked L1 loss (see _UpL1Loss); target NCHW at full resolution."""
+    return _UpL1Loss.apply(f_nhwc, target, vmask, float(sval), denom, float(cdenom), float(weight))
+
+
 def upsample_bilinear_ac(x: Tensor, scale: int) -> Tensor:
     """Bilinear ×scale upsampling with align_corners=True of NCHW x (torch forward, GEMM backward)."""
     return _UpsampleAC.apply(x, scale)

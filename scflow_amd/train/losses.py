@@ -11,7 +11,7 @@ knn_points).
 from __future__ import annotations
 
 import os
-from typing import Sequence, Tuple
+from typing import NamedTuple, Sequence, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -24,6 +24,14 @@ SYMMETRIC_CLASSES = (12, 15, 18, 19, 20)  # 0-based labels of cls_13, cls_16, cl
 POSE_WEIGHT, FLOW_WEIGHT, MASK_WEIGHT, GAMMA = 10.0, 0.1, 10.0, 0.8
 _KNN_TORCH = os.environ.get("SCFLOW_TRAIN_KNN_TORCH", "0") == "1"  # A/B switch (tuning)
 _PM_TORCH = os.environ.get("SCFLOW_TRAIN_PM_TORCH", "0") == "1"    # A/B switch (tuning)
+
+
+class LowRes(NamedTuple):
+    """A prediction kept at the decoder's resolution (channels-last [N, h, w, C]) whose loss
+    upsamples it inside the fused kernel (functions.up_l1_loss); value_scale multiplies the
+    upsampled values (the flow's ×8)."""
+    lr: Tensor
+    value_scale: float
 
 
 def flow_valid(gt: Tensor, valid: Tensor, max_flow: float = 400.) -> Tensor:
@@ -160,7 +168,17 @@ def refine_losses(outs, gt_r: Tensor, gt_t: Tensor, gt_flow: Tensor, render_mask
     lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam, pts=pts)
                         for R, t in zip(Rs, ts)])  # (symmetric matching always evaluated: no sync)
     v = flow_valid(gt_flow, render_mask, max_flow)  # iteration-invariant
-    lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow, v=v) for f in flow_pred])
     occ = (gt_flow.sum(1) < max_flow).to(gt_flow)
+    if flow_pred and isinstance(flow_pred[0], LowRes):  # fused upsample + L1 (HIP)
+        from .functions import up_l1_loss
+        denom = (v.sum() + 1e-10).reshape(1)
+        gt = gt_flow.contiguous()
+        lf = sequence_loss([up_l1_loss(f.lr, gt, v, f.value_scale, denom, 0.0, FLOW_WEIGHT)
+                            for f in flow_pred])
+        occ4 = occ[:, None].contiguous()
+        lm = sequence_loss([up_l1_loss(m.lr, occ4, None, m.value_scale, None, float(occ.numel()),
+                                       MASK_WEIGHT) for m in masks])
+        return lp, lf, lm
+    lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow, v=v) for f in flow_pred])
     lm = sequence_loss([mask_l1_loss(m[:, 0], occ) for m in masks])
     return lp, lf, lm

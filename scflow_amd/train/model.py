@@ -23,10 +23,11 @@ from .. import ops
 from ..ops import Chan
 from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid, gru_step,
                         instance_norm_nhwc, linear, pose_update6, upsample_bilinear_ac)
-from .losses import filter_flow_by_mask, matmul3, refine_losses
+from .losses import LowRes, filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
 _GRU_FUSED = os.environ.get("SCFLOW_TRAIN_GRU_FUSED", "1") != "0"  # A/B switch (tuning)
+_FUSED_LOSS = os.environ.get("SCFLOW_TRAIN_FUSED_LOSS", "1") != "0"  # A/B switch (tuning)
 
 
 def _act(x: Tensor, act) -> Tensor:
@@ -215,8 +216,12 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
         for m in dec.mask_encoder:
             mf = _cm(mf, m)
         drot, dtr = pose_head_train(dec.pose_pred, torch.cat([h, dff, mf], -1), label)
-        flow_pred = scale * upsample_bilinear_ac((f2 + dflow).permute(0, 3, 1, 2), scale)
-        up_mask = upsample_bilinear_ac(mask.permute(0, 3, 1, 2), scale)
+        if depth.is_cuda and _FUSED_LOSS:  # the losses upsample inside their fused kernel
+            flow_pred = LowRes(f2 + dflow, float(scale))
+            up_mask = LowRes(mask, 1.0)
+        else:
+            flow_pred = scale * upsample_bilinear_ac((f2 + dflow).permute(0, 3, 1, 2), scale)
+            up_mask = upsample_bilinear_ac(mask.permute(0, 3, 1, 2), scale)
         if dec.detach_pose:
             R, t = R.detach(), t.detach()
         R, t = pose_update(drot, dtr, R, t, depth_transform=dec.depth_transform,

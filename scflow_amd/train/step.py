@@ -213,6 +213,8 @@ class TrainStep:
 def _detach(v):
     if isinstance(v, Tensor):
         return v.detach()
+    if isinstance(v, tuple) and hasattr(v, "_fields"):  # named tuple (losses.LowRes)
+        return type(v)(*(_detach(x) for x in v))
     if isinstance(v, (list, tuple)):
         return type(v)(_detach(x) for x in v)
     return v

@@ -386,3 +386,33 @@ def test_point_matching_loss_fused():
     _close(l, lr.detach(), 1e-5, 1e-6, "loss")
     _close(dev[0].grad, ref_leaves[0].grad, 1e-4, 1e-6, "g_pred_r")
     _close(dev[1].grad, ref_leaves[1].grad, 1e-5, 1e-6, "g_pred_t")
+
+
+@pytest.mark.parametrize("c,use_v,sval", [(2, True, 8.0), (1, False, 1.0)])
+def test_up_l1_loss_fused(c, use_v, sval):
+    """The fused upsample + L1 loss (flow: valid-masked, ×8 values; mask: plain mean) against
+    fp64 torch F.interpolate(align_corners) + L1, value and gradient w.r.t. the low-res input."""
+    from scflow_amd.train.functions import up_l1_loss
+    g = torch.Generator().manual_seed(61)
+    n, h, w, S = 3, 32, 32, 256
+    f = torch.randn(n, h, w, c, generator=g) * 2
+    tgt = torch.randn(n, c, S, S, generator=g) * 16
+    v = (torch.rand(n, S, S, generator=g) > 0.3).float() if use_v else None
+    fr = f.double().requires_grad_()
+    up = sval * F.interpolate(fr.permute(0, 3, 1, 2), size=(S, S), mode="bilinear", align_corners=True)
+    d = (up - tgt.double()).abs()
+    if use_v:
+        ref = 0.1 * (v.double()[:, None] * d).sum() / (v.double().sum() + 1e-10)
+    else:
+        ref = 10.0 * d.mean()
+    ref.backward()
+    fd = f.cuda().requires_grad_()
+    if use_v:
+        denom = (v.cuda().sum() + 1e-10).reshape(1)
+        loss = up_l1_loss(fd, tgt.cuda(), v.cuda(), sval, denom, 0.0, 0.1)
+    else:
+        loss = up_l1_loss(fd, tgt.cuda(), None, sval, None, float(n * c * S * S), 10.0)
+    loss.backward()
+    torch.cuda.synchronize()
+    _close(loss, ref.detach(), 1e-5, 1e-6, "loss")
+    _close(fd.grad, fr.grad, 1e-4, 1e-7, "grad")
