@@ -1078,6 +1078,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     SCFLOW_THIN(2, 1, 1)
     SCFLOW_THIN(1, 3, 3)
     SCFLOW_THIN(2, 3, 3)
+    SCFLOW_THIN(2, 7, 7)  // training: dX of the 2 → 128 7×7 flow encoders
 #undef SCFLOW_THIN
   }
   const unsigned blocks = (unsigned)((M + 3) / 4);
