@@ -45,8 +45,11 @@ typedef float floatx2w __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float* __restrict__ slab,
                                                             float* __restrict__ bslab) {
   extern __shared__ float smem[];
-  float* Dl = smem;            // [4][32 co][WWD]
-  float* Xl = smem + WWD_FL;   // [6][64 ci][WWX]
+  // two LDS buffers of [4][32 co][WWD] dY + [6][64 ci][WWX] halo: chunk c + 1 is stored while
+  // the other waves still compute on chunk c (one barrier per chunk)
+  constexpr int WBUF = WWD_FL + WWX_FL;
+  float* Dl = smem;            // current chunk's dY
+  float* Xl = smem + WWD_FL;   // current chunk's halo
   const scflow_wgrad_args& a = P.a;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -97,12 +100,14 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       rx[j] = v;
     }
   };
-  auto lstore = [&]() {  // transposing stores: channel-major rows, columns contiguous
+  auto lstore = [&](int buf) {  // transposing stores: channel-major rows, columns contiguous
+    float* Dw = smem + buf * WBUF;
+    float* Xw = Dw + WWD_FL;
 #pragma unroll
     for (int j = 0; j < WW_ND; ++j) {
       const int idx = tid + WW_NT * j;
       const int p = idx >> 3, cq = 4 * (idx & 7);
-      float* d = Dl + ((p >> 5) * WWCO + cq) * WWD + (p & 31);
+      float* d = Dw + ((p >> 5) * WWCO + cq) * WWD + (p & 31);
 #pragma unroll
       for (int e = 0; e < 4; ++e) d[e * WWD] = rd[j][e];
     }
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       const int p = idx >> 4, cq = 4 * (idx & 15);
       if (p < 6 * 34) {
         const int hr = p / 34, hc = p - hr * 34;
-        float* d = Xl + (hr * WWCI + cq) * WWX + hc;
+        float* d = Xw + (hr * WWCI + cq) * WWX + hc;
 #pragma unroll
         for (int e = 0; e < 4; ++e) d[e * WWX] = rx[j][e];
       }
@@ -161,12 +166,16 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
     }
   };
 
-  if (c_begin < c_end) gload(c_begin);
+  if (c_begin < c_end) {
+    gload(c_begin);
+    lstore(0);
+    __syncthreads();
+    if (c_begin + 1 < c_end) gload(c_begin + 1);
+  }
   for (int ch = c_begin; ch < c_end; ++ch) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (ch + 1 < c_end) gload(ch + 1);
+    const int cur = (ch - c_begin) & 1;
+    Dl = smem + cur * WBUF;
+    Xl = Dl + WWD_FL;
     if (do_bias) {  // Σ dY per channel: thread (co = tid & 31) over every 16th pixel
       const int co = tid & 31;
       for (int p = tid >> 5; p < 128; p += WW_NT / 32) bsum += Dl[((p >> 5) * WWCO + co) * WWD + (p & 31)];
@@ -186,6 +195,11 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
           acc[j][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(yB[j], vB[cb][j], acc[j][cb], 0, 0, 0);
+    }
+    if (ch + 1 < c_end) {
+      lstore(cur ^ 1);
+      __syncthreads();
+      if (ch + 2 < c_end) gload(ch + 2);
     }
   }
   // the second k-step set's sums onto the first's
@@ -334,7 +348,7 @@ int wwino_launch(const WwParams& P, hipStream_t st) {
   const int splits = wwino_splits(P);
   float* slab = a.workspace;
   float* bslab = a.db ? a.workspace + (size_t)splits * 16 * P.copad * P.cinp : nullptr;
-  const size_t lds = sizeof(float) * (size_t)(WWD_FL + WWX_FL);
+  const size_t lds = sizeof(float) * (size_t)(2 * (WWD_FL + WWX_FL));
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)wgrad_wino_kernel,
