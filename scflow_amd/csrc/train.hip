@@ -168,6 +168,145 @@ __global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(
   }
 }
 
+// thread = (level, image, pixel): the whole D×D sample grid of one (pixel, level) map.  The grid
+// is separable — x taps depend on a only, y taps on b only — and the taps of sample column a
+// fall in window columns a..a+2 (rows likewise), so the (D+2)² window of the map accumulates in
+// registers (static indices after unrolling) and is written back with plain read-modify-writes:
+// this thread is the map's only writer.  No atomics, and a deterministic summation order.
+template <int R>
+__global__ __launch_bounds__(256) void corr_lookup_bwd_win_kernel(
+    const float* __restrict__ dout, int out_layout, int out_stride, const float* __restrict__ flow,
+    int flow_layout, float* __restrict__ dpyr, int N, int H, int W, int L, long long total) {
+#pragma clang fp contract(off)
+  constexpr int r = R;
+  constexpr int D = 2 * R + 1;
+  const int P = H * W;
+  const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const int p = (int)(idx % P);
+  long long t = idx / P;
+  const int n = (int)(t % N);
+  const int lvl = (int)(t / N);
+  if (idx >= total) return;
+  // (staging the block's gradient rows through LDS for coalesced loads measured slower: 98 vs
+  // 74 µs at configs[3]'s training shapes — one block per CU then waits on the whole stage)
+  const float* g = out_layout == SCFLOW_LAYOUT_NHWC
+                       ? dout + ((size_t)n * P + p) * out_stride + lvl * D * D
+                       : dout + ((size_t)n * L * D * D + lvl * D * D) * P + p;
+  const int gstep = out_layout == SCFLOW_LAYOUT_NHWC ? 1 : P;
+  const int y = p / W, x = p % W;
+  float fx, fy;
+  if (flow_layout == SCFLOW_LAYOUT_NHWC) {
+    fx = flow[((size_t)n * P + p) * 2 + 0];
+    fy = flow[((size_t)n * P + p) * 2 + 1];
+  } else {
+    fx = flow[((size_t)n * 2 + 0) * P + p];
+    fy = flow[((size_t)n * 2 + 1) * P + p];
+  }
+  size_t off = 0;
+  int Hl = H, Wl = W;
+  for (int l = 0; l < lvl; ++l) {
+    off += (size_t)N * P * Hl * Wl;
+    Hl >>= 1;
+    Wl >>= 1;
+  }
+  float* m = dpyr + off + ((size_t)n * P + p) * Hl * Wl;
+  const float scale = (float)(1 << lvl);
+  const float cx = ((float)x + fx) / scale;
+  const float cy = ((float)y + fy) / scale;
+  if (!(fabsf(cx) < 1e6f && fabsf(cy) < 1e6f)) return;  // every tap outside the map
+  // sample column a: west tap xw(a) = x0 + a + ox[a] with ox ∈ {0, 1}, east tap one further;
+  // x0 = rint(cx − r) − 1 (and the same in y).  Checked exhaustively over integer, half- and
+  // quarter-integer and random coordinates; a thread outside it takes the per-tap path.
+  const int x0 = (int)rintf(cx + (float)(-r)) - 1;
+  const int y0 = (int)rintf(cy + (float)(-r)) - 1;
+  float wxw[D], wxe[D], wyn[D], wys[D];
+  int ox[D], oy[D];
+  bool regular = true;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const float ix = unnorm_coord_b(cx + (float)(k - r), Wl);
+    const float ix_w = floorf(ix);
+    wxw[k] = (ix_w + 1.f) - ix;
+    wxe[k] = ix - ix_w;
+    ox[k] = (int)ix_w - x0 - k;
+    const float iy = unnorm_coord_b(cy + (float)(k - r), Hl);
+    const float iy_n = floorf(iy);
+    wyn[k] = (iy_n + 1.f) - iy;
+    wys[k] = iy - iy_n;
+    oy[k] = (int)iy_n - y0 - k;
+    regular = regular && (unsigned)ox[k] <= 1u && (unsigned)oy[k] <= 1u;
+  }
+  if (!regular) {
+    for (int a = 0; a < D; ++a) {
+      const int xw = x0 + a + ox[a];
+      for (int b = 0; b < D; ++b) {
+        const float gv = g[(size_t)(a * D + b) * gstep];
+        const int yn = y0 + b + oy[b];
+        tap_add(m, xw, yn, Wl, Hl, gv * (wxw[a] * wyn[b]));
+        tap_add(m, xw + 1, yn, Wl, Hl, gv * (wxe[a] * wyn[b]));
+        tap_add(m, xw, yn + 1, Wl, Hl, gv * (wxw[a] * wys[b]));
+        tap_add(m, xw + 1, yn + 1, Wl, Hl, gv * (wxe[a] * wys[b]));
+      }
+    }
+    return;
+  }
+  // per column a the x weights over window columns a, a+1, a+2 (and y likewise)
+  float ux0[D], ux1[D], ux2[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) {
+    ux0[a] = ox[a] ? 0.f : wxw[a];
+    ux1[a] = ox[a] ? wxw[a] : wxe[a];
+    ux2[a] = ox[a] ? wxe[a] : 0.f;
+  }
+  constexpr int WN = D + 2;
+  unsigned inb = 0;  // bit i: window column x0 + i inside the map
+#pragma unroll
+  for (int i = 0; i < WN; ++i) inb |= (x0 + i >= 0 && x0 + i < Wl) ? 1u << i : 0u;
+  // the window starts from the map's current values (all loads before any store: with the row
+  // pitch unknown to the compiler, interleaved read-modify-writes would serialise on aliasing)
+  float win[WN][WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int yy = y0 + j;
+    const bool rin = yy >= 0 && yy < Hl;
+    const float* row = m + (ptrdiff_t)yy * Wl + x0;
+#pragma unroll
+    for (int i = 0; i < WN; ++i) win[j][i] = (rin && (inb >> i & 1u)) ? row[i] : 0.f;
+  }
+  // separable accumulation: row b of samples → a window-wide vector, spread over 3 window rows
+#pragma unroll
+  for (int b = 0; b < D; ++b) {
+    float v[WN];
+#pragma unroll
+    for (int i = 0; i < WN; ++i) v[i] = 0.f;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+      const float gv = g[(size_t)(a * D + b) * gstep];
+      v[a] += gv * ux0[a];
+      v[a + 1] += gv * ux1[a];
+      v[a + 2] += gv * ux2[a];
+    }
+    const float u0 = oy[b] ? 0.f : wyn[b];
+    const float u1 = oy[b] ? wyn[b] : wys[b];
+    const float u2 = oy[b] ? wys[b] : 0.f;
+#pragma unroll
+    for (int i = 0; i < WN; ++i) {
+      win[b][i] += u0 * v[i];
+      win[b + 1][i] += u1 * v[i];
+      win[b + 2][i] += u2 * v[i];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int yy = y0 + j;
+    if (yy < 0 || yy >= Hl) continue;
+    float* row = m + (ptrdiff_t)yy * Wl + x0;
+#pragma unroll
+    for (int i = 0; i < WN; ++i)
+      if (inb >> i & 1u) row[i] = win[j][i];
+  }
+}
+
 // ------------------------------------------------------------------------------ wgrad
 struct WgParams {
   scflow_wgrad_args a;
@@ -1484,6 +1623,27 @@ SCFLOW_API int scflow_corr_lookup_backward(const float* dout, int out_layout, in
   const long long total = (long long)n * h * w * num_levels * D;
   const unsigned blocks = (unsigned)((total + 255) / 256);
   hipStream_t st = (hipStream_t)stream;
+  static const bool win_off = [] {
+    const char* e = getenv("SCFLOW_LOOKUP_BWD_WIN");
+    return e && e[0] == '0';
+  }();
+  if (radius <= 4 && !win_off) {
+    const long long tw = (long long)n * h * w * num_levels;
+    const unsigned bw = (unsigned)((tw + 255) / 256);
+    switch (radius) {
+#define SCFLOW_LKW(RR)                                                                             \
+  case RR:                                                                                         \
+    corr_lookup_bwd_win_kernel<RR><<<bw, 256, 0, st>>>(dout, out_layout, out_stride, flow,         \
+                                                       flow_layout, dpyr, n, h, w, num_levels, tw); \
+    break;
+      SCFLOW_LKW(1)
+      SCFLOW_LKW(2)
+      SCFLOW_LKW(3)
+      SCFLOW_LKW(4)
+#undef SCFLOW_LKW
+    }
+    return scflow_launch_status();
+  }
   switch (radius) {
 #define SCFLOW_LKB(RR)                                                                            \
   case RR:                                                                                        \

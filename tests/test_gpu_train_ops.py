@@ -180,10 +180,12 @@ def test_corr_pyramid_backward():
     _close(a2.grad, r2.grad, 1e-5, 1e-4, "df2")
 
 
-@pytest.mark.parametrize("radius", [4, 1])
-def test_corr_lookup_backward(radius):
+@pytest.mark.parametrize("radius,flow_kind", [(4, "rand"), (1, "rand"), (4, "grid"), (6, "rand")])
+def test_corr_lookup_backward(radius, flow_kind):
     """The adjoint of the lookup: ⟨lookup(pyr), g⟩ differentiated w.r.t. the pyramid, with flow
-    in ±6 px (zero padding) — against autograd of the oracle's explicit bilinear gather."""
+    in ±6 px (zero padding) — against autograd of the oracle's explicit bilinear gather.  "grid":
+    flows on the integer / half / quarter / eighth grid (zero where the reference's flow is
+    invalid), the coordinates where the float unnormalisation rounds across a tap boundary."""
     from scflow_amd import ops
     from scflow_amd.train.functions import corr_lookup
     g = torch.Generator().manual_seed(2 + radius)
@@ -192,6 +194,10 @@ def test_corr_lookup_backward(radius):
     f2 = torch.randn(n, c, h, w, generator=g)
     levels = [lv.double().requires_grad_() for lv in orc.corr_pyramid(f1.double(), f2.double(), 4)]
     flow = (torch.rand(n, 2, h, w, generator=g) - 0.5) * 12
+    if flow_kind == "grid":
+        d = torch.tensor([1., 2., 4., 8.])[torch.randint(0, 4, (n, 2, h, w), generator=g)]
+        flow = torch.round(flow * d) / d
+        flow[:, :, ::3] = 0.0
     out = orc.corr_lookup(levels, flow.double(), radius)          # [n, K, h, w]
     gout = torch.randn(out.shape, generator=g, dtype=torch.float64)
     (out * gout).sum().backward()
