@@ -438,6 +438,19 @@ int scflow_up_l1_loss(const float* f, int C, int h, int w, const float* target, 
  * point-matching loss (point_matching_loss.py:183-186; pytorch3d is absent, torch.argmin's rule). */
 int scflow_knn1(const float* gt, const float* pred, long long* idx, int batch, int P, int Q,
                 void* stream);
+/* GroupNorm (+ReLU) of the pose head's conv stack (pose_head.py:160-170, mmcv ConvModule with
+ * norm_cfg GN(32) and ReLU; torch.nn.GroupNorm semantics: biased variance, eps inside the root),
+ * channels-last x [n][hw][c] with exactly 4 channels per group (c == 4·groups), 16-byte aligned.
+ *   forward: y = act((x − μ_g)·rstd_g·γ_c + β_c); stats [n·groups][2] = (μ, rstd)
+ *   backward: dx; dγ / dβ summed over the images in order (part: n·c·2 floats of workspace),
+ *             written (accumulate 0) or added onto dgamma / dbeta (accumulate 1) */
+int scflow_group_norm_forward(const float* x, const float* gamma, const float* beta, float* y,
+                              float* stats, int n, int hw, int c, int groups, float eps, int relu,
+                              void* stream);
+int scflow_group_norm_backward(const float* dy, const float* x, const float* gamma,
+                               const float* beta, const float* stats, float* dx, float* part,
+                               float* dgamma, float* dbeta, int n, int hw, int c, int groups,
+                               int relu, int accumulate, void* stream);
 /* SepConvGRU gate algebra of the training step (raft_decoder.py:235-253), channels-last,
  * c % 4 == 0, zr = the z | r conv's sigmoid output [npix][2c]:
  *   scflow_gru_gate_forward mode 0: out = r·h;  mode 1: out = h + z·(q − h)

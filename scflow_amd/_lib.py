@@ -213,6 +213,10 @@ SIGNATURES = {
     "scflow_up_l1_loss": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_float,
                                   c_vp, c_float, c_float, c_vp, c_vp, c_vp, c_vp]),
     "scflow_knn1": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_group_norm_forward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                          c_float, c_int, c_vp]),
+    "scflow_group_norm_backward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "scflow_gru_gate_forward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp]),
     "scflow_gru_gate_backward_q": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,
                                            c_int, c_vp]),

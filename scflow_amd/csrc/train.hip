@@ -1378,6 +1378,142 @@ int gru_grid(long long total4) {
   return (int)(b < 8192 ? b : 8192);
 }
 
+
+// ------------------------------------------------------------------------------ group norm
+// GroupNorm (+ReLU) of the pose head (pose_head.py:160-170: conv → GN(32) → ReLU) on channels-last
+// data with 4 channels per group: block = (image, group), a float4 per pixel.
+template <int K>
+__device__ __forceinline__ void gn_block_sum(float (&v)[K], float* red) {
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wv * K + k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = ((red[k] + red[K + k]) + red[2 * K + k]) + red[3 * K + k];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void gn_fwd_kernel(const float* __restrict__ x,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta,
+                                                     float* __restrict__ y, float* __restrict__ stats,
+                                                     int HW, int C, int G, float eps, int relu) {
+#pragma clang fp contract(off)
+  __shared__ float red[4];
+  const int n = blockIdx.x / G, g = blockIdx.x % G;
+  const size_t base = (size_t)n * HW * C + g * 4;
+  float s[1] = {0.f};
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const floatx4 v = *(const floatx4*)(x + base + (size_t)p * C);
+    s[0] += (v[0] + v[1]) + (v[2] + v[3]);
+  }
+  gn_block_sum<1>(s, red);
+  const float M = (float)(4 * HW);
+  const float mean = s[0] / M;
+  float q[1] = {0.f};
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const floatx4 v = *(const floatx4*)(x + base + (size_t)p * C);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) q[0] += (v[c] - mean) * (v[c] - mean);
+  }
+  gn_block_sum<1>(q, red);
+  const float rstd = 1.f / sqrtf(q[0] / M + eps);
+  const floatx4 ga = *(const floatx4*)(gamma + g * 4);
+  const floatx4 be = *(const floatx4*)(beta + g * 4);
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const floatx4 v = *(const floatx4*)(x + base + (size_t)p * C);
+    floatx4 o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float z = ((v[c] - mean) * rstd) * ga[c] + be[c];
+      o[c] = relu && !(z > 0.f) ? 0.f : z;
+    }
+    *(floatx4*)(y + base + (size_t)p * C) = o;
+  }
+  if (threadIdx.x == 0) {
+    stats[blockIdx.x * 2 + 0] = mean;
+    stats[blockIdx.x * 2 + 1] = rstd;
+  }
+}
+
+// dx of one (image, group) and its per-channel Σdz·x̂ / Σdz partials (dz: dy through the ReLU,
+// recomputed from x exactly as the forward formed its output)
+__global__ __launch_bounds__(256) void gn_bwd_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ stats, float* __restrict__ dx,
+    float* __restrict__ part, int HW, int C, int G, int relu) {
+#pragma clang fp contract(off)
+  __shared__ float red[4 * 8];
+  const int n = blockIdx.x / G, g = blockIdx.x % G;
+  const size_t base = (size_t)n * HW * C + g * 4;
+  const float mean = stats[blockIdx.x * 2 + 0], rstd = stats[blockIdx.x * 2 + 1];
+  const floatx4 ga = *(const floatx4*)(gamma + g * 4);
+  const floatx4 be = *(const floatx4*)(beta + g * 4);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // Σdz[c], Σdz·x̂[c]
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const floatx4 v = *(const floatx4*)(x + base + (size_t)p * C);
+    const floatx4 d = *(const floatx4*)(dy + base + (size_t)p * C);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float xh = (v[c] - mean) * rstd;
+      const float z = xh * ga[c] + be[c];
+      const float dz = relu && !(z > 0.f) ? 0.f : d[c];
+      acc[c] += dz;
+      acc[4 + c] += dz * xh;
+    }
+  }
+  gn_block_sum<8>(acc, red);
+  const float M = (float)(4 * HW);
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    a += ga[c] * acc[c];
+    b += ga[c] * acc[4 + c];
+  }
+  a /= M;
+  b /= M;
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const floatx4 v = *(const floatx4*)(x + base + (size_t)p * C);
+    const floatx4 d = *(const floatx4*)(dy + base + (size_t)p * C);
+    floatx4 o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float xh = (v[c] - mean) * rstd;
+      const float z = xh * ga[c] + be[c];
+      const float dz = relu && !(z > 0.f) ? 0.f : d[c];
+      o[c] = rstd * ((dz * ga[c] - a) - xh * b);
+    }
+    *(floatx4*)(dx + base + (size_t)p * C) = o;
+  }
+  if (threadIdx.x < 4) {
+    part[((size_t)n * C + g * 4 + threadIdx.x) * 2 + 0] = acc[4 + threadIdx.x];
+    part[((size_t)n * C + g * 4 + threadIdx.x) * 2 + 1] = acc[threadIdx.x];
+  }
+}
+
+// dγ, dβ: the per-image partials summed in image order (deterministic), set or accumulated
+__global__ void gn_param_kernel(const float* __restrict__ part, float* __restrict__ dgamma,
+                                float* __restrict__ dbeta, int N, int C, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sg = 0.f, sb = 0.f;
+  for (int n = 0; n < N; ++n) {
+    sg += part[((size_t)n * C + c) * 2 + 0];
+    sb += part[((size_t)n * C + c) * 2 + 1];
+  }
+  if (accumulate) {
+    dgamma[c] += sg;
+    dbeta[c] += sb;
+  } else {
+    dgamma[c] = sg;
+    dbeta[c] = sb;
+  }
+}
+
 }  // namespace
 
 SCFLOW_API int scflow_pose_update6_train(const float* drot, const float* dt, const float* R,
@@ -1692,5 +1828,37 @@ SCFLOW_API int scflow_in_backward(const float* dy, const float* x, const float* 
   const long long total4 = (long long)n * hw * c / 4;
   const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
   in_bwd_apply_kernel<<<blocks, 256, 0, st>>>(dy, x, scale, shift, mm, dx, hw, c, relu ? 1 : 0, total4);
+  return scflow_launch_status();
+}
+
+static int gn_check(const void* a, const void* b, const void* c, int n, int hw, int ch, int groups) {
+  if (!a || !b || !c || n <= 0 || hw <= 0 || groups <= 0 || ch != 4 * groups) return SCFLOW_EINVAL;
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15) return SCFLOW_EINVAL;
+  return 0;
+}
+
+SCFLOW_API int scflow_group_norm_forward(const float* x, const float* gamma, const float* beta,
+                                         float* y, float* stats, int n, int hw, int c, int groups,
+                                         float eps, int relu, void* stream) {
+  if (int e = gn_check(x, y, gamma, n, hw, c, groups)) return e;
+  if (!beta || !stats || ((uintptr_t)beta & 15)) return SCFLOW_EINVAL;
+  gn_fwd_kernel<<<n * groups, 256, 0, (hipStream_t)stream>>>(x, gamma, beta, y, stats, hw, c, groups,
+                                                             eps, relu ? 1 : 0);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_group_norm_backward(const float* dy, const float* x, const float* gamma,
+                                          const float* beta, const float* stats, float* dx,
+                                          float* part, float* dgamma, float* dbeta, int n, int hw,
+                                          int c, int groups, int relu, int accumulate,
+                                          void* stream) {
+  if (int e = gn_check(dy, x, dx, n, hw, c, groups)) return e;
+  if (!gamma || !beta || !stats || !part || !dgamma || !dbeta || ((uintptr_t)(gamma) & 15) ||
+      ((uintptr_t)beta & 15))
+    return SCFLOW_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  gn_bwd_kernel<<<n * groups, 256, 0, st>>>(dy, x, gamma, beta, stats, dx, part, hw, c, groups,
+                                            relu ? 1 : 0);
+  gn_param_kernel<<<(c + 127) / 128, 128, 0, st>>>(part, dgamma, dbeta, n, c, accumulate ? 1 : 0);
   return scflow_launch_status();
 }

@@ -872,6 +872,37 @@ def knn1(gt: Tensor, pred: Tensor) -> Tensor:
     return idx
 
 
+def group_norm_forward(x: Tensor, gamma: Tensor, beta: Tensor, groups: int, eps: float,
+                       relu: bool) -> Tuple[Tensor, Tensor]:
+    """GroupNorm (+ReLU) of channels-last x [n, h, w, c] (c == 4·groups) → (y, stats [n·groups, 2]
+    = (mean, rstd))."""
+    for nm, t in (("x", x), ("gamma", gamma), ("beta", beta)):
+        _require(t, nm)
+    n, c = x.shape[0], x.shape[-1]
+    hw = x.numel() // (n * c)
+    y = torch.empty_like(x)
+    stats = torch.empty(n * groups, 2, device=x.device, dtype=torch.float32)
+    _launch("scflow_group_norm_forward", x, _p(x), _p(gamma), _p(beta), _p(y), _p(stats), n, hw, c,
+            groups, float(eps), int(relu))
+    return y, stats
+
+
+def group_norm_backward(dy: Tensor, x: Tensor, gamma: Tensor, beta: Tensor, stats: Tensor,
+                        groups: int, relu: bool, dgamma: Tensor, dbeta: Tensor,
+                        accumulate: bool) -> Tensor:
+    """dx of group_norm_forward; dγ / dβ written to (or, accumulate, added onto) dgamma / dbeta."""
+    for nm, t in (("dy", dy), ("x", x), ("gamma", gamma), ("beta", beta), ("stats", stats),
+                  ("dgamma", dgamma), ("dbeta", dbeta)):
+        _require(t, nm)
+    n, c = x.shape[0], x.shape[-1]
+    hw = x.numel() // (n * c)
+    dx = torch.empty_like(x)
+    part = torch.empty(n * c * 2, device=x.device, dtype=torch.float32)
+    _launch("scflow_group_norm_backward", x, _p(dy), _p(x), _p(gamma), _p(beta), _p(stats), _p(dx),
+            _p(part), _p(dgamma), _p(dbeta), n, hw, c, groups, int(relu), int(accumulate))
+    return dx
+
+
 def gru_gate_forward(zr: Tensor, h: Tensor, out: Tensor, q: Optional[Tensor] = None) -> Tensor:
     """SepConvGRU gate (training): out = r·h (q None) or h + z·(q − h); zr [..., 2c], h / q / out
     [..., c], channels-last contiguous."""

@@ -656,6 +656,41 @@ def upsample_bilinear_ac(x: Tensor, scale: int) -> Tensor:
     return _UpsampleAC.apply(x, scale)
 
 
+# ------------------------------------------------------------------------------- group norm
+class _GroupNormNHWC(torch.autograd.Function):
+    """GroupNorm (+ReLU) on channels-last data, 4 channels per group (the pose head's GN(32) on
+    128 channels): one HIP launch forward, two backward (dx + per-image γ/β partials, then their
+    ordered sum — added straight into the parameters' .grad under direct_weight_grads) instead of
+    the NCHW copies, native_group_norm(_backward), the ReLU and its backward and the
+    AccumulateGrad adds."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, groups, eps, relu):
+        x = x.contiguous()
+        y, stats = ops.group_norm_forward(x, w.detach().contiguous(), b.detach().contiguous(),
+                                          groups, eps, relu)
+        ctx.save_for_backward(x, w, b, stats)
+        ctx.groups, ctx.relu = groups, relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, stats = ctx.saved_tensors
+        sw, sb = _grad_sink(w), _grad_sink(b)
+        direct = sw is not None and sb is not None
+        dw = sw if direct else torch.empty_like(w)
+        db = sb if direct else torch.empty_like(b)
+        dx = ops.group_norm_backward(dy.contiguous(), x, w.detach().contiguous(), b.detach().contiguous(),
+                                     stats, ctx.groups, ctx.relu, dw, db, accumulate=direct)
+        return dx, (None if direct else dw), (None if direct else db), None, None, None
+
+
+def group_norm_nhwc(x: Tensor, weight: Tensor, bias: Tensor, groups: int, eps: float,
+                    relu: bool = False) -> Tensor:
+    """F.group_norm (+ReLU) of a channels-last tensor with 4 channels per group (HIP)."""
+    return _GroupNormNHWC.apply(x, weight, bias, groups, eps, relu)
+
+
 # ------------------------------------------------------------------------------- linear
 class _Linear(torch.autograd.Function):
     @staticmethod

@@ -110,17 +110,14 @@ class _PointMatchingLoss(torch.autograd.Function):
 def point_matching_loss(pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tensor, labels: Tensor,
                         points: Sequence[Tensor], diameters: Tensor,
                         weight: float = POSE_WEIGHT, any_symmetric: bool = True,
-                        pts: Tensor = None) -> Tensor:
+                        pts: Tensor = None, hoisted: Tuple[Tensor, Tensor] = None) -> Tensor:
     """DisentanglePointMatchingLoss (point_matching_loss.py:159-218) with loss_type l1,
     disentangle_z, no xy/depth scaling, reduction mean.  ``any_symmetric=False`` (the caller
-    knows no label is a symmetric class) skips the nearest-neighbour matching."""
+    knows no label is a symmetric class) skips the nearest-neighbour matching.  ``hoisted``:
+    (symmetric mask, per-sample diameter) from ``label_terms``, computed once per step."""
     B = pred_r.shape[0]
     labels = labels.long()
-    sym = None
-    if any_symmetric:
-        for c in SYMMETRIC_CLASSES:
-            sym = (labels == c) if sym is None else (sym | (labels == c))
-    diam = diameters[labels]
+    sym, diam = hoisted if hoisted is not None else label_terms(labels, diameters, any_symmetric)
     if len({int(p.shape[0]) for p in points}) == 1:
         if pts is None:
             pts = torch.stack(list(points))[labels]
@@ -135,6 +132,16 @@ def point_matching_loss(pred_r: Tensor, pred_t: Tensor, gt_r: Tensor, gt_t: Tens
                                    gt_r[i:i + 1], gt_t[i:i + 1], None if sym is None else sym[i:i + 1])
                          for i in range(B)])
     return weight * (per / diam).sum() / B
+
+
+def label_terms(labels: Tensor, diameters: Tensor, any_symmetric: bool = True):
+    """(symmetric-class mask or None, diameter per sample) of a batch's labels."""
+    labels = labels.long()
+    sym = None
+    if any_symmetric:
+        for c in SYMMETRIC_CLASSES:
+            sym = (labels == c) if sym is None else (sym | (labels == c))
+    return sym, diameters[labels]
 
 
 def sequence_loss(values: Sequence[Tensor], gamma: float = GAMMA) -> Tensor:
@@ -165,19 +172,35 @@ def refine_losses(outs, gt_r: Tensor, gt_t: Tensor, gt_flow: Tensor, render_mask
     diam = diameters if isinstance(diameters, Tensor) else torch.as_tensor(
         diameters, dtype=gt_r.dtype, device=gt_r.device)
     pts = torch.stack(list(points))[labels.long()] if len({int(p.shape[0]) for p in points}) == 1 else None
-    lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam, pts=pts)
-                        for R, t in zip(Rs, ts)])  # (symmetric matching always evaluated: no sync)
+    hoisted = label_terms(labels, diam)  # iteration-invariant label work, once per step
+    n = len(Rs)
+    fused = gt_r.is_cuda and pts is not None and flow_pred and isinstance(flow_pred[0], LowRes)
+    if fused:
+        if not _PM_TORCH:  # the kernel's operand types, converted once
+            hoisted = (None if hoisted[0] is None else hoisted[0].float(), hoisted[1].float().contiguous())
+        # the fused HIP losses scale by their weight argument: fold SequenceLoss's γ^(n−i−1)
+        # into it and sum the 8 terms with one stack + sum instead of 2·8 scalar ops
+        gam = [GAMMA ** (n - i - 1) for i in range(n)]
+        lp = torch.stack([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam, pts=pts,
+                                              hoisted=hoisted, weight=POSE_WEIGHT * gam[i]).reshape(())
+                          for i, (R, t) in enumerate(zip(Rs, ts))]).sum()
+    else:
+        lp = sequence_loss([point_matching_loss(R, t, gt_r, gt_t, labels, points, diam, pts=pts,
+                                                hoisted=hoisted)
+                            for R, t in zip(Rs, ts)])  # (symmetric matching always evaluated: no sync)
     v = flow_valid(gt_flow, render_mask, max_flow)  # iteration-invariant
     occ = (gt_flow.sum(1) < max_flow).to(gt_flow)
     if flow_pred and isinstance(flow_pred[0], LowRes):  # fused upsample + L1 (HIP)
         from .functions import up_l1_loss
         denom = (v.sum() + 1e-10).reshape(1)
         gt = gt_flow.contiguous()
-        lf = sequence_loss([up_l1_loss(f.lr, gt, v, f.value_scale, denom, 0.0, FLOW_WEIGHT)
-                            for f in flow_pred])
+        gam = [GAMMA ** (len(flow_pred) - i - 1) for i in range(len(flow_pred))]
+        lf = torch.stack([up_l1_loss(f.lr, gt, v, f.value_scale, denom, 0.0, FLOW_WEIGHT * gam[i]).reshape(())
+                          for i, f in enumerate(flow_pred)]).sum()
         occ4 = occ[:, None].contiguous()
-        lm = sequence_loss([up_l1_loss(m.lr, occ4, None, m.value_scale, None, float(occ.numel()),
-                                       MASK_WEIGHT) for m in masks])
+        gam = [GAMMA ** (len(masks) - i - 1) for i in range(len(masks))]
+        lm = torch.stack([up_l1_loss(m.lr, occ4, None, m.value_scale, None, float(occ.numel()),
+                                     MASK_WEIGHT * gam[i]).reshape(()) for i, m in enumerate(masks)]).sum()
         return lp, lf, lm
     lf = sequence_loss([flow_l1_loss(f, gt_flow, render_mask, max_flow, v=v) for f in flow_pred])
     lm = sequence_loss([mask_l1_loss(m[:, 0], occ) for m in masks])

@@ -21,13 +21,14 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid, gru_step,
-                        instance_norm_nhwc, linear, pose_update6, upsample_bilinear_ac)
+from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid, group_norm_nhwc,
+                        gru_step, instance_norm_nhwc, linear, pose_update6, upsample_bilinear_ac)
 from .losses import LowRes, filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
 _GRU_FUSED = os.environ.get("SCFLOW_TRAIN_GRU_FUSED", "1") != "0"  # A/B switch (tuning)
 _FUSED_LOSS = os.environ.get("SCFLOW_TRAIN_FUSED_LOSS", "1") != "0"  # A/B switch (tuning)
+_GN_FUSED = os.environ.get("SCFLOW_TRAIN_GN_FUSED", "1") != "0"  # A/B switch (tuning)
 
 
 def _act(x: Tensor, act) -> Tensor:
@@ -89,7 +90,11 @@ def pose_head_train(head, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
     for m in head.conv_layers:
         c = m.conv
         y = conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding)
-        y = F.group_norm(y.permute(0, 3, 1, 2), m.gn.num_groups, m.gn.weight, m.gn.bias, m.gn.eps)
+        gn = m.gn
+        if y.is_cuda and _GN_FUSED and gn.affine and y.shape[-1] == 4 * gn.num_groups:
+            x = group_norm_nhwc(y, gn.weight, gn.bias, gn.num_groups, gn.eps, relu=True)
+            continue
+        y = F.group_norm(y.permute(0, 3, 1, 2), gn.num_groups, gn.weight, gn.bias, gn.eps)
         x = torch.relu(y).permute(0, 2, 3, 1)
     v = x.permute(0, 3, 1, 2).reshape(x.shape[0], -1)  # nn.Flatten of NCHW
     for fc in head.fc_layers:

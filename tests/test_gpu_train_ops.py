@@ -422,3 +422,37 @@ def test_up_l1_loss_fused(c, use_v, sval):
     torch.cuda.synchronize()
     _close(loss, ref.detach(), 1e-5, 1e-6, "loss")
     _close(fd.grad, fr.grad, 1e-4, 1e-7, "grad")
+
+
+@pytest.mark.parametrize("n,h,w,c,relu", [(16, 16, 16, 128, True), (3, 4, 4, 128, True),
+                                          (2, 5, 7, 64, False)])
+def test_group_norm_nhwc(n, h, w, c, relu):
+    """Fused GroupNorm (+ReLU), 4 channels per group, channels-last: forward, dx, dγ, dβ against
+    fp64 torch GroupNorm (+ReLU) autograd on NCHW; then the accumulate mode adds onto .grad."""
+    from scflow_amd import ops
+    from scflow_amd.train.functions import group_norm_nhwc
+    g = torch.Generator().manual_seed(n * h + c)
+    x = torch.randn(n, h, w, c, generator=g) * 2 + 0.5
+    wt = torch.randn(c, generator=g)
+    bs = torch.randn(c, generator=g) * 0.3
+    dy = torch.randn(n, h, w, c, generator=g)
+    xr, wr, br = (t.double().requires_grad_() for t in (x, wt, bs))
+    yr = torch.nn.functional.group_norm(xr.permute(0, 3, 1, 2), c // 4, wr, br, 1e-5)
+    yr = (torch.relu(yr) if relu else yr).permute(0, 2, 3, 1)
+    (yr * dy.double()).sum().backward()
+    xc, wc, bc = (t.cuda().requires_grad_() for t in (x, wt, bs))
+    y = group_norm_nhwc(xc, wc, bc, c // 4, 1e-5, relu)
+    (y * dy.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    _close(y, yr.detach(), 1e-5, 1e-5, "gn forward")
+    _close(xc.grad, xr.grad, 1e-4, 1e-4, "gn dx")
+    _close(wc.grad, wr.grad, 1e-4, 1e-4, "gn dgamma")
+    _close(bc.grad, br.grad, 1e-4, 1e-4, "gn dbeta")
+    # accumulate mode: the partials' sum lands on top of what the buffers hold
+    _, stats = ops.group_norm_forward(xc.detach(), wc.detach(), bc.detach(), c // 4, 1e-5, relu)
+    dg, db = torch.ones(c, device="cuda"), torch.full((c,), 2.0, device="cuda")
+    ops.group_norm_backward(dy.cuda(), xc.detach(), wc.detach(), bc.detach(), stats, c // 4, relu,
+                            dg, db, accumulate=True)
+    torch.cuda.synchronize()
+    _close(dg, wr.grad + 1, 1e-4, 1e-4, "gn dgamma (accumulate)")
+    _close(db, br.grad + 2, 1e-4, 1e-4, "gn dbeta (accumulate)")

@@ -15,6 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--rows", type=int, default=45)
+    ap.add_argument("--shapes", action="store_true", help="group by input shapes (record_shapes)")
     a = ap.parse_args()
     import bench
     from scflow_amd import synthetic
@@ -29,11 +30,13 @@ def main():
         step(batch)
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                 record_shapes=a.shapes) as prof:
         step(batch)
         torch.cuda.synchronize()
-    print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=a.rows,
-                                    max_name_column_width=60))
+    print(prof.key_averages(group_by_input_shape=a.shapes).table(
+        sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=60,
+        max_shapes_column_width=90))
 
 
 if __name__ == "__main__":
