@@ -400,6 +400,11 @@ int scflow_enc_apply(const float* x, const float* scale, const float* shift, con
  *   SCFlow (scflow_decoder.py:193-194), so no flow gradient. */
 int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh, int kw,
                   int stride, int ph, int pw, void* stream);
+/* scflow_im2col_ex: scflow_im2col, or with channel_major the column order (c·kh + ty)·kw + tx —
+ * the conv weight's own [cout][cin][kh][kw] order, so dW (and its accumulation) is one GEMM
+ * written in place. */
+int scflow_im2col_ex(const float* x, int sx, float* cols, int n, int h, int w, int cin, int kh,
+                     int kw, int stride, int ph, int pw, int channel_major, void* stream);
 /* scflow_pose_update6_train: the training step's pose update for an ortho6d Δrotation
  * (pose.py:124-169), forward (backward = 0: o0 = Rn [n][3][3], o1 = tn [n][3]) or its gradient
  * (backward = 1, given gRn, gtn: o0 = g drot [n][6], o1 = g dt [n][3], o2 = g R, o3 = g t);

@@ -204,6 +204,8 @@ SIGNATURES = {
     "scflow_conv_wgrad": (c_int, [ctypes.POINTER(WgradArgs), c_vp]),
     "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_vp]),
+    "scflow_im2col_ex": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, c_int, c_int, c_vp]),
     "scflow_pose_update6_train": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                           c_int, c_float, c_int, c_int, c_int, c_vp]),
     "scflow_pm_loss": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

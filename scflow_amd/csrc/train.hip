@@ -26,15 +26,17 @@
 
 namespace {
 
+// column order (ty, tx, c), or with cmajor (c, ty, tx) — a conv weight's own [cout][cin][kh][kw]
+// order, so the weight-gradient GEMM writes (or accumulates into) dW in place
 __global__ void im2col_kernel(const float* __restrict__ x, int sx, float* __restrict__ cols, int h,
                               int w, int cin, int kh, int kw, int stride, int ph, int pw, int oh,
-                              int ow, long long total_vec, int vec) {
+                              int ow, long long total_vec, int vec, int cmajor) {
   const int K = kh * kw * cin;
   const int kv = K / vec;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total_vec; i += (long long)gridDim.x * 256) {
     const long long p = i / kv;
     const int k = (int)(i % kv) * vec;
-    const int tap = k / cin, c = k % cin;
+    const int tap = cmajor ? k % (kh * kw) : k / cin, c = cmajor ? k / (kh * kw) : k % cin;
     const int ty = tap / kw, tx = tap % kw;
     const int ox = (int)(p % ow);
     const long long t = p / ow;
@@ -1717,19 +1719,27 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
   return scflow_launch_status();
 }
 
-SCFLOW_API int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin,
-                             int kh, int kw, int stride, int ph, int pw, void* stream) {
+SCFLOW_API int scflow_im2col_ex(const float* x, int sx, float* cols, int n, int h, int w, int cin,
+                                int kh, int kw, int stride, int ph, int pw, int channel_major,
+                                void* stream) {
   if (!x || !cols || n <= 0 || h <= 0 || w <= 0 || cin <= 0 || kh <= 0 || kw <= 0 || stride <= 0 ||
       ph < 0 || pw < 0 || sx < cin)
     return SCFLOW_EINVAL;
   const int oh = (h + 2 * ph - kh) / stride + 1, ow = (w + 2 * pw - kw) / stride + 1;
   if (oh <= 0 || ow <= 0) return SCFLOW_EINVAL;
-  const int vec = (cin % 4 == 0 && sx % 4 == 0 && aligned16(x) && aligned16(cols)) ? 4 : 1;
+  const int vec =
+      (!channel_major && cin % 4 == 0 && sx % 4 == 0 && aligned16(x) && aligned16(cols)) ? 4 : 1;
   const long long total = (long long)n * oh * ow * kh * kw * cin / vec;
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   im2col_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, sx, cols, h, w, cin, kh, kw, stride, ph,
-                                                         pw, oh, ow, total, vec);
+                                                         pw, oh, ow, total, vec,
+                                                         channel_major ? 1 : 0);
   return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_im2col(const float* x, int sx, float* cols, int n, int h, int w, int cin,
+                             int kh, int kw, int stride, int ph, int pw, void* stream) {
+  return scflow_im2col_ex(x, sx, cols, n, h, w, cin, kh, kw, stride, ph, pw, 0, stream);
 }
 
 SCFLOW_API int scflow_col2im(const float* cols, float* dx, int sdx, int n, int h, int w, int cin,

@@ -782,8 +782,9 @@ def conv_wgrad(dy: Tensor, src0, src1: Optional[Chan], dw: Tensor, db: Optional[
 
 
 def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, ph: int, pw: int,
-           out: Optional[Tensor] = None) -> Tensor:
-    """Patch matrix [n·oh·ow, kh·kw·cin] of a channels-last input (tensor or Chan)."""
+           out: Optional[Tensor] = None, channel_major: bool = False) -> Tensor:
+    """Patch matrix [n·oh·ow, kh·kw·cin] of a channels-last input (tensor or Chan); columns in
+    (ty, tx, c) order, or (c, ty, tx) with channel_major (a conv weight's own order)."""
     if isinstance(x, Chan):
         _require(x.buf, "x")
         ptr, sx, dev = x.ptr, x.stride, x.buf.device
@@ -793,8 +794,9 @@ def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, p
     oh, ow = (h + 2 * ph - kh) // stride + 1, (w + 2 * pw - kw) // stride + 1
     if out is None:
         out = torch.empty(n * oh * ow, kh * kw * cin, device=dev)
-    check(_lib.load().scflow_im2col(ptr, sx, _p(out), n, h, w, cin, kh, kw, stride, ph, pw,
-                                    torch.cuda.current_stream(dev).cuda_stream), "scflow_im2col")
+    check(_lib.load().scflow_im2col_ex(ptr, sx, _p(out), n, h, w, cin, kh, kw, stride, ph, pw,
+                                       int(channel_major), torch.cuda.current_stream(dev).cuda_stream),
+          "scflow_im2col_ex")
     return out
 
 

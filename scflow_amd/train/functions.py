@@ -247,18 +247,19 @@ def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int,
         return dw, db
     except ScflowError:
         pass
-    if accumulate:
-        gw, gb = _weight_grad(g, x0, x1, w, s, ph, pw, with_bias)
-        dw += gw
-        if with_bias:
-            db += gb
-        return dw, db
-    # shapes outside the wgrad kernel (7×7): HIP im2col + one HIP GEMM
+    # shapes outside the wgrad kernels (7×7): HIP im2col in the weight's own column order + one
+    # HIP GEMM written (or accumulated) straight into dW.  (The bias sum as a ones-row GEMM ran
+    # 44 µs against torch's 19 µs column sum: kept on torch.)
     x = x0 if x1 is None else torch.cat([x0, x1], -1)
-    cols = ops.im2col(x.contiguous(), n, h, wd, cin, kh, kw, s, ph, pw)
-    dwm = ops.gemm(g2.t(), cols)  # [cout, kh·kw·cin]
-    dw = dwm.view(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
-    return dw, (g2.sum(0) if with_bias else None)
+    cols = ops.im2col(x.contiguous(), n, h, wd, cin, kh, kw, s, ph, pw, channel_major=True)
+    beta = 1.0 if accumulate else 0.0
+    ops.gemm(g2.t(), cols, out=dw.view(cout, cin * kh * kw), beta=beta)
+    if with_bias:
+        if accumulate:
+            db += g2.sum(0)
+        else:
+            torch.sum(g2, 0, out=db)
+    return dw, db
 
 
 class _Conv2dNHWC(torch.autograd.Function):
