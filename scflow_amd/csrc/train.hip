@@ -27,25 +27,28 @@
 namespace {
 
 // column order (ty, tx, c), or with cmajor (c, ty, tx) — a conv weight's own [cout][cin][kh][kw]
-// order, so the weight-gradient GEMM writes (or accumulates into) dW in place
+// order, so the weight-gradient GEMM writes (or accumulates into) dW in place.  Index maths in
+// 32 bits when the matrix allows (I = unsigned): 64-bit division is a long software sequence.
+template <typename I>
 __global__ void im2col_kernel(const float* __restrict__ x, int sx, float* __restrict__ cols, int h,
                               int w, int cin, int kh, int kw, int stride, int ph, int pw, int oh,
                               int ow, long long total_vec, int vec, int cmajor) {
-  const int K = kh * kw * cin;
-  const int kv = K / vec;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total_vec; i += (long long)gridDim.x * 256) {
-    const long long p = i / kv;
-    const int k = (int)(i % kv) * vec;
-    const int tap = cmajor ? k % (kh * kw) : k / cin, c = cmajor ? k / (kh * kw) : k % cin;
-    const int ty = tap / kw, tx = tap % kw;
-    const int ox = (int)(p % ow);
-    const long long t = p / ow;
-    const int oy = (int)(t % oh);
-    const int img = (int)(t / oh);
+  const I K = (I)(kh * kw * cin);
+  const I kv = K / (I)vec;
+  const I taps = (I)(kh * kw);
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < (I)total_vec; i += (I)gridDim.x * 256) {
+    const I p = i / kv;
+    const int k = (int)(i - p * kv) * vec;
+    const int tap = cmajor ? (int)((I)k % taps) : k / cin, c = cmajor ? (int)((I)k / taps) : k % cin;
+    const int ty = tap / kw, tx = tap - ty * kw;
+    const I t = p / (I)ow;
+    const int ox = (int)(p - t * (I)ow);
+    const I img = t / (I)oh;
+    const int oy = (int)(t - img * (I)oh);
     const int iy = oy * stride - ph + ty, ix = ox * stride - pw + tx;
     const bool ok = iy >= 0 && iy < h && ix >= 0 && ix < w;
-    const float* src = x + ((size_t)(img * h + iy) * w + ix) * sx + c;
-    float* dst = cols + p * K + k;
+    const float* src = x + ((size_t)((size_t)img * h + iy) * w + ix) * sx + c;
+    float* dst = cols + (size_t)p * K + k;
     if (vec == 4) {
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (ok) v = *(const floatx4*)src;
@@ -60,18 +63,19 @@ __global__ void im2col_kernel(const float* __restrict__ x, int sx, float* __rest
 // oy = (iy + ph − ty)/s, ox = (ix + pw − tx)/s is integral and inside the output grid of
 // cols[(n, oy, ox)][(ty·kw + tx)·cin + c].  A gather (no atomics, fixed order): the strided
 // conv's dX as cols = dY·Wmat (one GEMM with exactly the needed products) + this.
+template <typename I>
 __global__ void col2im_kernel(const float* __restrict__ cols, float* __restrict__ dx, int sdx,
                               int h, int w, int cin, int kh, int kw, int stride, int ph, int pw,
                               int oh, int ow, long long total_vec, int vec) {
   const int K = kh * kw * cin;
-  const int cv = cin / vec;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total_vec; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % cv) * vec;
-    const long long pix = i / cv;
-    const int ix = (int)(pix % w);
-    const long long t = pix / w;
-    const int iy = (int)(t % h);
-    const int img = (int)(t / h);
+  const I cv = (I)(cin / vec);
+  for (I i = (I)blockIdx.x * 256 + threadIdx.x; i < (I)total_vec; i += (I)gridDim.x * 256) {
+    const I pix = i / cv;
+    const int c = (int)(i - pix * cv) * vec;
+    const I t = pix / (I)w;
+    const int ix = (int)(pix - t * (I)w);
+    const int img = (int)(t / (I)h);
+    const int iy = (int)(t - (I)img * (I)h);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int ty = 0; ty < kh; ++ty) {
       const int ny = iy + ph - ty;
@@ -1731,9 +1735,12 @@ SCFLOW_API int scflow_im2col_ex(const float* x, int sx, float* cols, int n, int 
       (!channel_major && cin % 4 == 0 && sx % 4 == 0 && aligned16(x) && aligned16(cols)) ? 4 : 1;
   const long long total = (long long)n * oh * ow * kh * kw * cin / vec;
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
-  im2col_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, sx, cols, h, w, cin, kh, kw, stride, ph,
-                                                         pw, oh, ow, total, vec,
-                                                         channel_major ? 1 : 0);
+  if (total * vec < (1LL << 31) - 256LL * 65536)
+    im2col_kernel<unsigned><<<blocks, 256, 0, (hipStream_t)stream>>>(
+        x, sx, cols, h, w, cin, kh, kw, stride, ph, pw, oh, ow, total, vec, channel_major ? 1 : 0);
+  else
+    im2col_kernel<unsigned long long><<<blocks, 256, 0, (hipStream_t)stream>>>(
+        x, sx, cols, h, w, cin, kh, kw, stride, ph, pw, oh, ow, total, vec, channel_major ? 1 : 0);
   return scflow_launch_status();
 }
 
@@ -1752,8 +1759,12 @@ SCFLOW_API int scflow_col2im(const float* cols, float* dx, int sdx, int n, int h
   const int vec = (cin % 4 == 0 && sdx % 4 == 0 && aligned16(dx) && aligned16(cols)) ? 4 : 1;
   const long long total = (long long)n * h * w * cin / vec;
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
-  col2im_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(cols, dx, sdx, h, w, cin, kh, kw, stride,
-                                                         ph, pw, oh, ow, total, vec);
+  if (total * vec < (1LL << 31) - 256LL * 65536)
+    col2im_kernel<unsigned><<<blocks, 256, 0, (hipStream_t)stream>>>(cols, dx, sdx, h, w, cin, kh, kw,
+                                                                     stride, ph, pw, oh, ow, total, vec);
+  else
+    col2im_kernel<unsigned long long><<<blocks, 256, 0, (hipStream_t)stream>>>(
+        cols, dx, sdx, h, w, cin, kh, kw, stride, ph, pw, oh, ow, total, vec);
   return scflow_launch_status();
 }
 
