@@ -1674,23 +1674,31 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
   const bool vec = a.cout % 4 == 0 && a.sdy % 4 == 0 && aligned16(a.dy) && a.cin0 % 4 == 0 &&
                    a.s0 % 4 == 0 && aligned16(a.src0) &&
                    (a.cin1 == 0 || (a.cin1 % 4 == 0 && a.s1 % 4 == 0 && aligned16(a.src1)));
+  // (3×3: one workgroup per CU; SCFLOW_WGRAD_KS=1 keeps one wave set, tuning only)
+  static const int ks_env = [] {
+    const char* e = getenv("SCFLOW_WGRAD_KS");
+    return e ? atoi(e) : 2;
+  }();
+  // the GRU's 1×5 / 5×1: two wave sets when cout ≤ 128 (q: 90 → 81 µs for 5×1, 80 → 71 for 1×5
+  // at configs[3]); one for the 256-wide z | r, which two sets slow (131 → 137, 146 → 155 µs).
+  // SCFLOW_WGRAD_KS5=0 never, 2 always (tuning)
+  static const int ks5_env = [] {
+    const char* e = getenv("SCFLOW_WGRAD_KS5");
+    return e ? atoi(e) : 1;
+  }();
   const size_t lds1 = sizeof(float) * (size_t)(P.cp + P.hr * P.hc) * WT;
-  const int occ = taps >= 9 ? 1 : 2;
+  const bool ks5 = taps == 5 && (ks5_env == 2 || (ks5_env == 1 && a.cout <= 128));
+  const int occ = taps >= 9 || ks5 ? 1 : 2;
   const bool db2 = vec && 2 * lds1 * occ <= 160 * 1024;  // double-buffer if it keeps occupancy
   const size_t lds = lds1 * (db2 ? 2 : 1);
   if (lds > 160 * 1024) return SCFLOW_EUNSUPPORTED;
   const dim3 grid((unsigned)(P.co_tiles * (P.cinp / WT)), (unsigned)splits);
   hipStream_t st = (hipStream_t)stream;
-  // 3×3 (one workgroup per CU): two wave sets splitting each chunk's k-steps (SCFLOW_WGRAD_KS=1
-  // keeps one set; tuning only)
-  static const int ks_env = [] {
-    const char* e = getenv("SCFLOW_WGRAD_KS");
-    return e ? atoi(e) : 2;
-  }();
-  const bool ks2 = vec && taps >= 9 && ks_env == 2;
+  // two wave sets splitting each chunk's k-steps
+  const bool ks2 = vec && ((taps >= 9 && ks_env == 2) || ks5);
 #define SCFLOW_WG(KH_, KW_, S_)                                                                  \
   if (a.kh == KH_ && a.kw == KW_ && a.stride == S_) {                                            \
-    if (KH_ * KW_ >= 9 && ks2) {                                                                 \
+    if (KH_ * KW_ >= 5 && ks2) {                                                                 \
       if (db2)                                                                                   \
         wgrad_kernel<KH_, KW_, S_, true, true, 64, 2><<<grid, 512, lds, st>>>(P, slab, bslab);   \
       else                                                                                       \

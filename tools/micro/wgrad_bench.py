@@ -15,7 +15,8 @@ SHAPES = [  # n, h, w, cin, cout, kh, kw, stride
     (16, 32, 32, 256, 2, 3, 3, 1), (16, 32, 32, 1, 64, 3, 3, 1), (16, 32, 32, 256, 1, 1, 1, 1),
     (16, 32, 32, 64, 32, 3, 3, 1), (16, 32, 32, 128, 64, 3, 3, 1), (16, 32, 32, 256, 128, 3, 3, 1),
     (16, 32, 32, 128, 256, 3, 3, 1), (16, 32, 32, 256, 192, 3, 3, 1), (16, 32, 32, 256, 256, 1, 5, 1),
-    (16, 32, 32, 256, 128, 5, 1, 1), (16, 32, 32, 324, 256, 1, 1, 1), (16, 32, 32, 224, 128, 3, 3, 2),
+    (16, 32, 32, 256, 128, 5, 1, 1),
+    (16, 32, 32, 256, 256, 5, 1, 1), (16, 32, 32, 256, 128, 1, 5, 1), (16, 32, 32, 324, 256, 1, 1, 1), (16, 32, 32, 224, 128, 3, 3, 2),
     (16, 16, 16, 128, 128, 3, 3, 2), (16, 8, 8, 128, 128, 3, 3, 2), (32, 128, 128, 64, 64, 3, 3, 1),
     (32, 64, 64, 96, 96, 3, 3, 1), (16, 32, 32, 256, 128, 3, 3, 1), (16, 32, 32, 2, 128, 7, 7, 1),
     (32, 256, 256, 3, 64, 7, 7, 2),
