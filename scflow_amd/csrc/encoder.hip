@@ -281,6 +281,109 @@ __global__ __launch_bounds__(256) void enc_stem_kernel(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// stem on the matrix cores (npad = 64): implicit GEMM, M = 128 output pixels of one row (wave
+// w: pixels 32w..32w+31), N = 64 channels (two 32-column blocks), K = KH·KW·CIN taps (147 → 74
+// k-pairs of v_mfma_f32_32x32x2_f32).  A workgroup runs STEM_ROWS consecutive output rows: the
+// packed weights [K][64] are staged in LDS once, each row's input halo [KH][HC][CIN] is staged
+// in LDS from registers that were loaded while the previous row's MFMAs ran.  A lane reads its A
+// value (pixel li, tap k = 2kp + hh) and its two B values straight from LDS — the tap offsets
+// fold to constants in the unrolled K loop.  Same epilogue as enc_stem_kernel.  (The VALU kernel
+// paid one LDS broadcast per FMA: ~25 TFLOP/s.)
+// ------------------------------------------------------------------------------------------
+constexpr int STEM_ROWS = 4;
+template <int CIN, int KH, int KW, int S>
+__global__ __launch_bounds__(256, 2) void enc_stem_mfma_kernel(
+    const float* __restrict__ img_in, const float* __restrict__ wpk, const float* __restrict__ bias,
+    const float* __restrict__ osc_, const float* __restrict__ osh_, float* __restrict__ out, int h,
+    int w, int oh, int ow, int cout, int pad, int act) {
+  constexpr int K = KH * KW * CIN;
+  constexpr int KP = (K + 1) / 2;
+  constexpr int HC = 127 * S + KW;
+  constexpr int NH = KH * HC * CIN;
+  constexpr int NJ = (NH + 255) / 256;
+  __shared__ float halo[NH];
+  __shared__ float ws[2 * KP * 64];
+  const int tiles_x = (ow + 127) / 128;
+  const int row_blocks = (oh + STEM_ROWS - 1) / STEM_ROWS;
+  const int t = blockIdx.x;
+  const int tx0 = (t % tiles_x) * 128;
+  const int oy0 = ((t / tiles_x) % row_blocks) * STEM_ROWS;
+  const int img = t / (tiles_x * row_blocks);
+  const int oy1 = oy0 + STEM_ROWS < oh ? oy0 + STEM_ROWS : oh;
+  float pre[NJ];
+  auto gload = [&](int oy) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int col = i % HC, row = (i / HC) % KH, c = i / (HC * KH);
+      const int iy = oy * S - pad + row, ix = tx0 * S - pad + col;
+      float v = 0.f;
+      if (i < NH && iy >= 0 && iy < h && ix >= 0 && ix < w)
+        v = img_in[(((size_t)img * CIN + c) * h + iy) * w + ix];
+      pre[j] = v;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int col = i % HC, row = (i / HC) % KH, c = i / (HC * KH);
+      if (i < NH) halo[(row * HC + col) * CIN + c] = pre[j];
+    }
+  };
+  gload(oy0);
+  for (int i = threadIdx.x; i < 2 * KP * 64; i += 256) ws[i] = i < K * 64 ? wpk[i] : 0.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 31, hh = lane >> 5;
+  const float* hp = halo + (wave * 32 + li) * S * CIN;
+  const float* wp = ws + hh * 64 + li;
+  float bv[2], sc[2], sh[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int co = nb * 32 + li;
+    const bool ok = co < cout;
+    bv[nb] = (bias && ok) ? bias[co] : 0.f;
+    sc[nb] = (osc_ && ok) ? osc_[co] : 1.f;
+    sh[nb] = (osc_ && ok) ? osh_[co] : 0.f;
+  }
+  for (int oy = oy0; oy < oy1; ++oy) {
+    __syncthreads();  // the previous row's MFMAs are done with the halo
+    lstore();
+    __syncthreads();
+    if (oy + 1 < oy1) gload(oy + 1);
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc0[e] = acc1[e] = 0.f;
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      // tap offsets of k = 2kp and 2kp + 1 in the halo (the padding tap k = K reads tap 0: its
+      // weight row is zero)
+      const int k0 = 2 * kp, k1 = 2 * kp + 1 < K ? 2 * kp + 1 : 0;
+      const int o0 = ((k0 / CIN) / KW * HC + (k0 / CIN) % KW) * CIN + k0 % CIN;
+      const int o1 = ((k1 / CIN) / KW * HC + (k1 / CIN) % KW) * CIN + k1 % CIN;
+      const float a = hp[hh ? o1 : o0];
+      const float b0 = wp[kp * 128], b1 = wp[kp * 128 + 32];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+    }
+    // C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+    float* orow = out + (size_t)(img * oh + oy) * ow * cout;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int co = nb * 32 + li;
+      if (co >= cout) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ox = tx0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (ox >= ow) continue;
+        float v = (nb ? acc1[r] : acc0[r]) + bv[nb];
+        if (osc_) v = v * sc[nb] + sh[nb];
+        orow[(size_t)ox * cout + co] = act_apply(v, act);
+      }
+    }
+  }
+}
+
 __global__ void enc_stem_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,
                                      int cin, int taps, int npad, long long total) {
   for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total;
@@ -492,6 +595,22 @@ SCFLOW_API int scflow_enc_stem(const float* img, const float* packed, const floa
   if (oh <= 0 || ow <= 0) return SCFLOW_EINVAL;
   const unsigned tiles = (unsigned)((long long)n * oh * ((ow + 31) / 32));
   hipStream_t st = (hipStream_t)stream;
+  static int mfma = -1;  // SCFLOW_STEM_MFMA=0 keeps the VALU kernel (A/B only)
+  if (mfma < 0) {
+    const char* e = getenv("SCFLOW_STEM_MFMA");
+    mfma = e ? atoi(e) != 0 : 1;
+  }
+  if (mfma && npad == 64 && cin == 3 && kh == 7 && kw == 7 && (stride == 1 || stride == 2)) {
+    const unsigned rows =
+        (unsigned)((long long)n * ((oh + STEM_ROWS - 1) / STEM_ROWS) * ((ow + 127) / 128));
+    if (stride == 2)
+      enc_stem_mfma_kernel<3, 7, 7, 2><<<rows, 256, 0, st>>>(img, packed, bias, out_scale, out_shift,
+                                                             out, h, w, oh, ow, cout, pad, act);
+    else
+      enc_stem_mfma_kernel<3, 7, 7, 1><<<rows, 256, 0, st>>>(img, packed, bias, out_scale, out_shift,
+                                                             out, h, w, oh, ow, cout, pad, act);
+    return scflow_launch_status();
+  }
   if (cin == 3 && kh == 7 && kw == 7 && stride == 2) {
     enc_stem_kernel<3, 7, 7, 2><<<tiles, 256, 0, st>>>(img, packed, bias, out_scale, out_shift, out,
                                                        h, w, oh, ow, cout, npad, pad, act);
