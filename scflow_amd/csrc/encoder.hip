@@ -18,8 +18,9 @@
 //    and shift; padding stays zero) so normalised activations are never written to HBM;
 //    the epilogue fuses bias, an eval-BatchNorm affine, the residual add and the activation
 //    (or a split tanh | relu for the context output).
-//  * enc_stem_kernel — the 3-channel 7×7/2 stem: lane = output channel with its 147 weights in
-//    VGPRs, the tile's input halo staged from the NCHW image in LDS and read as broadcasts.
+//  * enc_stem_mfma_kernel — the 3-channel 7×7 stem as an implicit GEMM on fp32 MFMA (64 output
+//    channels); enc_stem_kernel — the VALU form for wider stems: lane = output channel with its
+//    147 weights in VGPRs, the tile's input halo staged from the NCHW image in LDS.
 //  * enc_stats_kernel / enc_norm_finalize_kernel — InstanceNorm statistics in fp64 (partial sums
 //    over pixel chunks, deterministic order), → per (image, channel) scale/shift.
 //  * enc_apply_kernel — relu(norm(x) + identity') where the block output must be materialised
@@ -284,15 +285,14 @@ __global__ __launch_bounds__(256) void enc_stem_kernel(const float* __restrict__
 // ------------------------------------------------------------------------------------------
 // stem on the matrix cores (npad = 64): implicit GEMM, M = 128 output pixels of one row (wave
 // w: pixels 32w..32w+31), N = 64 channels (two 32-column blocks), K = KH·KW·CIN taps (147 → 74
-// k-pairs of v_mfma_f32_32x32x2_f32).  A workgroup runs STEM_ROWS consecutive output rows: the
+// k-pairs of v_mfma_f32_32x32x2_f32).  A workgroup runs STEM_ROWS (8) consecutive output rows: the
 // packed weights [K][64] are staged in LDS once, each row's input halo [KH][HC][CIN] is staged
 // in LDS from registers that were loaded while the previous row's MFMAs ran.  A lane reads its A
 // value (pixel li, tap k = 2kp + hh) and its two B values straight from LDS — the tap offsets
 // fold to constants in the unrolled K loop.  Same epilogue as enc_stem_kernel.  (The VALU kernel
 // paid one LDS broadcast per FMA: ~25 TFLOP/s.)
 // ------------------------------------------------------------------------------------------
-constexpr int STEM_ROWS = 4;
-template <int CIN, int KH, int KW, int S>
+template <int CIN, int KH, int KW, int S, int STEM_ROWS>
 __global__ __launch_bounds__(256, 2) void enc_stem_mfma_kernel(
     const float* __restrict__ img_in, const float* __restrict__ wpk, const float* __restrict__ bias,
     const float* __restrict__ osc_, const float* __restrict__ osh_, float* __restrict__ out, int h,
@@ -601,14 +601,25 @@ SCFLOW_API int scflow_enc_stem(const float* img, const float* packed, const floa
     mfma = e ? atoi(e) != 0 : 1;
   }
   if (mfma && npad == 64 && cin == 3 && kh == 7 && kw == 7 && (stride == 1 || stride == 2)) {
-    const unsigned rows =
-        (unsigned)((long long)n * ((oh + STEM_ROWS - 1) / STEM_ROWS) * ((ow + 127) / 128));
-    if (stride == 2)
-      enc_stem_mfma_kernel<3, 7, 7, 2><<<rows, 256, 0, st>>>(img, packed, bias, out_scale, out_shift,
-                                                             out, h, w, oh, ow, cout, pad, act);
-    else
-      enc_stem_mfma_kernel<3, 7, 7, 1><<<rows, 256, 0, st>>>(img, packed, bias, out_scale, out_shift,
-                                                             out, h, w, oh, ow, cout, pad, act);
+    static int srows = 0;  // output rows per workgroup (SCFLOW_STEM_ROWS=4|8|16, tuning)
+    if (!srows) {
+      const char* e = getenv("SCFLOW_STEM_ROWS");
+      srows = e ? atoi(e) : 8;  // 4 / 8 / 16 rows: 226 / 208 / 230 us per e2e stem call
+      if (srows != 4 && srows != 16) srows = 8;
+    }
+    const unsigned rows = (unsigned)((long long)n * ((oh + srows - 1) / srows) * ((ow + 127) / 128));
+#define STEM_LAUNCH(S_, R_)                                                                   \
+  enc_stem_mfma_kernel<3, 7, 7, S_, R_><<<rows, 256, 0, st>>>(img, packed, bias, out_scale, \
+                                                              out_shift, out, h, w, oh, ow,  \
+                                                              cout, pad, act)
+    if (stride == 2) {
+      if (srows == 16) STEM_LAUNCH(2, 16);
+      else if (srows == 4) STEM_LAUNCH(2, 4);
+      else STEM_LAUNCH(2, 8);
+    } else {
+      STEM_LAUNCH(1, 4);
+    }
+#undef STEM_LAUNCH
     return scflow_launch_status();
   }
   if (cin == 3 && kh == 7 && kw == 7 && stride == 2) {
