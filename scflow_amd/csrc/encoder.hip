@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void enc_stem_kernel(const float* __restrict__
 // stem on the matrix cores (npad = 64): implicit GEMM, M = 128 output pixels of one row (wave
 // w: pixels 32w..32w+31), N = 64 channels (two 32-column blocks), K = KH·KW·CIN taps (147 → 74
 // k-pairs of v_mfma_f32_32x32x2_f32).  A workgroup runs STEM_ROWS (8) consecutive output rows: the
-// packed weights [K][64] are staged in LDS once, each row's input halo [KH][HC][CIN] is staged
+// packed weights [K][64] are staged in LDS once, each row's input halo [CIN][KH][HC] is staged
 // in LDS from registers that were loaded while the previous row's MFMAs ran.  A lane reads its A
 // value (pixel li, tap k = 2kp + hh) and its two B values straight from LDS — the tap offsets
 // fold to constants in the unrolled K loop.  Same epilogue as enc_stem_kernel.  (The VALU kernel
@@ -328,14 +328,13 @@ __global__ __launch_bounds__(256, 2) void enc_stem_mfma_kernel(
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int i = threadIdx.x + 256 * j;
-      const int col = i % HC, row = (i / HC) % KH, c = i / (HC * KH);
-      if (i < NH) halo[(row * HC + col) * CIN + c] = pre[j];
+      if (i < NH) halo[i] = pre[j];
     }
   };
   gload(oy0);
   for (int i = threadIdx.x; i < 2 * KP * 64; i += 256) ws[i] = i < K * 64 ? wpk[i] : 0.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 31, hh = lane >> 5;
-  const float* hp = halo + (wave * 32 + li) * S * CIN;
+  const float* hp = halo + (wave * 32 + li) * S;
   const float* wp = ws + hh * 64 + li;
   float bv[2], sc[2], sh[2];
 #pragma unroll
@@ -359,8 +358,8 @@ __global__ __launch_bounds__(256, 2) void enc_stem_mfma_kernel(
       // tap offsets of k = 2kp and 2kp + 1 in the halo (the padding tap k = K reads tap 0: its
       // weight row is zero)
       const int k0 = 2 * kp, k1 = 2 * kp + 1 < K ? 2 * kp + 1 : 0;
-      const int o0 = ((k0 / CIN) / KW * HC + (k0 / CIN) % KW) * CIN + k0 % CIN;
-      const int o1 = ((k1 / CIN) / KW * HC + (k1 / CIN) % KW) * CIN + k1 % CIN;
+      const int o0 = ((k0 % CIN) * KH + (k0 / CIN) / KW) * HC + (k0 / CIN) % KW;
+      const int o1 = ((k1 % CIN) * KH + (k1 / CIN) / KW) * HC + (k1 / CIN) % KW;
       const float a = hp[hh ? o1 : o0];
       const float b0 = wp[kp * 128], b1 = wp[kp * 128 + 32];
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);

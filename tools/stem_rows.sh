@@ -3,7 +3,7 @@
 # setting, then a kernel-trace profile of the end-to-end leg → gpurun_out/stem_rows.txt
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 : > $OUT/stem_rows.txt
-for rows in 4 8 16; do
+for rows in ${STEM_ROWS_LIST:-4 8 16}; do
   SCFLOW_STEM_ROWS=$rows timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu $R/tests/test_gpu_encoder.py > $OUT/stem_rows_$rows.log 2>&1 || { tail -20 $OUT/stem_rows_$rows.log; exit 1; }
   echo "rows=$rows $(tail -1 $OUT/stem_rows_$rows.log)" >> $OUT/stem_rows.txt
   cd /tmp
