@@ -343,8 +343,9 @@ int scflow_ph_tail(const scflow_ph_tail_args* args, void* stream);
  *   where x' = relu(x·in_scale[img][c] + in_shift[img][c]) if in_scale is given (the previous
  *   InstanceNorm + ReLU applied on load; zero padding stays zero), else x.
  *   Weights packed by scflow_enc_conv_pack (same shape).
- * scflow_enc_stem: 7×7 (any kh,kw ≤ 7) conv of an NCHW image batch [n][cin≤4][h][w], stride s,
- *   written channels-last with the same bias / out_scale / act epilogue (the stem conv1).
+ * scflow_enc_stem: 7×7 conv of an NCHW image batch [n][3][h][w], stride 1 or 2 (other shapes:
+ *   SCFLOW_EUNSUPPORTED), written channels-last with the same bias / out_scale / act epilogue
+ *   (the stem conv1); cout ≤ 64 runs as an implicit GEMM on fp32 MFMA, wider stems on VALU.
  *   Weights packed by scflow_enc_stem_pack ([kh·kw·cin][roundup(cout,64)]).
  *   With src1 the input is cat[src, src1] (both normalised on load when in_scale is given,
  *   in_scale then covering cin + cin1 channels).
