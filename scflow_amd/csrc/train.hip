@@ -964,6 +964,8 @@ __global__ void in_bwd_finalize_kernel(const double* __restrict__ partial, int n
   if (i >= n * c) return;
   const int img = i / c, ch = i % c;
   double s = 0, s2 = 0;
+  // unrolled so the chunks' loads are in flight together (the fp64 sums keep their order)
+#pragma unroll 16
   for (int k = 0; k < chunks; ++k) {
     const double* o = partial + (((size_t)img * chunks + k) * 2) * c;
     s += o[ch];
