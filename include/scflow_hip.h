@@ -326,6 +326,9 @@ typedef struct scflow_ph_tail_args {
   int* sync;
   void* stamps;                           /* NULL, or (profiling) 4 u64 real-time-clock stamps per
                                              work item: start, dependencies met, body done, signalled */
+  int* error;                             /* NULL, or a word the launch ORs 1 into when a wait gives
+                                             up; never cleared by the call, so one word checked after
+                                             a sequence of launches covers all of them */
 } scflow_ph_tail_args;
 int scflow_ph_tail_sync_ints(int n);
 int scflow_ph_tail(const scflow_ph_tail_args* args, void* stream);

@@ -100,7 +100,7 @@ class PhTailArgs(ctypes.Structure):
         ("fc2_w", c_vp), ("fc2_b", c_vp), ("fc2_n", c_int), ("fc2_split", c_int), ("fc2_parts", c_vp),
         ("rot_w", c_vp), ("rot_b", c_vp), ("rch", c_int), ("trans_w", c_vp), ("trans_b", c_vp),
         ("label", c_vp), ("num_class", c_int), ("drot", c_vp), ("dt", c_vp),
-        ("pose", ctypes.POINTER(PoseStepArgs)), ("sync", c_vp), ("stamps", c_vp),
+        ("pose", ctypes.POINTER(PoseStepArgs)), ("sync", c_vp), ("stamps", c_vp), ("error", c_vp),
     ]
 
 
@@ -236,6 +236,21 @@ SIGNATURES = {
 }
 
 _lib = None
+
+# Weight-derived caches (packed / flipped / affine forms) are keyed by (data_ptr, _version) of
+# the weights AND by this generation: an update that does not move the version counters — a
+# replayed hipGraph of the optimizer step (TrainStep(graph=True)) writes the parameters without
+# autograd seeing it — bumps the generation so every cache re-derives its forms.
+_WEIGHTS_GEN = 0
+
+
+def weights_generation() -> int:
+    return _WEIGHTS_GEN
+
+
+def bump_weights_generation() -> None:
+    global _WEIGHTS_GEN
+    _WEIGHTS_GEN += 1
 
 
 class ScflowError(RuntimeError):

@@ -446,6 +446,7 @@ struct PhTail {
   int off[10];  // first ticket of phase p; off[9] = total
   int dbg;      // debugging (SCFLOW_PHT_DBG): bit 0 skips the item bodies, bit 1 the publishes
   unsigned long long* stamps;  // debugging: per ticket 4 real-time stamps (start, waited, body, out)
+  int* error;                  // sticky give-up flag across launches (host-checked), or null
 };
 
 enum { PHT_GN0, PHT_CONV2, PHT_GN1, PHT_CONV3, PHT_GN2, PHT_FC1, PHT_FC2, PHT_HEADS, PHT_POSE };
@@ -668,7 +669,9 @@ __global__ __launch_bounds__(PHT_WAVES * 64) void ph_tail_kernel(PhTail A) {
     if (st && tid == 0) st[4 * t] = __builtin_amdgcn_s_memrealtime();
     if (d.wait_count > 0) {
       if (tid == 0)
-        for (int k = 0; k < d.wait_count; ++k) pht_wait(S, d.wait0 + k, d.target, t, ph);
+        for (int k = 0; k < d.wait_count; ++k)
+          if (!pht_wait(S, d.wait0 + k, d.target, t, ph) && K->error)
+            __hip_atomic_fetch_or(K->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pht_join_after_wait();
     }
     const int dbg = K->dbg;
@@ -995,6 +998,7 @@ SCFLOW_API int scflow_ph_tail(const scflow_ph_tail_args* p, void* stream) {
   for (int k = 0; k < 9; ++k) A.off[k + 1] = A.off[k] + items[k];
   if (const char* e = getenv("SCFLOW_PHT_DBG")) A.dbg = atoi(e);
   A.stamps = (unsigned long long*)p->stamps;
+  A.error = p->error;
   if (const char* e = getenv("SCFLOW_PHT_PHASES")) {  // debugging: run only the first k phases
     const int k = atoi(e);
     if (k >= 0 && k < 9) A.off[9] = A.off[k];

@@ -1794,7 +1794,7 @@ SCFLOW_API int scflow_corr_lookup_backward(const float* dout, int out_layout, in
     const char* e = getenv("SCFLOW_LOOKUP_BWD_WIN");
     return e && e[0] == '0';
   }();
-  if (radius <= 4 && !win_off) {
+  if (radius >= 1 && radius <= 4 && !win_off) {
     const long long tw = (long long)n * h * w * num_levels;
     const unsigned bw = (unsigned)((tw + 255) / 256);
     switch (radius) {
@@ -1808,6 +1808,8 @@ SCFLOW_API int scflow_corr_lookup_backward(const float* dout, int out_layout, in
       SCFLOW_LKW(3)
       SCFLOW_LKW(4)
 #undef SCFLOW_LKW
+      default:
+        return SCFLOW_EUNSUPPORTED;
     }
     return scflow_launch_status();
   }

@@ -596,5 +596,9 @@ class SCFlowDecoder(nn.Module):
             dts.append(dtr)
             yield "tail"
 
+        if fuse_ph and ph_ctx:
+            # the opt-in persistent tail: a dependency wait that gave up leaves invalid poses —
+            # check the launches' sticky error word once per forward (one host sync)
+            self.pose_pred.tail_check(ph_ctx[0])
         return (list(o_flow_pose.unbind(0)), list(o_flow_pred.unbind(0)), list(o_R.unbind(0)),
                 list(o_t.unbind(0)), list(o_mask.unbind(0)), drots, dts)

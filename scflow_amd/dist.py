@@ -39,7 +39,9 @@ def shard_batch(batch: Dict[str, Tensor], rank: int, world: int, batch_dim: int 
     the pose head's label: sharded output then equals unsharded output for multi-class
     batches.  (The reference's own DDP runs — ``train.py:42-45``, ``tools/eval.py`` — shard
     through the data loader, so there every rank uses its local ``label[0]``; pass
-    ``head_label_key=None`` for that behaviour.)"""
+    ``head_label_key=None`` for that behaviour.  Training shards should: the reference's DDP
+    gradient is the mean of per-replica gradients, each with its local ``label[0]`` and its
+    own BatchNorm statistics — ``shard_train_batch``.)"""
     sizes = {v.shape[batch_dim] for v in batch.values() if isinstance(v, Tensor) and v.dim() > 0}
     if len(sizes) != 1:
         raise ValueError(f"inconsistent batch sizes {sizes}")
@@ -50,6 +52,16 @@ def shard_batch(batch: Dict[str, Tensor], rank: int, world: int, batch_dim: int 
     if head_label_key is not None and head_label_key in batch and "head_label" not in batch:
         out["head_label"] = batch[head_label_key].narrow(batch_dim, 0, 1)
     return out
+
+
+def shard_train_batch(batch: Dict[str, Tensor], rank: int, world: int) -> Dict[str, Tensor]:
+    """``shard_batch`` for the training step, with the reference's DDP semantics: no global
+    ``head_label`` — each replica's pose head takes its local ``label[0]`` (pose_head.py:208-209
+    under the DataLoader's per-rank sampling, train.py:42-45), and its context-encoder BatchNorm
+    normalises with its own shard's statistics (plain BN, scflow_ycbv_real.py:198), so the
+    all-reduced gradient is the mean of the per-shard single-process gradients
+    (tests/test_train_dist_cpu.py)."""
+    return shard_batch(batch, rank, world, head_label_key=None)
 
 
 def gather_shards(x: Tensor, group=None) -> Tensor:

@@ -103,7 +103,7 @@ class ResLayer(nn.Sequential):
 def _bn_affine(bn: nn.BatchNorm2d) -> Tuple[Tensor, Tensor]:
     """Eval BatchNorm as y = x·scale + shift (per channel), cached per parameter version."""
     key = tuple((t.data_ptr(), t._version) for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)
-                if t is not None)
+                if t is not None) + (_lib.weights_generation(),)
     if getattr(bn, "_scflow_key", None) != key:
         with torch.no_grad():
             inv = torch.rsqrt(bn.running_var.float() + bn.eps)
@@ -118,7 +118,7 @@ def _bn_affine(bn: nn.BatchNorm2d) -> Tuple[Tensor, Tensor]:
 
 def _packed(conv: nn.Conv2d, stem: bool = False) -> Tensor:
     w = conv.weight
-    key = (w.data_ptr(), w._version, stem)
+    key = (w.data_ptr(), w._version, stem, _lib.weights_generation())
     if getattr(conv, "_scflow_enc_key", None) != key:
         conv._scflow_enc_packed = ops.enc_stem_pack(w) if stem else ops.enc_conv_pack(w)
         conv._scflow_enc_key = key
@@ -138,7 +138,7 @@ def _wino_conv(conv: nn.Conv2d, x: Tensor, out: Tensor, n: int, h: int, w: int, 
                out_scale: Optional[Tensor] = None, out_shift: Optional[Tensor] = None,
                res: Optional[Tensor] = None, act: Optional[str] = None) -> None:
     wt = conv.weight
-    key = (wt.data_ptr(), wt._version, cin, w)
+    key = (wt.data_ptr(), wt._version, cin, w, _lib.weights_generation())
     cache = getattr(conv, "_scflow_wino", None)
     if cache is None or cache[0] != key:
         cache = (key, ops.pack_conv_weight(wt.detach().float(), cin, 0, w, 1, _lib.CONV_WINO))

@@ -27,8 +27,9 @@ Tensor = torch.Tensor
 
 
 def _param_versions(module: torch.nn.Module):
+    from ._lib import weights_generation
     return tuple((p.data_ptr(), p._version) for p in module.state_dict().values()
-                 if isinstance(p, torch.Tensor))
+                 if isinstance(p, torch.Tensor)) + (weights_generation(),)
 
 
 class GraphedForward:

@@ -30,7 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib, ops
-from ._lib import EPI_GRU_Q, EPI_GRU_ZR, EPI_PLAIN
+from ._lib import EPI_GRU_Q, EPI_GRU_ZR, EPI_PLAIN, ScflowError
 from .ops import Chan
 from .registry import MODELS
 
@@ -132,7 +132,7 @@ class ConvRunner:
         return r
 
     def packed(self, c0: int, c1: int, w: int, bk: int = 16) -> Tuple[Tensor, Optional[Tensor]]:
-        key = (c0, c1, w, bk) + tuple((c.weight.data_ptr(), c.weight._version,
+        key = (c0, c1, w, bk, _lib.weights_generation()) + tuple((c.weight.data_ptr(), c.weight._version,
                                    None if c.bias is None else (c.bias.data_ptr(), c.bias._version))
                                   for c in self.convs)
         if key != self._key:
@@ -595,7 +595,7 @@ class MultiClassPoseHead(nn.Module):
     def _packs(self, c_last: int, hw_last: int):
         w1 = self.fc_layers[0][0].weight
         key = tuple((m.conv.weight.data_ptr(), m.conv.weight._version) for m in self.conv_layers) + (
-            w1.data_ptr(), w1._version, c_last, hw_last)
+            w1.data_ptr(), w1._version, c_last, hw_last, _lib.weights_generation())
         if getattr(self, "_pack_key", None) != key:
             self._packed = [ops.ph_conv_pack(m.conv.weight) for m in self.conv_layers]
             self._fc1_perm = ops.ph_fc_permute(w1, c_last, hw_last)
@@ -622,7 +622,7 @@ class MultiClassPoseHead(nn.Module):
         packs = getattr(self, "_mfma_packs", None)
         if packs is None:
             packs = self._mfma_packs = {}
-        key = (wt.data_ptr(), wt._version)
+        key = (wt.data_ptr(), wt._version, _lib.weights_generation())
         if packs.get(i, (None,))[0] != key:
             packs[i] = (key, ops.enc_conv_pack(wt))
         tiles = n * (oh // (tm // tc)) * (ow // tc) * ((conv.out_channels + 63) // 64)
@@ -829,13 +829,15 @@ class MultiClassPoseHead(nn.Module):
             sync = torch.zeros(_lib.load().scflow_ph_tail_sync_ints(n), device=dev,
                                dtype=torch.int32)
             keep.append(sync)
+            err = torch.zeros(4, device=dev, dtype=torch.int32)  # sticky give-up flag
+            keep.append(err)
             ctx["tail_ws"] = dict(
                 y=[empty(n * hs[l] * wsz[l], c) for l in range(3)],
                 scale=[empty(n, c) for _ in range(3)], shift=[empty(n, c) for _ in range(3)],
                 splits=splits,
                 conv_parts=[empty(splits[j] * n * hs[j + 1] * wsz[j + 1], c) for j in range(2)],
                 fc1_parts=empty(self.tail_fc_split[0], n, f1),
-                fc2_parts=empty(self.tail_fc_split[1], n, f2), sync=sync)
+                fc2_parts=empty(self.tail_fc_split[1], n, f2), sync=sync, err=err)
         t = ctx["tail_ws"]
         a = _lib.PhTailArgs()
         a.n, a.c, a.groups = n, c, self.conv_layers[0].gn.num_groups
@@ -867,7 +869,17 @@ class MultiClassPoseHead(nn.Module):
         if pose is not None:
             a.pose = ctypes.pointer(pose)
         a.sync = t["sync"].data_ptr()
+        a.error = t["err"].data_ptr()
         return a
+
+    @staticmethod
+    def tail_check(ctx: dict) -> None:
+        """Raise if any ``scflow_ph_tail`` launch made with this context gave up a dependency wait
+        (its results are then invalid).  Reads the sticky error word: a host synchronisation."""
+        t = ctx.get("tail_ws")
+        if t is not None and int(t["err"][0].item()):
+            raise ScflowError("scflow_ph_tail: a work item's dependency wait gave up (protocol "
+                              "stall); the pose-head results of this forward are invalid")
 
     def forward_fused(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
                       label: Tensor) -> Tuple[Tensor, Tensor]:
@@ -878,6 +890,7 @@ class MultiClassPoseHead(nn.Module):
         dt = torch.empty(n, 3, device=dev)
         ops.ph_tail(self.tail_args(ctx, label.to(dev), drot, dt), drot)
         ctx["result"] = (drot, dt)
+        self.tail_check(ctx)
         return drot, dt
 
     def forward(self, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:

@@ -33,7 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from .._lib import EPI_PLAIN, ScflowError
+from .._lib import EPI_PLAIN, ScflowError, weights_generation
 from ..ops import Chan
 
 Tensor = torch.Tensor
@@ -77,7 +77,7 @@ def _cached(w: Tensor, key: tuple, make):
         if hit is None:
             hit = _CAPTURE_CACHE[k] = (w, make())  # w kept alive so its id stays unique
         return hit[1]
-    ver = w._version
+    ver = (w._version, weights_generation())
     cache = getattr(w, "_scflow_cache", None)
     if cache is None or cache[0] != ver:
         cache = (ver, {})
@@ -363,20 +363,28 @@ def _shared_grad_holder(w: Tensor) -> dict:
     concatenated weights, used by all 8 iterations)."""
     holder = getattr(w, "_scflow_gacc", None)
     if holder is None:
-        holder = {"buf": None}
+        holder = {"buf": None, "uses": 0, "seen": 0}
         w._scflow_gacc = holder
+    holder["uses"] += 1
     return holder
 
 
 def _shared_wgrad(holder: dict, w: Tensor, add) -> Optional[Tensor]:
     """Add this use's weight gradient into the shared buffer (``add(buf)``); the first backward
     call hands the buffer to autograd, the later ones nothing — autograd runs the backward of
-    ``w``'s producer only after every use, so it receives the complete sum with no per-use adds."""
+    ``w``'s producer only after every use, so it receives the complete sum with no per-use adds.
+    Once a backward pass has seen every use the buffer is released, so a second pass over the
+    same graph (retain_graph) accumulates into a fresh one."""
     first = holder["buf"] is None
     if first:
         holder["buf"] = torch.zeros_like(w)
-    add(holder["buf"])
-    return holder["buf"] if first else None
+    buf = holder["buf"]
+    add(buf)
+    holder["seen"] += 1
+    if holder["seen"] >= holder["uses"]:
+        holder["buf"] = None
+        holder["seen"] = 0
+    return buf if first else None
 
 
 class _GruStep(torch.autograd.Function):
@@ -505,10 +513,15 @@ class _CorrPyramid(torch.autograd.Function):
         ctx.save_for_backward(f1, f2)
         ctx.num_levels = num_levels
         buf, _ = ops.corr_pyramid(f1, f2, num_levels)
+        ctx.holder = _dpyr_holder(buf)
         return buf
 
     @staticmethod
     def backward(ctx, dbuf):
+        # the lookups' shared gradient buffer is consumed: the next backward pass over this graph
+        # (retain_graph, torch.autograd.grad) starts from a fresh one
+        ctx.holder["buf"] = None
+        ctx.holder["seen"] = 0
         f1, f2 = ctx.saved_tensors
         n, c, h, w = f1.shape
         P = h * w
@@ -531,6 +544,20 @@ def corr_pyramid(f1: Tensor, f2: Tensor, num_levels: int = 4) -> Tensor:
     return _CorrPyramid.apply(f1, f2, num_levels)
 
 
+def _dpyr_holder(pyr: Tensor) -> dict:
+    """The lookups' shared pyramid-gradient accumulator, kept on the pyramid tensor: ``uses`` =
+    lookups recorded on it, ``seen`` = lookup backwards run in the current backward pass; the
+    buffer is released when a pass has seen every use or when the pyramid's backward consumes it."""
+    holder = getattr(pyr, "_scflow_dpyr", None)
+    if holder is None:
+        holder = {"buf": None, "uses": 0, "seen": 0}
+        try:
+            pyr._scflow_dpyr = holder
+        except (AttributeError, RuntimeError):
+            pass
+    return holder
+
+
 class _CorrLookup(torch.autograd.Function):
     """The pyramid is looked up once per refinement iteration; every iteration's backward
     scatters into ONE gradient buffer shared through the pyramid tensor (zeroed once per step):
@@ -542,14 +569,8 @@ class _CorrLookup(torch.autograd.Function):
     def forward(ctx, pyr, flow_nhwc, n, h, w, num_levels, radius):
         flow_nhwc = flow_nhwc.contiguous()
         ctx.save_for_backward(flow_nhwc)
-        holder = getattr(pyr, "_scflow_dpyr", None)
-        if holder is None:
-            holder = {"buf": None}
-            try:
-                pyr._scflow_dpyr = holder
-            except (AttributeError, RuntimeError):
-                pass
-        ctx.holder = holder
+        holder = ctx.holder = _dpyr_holder(pyr)
+        holder["uses"] += 1
         ctx.dims = (n, h, w, num_levels, radius, pyr.numel())
         out = torch.empty(n * h * w, num_levels * (2 * radius + 1) ** 2, device=pyr.device)
         ops.corr_lookup(pyr, flow_nhwc, n, h, w, num_levels, radius, out=Chan.whole(out),
@@ -560,11 +581,16 @@ class _CorrLookup(torch.autograd.Function):
     def backward(ctx, dout):
         (flow,) = ctx.saved_tensors
         n, h, w, L, r, size = ctx.dims
-        first = ctx.holder["buf"] is None
+        hd = ctx.holder
+        first = hd["buf"] is None
         if first:
-            ctx.holder["buf"] = torch.zeros(size, device=dout.device)
-        dpyr = ctx.holder["buf"]
+            hd["buf"] = torch.zeros(size, device=dout.device)
+        dpyr = hd["buf"]
         ops.corr_lookup_backward(dout.contiguous().view(n * h * w, -1), flow, dpyr, n, h, w, L, r)
+        hd["seen"] += 1
+        if hd["seen"] >= hd["uses"]:  # every lookup of this pass added its share: release it
+            hd["buf"] = None
+            hd["seen"] = 0
         return (dpyr if first else None), None, None, None, None, None, None
 
 

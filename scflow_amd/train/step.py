@@ -20,11 +20,18 @@ from typing import Dict, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from .._lib import bump_weights_generation
 from .functions import capture_cache, direct_weight_grads
 from .model import refiner_train_forward
 
 Tensor = torch.Tensor
 _MT_BACKWARD = os.environ.get("SCFLOW_TRAIN_MT_BACKWARD", "1") == "1"  # A/B switch (tuning)
+
+
+def trainable_parameters(refiner) -> List[torch.nn.Parameter]:
+    """The refiner's parameters, each once (the shared render / real feature encoder appears
+    under both names) — what the gradient buckets and the optimizer hold."""
+    return list(dict.fromkeys(refiner.parameters()))
 
 
 class GradBuckets:
@@ -130,7 +137,7 @@ class TrainStep:
         self.diameters = list(diameters)
         self.max_norm = max_norm
         self.iters = iters
-        params = list(dict.fromkeys(refiner.parameters()))  # the shared encoder appears twice
+        params = trainable_parameters(refiner)
         self.grads = GradBuckets(params, bucket_bytes, group, overlap)
         self.opt = torch.optim.AdamW(self.grads.params, lr=lr, betas=betas, eps=eps,
                                      weight_decay=weight_decay, foreach=True, capturable=graph)
@@ -174,6 +181,9 @@ class TrainStep:
             if self._g is None:
                 self._capture(batch)
             else:
+                if set(batch) != set(self._static):  # a replay reads exactly the captured inputs
+                    raise ValueError(f"TrainStep(graph=True): batch keys {sorted(batch)} differ from "
+                                     f"the captured ones {sorted(self._static)}")
                 for k, v in batch.items():
                     self._static[k].copy_(v)
             self._g.replay()
@@ -188,6 +198,9 @@ class TrainStep:
                     self._gn = self.grads.clip_(self.max_norm)
                     self.opt.step()
             self._g_opt.replay()
+            # the replay wrote the parameters without moving their version counters: make every
+            # weight-derived cache (packed / flipped forms) re-derive before its next eager use
+            bump_weights_generation()
             out["grad_norm"] = self._gn.clone()
             return out
         out = self._fwd_bwd(batch)

@@ -540,6 +540,31 @@ def test_pose_head_hip_vs_oracle(ops, n, feat):
         close(r3, r_ref, 2e-5, 1e-5, "fused pose head rotation")
         close(t3, t_ref, 2e-5, 1e-5, "fused pose head translation")
         close(r3, r, 1e-5, 1e-6, "fused vs unfused pose head rotation")
+        head.tail_check(ctx)  # the sticky error word stayed clear too
+
+
+def test_pose_head_fused_tail_give_up_raises(ops, monkeypatch):
+    """A protocol stall in the persistent pose-head tail is reported, not silently wrong:
+    SCFLOW_PHT_DBG=2 makes every work item skip its completion signal, so the first dependency
+    wait gives up after its 50 ms bound (every later wait falls through) and sets the sticky error
+    word; forward_fused (and the decoder, once per forward) raise ScflowError."""
+    from scflow_amd import synthetic
+    from scflow_amd._lib import ScflowError
+    from scflow_amd.modules import MultiClassPoseHead
+    n, feat = 4, 32
+    head = MultiClassPoseHead(21, 224, "Basic", dict(type="GN", num_groups=32),
+                              dict(type="ReLU"), feat_size=(feat, feat), rotation_mode="ortho6d")
+    synthetic.fill_module_(head, seed=7)
+    head = head.cuda()
+    x = torch.relu(torch.randn(n * feat * feat, 224, device="cuda"))
+    label = torch.zeros(n, dtype=torch.long, device="cuda")
+    src = ops.Chan.whole(x)
+    head.forward_fused(src, None, n, feat, feat, label)  # clean run: no error
+    monkeypatch.setenv("SCFLOW_PHT_DBG", "2")
+    with pytest.raises(ScflowError, match="gave up"):
+        head.forward_fused(src, None, n, feat, feat, label)
+    monkeypatch.delenv("SCFLOW_PHT_DBG")
+    head.forward_fused(src, None, n, feat, feat, label)  # a fresh context starts clean again
 
 
 def test_corr_lookup_far_out_of_bounds(ops):

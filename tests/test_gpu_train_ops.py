@@ -211,6 +211,43 @@ def test_corr_lookup_backward(radius, flow_kind):
     _close(pyr.grad, ref, 1e-5, 1e-5, "lookup backward")
 
 
+def test_shared_gradient_buffers_across_backward_passes():
+    """The lookups' shared pyramid-gradient buffer and the GRU's shared weight-gradient buffers
+    are released after each backward pass: a second pass over the same graph (retain_graph, and
+    torch.autograd.grad) yields the same gradients, not None and not an accumulation into the
+    first pass's buffer."""
+    from scflow_amd import ops
+    from scflow_amd.train.functions import corr_lookup, corr_pyramid, gru_step
+    g = torch.Generator().manual_seed(41)
+    n, c, h, w = 2, 16, 16, 16
+    f1 = torch.randn(n, c, h, w, generator=g).cuda().requires_grad_()
+    f2 = torch.randn(n, c, h, w, generator=g).cuda()
+    pyr = corr_pyramid(f1, f2, 4)
+    fl = [((torch.rand(n, h, w, 2, generator=g) - 0.5) * 8).cuda() for _ in range(3)]
+    loss = sum((corr_lookup(pyr, f, n, h, w, 4, 4) * (i + 1)).sum() for i, f in enumerate(fl))
+    loss.backward(retain_graph=True)
+    g1 = f1.grad.clone()
+    f1.grad = None
+    loss.backward(retain_graph=True)
+    torch.testing.assert_close(f1.grad, g1, rtol=1e-6, atol=1e-6)
+    (g3,) = torch.autograd.grad(loss, f1)
+    torch.testing.assert_close(g3, g1, rtol=1e-6, atol=1e-6)
+    # GRU weights used by two steps (like the 8 refinement iterations)
+    hh = torch.tanh(torch.randn(1, 32, 32, 128, generator=g)).cuda()
+    x = torch.randn(1, 32, 32, 128, generator=g).cuda()
+    wzr = (torch.randn(256, 256, 1, 5, generator=g) * 0.02).cuda().requires_grad_()
+    wq = (torch.randn(128, 256, 1, 5, generator=g) * 0.02).cuda().requires_grad_()
+    pzr = torch.zeros(1, 32, 32, 256).cuda()
+    pq = torch.zeros(1, 32, 32, 128).cuda()
+    y = gru_step(gru_step(hh, x, wzr, wq, pzr, pq, (0, 2)), x, wzr, wq, pzr, pq, (0, 2))
+    out = (y * y).sum()
+    a = torch.autograd.grad(out, [wzr, wq], retain_graph=True)
+    b = torch.autograd.grad(out, [wzr, wq])
+    for u, v in zip(a, b):
+        assert u is not None and v is not None
+        torch.testing.assert_close(u, v, rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("bt,M,N,K,ta,tb", [
     (1, 16, 1024, 2048, False, True),     # pose head FC forward: x · Wᵀ
     (1, 1024, 2048, 16, True, False),     # FC weight grad: dYᵀ · x

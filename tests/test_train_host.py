@@ -101,15 +101,15 @@ def train_batch(B, S, seed, labels=None, dtype=torch.float32, device="cpu"):
     return out, list(pts), list(synthetic.YCBV_DIAMETERS)
 
 
-def oracle_loss_and_grads(batch, points, diameters, iters, names):
-    """fp64 CPU autograd of the oracle's SCFlowRefiner.loss restatement; grads keyed by the
-    product module's parameter names."""
-    sd = {k: v.double().requires_grad_(v.is_floating_point()) for k, v in refiner_state_dict().items()}
-    b = {k: (v.double() if v.is_floating_point() else v).cpu() for k, v in batch.items()}
+def oracle_loss_and_grads(batch, points, diameters, iters, names, dtype=torch.float64):
+    """CPU autograd (fp64 by default) of the oracle's SCFlowRefiner.loss restatement; grads keyed
+    by the product module's parameter names."""
+    sd = {k: v.to(dtype).requires_grad_(v.is_floating_point()) for k, v in refiner_state_dict().items()}
+    b = {k: (v.to(dtype) if v.is_floating_point() else v).cpu() for k, v in batch.items()}
     loss, lp, lf, lm, outs, gt_flow = orc.refine_train_forward(
         sd, b["render_images"], b["real_images"], b["ref_rotation"], b["ref_translation"],
         b["gt_rotation"], b["gt_translation"], b["depth"], b["internel_k"], b["label"],
-        [p.double().cpu() for p in points], diameters, gt_masks=b["gt_masks"], iters=iters)
+        [p.to(dtype).cpu() for p in points], diameters, gt_masks=b["gt_masks"], iters=iters)
     loss.backward()
     grads = {}
     for n in names:
