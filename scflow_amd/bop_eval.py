@@ -16,10 +16,12 @@ metric (metrics/add.py) around the numeric core in ``metrics.py``.
 
 Inputs are plain dicts / arrays (the reference's ``results`` entries: ``img_metas.img_path``,
 ``pred.labels / rotations / translations``); model points are passed in (the reference samples
-1000 mesh vertices at random per class with trimesh, add.py:157 — trimesh and the meshes are
-absent here, so the caller supplies the points).  Parity: against a numpy restatement of the
-reference's logic on synthetic BOP trees (tests/test_bop_eval.py) — no reference fixture exists
-for this path (parity unpinned).
+1000 mesh vertices at random per class with trimesh — once in match_results, add.py:190, and
+again in compute_metrics, add.py:157 — trimesh and the meshes are absent here, so the caller
+supplies both point sets).  Parity: pinned by ``tests/golden/golden_metric_add.npz``, generated
+from the reference's own ``ADD`` class (constructed with its real ``__init__`` on a synthetic BOP
+tree, ``make_golden.py metric``) — compute_metrics end to end, match_results, eval_pose_error,
+parse_error_to_metric and the scene_gt.json text (tests/test_metric_golden.py).
 """
 from __future__ import annotations
 
@@ -169,11 +171,20 @@ def to_flat_dict(metric_dict: Dict[str, List[float]], headers: Sequence[str]) ->
 def evaluate(results: Sequence[dict], gt_annots: Dict[str, dict], points: Sequence[np.ndarray],
              class_names: Sequence[str], symmetric: Sequence[int], diameters: Sequence[float],
              metrics: Optional[Dict[str, Sequence[float]]] = None,
-             inverse_label_mapping: Optional[Dict[int, int]] = None) -> Dict[str, float]:
-    """compute_metrics (add.py:134-180) → the flat '{class}/{metric}' dictionary."""
+             inverse_label_mapping: Optional[Dict[int, int]] = None,
+             match_points: Optional[Sequence[np.ndarray]] = None,
+             round_digits: Optional[int] = 4) -> Dict[str, float]:
+    """compute_metrics (add.py:134-180) → the flat '{class}/{metric}' dictionary.
+
+    ``points``: the model points the errors are measured on (add.py:157); ``match_points``: those
+    the duplicate-prediction matching uses (add.py:190; default ``points`` — the reference draws
+    the two sets separately).  ``round_digits``: the reference's print_metric rounds every value
+    to 4 decimals in place before parse_metric_to_tensorboard (add.py:334-339), so its returned
+    dictionary holds rounded values; None keeps full precision."""
     metrics = metrics if metrics is not None else {"auc": [], "add": [0.05, 0.10, 0.20, 0.50]}
-    gR, gT, pR, pT, labels, valid, K = match_results(results, gt_annots, points, symmetric, diameters,
-                                                     inverse_label_mapping)
+    gR, gT, pR, pT, labels, valid, K = match_results(
+        results, gt_annots, points if match_points is None else match_points, symmetric, diameters,
+        inverse_label_mapping)
     add = np.ones(labels.shape, np.float32)
     rep = np.full(labels.shape, 50.0, np.float32)
     if valid.any():
@@ -182,14 +193,36 @@ def evaluate(results: Sequence[dict], gt_annots: Dict[str, dict], points: Sequen
         add[valid] = a
         rep[valid] = r
     md, headers = parse_error_to_metric({"add": add, "rep": rep}, labels, metrics, class_names)
+    if round_digits is not None:
+        md = {k: [round(x, round_digits) for x in v] for k, v in md.items()}
     return to_flat_dict(md, headers)
+
+
+def dumps_json(data, indent: int = 2, depth: int = 2) -> str:
+    """JSON text as the reference's BOP dumps write it (datasets/utils.py:39-67): indented
+    ``indent`` spaces per level, except that every container whose children would sit deeper
+    than ``depth`` levels is written compactly on its opening line — for scene_gt.json, one line
+    per predicted object."""
+    def enc(v, level):
+        if isinstance(v, (dict, list)) and v:
+            if level >= depth:
+                return json.dumps(v)
+            pad = " " * (indent * (level + 1))
+            end = "\n" + " " * (indent * level)
+            if isinstance(v, dict):
+                body = ",\n".join(f"{pad}{json.dumps(k)}: {enc(x, level + 1)}" for k, x in v.items())
+                return "{\n" + body + end + "}"
+            body = ",\n".join(pad + enc(x, level + 1) for x in v)
+            return "[\n" + body + end + "]"
+        return json.dumps(v)
+    return enc(data, 0)
 
 
 def format_results(results: Sequence[dict], data_root: str, save_dir: str,
                    inverse_label_mapping: Optional[Dict[int, int]] = None,
                    time: Optional[float] = None) -> List[str]:
-    """Predictions written as BOP ``scene_gt.json`` per sequence under save_dir (add.py:402-446);
-    returns the written paths."""
+    """Predictions written as BOP ``scene_gt.json`` per sequence under save_dir (add.py:402-446,
+    the reference's dumps_json layout); returns the written paths."""
     inv = inverse_label_mapping or {}
     per_seq: Dict[str, Dict[str, list]] = {}
     for res in results:
@@ -215,6 +248,6 @@ def format_results(results: Sequence[dict], data_root: str, save_dir: str,
         os.makedirs(seq_dir, exist_ok=True)
         path = os.path.join(seq_dir, "scene_gt.json")
         with open(path, "w") as f:
-            json.dump(content, f)
+            f.write(dumps_json(content))
         paths.append(path)
     return paths

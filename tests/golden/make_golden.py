@@ -3,6 +3,8 @@
 Run in the development container only (needs ``/root/reference``; never on the GPU box):
 
     python tests/golden/make_golden.py            # writes tests/golden/*.npz
+    python tests/golden/make_golden.py train      # only the training-step fixtures
+    python tests/golden/make_golden.py metric     # only golden_metric_add.npz (metrics/add.py ADD)
 
 The reference (GiaKhangLuu/SCFlow) is pure Python/PyTorch; its hot-path modules import
 mmcv / mmengine / kornia / cv2 / turtle / a registry, none of which are installed here
@@ -445,6 +447,139 @@ def gen_train(ref, out, labels, B=2, S=256, iters=2, seed=5):
     out["meta"] = np.array([B, S, iters, seed, *labels])
 
 
+# ------------------------------------------------------------------ §8(f)-4: the ADD metric
+def load_metric(ref, mesh_verts):
+    """The reference's ``metrics/add.py`` (class ``ADD``) with test-only stand-ins for its absent
+    imports: ``mmengine.evaluator.BaseMetric`` (keeps ``results``), ``mmengine.load`` (json),
+    ``mmengine.logging.print_log`` and ``terminaltables.AsciiTable`` (printing only),
+    ``trimesh.load`` (the synthetic vertices of the class whose ``obj_XXXXXX.ply`` it is asked
+    for), ``datasets.Compose``, and cv2 / matplotlib / mmcv for ``datasets/utils.py``'s imports.
+    ``datasets/pose.py`` (project_3d_point) and ``datasets/utils.py`` (dumps_json) are the
+    reference's own."""
+    import json as _json
+
+    class _BaseMetric:
+        def __init__(self, collect_device="cpu", prefix=None):
+            self.results = []
+
+    def _mm_load(path):
+        with open(path) as f:
+            return _json.load(f)
+
+    def _trimesh_load(path):
+        c = int(os.path.basename(path)[4:10]) - 1
+        return types.SimpleNamespace(vertices=np.asarray(mesh_verts[c]))
+    mm = sys.modules.get("mmengine") or _stub("mmengine")
+    mm.load = _mm_load
+    _stub("mmengine.evaluator", BaseMetric=_BaseMetric)
+    _stub("mmengine.logging", print_log=lambda *a, **k: None)
+    _stub("terminaltables", AsciiTable=lambda data: types.SimpleNamespace(table=""))
+    _stub("trimesh", load=_trimesh_load)
+    _stub("cv2")
+    _stub("matplotlib")
+    _stub("matplotlib.pyplot")
+    _stub("mmcv", is_str=lambda x: isinstance(x, str))
+    ds = _pkg("datasets", os.path.join(REF, "datasets"))
+    ds.Compose = None
+    _load("datasets.utils", "datasets/utils.py")
+    _load("datasets.pose", "datasets/pose.py")
+    reg = sys.modules.get("registry") or _stub("registry")
+    reg.METRICS = _Registry()
+    _pkg("metrics", os.path.join(REF, "metrics"))
+    return _load("metrics.add", "metrics/add.py")
+
+
+def gen_metric(out, seed=11):
+    """§8(f)-4 fixture from the reference's own ``ADD`` (metrics/add.py), constructed with its real
+    ``__init__`` on a synthetic BOP tree (gt = ref annotations root): ``compute_metrics`` end to
+    end (match_results → eval_pose_error → parse_error_to_metric → print_metric's 4-decimal
+    rounding → parse_metric_to_tensorboard) under a fixed numpy seed, with the vertex subsamples
+    its two ``np.random.choice`` rounds draw (match_results :190, compute_metrics :157) recorded
+    as indices; ``match_results`` alone; ``eval_pose_error`` on a direct batch (symmetric classes
+    included); ``parse_error_to_metric`` for several metric configurations; and the
+    ``format_results`` scene_gt.json text."""
+    import copy
+    import json as _json
+    import tempfile
+    root = tempfile.mkdtemp(prefix="scflow_bop_")
+    from tests.helpers import _rot_np, make_bop_case
+    results, verts, lines = make_bop_case(root, seed)
+    add_mod = load_metric(None, verts)
+    names = tuple(f"obj_{c + 1:02d}" for c in range(verts.shape[0]))
+    diam = list(synthetic.YCBV_DIAMETERS)
+    data = os.path.join(root, "data")
+    metric = add_mod.ADD(data_root=data, image_list=os.path.join(root, "test.txt"),
+                         keypoints_json=os.path.join(root, "bbox.json"), class_names=names,
+                         ref_annots_root=data, keypoints_num=8, mesh_symmetry=YCBV_SYMMETRY,
+                         meshes_eval=os.path.join(root, "models_eval"), mesh_diameter=diam,
+                         metrics={"auc": [], "add": [0.05, 0.10, 0.20, 0.50], "rep": [2, 5, 10]})
+    n_cls = verts.shape[0]
+
+    def draws(s, rounds):
+        np.random.seed(s)
+        return np.stack([np.stack([np.random.choice(verts.shape[1], 1000) for _ in range(n_cls)])
+                         for _ in range(rounds)])
+    # compute_metrics end to end
+    out["cm_seed"] = np.array(1234)
+    out["cm_draws"] = draws(1234, 2).astype(np.int16)  # [round (match, eval), class, 1000]
+    np.random.seed(1234)
+    flat = metric.compute_metrics(copy.deepcopy(results))
+    out["cm_flat"] = np.array(_json.dumps(flat))
+    # match_results alone
+    out["mr_draws"] = draws(99, 1).astype(np.int16)
+    np.random.seed(99)
+    mr = metric.match_results(copy.deepcopy(results))
+    for k, v in zip(("gt_R", "gt_t", "pred_R", "pred_t", "labels", "valid", "K"), mr):
+        out["mr_" + k] = v
+    # eval_pose_error on a direct batch (every class, symmetric ones included)
+    rng = np.random.default_rng(seed + 1)
+    n = 48
+    labels = np.arange(n) % n_cls
+    gR = np.stack([_rot_np(rng) for _ in range(n)])
+    gT = np.stack([[rng.normal() * 50, rng.normal() * 50, 700 + 300 * rng.random()] for _ in range(n)]
+                  ).astype(np.float32)
+    pR = np.stack([gR[i] if i % 3 else _rot_np(rng) for i in range(n)])
+    pT = (gT + rng.normal(size=gT.shape) * 10).astype(np.float32)
+    K = np.repeat(np.array([[572.4, 0, 325.3], [0, 573.6, 242.0], [0, 0, 1]], np.float32)[None], n, 0)
+    vsub = verts[:, :1000]
+    e3n, e2, e3 = metric.eval_pose_error(list(vsub), gt_t=gT, gt_r=gR, pred_t=pT, pred_r=pR,
+                                         labels=labels, k=K, symmetry_types=YCBV_SYMMETRY,
+                                         mesh_diameters=np.array(diam))
+    for k, v in (("gR", gR), ("gT", gT), ("pR", pR), ("pT", pT), ("labels", labels), ("K", K),
+                 ("add", e3n), ("rep", e2), ("add_mm", e3)):
+        out["ep_" + k] = v
+    # parse_error_to_metric: thresholds on add / rep, a threshold-free metric, a skipped one,
+    # classes absent from the labels
+    lab = np.array([0, 0, 3, 3, 3, 12, 12, 15, 20, 20, 20, 20])
+    err = dict(add=np.linspace(0.01, 0.6, lab.size), rep=np.linspace(0.5, 12.0, lab.size)[::-1].copy())
+    pcs = []
+    for m in ({"auc": [], "add": [0.05, 0.10, 0.20, 0.50]}, {"add": [0.1], "rep": [2, 5, 10]},
+              {"rep": []}, {"add": [0.05, 0.5], "x": [1]}):
+        md, headers = metric.parse_error_to_metric(err, lab, m, classnames=names)
+        pcs.append(dict(metrics=m, metric_dict=md, headers=headers))
+    out["pe_labels"] = lab
+    out["pe_add"] = err["add"]
+    out["pe_rep"] = err["rep"]
+    out["pe_cases"] = np.array(_json.dumps(pcs))
+    # format_results: the BOP scene_gt.json dump (reference formatting, datasets/utils.py dumps_json)
+    save = os.path.join(root, "dump")
+    metric.format_results(copy.deepcopy(results), save)
+    texts = {}
+    for seq in sorted(os.listdir(save)):
+        with open(os.path.join(save, seq, "scene_gt.json")) as f:
+            texts[seq] = f.read()
+    out["fr_texts"] = np.array(_json.dumps(texts))
+    # the inputs the tests rebuild the tree from
+    out["in_seed"] = np.array(seed)
+    out["in_verts_sum"] = np.array(float(verts.astype(np.float64).sum()))
+    out["in_results"] = np.array(_json.dumps([
+        dict(img_path=os.path.relpath(r["img_metas"]["img_path"], data),
+             labels=r["pred"]["labels"].tolist(), rotations=r["pred"]["rotations"].tolist(),
+             translations=r["pred"]["translations"].tolist()) for r in results]))
+    with open(os.path.join(data, "000048", "scene_gt.json")) as f:
+        out["in_scene_gt_48"] = np.array(f.read())
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = load_reference()
@@ -452,6 +587,12 @@ def main():
         ops = {}
         gen_ops(ref, ops)
         np.savez_compressed(os.path.join(HERE, "golden_ops.npz"), **ops)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "metric":  # only the ADD-metric fixture
+        mt = {}
+        gen_metric(mt)
+        np.savez_compressed(os.path.join(HERE, "golden_metric_add.npz"), **mt)
+        print({k: getattr(v, "shape", None) for k, v in mt.items()})
         return
     if len(sys.argv) > 1 and sys.argv[1] == "train":  # only the training fixtures
         for tag, labels in (("", (4, 9)), ("_sym", (15, 20))):

@@ -1,8 +1,8 @@
 """BOP-format ADD evaluation (scflow_amd/bop_eval.py) on a synthetic BOP tree: annotation loading,
 prediction↔GT matching (single / duplicate / missing predictions), ADD(-S) class-wise precision
 and the flat metric dict, against a numpy restatement of the reference's metrics/add.py logic
-written independently here (parity unpinned: no reference fixture exists for this path); plus
-the scene_gt.json dump round trip."""
+written independently here; plus the scene_gt.json dump round trip.  (The reference's own ADD
+metric pins the same functions in tests/test_metric_golden.py.)"""
 import json
 import os
 
@@ -82,7 +82,7 @@ def test_load_match_evaluate(bop_tree):
     root, results, gt, points, diam, sym, names = bop_tree
     ann = bop_eval.load_bop_annotations(str(root / "data"), ["000048", "000051"])
     assert ann["000048"]["pose"] == gt["000048"]["pose"]
-    flat = bop_eval.evaluate(results, ann, points, names, sym, diam)
+    flat = bop_eval.evaluate(results, ann, points, names, sym, diam, round_digits=None)
     # the reference's flow restated: matching (min normalised ADD among duplicates), fill values
     # for missing predictions, ADD(-S) precision per class at 5/10/20/50 % of the diameter
     add_all, labels = [], []

@@ -53,16 +53,16 @@ def test_train_forward_backward_matches_oracle():
         assert sub[worst] <= tol, f"{worst}: relative gradient error {sub[worst]:.3e}"
 
 
+@pytest.mark.timeout(600)
 def test_train_forward_backward_configs3_shard():
     """BASELINE configs[3]'s per-GPU shard — B = 16 pairs, 256², 8 refinement iterations
     (scflow_refiner.py:182-256; the bench's training leg) — HIP forward + backward against CPU
-    fp32 autograd of the oracle on the same batch (mixed labels: the pose head takes label[0]'s
+    fp64 autograd of the oracle on the same batch (mixed labels: the pose head takes label[0]'s
     class for the shard, pose_head.py:208-209).  Losses rtol 1e-4; every one of the 149
     parameters' gradients: norm within 1e-3 of the decoder's largest norm (+1e-3 relative) /
     2e-2 of the encoders' (the tolerances of the reference-fixture test below) and relative L2
-    error (floored at 1e-4·‖G‖) ≤ 2e-3 for the decoder, ≤ 3e-2 for the encoders — both sides are
-    fp32 here, so the CPU side's own error (6e-3 on the encoders vs fp64, test docstring above)
-    adds to the HIP side's."""
+    error (floored at 1e-4·‖G‖) ≤ 1e-3 for the decoder, ≤ 1e-2 for the encoders (the B = 2
+    test's bounds)."""
     from scflow_amd.train.model import refiner_train_forward
     iters, B = 8, 16
     torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -74,14 +74,20 @@ def test_train_forward_backward_configs3_shard():
     res["loss"].backward()
     torch.cuda.synchronize()
     names = [n for n, _ in r.named_parameters()]
-    (loss, lp, lf, lm), outs, gt_flow, grads = oracle_loss_and_grads(batch, points, diam, iters, names,
-                                                                      dtype=torch.float32)
-    assert float(orc.cal_epe_mean(gt_flow.float(), res["gt_flow"].cpu()).max()) <= 1e-3
+    (loss, lp, lf, lm), outs, gt_flow, grads = oracle_loss_and_grads(batch, points, diam, iters, names)
+    # GT flow: a pixel whose projection lands within rounding of the GT mask's edge may flip
+    # between valid and invalid (400) in fp32 vs fp64 — at most 1e-4 of the pixels; the flow on
+    # the pixels valid in both within 1e-3 px
+    got = res["gt_flow"].cpu().double()
+    va, vb = (got < 400).all(1), (gt_flow < 400).all(1)
+    assert int((va != vb).sum()) <= 1e-4 * va.numel(), int((va != vb).sum())
+    both = (va & vb)[:, None].expand_as(got)
+    assert float((got - gt_flow)[both].abs().max()) <= 1e-3
     for a, b in ((res["loss"], loss), (res["loss_pose"], lp), (res["loss_flow"], lf),
                  (res["loss_mask"], lm)):
         np.testing.assert_allclose(a.item(), b.item(), rtol=1e-4)
     for i in range(iters):  # per-iteration poses of all 16 pairs
-        torch.testing.assert_close(res["outs"][2][i].detach().cpu(), outs[2][i].detach().float(),
+        torch.testing.assert_close(res["outs"][2][i].detach().cpu().double(), outs[2][i].detach(),
                                    rtol=0, atol=1e-4)
     G = sum(float(g.double().norm()) ** 2 for g in grads.values() if g is not None) ** 0.5
     ref_n = {n: float(g.double().norm()) for n, g in grads.items() if g is not None}
@@ -106,7 +112,7 @@ def test_train_forward_backward_configs3_shard():
         with open(out, "w") as f:
             json.dump(dict(sorted(errs.items(), key=lambda kv: -kv[1])), f, indent=1)
     assert len(names) == 149 and checked >= 140, (len(names), checked)
-    for part, tol in (("decoder.", 2e-3), ("", 3e-2)):
+    for part, tol in (("decoder.", 1e-3), ("", 1e-2)):
         sub = {k: v for k, v in errs.items() if k.startswith(part)}
         worst = max(sub, key=sub.get)
         assert sub[worst] <= tol, f"{worst}: relative gradient error {sub[worst]:.3e}"
