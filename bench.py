@@ -13,17 +13,22 @@ SURVEY.md §8(e)); ``value`` = all pairs·iterations of all ranks ÷ the slowest
 
 Extra JSON fields:
 * ``roofline``: the kernel with the most GPU time in the step, ``conv_wino_kernel`` — the
-  F(2×2,3×3) Winograd convolution on fp32 MFMA — on its two largest launch shapes, the XHead
-  hidden convs (128→512, both heads in one launch, 64-channel workgroups) and corr_net.1
-  (256→192, 96-channel workgroups), once per iteration each.  Both launches are bracketed live with HIP events inside the timed region (one of each
-  per step).  ``achieved``/``frac`` count the FLOPs the matrix cores EXECUTE (Winograd: 16
-  transform points per 2×2 tile, 2.25× fewer multiplies than a direct conv), so ``frac`` ≤ 1 is
-  a true roofline fraction; ``direct_conv_flops_per_launch`` / ``direct_equiv_tflops`` give the
-  direct-conv count for comparison.  ``traffic`` = memory-side bytes per launch from the
-  rocprofv3 FETCH_SIZE / WRITE_SIZE passes in ``profiles/traffic_*.json``.
-* ``rooflines_secondary``: the SepConvGRU z|r conv (F(4,5) Winograd, same FLOP basis), the
-  pyramid lookup (HBM/gather), the persistent pose-head + pose-step tail ``ph_tail_kernel``
-  (or, unfused, ``pose_step_kernel``) and the correlation pyramid — the same events in a short untimed pass after the timed region.
+  F(2×2,3×3) Winograd convolution on fp32 MFMA — over ALL six of its launches per refinement
+  iteration (XHead hidden 128→512, corr_net.1 256→192, out_net 256→126, flow_net.1 and
+  delta_flow_encoder.1 128→64, mask_encoder.1 64→32), every one bracketed live with HIP events
+  inside the timed region (each on one launch every other step).  ``achieved`` = Σ executed
+  FLOPs of one launch of each shape ÷ Σ their mean durations; ``achieved``/``frac`` count the
+  FLOPs the matrix cores EXECUTE (Winograd: 16 transform points per 2×2 tile, 2.25× fewer
+  multiplies than a direct conv), so ``frac`` ≤ 1 is a true roofline fraction;
+  ``direct_conv_flops_per_launch`` / ``direct_equiv_tflops`` give the direct-conv count for
+  comparison.  ``traffic`` = memory-side bytes per launch from the rocprofv3 FETCH_SIZE /
+  WRITE_SIZE passes in ``profiles/traffic_*.json``.
+* ``rooflines_secondary``: the same kernel split into its two large launches (<32,2>, <32,3>)
+  and its four 32-channel-workgroup launches (<32,1>); the SepConvGRU z|r conv (F(4,5)
+  Winograd, same FLOP basis), the pyramid lookup (HBM/gather), the pose step and the
+  correlation pyramid — the last four from the same events in a short untimed pass after the
+  timed region.  HBM entries give ``frac`` against the 8 TB/s spec and ``frac_of_measured``
+  against the STREAM ceiling measured on the box (tools/micro/stream.hip).
 * ``cpu_baseline``: the CPU oracle (oracle/scflow_oracle.py, a parity-pinned PyTorch-CPU
   restatement of the reference decoder) on the same B=16 × 8-iteration workload, rank 0 at N=1.
 
@@ -118,6 +123,11 @@ def time_steps(step, steps, warmup, world, dev):
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
+# measured on the box: tools/micro/stream.hip, 16-B/lane copy over 2 GiB buffers (8× the Infinity
+# Cache), best of 20 — profiles/r03_stream.txt.  HBM entries report frac against both.
+HBM_MEASURED_GBS = 6290.0
+# every conv_wino_kernel launch of one refinement iteration (decoder.kernel_hooks names)
+WINO_LAUNCHES = ("heads", "corr_net1", "out_net", "flow_net1", "dflow1", "mask_enc1")
 
 
 def load_traffic(path):
@@ -197,12 +207,16 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
         ms = t.mean_ms()
         if bound == "hbm":
             ach, peak, unit = amount / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+            extra = {"peak_measured": HBM_MEASURED_GBS,
+                     "frac_of_measured": round(ach / HBM_MEASURED_GBS, 4)}
         else:
             ach, peak, unit = amount / (ms * 1e-3) / 1e12, FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
         e = {"kernel": kernel, "bound": bound, "achieved": round(ach, 2), "peak": peak,
              "unit": unit, "frac": round(ach / peak, 4), "avg_launch_ms": round(ms, 4),
              "launches": t.count(),
              ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): amount}
+        if bound == "hbm":
+            e.update(extra)
         if bound == "hbm":
             tr = traffic.get(tkey)
             e["traffic"] = tr
@@ -352,8 +366,13 @@ def main():
     per_step = {"heads": args.iters, "corr_net1": args.iters, "gru_zr": 2 * args.iters,
                 "corr_lookup": args.iters, "pose_flow": args.iters, "pose_tail": args.iters,
                 "corr_pyramid": 1}
-    live = ("heads", "corr_net1")  # the headline kernel's launches: bracketed in the timed region
-    timers = {name: (KernelTimer() if args.graph else EventTimer(stride=n + 1 if n > 1 else 1))
+    per_step.update({n: args.iters for n in WINO_LAUNCHES[2:]})
+    # the headline kernel's launches (every conv_wino_kernel launch of an iteration): bracketed in
+    # the timed region, each timer on one launch every other step (an event pair costs a few µs
+    # of queue time), the bracketed position walking through the iterations
+    live = WINO_LAUNCHES
+    timers = {name: (KernelTimer() if args.graph else
+                     EventTimer(stride=(2 * n + 1) if name in live else (n + 1 if n > 1 else 1)))
               for name, n in per_step.items()}
     for t in timers.values():
         t.enabled = False
@@ -447,19 +466,34 @@ def main():
     alg = {k: v.get("algorithmic_bytes_per_launch") for k, v in (tj or {}).get("kernels", {}).items()}
 
     heads_r = dec._hidden_heads()
-    c1 = dec.encoder.corr_net[-1].conv
-    corr1_r = ConvRunner.of(c1, dec.encoder.corr_net[-1].act_type)
+
+    def runner(m):
+        return ConvRunner.of(m.conv, m.act_type), m.conv.in_channels
+    wino = {"heads": (heads_r, hc), "corr_net1": runner(dec.encoder.corr_net[-1]),
+            "out_net": runner(dec.encoder.out_net[-1]), "flow_net1": runner(dec.encoder.flow_net[-1]),
+            "dflow1": runner(dec.delta_flow_encoder[-1]), "mask_enc1": runner(dec.mask_encoder[-1])}
+    parts = [(n, wino[n][0], wino[n][1], 0) for n in WINO_LAUNCHES if timers[n].count()]
     headline = conv_roofline(
-        "conv_wino_kernel (F(2x2,3x3) Winograd on fp32 MFMA): XHead hidden convs 128->512 "
-        "(<32,2>: 64-channel workgroups) + corr_net.1 256->192 (<32,3>: 96-channel workgroups, one "
-        "per CU)",
-        [("heads", heads_r, hc, 0), ("corr_net1", corr1_r, c1.in_channels, 0)], timers, m_px,
-        traffic.get("conv_wino_kernel", traffic.get("conv_wino_kernel<32,2>")),
-        alg.get("conv_wino_kernel", alg.get("conv_wino_kernel<32,2>")))
-    if not (heads_r.winograd and corr1_r.winograd):
-        headline["kernel"] = "direct conv_mfma_kernel (Winograd off): XHead hidden + corr_net.1"
+        "conv_wino_kernel (F(2x2,3x3) Winograd on fp32 MFMA), ALL its launches of an iteration: "
+        "XHead hidden 128->512 <32,2>, corr_net.1 256->192 <32,3>, out_net 256->126, flow_net.1 "
+        "128->64, delta_flow_encoder.1 128->64, mask_encoder.1 64->32 (<32,1>)",
+        parts, timers, m_px, traffic.get("conv_wino_kernel_all"), alg.get("conv_wino_kernel_all"))
+    if not all(r.winograd for _, r, _, _ in parts):
+        headline["kernel"] += " [some launches on the direct conv_mfma_kernel: Winograd off]"
 
     secondary = []
+    big = [p for p in parts if p[0] in ("heads", "corr_net1")]
+    small = [p for p in parts if p[0] not in ("heads", "corr_net1")]
+    if big:
+        secondary.append(conv_roofline(
+            "conv_wino_kernel<32,2> + <32,3>: XHead hidden 128->512 + corr_net.1 256->192",
+            big, timers, m_px, traffic.get("conv_wino_kernel"), alg.get("conv_wino_kernel")))
+    if small:
+        secondary.append(conv_roofline(
+            "conv_wino_kernel<32,1>: out_net 256->126, flow_net.1 / delta_flow_encoder.1 128->64, "
+            "mask_encoder.1 64->32",
+            small, timers, m_px, traffic.get("conv_wino_kernel<32,1>"),
+            alg.get("conv_wino_kernel<32,1>")))
     if timers["gru_zr"].count():
         cxt = xc if dec.hoist_context else 0
         zr = dec.gru.zr_runner(cxt)

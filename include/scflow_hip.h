@@ -255,6 +255,51 @@ int scflow_ph_gn_reduce(const float* parts, int nsplit, long long split_stride, 
                         int hw, int c, int groups, const float* gamma, const float* beta, float eps,
                         float* scale, float* shift, void* stream);
 int scflow_ph_fc_permute(const float* W, float* Wp, int n, int c, int hw, void* stream);
+/* Fused-statistics pose head (pose_head.py:201-211): every conv writes its RAW output and its
+ * GroupNorm partial statistics per output tile, and the consumer (the next conv, or FC1)
+ * turns its producer's partials into the GroupNorm affine in its own prologue — no separate
+ * GroupNorm launch, no K-split slabs.
+ * scflow_ph_gn_tpi(oh, ow): partials per image of a path-0 conv output of oh×ow pixels (oh·ow a
+ *   multiple of 32: one per 32-pixel tile; oh·ow = 16: one per image); SCFLOW_EUNSUPPORTED
+ *   otherwise.  (Path 1 writes two per output tile; the plan gives tpi for either.)
+ * scflow_ph_conv_gn: like scflow_ph_conv (no bias) with the input GroupNorm(in_groups) + ReLU built
+ *   from in_stats [n][in_tpi][in_groups][2] (fp64 sum, sum of squares over h·w pixels; NULL: raw
+ *   input) and this conv's partials into out_stats [n][plan.tpi][out_groups][2] (NULL: none;
+ *   cout % 32 == 0, (cout / out_groups) | 32).  Statistics are summed in fp64 in a fixed order:
+ *   deterministic.
+ * scflow_ph_fc_split_gn: scflow_ph_fc_split in GN mode (x = a conv's raw channels-last output,
+ *   gn_c channels, W permuted by scflow_ph_fc_permute) with the GroupNorm affine built from that
+ *   conv's partials (stats [m][tpi][groups][2] over hw pixels; m·gn_c ≤ 4096). */
+typedef struct scflow_ph_conv_gn_args {
+  const float* src0; int c0, s0;
+  const float* src1; int c1, s1;
+  const double* in_stats; int in_tpi, in_groups;
+  const float* in_gamma; const float* in_beta; float in_eps;
+  const float* weight;      /* packed for the plan's path: scflow_enc_conv_pack (path 1) or
+                               scflow_ph_conv_pack (path 0) */
+  float* out;
+  double* out_stats; int out_groups;
+  int n, h, w, cout, kh, kw, stride, pad;
+  int ksplit;               /* the plan's K split; > 1 needs parts and counters: */
+  float* parts;             /* [ksplit][n·oh·ow][cout] partial slabs */
+  int* counters;            /* plan.counters ints, zero before the first launch (every launch
+                               leaves them zero: the last-arriving workgroup of an output tile
+                               sums the slabs in slab order — deterministic — and resets it) */
+} scflow_ph_conv_gn_args;
+/* How scflow_ph_conv_gn runs a shape: path 1 = the halo-staged MFMA conv (scflow_enc_conv's
+ * kernel; 3×3, pad 1, stride 1/2, channels % 16, cout % 64), path 0 = the gather MFMA conv
+ * (scflow_ph_conv's); the K split that fills the GPU; out_stats partials per image (tpi); the
+ * counter and slab sizes the caller allocates. */
+typedef struct scflow_ph_conv_gn_plan {
+  int path, ksplit, tpi, counters;
+  long long parts_floats;
+} scflow_ph_conv_gn_plan;
+int scflow_ph_gn_tpi(int oh, int ow);
+int scflow_ph_conv_gn_plan_for(const scflow_ph_conv_gn_args* args, scflow_ph_conv_gn_plan* plan);
+int scflow_ph_conv_gn(const scflow_ph_conv_gn_args* args, void* stream);
+int scflow_ph_fc_split_gn(const float* x, int m, int k, const float* W, float* parts, int n,
+                          int ksplit, int gn_c, const double* stats, int tpi, int groups, int hw,
+                          const float* gamma, const float* beta, float eps, void* stream);
 int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias, float* y,
                  int n, int relu, int gn_c, const float* scale, const float* shift, void* stream);
 /* scflow_ph_fc with K split over ksplit workgroup slices (m ≤ 32): parts [ksplit][m][n] = partial

@@ -104,6 +104,27 @@ class PhTailArgs(ctypes.Structure):
     ]
 
 
+class PhConvGnArgs(ctypes.Structure):
+    """Mirror of ``scflow_ph_conv_gn_args`` (include/scflow_hip.h)."""
+    _fields_ = [
+        ("src0", c_vp), ("c0", c_int), ("s0", c_int),
+        ("src1", c_vp), ("c1", c_int), ("s1", c_int),
+        ("in_stats", c_vp), ("in_tpi", c_int), ("in_groups", c_int),
+        ("in_gamma", c_vp), ("in_beta", c_vp), ("in_eps", c_float),
+        ("weight", c_vp), ("out", c_vp),
+        ("out_stats", c_vp), ("out_groups", c_int),
+        ("n", c_int), ("h", c_int), ("w", c_int), ("cout", c_int), ("kh", c_int), ("kw", c_int),
+        ("stride", c_int), ("pad", c_int),
+        ("ksplit", c_int), ("parts", c_vp), ("counters", c_vp),
+    ]
+
+
+class PhConvGnPlan(ctypes.Structure):
+    """Mirror of ``scflow_ph_conv_gn_plan`` (include/scflow_hip.h)."""
+    _fields_ = [("path", c_int), ("ksplit", c_int), ("tpi", c_int), ("counters", c_int),
+                ("parts_floats", c_ll)]
+
+
 class RenderArgs(ctypes.Structure):
     """Mirror of ``scflow_render_args`` (include/scflow_hip.h)."""
     _fields_ = [
@@ -184,6 +205,11 @@ SIGNATURES = {
     "scflow_ph_gn_reduce": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                     c_float, c_vp, c_vp, c_vp]),
     "scflow_ph_fc_permute": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_ph_gn_tpi": (c_int, [c_int, c_int]),
+    "scflow_ph_conv_gn": (c_int, [ctypes.POINTER(PhConvGnArgs), c_vp]),
+    "scflow_ph_conv_gn_plan_for": (c_int, [ctypes.POINTER(PhConvGnArgs), ctypes.POINTER(PhConvGnPlan)]),
+    "scflow_ph_fc_split_gn": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int,
+                                      c_int, c_int, c_vp, c_vp, c_float, c_vp]),
     "scflow_ph_fc": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                              c_vp, c_vp]),
     "scflow_ph_heads": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp,

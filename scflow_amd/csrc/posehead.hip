@@ -28,6 +28,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace {
 
 constexpr int PH_K = 16;  // K chunk per MFMA group
@@ -42,9 +44,28 @@ struct PhConvArgs {
   float* out;           // [n][oh][ow][cout], or [ksplit][n][oh][ow][cout] partial slabs
   int n, h, w, oh, ow, cout, kh, kw, stride, pad, cinp;
   int ksplit;           // K chunks split over grid.z (partial slab z = out + z·M·cout)
+  // scflow_ph_conv_gn: the input's GroupNorm (+ ReLU) from its producer's per-tile partial
+  // statistics (in_stats [n][in_tpi][in_groups][2] fp64 sum / sum of squares over in_hw pixels),
+  // made into a per-workgroup affine table in LDS; this conv's own per-tile statistics into
+  // out_stats [n][ph_gn_tpi(oh·ow)][out_groups][2].  All zero / NULL otherwise.
+  const double* in_stats; int in_tpi, in_groups; const float* in_gamma; const float* in_beta;
+  float in_eps;
+  double* out_stats; int out_groups;
+  float* parts; int* counters;  // scflow_ph_conv_gn K split: slabs + per-tile arrival counters
 };
 
-__device__ __forceinline__ floatx4 ph_load_a(const PhConvArgs& a, int img, int iy, int ix, int c) {
+// partial statistics per image of a conv output with P = oh·ow pixels per image and 32-pixel
+// tiles: one per tile when P % 32 == 0, one per image when a tile holds 32 / P whole images
+// (P ∈ {16, 32}: at most two images per tile); 0 = unsupported
+__host__ __device__ __forceinline__ int ph_gn_tpi(int P) {
+  return P % 32 == 0 ? P / 32 : (P == 16 ? 1 : 0);
+}
+
+// input element quad (channels c..c+3 of pixel (iy, ix) of image img), the input GroupNorm +
+// ReLU applied from the affine table sc/sh (row (img − img_base), ld floats per row; NULL: raw)
+__device__ __forceinline__ floatx4 ph_load_a(const PhConvArgs& a, int img, int iy, int ix, int c,
+                                             const float* sc_t, const float* sh_t, int img_base,
+                                             int ld) {
   floatx4 v = {0.f, 0.f, 0.f, 0.f};
   if (iy < 0 || iy >= a.h || ix < 0 || ix >= a.w) return v;
   const size_t pix = (size_t)(img * a.h + iy) * a.w + ix;
@@ -52,9 +73,9 @@ __device__ __forceinline__ floatx4 ph_load_a(const PhConvArgs& a, int img, int i
   if (c >= cin) return v;
   v = c < a.c0 ? *(const floatx4*)(a.src0 + pix * a.s0 + c)
                : *(const floatx4*)(a.src1 + pix * a.s1 + (c - a.c0));
-  if (a.scale) {
-    const floatx4 sc = *(const floatx4*)(a.scale + (size_t)img * cin + c);
-    const floatx4 sh = *(const floatx4*)(a.shift + (size_t)img * cin + c);
+  if (sc_t) {
+    const floatx4 sc = *(const floatx4*)(sc_t + (size_t)(img - img_base) * ld + c);
+    const floatx4 sh = *(const floatx4*)(sh_t + (size_t)(img - img_base) * ld + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
   }
@@ -74,7 +95,8 @@ constexpr int PH_BATCH = SCFLOW_PH_BATCH;  // K chunks whose loads a wave issues
 // red: (NW/2)·32·33 floats of LDS
 template <int NW>
 __device__ __forceinline__ void ph_conv_body(const PhConvArgs& a, int bx, int by, int bz,
-                                             float* red) {
+                                             float* red, const float* sc_t, const float* sh_t,
+                                             int img_base, int ld) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 31, hh = lane >> 5;
   const int M = a.n * a.oh * a.ow;
@@ -108,8 +130,8 @@ __device__ __forceinline__ void ph_conv_body(const PhConvArgs& a, int bx, int by
         const int ty = tap / a.kw, tx = tap % a.kw;
         const int iy = oy * a.stride - a.pad + ty, ix = ox * a.stride - a.pad + tx;
         if (mvalid) {
-          A0[c] = ph_load_a(a, img, iy, ix, c0 + 4 * hh);
-          A1[c] = ph_load_a(a, img, iy, ix, c0 + 8 + 4 * hh);
+          A0[c] = ph_load_a(a, img, iy, ix, c0 + 4 * hh, sc_t, sh_t, img_base, ld);
+          A1[c] = ph_load_a(a, img, iy, ix, c0 + 8 + 4 * hh, sc_t, sh_t, img_base, ld);
         }
         if (nvalid) {
           const float* wp = a.weight + ((size_t)col * taps + tap) * a.cinp + c0 + 4 * hh;
@@ -139,20 +161,122 @@ __device__ __forceinline__ void ph_conv_body(const PhConvArgs& a, int bx, int by
     }
     __syncthreads();
   }
+  if (a.counters && a.ksplit > 1) {
+    // K-split fixup (scflow_ph_conv_gn): slab bz, then the tile's last-arriving workgroup sums
+    // the slabs in slab order (its own from registers) and carries on with the full tile
+    __shared__ int s_last;
+    if (wave == 0 && nvalid) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (mm < M) a.parts[((size_t)bz * M + mm) * a.cout + col] = acc[r];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int tile = by * gridDim.x + bx;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const int old = __hip_atomic_fetch_add(a.counters + tile, 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == a.ksplit - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (wave == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        float v = 0.f;
+        if (mm < M && nvalid)
+          for (int zz = 0; zz < a.ksplit; ++zz)
+            v += zz == bz ? acc[r] : a.parts[((size_t)zz * M + mm) * a.cout + col];
+        acc[r] = v;
+      }
+      if (threadIdx.x == 0)
+        __hip_atomic_store(a.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (wave == 0 && nvalid) {
     const float b = a.bias ? a.bias[col] : 0.f;
-    float* out = a.out + (size_t)bz * M * a.cout;
+    float* out = a.out + (a.counters ? 0 : (size_t)bz * M * a.cout);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
       if (mm < M) out[(size_t)mm * a.cout + col] = acc[r] + b;
     }
   }
+  if (a.out_stats && wave == 0) {
+    // this tile's GroupNorm partials: per lane (channel col, half hh) fp64 sums over its 16 rows
+    // by image slot (rows of a second image when a tile holds two), then over hh (lane ^ 32) and
+    // the group's channels (cpg adjacent lanes, cpg | 32), fixed order
+    const int P = a.oh * a.ow;
+    const int img0 = m0 / P;
+    double s[2] = {0, 0}, q[2] = {0, 0};
+    const float b = (nvalid && a.bias) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (mm < M && nvalid) {
+        const double v = (double)(acc[r] + b);
+        if (mm / P == img0) { s[0] += v; q[0] += v * v; } else { s[1] += v; q[1] += v * v; }
+      }
+    }
+    const int cpg = a.cout / a.out_groups;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      s[k] += __shfl_xor(s[k], 32);
+      q[k] += __shfl_xor(q[k], 32);
+      for (int d = 1; d < cpg; d <<= 1) {
+        s[k] += __shfl_xor(s[k], d);
+        q[k] += __shfl_xor(q[k], d);
+      }
+    }
+    if (hh == 0 && nvalid && col % cpg == 0) {
+      const int tpi = ph_gn_tpi(P), g = col / cpg;
+      const int t = P >= 32 ? (m0 % P) / 32 : 0;
+      const int nimg = P >= 32 ? 1 : 2;
+      for (int k = 0; k < nimg; ++k) {
+        const int im = img0 + k;
+        if (im >= a.n) break;
+        double* o = a.out_stats + (((size_t)im * tpi + t) * a.out_groups + g) * 2;
+        o[0] = s[k];
+        o[1] = q[k];
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
   __shared__ float red[PH_WAVES / 2 * 32 * 33];
-  ph_conv_body<PH_WAVES>(a, blockIdx.x, blockIdx.y, blockIdx.z, red);
+  ph_conv_body<PH_WAVES>(a, blockIdx.x, blockIdx.y, blockIdx.z, red, a.scale, a.shift, 0,
+                         a.c0 + a.c1);
+}
+
+// scflow_ph_conv_gn: the input GroupNorm affine of the (at most two) images this workgroup's
+// output tile reads, from the producer's partial statistics, in LDS; then ph_conv_body
+constexpr int PH_GN_MAXC = 256;
+__global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_gn_kernel(PhConvArgs a) {
+  __shared__ float red[PH_WAVES / 2 * 32 * 33];
+  __shared__ float tsc[2 * PH_GN_MAXC], tsh[2 * PH_GN_MAXC];
+  const int cin = a.c0 + a.c1;
+  const int P = a.oh * a.ow;
+  const int img_lo = (blockIdx.x * 32) / P;
+  if (a.in_stats) {
+    for (int i = threadIdx.x; i < 2 * cin; i += blockDim.x) {
+      const int im = img_lo + i / cin, c = i % cin;
+      float sc = 0.f, sh = 0.f;
+      if (im < a.n)
+        ph_gn_affine(a.in_stats, a.in_tpi, a.in_groups, c, cin, im, a.h * a.w, a.in_gamma,
+                     a.in_beta, a.in_eps, sc, sh);
+      tsc[i] = sc;
+      tsh[i] = sh;
+    }
+    __syncthreads();
+  }
+  ph_conv_body<PH_WAVES>(a, blockIdx.x, blockIdx.y, blockIdx.z, red, a.in_stats ? tsc : nullptr,
+                         a.in_stats ? tsh : nullptr, img_lo, cin);
 }
 
 // GroupNorm statistics of x [n][hw][c] → per-channel scale/shift for y = relu(x·scale + shift),
@@ -270,11 +394,16 @@ struct FcArgs {
   int ksplit;                            // >1: grid.y splits K, y + z·m·n gets partial sums
   int xsplit; long long xstride;         // >0: X = relu(Σ_z x[z·xstride] + xbias) (split producer)
   const float* xbias;
+  // GN mode from the producer's partial statistics (scflow_ph_fc_split_gn): the per-(row,
+  // channel) affine is built in LDS from gst [m][gst_tpi][gst_groups][2] over gst_hw pixels
+  const double* gst; int gst_tpi, gst_groups, gst_hw; const float* gamma; const float* beta;
+  float eps;
 };
 
 // one 16-neuron tile bx of K slice by; NW waves; red: (NW/2)·FC_RT·64·5 floats of LDS
 template <int NW, int FC_RT>  // row tiles of 16 per pass
-__device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, float* red) {
+__device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, float* red,
+                                           const float* sc_t, const float* sh_t) {
   constexpr int FB = FC_RT == 1 ? PH_BATCH : 2;  // K groups whose loads are issued together
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, kq = lane >> 4;
@@ -320,8 +449,8 @@ __device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, floa
             }
             if (f.gn_c > 0) {
               const int ch = kk % f.gn_c;
-              const floatx4 sc = *(const floatx4*)(f.scale + (size_t)row * f.gn_c + ch);
-              const floatx4 sh = *(const floatx4*)(f.shift + (size_t)row * f.gn_c + ch);
+              const floatx4 sc = *(const floatx4*)(sc_t + (size_t)row * f.gn_c + ch);
+              const floatx4 sh = *(const floatx4*)(sh_t + (size_t)row * f.gn_c + ch);
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
             }
@@ -386,7 +515,24 @@ __device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, floa
 template <int FC_RT>
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
   __shared__ float red[PH_WAVES / 2 * FC_RT * 64 * 5];
-  ph_fc_body<PH_WAVES, FC_RT>(f, blockIdx.x, blockIdx.y, red);
+  ph_fc_body<PH_WAVES, FC_RT>(f, blockIdx.x, blockIdx.y, red, f.scale, f.shift);
+}
+
+// FC with the input GroupNorm built from partial statistics: the [m][gn_c] affine in LDS first
+constexpr int PH_FCGN_MAX = 32 * 128;
+template <int FC_RT>
+__global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_gn_kernel(FcArgs f) {
+  __shared__ float red[PH_WAVES / 2 * FC_RT * 64 * 5];
+  __shared__ float tsc[PH_FCGN_MAX], tsh[PH_FCGN_MAX];
+  for (int i = threadIdx.x; i < f.m * f.gn_c; i += blockDim.x) {
+    float sc, sh;
+    ph_gn_affine(f.gst, f.gst_tpi, f.gst_groups, i % f.gn_c, f.gn_c, i / f.gn_c, f.gst_hw, f.gamma,
+                 f.beta, f.eps, sc, sh);
+    tsc[i] = sc;
+    tsh[i] = sh;
+  }
+  __syncthreads();
+  ph_fc_body<PH_WAVES, FC_RT>(f, blockIdx.x, blockIdx.y, red, tsc, tsh);
 }
 
 // W [n][c·hw] with columns in NCHW-flatten order (c·hw + p) → Wp [n][hw·c] channels-last order
@@ -685,11 +831,12 @@ __global__ __launch_bounds__(PHT_WAVES * 64) void ph_tail_kernel(PhTail A) {
       } else if (ph == PHT_CONV2 || ph == PHT_CONV3) {
         const PhConvArgs cv = pht_kcopy(&K->conv[ph == PHT_CONV2 ? 0 : 1]);
         const int nt = (cv.cout + 31) / 32;
-        ph_conv_body<PHT_WAVES>(cv, i / (cv.ksplit * nt), (i / cv.ksplit) % nt, i % cv.ksplit, smem);
+        ph_conv_body<PHT_WAVES>(cv, i / (cv.ksplit * nt), (i / cv.ksplit) % nt, i % cv.ksplit, smem,
+                                cv.scale, cv.shift, 0, cv.c0 + cv.c1);
       } else if (ph == PHT_FC1 || ph == PHT_FC2 || ph == PHT_HEADS) {
         const FcArgs f = pht_kcopy(ph == PHT_FC1 ? &K->fc1 : ph == PHT_FC2 ? &K->fc2 : &K->heads);
         const int split = ph == PHT_FC1 ? K->fc1_split : ph == PHT_FC2 ? K->fc2_split : 1;
-        ph_fc_body<PHT_WAVES, RT>(f, i / split, i % split, smem);
+        ph_fc_body<PHT_WAVES, RT>(f, i / split, i % split, smem, f.scale, f.shift);
       } else {
         const PoseStepArgs ps = pht_kcopy(&K->ps);
         const int nb = ps.bf + ps.bl;
@@ -750,7 +897,7 @@ SCFLOW_API int scflow_ph_conv_split(const float* src0, int c0, int s0, const flo
   if ((c0 & 3) || (c1 & 3) || (s0 & 3) || (c1 && (s1 & 3)) || !aligned16(src0) ||
       (c1 && !aligned16(src1)) || !aligned16(packed))
     return SCFLOW_EALIGN;
-  PhConvArgs a;
+  PhConvArgs a{};
   a.src0 = src0; a.c0 = c0; a.s0 = s0;
   a.src1 = src1; a.c1 = c1; a.s1 = s1;
   a.scale = scale; a.shift = shift;
@@ -765,6 +912,128 @@ SCFLOW_API int scflow_ph_conv_split(const float* src0, int c0, int s0, const flo
   const long long M = (long long)n * a.oh * a.ow;
   dim3 grid((unsigned)((M + 31) / 32), (unsigned)((cout + 31) / 32), (unsigned)ksplit);
   ph_conv_kernel<<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_gn_tpi(int oh, int ow) {
+  if (oh <= 0 || ow <= 0) return SCFLOW_EINVAL;
+  const int t = ph_gn_tpi(oh * ow);
+  return t > 0 ? t : SCFLOW_EUNSUPPORTED;
+}
+
+SCFLOW_API int scflow_ph_conv_gn_plan_for(const scflow_ph_conv_gn_args* p,
+                                          scflow_ph_conv_gn_plan* plan) {
+  if (!p || !plan || p->n <= 0 || p->h <= 0 || p->w <= 0 || p->cout <= 0 || p->c0 <= 0 ||
+      p->c1 < 0 || p->kh <= 0 || p->kw <= 0 || p->stride <= 0 || p->pad < 0)
+    return SCFLOW_EINVAL;
+  const int oh = (p->h + 2 * p->pad - p->kh) / p->stride + 1;
+  const int ow = (p->w + 2 * p->pad - p->kw) / p->stride + 1;
+  if (oh <= 0 || ow <= 0) return SCFLOW_EINVAL;
+  const long long M = (long long)p->n * oh * ow;
+  const int cin = p->c0 + p->c1;
+  *plan = scflow_ph_conv_gn_plan{};
+  // path 1: the halo-staged MFMA conv (tiles of whole output rows of one image)
+  const int tm = p->stride == 1 ? 128 : 64;
+  const int tc = ow < tm ? ow : tm;
+  if (p->kh == 3 && p->kw == 3 && p->pad == 1 && (p->stride == 1 || p->stride == 2) &&
+      p->c0 % 16 == 0 && p->c1 % 16 == 0 && p->cout % 64 == 0 && tc >= 8 && tm % tc == 0 &&
+      ow % tc == 0 && oh % (tm / tc) == 0 && cin <= PH_GN_MAXC) {
+    const int tpi_tiles = (oh / (tm / tc)) * (ow / tc);
+    const long long tiles = (long long)p->n * tpi_tiles * (p->cout / 64);
+    const int nst = cin / 16;
+    plan->path = 1;
+    plan->ksplit = (int)std::max(1LL, std::min((long long)nst, (512 + tiles - 1) / tiles));
+    plan->tpi = 2 * tpi_tiles;
+    plan->counters = (int)tiles;
+  } else {
+    const int tpi = ph_gn_tpi(oh * ow);
+    if (!tpi || oh * ow < 16) return SCFLOW_EUNSUPPORTED;
+    const long long tiles = ((M + 31) / 32) * ((p->cout + 31) / 32);
+    const int nall = p->kh * p->kw * ((cin + PH_K - 1) / PH_K);
+    plan->path = 0;
+    plan->ksplit = (int)std::max(1LL, std::min((long long)(nall / 16), (256 + tiles - 1) / tiles));
+    plan->tpi = tpi;
+    plan->counters = (int)tiles;
+  }
+  plan->parts_floats = plan->ksplit > 1 ? (long long)plan->ksplit * M * p->cout : 0;
+  if (plan->ksplit == 1) plan->counters = 0;
+  return SCFLOW_OK;
+}
+
+int scflow_enc_conv_gn_launch(const scflow_ph_conv_gn_args* g, int tm, void* stream);
+
+SCFLOW_API int scflow_ph_conv_gn(const scflow_ph_conv_gn_args* p, void* stream) {
+  if (!p || !p->src0 || !p->weight || !p->out || p->n <= 0 || p->h <= 0 || p->w <= 0 ||
+      p->cout <= 0 || p->c0 <= 0 || p->c1 < 0 || (p->c1 > 0 && !p->src1) || p->kh <= 0 ||
+      p->kw <= 0 || p->stride <= 0 || p->pad < 0 || p->ksplit < 1 ||
+      (p->ksplit > 1 && (!p->parts || !p->counters)))
+    return SCFLOW_EINVAL;
+  scflow_ph_conv_gn_plan plan;
+  const int pr = scflow_ph_conv_gn_plan_for(p, &plan);
+  if (pr != SCFLOW_OK) return pr;
+  if (p->ksplit != plan.ksplit) return SCFLOW_EINVAL;  // buffers were sized for the plan
+  if (p->in_stats && (!p->in_gamma || !p->in_beta || p->in_groups <= 0 ||
+                      (p->c0 + p->c1) % p->in_groups || p->in_tpi <= 0 || p->c0 + p->c1 > PH_GN_MAXC))
+    return SCFLOW_EINVAL;
+  if (p->out_stats && (p->out_groups <= 0 || p->cout % p->out_groups ||
+                       32 % (p->cout / p->out_groups) || p->cout % 32))
+    return SCFLOW_EUNSUPPORTED;
+  if (plan.path == 1) {
+    if (!aligned16(p->src0) || (p->s0 & 3) || !aligned16(p->weight) ||
+        (p->c1 > 0 && (!aligned16(p->src1) || (p->s1 & 3))))
+      return SCFLOW_EALIGN;
+    return scflow_enc_conv_gn_launch(p, p->stride == 1 ? 128 : 64, stream);
+  }
+  if ((p->c0 & 3) || (p->c1 & 3) || (p->s0 & 3) || (p->c1 && (p->s1 & 3)) || !aligned16(p->src0) ||
+      (p->c1 && !aligned16(p->src1)) || !aligned16(p->weight))
+    return SCFLOW_EALIGN;
+  PhConvArgs a{};
+  a.src0 = p->src0; a.c0 = p->c0; a.s0 = p->s0;
+  a.src1 = p->src1; a.c1 = p->c1; a.s1 = p->s1;
+  a.weight = p->weight; a.out = p->out;
+  a.n = p->n; a.h = p->h; a.w = p->w;
+  a.oh = (p->h + 2 * p->pad - p->kh) / p->stride + 1;
+  a.ow = (p->w + 2 * p->pad - p->kw) / p->stride + 1;
+  if (a.oh <= 0 || a.ow <= 0) return SCFLOW_EINVAL;
+  a.cout = p->cout; a.kh = p->kh; a.kw = p->kw; a.stride = p->stride; a.pad = p->pad;
+  a.cinp = (p->c0 + p->c1 + PH_K - 1) / PH_K * PH_K;
+  a.ksplit = p->ksplit;
+  if (p->ksplit > 1) {
+    a.parts = p->parts;
+    a.counters = p->counters;
+  }
+  if (p->in_stats) {
+    a.in_stats = p->in_stats; a.in_tpi = p->in_tpi; a.in_groups = p->in_groups;
+    a.in_gamma = p->in_gamma; a.in_beta = p->in_beta; a.in_eps = p->in_eps;
+  }
+  if (p->out_stats) {
+    a.out_stats = p->out_stats; a.out_groups = p->out_groups;
+  }
+  const long long M = (long long)p->n * a.oh * a.ow;
+  dim3 grid((unsigned)((M + 31) / 32), (unsigned)((p->cout + 31) / 32), (unsigned)p->ksplit);
+  ph_conv_gn_kernel<<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_fc_split_gn(const float* x, int m, int k, const float* W, float* parts,
+                                     int n, int ksplit, int gn_c, const double* stats, int tpi,
+                                     int groups, int hw, const float* gamma, const float* beta,
+                                     float eps, void* stream) {
+  if (!x || !W || !parts || !stats || !gamma || !beta || m <= 0 || m > 32 || k <= 0 || n <= 0 ||
+      (k & 15) || ksplit <= 0 || ksplit > k / 16 || gn_c <= 0 || (gn_c & 3) || k % gn_c ||
+      groups <= 0 || gn_c % groups || tpi <= 0 || hw <= 0 || m * gn_c > PH_FCGN_MAX ||
+      !aligned16(W) || !aligned16(x))
+    return SCFLOW_EINVAL;
+  FcArgs f{};
+  f.x = x; f.ldx = k; f.m = m; f.k = k; f.W = W; f.y = parts; f.n = n; f.gn_c = gn_c;
+  f.ksplit = ksplit;
+  f.gst = stats; f.gst_tpi = tpi; f.gst_groups = groups; f.gst_hw = hw; f.gamma = gamma;
+  f.beta = beta; f.eps = eps;
+  dim3 grid((unsigned)((n + 15) / 16), (unsigned)ksplit);
+  if (m <= 16)
+    ph_fc_gn_kernel<1><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  else
+    ph_fc_gn_kernel<2><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
   return scflow_launch_status();
 }
 

@@ -161,6 +161,14 @@ class SCFlowDecoder(nn.Module):
         if h is not None:
             h(start)
 
+    def _hooks_for(self, *names):
+        """Per-layer hooks for run_chain (None where no timer is installed); recorded with the
+        segment's launches, so replays bracket the same launches."""
+        if not self._hooks_on:
+            return None
+        hs = [self.kernel_hooks.get(n) if n else None for n in names]
+        return hs if any(hs) else None
+
     # ------------------------------------------------------------------ forward
     def forward(self, feat_render: Tensor, feat_real: Tensor, h_feat: Tensor, cxt_feat: Tensor,
                 ref_rotation: Tensor, ref_translation: Tensor, depth: Tensor, internel_k: Tensor,
@@ -438,7 +446,8 @@ class SCFlowDecoder(nn.Module):
         flow_in = F2 * mask_lr if self.mask_flow else F2
 
         def seg_flow_branch():
-            run_chain(self.encoder.flow_net, Chan.whole(flow_in), Chan(MF, cc, cf), N, h, w, s_flow)
+            run_chain(self.encoder.flow_net, Chan.whole(flow_in), Chan(MF, cc, cf), N, h, w, s_flow,
+                      hooks=self._hooks_for(None, "flow_net1"))
 
         def seg_lookup():
             ops.corr_lookup(pyr, F2, N, h, w, self.num_levels, self.radius, out=Chan.whole(CORR),
@@ -457,7 +466,8 @@ class SCFlowDecoder(nn.Module):
             ConvRunner.of(corr_net[-1].conv, corr_net[-1].act_type).run(src, Chan(MF, 0, cc), N, h, w)
 
         def seg_out():
-            run_chain(self.encoder.out_net, Chan.whole(MF), hx_motion, N, h, w, s_out)
+            run_chain(self.encoder.out_net, Chan.whole(MF), hx_motion, N, h, w, s_out,
+                      hooks=self._hooks_for("out_net"))
 
         def seg_heads():
             if head_runner is not None:
@@ -468,11 +478,13 @@ class SCFlowDecoder(nn.Module):
 
         def seg_mask_branch():
             mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MASK), N, h, w)
-            run_chain(self.mask_encoder, Chan.whole(MASK), Chan(FM, dfc, mfc), N, h, w, s_me)
+            run_chain(self.mask_encoder, Chan.whole(MASK), Chan(FM, dfc, mfc), N, h, w, s_me,
+                      hooks=self._hooks_for(None, "mask_enc1"))
 
         def seg_flow_pred():
             flow_pred_r.run(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w)
-            run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe)
+            run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe,
+                      hooks=self._hooks_for(None, "dflow1"))
 
         pose_x = []
         tail_calls = None  # fused tail: per-iteration (heads, pose_step) launches, built once

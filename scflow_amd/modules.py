@@ -327,10 +327,14 @@ def bind_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: in
 
 
 def run_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int, w: int,
-              scratch: Optional[List[Tensor]] = None) -> None:
-    """Run a Sequential of stride-1 ConvModules channels-last; the last one writes ``dst``."""
+              scratch: Optional[List[Tensor]] = None, hooks: Optional[Sequence] = None) -> None:
+    """Run a Sequential of stride-1 ConvModules channels-last; the last one writes ``dst``.
+    ``hooks[i]``: optional callable(start: bool) bracketing layer i's launch (kernel timers)."""
     cur = src
     for i, m in enumerate(layers):
+        hk = hooks[i] if hooks is not None and i < len(hooks) else None
+        if hk is not None:
+            ops.host_call(lambda hk=hk: hk(True))
         r = ConvRunner.of(m.conv, m.act_type)
         if i == len(layers) - 1:
             out = dst
@@ -339,6 +343,8 @@ def run_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int
                                                                       device=src.buf.device)
             out = Chan.whole(buf)
         r.run(cur, out, n, h, w)
+        if hk is not None:
+            ops.host_call(lambda hk=hk: hk(False))
         cur = out
 
 
@@ -655,6 +661,8 @@ class MultiClassPoseHead(nn.Module):
         else on the gather conv (conv3's 4×4 output)."""
         if any(m.norm_type != "GN" or m.act_type != "ReLU" for m in self.conv_layers):
             raise NotImplementedError("HIP pose head: conv + GroupNorm + ReLU layers only")
+        if self.fused_gn and self._gn_fused_ok(src0, src1, n, h, w):
+            return self._trunk_gn(src0, src1, n, h, w, ws)
         dev = src0.buf.device
         keep = ws if ws is not None else []
 
@@ -729,6 +737,114 @@ class MultiClassPoseHead(nn.Module):
                                 xsplit=xsplit, xbias=xbias)
             x, xsplit, xbias, ldx = y, ks, lin.bias.detach(), lin.out_features
         return x
+
+    #: the fused-statistics trunk (scflow_ph_conv_gn / scflow_ph_fc_split_gn: 5 launches + heads,
+    #: no GroupNorm launches, no K-split slabs) when the shapes allow it
+    fused_gn = True
+
+    def _gn_plans(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int):
+        """[(args, plan, oh, ow)] per conv layer for the fused-statistics trunk, or None."""
+        if not 1 <= n <= 32 or len(self.fc_layers) != 2:
+            return None
+        if any(fc[0].in_features % 64 for fc in self.fc_layers):
+            return None
+        c1 = 0 if src1 is None else src1.c
+        if src0.c % 4 or c1 % 4:
+            return None
+        out, hh, ww, s0, s1 = [], h, w, src0, src1
+        for m in self.conv_layers:
+            cv = m.conv
+            if cv.bias is not None or cv.kernel_size[0] != cv.kernel_size[1] or \
+                    cv.stride[0] != cv.stride[1] or cv.padding[0] != cv.padding[1]:
+                return None
+            k, st, p = cv.kernel_size[0], cv.stride[0], cv.padding[0]
+            oh, ow = (hh + 2 * p - k) // st + 1, (ww + 2 * p - k) // st + 1
+            g = m.gn.num_groups
+            if cv.out_channels % 32 or cv.out_channels % g or 32 % (cv.out_channels // g):
+                return None
+            a = ops.ph_conv_gn_args(s0, s1, n, hh, ww, cv.out_channels, k, st, p)
+            plan = ops.ph_conv_gn_plan(a)
+            if plan is None:
+                return None
+            out.append((a, plan, oh, ow))
+            # the next layer reads this one's raw output (same geometry checks, pointer unused)
+            s0, s1, hh, ww = Chan(src0.buf, 0, cv.out_channels), None, oh, ow
+        c_last = self.conv_layers[-1].conv.out_channels
+        if n * c_last > 4096 or self.fc_layers[0][0].in_features != c_last * hh * ww:
+            return None
+        return out
+
+    def _gn_fused_ok(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int) -> bool:
+        return self._gn_plans(src0, src1, n, h, w) is not None
+
+    def _gn_weight(self, i: int, path: int) -> Tensor:
+        """conv_layers[i]'s weights packed for plan path 1 (enc_conv) or 0 (ph_conv)."""
+        wt = self.conv_layers[i].conv.weight
+        packs = getattr(self, "_gn_packs", None)
+        if packs is None:
+            packs = self._gn_packs = {}
+        key = (wt.data_ptr(), wt._version, path, _lib.weights_generation())
+        if packs.get(i, (None,))[0] != key:
+            packs[i] = (key, ops.enc_conv_pack(wt) if path == 1 else ops.ph_conv_pack(wt))
+        return packs[i][1]
+
+    def _trunk_gn(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
+                  ws: Optional[list] = None) -> Tensor:
+        """trunk_hip with every GroupNorm fused (pose_head.py:201-211): each
+        conv (scflow_ph_conv_gn: the halo-staged MFMA conv or the gather conv, its K split
+        summed by the last-arriving workgroup of each tile) writes its raw output and fp64
+        GroupNorm partials; the next conv (or FC1) builds the affine from them in its
+        prologue.  Returns FC2's K-split partials."""
+        dev = src0.buf.device
+        keep = ws if ws is not None else []
+
+        def empty(*shape, dtype=torch.float32):
+            t = torch.empty(*shape, device=dev, dtype=dtype)
+            keep.append(t)
+            return t
+        plans = self._gn_plans(src0, src1, n, h, w)
+        ohl, owl = plans[-1][2], plans[-1][3]
+        c_last = self.conv_layers[-1].conv.out_channels
+        _, fc1_w = self._packs(c_last, ohl * owl)
+        cur0, cur1 = src0, src1
+        prev, prev_st = None, None
+        for i, (m, (a, plan, oh, ow)) in enumerate(zip(self.conv_layers, plans)):
+            cout = m.conv.out_channels
+            y = empty(n * oh * ow, cout)
+            st = empty(n, plan.tpi, m.gn.num_groups, 2, dtype=torch.float64)
+            a.src0, a.c0, a.s0 = cur0.ptr, cur0.c, cur0.stride
+            if cur1 is not None:
+                a.src1, a.c1, a.s1 = cur1.ptr, cur1.c, cur1.stride
+            else:
+                a.src1, a.c1, a.s1 = None, 0, 0
+            if prev is not None:
+                a.in_stats, a.in_tpi, a.in_groups = prev_st.data_ptr(), prev_st.shape[1], prev.gn.num_groups
+                g, b = prev.gn.weight.detach(), prev.gn.bias.detach()
+                keep += [g, b]
+                a.in_gamma, a.in_beta, a.in_eps = g.data_ptr(), b.data_ptr(), float(prev.gn.eps)
+            wpk = self._gn_weight(i, plan.path)
+            keep.append(wpk)
+            a.weight, a.out = wpk.data_ptr(), y.data_ptr()
+            a.out_stats, a.out_groups = st.data_ptr(), m.gn.num_groups
+            a.ksplit = plan.ksplit
+            if plan.ksplit > 1:
+                a.parts = empty(plan.parts_floats).data_ptr()
+                a.counters = empty(plan.counters, dtype=torch.int32).zero_().data_ptr()
+            ops.ph_conv_gn(a, y)
+            cur0, cur1, prev, prev_st = Chan.whole(y), None, m, st
+        c = cur0.c
+        k_in = c * ohl * owl
+        ks = 4
+        l1, l2 = self.fc_layers[0][0], self.fc_layers[1][0]
+        y1 = empty(ks, n, l1.out_features)
+        ops.ph_fc_split_gn(cur0.buf, n, k_in, fc1_w, y1, l1.out_features, ks, c, prev_st,
+                           prev.gn.num_groups, ohl * owl, prev.gn.weight.detach(),
+                           prev.gn.bias.detach(), prev.gn.eps)
+        y2 = empty(ks, n, l2.out_features)
+        ops.ph_fc_split(y1, l1.out_features, n, l1.out_features, l2.weight.detach(), y2,
+                        l2.out_features, ks, xsplit=ks, xbias=l1.bias.detach())
+        self._split_fc = True
+        return y2
 
     def heads_hip(self, x: Tensor, label: Tensor, drot: Tensor, dt: Tensor) -> None:
         """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt

@@ -71,6 +71,16 @@ class binding:
         _BINDING, _BINDING_RUN = self._prev, self._prev_run
 
 
+def host_call(fn) -> None:
+    """Run a host-side callable (a kernel-timer hook) in launch order: inside ``binding`` it is
+    recorded with the launches (and replayed with them), else it just runs."""
+    if _BINDING is not None:
+        _BINDING.append(fn)
+        if not _BINDING_RUN:
+            return
+    fn()
+
+
 def _launch(name: str, dev_tensor: Tensor, *args) -> None:
     fn = getattr(_lib.load(), name)
     if _BINDING is not None:
@@ -597,6 +607,50 @@ def ph_gn_reduce(parts: Tensor, nsplit: int, y: Tensor, n: int, hw: int, c: int,
     """y = sum of the nsplit partial slabs of ``parts`` [nsplit, n·hw, c]; GN scale/shift of y."""
     _launch("scflow_ph_gn_reduce", parts,_p(parts), nsplit, n * hw * c, _p(y), n, hw, c, groups,
                                           _p(gamma), _p(beta), float(eps), _p(scale), _p(shift))
+
+
+def ph_gn_tpi(oh: int, ow: int) -> int:
+    """GroupNorm partial statistics per image of an oh×ow conv output (scflow_ph_gn_tpi); 0 if
+    the fused-statistics pose head does not support the size."""
+    v = int(_lib.load().scflow_ph_gn_tpi(oh, ow))
+    return v if v > 0 else 0
+
+
+def ph_conv_gn_args(src0: Chan, src1: Optional[Chan], n: int, h: int, w: int, cout: int, k: int,
+                    stride: int, pad: int) -> "_lib.PhConvGnArgs":
+    """A ``scflow_ph_conv_gn_args`` with the geometry filled in (buffers are set by the caller
+    after ``ph_conv_gn_plan``)."""
+    a = _lib.PhConvGnArgs()
+    a.src0, a.c0, a.s0 = src0.ptr, src0.c, src0.stride
+    if src1 is not None:
+        a.src1, a.c1, a.s1 = src1.ptr, src1.c, src1.stride
+    a.n, a.h, a.w, a.cout, a.kh, a.kw, a.stride, a.pad = n, h, w, cout, k, k, stride, pad
+    a.ksplit = 1
+    return a
+
+
+def ph_conv_gn_plan(a: "_lib.PhConvGnArgs") -> Optional["_lib.PhConvGnPlan"]:
+    """scflow_ph_conv_gn_plan_for: path, K split, partials per image and buffer sizes (None if
+    the shape is unsupported)."""
+    plan = _lib.PhConvGnPlan()
+    rc = _lib.load().scflow_ph_conv_gn_plan_for(ctypes.byref(a), ctypes.byref(plan))
+    return plan if rc == 0 else None
+
+
+def ph_conv_gn(a: "_lib.PhConvGnArgs", dev_tensor: Tensor) -> None:
+    """scflow_ph_conv_gn (arguments from ``ph_conv_gn_args`` + the plan's buffers)."""
+    _require(dev_tensor, "device tensor", contiguous=False)
+    _launch("scflow_ph_conv_gn", dev_tensor, ctypes.byref(a))
+
+
+def ph_fc_split_gn(x: Tensor, m: int, k: int, W: Tensor, parts: Tensor, n: int, ksplit: int,
+                   gn_c: int, stats: Tensor, groups: int, hw: int, gamma: Tensor, beta: Tensor,
+                   eps: float) -> None:
+    """scflow_ph_fc_split_gn: K-split FC partials of relu(GN(x)) with the GroupNorm built from the
+    producing conv's partial statistics ``stats`` [m, tpi, groups, 2]."""
+    _require(stats, "stats", dtype=torch.float64)
+    _launch("scflow_ph_fc_split_gn", x, _p(x), m, k, _p(W), _p(parts), n, ksplit, gn_c, _p(stats),
+            stats.shape[1], groups, hw, _p(gamma), _p(beta), float(eps))
 
 
 def ph_fc_permute(W: Tensor, c: int, hw: int) -> Tensor:

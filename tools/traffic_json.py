@@ -27,7 +27,17 @@ def groups(B, S):
     zr = f * M * (256 + 256 + 128 + 256) + f * 256 * 256 * 5   # h|motion, bias map, h, z|rh, W
     lookup = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
     pose_step = B * 36 * S * S
+
+    def conv(cin, cout, taps=9):
+        return f * (M * cin + M * cout + cout * cin * taps)
+    small = [conv(256, 126), conv(128, 64), conv(128, 64), conv(64, 32)]  # the <32,1> launches
     return {
+        "conv_wino_kernel_all": (["conv_wino_kernel<"], (heads + corr1 + sum(small)) / 6,
+                                 "F(2x2,3x3) Winograd, every launch of an iteration (6 shapes, "
+                                 "launches averaged)"),
+        "conv_wino_kernel<32,1>": (["conv_wino_kernel<32, 1>"], sum(small) / 4,
+                                   "F(2x2,3x3) Winograd <32,1>: out_net 256→126, flow_net.1 / "
+                                   "delta_flow_encoder.1 128→64, mask_encoder.1 64→32"),
         "conv_wino_kernel": (["conv_wino_kernel<32, 2>", "conv_wino_kernel<32, 3>"], (heads + corr1) / 2,
                              "F(2x2,3x3) Winograd: XHead hidden 128→512 <32,2> + corr_net.1 256→192 "
                              "<32,3> (launches averaged)"),
