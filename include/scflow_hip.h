@@ -214,6 +214,10 @@ int scflow_stream_wait_event(void* stream, void* event);
 /* Timing events (device-scope release; destroy with scflow_sync_event_destroy, record with
  * scflow_sync_event_record); *ms = end − start after waiting for end. */
 int scflow_timing_event_create(void** event);
+/* Uncached (MTYPE UC), zero-filled device memory (every access goes to memory; no cache to
+ * write back or invalidate). */
+int scflow_alloc_uncached(long long bytes, void** ptr);
+int scflow_free_uncached(void* ptr);
 int scflow_event_elapsed_ms(void* start, void* end, float* ms);
 
 /* out[n·ons + b·obs + a] = in[n·ins + a·ias + b] for a < A, b < B (batched 2-D transpose; e.g.
@@ -300,6 +304,17 @@ int scflow_ph_conv_gn(const scflow_ph_conv_gn_args* args, void* stream);
 int scflow_ph_fc_split_gn(const float* x, int m, int k, const float* W, float* parts, int n,
                           int ksplit, int gn_c, const double* stats, int tpi, int groups, int hw,
                           const float* gamma, const float* beta, float eps, void* stream);
+/* scflow_ph_fc2_heads: FC2 on FC1's K-split partials (x = relu(Σ parts1 + b1), k = FC1's width)
+ *   into its own K-split partials parts2 [ksplit][m][n2], then — in the same launch, by the
+ *   last-arriving workgroup (counter: (1 + ceil(n2/16))·64 ints, zero before the first launch and
+ *   after every launch) —
+ *   x2 = relu(Σ parts2 + b2) and the label[0] class's heads → drot [m][rch], dt [m][3]
+ *   (scflow_ph_heads_sum's result up to summation order).  m ≤ 32, m·n2 ≤ 8192. */
+int scflow_ph_fc2_heads(const float* parts1, int xsplit, const float* b1, int m, int k,
+                        const float* W2, const float* b2, float* parts2, int n2, int ksplit,
+                        const float* Wr, const float* br, int rch, const float* Wt, const float* bt,
+                        const long long* label, int num_class, float* drot, float* dt,
+                        int* counter, void* stream);
 int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias, float* y,
                  int n, int relu, int gn_c, const float* scale, const float* shift, void* stream);
 /* scflow_ph_fc with K split over ksplit workgroup slices (m ≤ 32): parts [ksplit][m][n] = partial
@@ -321,6 +336,17 @@ int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* 
                     const float* Wt, const float* bt, const long long* label, int num_class,
                     float* drot, float* dt, void* stream);
 
+/* scflow_pose_step_part: scflow_pose_step restricted to parts (bit 0: the full-resolution outputs
+ *   — pose flow, ×8 flow prediction and mask; bit 1: the next iteration's ↓8 flow, lr_next /
+ *   hx_next).  Each part recomputes the pose update; the part with the lowest block writes
+ *   R_dst / t_dst.  The decoder runs bit 1 on its critical path and bit 0 on a side stream. */
+int scflow_pose_step_part(const float* drot6, const float* dt, const float* R_src,
+                          const float* t_src, const float* K, const float* points, float* R_dst,
+                          float* t_dst, float* flow, int n, int H, int W, float weight,
+                          int depth_transform, float invalid_num, const float* lr,
+                          const float* delta, const float* mask, float* flow_up, float* mask_up,
+                          float* lr_next, int s_next, float* hx_next, int s_hx, int h, int w,
+                          float up_scale, float down_scale, int parts, void* stream);
 /* scflow_pose_step's arguments as a struct (stream aside) — used by scflow_ph_tail. */
 typedef struct scflow_pose_step_args {
   const float* drot6; const float* dt; const float* R_src; const float* t_src; const float* K;

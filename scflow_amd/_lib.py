@@ -178,6 +178,9 @@ SIGNATURES = {
                                      c_float, c_vp]),
     "scflow_pose_step": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_float, c_int, c_float] +
                          [c_vp] * 6 + [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_vp]),
+    "scflow_pose_step_part": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_float, c_int, c_float] +
+                              [c_vp] * 6 + [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_int,
+                                            c_vp]),
     "scflow_ph_tail": (c_int, [ctypes.POINTER(PhTailArgs), c_vp]),
     "scflow_ph_tail_sync_ints": (c_int, [c_int]),
     "scflow_sync_event_create": (c_int, [ctypes.POINTER(c_vp)]),
@@ -185,6 +188,8 @@ SIGNATURES = {
     "scflow_sync_event_record": (c_int, [c_vp, c_vp]),
     "scflow_stream_wait_event": (c_int, [c_vp, c_vp]),
     "scflow_timing_event_create": (c_int, [ctypes.POINTER(c_vp)]),
+    "scflow_alloc_uncached": (c_int, [c_ll, ctypes.POINTER(c_vp)]),
+    "scflow_free_uncached": (c_int, [c_vp]),
     "scflow_event_elapsed_ms": (c_int, [c_vp, c_vp, ctypes.POINTER(c_float)]),
     "scflow_transpose": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_int, c_ll, c_int, c_vp]),
     "scflow_ph_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
@@ -207,6 +212,8 @@ SIGNATURES = {
     "scflow_ph_fc_permute": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_ph_gn_tpi": (c_int, [c_int, c_int]),
     "scflow_ph_conv_gn": (c_int, [ctypes.POINTER(PhConvGnArgs), c_vp]),
+    "scflow_ph_fc2_heads": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int,
+                                    c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "scflow_ph_conv_gn_plan_for": (c_int, [ctypes.POINTER(PhConvGnArgs), ctypes.POINTER(PhConvGnPlan)]),
     "scflow_ph_fc_split_gn": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int,
                                       c_int, c_int, c_vp, c_vp, c_float, c_vp]),

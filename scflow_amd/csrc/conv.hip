@@ -551,6 +551,87 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
   }
 }
 
+// thin conv, whole halo at once (the decoder's XHead predictors, 256 → 2 / 1, raft_decoder.py:
+// 256-294): one workgroup of 1024 threads per 64-pixel tile stages the tile's input halo for ALL
+// channels in LDS with a single round of coalesced 16-B loads (one memory latency, where the
+// chunked kernel above pays one per 32 channels), then each of the 16 waves contracts a 1/16
+// share of the channels for the 64 pixels (lane = pixel, weights as wave-uniform scalar loads)
+// and the 16 partials are summed in wave order through LDS: deterministic.
+constexpr int THINF_WAVES = 16;
+__host__ __device__ constexpr int thinf_ld(int cin) { return cin + 4; }  // pixel stride (floats)
+
+template <int COUT, int KH, int KW>
+__global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow_conv_args a,
+                                                                          int oh, int ow) {
+  extern __shared__ float halo[];  // [(tr+KH-1)·(ow+KW-1)][cin + 4], reused for the partials
+  const int tr = 64 / ow;
+  const int hcols = ow + KW - 1;
+  const int cin = a.c0;
+  const int ld = thinf_ld(cin);
+  const int q4 = cin / 4;
+  const int nh = (tr + KH - 1) * hcols * q4;  // float4 of the halo
+  const int tiles_per_img = oh / tr;
+  const int img = blockIdx.x / tiles_per_img;
+  const int oy0 = (blockIdx.x % tiles_per_img) * tr;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // every load first, then every LDS store (at most 9 float4 per thread at 4 × 34 × 256)
+  constexpr int NL = 12;
+  floatx4 v[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int idx = tid + THINF_WAVES * 64 * j;
+    v[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (idx < nh) {
+      const int q = idx % q4, pix = idx / q4;
+      const int hr = pix / hcols, hcol = pix % hcols;
+      const int iy = oy0 - a.ph + hr, ix = hcol - a.pw;
+      if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w)
+        v[j] = *(const floatx4*)(a.src0 + ((size_t)(img * a.h + iy) * a.w + ix) * a.s0 + 4 * q);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int idx = tid + THINF_WAVES * 64 * j;
+    if (idx < nh) *(floatx4*)(halo + (idx / q4) * ld + 4 * (idx % q4)) = v[j];
+  }
+  __syncthreads();
+  const int py = lane / ow, px = lane % ow;
+  const int cw = cin / THINF_WAVES;  // channels of this wave (a multiple of 4)
+  const int c0 = wave * cw;
+  float acc[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
+  // packed weights [o][tap][ci]: wave-uniform addresses → scalar loads
+  for (int ty = 0; ty < KH; ++ty)
+    for (int tx = 0; tx < KW; ++tx) {
+      const float* hp = halo + ((py + ty) * hcols + px + tx) * ld + c0;
+      const float* wp = a.weight + (size_t)(ty * KW + tx) * cin + c0;
+      for (int c = 0; c < cw; c += 4) {
+        const floatx4 x = *(const floatx4*)(hp + c);
+#pragma unroll
+        for (int o = 0; o < COUT; ++o) {
+          const float* w = wp + (size_t)o * KH * KW * cin + c;
+          acc[o] += x[0] * w[0] + x[1] * w[1] + x[2] * w[2] + x[3] * w[3];
+        }
+      }
+    }
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) halo[(wave * COUT + o) * 64 + lane] = acc[o];
+  __syncthreads();
+  if (wave == 0) {
+    const size_t pix = ((size_t)img * oh + oy0 + py) * ow + px;
+#pragma unroll
+    for (int o = 0; o < COUT; ++o) {
+      float r = 0.f;
+      for (int w = 0; w < THINF_WAVES; ++w) r += halo[(w * COUT + o) * 64 + lane];
+      const float b = a.bias ? a.bias[o] : 0.f;
+      a.out[pix * a.so + o] = act_apply(r + b, a.act);
+    }
+  }
+}
+
 // generic thin fallback: one wave per output pixel, lanes split the channels
 template <int COUT>
 __global__ __launch_bounds__(256) void conv_thin_generic(scflow_conv_args a, int oh, int ow) {
@@ -1060,6 +1141,20 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     return SCFLOW_EALIGN;
   const bool tiled = (g.ow == 32 || g.ow == 64) && (a.c0 % 8) == 0 && (a.c1 % 8) == 0 &&
                      g.oh % (64 / g.ow) == 0 && g.ow == a.w && g.oh == a.h;
+  // whole-halo variant: one source, channels a multiple of 64, the halo within 160 KB of LDS
+  static const bool thin_full_off = [] {
+    const char* e = getenv("SCFLOW_THIN_FULL");
+    return e && e[0] == '0';
+  }();
+  if (tiled && !thin_full_off && a.c1 == 0 && a.c0 % (4 * THINF_WAVES) == 0) {
+    const int tr = 64 / g.ow;
+    const unsigned blocks = (unsigned)(a.n * (g.oh / tr));
+#define SCFLOW_THINF(CO, KH_, KW_)                                                                if (a.cout == CO && a.kh == KH_ && a.kw == KW_) {                                                 const size_t nh4 = (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * (a.c0 / 4);                      size_t lds = sizeof(float) * (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * thinf_ld(a.c0);        if (lds < sizeof(float) * THINF_WAVES * CO * 64) lds = sizeof(float) * THINF_WAVES * CO * 64;     if (lds <= 160 * 1024 && nh4 <= (size_t)12 * THINF_WAVES * 64) {                                  static bool attr = false;                                                                       if (!attr) {                                                                                      (void)hipFuncSetAttribute((const void*)conv_thin_full_kernel<CO, KH_, KW_>,                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              attr = true;                                                                                  }                                                                                               conv_thin_full_kernel<CO, KH_, KW_><<<blocks, THINF_WAVES * 64, lds, st>>>(a, g.oh, g.ow);       return scflow_launch_status();                                                                }                                                                                             }
+    // (1×1: the chunked kernel below is faster — its 32-channel chunks need no halo)
+    SCFLOW_THINF(1, 3, 3)
+    SCFLOW_THINF(2, 3, 3)
+#undef SCFLOW_THINF
+  }
   if (tiled) {
     const int tr = 64 / g.ow;
     const unsigned blocks = (unsigned)(a.n * (g.oh / tr));

@@ -209,35 +209,55 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
         pixg[rr][r] = (img * P.oh + oy0 + m / tc) * ow + ox0 + m % tc;
       }
     if (nsplit > 1) {
-      __shared__ int s_last;
+      // the arrival flag lives in the dynamic LDS (after the affine table): a static __shared__
+      // variable would make the 160 KB dynamic-LDS attribute of this kernel invalid
+      int& s_last = *(int*)(Tg + 2 * ctot);
       float* mine = a.out + (size_t)z * slab;
 #pragma unroll
       for (int rr = 0; rr < RB; ++rr)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mine[(size_t)pixg[rr][r] * a.cout + col] = acc[rr][r];
+        for (int r = 0; r < 16; ++r)  // agent-scope stores: written through to the memory side
+          __hip_atomic_store(mine + (size_t)pixg[rr][r] * a.cout + col, acc[rr][r], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slab stores drained
       __syncthreads();
       const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+      // the slab stores are agent-scope (memory side) and drained: visible to the last arriver's
+      // agent-scope loads without a release fence (which would write back the XCD's whole L2)
       if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const int old = __hip_atomic_fetch_add(P.gcnt + tile, 1, __ATOMIC_RELAXED,
+        // one counter per 256 B (scflow_ph_conv_gn_plan): device-scope atomics on one line
+        // serialise at the memory side
+        const int old = __hip_atomic_fetch_add(P.gcnt + tile * 64, 1, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
         s_last = old == nsplit - 1;
       }
       __syncthreads();
       if (!s_last) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      // the tile's sum in slab order 0..nsplit-1 (this workgroup's own slab from registers)
+      // the tile's sum in slab order 0..nsplit-1 (this workgroup's own slab from registers);
+      // every other slab's values are loaded first (≤ 3 × 16·RB: one memory latency)
+      constexpr int KS = 4;  // the plan's K split at most
+      float sv[KS][RB][16];
+#pragma unroll
+      for (int zz = 0; zz < KS; ++zz)
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            sv[zz][rr][r] = (zz < nsplit && zz != z)
+                                ? __hip_atomic_load(a.out + zz * slab + (size_t)pixg[rr][r] * a.cout + col,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0.f;
 #pragma unroll
       for (int rr = 0; rr < RB; ++rr)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float v = 0.f;
-          for (int zz = 0; zz < nsplit; ++zz)
-            v += zz == z ? acc[rr][r] : a.out[zz * slab + (size_t)pixg[rr][r] * a.cout + col];
+#pragma unroll
+          for (int zz = 0; zz < KS; ++zz)
+            if (zz < nsplit) v += zz == z ? acc[rr][r] : sv[zz][rr][r];
           acc[rr][r] = v;
         }
-      if (tid == 0) __hip_atomic_store(P.gcnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(P.gcnt + tile * 64, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
     for (int rr = 0; rr < RB; ++rr)
@@ -598,7 +618,7 @@ int launch_enc(EncParams p, hipStream_t st) {
   p.hc = (p.tc - 1) * S + KW;
   const int ctot = p.a.cin + p.a.cin1;
   const size_t lds = sizeof(float) * ((size_t)p.hr * p.hc * ELDA + (size_t)KH * KW * EBN * ELDA +
-                                      (GNF ? 2 * (size_t)ctot : 0));
+                                      (GNF ? 2 * (size_t)ctot + 4 : 0));
   if ((size_t)p.hr * p.hc * (EBK / 4) > (size_t)256 * enc_na(TM, KH, KW, S)) return SCFLOW_EUNSUPPORTED;
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {

@@ -260,6 +260,28 @@ SCFLOW_API int scflow_pose_step(const float* drot6, const float* dt, const float
   return scflow_launch_status();
 }
 
+SCFLOW_API int scflow_pose_step_part(const float* drot6, const float* dt, const float* R_src,
+                                     const float* t_src, const float* K, const float* points,
+                                     float* R_dst, float* t_dst, float* flow, int n, int H, int W,
+                                     float weight, int depth_transform, float invalid_num,
+                                     const float* lr, const float* delta, const float* mask,
+                                     float* flow_up, float* mask_up, float* lr_next, int s_next,
+                                     float* hx_next, int s_hx, int h, int w, float up_scale,
+                                     float down_scale, int parts, void* stream) {
+  if (parts < 1 || parts > 3) return SCFLOW_EINVAL;
+  PoseStepArgs a;
+  const int st = pose_step_args(&a, drot6, dt, R_src, t_src, K, points, R_dst, t_dst, flow, n, H, W,
+                                weight, depth_transform, invalid_num, lr, delta, mask, flow_up,
+                                mask_up, lr_next, s_next, hx_next, s_hx, h, w, up_scale, down_scale,
+                                256);
+  if (st != SCFLOW_OK) return st;
+  if (!(parts & 1)) a.bf = 0;
+  if (!(parts & 2)) a.bl = 0;
+  if (a.bf + a.bl == 0) return SCFLOW_EINVAL;  // parts = 2 needs lr_next
+  pose_step_kernel<<<dim3(a.bf + a.bl, n), 256, 0, (hipStream_t)stream>>>(a);
+  return scflow_launch_status();
+}
+
 SCFLOW_API int scflow_transpose(const float* in, float* out, int n, int A, int B, long long ins,
                                 int ias, long long ons, int obs, void* stream) {
   if (!in || !out || n <= 0 || A <= 0 || B <= 0 || ias < B || obs < A) return SCFLOW_EINVAL;

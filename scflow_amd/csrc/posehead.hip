@@ -33,6 +33,9 @@
 namespace {
 
 constexpr int PH_K = 16;  // K chunk per MFMA group
+constexpr int PH_GN_KSMAX = 4;  // scflow_ph_conv_gn's K split at most (last-arriver fixup)
+// arrival counters one per 256 B: device-scope atomics on one line serialise at the memory side
+constexpr int PH_CNT_STRIDE = 64;
 
 struct PhConvArgs {
   const float* src0; int c0; int s0;
@@ -169,33 +172,45 @@ __device__ __forceinline__ void ph_conv_body(const PhConvArgs& a, int bx, int by
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (mm < M) a.parts[((size_t)bz * M + mm) * a.cout + col] = acc[r];
+        if (mm < M)  // agent-scope stores: written through to the memory side
+          __hip_atomic_store(a.parts + ((size_t)bz * M + mm) * a.cout + col, acc[r], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int tile = by * gridDim.x + bx;
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const int old = __hip_atomic_fetch_add(a.counters + tile, 1, __ATOMIC_RELAXED,
+    if (threadIdx.x == 0) {  // agent-scope slab stores drained: no release fence needed
+      const int old = __hip_atomic_fetch_add(a.counters + tile * PH_CNT_STRIDE, 1, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
       s_last = old == a.ksplit - 1;
     }
     __syncthreads();
     if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (wave == 0) {
+      // every slab value first (≤ 4 slabs × 16: one memory latency), then the sums in slab order
+      float sv[PH_GN_KSMAX][16];
+#pragma unroll
+      for (int zz = 0; zz < PH_GN_KSMAX; ++zz)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          sv[zz][r] = (zz < a.ksplit && zz != bz && mm < M && nvalid)
+                          ? __hip_atomic_load(a.parts + ((size_t)zz * M + mm) * a.cout + col,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0.f;
+        }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
         float v = 0.f;
-        if (mm < M && nvalid)
-          for (int zz = 0; zz < a.ksplit; ++zz)
-            v += zz == bz ? acc[r] : a.parts[((size_t)zz * M + mm) * a.cout + col];
+#pragma unroll
+        for (int zz = 0; zz < PH_GN_KSMAX; ++zz)
+          if (zz < a.ksplit) v += zz == bz ? acc[r] : sv[zz][r];
         acc[r] = v;
       }
       if (threadIdx.x == 0)
-        __hip_atomic_store(a.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.counters + tile * PH_CNT_STRIDE, 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (wave == 0 && nvalid) {
@@ -398,6 +413,7 @@ struct FcArgs {
   // channel) affine is built in LDS from gst [m][gst_tpi][gst_groups][2] over gst_hw pixels
   const double* gst; int gst_tpi, gst_groups, gst_hw; const float* gamma; const float* beta;
   float eps;
+  int coherent_out;  // ksplit outputs stored at agent scope (read by a last-arriving workgroup)
 };
 
 // one 16-neuron tile bx of K slice by; NW waves; red: (NW/2)·FC_RT·64·5 floats of LDS
@@ -504,7 +520,11 @@ __device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, floa
               v += f.bias ? f.bias[i] : 0.f;
               if (f.relu) v = fmaxf(v, 0.f);
             }
-            yout[(size_t)row * f.n + i] = v;
+            if (f.coherent_out)  // a last-arriver reads these from another XCD (fc2 + heads)
+              __hip_atomic_store(yout + (size_t)row * f.n + i, v, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            else
+              yout[(size_t)row * f.n + i] = v;
           }
         }
       }
@@ -516,6 +536,98 @@ template <int FC_RT>
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
   __shared__ float red[PH_WAVES / 2 * FC_RT * 64 * 5];
   ph_fc_body<PH_WAVES, FC_RT>(f, blockIdx.x, blockIdx.y, red, f.scale, f.shift);
+}
+
+// FC2 + heads in one launch (scflow_ph_fc2_heads): the K-split FC2 partials as ph_fc_kernel,
+// then the last-arriving workgroup (arrival counter hc, left at zero) sums them in slab order
+// with FC2's bias + ReLU into LDS and computes label[0]'s rotation / translation rows
+struct HeadsArgs {
+  int dbg;  // tuning (SCFLOW_FC2H_DBG): bit 0 skips the heads, bit 1 plain FC2 stores, bit 2 the
+            // arrival protocol
+  int* counter;
+  const float* b2;                      // FC2 bias [n2]
+  const float* Wr; const float* br; int rch;
+  const float* Wt; const float* bt;
+  const long long* label; int num_class;
+  float* drot; float* dt;
+};
+
+template <int FC_RT>
+__global__ __launch_bounds__(PH_WAVES * 64) void ph_fc2_heads_kernel(FcArgs f, HeadsArgs h) {
+  __shared__ float red[PH_WAVES / 2 * FC_RT * 64 * 5];
+  __shared__ float x2[32 * 256];
+  __shared__ float wrows[16 * 256];
+  __shared__ int s_last;
+  ph_fc_body<PH_WAVES, FC_RT>(f, blockIdx.x, blockIdx.y, red, f.scale, f.shift);
+  if (h.dbg & 4) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {  // agent-scope slab stores drained: no release fence needed
+    // two levels (one counter per 256 B): the K slices of a neuron tile, then the tiles — short
+    // chains of device-scope atomics instead of one chain through every workgroup
+    int* ct = h.counter + (1 + blockIdx.x) * PH_CNT_STRIDE;
+    int last = __hip_atomic_fetch_add(ct, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (int)gridDim.y - 1;
+    if (last) {
+      __hip_atomic_store(ct, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(h.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (int)gridDim.x - 1;
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last || (h.dbg & 1)) return;
+  const int m = f.m, n2 = f.n;
+  long long cls = h.label[0];
+  if (cls < 0 || cls >= h.num_class) cls = 0;
+  const int nout = h.rch + 3;
+  float* wl = wrows;  // the class's nout ≤ 16 weight rows
+  // every load first (one memory latency): FC2's ≤ 8 slabs per float4 of x2, the weight rows
+  {
+    constexpr int KSMAX = 8;
+    for (int i4 = threadIdx.x; i4 < m * n2 / 4; i4 += blockDim.x) {
+      floatx4 v[KSMAX];
+#pragma unroll
+      for (int z = 0; z < KSMAX; ++z)
+        if (z < f.ksplit)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[z][e] = __hip_atomic_load(f.y + (size_t)z * m * n2 + 4 * i4 + e, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+      floatx4 sum = v[0];
+#pragma unroll
+      for (int z = 1; z < KSMAX; ++z)
+        if (z < f.ksplit) sum += v[z];
+      const floatx4 b = *(const floatx4*)(h.b2 + (4 * i4) % n2);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x2[4 * i4 + e] = fmaxf(sum[e] + b[e], 0.f);
+    }
+    for (int i = threadIdx.x; i < nout * n2; i += blockDim.x) {
+      const int o = i / n2, k = i % n2;
+      wl[i] = o < h.rch ? h.Wr[((size_t)cls * h.rch + o) * n2 + k]
+                        : h.Wt[((size_t)cls * 3 + (o - h.rch)) * n2 + k];
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(h.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  // one wave per (row, output) pair: the lanes take consecutive k (conflict-free LDS reads),
+  // then a fixed-order shuffle reduction
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int pr = wv; pr < m * nout; pr += blockDim.x / 64) {
+      const int row = pr / nout, o = pr % nout;
+      float acc = 0.f;
+      for (int k = lane; k < n2; k += 64) acc += wl[o * n2 + k] * x2[row * n2 + k];
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d);
+      if (lane == 0) {
+        if (o < h.rch)
+          h.drot[(size_t)row * h.rch + o] = acc + h.br[cls * h.rch + o];
+        else
+          h.dt[(size_t)row * 3 + (o - h.rch)] = acc + h.bt[cls * 3 + (o - h.rch)];
+      }
+    }
+  }
 }
 
 // FC with the input GroupNorm built from partial statistics: the [m][gn_c] affine in LDS first
@@ -942,7 +1054,8 @@ SCFLOW_API int scflow_ph_conv_gn_plan_for(const scflow_ph_conv_gn_args* p,
     const long long tiles = (long long)p->n * tpi_tiles * (p->cout / 64);
     const int nst = cin / 16;
     plan->path = 1;
-    plan->ksplit = (int)std::max(1LL, std::min((long long)nst, (512 + tiles - 1) / tiles));
+    plan->ksplit = (int)std::max(1LL, std::min({(long long)nst, (512 + tiles - 1) / tiles,
+                                                (long long)PH_GN_KSMAX}));
     plan->tpi = 2 * tpi_tiles;
     plan->counters = (int)tiles;
   } else {
@@ -951,12 +1064,13 @@ SCFLOW_API int scflow_ph_conv_gn_plan_for(const scflow_ph_conv_gn_args* p,
     const long long tiles = ((M + 31) / 32) * ((p->cout + 31) / 32);
     const int nall = p->kh * p->kw * ((cin + PH_K - 1) / PH_K);
     plan->path = 0;
-    plan->ksplit = (int)std::max(1LL, std::min((long long)(nall / 16), (256 + tiles - 1) / tiles));
+    plan->ksplit = (int)std::max(1LL, std::min({(long long)(nall / 16), (256 + tiles - 1) / tiles,
+                                                (long long)PH_GN_KSMAX}));
     plan->tpi = tpi;
     plan->counters = (int)tiles;
   }
   plan->parts_floats = plan->ksplit > 1 ? (long long)plan->ksplit * M * p->cout : 0;
-  if (plan->ksplit == 1) plan->counters = 0;
+  plan->counters = plan->ksplit > 1 ? plan->counters * PH_CNT_STRIDE : 0;
   return SCFLOW_OK;
 }
 
@@ -1034,6 +1148,35 @@ SCFLOW_API int scflow_ph_fc_split_gn(const float* x, int m, int k, const float* 
     ph_fc_gn_kernel<1><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
   else
     ph_fc_gn_kernel<2><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_ph_fc2_heads(const float* parts1, int xsplit, const float* b1, int m, int k,
+                                   const float* W2, const float* b2, float* parts2, int n2,
+                                   int ksplit, const float* Wr, const float* br, int rch,
+                                   const float* Wt, const float* bt, const long long* label,
+                                   int num_class, float* drot, float* dt, int* counter,
+                                   void* stream) {
+  if (!parts1 || xsplit <= 0 || !b1 || !W2 || !b2 || !parts2 || !Wr || !br || !Wt || !bt ||
+      !label || !drot || !dt || !counter || m <= 0 || m > 32 || k <= 0 || (k & 15) || n2 <= 0 ||
+      n2 % 4 || m * n2 > 32 * 256 || (rch + 3) * n2 > 16 * 256 || ksplit <= 0 || ksplit > 8 ||
+      ksplit > k / 16 || rch <= 0 || num_class <= 0 ||
+      !aligned16(parts1) || !aligned16(W2) || !aligned16(b1))
+    return SCFLOW_EINVAL;
+  FcArgs f{};
+  f.x = parts1; f.ldx = k; f.m = m; f.k = k; f.W = W2; f.y = parts2; f.n = n2; f.ksplit = ksplit;
+  f.xsplit = xsplit; f.xstride = (long long)m * k; f.xbias = b1;
+  static const int dbg = [] {
+    const char* e = getenv("SCFLOW_FC2H_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  f.coherent_out = (dbg & 2) ? 0 : 1;
+  HeadsArgs h{dbg, counter, b2, Wr, br, rch, Wt, bt, label, num_class, drot, dt};
+  dim3 grid((unsigned)((n2 + 15) / 16), (unsigned)ksplit);
+  if (m <= 16)
+    ph_fc2_heads_kernel<1><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f, h);
+  else
+    ph_fc2_heads_kernel<2><<<grid, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f, h);
   return scflow_launch_status();
 }
 

@@ -108,6 +108,11 @@ class SCFlowDecoder(nn.Module):
         # (agent release + acquire + L2 misses on the producer's lines) that a kernel boundary
         # (≈2 µs) does not
         self.fuse_posehead = False
+        # with fuse_tail: the iteration's pose step runs only its ↓8 part (the next iteration's
+        # flow, scflow_pose_step_part) on the critical path; its full-resolution outputs (pose
+        # flow, ×8 prediction, mask) run on the side stream at the start of the next iteration,
+        # beside the lookup (they only feed the returned lists)
+        self.defer_full_res = True
         # correlation pyramid in the tiled layout (4×4 tiles of 16 floats per map, pooling fused
         # into the GEMM epilogue; ops.corr_pyramid_tiled) when the geometry allows it
         self.tiled_pyramid = True
@@ -482,15 +487,26 @@ class SCFlowDecoder(nn.Module):
                       hooks=self._hooks_for(None, "mask_enc1"))
 
         def seg_flow_pred():
+            D2 = D2s[cur_par[0]]
             flow_pred_r.run(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w)
             run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe,
                       hooks=self._hooks_for(None, "dflow1"))
 
         pose_x = []
         tail_calls = None  # fused tail: per-iteration (heads, pose_step) launches, built once
+        defer = fuse_tail and self.defer_full_res and not self.fuse_posehead and iters > 1
+        # Δflow alternates between two buffers when the full-resolution outputs are deferred: the
+        # previous iteration's deferred launch reads its Δflow on the side stream while this
+        # iteration's flow predictor writes the other one on the main stream
+        D2s = [D2, torch.empty_like(D2)] if defer else [D2, D2]
+        cur_par = [0]
+        pending = []  # the previous iteration's deferred full-resolution launches
+        if defer:  # the deferred launches' pose outputs (duplicates of o_R / o_t: not read)
+            R_scr = torch.empty(N, 3, 3, device=dev, dtype=f32)
+            t_scr = torch.empty(N, 3, device=dev, dtype=f32)
 
         def seg_pose_trunk():
-            pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep))
+            pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep, slot=slot))
 
         fuse_ph = fuse_tail and self.fuse_posehead and \
             self.pose_pred.tail_supported(hid, Chan.whole(FM), N, h, w)
@@ -539,12 +555,21 @@ class SCFlowDecoder(nn.Module):
             if pp is not None:
                 pp[1](it)
             yield "heavy"
-            # mask predictor + mask encoder (a5, a6) on the side stream
+            # mask predictor + mask encoder (a5, a6) on the side stream, after the previous
+            # iteration's deferred full-resolution outputs (they read its MASK; the side branch
+            # is the shorter one here)
             fork()
             with torch.cuda.stream(side):
+                if pending:
+                    self._hook("pose_flow", True)
+                    for c in pending:
+                        c()
+                    self._hook("pose_flow", False)
+                    pending = []
                 segment("mask_branch", seg_mask_branch)
-            # flow predictor + Δflow encoder
-            segment("flow_pred", seg_flow_pred)
+            # flow predictor + Δflow encoder (into this iteration's Δflow buffer)
+            cur_par[0] = it % 2 if defer else 0
+            segment("flow_pred" + (par if defer else ""), seg_flow_pred)
             join()
             if mask_lr is not None:
                 mask_lr = MASK
@@ -564,9 +589,9 @@ class SCFlowDecoder(nn.Module):
                     Rp, tp = R_prev, t_prev
                     for j in range(iters):
                         last = j == iters - 1
-                        hc, pc = [], []
+                        hc, pc, fc = [], [], []
                         step = (o_drot[j], o_dt[j], Rp, tp, K, points, o_R[j], o_t[j],
-                                o_flow_pose[j], invalid, F2s[j % 2], D2, MASK, o_flow_pred[j],
+                                o_flow_pose[j], invalid, F2s[j % 2], D2s[j % 2], MASK, o_flow_pred[j],
                                 o_mask[j], h, w, float(scale))
                         nxt = dict(lr_next=None if last else Chan.whole(F2s[(j + 1) % 2]),
                                    hx_next=None if last else hx_flow,
@@ -580,22 +605,32 @@ class SCFlowDecoder(nn.Module):
                         else:
                             with ops.binding(hc, run=False):
                                 self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
-                            with ops.binding(pc, run=False):
-                                ops.pose_step(*step, **nxt)
-                        tail_calls.append((hc, pc))
+                            if defer and not last:
+                                with ops.binding(pc, run=False):
+                                    ops.pose_step(*step, **nxt, parts=2)
+                                fstep = step[:6] + (R_scr, t_scr) + step[8:]
+                                with ops.binding(fc, run=False):
+                                    ops.pose_step(*fstep, **nxt, parts=1)
+                            else:
+                                with ops.binding(pc, run=False):
+                                    ops.pose_step(*step, **nxt)
+                        tail_calls.append((hc, pc, fc))
                         Rp, tp = o_R[j], o_t[j]
-                hc, pc = tail_calls[it]
+                hc, pc, fc = tail_calls[it]
                 for c in hc:
                     c()
                 hook = "pose_tail" if fuse_ph else "pose_flow"
-                self._hook(hook, True)
+                if not fc:
+                    self._hook(hook, True)
                 for c in pc:
                     c()
-                self._hook(hook, False)
+                if not fc:
+                    self._hook(hook, False)
+                pending = fc
             else:
                 self.pose_pred.heads_hip(pose_x[0], label, drot, dtr)
                 # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
-                ops.flow_upsample(F2, D2, MASK, N, h, w, H, W, float(scale), o_flow_pred[it],
+                ops.flow_upsample(F2, D2s[0], MASK, N, h, w, H, W, float(scale), o_flow_pred[it],
                                   o_mask[it])
                 # a8 + a10: pose update + pose-induced flow (one launch)
                 self._hook("pose_flow", True)

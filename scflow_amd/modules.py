@@ -348,6 +348,24 @@ def run_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int
         cur = out
 
 
+class _LaBuf:
+    """A zero-filled byte buffer with a raw pointer (last-arriver slabs / counters)."""
+    __slots__ = ("t", "ptr", "nbytes")
+
+    def __init__(self, nbytes: int, dev: int) -> None:
+        self.t = torch.zeros((int(nbytes) + 15) // 16 * 4, device=dev, dtype=torch.int32)
+        self.ptr, self.nbytes = self.t.data_ptr(), int(nbytes)
+
+
+class _Fc1Partials:
+    """The fused-statistics trunk's output when FC2 runs with the heads: FC1's K-split partials
+    plus FC2's slab buffer and the heads launch's arrival counter (kept zero between launches)."""
+    __slots__ = ("y1", "parts2", "counter", "ks")
+
+    def __init__(self, y1: Tensor, parts2, counter, ks: int) -> None:
+        self.y1, self.parts2, self.counter, self.ks = y1, parts2, counter, ks
+
+
 # ---------------------------------------------------------------------------------- a4
 class ConvGRU(nn.Module):
     """raft_decoder.py:168-253.  z and r share one conv launch (cout = 2·h_channels) whose
@@ -652,7 +670,7 @@ class MultiClassPoseHead(nn.Module):
         return drot, dt
 
     def trunk_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                  ws: Optional[list] = None) -> Tensor:
+                  ws: Optional[list] = None, slot: int = 0) -> Tensor:
         """Convs + FCs of forward_hip → the last FC's output [n, 256].  Every buffer it allocates
         is appended to ``ws`` (the decoder keeps them alive while replaying these launches).
 
@@ -662,7 +680,9 @@ class MultiClassPoseHead(nn.Module):
         if any(m.norm_type != "GN" or m.act_type != "ReLU" for m in self.conv_layers):
             raise NotImplementedError("HIP pose head: conv + GroupNorm + ReLU layers only")
         if self.fused_gn and self._gn_fused_ok(src0, src1, n, h, w):
-            return self._trunk_gn(src0, src1, n, h, w, ws)
+            # slot: trunks that may run concurrently (the decoder's ping-pong halves) take
+            # separate last-arriver buffers
+            return self._trunk_gn(src0, src1, n, h, w, ws, slot)
         dev = src0.buf.device
         keep = ws if ws is not None else []
 
@@ -777,6 +797,20 @@ class MultiClassPoseHead(nn.Module):
     def _gn_fused_ok(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int) -> bool:
         return self._gn_plans(src0, src1, n, h, w) is not None
 
+    def _uncached(self, key, nbytes: int) -> "_LaBuf":
+        """A zero-filled device buffer of at least ``nbytes`` for a last-arriver reduction (the
+        kernels reach it with agent-scope accesses), kept on the module (one per key and
+        device; the counters stay zero between launches, so every launch that uses a buffer
+        must run to completion before the next starts)."""
+        bufs = getattr(self, "_uc_bufs", None)
+        if bufs is None:
+            bufs = self._uc_bufs = {}
+        dev = torch.cuda.current_device()
+        b = bufs.get((key, dev))
+        if b is None or b.nbytes < nbytes:
+            b = bufs[(key, dev)] = _LaBuf(nbytes, dev)
+        return b
+
     def _gn_weight(self, i: int, path: int) -> Tensor:
         """conv_layers[i]'s weights packed for plan path 1 (enc_conv) or 0 (ph_conv)."""
         wt = self.conv_layers[i].conv.weight
@@ -789,7 +823,7 @@ class MultiClassPoseHead(nn.Module):
         return packs[i][1]
 
     def _trunk_gn(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                  ws: Optional[list] = None) -> Tensor:
+                  ws: Optional[list] = None, slot: int = 0) -> Tensor:
         """trunk_hip with every GroupNorm fused (pose_head.py:201-211): each
         conv (scflow_ph_conv_gn: the halo-staged MFMA conv or the gather conv, its K split
         summed by the last-arriving workgroup of each tile) writes its raw output and fp64
@@ -828,8 +862,8 @@ class MultiClassPoseHead(nn.Module):
             a.out_stats, a.out_groups = st.data_ptr(), m.gn.num_groups
             a.ksplit = plan.ksplit
             if plan.ksplit > 1:
-                a.parts = empty(plan.parts_floats).data_ptr()
-                a.counters = empty(plan.counters, dtype=torch.int32).zero_().data_ptr()
+                a.parts = self._uncached(("parts", i, slot), 4 * plan.parts_floats).ptr
+                a.counters = self._uncached(("cnt", i, slot), 4 * plan.counters).ptr
             ops.ph_conv_gn(a, y)
             cur0, cur1, prev, prev_st = Chan.whole(y), None, m, st
         c = cur0.c
@@ -840,15 +874,34 @@ class MultiClassPoseHead(nn.Module):
         ops.ph_fc_split_gn(cur0.buf, n, k_in, fc1_w, y1, l1.out_features, ks, c, prev_st,
                            prev.gn.num_groups, ohl * owl, prev.gn.weight.detach(),
                            prev.gn.bias.detach(), prev.gn.eps)
+        self._split_fc = True
+        if self.fused_fc2_heads and n * l2.out_features <= 8192 and l2.out_features % 4 == 0:
+            # FC2 and the heads run as ONE launch per call of heads_hip (last-arriver heads)
+            return _Fc1Partials(y1, self._uncached(("fc2", slot), 4 * ks * n * l2.out_features),
+                                self._uncached(("fc2cnt", slot), 4 * 64 * (1 + -(-l2.out_features // 16))),
+                                ks)
         y2 = empty(ks, n, l2.out_features)
         ops.ph_fc_split(y1, l1.out_features, n, l1.out_features, l2.weight.detach(), y2,
                         l2.out_features, ks, xsplit=ks, xbias=l1.bias.detach())
-        self._split_fc = True
         return y2
 
-    def heads_hip(self, x: Tensor, label: Tensor, drot: Tensor, dt: Tensor) -> None:
+    #: FC2 + heads as one launch (scflow_ph_fc2_heads) after the fused-statistics trunk
+    fused_fc2_heads = True
+
+    def heads_hip(self, x, label: Tensor, drot: Tensor, dt: Tensor) -> None:
         """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt
-        (x: [n, 256], or the last FC's split partial sums [split, n, 256])."""
+        (x: [n, 256], the last FC's split partial sums [split, n, 256], or FC1's partials from
+        the fused trunk — then FC2 runs here too, in the same launch)."""
+        if isinstance(x, _Fc1Partials):
+            l1, l2 = self.fc_layers[0][0], self.fc_layers[1][0]
+            n = x.y1.shape[1]
+            ops.ph_fc2_heads(x.y1, l1.bias.detach(), n, l1.out_features, l2.weight.detach(),
+                             l2.bias.detach(), x.parts2, l2.out_features, x.ks,
+                             self.rotation_pred.weight.detach(), self.rotation_pred.bias.detach(),
+                             self.rotation_out_channels, self.translation_pred.weight.detach(),
+                             self.translation_pred.bias.detach(), label.long(), self.num_class,
+                             drot, dt, x.counter)
+            return
         if x.dim() == 3:
             n, k = x.shape[1], x.shape[2]
             ops.ph_heads(x, n, k, self.rotation_pred.weight.detach(),

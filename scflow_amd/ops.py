@@ -327,6 +327,22 @@ class BoundLaunch:
             check(rc, self.name)
 
 
+class UncachedBuffer:
+    """Zero-filled uncached device memory (scflow_alloc_uncached) on the current device — the
+    pose head's last-arriver slabs and counters; freed when the object dies."""
+
+    def __init__(self, nbytes: int) -> None:
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(lib.scflow_alloc_uncached(int(nbytes), ctypes.byref(h)), "scflow_alloc_uncached")
+        self.ptr, self.nbytes = h.value, int(nbytes)
+
+    def __del__(self) -> None:
+        if getattr(self, "ptr", None):
+            _lib.load().scflow_free_uncached(self.ptr)
+            self.ptr = None
+
+
 class SyncEvent:
     """A device-scope cross-stream event (scflow_sync_event_*): ``record(stream)`` then
     ``wait(stream)`` orders the second stream after the first without the system-scope cache
@@ -480,10 +496,11 @@ def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points:
               lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], flow_up: Tensor,
               mask_up: Optional[Tensor], h: int, w: int, up_scale: float,
               lr_next: Optional[Chan] = None, hx_next: Optional[Chan] = None,
-              weight: float = 10.0, depth_transform: str = "exp") -> None:
+              weight: float = 10.0, depth_transform: str = "exp", parts: int = 3) -> None:
     """One launch: ``pose_update_flow`` + ``flow_upsample(lr, delta, mask → flow_up, mask_up)``
     + (if ``lr_next``) the next iteration's ``flow_downsample`` of the new pose flow into
-    ``lr_next`` / ``hx_next``, computed from the pose directly (scflow_pose_step)."""
+    ``lr_next`` / ``hx_next``, computed from the pose directly (scflow_pose_step).  ``parts``
+    (scflow_pose_step_part): 1 = only the full-resolution outputs, 2 = only the ↓8 flow."""
     for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t), ("K", K), ("points", points),
                   ("R_out", R_out), ("t_out", t_out), ("flow_out", flow_out), ("lr", lr),
                   ("flow_up", flow_up)):
@@ -491,13 +508,16 @@ def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points:
     n, H, W, _ = points.shape
     if lr_next is not None and lr_next.buf.data_ptr() == lr.data_ptr():
         raise ValueError("pose_step: lr_next must not alias lr")
-    _launch("scflow_pose_step", drot,
-        _p(drot), _p(dt), _p(R), _p(t), _p(K), _p(points), _p(R_out), _p(t_out), _p(flow_out), n,
-        H, W, float(weight), pose_mode(drot, depth_transform), float(invalid_num), _p(lr),
-        _p(delta), _p(mask), _p(flow_up), _p(mask_up),
-        None if lr_next is None else lr_next.ptr, 0 if lr_next is None else lr_next.stride,
-        None if hx_next is None else hx_next.ptr, 0 if hx_next is None else hx_next.stride,
-        h, w, float(up_scale), 1.0 / float(up_scale))
+    args = (_p(drot), _p(dt), _p(R), _p(t), _p(K), _p(points), _p(R_out), _p(t_out), _p(flow_out), n,
+            H, W, float(weight), pose_mode(drot, depth_transform), float(invalid_num), _p(lr),
+            _p(delta), _p(mask), _p(flow_up), _p(mask_up),
+            None if lr_next is None else lr_next.ptr, 0 if lr_next is None else lr_next.stride,
+            None if hx_next is None else hx_next.ptr, 0 if hx_next is None else hx_next.stride,
+            h, w, float(up_scale), 1.0 / float(up_scale))
+    if parts == 3:
+        _launch("scflow_pose_step", drot, *args)
+    else:
+        _launch("scflow_pose_step_part", drot, *args, int(parts))
 
 
 def pose_step_struct(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points: Tensor,
@@ -651,6 +671,22 @@ def ph_fc_split_gn(x: Tensor, m: int, k: int, W: Tensor, parts: Tensor, n: int, 
     _require(stats, "stats", dtype=torch.float64)
     _launch("scflow_ph_fc_split_gn", x, _p(x), m, k, _p(W), _p(parts), n, ksplit, gn_c, _p(stats),
             stats.shape[1], groups, hw, _p(gamma), _p(beta), float(eps))
+
+
+def ph_fc2_heads(parts1: Tensor, b1: Tensor, m: int, k: int, W2: Tensor, b2: Tensor,
+                 parts2, n2: int, ksplit: int, Wr: Tensor, br: Tensor, rch: int,
+                 Wt: Tensor, bt: Tensor, label: Tensor, num_class: int, drot: Tensor, dt: Tensor,
+                 counter) -> None:
+    """FC2 on FC1's K-split partials + the label[0] heads in one launch (scflow_ph_fc2_heads);
+    ``parts2`` / ``counter``: buffers with ``ptr`` / ``nbytes`` (FC2's slabs, the zeroed arrival
+    counter)."""
+    if label.dtype != torch.int64 or label.device != parts1.device:
+        raise TypeError("label must be an int64 tensor on the same device")
+    if parts2.nbytes < 4 * ksplit * m * n2 or counter.nbytes < 4 * 64 * (1 + -(-n2 // 16)):
+        raise ValueError("ph_fc2_heads: uncached buffers too small")
+    _launch("scflow_ph_fc2_heads", parts1, _p(parts1), parts1.shape[0], _p(b1), m, k, _p(W2), _p(b2),
+            parts2.ptr, n2, ksplit, _p(Wr), _p(br), rch, _p(Wt), _p(bt), _p(label), num_class,
+            _p(drot), _p(dt), counter.ptr)
 
 
 def ph_fc_permute(W: Tensor, c: int, hw: int) -> Tensor:

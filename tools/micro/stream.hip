@@ -13,6 +13,7 @@
 //   read_b32  sum of a               4 B/lane coalesced loads
 //   gather_b32  the pyramid lookup's pattern (csrc/lookup.hip): 16 lanes read one 64-B 4×4 tile
 //               with 4-byte loads, tiles visited in a scattered (hashed) order, each tile once
+//   gather2_b32 the same with 128-B pieces (two adjacent tiles per 32 lanes)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -69,6 +70,18 @@ __global__ __launch_bounds__(256) void gather_b32(const float* __restrict__ a, f
   if (s == 12345.678f) out[blockIdx.x] = s;
 }
 
+// as gather_b32 but with 128-B pieces: 32 lanes read two adjacent 64-B tiles (one 128-B line)
+__global__ __launch_bounds__(256) void gather2_b32(const float* __restrict__ a, float* __restrict__ out,
+                                                   long long lines) {
+  float s = 0.f;
+  const long long groups = (long long)gridDim.x * 8;
+  for (long long g = blockIdx.x * 8LL + (threadIdx.x >> 5); g < lines; g += groups) {
+    const long long t = (g * 2654435761LL) & (lines - 1);
+    s += a[t * 32 + (threadIdx.x & 31)];
+  }
+  if (s == 12345.678f) out[blockIdx.x] = s;
+}
+
 int main(int argc, char** argv) {
   const bool once = argc > 1;  // profiling: one launch per kernel
   const long long bytes = 2LL << 30;  // 2 GiB per buffer: 8× the Infinity Cache
@@ -90,7 +103,8 @@ int main(int argc, char** argv) {
     double moved;  // compulsory bytes per launch
     int which;
   } ks[] = {{"copy_f4", 2.0 * bytes, 0}, {"read_f4", 1.0 * bytes, 1}, {"write_f4", 1.0 * bytes, 2},
-            {"read_b32", 1.0 * bytes, 3}, {"gather_b32", 1.0 * bytes, 4}};
+            {"read_b32", 1.0 * bytes, 3}, {"gather_b32", 1.0 * bytes, 4},
+            {"gather2_b32", 1.0 * bytes, 5}};
   for (const K& k : ks) {
     float best = 1e30f;
     const int reps = once ? 1 : 20;
@@ -102,6 +116,7 @@ int main(int argc, char** argv) {
         case 2: write_f4<<<grid, 256>>>((float4*)b, n4, 1.f); break;
         case 3: read_b32<<<grid, 256>>>(a, out, n1); break;
         case 4: gather_b32<<<grid, 256>>>(a, out, tiles); break;
+        case 5: gather2_b32<<<grid, 256>>>(a, out, tiles / 2); break;
       }
       CK(hipGetLastError());
       CK(hipEventRecord(e));

@@ -7,6 +7,7 @@ OUT=$R/gpurun_out/stream_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 $R/tools/micro/stream > $OUT/stream.txt 2>&1 || exit $?
+timeout -k 10 60 rocprofv3 -L > $OUT/counters_avail.txt 2>&1 || true
 cat $OUT/stream.txt
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $R/tools/micro/stream 1 > $OUT/fetch.log 2>&1 || exit $?
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $R/tools/micro/stream 1 > $OUT/write.log 2>&1 || exit $?
