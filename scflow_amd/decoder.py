@@ -110,8 +110,8 @@ class SCFlowDecoder(nn.Module):
         self.fuse_posehead = False
         # with fuse_tail: the iteration's pose step runs only its ↓8 part (the next iteration's
         # flow, scflow_pose_step_part) on the critical path; its full-resolution outputs (pose
-        # flow, ×8 prediction, mask) run on the side stream at the start of the next iteration,
-        # beside the lookup (they only feed the returned lists)
+        # flow, ×8 prediction, mask) run on the side stream during the next iteration's GRU
+        # (they only feed the returned lists)
         self.defer_full_res = True
         # correlation pyramid in the tiled layout (4×4 tiles of 16 floats per map, pooling fused
         # into the GEMM epilogue; ops.corr_pyramid_tiled) when the geometry allows it
@@ -545,6 +545,17 @@ class SCFlowDecoder(nn.Module):
             segment("corr_last", seg_corr_last)
             self._hook("corr_net1", False)
             join()
+            if pending:
+                # the previous iteration's full-resolution outputs on the side stream AFTER the
+                # join's record: they overlap out_net and the GRU (MFMA-bound) instead of
+                # lengthening a joined branch; the mask branch queued behind them reads MASK after
+                # they do, and Δflow / F2 are double-buffered against this iteration's writes
+                with torch.cuda.stream(side):
+                    self._hook("pose_flow", True)
+                    for c in pending:
+                        c()
+                    self._hook("pose_flow", False)
+                pending = []
             segment("out", seg_out)
             # a4 GRU (in place on HX[:, :hc])
             gru_step(self.kernel_hooks)
@@ -560,12 +571,6 @@ class SCFlowDecoder(nn.Module):
             # is the shorter one here)
             fork()
             with torch.cuda.stream(side):
-                if pending:
-                    self._hook("pose_flow", True)
-                    for c in pending:
-                        c()
-                    self._hook("pose_flow", False)
-                    pending = []
                 segment("mask_branch", seg_mask_branch)
             # flow predictor + Δflow encoder (into this iteration's Δflow buffer)
             cur_par[0] = it % 2 if defer else 0

@@ -759,8 +759,11 @@ class MultiClassPoseHead(nn.Module):
         return x
 
     #: the fused-statistics trunk (scflow_ph_conv_gn / scflow_ph_fc_split_gn: 5 launches + heads,
-    #: no GroupNorm launches, no K-split slabs) when the shapes allow it
-    fused_gn = True
+    #: no GroupNorm launches; K-split slabs summed by each tile's last-arriving workgroup).  Off:
+    #: measured slower in the decoder at B=16 (101 vs 96 µs per pose head) — the last-arriver
+    #: hand-off (agent-scope slab stores drained, arrival atomic, slab loads from the memory
+    #: side) costs about what the GroupNorm launch it replaces does
+    fused_gn = False
 
     def _gn_plans(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int):
         """[(args, plan, oh, ow)] per conv layer for the fused-statistics trunk, or None."""
@@ -885,8 +888,10 @@ class MultiClassPoseHead(nn.Module):
                         l2.out_features, ks, xsplit=ks, xbias=l1.bias.detach())
         return y2
 
-    #: FC2 + heads as one launch (scflow_ph_fc2_heads) after the fused-statistics trunk
-    fused_fc2_heads = True
+    #: FC2 + heads as one launch (scflow_ph_fc2_heads) after the fused-statistics trunk.  Off:
+    #: 21.8 µs vs 7.1 + 7.1 µs for the two launches (the single last workgroup's heads work and
+    #: the hand-off are slower than a second launch)
+    fused_fc2_heads = False
 
     def heads_hip(self, x, label: Tensor, drot: Tensor, dt: Tensor) -> None:
         """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt

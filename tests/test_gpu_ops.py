@@ -524,18 +524,20 @@ def test_pose_head_hip_vs_oracle(ops, n, feat):
     # NCHW module API
     r2, t2 = head(x.cuda(), label.cuda())
     close(r2, r, 1e-6, 1e-6, "pose head NCHW api")
-    # the fused-statistics trunk (default where supported) against the GroupNorm-launch trunk
+    # the opt-in fused-statistics trunk (scflow_ph_conv_gn: no GroupNorm launches, last-arriver
+    # K-split sums), with and without FC2 + heads in one launch, against the default trunk
     fused = head._gn_fused_ok(ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf), n, feat, feat)
-    assert fused  # every configuration here (n ≤ 32, 32² and 64² features) takes the fused trunk
-    head.fused_gn = False
-    try:
-        r4, t4 = head.forward_hip(ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf), n, feat, feat,
-                                  label.cuda())
-    finally:
-        head.fused_gn = True
-    close(r4, r_ref, 2e-5, 1e-5, "pose head rotation (GroupNorm launches)")
-    close(t4, t_ref, 2e-5, 1e-5, "pose head translation (GroupNorm launches)")
-    close(r4, r, 1e-5, 1e-6, "fused-statistics vs GroupNorm-launch trunk")
+    assert fused  # every configuration here (n ≤ 32, 32² and 64² features) supports it
+    for fc2h in (False, True):
+        head.fused_gn, head.fused_fc2_heads = True, fc2h
+        try:
+            r4, t4 = head.forward_hip(ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf), n, feat, feat,
+                                      label.cuda())
+        finally:
+            head.fused_gn, head.fused_fc2_heads = False, False
+        close(r4, r_ref, 2e-5, 1e-5, f"pose head rotation (fused statistics, fc2+heads {fc2h})")
+        close(t4, t_ref, 2e-5, 1e-5, f"pose head translation (fused statistics, fc2+heads {fc2h})")
+        close(r4, r, 1e-5, 1e-6, "fused-statistics vs GroupNorm-launch trunk")
     # fused tail (first conv + ONE persistent launch: scflow_ph_tail), twice (the second launch
     # reuses the sync words); its error word must stay clear
     src0, src1 = ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf)

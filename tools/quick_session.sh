@@ -19,6 +19,6 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run -- python3 $R/bench.py $B > /dev/null 2> $OUT/kt.err || exit $?
 DB=$(find $OUT/kt -name "*.db" | head -1)
 python3 $R/tools/prof_summary.py $DB 24 > $OUT/per_forward.txt
-python3 $R/tools/timeline.py $DB --iteration 60 > $OUT/timeline.txt 2>&1
+python3 $R/tools/timeline.py $DB --iteration 61 > $OUT/timeline.txt 2>&1
 rm -rf $OUT/kt
 head -16 $OUT/per_forward.txt; tail -1 $OUT/timeline.txt

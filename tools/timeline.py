@@ -1,10 +1,10 @@
 """Per-iteration kernel timeline from a rocprofv3 kernel-trace db (both streams).
 
-usage: python tools/timeline.py DB [--skip-forwards K] [--iteration I]
-Finds SCFlowDecoder iterations by the pose_flow / pose_step kernel (last launch of an iteration) and
-prints, for one iteration, every kernel: start offset, duration, stream, gap to the previous
-kernel on any stream; then the iteration's wall time, busy time (union of kernel intervals)
-and idle gaps.
+usage: python tools/timeline.py DB [--iteration I] [--marker NAME]
+Finds SCFlowDecoder iterations by a marker kernel that starts every iteration once (default the
+pyramid lookup) and prints, for one iteration (marker I to marker I+1), every kernel: start
+offset, duration, stream, gap to the previous kernel on any stream; then the iteration's wall
+time, busy time (union of kernel intervals) and idle gaps.
 """
 import argparse
 import re
@@ -21,12 +21,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--iteration", type=int, default=20, help="global index of the iteration")
+    ap.add_argument("--marker", default="corr_lookup", help="kernel-name substring starting an iteration")
     a = ap.parse_args()
     con = sqlite3.connect(a.db)
     rows = list(con.execute("select name, start, end, stream_id, queue_id from kernels order by start"))
-    ends = [i for i, r in enumerate(rows) if "pose_flow_kernel" in r[0] or "pose_step_kernel" in r[0]]
+    starts = [i for i, r in enumerate(rows) if a.marker in r[0]]
     it = a.iteration
-    lo, hi = ends[it - 1] + 1, ends[it] + 1
+    lo, hi = starts[it], starts[it + 1]
     seg = rows[lo:hi]
     t0 = seg[0][1]
     busy_end = t0
