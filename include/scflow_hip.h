@@ -535,16 +535,18 @@ int scflow_group_norm_backward(const float* dy, const float* x, const float* gam
  * c % 4 == 0, zr = the z | r conv's sigmoid output [npix][2c]:
  *   scflow_gru_gate_forward mode 0: out = r·h;  mode 1: out = h + z·(q − h)
  *   scflow_gru_gate_backward_q: dq = dh2·z·(1 − q²); dzr[:, :c] = dh2·(q − h)·z(1 − z);
- *                               dha = dh2·(1 − z)
- *   scflow_gru_gate_backward_r: dzr[:, c:] = drh·h·r(1 − r); dh = dha + drh·r (drh pixel stride sdrh) */
+ *                               dha = dh2·(1 − z)   (dh2 pixel stride sdh2 ≥ c)
+ *   scflow_gru_gate_backward_r: dzr[:, c:] = drh·h·r(1 − r); dh = dha + drh·r (drh / dh pixel
+ *                               strides sdrh / sdh ≥ c; dh may alias drh: each element is read
+ *                               before it is written, by the same thread) */
 int scflow_gru_gate_forward(const float* zr, const float* h, const float* q, float* out,
                             long long npix, int c, int mode, void* stream);
-int scflow_gru_gate_backward_q(const float* dh2, const float* zr, const float* h, const float* q,
-                               float* dq, float* dzr, float* dha, long long npix, int c,
-                               void* stream);
+int scflow_gru_gate_backward_q(const float* dh2, int sdh2, const float* zr, const float* h,
+                               const float* q, float* dq, float* dzr, float* dha, long long npix,
+                               int c, void* stream);
 int scflow_gru_gate_backward_r(const float* drh, int sdrh, const float* zr, const float* h,
-                               const float* dha, float* dzr, float* dh, long long npix, int c,
-                               void* stream);
+                               const float* dha, float* dzr, float* dh, int sdh, long long npix,
+                               int c, void* stream);
 /* scflow_col2im: the adjoint of scflow_im2col (same geometry; dx has pixel stride sdx ≥ cin):
  *   dx[n][iy][ix][c] = Σ_{ty,tx: (iy+ph−ty)/s, (ix+pw−tx)/s integral, inside} cols[(n,oy,ox)][(ty·kw+tx)·cin+c]
  * — a fixed-order gather, written (not accumulated).  With cols = dY·Wmat (Wmat[co][(ty·kw+tx)·cin+ci]

@@ -253,10 +253,10 @@ SIGNATURES = {
     "scflow_group_norm_backward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "scflow_gru_gate_forward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_int, c_vp]),
-    "scflow_gru_gate_backward_q": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,
-                                           c_int, c_vp]),
-    "scflow_gru_gate_backward_r": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,
-                                           c_int, c_vp]),
+    "scflow_gru_gate_backward_q": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_ll, c_int, c_vp]),
+    "scflow_gru_gate_backward_r": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int,
+                                           c_ll, c_int, c_vp]),
     "scflow_col2im": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_vp]),
     "scflow_corr_lookup_backward": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int,

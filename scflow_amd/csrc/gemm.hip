@@ -10,20 +10,24 @@
 //
 // Every operand is addressed through explicit (batch, row, column) element strides, so
 // transposes are free.  v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains).  The workgroup tile is
-// T×T (T = 128: 4 waves of 64×64, or T = 64: 4 waves of 32×32 for thin problems), K staged 16
-// deep through LDS with the next stage's global loads in flight during the MFMAs.  A tile is
+// T×T (T = 128: 4 waves of 64×64, or T = 64: 4 waves of 32×32 for thin problems), K staged GK
+// deep through LDS with the next stage's global loads in flight during the MFMAs.  A stage costs
+// about one global-load latency (≈1 µs) when its MFMAs are few, so the thin, latency-bound
+// products (under two rounds of workgroups: the FC layers, the deep-K weight gradients) take
+// 32-deep stages and splits of K that leave each workgroup a few of them; products with many
+// workgroups keep 16-deep stages (more workgroups resident to hide the latency).  A tile is
 // loaded as float4 along whichever of its dimensions has unit stride (template AV / BV: 0 =
 // along M / N, 1 = along K), element-wise with bounds checks at the edges or when unaligned.
 // Deep, narrow products (the 7×7 weight gradients: K = every output pixel, M·N one or two
-// tiles) split K over the grid into a caller-provided workspace, summed in split order by a
-// second launch (deterministic; no atomics).
+// tiles; the pose head's FC layers: M = 16 rows) split K over the grid into a caller-provided
+// workspace, summed in split order by a second launch (deterministic; no atomics).  The
+// epilogue reads every C element it accumulates onto (beta ≠ 0) before writing any: the reads
+// are independent of the stores, not a load→store chain per element.
 #include "common.h"
 
 #include <algorithm>
 
 namespace {
-
-constexpr int GK = 16;  // K per LDS stage
 
 struct GemmArgs {
   const float* A;
@@ -39,14 +43,16 @@ struct GemmArgs {
   float* ws;          // split > 1: raw partial sums [split][batch][M][N]; the epilogue is the reduce's
 };
 
+constexpr int gemm_nj(int T, int GK) { return GK * T / 1024; }  // float4 per thread per operand stage
+
 // one operand tile [GK][T] (k-major in LDS) from X[k][t] = X + t·st + k·sk; V = 0: float4 along t
 // (st == 1), V = 1: float4 along k (sk == 1)
-template <int T, int V>
+template <int T, int GK, int V>
 __device__ __forceinline__ void gemm_gload(const float* X, long long st, long long sk, int t0, int k0,
-                                           int T_lim, int K, bool vec, floatx4 (&r)[T / 64]) {
+                                           int T_lim, int K, bool vec, floatx4 (&r)[gemm_nj(T, GK)]) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int j = 0; j < T / 64; ++j) {
+  for (int j = 0; j < gemm_nj(T, GK); ++j) {
     const int idx = tid + 256 * j;
     int t, k;
     if (V == 0) {
@@ -71,11 +77,11 @@ __device__ __forceinline__ void gemm_gload(const float* X, long long st, long lo
   }
 }
 
-template <int T, int V>
-__device__ __forceinline__ void gemm_lstore(float (*S)[T + 4], const floatx4 (&r)[T / 64]) {
+template <int T, int GK, int V>
+__device__ __forceinline__ void gemm_lstore(float (*S)[T + 4], const floatx4 (&r)[gemm_nj(T, GK)]) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int j = 0; j < T / 64; ++j) {
+  for (int j = 0; j < gemm_nj(T, GK); ++j) {
     const int idx = tid + 256 * j;
     if (V == 0) {
       *(floatx4*)&S[idx / (T / 4)][(idx % (T / 4)) * 4] = r[j];
@@ -87,7 +93,7 @@ __device__ __forceinline__ void gemm_lstore(float (*S)[T + 4], const floatx4 (&r
   }
 }
 
-template <int T, int AV, int BV>
+template <int T, int GK, int AV, int BV>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   constexpr int WT = T / 2;       // wave tile (2×2 waves)
   constexpr int NB = WT / 32;     // 32×32 MFMA blocks per wave dimension
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
   const float* A = g.A + (size_t)b * g.sab + (size_t)kbeg * g.sak;
   const float* B = g.B + (size_t)b * g.sbb + (size_t)kbeg * g.sbk;
   // A as [k][m]: element (m, k) at m·sam + k·sak;  B as [k][n]: (k, n) at n·sbn + k·sbk
-  floatx4 ra[T / 64], rb[T / 64];
+  floatx4 ra[gemm_nj(T, GK)], rb[gemm_nj(T, GK)];
   floatx16 acc[NB][NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i)
@@ -111,16 +117,16 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  gemm_gload<T, AV>(A, g.sam, g.sak, m0, 0, g.M, K, g.vec_a, ra);
-  gemm_gload<T, BV>(B, g.sbn, g.sbk, n0, 0, g.N, K, g.vec_b, rb);
+  gemm_gload<T, GK, AV>(A, g.sam, g.sak, m0, 0, g.M, K, g.vec_a, ra);
+  gemm_gload<T, GK, BV>(B, g.sbn, g.sbk, n0, 0, g.N, K, g.vec_b, rb);
   for (int k0 = 0; k0 < K; k0 += GK) {
     __syncthreads();
-    gemm_lstore<T, AV>(As, ra);
-    gemm_lstore<T, BV>(Bs, rb);
+    gemm_lstore<T, GK, AV>(As, ra);
+    gemm_lstore<T, GK, BV>(Bs, rb);
     __syncthreads();
     if (k0 + GK < K) {
-      gemm_gload<T, AV>(A, g.sam, g.sak, m0, k0 + GK, g.M, K, g.vec_a, ra);
-      gemm_gload<T, BV>(B, g.sbn, g.sbk, n0, k0 + GK, g.N, K, g.vec_b, rb);
+      gemm_gload<T, GK, AV>(A, g.sam, g.sak, m0, k0 + GK, g.M, K, g.vec_a, ra);
+      gemm_gload<T, GK, BV>(B, g.sbn, g.sbk, n0, k0 + GK, g.N, K, g.vec_b, rb);
     }
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 2) {
@@ -160,57 +166,73 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int n = n0 + wn * WT + j * 32 + li;
-      if (n >= g.N) continue;
-      const float bn = g.bias_mode == 1 ? g.bias[n] : 0.f;
+      const bool nok = n < g.N;
+      const float bn = g.bias_mode == 1 && nok ? g.bias[n] : 0.f;
+      float old[16];
+      if (g.beta != 0.f) {  // every read first (independent loads in flight together)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * WT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          old[r] = nok && m < g.M ? C[(size_t)m * g.scm + (size_t)n * g.scn] : 0.f;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (m >= g.M) continue;
+        if (!nok || m >= g.M) continue;
         float v = g.alpha * acc[i][j][r] + bn;
         if (g.bias_mode == 2) v += g.bias[m];
-        float* c = C + (size_t)m * g.scm + (size_t)n * g.scn;
-        if (g.beta != 0.f) v += g.beta * *c;
-        *c = v;
+        if (g.beta != 0.f) v += g.beta * old[r];
+        C[(size_t)m * g.scm + (size_t)n * g.scn] = v;
       }
     }
 }
 
-// C = alpha·Σ_split ws + beta·C + bias, splits summed in order (deterministic)
+// C = alpha·Σ_split ws + beta·C + bias.  Block = 64 outputs × 4 split lanes: lane group q sums
+// the splits ≡ q (mod 4) in order (unrolled: independent loads in flight), then the four partial
+// sums are added in a fixed order through LDS (deterministic).
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmArgs g, int splits) {
+  __shared__ float part[4][64];
   const long long total = (long long)g.batch * g.M * g.N;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int n = (int)(i % g.N);
-    const int m = (int)((i / g.N) % g.M);
-    const int b = (int)(i / ((long long)g.N * g.M));
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += g.ws[(size_t)k * total + i];
-    float v = g.alpha * s;
-    if (g.bias_mode == 1) v += g.bias[n];
-    if (g.bias_mode == 2) v += g.bias[m];
-    float* c = g.C + (size_t)b * g.scb + (size_t)m * g.scm + (size_t)n * g.scn;
-    if (g.beta != 0.f) v += g.beta * *c;
-    *c = v;
+  const int o = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const long long i = blockIdx.x * 64LL + o;
+  float s = 0.f;
+  if (i < total) {
+#pragma unroll 8
+    for (int k = q; k < splits; k += 4) s += g.ws[(size_t)k * total + i];
   }
+  part[q][o] = s;
+  __syncthreads();
+  if (q != 0 || i >= total) return;
+  s = (part[0][o] + part[1][o]) + (part[2][o] + part[3][o]);
+  const int n = (int)(i % g.N);
+  const int m = (int)((i / g.N) % g.M);
+  const int b = (int)(i / ((long long)g.N * g.M));
+  float v = g.alpha * s;
+  if (g.bias_mode == 1) v += g.bias[n];
+  if (g.bias_mode == 2) v += g.bias[m];
+  float* c = g.C + (size_t)b * g.scb + (size_t)m * g.scm + (size_t)n * g.scn;
+  if (g.beta != 0.f) v += g.beta * *c;
+  *c = v;
 }
 
-template <int T, int AV, int BV>
+template <int T, int GK, int AV, int BV>
 int gemm_launch(const GemmArgs& g, int splits, hipStream_t st) {
   dim3 grid(ceil_div(g.N, T), ceil_div(g.M, T), g.batch * splits);
-  gemm_f32_kernel<T, AV, BV><<<grid, 256, 0, st>>>(g);
+  gemm_f32_kernel<T, GK, AV, BV><<<grid, 256, 0, st>>>(g);
   int s = scflow_launch_status();
   if (s || splits == 1) return s;
   const long long total = (long long)g.batch * g.M * g.N;
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 4LL * device_cus());
-  gemm_reduce_kernel<<<blocks, 256, 0, st>>>(g, splits);
+  gemm_reduce_kernel<<<(unsigned)((total + 63) / 64), 256, 0, st>>>(g, splits);
   return scflow_launch_status();
 }
 
-template <int T>
+template <int T, int GK>
 int gemm_dispatch(const GemmArgs& g, int av, int bv, int splits, hipStream_t st) {
-  if (av == 0 && bv == 0) return gemm_launch<T, 0, 0>(g, splits, st);
-  if (av == 0 && bv == 1) return gemm_launch<T, 0, 1>(g, splits, st);
-  if (av == 1 && bv == 0) return gemm_launch<T, 1, 0>(g, splits, st);
-  return gemm_launch<T, 1, 1>(g, splits, st);
+  if (av == 0 && bv == 0) return gemm_launch<T, GK, 0, 0>(g, splits, st);
+  if (av == 0 && bv == 1) return gemm_launch<T, GK, 0, 1>(g, splits, st);
+  if (av == 1 && bv == 0) return gemm_launch<T, GK, 1, 0>(g, splits, st);
+  return gemm_launch<T, GK, 1, 1>(g, splits, st);
 }
 
 // workgroup tile: 128 when that still gives a full round of workgroups, else 64
@@ -219,15 +241,24 @@ int gemm_tile(int M, int N, int batch) {
   return (M >= 128 && N >= 128 && t128 >= device_cus()) ? 128 : 64;
 }
 
+// stage depth: 32 for the latency-bound thin products (under two rounds of workgroups before
+// any K split), 16 otherwise
+int gemm_gk(int M, int N, int batch) {
+  const int T = gemm_tile(M, N, batch);
+  const long long tiles = (long long)ceil_div(M, T) * ceil_div(N, T) * batch;
+  return tiles < 2LL * device_cus() ? 32 : 16;
+}
+
 }  // namespace
 
 SCFLOW_API int scflow_gemm_f32_splits(int batch, int M, int N, int K) {
   if (batch <= 0 || M <= 0 || N <= 0 || K <= 0) return SCFLOW_EINVAL;
   const int T = gemm_tile(M, N, batch);
   const long long tiles = (long long)ceil_div(M, T) * ceil_div(N, T) * batch;
-  // split K while a round of the chip is not covered and every split keeps ≥ 16 stages
+  // split K up to four workgroups per CU while every split keeps ≥ 4 stages of 32 (each stage
+  // is about one load latency: few deep splits were latency-bound); at most 256 splits
   long long s = 1;
-  while (tiles * s * 2 <= 2LL * device_cus() && K / (s * 2) >= 16 * GK && s < 64) s *= 2;
+  while (tiles * s * 2 <= 4LL * device_cus() && K / (s * 2) >= 4 * 32 && s < 256) s *= 2;
   return (int)s;
 }
 
@@ -240,7 +271,8 @@ SCFLOW_API int scflow_gemm_f32(const float* A, const float* B, float* C, const f
       (bias_mode && !bias) || splits < 1 || (splits > 1 && !workspace) ||
       (long long)batch * splits > 65535 || ceil_div(M, 64) > 65535)
     return SCFLOW_EINVAL;
-  const int kchunk = ceil_div(ceil_div(K, splits), GK) * GK;
+  const int gk = gemm_gk(M, N, batch);
+  const int kchunk = ceil_div(ceil_div(K, splits), gk) * gk;
   splits = ceil_div(K, kchunk);  // no empty split
   GemmArgs g{A, B, C, bias, M, N, K, sab, sam, sak, sbb, sbk, sbn, scb, scm, scn, alpha, beta, bias_mode,
              0, 0, batch, kchunk, splits > 1 ? workspace : nullptr};
@@ -252,6 +284,9 @@ SCFLOW_API int scflow_gemm_f32(const float* A, const float* B, float* C, const f
   g.vec_a = a_unit && aligned16(A) && a_outer % 4 == 0 && (batch == 1 || sab % 4 == 0);
   g.vec_b = b_unit && aligned16(B) && b_outer % 4 == 0 && (batch == 1 || sbb % 4 == 0);
   hipStream_t st = (hipStream_t)stream;
-  if (gemm_tile(M, N, batch) == 128) return gemm_dispatch<128>(g, av, bv, splits, st);
-  return gemm_dispatch<64>(g, av, bv, splits, st);
+  if (gemm_tile(M, N, batch) == 128)
+    return gk == 32 ? gemm_dispatch<128, 32>(g, av, bv, splits, st)
+                    : gemm_dispatch<128, 16>(g, av, bv, splits, st);
+  return gk == 32 ? gemm_dispatch<64, 32>(g, av, bv, splits, st)
+                  : gemm_dispatch<64, 16>(g, av, bv, splits, st);
 }

@@ -14,8 +14,8 @@
 //
 // Three launches:
 //   render_project_kernel — one thread per packed vertex: NDC + depth into the per-image vertex
-//     slots, and the image's minimum vertex depth (atomicMin on the float bits; depths > 0) for
-//     the light placement.
+//     slots, and the image's minimum vertex depth (a wave-level min per image, then one atomicMin
+//     on the float bits per image and wave; depths > 0) for the light placement.
 //   render_raster_kernel  — one thread per packed face: every pixel centre of its screen bbox is
 //     tested; hits do a 64-bit atomicMin of (depth bits << 32 | face) into the image's z-buffer
 //     (positive floats order like their bit patterns), so the nearest face wins and equal depths
@@ -34,22 +34,40 @@ __global__ void render_project_kernel(scflow_render_args a, const int* __restric
                                       float* __restrict__ vproj, unsigned* __restrict__ zmin_bits,
                                       int nverts) {
   const int vi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (vi >= nverts) return;
-  const int n = vert_img[vi];
-  const float* R = a.R + 9 * n;
-  const float* t = a.t + 3 * n;
-  const float* K = a.K + 9 * n;
-  const float x = a.verts[3 * vi], y = a.verts[3 * vi + 1], z = a.verts[3 * vi + 2];
-  const float X = R[0] * x + R[1] * y + R[2] * z + t[0];
-  const float Y = R[3] * x + R[4] * y + R[5] * z + t[1];
-  const float Z = R[6] * x + R[7] * y + R[8] * z + t[2];
-  const float u = K[0] * X / Z + K[2];
-  const float v = K[4] * Y / Z + K[5];
-  const float c0 = 0.5f * (float)(a.size - 1);
-  vproj[3 * vi] = -(u - c0) / c0;
-  vproj[3 * vi + 1] = -(v - c0) / c0;
-  vproj[3 * vi + 2] = Z;
-  if (Z > 0.f) atomicMin(zmin_bits + n, __float_as_uint(Z));
+  const bool valid = vi < nverts;
+  int n = -1;
+  unsigned key = 0xFFFFFFFFu;  // this vertex's depth bits (positive floats order like their bits)
+  if (valid) {
+    n = vert_img[vi];
+    const float* R = a.R + 9 * n;
+    const float* t = a.t + 3 * n;
+    const float* K = a.K + 9 * n;
+    const float x = a.verts[3 * vi], y = a.verts[3 * vi + 1], z = a.verts[3 * vi + 2];
+    const float X = R[0] * x + R[1] * y + R[2] * z + t[0];
+    const float Y = R[3] * x + R[4] * y + R[5] * z + t[1];
+    const float Z = R[6] * x + R[7] * y + R[8] * z + t[2];
+    const float u = K[0] * X / Z + K[2];
+    const float v = K[4] * Y / Z + K[5];
+    const float c0 = 0.5f * (float)(a.size - 1);
+    vproj[3 * vi] = -(u - c0) / c0;
+    vproj[3 * vi + 1] = -(v - c0) / c0;
+    vproj[3 * vi + 2] = Z;
+    if (Z > 0.f) key = __float_as_uint(Z);
+  }
+  // per-image minimum: the wave's lanes of one image (vertices are packed image by image, so a
+  // wave spans one or two) reduce their depths first, then one atomicMin per image and wave
+  const int lane = threadIdx.x & 63;
+  unsigned long long pending = __ballot(valid);
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const int ln = __shfl(n, leader);
+    const bool mine = valid && n == ln;
+    unsigned m = mine ? key : 0xFFFFFFFFu;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, off));
+    if (lane == leader && m != 0xFFFFFFFFu) atomicMin(zmin_bits + ln, m);
+    pending &= ~__ballot(mine);
+  }
 }
 
 struct Bary {

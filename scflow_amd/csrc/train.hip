@@ -1031,7 +1031,7 @@ __global__ void gru_fwd_kernel(const float* __restrict__ zr, const float* __rest
   }
 }
 
-__global__ void gru_bwd_q_kernel(const float* __restrict__ dh2, const float* __restrict__ zr,
+__global__ void gru_bwd_q_kernel(const float* __restrict__ dh2, int sdh2, const float* __restrict__ zr,
                                  const float* __restrict__ h, const float* __restrict__ q,
                                  float* __restrict__ dq, float* __restrict__ dzr,
                                  float* __restrict__ dha, int c, long long total4) {
@@ -1039,7 +1039,7 @@ __global__ void gru_bwd_q_kernel(const float* __restrict__ dh2, const float* __r
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
     const long long p = i / c4;
     const int cq = (int)(i % c4) * 4;
-    const floatx4 g = *(const floatx4*)(dh2 + p * c + cq);
+    const floatx4 g = *(const floatx4*)(dh2 + p * sdh2 + cq);
     const floatx4 zv = *(const floatx4*)(zr + p * 2 * c + cq);
     const floatx4 hv = *(const floatx4*)(h + p * c + cq);
     const floatx4 qv = *(const floatx4*)(q + p * c + cq);
@@ -1056,10 +1056,11 @@ __global__ void gru_bwd_q_kernel(const float* __restrict__ dh2, const float* __r
   }
 }
 
-__global__ void gru_bwd_r_kernel(const float* __restrict__ drh, int sdrh,
-                                 const float* __restrict__ zr, const float* __restrict__ h,
-                                 const float* __restrict__ dha, float* __restrict__ dzr,
-                                 float* __restrict__ dh, int c, long long total4) {
+// dh may alias drh (the dX buffer's h channels, overwritten in place): no __restrict__ on those two
+__global__ void gru_bwd_r_kernel(const float* drh, int sdrh, const float* __restrict__ zr,
+                                 const float* __restrict__ h, const float* __restrict__ dha,
+                                 float* __restrict__ dzr, float* dh, int sdh, int c,
+                                 long long total4) {
   const int c4 = c / 4;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
     const long long p = i / c4;
@@ -1075,7 +1076,7 @@ __global__ void gru_bwd_r_kernel(const float* __restrict__ drh, int sdrh,
       b[e] = av[e] + g[e] * rv[e];
     }
     *(floatx4*)(dzr + p * 2 * c + c + cq) = a;
-    *(floatx4*)(dh + p * c + cq) = b;
+    *(floatx4*)(dh + p * sdh + cq) = b;
   }
 }
 
@@ -1604,27 +1605,30 @@ SCFLOW_API int scflow_gru_gate_forward(const float* zr, const float* h, const fl
   return scflow_launch_status();
 }
 
-SCFLOW_API int scflow_gru_gate_backward_q(const float* dh2, const float* zr, const float* h,
-                                          const float* q, float* dq, float* dzr, float* dha,
-                                          long long npix, int c, void* stream) {
+SCFLOW_API int scflow_gru_gate_backward_q(const float* dh2, int sdh2, const float* zr,
+                                          const float* h, const float* q, float* dq, float* dzr,
+                                          float* dha, long long npix, int c, void* stream) {
   if (!dh2 || !zr || !h || !q || !dq || !dzr || !dha || npix <= 0 || c <= 0 || (c & 3) ||
+      sdh2 < c || (sdh2 & 3) ||
       !aligned16(dh2) || !aligned16(zr) || !aligned16(h) || !aligned16(q) || !aligned16(dq) ||
       !aligned16(dzr) || !aligned16(dha))
     return SCFLOW_EINVAL;
   const long long t4 = npix * c / 4;
-  gru_bwd_q_kernel<<<gru_grid(t4), 256, 0, (hipStream_t)stream>>>(dh2, zr, h, q, dq, dzr, dha, c, t4);
+  gru_bwd_q_kernel<<<gru_grid(t4), 256, 0, (hipStream_t)stream>>>(dh2, sdh2, zr, h, q, dq, dzr, dha,
+                                                                  c, t4);
   return scflow_launch_status();
 }
 
 SCFLOW_API int scflow_gru_gate_backward_r(const float* drh, int sdrh, const float* zr,
                                           const float* h, const float* dha, float* dzr, float* dh,
-                                          long long npix, int c, void* stream) {
+                                          int sdh, long long npix, int c, void* stream) {
   if (!drh || !zr || !h || !dha || !dzr || !dh || npix <= 0 || c <= 0 || (c & 3) || sdrh < c ||
-      (sdrh & 3) || !aligned16(drh) || !aligned16(zr) || !aligned16(h) || !aligned16(dha) ||
+      (sdrh & 3) || sdh < c || (sdh & 3) || !aligned16(drh) || !aligned16(zr) || !aligned16(h) || !aligned16(dha) ||
       !aligned16(dzr) || !aligned16(dh))
     return SCFLOW_EINVAL;
   const long long t4 = npix * c / 4;
-  gru_bwd_r_kernel<<<gru_grid(t4), 256, 0, (hipStream_t)stream>>>(drh, sdrh, zr, h, dha, dzr, dh, c, t4);
+  gru_bwd_r_kernel<<<gru_grid(t4), 256, 0, (hipStream_t)stream>>>(drh, sdrh, zr, h, dha, dzr, dh,
+                                                                  sdh, c, t4);
   return scflow_launch_status();
 }
 

@@ -111,6 +111,18 @@ def _require(t: Tensor, name: str, dtype=torch.float32, contiguous=True) -> None
         raise ValueError(f"{name} must be contiguous")
 
 
+def _require_rows(t: Tensor, name: str) -> None:
+    """``t`` [..., c] is a channel slice of a channels-last buffer: unit channel stride and one
+    pixel stride (``t.stride(-2)``, a multiple of 4) over all leading dimensions."""
+    _require(t, name, contiguous=False)
+    ok = t.stride(-1) == 1 and t.stride(-2) >= t.shape[-1] and t.stride(-2) % 4 == 0
+    for i in range(t.dim() - 3, -1, -1):
+        ok = ok and (t.shape[i] == 1 or t.stride(i) == t.stride(i + 1) * t.shape[i + 1])
+    if not ok:
+        raise ValueError(f"{name} must be channels-last rows with one pixel stride, got strides "
+                         f"{tuple(t.stride())} for shape {tuple(t.shape)}")
+
+
 def _p(t: Optional[Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -1008,24 +1020,27 @@ def gru_gate_forward(zr: Tensor, h: Tensor, out: Tensor, q: Optional[Tensor] = N
 
 def gru_gate_backward_q(dh2: Tensor, zr: Tensor, h: Tensor, q: Tensor, dq: Tensor, dzr: Tensor,
                         dha: Tensor) -> None:
-    """dq = dh2·z·(1 − q²), dzr[..., :c] = dh2·(q − h)·z(1 − z), dha = dh2·(1 − z)."""
-    for nm, t in (("dh2", dh2), ("zr", zr), ("h", h), ("q", q), ("dq", dq), ("dzr", dzr), ("dha", dha)):
+    """dq = dh2·z·(1 − q²), dzr[..., :c] = dh2·(q − h)·z(1 − z), dha = dh2·(1 − z); dh2 may be
+    a channel slice (pixel stride ≥ c)."""
+    for nm, t in (("zr", zr), ("h", h), ("q", q), ("dq", dq), ("dzr", dzr), ("dha", dha)):
         _require(t, nm)
+    _require_rows(dh2, "dh2")
     c = h.shape[-1]
-    _launch("scflow_gru_gate_backward_q", h, _p(dh2), _p(zr), _p(h), _p(q), _p(dq), _p(dzr), _p(dha),
-            h.numel() // c, c)
+    _launch("scflow_gru_gate_backward_q", h, _p(dh2), dh2.stride(-2), _p(zr), _p(h), _p(q), _p(dq),
+            _p(dzr), _p(dha), h.numel() // c, c)
 
 
 def gru_gate_backward_r(drh: Tensor, zr: Tensor, h: Tensor, dha: Tensor, dzr: Tensor,
                         dh: Tensor) -> None:
-    """dzr[..., c:] = drh·h·r(1 − r), dh = dha + drh·r; drh may be a channel slice (pixel stride
-    ≥ c)."""
-    for nm, t in (("zr", zr), ("h", h), ("dha", dha), ("dzr", dzr), ("dh", dh)):
+    """dzr[..., c:] = drh·h·r(1 − r), dh = dha + drh·r; drh and dh may be channel slices (pixel
+    stride ≥ c), and dh may be drh itself (overwritten in place)."""
+    for nm, t in (("zr", zr), ("h", h), ("dha", dha), ("dzr", dzr)):
         _require(t, nm)
-    _require(drh, "drh", contiguous=False)
+    _require_rows(drh, "drh")
+    _require_rows(dh, "dh")
     c = h.shape[-1]
     _launch("scflow_gru_gate_backward_r", h, _p(drh), drh.stride(-2), _p(zr), _p(h), _p(dha),
-            _p(dzr), _p(dh), h.numel() // c, c)
+            _p(dzr), _p(dh), dh.stride(-2), h.numel() // c, c)
 
 
 def col2im(cols: Tensor, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, ph: int,

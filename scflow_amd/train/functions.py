@@ -387,6 +387,14 @@ def _shared_wgrad(holder: dict, w: Tensor, add) -> Optional[Tensor]:
     return buf if first else None
 
 
+def _channel_rows(t: Tensor) -> bool:
+    """``t`` [..., c] is a channel slice of a channels-last buffer (one pixel stride)."""
+    if t.stride(-1) != 1 or t.stride(-2) < t.shape[-1] or t.stride(-2) % 4:
+        return False
+    return all(t.shape[i] == 1 or t.stride(i) == t.stride(i + 1) * t.shape[i + 1]
+               for i in range(t.dim() - 2))
+
+
 class _GruStep(torch.autograd.Function):
     """One SepConvGRU direction (raft_decoder.py:235-253) as one autograd node:
         zr = σ(conv([h, x]; w_zr) + pre_zr)      (z | r from one launch)
@@ -394,7 +402,7 @@ class _GruStep(torch.autograd.Function):
         h' = h + z·(q − h)
     forward: the two HIP convs (activation and the hoisted context map fused) and two HIP gate
     kernels; backward: the gate / activation derivatives in two HIP kernels, the two convs' dX
-    and dW, and one add each for dh and dx — instead of ~17 separate autograd kernels
+    (the second adds the first's in its epilogue) and dW — instead of ~17 separate autograd kernels
     (lerp, mul, the activation backwards, slice concatenation, gradient accumulation)."""
 
     @staticmethod
@@ -421,16 +429,18 @@ class _GruStep(torch.autograd.Function):
         dq = torch.empty_like(h)
         dzr = torch.empty_like(zr)
         dha = torch.empty_like(h)
-        ops.gru_gate_backward_q(dh2.contiguous(), zr, h, q, dq, dzr, dha)
+        if not _channel_rows(dh2):
+            dh2 = dh2.contiguous()
+        ops.gru_gate_backward_q(dh2, zr, h, q, dq, dzr, dha)
         dxq = _conv_forward(dq, None, _flip_t(w_q), None, 1, (kh - 1 - ph, kw - 1 - pw))
         dw_q = _shared_wgrad(ctx.acc[1], w_q, lambda buf: _weight_grad(dq, rh, x, w_q, 1, ph, pw, False, dw=buf))
-        dh = torch.empty_like(h)
-        ops.gru_gate_backward_r(dxq[..., :c], zr, h, dha, dzr, dh)
-        dxz = _conv_forward(dzr, None, _flip_t(w_zr), None, 1, (kh - 1 - ph, kw - 1 - pw))
+        # dh = dha + drh·r written over drh = dxq[..., :c] itself, so that dxq becomes [dh | dx_q]
+        # and the z | r conv's dX, with dxq as its added map, yields both sums in its epilogue:
+        # T = [dh + dxz_h | dx_q + dxz_x] (no separate adds; dh and dx leave as channel views)
+        ops.gru_gate_backward_r(dxq[..., :c], zr, h, dha, dzr, dxq[..., :c])
+        t = _conv_forward(dzr, None, _flip_t(w_zr), None, 1, (kh - 1 - ph, kw - 1 - pw), bias_map=dxq)
         dw_zr = _shared_wgrad(ctx.acc[0], w_zr, lambda buf: _weight_grad(dzr, h, x, w_zr, 1, ph, pw, False, dw=buf))
-        dh += dxz[..., :c]
-        dx = dxq[..., c:] + dxz[..., c:]
-        return dh, dx, dw_zr, dw_q, dzr, dq, None
+        return t[..., :c], t[..., c:], dw_zr, dw_q, dzr, dq, None
 
 
 def gru_step(h: Tensor, x: Tensor, w_zr: Tensor, w_q: Tensor, pre_zr: Tensor, pre_q: Tensor,

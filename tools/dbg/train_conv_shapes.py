@@ -56,7 +56,18 @@ def main():
         oh, ow = (h + 2 * pad[0] - kh) // stride + 1, (wd + 2 * pad[1] - kw) // stride + 1
         return ((n, h, wd, cin, cout, kh, kw, stride), 2.0 * n * oh * ow * cout * cin * kh * kw)
 
+    def gemm_flops(a_, b_, out=None, alpha=1.0, beta=0.0, bias=None, bias_dim="n"):
+        bt = a_.shape[0] if a_.dim() == 3 else 1
+        m, k = a_.shape[-2:]
+        nn = b_.shape[-1]
+        # caller: the innermost frame outside ops.py (which Function's forward / backward)
+        import inspect
+        fr = inspect.currentframe().f_back.f_back
+        tag = f"{os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
+        return ((bt, m, nn, k, tag, 0, 0, 0), 2.0 * bt * m * nn * k)
+
     ops.conv_wgrad = wrap("wgrad", ops.conv_wgrad, wg_flops)
+    ops.gemm = wrap("gemm", ops.gemm, gemm_flops)
     functions._conv_forward = wrap("conv", functions._conv_forward, fw_flops)
 
     dev = torch.device("cuda", 0)
@@ -82,6 +93,10 @@ def main():
     print(f"conv + wgrad launches of one step: {len(rec)} calls, {tot / 1e3:.2f} ms (host-timed events)")
     print(" op     n   h   w  cin cout kh kw s | calls   total_us  avg_us  GFLOP/call  TF/s")
     for k, (c, us, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        if k[0] == "gemm":  # (batch, M, N, K, caller)
+            print(f" gemm  bt={k[1]} M={k[2]} N={k[3]} K={k[4]} {k[5]} | {c:5d} {us:10.1f} {us / c:7.1f}"
+                  f" {fl / c / 1e9:10.3f} {fl / us / 1e6:6.1f}")
+            continue
         print(f" {k[0]:5s} {k[1]:3d} {k[2]:3d} {k[3]:3d} {k[4]:4d} {k[5]:4d} {k[6]:2d} {k[7]:2d} {k[8]:1d} |"
               f" {c:5d} {us:10.1f} {us / c:7.1f} {fl / c / 1e9:10.3f} {fl / us / 1e6:6.1f}")
 
