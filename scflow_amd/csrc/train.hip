@@ -605,6 +605,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
 }
 
 #include "wgrad_wino.h"
+#include "wgrad_wino5.h"
 
 bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   if (a.stride != 1 && a.stride != 2) return false;
@@ -1644,6 +1645,11 @@ SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long l
     *floats = wwino_workspace(R);
     return SCFLOW_OK;
   }
+  W5wParams R5;
+  if (wwino5_geometry(*args, &R5)) {
+    *floats = wwino5_workspace(R5);
+    return SCFLOW_OK;
+  }
   WgParams P;
   int splits = 0;
   if (!wgrad_geometry(*args, &P, &splits)) return SCFLOW_EUNSUPPORTED;
@@ -1668,6 +1674,11 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
   if (wwino_geometry(a, &R)) {
     if (a.workspace_floats < wwino_workspace(R)) return SCFLOW_EINVAL;
     return wwino_launch(R, (hipStream_t)stream);
+  }
+  W5wParams R5;
+  if (wwino5_geometry(a, &R5)) {
+    if (a.workspace_floats < wwino5_workspace(R5)) return SCFLOW_EINVAL;
+    return wwino5_launch(R5, (hipStream_t)stream);
   }
   WgParams P;
   int splits = 0;

@@ -35,6 +35,22 @@ constexpr int WW_NT = 512;        // threads
 constexpr int WW_ND = 4 * 32 * (WWCO / 4) / WW_NT;                // dY float4 per thread (2)
 constexpr int WW_NX = (6 * 34 * (WWCI / 4) + WW_NT - 1) / WW_NT;  // halo float4 per thread (7)
 
+// XCD-aware (tile, split) of this workgroup on a grid of (tiles, splits): workgroups are dispatched
+// round-robin over the 8 XCDs by linear id, so the ids are re-assigned such that all tiles of a
+// split (which read the same dY / input chunks) run on one XCD and share its L2 — instead of
+// every XCD fetching every chunk from HBM / MALL.  Identity when splits is not a multiple of 8.
+__device__ __forceinline__ void wgrad_xcd_map(int tiles, int splits, int* tile, int* split) {
+  if (splits % 8 == 0) {
+    const int L = blockIdx.x + gridDim.x * blockIdx.y;
+    const int xcd = L & 7, k = L >> 3;
+    *split = (k / tiles) * 8 + xcd;
+    *tile = k % tiles;
+  } else {
+    *tile = blockIdx.x;
+    *split = blockIdx.y;
+  }
+}
+
 struct WwParams {
   scflow_wgrad_args a;
   int cg, rg, nchunks, cps, co_tiles, copad, cinp;
@@ -55,10 +71,12 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wave = wv & 3, ks = wv >> 2;  // Winograd row i, k-step set
   const int li = lane & 31, hh = lane >> 5;
-  const int co_t = blockIdx.x % P.co_tiles, ci_t = blockIdx.x / P.co_tiles;
+  int tile, split;
+  wgrad_xcd_map(gridDim.x, gridDim.y, &tile, &split);
+  const int co_t = tile % P.co_tiles, ci_t = tile / P.co_tiles;
   const int co0 = co_t * WWCO, ci0 = ci_t * WWCI;
   const int cin = a.cin0 + a.cin1;
-  const int c_begin = blockIdx.y * P.cps;
+  const int c_begin = split * P.cps;
   const int c_end = min(P.nchunks, c_begin + P.cps);
   const bool do_bias = bslab != nullptr && ci_t == 0;
 
@@ -218,7 +236,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
     }
   // partial slab [split][ξ = 4i + j][copad][cinp]; C/D layout: col = lane&31, row = (r&3)+8(r>>2)+4hh
   const size_t plane = (size_t)P.copad * P.cinp;
-  float* sl = slab + (size_t)blockIdx.y * 16 * plane;
+  float* sl = slab + (size_t)split * 16 * plane;
   if (ks == 0)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -239,7 +257,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       float b = 0.f;
 #pragma unroll
       for (int g = 0; g < WW_NT / 32; ++g) b += smem[tid + 32 * g];
-      bslab[(size_t)blockIdx.y * P.copad + co0 + tid] = b;
+      bslab[(size_t)split * P.copad + co0 + tid] = b;
     }
   }
 }

@@ -160,6 +160,44 @@ def test_conv_wgrad_thin(case):
     _close(db - 1, dy.double().sum((0, 1, 2)), 1e-5, 1e-4 * np.sqrt(n * oh * ow), "db")
 
 
+@pytest.mark.parametrize("case", [
+    # (n, h, w, c0, c1, cout, kh, kw, bias)
+    (4, 32, 32, 128, 128, 256, 1, 5, False),   # GRU z | r 1×5 (h ⊕ motion), configs' width
+    (4, 32, 32, 128, 128, 128, 5, 1, False),   # GRU q 5×1
+    (3, 32, 32, 128, 0, 256, 1, 5, True),      # the hoisted context part (bias)
+    (2, 64, 36, 64, 32, 96, 5, 1, True),       # ragged cout / cin blocks, two column chunks
+    (2, 8, 64, 64, 32, 96, 1, 5, False),
+])
+def test_conv_wgrad_wino5(case):
+    """The Winograd F(4, 5) weight gradient of the GRU's 1×5 / 5×1 convs (wgrad_wino5.h) vs an
+    fp64 reference, accumulate = 1 onto dw / db, a Chan slice as the second source.  Tolerance:
+    the transform-domain sums carry Winograd's larger fp32 rounding (points up to ±8 / ±5.25 in
+    A / Bᵀ), bounded here at 2e-5 of the gradient's magnitude."""
+    from scflow_amd import ops
+    from scflow_amd.ops import Chan
+    n, h, w, c0, c1, cout, kh, kw, bias = case
+    g = torch.Generator().manual_seed(sum(case))
+    ph, pw = kh // 2, kw // 2
+    x0 = torch.randn(n, h, w, c0, generator=g)
+    buf = torch.randn(n, h, w, c1 + 8, generator=g)
+    x1 = buf[..., 4:4 + c1]
+    dy = torch.randn(n, h, w, cout, generator=g)
+    xc = torch.cat([x0, x1], -1) if c1 else x0
+    ref = torch.nn.grad.conv2d_weight(xc.permute(0, 3, 1, 2).double(), (cout, c0 + c1, kh, kw),
+                                      dy.permute(0, 3, 1, 2).double(), padding=(ph, pw))
+    dw = torch.ones(cout, c0 + c1, kh, kw).cuda()
+    db = torch.ones(cout).cuda() if bias else None
+    src1 = Chan(buf.cuda().view(-1, c1 + 8), 4, c1) if c1 else None
+    ops.conv_wgrad(dy.cuda().view(-1, cout), x0.cuda(), src1, dw, db, n, h, w, kh, kw, 1, ph, pw,
+                   accumulate=True)
+    torch.cuda.synchronize()
+    err = float(((dw - 1).cpu().double() - ref).abs().max() / ref.abs().max())
+    print(f"wino5 wgrad {case}: max error / max |dW| = {err:.2e}")
+    _close(dw - 1, ref, 2e-5, 0.0, "dw")
+    if bias:
+        _close(db - 1, dy.double().sum((0, 1, 2)), 1e-5, 1e-4 * np.sqrt(n * h * w), "db")
+
+
 def test_corr_pyramid_backward():
     from scflow_amd import ops
     from scflow_amd.train.functions import corr_pyramid
