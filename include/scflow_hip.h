@@ -608,6 +608,15 @@ int scflow_gemm_f32(const float* A, const float* B, float* C, const float* bias,
                     void* stream);
 int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats);
 int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream);
+/* scflow_conv_wgrad_batched: the weight (and bias) gradient summed over `segs` (1..8) equally
+ * shaped segments in one launch and one split reduction — the decoder's per-iteration uses of
+ * one conv (its 8 refinement iterations under SCFlowRefiner.loss → backward,
+ * scflow_refiner.py:182-256).  `args` describes one segment (n images; its dy / src0 / src1 are
+ * ignored), dys[i] / src0s[i] / src1s[i] are segment i's bases with args' strides.  Shapes: the
+ * Winograd ones (3×3 stride 1 pad 1; 1×5 / 5×1 stride 1 pad 2); others return
+ * SCFLOW_EUNSUPPORTED.  `workspace`: scflow_conv_wgrad_workspace() of args with n·segs images. */
+int scflow_conv_wgrad_batched(const scflow_wgrad_args* args, int segs, const float* const* dys,
+                              const float* const* src0s, const float* const* src1s, void* stream);
 int scflow_corr_lookup_backward(const float* dout, int out_layout, int out_stride, const float* flow,
                                 int flow_layout, float* dpyr, int n, int h, int w, int num_levels,
                                 int radius, void* stream);

@@ -235,6 +235,7 @@ SIGNATURES = {
     "scflow_render": (c_int, [ctypes.POINTER(RenderArgs), c_vp]),
     "scflow_conv_wgrad_workspace": (c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_ll)]),
     "scflow_conv_wgrad": (c_int, [ctypes.POINTER(WgradArgs), c_vp]),
+    "scflow_conv_wgrad_batched": (c_int, [ctypes.POINTER(WgradArgs), c_int, c_vp, c_vp, c_vp, c_vp]),
     "scflow_im2col": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_vp]),
     "scflow_im2col_ex": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

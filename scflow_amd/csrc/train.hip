@@ -314,9 +314,27 @@ __global__ __launch_bounds__(256) void corr_lookup_bwd_win_kernel(
 }
 
 // ------------------------------------------------------------------------------ wgrad
+// equally shaped segments summed by one launch (scflow_conv_wgrad_batched): segment s holds
+// images [s·nimg, (s+1)·nimg) of the walk, at its own dY / input bases (one segment: the args')
+constexpr int WG_MAXSEG = 8;
+struct WgSegs {
+  int nimg;
+  const float* dy[WG_MAXSEG];
+  const float* src0[WG_MAXSEG];
+  const float* src1[WG_MAXSEG];
+};
+
+inline void wg_single_seg(const scflow_wgrad_args& a, WgSegs* s) {
+  s->nimg = a.n;
+  s->dy[0] = a.dy;
+  s->src0[0] = a.src0;
+  s->src1[0] = a.src1;
+}
+
 struct WgParams {
   scflow_wgrad_args a;
   int oh, ow, tr, tc, ltc, hr, hc, cp, nchunks, cps, co_tiles, copad, cinp, wco;
+  WgSegs sg;
 };
 
 constexpr int WT = 64;  // ci tile of a workgroup (and the co tile of the 4-wave variant)
@@ -381,6 +399,11 @@ __global__ __launch_bounds__(WCO * 4 * KS, (KH * KW >= 9 || WCO * KS > 64) ? 1 :
   auto gload = [&](int ch) {
     int img, oy0, ox0;
     chunk_origin(ch, &img, &oy0, &ox0);
+    const int seg = img / P.sg.nimg;  // workgroup-uniform
+    img -= seg * P.sg.nimg;
+    const float* dyp = P.sg.dy[seg];
+    const float* s0p = P.sg.src0[seg];
+    const float* s1p = P.sg.src1[seg];
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const int idx = tid + NT * j;
@@ -388,7 +411,7 @@ __global__ __launch_bounds__(WCO * 4 * KS, (KH * KW >= 9 || WCO * KS > 64) ? 1 :
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (p < P.cp && co < a.cout) {
         const size_t m = ((size_t)img * P.oh + oy0 + (p >> P.ltc)) * P.ow + ox0 + (p & (P.tc - 1));
-        v = *(const floatx4*)(a.dy + m * a.sdy + co);
+        v = *(const floatx4*)(dyp + m * a.sdy + co);
       }
       rd[j] = v;
     }
@@ -402,8 +425,8 @@ __global__ __launch_bounds__(WCO * 4 * KS, (KH * KW >= 9 || WCO * KS > 64) ? 1 :
         const int iy = oy0 * S - a.ph + hy, ix = ox0 * S - a.pw + hx;
         if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) {
           const size_t pix = ((size_t)img * a.h + iy) * a.w + ix;
-          v = c < a.cin0 ? *(const floatx4*)(a.src0 + pix * a.s0 + c)
-                         : *(const floatx4*)(a.src1 + pix * a.s1 + (c - a.cin0));
+          v = c < a.cin0 ? *(const floatx4*)(s0p + pix * a.s0 + c)
+                         : *(const floatx4*)(s1p + pix * a.s1 + (c - a.cin0));
         }
       }
       rx[j] = v;
@@ -426,10 +449,15 @@ __global__ __launch_bounds__(WCO * 4 * KS, (KH * KW >= 9 || WCO * KS > 64) ? 1 :
   auto stage_scalar = [&](int ch) {  // cin or cout not a multiple of 4: element-wise staging
     int img, oy0, ox0;
     chunk_origin(ch, &img, &oy0, &ox0);
+    const int seg = img / P.sg.nimg;
+    img -= seg * P.sg.nimg;
+    const float* dyp = P.sg.dy[seg];
+    const float* s0p = P.sg.src0[seg];
+    const float* s1p = P.sg.src1[seg];
     for (int idx = tid; idx < P.cp * WCO; idx += NT) {
       const int p = idx / WCO, co = co0 + (idx % WCO);
       const size_t m = ((size_t)img * P.oh + oy0 + (p >> P.ltc)) * P.ow + ox0 + (p & (P.tc - 1));
-      Ds[idx] = co < a.cout ? a.dy[m * a.sdy + co] : 0.f;
+      Ds[idx] = co < a.cout ? dyp[m * a.sdy + co] : 0.f;
     }
     for (int idx = tid; idx < nh * WT; idx += NT) {
       const int hp = idx >> 6, c = ci0 + (idx & 63);
@@ -438,7 +466,7 @@ __global__ __launch_bounds__(WCO * 4 * KS, (KH * KW >= 9 || WCO * KS > 64) ? 1 :
       float v = 0.f;
       if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w && c < cin) {
         const size_t pix = ((size_t)img * a.h + iy) * a.w + ix;
-        v = c < a.cin0 ? a.src0[pix * a.s0 + c] : a.src1[pix * a.s1 + (c - a.cin0)];
+        v = c < a.cin0 ? s0p[pix * a.s0 + c] : s1p[pix * a.s1 + (c - a.cin0)];
       }
       Xs[idx] = v;
     }
@@ -1658,31 +1686,13 @@ SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long l
   return SCFLOW_OK;
 }
 
-SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
-  if (!args) return SCFLOW_EINVAL;
-  const scflow_wgrad_args& a = *args;
-  if (!a.dy || !a.src0 || !a.dw || !a.workspace || a.n <= 0 || a.h <= 0 || a.w <= 0 ||
-      a.cout <= 0 || a.cin0 <= 0 || a.cin1 < 0 || (a.cin1 > 0 && !a.src1) || a.sdy < a.cout ||
-      a.s0 < a.cin0 || (a.cin1 > 0 && a.s1 < a.cin1) || a.ph < 0 || a.pw < 0)
-    return SCFLOW_EINVAL;
-  WtParams Q;
-  if (wthin_geometry(a, &Q)) {
-    if (a.workspace_floats < wthin_workspace(Q)) return SCFLOW_EINVAL;
-    return wthin_launch(Q, (hipStream_t)stream);
-  }
-  WwParams R;
-  if (wwino_geometry(a, &R)) {
-    if (a.workspace_floats < wwino_workspace(R)) return SCFLOW_EINVAL;
-    return wwino_launch(R, (hipStream_t)stream);
-  }
-  W5wParams R5;
-  if (wwino5_geometry(a, &R5)) {
-    if (a.workspace_floats < wwino5_workspace(R5)) return SCFLOW_EINVAL;
-    return wwino5_launch(R5, (hipStream_t)stream);
-  }
+// the direct implicit-GEMM weight gradient (wgrad_kernel) over the segments sg: geometry, the
+// variant's launch and the split reduction
+static int wgrad_direct_launch(const scflow_wgrad_args& a, const WgSegs& sg, hipStream_t st) {
   WgParams P;
   int splits = 0;
   if (!wgrad_geometry(a, &P, &splits)) return SCFLOW_EUNSUPPORTED;
+  P.sg = sg;
   const int taps = a.kh * a.kw;
   const long long need = (long long)splits * P.copad * taps * P.cinp + (long long)splits * P.copad;
   if (a.workspace_floats < need) return SCFLOW_EINVAL;
@@ -1710,7 +1720,6 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
   const size_t lds = lds1 * (db2 ? 2 : 1);
   if (lds > 160 * 1024) return SCFLOW_EUNSUPPORTED;
   const dim3 grid((unsigned)(P.co_tiles * (P.cinp / WT)), (unsigned)splits);
-  hipStream_t st = (hipStream_t)stream;
   // two wave sets splitting each chunk's k-steps
   const bool ks2 = vec && ((taps >= 9 && ks_env == 2) || ks5);
 #define SCFLOW_WG(KH_, KW_, S_)                                                                  \
@@ -1746,6 +1755,75 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
                                                a.cin0 + a.cin1, taps, P.copad, P.cinp, a.accumulate,
                                                lg);
   return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_conv_wgrad_batched(const scflow_wgrad_args* args, int segs,
+                                         const float* const* dys, const float* const* src0s,
+                                         const float* const* src1s, void* stream) {
+  if (!args || segs < 1 || segs > WG_MAXSEG || !dys || !src0s || (args->cin1 > 0 && !src1s) ||
+      !args->dw || !args->workspace || args->n <= 0)
+    return SCFLOW_EINVAL;
+  for (int i = 0; i < segs; ++i)
+    if (!dys[i] || !src0s[i] || !aligned16(dys[i]) || !aligned16(src0s[i]) ||
+        (args->cin1 > 0 && (!src1s[i] || !aligned16(src1s[i]))))
+      return SCFLOW_EINVAL;
+  scflow_wgrad_args t = *args;  // the walk: all segments' images in a row
+  t.n = args->n * segs;
+  t.dy = dys[0];
+  t.src0 = src0s[0];
+  t.src1 = args->cin1 > 0 ? src1s[0] : nullptr;
+  WgSegs sg;
+  sg.nimg = args->n;
+  for (int i = 0; i < WG_MAXSEG; ++i) {
+    const int j = i < segs ? i : 0;
+    sg.dy[i] = dys[j];
+    sg.src0[i] = src0s[j];
+    sg.src1[i] = args->cin1 > 0 ? src1s[j] : nullptr;
+  }
+  WwParams R;
+  if (wwino_geometry(t, &R)) {
+    if (t.workspace_floats < wwino_workspace(R)) return SCFLOW_EINVAL;
+    R.sg = sg;
+    return wwino_launch(R, (hipStream_t)stream);
+  }
+  W5wParams R5;
+  if (wwino5_geometry(t, &R5)) {
+    if (t.workspace_floats < wwino5_workspace(R5)) return SCFLOW_EINVAL;
+    R5.sg = sg;
+    return wwino5_launch(R5, (hipStream_t)stream);
+  }
+  WtParams Q;
+  if (wthin_geometry(t, &Q)) return SCFLOW_EUNSUPPORTED;  // thin shapes: per-segment launches
+  return wgrad_direct_launch(t, sg, (hipStream_t)stream);
+}
+
+SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
+  if (!args) return SCFLOW_EINVAL;
+  const scflow_wgrad_args& a = *args;
+  if (!a.dy || !a.src0 || !a.dw || !a.workspace || a.n <= 0 || a.h <= 0 || a.w <= 0 ||
+      a.cout <= 0 || a.cin0 <= 0 || a.cin1 < 0 || (a.cin1 > 0 && !a.src1) || a.sdy < a.cout ||
+      a.s0 < a.cin0 || (a.cin1 > 0 && a.s1 < a.cin1) || a.ph < 0 || a.pw < 0)
+    return SCFLOW_EINVAL;
+  WtParams Q;
+  if (wthin_geometry(a, &Q)) {
+    if (a.workspace_floats < wthin_workspace(Q)) return SCFLOW_EINVAL;
+    return wthin_launch(Q, (hipStream_t)stream);
+  }
+  WwParams R;
+  if (wwino_geometry(a, &R)) {
+    if (a.workspace_floats < wwino_workspace(R)) return SCFLOW_EINVAL;
+    wg_single_seg(a, &R.sg);
+    return wwino_launch(R, (hipStream_t)stream);
+  }
+  W5wParams R5;
+  if (wwino5_geometry(a, &R5)) {
+    if (a.workspace_floats < wwino5_workspace(R5)) return SCFLOW_EINVAL;
+    wg_single_seg(a, &R5.sg);
+    return wwino5_launch(R5, (hipStream_t)stream);
+  }
+  WgSegs sg;
+  wg_single_seg(a, &sg);
+  return wgrad_direct_launch(a, sg, (hipStream_t)stream);
 }
 
 SCFLOW_API int scflow_im2col_ex(const float* x, int sx, float* cols, int n, int h, int w, int cin,

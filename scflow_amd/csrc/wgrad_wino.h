@@ -54,6 +54,7 @@ __device__ __forceinline__ void wgrad_xcd_map(int tiles, int splits, int* tile, 
 struct WwParams {
   scflow_wgrad_args a;
   int cg, rg, nchunks, cps, co_tiles, copad, cinp;
+  WgSegs sg;
 };
 
 typedef float floatx2w __attribute__((ext_vector_type(2)));
@@ -90,6 +91,11 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
   auto gload = [&](int ch) {
     int img, oy0, ox0;
     origin(ch, &img, &oy0, &ox0);
+    const int seg = img / P.sg.nimg;  // workgroup-uniform
+    img -= seg * P.sg.nimg;
+    const float* dyp = P.sg.dy[seg];
+    const float* s0p = P.sg.src0[seg];
+    const float* s1p = P.sg.src1[seg];
 #pragma unroll
     for (int j = 0; j < WW_ND; ++j) {  // dY: 128 pixels × 8 co quads
       const int idx = tid + WW_NT * j;
@@ -97,7 +103,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (co < a.cout) {
         const size_t m = ((size_t)img * a.h + oy0 + (p >> 5)) * a.w + ox0 + (p & 31);
-        v = *(const floatx4*)(a.dy + m * a.sdy + co);
+        v = *(const floatx4*)(dyp + m * a.sdy + co);
       }
       rd[j] = v;
     }
@@ -111,8 +117,8 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
         const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
         if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) {
           const size_t pix = ((size_t)img * a.h + iy) * a.w + ix;
-          v = c < a.cin0 ? *(const floatx4*)(a.src0 + pix * a.s0 + c)
-                         : *(const floatx4*)(a.src1 + pix * a.s1 + (c - a.cin0));
+          v = c < a.cin0 ? *(const floatx4*)(s0p + pix * a.s0 + c)
+                         : *(const floatx4*)(s1p + pix * a.s1 + (c - a.cin0));
         }
       }
       rx[j] = v;

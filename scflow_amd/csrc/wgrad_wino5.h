@@ -50,6 +50,7 @@ struct W5wParams {
   int H, W;        // the walked image: 1×5 (h, w); 5×1 the transpose (w, h)
   long long sy, sx;  // pixel strides of its rows / columns: (w, 1) or (1, w)
   int cg, rg, nchunks, cps, co_tiles, copad, cinp;
+  WgSegs sg;       // segments (wgrad_wino.h)
 };
 
 __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, float* __restrict__ slab,
@@ -90,6 +91,9 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
   auto gload = [&](int ch) __attribute__((always_inline)) {
     int img, oy0, ox0;
     origin(ch, &img, &oy0, &ox0);
+    const int seg = img / P.sg.nimg;  // workgroup-uniform
+    img -= seg * P.sg.nimg;
+    const float* dyp = P.sg.dy[seg];
     const int co = co0 + cl, c = ci0 + cl;
 #pragma unroll
     for (int j = 0; j < W5W_ND; ++j) {  // dY: row q >> 3, columns 4(q & 7) + k
@@ -97,11 +101,11 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (co < a.cout) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = a.dy[pix(img, oy0 + (q >> 3), ox0 + 4 * (q & 7) + k) * a.sdy + co];
+        for (int k = 0; k < 4; ++k) v[k] = dyp[pix(img, oy0 + (q >> 3), ox0 + 4 * (q & 7) + k) * a.sdy + co];
       }
       rd[j] = v;
     }
-    const float* src = c < a.cin0 ? a.src0 + c : a.src1 + (c - a.cin0);
+    const float* src = c < a.cin0 ? P.sg.src0[seg] + c : P.sg.src1[seg] + (c - a.cin0);
     const int ss = c < a.cin0 ? a.s0 : a.s1;
 #pragma unroll
     for (int j = 0; j < W5W_NX; ++j) {  // halo: row q / 9, columns x = ox0 − 2 + 4(q % 9) + k

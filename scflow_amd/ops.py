@@ -883,6 +883,54 @@ def conv_wgrad(dy: Tensor, src0, src1: Optional[Chan], dw: Tensor, db: Optional[
     check(lib.scflow_conv_wgrad(ctypes.byref(a), _stream(dy)), "scflow_conv_wgrad")
 
 
+def conv_wgrad_batched(dys: List[Tensor], src0s: list, src1s: Optional[list], dw: Tensor,
+                       db: Optional[Tensor], n: int, h: int, w: int, kh: int, kw: int, stride: int,
+                       ph: int, pw: int, accumulate: bool = False) -> None:
+    """dw (+)= Σ_i weight gradient of segment i (dys[i] with src0s[i] / src1s[i], each n images
+    of h×w) in one launch (scflow_conv_wgrad_batched; ≤ 8 equally shaped segments, Winograd
+    shapes only — ScflowError(SCFLOW_EUNSUPPORTED) otherwise)."""
+    segs = len(dys)
+    if not 1 <= segs <= 8 or len(src0s) != segs or (src1s is not None and len(src1s) != segs):
+        raise ValueError(f"conv_wgrad_batched: 1..8 segments with matching sources, got {segs}")
+    _require(dw, "dw")
+
+    def desc(x, nm):
+        if isinstance(x, Chan):
+            _require(x.buf, nm)
+            return x.ptr, x.c, x.stride
+        _require(x, nm)
+        return x.data_ptr(), x.shape[-1], x.shape[-1]
+
+    d0 = [desc(x, "src0") for x in src0s]
+    d1 = [desc(x, "src1") for x in src1s] if src1s is not None else None
+    for t in dys:
+        _require(t, "dy")
+        if t.shape != dys[0].shape:
+            raise ValueError("conv_wgrad_batched: segments differ in dY shape")
+    if len({d[1:] for d in d0}) != 1 or (d1 is not None and len({d[1:] for d in d1}) != 1):
+        raise ValueError("conv_wgrad_batched: segments differ in source channels / strides")
+    a = _lib.WgradArgs()
+    a.dy, a.sdy = dys[0].data_ptr(), dys[0].shape[-1]
+    a.src0, a.cin0, a.s0 = d0[0]
+    a.src1, a.cin1, a.s1 = d1[0] if d1 is not None else (None, 0, 0)
+    a.dw, a.db = dw.data_ptr(), _p(db)
+    a.n, a.h, a.w, a.cout, a.kh, a.kw = n * segs, h, w, dys[0].shape[-1], kh, kw
+    a.stride, a.ph, a.pw, a.accumulate = stride, ph, pw, int(accumulate)
+    lib = _lib.load()
+    need = ctypes.c_longlong(0)
+    check(lib.scflow_conv_wgrad_workspace(ctypes.byref(a), ctypes.byref(need)),
+          "scflow_conv_wgrad_workspace")
+    ws = torch.empty(max(1, need.value), device=dw.device)
+    a.workspace, a.workspace_floats = ws.data_ptr(), need.value
+    a.n = n
+    arr = ctypes.c_void_p * segs
+    p_dy = arr(*[t.data_ptr() for t in dys])
+    p_s0 = arr(*[d[0] for d in d0])
+    p_s1 = arr(*[d[0] for d in d1]) if d1 is not None else None
+    check(lib.scflow_conv_wgrad_batched(ctypes.byref(a), segs, p_dy, p_s0, p_s1, _stream(dw)),
+          "scflow_conv_wgrad_batched")
+
+
 def im2col(x, n: int, h: int, w: int, cin: int, kh: int, kw: int, stride: int, ph: int, pw: int,
            out: Optional[Tensor] = None, channel_major: bool = False) -> Tensor:
     """Patch matrix [n·oh·ow, kh·kw·cin] of a channels-last input (tensor or Chan); columns in

@@ -262,6 +262,128 @@ def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int,
     return dw, db
 
 
+# ------------------------------------------------------------------ batched weight gradients
+# A decoder conv runs once per refinement iteration: its weight gradient is the sum of 8 per-use
+# weight gradients.  Instead of 8 launches (each with its own split reduction, and short per-use
+# pixel walks at B = 16), the uses' (dY, input) pairs are collected as their backward runs and
+# summed by ONE scflow_conv_wgrad_batched launch when the last use's backward arrives (autograd
+# consumes a weight's gradient only after every use has produced its part).
+_FWD_ID = 0
+
+
+def begin_forward() -> None:
+    """Start of a training forward pass: per-weight use counts restart (refiner_train_forward)."""
+    global _FWD_ID
+    _FWD_ID += 1
+
+
+def _batchable(kh: int, kw: int, s: int, ph: int, pw: int) -> bool:
+    """Shapes scflow_conv_wgrad_batched takes (the Winograd and implicit-GEMM weight gradients;
+    thin and 7×7 ones are recorded too and fall back to one launch per use)."""
+    return (kh, kw) in ((1, 1), (3, 3), (1, 5), (5, 1)) and s in (1, 2)
+
+
+def _use_holder(w: Tensor) -> dict:
+    """The per-forward-pass use record of weight ``w`` (module parameters persist across steps:
+    the record restarts with each forward pass, begin_forward)."""
+    hold = getattr(w, "_scflow_uses", None)
+    if hold is None or hold["fwd"] != _FWD_ID:
+        hold = {"fwd": _FWD_ID, "uses": 0, "seen": 0, "items": [], "buf": None}
+        try:
+            w._scflow_uses = hold
+        except (AttributeError, RuntimeError):
+            return None
+    hold["uses"] += 1
+    return hold
+
+
+def _flush_wgrad(items, w: Tensor, with_bias: bool, dw: Tensor, db: Optional[Tensor],
+                 accumulate: bool, s: int, ph: int, pw: int) -> None:
+    """dw (db) (+)= Σ over items (g, x0, x1) of the conv weight (bias) gradient: batched launches
+    of ≤ 8 segments, per-item launches where the batched kernel does not take the shape."""
+    g0, x00, x10 = items[0]
+    n, h, wd, _ = x00.shape
+    cout, cin, kh, kw = w.shape
+    padded = g0.shape[-1] != cout  # out_net's 126 output channels, padded to 128 in dY
+    if padded:
+        tw = torch.empty(g0.shape[-1], cin, kh, kw, device=g0.device)
+        tb = torch.empty(g0.shape[-1], device=g0.device) if with_bias else None
+    else:
+        tw, tb = dw, db
+    try:
+        for i in range(0, len(items), 8):
+            part = items[i:i + 8]
+            ops.conv_wgrad_batched([g.reshape(-1, g.shape[-1]) for g, _, _ in part],
+                                   [x0 for _, x0, _ in part],
+                                   None if x10 is None else [x1 for _, _, x1 in part],
+                                   tw, tb, n, h, wd, kh, kw, s, ph, pw,
+                                   accumulate=(accumulate and not padded) or i > 0)
+    except ScflowError:  # shapes outside the batched kernels: one launch per use
+        if not accumulate:
+            dw.zero_()
+            if with_bias:
+                db.zero_()
+        for g, x0, x1 in items:
+            _weight_grad(g, x0, x1, w, s, ph, pw, with_bias, dw=dw, db=db)
+        return
+    if padded:
+        if accumulate:
+            dw += tw[:cout]
+            if with_bias:
+                db += tb[:cout]
+        else:
+            dw.copy_(tw[:cout])
+            if with_bias:
+                db.copy_(tb[:cout])
+
+
+_PENDING: dict = {}  # id(holder) → holder with recorded uses not yet summed
+
+
+def _deferred_wgrad(hold: dict, w: Tensor, item, with_bias: bool, s: int, ph: int, pw: int,
+                    sink_w: Optional[Tensor], sink_b: Optional[Tensor]):
+    """Record this use's (g, x0, x1); on the last use, one batched weight gradient over all of
+    them.  With sinks (direct_weight_grads) the sum is added into them and nothing is returned;
+    otherwise the first call hands autograd the (dw, db) buffers the last call fills (only for
+    tensors whose every use is differentiated: the GRU's per-pass concatenated weights)."""
+    direct = sink_w is not None and (sink_b is not None or not with_bias)
+    first = not hold["items"]
+    out = (None, None)
+    if first:
+        hold["flush"] = (w, with_bias, s, ph, pw, sink_w, sink_b) if direct else None
+        if not direct:
+            hold["buf"] = (torch.empty_like(w), w.new_empty(w.shape[0]) if with_bias else None)
+            out = hold["buf"]
+        _PENDING[id(hold)] = hold
+    hold["items"].append(item)
+    hold["seen"] += 1
+    if hold["seen"] >= hold["uses"]:
+        _flush_holder(hold)
+    return out
+
+
+def _flush_holder(hold: dict) -> None:
+    items = hold["items"]
+    if items:
+        if hold["flush"] is not None:
+            w, with_bias, s, ph, pw, sink_w, sink_b = hold["flush"]
+            _flush_wgrad(items, w, with_bias, sink_w, sink_b, True, s, ph, pw)
+        else:
+            raise RuntimeError("deferred weight gradient flushed without sinks")
+    hold["items"] = []
+    hold["seen"] = 0
+    hold["buf"] = None
+    _PENDING.pop(id(hold), None)
+
+
+def flush_pending_wgrads() -> None:
+    """Sum the weight gradients of uses a backward pass recorded but whose last use it never
+    reached (a conv output that does not reach the loss): call after backward, before the
+    gradients are read (TrainStep does)."""
+    for hold in list(_PENDING.values()):
+        _flush_holder(hold)
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act):
@@ -273,6 +395,8 @@ class _Conv2dNHWC(torch.autograd.Function):
         ctx.save_for_backward(x0, x1, w, y if act is not None else None)
         ctx.stride, ctx.pad, ctx.has_b, ctx.act = stride, (ph, pw), b is not None, act
         ctx.bias = b  # the leaf itself (direct gradient accumulation), not saved data
+        kh, kw = w.shape[2], w.shape[3]
+        ctx.uses = _use_holder(w) if _batchable(kh, kw, stride, ph, pw) and w.requires_grad else None
         return y
 
     @staticmethod
@@ -318,7 +442,11 @@ def _conv_backward(ctx, dy):
     pad_co = (-cout) % 4 if cout > 4 else 0
     gp = F.pad(g, (0, pad_co)) if pad_co else g
     if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-        if s == 1:  # a 'same' conv of dY with the flipped, transposed weights
+        if s == 1 and kh == kw == 1 and cout == 1:
+            # 1×1 to one channel (the mask predictor): dX = dY ⊗ w, one broadcast multiply
+            # (a 1 → cin conv launch took 27 µs for the 16 MB it writes)
+            dx = g * w.detach().reshape(1, 1, 1, cin)
+        elif s == 1:  # a 'same' conv of dY with the flipped, transposed weights
             dx = _conv_forward(gp, None, _flip_t(w, pad_co), None, 1, (kh - 1 - ph, kw - 1 - pw))
         else:
             # strided: cols = dY·Wmat (exactly the products the transposed conv needs, no
@@ -329,7 +457,15 @@ def _conv_backward(ctx, dy):
         dx0 = dx if x1 is None else dx[..., :c0]
         dx1 = None if x1 is None else dx[..., c0:]
     want_b = ctx.has_b and ctx.needs_input_grad[3]
-    if ctx.needs_input_grad[2] or want_b:
+    hold = getattr(ctx, "uses", None)
+    sw = _grad_sink(w) if ctx.needs_input_grad[2] else None
+    sb = _grad_sink(ctx.bias) if want_b else None
+    if (hold is not None and hold["uses"] > 1 and sw is not None and (sb is not None or not want_b)
+            and (want_b or not ctx.has_b)):
+        # a weight used by several convs of this pass (the decoder's 8 iterations), gradients
+        # added straight into the parameters: one batched weight gradient at the last use
+        _deferred_wgrad(hold, w, (gp, x0, x1), want_b, s, ph, pw, sw, sb)
+    elif ctx.needs_input_grad[2] or want_b:
         sw = _grad_sink(w) if ctx.needs_input_grad[2] else None
         sb = _grad_sink(ctx.bias) if want_b else None
         if sw is not None and (sb is not None or not want_b):
@@ -363,26 +499,29 @@ def _shared_grad_holder(w: Tensor) -> dict:
     concatenated weights, used by all 8 iterations)."""
     holder = getattr(w, "_scflow_gacc", None)
     if holder is None:
-        holder = {"buf": None, "uses": 0, "seen": 0}
+        holder = {"buf": None, "uses": 0, "seen": 0, "items": []}
         w._scflow_gacc = holder
     holder["uses"] += 1
     return holder
 
 
-def _shared_wgrad(holder: dict, w: Tensor, add) -> Optional[Tensor]:
-    """Add this use's weight gradient into the shared buffer (``add(buf)``); the first backward
-    call hands the buffer to autograd, the later ones nothing — autograd runs the backward of
-    ``w``'s producer only after every use, so it receives the complete sum with no per-use adds.
-    Once a backward pass has seen every use the buffer is released, so a second pass over the
-    same graph (retain_graph) accumulates into a fresh one."""
+def _shared_wgrad(holder: dict, w: Tensor, item, ph: int, pw: int) -> Optional[Tensor]:
+    """Record this use's (g, x0, x1) for the shared weight ``w``; the first backward call hands
+    autograd the gradient buffer, the later ones nothing — autograd runs the backward of ``w``'s
+    producer only after every use, so the last call fills it first: ONE batched weight gradient
+    over all uses (scflow_conv_wgrad_batched), no per-use launches or adds.  A pass that has seen
+    every use starts over, so a second pass over the same graph (retain_graph) sums afresh."""
     first = holder["buf"] is None
     if first:
-        holder["buf"] = torch.zeros_like(w)
+        holder["buf"] = torch.empty_like(w)
+        holder["items"] = []
     buf = holder["buf"]
-    add(buf)
+    holder["items"].append(item)
     holder["seen"] += 1
     if holder["seen"] >= holder["uses"]:
+        _flush_wgrad(holder["items"], w, False, buf, None, False, 1, ph, pw)
         holder["buf"] = None
+        holder["items"] = []
         holder["seen"] = 0
     return buf if first else None
 
@@ -433,13 +572,13 @@ class _GruStep(torch.autograd.Function):
             dh2 = dh2.contiguous()
         ops.gru_gate_backward_q(dh2, zr, h, q, dq, dzr, dha)
         dxq = _conv_forward(dq, None, _flip_t(w_q), None, 1, (kh - 1 - ph, kw - 1 - pw))
-        dw_q = _shared_wgrad(ctx.acc[1], w_q, lambda buf: _weight_grad(dq, rh, x, w_q, 1, ph, pw, False, dw=buf))
+        dw_q = _shared_wgrad(ctx.acc[1], w_q, (dq, rh, x), ph, pw)
         # dh = dha + drh·r written over drh = dxq[..., :c] itself, so that dxq becomes [dh | dx_q]
         # and the z | r conv's dX, with dxq as its added map, yields both sums in its epilogue:
         # T = [dh + dxz_h | dx_q + dxz_x] (no separate adds; dh and dx leave as channel views)
         ops.gru_gate_backward_r(dxq[..., :c], zr, h, dha, dzr, dxq[..., :c])
         t = _conv_forward(dzr, None, _flip_t(w_zr), None, 1, (kh - 1 - ph, kw - 1 - pw), bias_map=dxq)
-        dw_zr = _shared_wgrad(ctx.acc[0], w_zr, lambda buf: _weight_grad(dzr, h, x, w_zr, 1, ph, pw, False, dw=buf))
+        dw_zr = _shared_wgrad(ctx.acc[0], w_zr, (dzr, h, x), ph, pw)
         return t[..., :c], t[..., c:], dw_zr, dw_q, dzr, dq, None
 
 

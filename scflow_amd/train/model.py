@@ -21,8 +21,9 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import (conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid, group_norm_nhwc,
-                        gru_step, instance_norm_nhwc, linear, pose_update6, upsample_bilinear_ac)
+from .functions import (begin_forward, conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid,
+                        group_norm_nhwc, gru_step, instance_norm_nhwc, linear, pose_update6,
+                        upsample_bilinear_ac)
 from .losses import LowRes, filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
@@ -246,6 +247,7 @@ def refiner_train_forward(refiner, batch: Dict[str, Tensor], model_points: Seque
     render_images, real_images [N,3,S,S]; ref_rotation, ref_translation, gt_rotation,
     gt_translation, internel_k, depth, label; optional head_label (the pose head's class label,
     default label — a data-parallel shard passes the global batch's label[:1], dist.shard_batch)."""
+    begin_forward()  # per-weight use counts of this pass (batched weight gradients)
     dec = refiner.decoder
     iters = int(dec.iters if iters is None else iters)
     real = batch["real_images"].permute(0, 2, 3, 1).contiguous()

@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from .._lib import bump_weights_generation
-from .functions import capture_cache, direct_weight_grads
+from .functions import capture_cache, direct_weight_grads, flush_pending_wgrads
 from .model import refiner_train_forward
 
 Tensor = torch.Tensor
@@ -162,6 +162,7 @@ class TrainStep:
             else:
                 with direct_weight_grads():
                     out["loss"].backward()
+                flush_pending_wgrads()  # uses whose last use the pass did not reach
         # detached: a returned tensor must not keep this step's autograd graph (and its
         # AccumulateGrad nodes) alive into the next step or a capture
         return {k: _detach(v) for k, v in out.items()}

@@ -198,6 +198,44 @@ def test_conv_wgrad_wino5(case):
         _close(db - 1, dy.double().sum((0, 1, 2)), 1e-5, 1e-4 * np.sqrt(n * h * w), "db")
 
 
+@pytest.mark.parametrize("case", [
+    # (segs, n, h, w, c0, c1, cout, kh, kw, bias)
+    (8, 2, 32, 32, 128, 128, 256, 1, 5, False),   # the GRU's 8 iterations, z | r 1×5
+    (8, 2, 32, 32, 128, 128, 128, 5, 1, False),   # q 5×1
+    (8, 2, 32, 32, 256, 0, 192, 3, 3, True),      # corr_net.1 over 8 iterations (bias)
+    (3, 2, 32, 64, 64, 32, 96, 3, 3, True),       # 3 segments, ragged channel blocks
+])
+def test_conv_wgrad_batched(case):
+    """scflow_conv_wgrad_batched (one launch over equally shaped segments) = the sum of the
+    segments' fp64 weight gradients, accumulate = 1 onto dw / db, Chan slices as second sources."""
+    from scflow_amd import ops
+    from scflow_amd.ops import Chan
+    segs, n, h, w, c0, c1, cout, kh, kw, bias = case
+    g = torch.Generator().manual_seed(sum(case))
+    ph, pw = kh // 2, kw // 2
+    ref = torch.zeros(cout, c0 + c1, kh, kw, dtype=torch.float64)
+    dys, s0, s1, dbr = [], [], [], torch.zeros(cout, dtype=torch.float64)
+    for _ in range(segs):
+        x0 = torch.randn(n, h, w, c0, generator=g)
+        buf = torch.randn(n, h, w, c1 + 8, generator=g)
+        dy = torch.randn(n, h, w, cout, generator=g)
+        xc = torch.cat([x0, buf[..., 4:4 + c1]], -1) if c1 else x0
+        ref += torch.nn.grad.conv2d_weight(xc.permute(0, 3, 1, 2).double(), (cout, c0 + c1, kh, kw),
+                                           dy.permute(0, 3, 1, 2).double(), padding=(ph, pw))
+        dbr += dy.double().sum((0, 1, 2))
+        dys.append(dy.cuda().view(-1, cout))
+        s0.append(x0.cuda())
+        s1.append(Chan(buf.cuda().view(-1, c1 + 8), 4, c1))
+    dw = torch.ones(cout, c0 + c1, kh, kw).cuda()
+    db = torch.ones(cout).cuda() if bias else None
+    ops.conv_wgrad_batched(dys, s0, s1 if c1 else None, dw, db, n, h, w, kh, kw, 1, ph, pw,
+                           accumulate=True)
+    torch.cuda.synchronize()
+    _close(dw - 1, ref, 2e-5, 0.0, "dw")
+    if bias:
+        _close(db - 1, dbr, 1e-5, 1e-4 * np.sqrt(segs * n * h * w), "db")
+
+
 def test_corr_pyramid_backward():
     from scflow_amd import ops
     from scflow_amd.train.functions import corr_pyramid

@@ -66,7 +66,13 @@ def main():
         tag = f"{os.path.basename(fr.f_code.co_filename)}:{fr.f_lineno}"
         return ((bt, m, nn, k, tag, 0, 0, 0), 2.0 * bt * m * nn * k)
 
+    def wgb_flops(dys, src0s, src1s, dw, db, n, h, w, kh, kw, stride, ph, pw, accumulate=False):
+        cout, cin = dw.shape[0], dw.shape[1]
+        segs = len(dys)
+        return ((segs * n, h, w, cin, cout, kh, kw, stride), 2.0 * segs * n * h * w * cout * cin * kh * kw)
+
     ops.conv_wgrad = wrap("wgrad", ops.conv_wgrad, wg_flops)
+    ops.conv_wgrad_batched = wrap("wgb", ops.conv_wgrad_batched, wgb_flops)
     ops.gemm = wrap("gemm", ops.gemm, gemm_flops)
     functions._conv_forward = wrap("conv", functions._conv_forward, fw_flops)
 
