@@ -586,6 +586,16 @@ typedef struct {
  * mm: n·2·c floats. */
 int scflow_in_apply(const float* x, const float* scale, const float* shift, float* y, int n, int hw,
                     int c, int relu, void* stream);
+/* The residual block's tail in one pass each way (raft_encoder.py BasicBlock: y = relu(norm2(·) +
+ * identity)): scflow_in_apply_residual: y = max(x·scale + shift + res, 0);
+ * scflow_in_backward_residual: g = dy·(y > 0) → dres = g and dx = the InstanceNorm backward of g
+ * (same workspace as scflow_in_backward). */
+int scflow_in_apply_residual(const float* x, const float* scale, const float* shift, const float* res,
+                             float* y, int n, int hw, int c, void* stream);
+int scflow_in_backward_residual(const float* dy, const float* x, const float* scale,
+                                const float* shift, const float* y, float* dx, float* dres,
+                                double* partial, float* mm, int n, int hw, int c, int chunks,
+                                void* stream);
 int scflow_in_backward(const float* dy, const float* x, const float* scale, const float* shift,
                        float* dx, double* partial, float* mm, int n, int hw, int c, int chunks,
                        int relu, void* stream);

@@ -157,6 +157,9 @@ SIGNATURES = {
     "scflow_corr_lookup_tiled": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_vp]),
     "scflow_in_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_in_apply_residual": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    "scflow_in_backward_residual": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_int, c_int, c_int, c_int, c_vp]),
     "scflow_in_backward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                                    c_int, c_int, c_vp]),
     "scflow_debug_lookup_stamps": (c_int, [c_vp]),

@@ -919,9 +919,12 @@ int wthin_launch(const WtParams& P, hipStream_t st) {
 // in three launches: fp64 partial sums of g and g·x̂ per (image, pixel chunk) in a fixed order,
 // their finalisation per (image, channel), and the elementwise dx.
 
+// y = act(x·scale + shift [+ res]) — res: the residual block's identity, added before the ReLU
+// (raft_encoder.py BasicBlock: relu(norm2(conv2(·)) + x)), so the block's sum and ReLU cost no
+// launches of their own
 __global__ void in_apply_kernel(const float* __restrict__ x, const float* __restrict__ sc,
-                                const float* __restrict__ sh, float* __restrict__ y, int hw, int c,
-                                int relu, long long total4) {
+                                const float* __restrict__ sh, const float* __restrict__ res,
+                                float* __restrict__ y, int hw, int c, int relu, long long total4) {
   const int c4 = c / 4;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
     const int cq = (int)(i % c4) * 4;
@@ -929,10 +932,13 @@ __global__ void in_apply_kernel(const float* __restrict__ x, const float* __rest
     const size_t so = (size_t)img * c + cq;
     const floatx4 v = ((const floatx4*)x)[i];
     const floatx4 a = *(const floatx4*)(sc + so), b = *(const floatx4*)(sh + so);
+    floatx4 rv = {0.f, 0.f, 0.f, 0.f};
+    if (res) rv = ((const floatx4*)res)[i];
     floatx4 r;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       r[e] = v[e] * a[e] + b[e];
+      if (res) r[e] += rv[e];
       if (relu) r[e] = fmaxf(r[e], 0.f);
     }
     ((floatx4*)y)[i] = r;
@@ -942,7 +948,8 @@ __global__ void in_apply_kernel(const float* __restrict__ x, const float* __rest
 __global__ __launch_bounds__(256) void in_bwd_stats_kernel(const float* __restrict__ dy,
                                                            const float* __restrict__ x,
                                                            const float* __restrict__ sc,
-                                                           const float* __restrict__ sh, int hw,
+                                                           const float* __restrict__ sh,
+                                                           const float* __restrict__ ym, int hw,
                                                            int c, int chunks, int relu,
                                                            double* __restrict__ partial) {
   __shared__ double red[2][256][4];
@@ -958,10 +965,13 @@ __global__ __launch_bounds__(256) void in_bwd_stats_kernel(const float* __restri
     for (int p = p_begin + ps; p < p_end; p += ppp) {
       const floatx4 g = *(const floatx4*)(dy + base + (size_t)p * c);
       const floatx4 v = *(const floatx4*)(x + base + (size_t)p * c);
+      floatx4 mk = {1.f, 1.f, 1.f, 1.f};
+      if (ym) mk = *(const floatx4*)(ym + base + (size_t)p * c);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float xh = v[e] * a[e] + b[e];
-        const float gg = relu && !(xh > 0.f) ? 0.f : g[e];
+        // ReLU mask: of the block output y (residual form), else of x̂ itself
+        const float gg = ym ? (mk[e] > 0.f ? g[e] : 0.f) : (relu && !(xh > 0.f) ? 0.f : g[e]);
         s[e] += (double)gg;
         s2[e] += (double)gg * (double)xh;
       }
@@ -1006,7 +1016,8 @@ __global__ void in_bwd_finalize_kernel(const double* __restrict__ partial, int n
 
 __global__ void in_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                     const float* __restrict__ sc, const float* __restrict__ sh,
-                                    const float* __restrict__ mm, float* __restrict__ dx, int hw,
+                                    const float* __restrict__ mm, const float* __restrict__ ym,
+                                    float* __restrict__ dres, float* __restrict__ dx, int hw,
                                     int c, int relu, long long total4) {
   const int c4 = c / 4;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
@@ -1017,14 +1028,18 @@ __global__ void in_bwd_apply_kernel(const float* __restrict__ dy, const float* _
     const floatx4 a = *(const floatx4*)(sc + so), b = *(const floatx4*)(sh + so);
     const floatx4 m1 = *(const floatx4*)(mm + (size_t)img * 2 * c + cq);
     const floatx4 m2 = *(const floatx4*)(mm + (size_t)img * 2 * c + c + cq);
-    floatx4 r;
+    floatx4 mk = {1.f, 1.f, 1.f, 1.f};
+    if (ym) mk = ((const floatx4*)ym)[i];
+    floatx4 r, gr;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = v[e] * a[e] + b[e];
-      const float gg = relu && !(xh > 0.f) ? 0.f : g[e];
+      const float gg = ym ? (mk[e] > 0.f ? g[e] : 0.f) : (relu && !(xh > 0.f) ? 0.f : g[e]);
+      gr[e] = gg;
       r[e] = a[e] * (gg - m1[e] - xh * m2[e]);
     }
     ((floatx4*)dx)[i] = r;
+    if (dres) ((floatx4*)dres)[i] = gr;  // the identity branch's gradient (residual form)
   }
 }
 
@@ -1933,7 +1948,21 @@ SCFLOW_API int scflow_in_apply(const float* x, const float* scale, const float* 
   if (!aligned16(x) || !aligned16(y) || !aligned16(scale) || !aligned16(shift)) return SCFLOW_EALIGN;
   const long long total4 = (long long)n * hw * c / 4;
   const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
-  in_apply_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, scale, shift, y, hw, c, relu ? 1 : 0, total4);
+  in_apply_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, scale, shift, nullptr, y, hw, c,
+                                                            relu ? 1 : 0, total4);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_in_apply_residual(const float* x, const float* scale, const float* shift,
+                                        const float* res, float* y, int n, int hw, int c,
+                                        void* stream) {
+  if (!x || !scale || !shift || !res || !y || n <= 0 || hw <= 0 || c <= 0) return SCFLOW_EINVAL;
+  if (c % 4) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(x) || !aligned16(y) || !aligned16(res) || !aligned16(scale) || !aligned16(shift))
+    return SCFLOW_EALIGN;
+  const long long total4 = (long long)n * hw * c / 4;
+  const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
+  in_apply_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, scale, shift, res, y, hw, c, 1, total4);
   return scflow_launch_status();
 }
 
@@ -1948,12 +1977,34 @@ SCFLOW_API int scflow_in_backward(const float* dy, const float* x, const float* 
       !aligned16(mm))
     return SCFLOW_EALIGN;
   hipStream_t st = (hipStream_t)stream;
-  in_bwd_stats_kernel<<<dim3(chunks, n), 256, 0, st>>>(dy, x, scale, shift, hw, c, chunks, relu ? 1 : 0,
+  in_bwd_stats_kernel<<<dim3(chunks, n), 256, 0, st>>>(dy, x, scale, shift, nullptr, hw, c, chunks,
+                                                       relu ? 1 : 0, partial);
+  in_bwd_finalize_kernel<<<ceil_div((long long)n * c, 256), 256, 0, st>>>(partial, n, chunks, c, hw, mm);
+  const long long total4 = (long long)n * hw * c / 4;
+  const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
+  in_bwd_apply_kernel<<<blocks, 256, 0, st>>>(dy, x, scale, shift, mm, nullptr, nullptr, dx, hw, c,
+                                              relu ? 1 : 0, total4);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_in_backward_residual(const float* dy, const float* x, const float* scale,
+                                           const float* shift, const float* y, float* dx,
+                                           float* dres, double* partial, float* mm, int n, int hw,
+                                           int c, int chunks, void* stream) {
+  if (!dy || !x || !scale || !shift || !y || !dx || !dres || !partial || !mm || n <= 0 ||
+      hw <= 0 || c <= 0 || chunks <= 0)
+    return SCFLOW_EINVAL;
+  if (c % 4 || c > 256) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(dy) || !aligned16(x) || !aligned16(y) || !aligned16(dx) || !aligned16(dres) ||
+      !aligned16(scale) || !aligned16(shift) || !aligned16(mm))
+    return SCFLOW_EALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  in_bwd_stats_kernel<<<dim3(chunks, n), 256, 0, st>>>(dy, x, scale, shift, y, hw, c, chunks, 1,
                                                        partial);
   in_bwd_finalize_kernel<<<ceil_div((long long)n * c, 256), 256, 0, st>>>(partial, n, chunks, c, hw, mm);
   const long long total4 = (long long)n * hw * c / 4;
   const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
-  in_bwd_apply_kernel<<<blocks, 256, 0, st>>>(dy, x, scale, shift, mm, dx, hw, c, relu ? 1 : 0, total4);
+  in_bwd_apply_kernel<<<blocks, 256, 0, st>>>(dy, x, scale, shift, mm, y, dres, dx, hw, c, 1, total4);
   return scflow_launch_status();
 }
 

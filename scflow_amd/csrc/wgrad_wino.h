@@ -59,6 +59,16 @@ struct WwParams {
 
 typedef float floatx2w __attribute__((ext_vector_type(2)));
 
+// halo float4 slot j of thread tid: (pixel p of the 6 × 34 halo, first channel cq).  A wave-load
+// covers 8 consecutive pixels × 8 channel quads (one 32-channel half, 128 B per pixel), so the
+// transposing scalar LDS stores of a wave — bank (8·quad + 34·e + column) mod 64 — land on 64
+// distinct banks (16 quads × 4 pixels per wave put two lanes on every bank)
+__device__ __forceinline__ void ww_halo_slot(int tid, int j, int* p, int* cq) {
+  const int b = (tid >> 6) + 8 * j, l = tid & 63;  // wave-load block b (0..55): 8 px × 8 quads
+  *p = (b >> 1) * 8 + (l >> 3);
+  *cq = 4 * ((b & 1) * 8 + (l & 7));
+}
+
 __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float* __restrict__ slab,
                                                             float* __restrict__ bslab) {
   extern __shared__ float smem[];
@@ -108,9 +118,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       rd[j] = v;
     }
 #pragma unroll
-    for (int j = 0; j < WW_NX; ++j) {  // halo: 6 × 34 pixels × 16 ci quads
-      const int idx = tid + WW_NT * j;
-      const int p = idx >> 4, c = ci0 + 4 * (idx & 15);
+    for (int j = 0; j < WW_NX; ++j) {  // halo: 6 × 34 pixels × 16 ci quads (ww_halo_slot)
+      int p, cq;
+      ww_halo_slot(tid, j, &p, &cq);
+      const int c = ci0 + cq;
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (p < 6 * 34 && c < cin) {
         const int hr = p / 34, hc = p - hr * 34;
@@ -137,8 +148,8 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
     }
 #pragma unroll
     for (int j = 0; j < WW_NX; ++j) {
-      const int idx = tid + WW_NT * j;
-      const int p = idx >> 4, cq = 4 * (idx & 15);
+      int p, cq;
+      ww_halo_slot(tid, j, &p, &cq);
       if (p < 6 * 34) {
         const int hr = p / 34, hc = p - hr * 34;
         float* d = Xw + (hr * WWCI + cq) * WWX + hc;

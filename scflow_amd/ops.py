@@ -842,6 +842,24 @@ def in_backward(dy: Tensor, x: Tensor, scale: Tensor, shift: Tensor, dx: Tensor,
             _p(mm), n, hw, c, chunks, int(bool(relu)))
 
 
+def in_apply_residual(x: Tensor, scale: Tensor, shift: Tensor, res: Tensor, y: Tensor, n: int,
+                      hw: int, c: int) -> None:
+    """y = relu(x·scale + shift + res) (scflow_in_apply_residual: a residual block's tail)."""
+    _require(res, "res")
+    _launch("scflow_in_apply_residual", x, _p(x), _p(scale), _p(shift), _p(res), _p(y), n, hw, c)
+
+
+def in_backward_residual(dy: Tensor, x: Tensor, scale: Tensor, shift: Tensor, y: Tensor,
+                         dx: Tensor, dres: Tensor, n: int, hw: int, c: int) -> None:
+    """Backward of y = relu(IN(x) + res) (scflow_in_backward_residual): dres = dy·(y > 0), dx
+    the InstanceNorm backward of it."""
+    chunks = max(1, min(64, hw // 256))
+    partial = torch.empty(n * chunks * 2 * c, dtype=torch.float64, device=x.device)
+    mm = torch.empty(n * 2 * c, device=x.device)
+    _launch("scflow_in_backward_residual", x, _p(dy), _p(x), _p(scale), _p(shift), _p(y), _p(dx),
+            _p(dres), _p(partial), _p(mm), n, hw, c, chunks)
+
+
 def enc_apply(x: Tensor, scale: Tensor, shift: Tensor, out: Tensor, n: int, hw: int, c: int,
               id: Optional[Tensor] = None, id_scale: Optional[Tensor] = None,
               id_shift: Optional[Tensor] = None) -> None:

@@ -646,6 +646,40 @@ class _InstanceNormNHWC(torch.autograd.Function):
         return dx, None, None
 
 
+class _InstanceNormResidualNHWC(torch.autograd.Function):
+    """relu(InstanceNorm2d(x) + res): a residual block's tail (raft_encoder.py BasicBlock) as one
+    HIP pass forward (statistics + scflow_in_apply_residual) and a three-launch backward that
+    also writes the identity branch's gradient — instead of the norm's apply, the add, the ReLU
+    and the ReLU's backward as separate kernels."""
+
+    @staticmethod
+    def forward(ctx, x, res, eps):
+        x = x.contiguous()
+        res = res.contiguous()
+        n, h, w, c = x.shape
+        scale = torch.empty(n, c, device=x.device)
+        shift = torch.empty(n, c, device=x.device)
+        ops.enc_instance_norm_stats(x, n, h * w, c, scale, shift, eps)
+        y = torch.empty_like(x)
+        ops.in_apply_residual(x, scale, shift, res, y, n, h * w, c)
+        ctx.save_for_backward(x, scale, shift, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, scale, shift, y = ctx.saved_tensors
+        n, h, w, c = x.shape
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x)
+        ops.in_backward_residual(dy.contiguous(), x, scale, shift, y, dx, dres, n, h * w, c)
+        return dx, dres, None
+
+
+def instance_norm_residual_relu_nhwc(x: Tensor, res: Tensor, eps: float = 1e-5) -> Tensor:
+    """relu(InstanceNorm2d(affine=False)(x) + res) of channels-last tensors (HIP fwd + bwd)."""
+    return _InstanceNormResidualNHWC.apply(x, res, float(eps))
+
+
 def instance_norm_nhwc(x: Tensor, eps: float = 1e-5, relu: bool = False) -> Tensor:
     """InstanceNorm2d(affine=False) (then ReLU if ``relu``) of channels-last x, HIP fwd + bwd
     (channels a multiple of 4, at most 256)."""

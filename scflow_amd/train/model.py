@@ -22,8 +22,8 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import Chan
 from .functions import (begin_forward, conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid,
-                        group_norm_nhwc, gru_step, instance_norm_nhwc, linear, pose_update6,
-                        upsample_bilinear_ac)
+                        group_norm_nhwc, gru_step, instance_norm_nhwc,
+                        instance_norm_residual_relu_nhwc, linear, pose_update6, upsample_bilinear_ac)
 from .losses import LowRes, filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
@@ -79,9 +79,14 @@ def encoder_train(enc, x_nhwc: Tensor) -> Tensor:
     for name in enc.res_layers:
         for blk in getattr(enc, name):
             out = _norm(_conv(x, blk.conv1), blk.norm1, relu=True)
-            out = _norm(_conv(out, blk.conv2), blk.norm2)
             ident = x if blk.downsample is None else _norm(_conv(x, blk.downsample[0]), blk.downsample[1])
-            x = torch.relu(out + ident)
+            y2 = _conv(out, blk.conv2)
+            n2 = blk.norm2
+            if (isinstance(n2, torch.nn.InstanceNorm2d) and not n2.affine and y2.is_cuda and
+                    y2.shape[-1] % 4 == 0 and y2.shape[-1] <= 256 and ident.shape == y2.shape):
+                x = instance_norm_residual_relu_nhwc(y2, ident, n2.eps)  # norm + sum + ReLU
+            else:
+                x = torch.relu(_norm(y2, n2) + ident)
     return _conv(x, enc.conv2)
 
 

@@ -376,6 +376,28 @@ def test_instance_norm_nhwc_forward_backward(n, h, w, c, relu):
     _close(xg.grad, xr.grad, 1e-4, 1e-5, "instance norm input gradient")
 
 
+@pytest.mark.parametrize("n,h,w,c", [(4, 64, 64, 64), (3, 32, 32, 96), (2, 16, 16, 128)])
+def test_instance_norm_residual_relu(n, h, w, c):
+    """relu(InstanceNorm2d(x) + res) — the encoder residual block's tail in one HIP pass each way:
+    output and both input gradients against fp64 autograd."""
+    from scflow_amd.train.functions import instance_norm_residual_relu_nhwc
+    g = torch.Generator().manual_seed(33 + c)
+    x = torch.randn(n, h, w, c, generator=g) * 2 + 0.5
+    r = torch.randn(n, h, w, c, generator=g)
+    dy = torch.randn(n, h, w, c, generator=g)
+    xr = x.double().requires_grad_(True)
+    rr = r.double().requires_grad_(True)
+    yr = torch.relu(F.instance_norm(xr.permute(0, 3, 1, 2), eps=1e-5).permute(0, 2, 3, 1) + rr)
+    (yr * dy.double()).sum().backward()
+    xg = x.cuda().requires_grad_(True)
+    rg = r.cuda().requires_grad_(True)
+    y = instance_norm_residual_relu_nhwc(xg, rg, 1e-5)
+    (y * dy.cuda()).sum().backward()
+    _close(y, yr, 1e-5, 1e-5, "forward")
+    _close(xg.grad, xr.grad, 1e-4, 1e-5, "input gradient")
+    _close(rg.grad, rr.grad, 0.0, 0.0, "residual gradient")
+
+
 def test_conv2d_nhwc_split_matches_whole():
     """The split-output conv (GRU z | r) gives the whole conv's outputs and the same gradients,
     including when one half receives no gradient."""
