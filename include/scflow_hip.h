@@ -590,6 +590,13 @@ int scflow_in_apply(const float* x, const float* scale, const float* shift, floa
  * identity)): scflow_in_apply_residual: y = max(x·scale + shift + res, 0);
  * scflow_in_backward_residual: g = dy·(y > 0) → dres = g and dx = the InstanceNorm backward of g
  * (same workspace as scflow_in_backward). */
+/* scflow_colsum: out[c] (+)= Σ_r x[r·ld + c] for a row-major [rows][ld] matrix — the bias
+ * gradient Σ_p dY[p][c] of the 7×7 convs and the FC layers in training (deterministic: fixed
+ * row chunks, then the chunks in order).  workspace: scflow_colsum_workspace(rows, cols) floats
+ * (0 for rows ≤ 256: one pass). */
+int scflow_colsum(const float* x, int rows, int cols, int ld, float* out, int accumulate,
+                  float* workspace, void* stream);
+int scflow_colsum_workspace(int rows, int cols);
 int scflow_in_apply_residual(const float* x, const float* scale, const float* shift, const float* res,
                              float* y, int n, int hw, int c, void* stream);
 int scflow_in_backward_residual(const float* dy, const float* x, const float* scale,

@@ -157,6 +157,8 @@ SIGNATURES = {
     "scflow_corr_lookup_tiled": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_vp]),
     "scflow_in_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_colsum": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp]),
+    "scflow_colsum_workspace": (c_int, [c_int, c_int]),
     "scflow_in_apply_residual": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_in_backward_residual": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_int, c_int, c_int, c_int, c_vp]),

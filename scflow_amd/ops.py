@@ -842,6 +842,21 @@ def in_backward(dy: Tensor, x: Tensor, scale: Tensor, shift: Tensor, dx: Tensor,
             _p(mm), n, hw, c, chunks, int(bool(relu)))
 
 
+def colsum(x: Tensor, out: Tensor, accumulate: bool = False) -> Tensor:
+    """out (+)= x.sum(0) of a 2-D row-major x with unit column stride (scflow_colsum)."""
+    _require(out, "out")
+    _require(x, "x", contiguous=False)
+    if x.dim() != 2 or x.stride(1) != 1 or out.numel() != x.shape[1]:
+        raise ValueError(f"colsum: 2-D row-major x and a [{x.shape[-1]}] out expected")
+    rows, cols = x.shape
+    lib = _lib.load()
+    nws = int(lib.scflow_colsum_workspace(rows, cols))
+    ws = torch.empty(max(1, nws), device=x.device) if nws > 0 else None
+    check(lib.scflow_colsum(_p(x), rows, cols, x.stride(0), _p(out), int(accumulate), _p(ws),
+                            _stream(x)), "scflow_colsum")
+    return out
+
+
 def in_apply_residual(x: Tensor, scale: Tensor, shift: Tensor, res: Tensor, y: Tensor, n: int,
                       hw: int, c: int) -> None:
     """y = relu(x·scale + shift + res) (scflow_in_apply_residual: a residual block's tail)."""

@@ -255,10 +255,7 @@ def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int,
     beta = 1.0 if accumulate else 0.0
     ops.gemm(g2.t(), cols, out=dw.view(cout, cin * kh * kw), beta=beta)
     if with_bias:
-        if accumulate:
-            db += g2.sum(0)
-        else:
-            torch.sum(g2, 0, out=db)
+        ops.colsum(g2, db, accumulate=accumulate)
     return dw, db
 
 
@@ -924,11 +921,11 @@ class _Linear(torch.autograd.Function):
             else:
                 dw = ops.gemm(dy.t(), x)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy.sum(0)
             sb = _grad_sink(ctx.bias)
             if sb is not None:
-                sb += db
-                db = None
+                ops.colsum(dy, sb, accumulate=True)
+            else:
+                db = ops.colsum(dy, torch.empty(dy.shape[1], device=dy.device))
         return dx, dw, db
 
 

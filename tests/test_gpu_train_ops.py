@@ -236,6 +236,22 @@ def test_conv_wgrad_batched(case):
         _close(db - 1, dbr, 1e-5, 1e-4 * np.sqrt(segs * n * h * w), "db")
 
 
+@pytest.mark.parametrize("rows,cols,acc", [(16384, 128, False), (16, 1024, True), (524288, 64, True),
+                                           (1000, 3, False), (300, 257, True)])
+def test_colsum(rows, cols, acc):
+    """scflow_colsum (bias gradients) against an fp64 column sum, with a row-major view whose
+    row stride exceeds its width; accumulate onto an existing vector."""
+    from scflow_amd import ops
+    g = torch.Generator().manual_seed(rows + cols)
+    base = torch.randn(rows, cols + 5, generator=g)
+    x = base[:, 2:2 + cols]
+    out0 = torch.randn(cols, generator=g)
+    out = out0.clone().cuda()
+    ops.colsum(base.cuda()[:, 2:2 + cols], out, accumulate=acc)
+    ref = x.double().sum(0) + (out0.double() if acc else 0)
+    _close(out, ref, 1e-6, 1e-5 * np.sqrt(rows), "colsum")
+
+
 def test_corr_pyramid_backward():
     from scflow_amd import ops
     from scflow_amd.train.functions import corr_pyramid
