@@ -661,7 +661,8 @@ typedef struct {
   const float* colors;   /* [total_verts][3] vertex colours in [0, 1] */
   const int* faces;      /* [total_faces][3] packed vertex indices */
   const int* vert_img;   /* [total_verts] image of each packed vertex */
-  const int* face_img;   /* [total_faces] image of each packed face */
+  const int* face_img;   /* [total_faces] image of each packed face, non-decreasing (faces packed
+                            image by image: the rasteriser bins each image's contiguous range) */
   const float* R;        /* [n_img][3][3] OpenCV rotation (object → camera) */
   const float* t;        /* [n_img][3] */
   const float* K;        /* [n_img][3][3] intrinsics */

@@ -16,10 +16,10 @@
 //   render_project_kernel — one thread per packed vertex: NDC + depth into the per-image vertex
 //     slots, and the image's minimum vertex depth (a wave-level min per image, then one atomicMin
 //     on the float bits per image and wave; depths > 0) for the light placement.
-//   render_raster_kernel  — one thread per packed face: every pixel centre of its screen bbox is
-//     tested; hits do a 64-bit atomicMin of (depth bits << 32 | face) into the image's z-buffer
-//     (positive floats order like their bit patterns), so the nearest face wins and equal depths
-//     resolve to the lower index, independent of thread order.
+//   render_tile_kernel    — one workgroup per 16×16 screen tile of an image: the image's faces
+//     whose screen bbox meets the tile are binned into LDS, and each pixel keeps the minimum of
+//     (depth bits << 32 | face) over them (positive floats order like their bit patterns), so the
+//     nearest face wins and equal depths resolve to the lower index, independent of order.
 //   render_shade_kernel   — one thread per pixel: decodes the winner, recomputes its perspective-
 //     correct barycentrics and depth, writes zbuf / pix_to_face / bary, interpolates position,
 //     normal and vertex colour and applies pytorch3d's Phong model (ambient + diffuse·texel +
@@ -94,39 +94,93 @@ __device__ __forceinline__ Bary bary_at(float px, float py, const float* p0, con
   return r;
 }
 
-__global__ void render_raster_kernel(scflow_render_args a, const int* __restrict__ face_img,
-                                     const float* __restrict__ vproj,
-                                     unsigned long long* __restrict__ zf, int nfaces) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nfaces) return;
-  const int n = face_img[f];
-  const int S = a.size;
-  const float* p0 = vproj + 3 * a.faces[3 * f];
-  const float* p1 = vproj + 3 * a.faces[3 * f + 1];
-  const float* p2 = vproj + 3 * a.faces[3 * f + 2];
-  if (p0[2] <= 0.f && p1[2] <= 0.f && p2[2] <= 0.f) return;  // entirely behind the camera
+// the pixel range (margined, clamped screen bbox) a face is tested on; false when culled
+// (entirely behind the camera) or off-screen
+__device__ __forceinline__ bool face_bbox(const float* p0, const float* p1, const float* p2, int S,
+                                          int* c_lo, int* c_hi, int* r_lo, int* r_hi) {
+  if (p0[2] <= 0.f && p1[2] <= 0.f && p2[2] <= 0.f) return false;  // entirely behind the camera
   const float xmin = fminf(p0[0], fminf(p1[0], p2[0])), xmax = fmaxf(p0[0], fmaxf(p1[0], p2[0]));
   const float ymin = fminf(p0[1], fminf(p1[1], p2[1])), ymax = fmaxf(p0[1], fmaxf(p1[1], p2[1]));
   // pixel c samples x = 1 − (2c+1)/S  ⇒  c = ((1 − x)·S − 1)/2 (one pixel of margin)
-  int c_lo = (int)floorf(((1.f - xmax) * S - 1.f) * 0.5f) - 1;
-  int c_hi = (int)ceilf(((1.f - xmin) * S - 1.f) * 0.5f) + 1;
-  int r_lo = (int)floorf(((1.f - ymax) * S - 1.f) * 0.5f) - 1;
-  int r_hi = (int)ceilf(((1.f - ymin) * S - 1.f) * 0.5f) + 1;
-  c_lo = max(c_lo, 0);
-  r_lo = max(r_lo, 0);
-  c_hi = min(c_hi, S - 1);
-  r_hi = min(r_hi, S - 1);
-  unsigned long long* img = zf + (size_t)n * S * S;
-  for (int r = r_lo; r <= r_hi; ++r) {
-    const float py = 1.f - (float)(2 * r + 1) / (float)S;
-    for (int c = c_lo; c <= c_hi; ++c) {
-      const float px = 1.f - (float)(2 * c + 1) / (float)S;
-      const Bary b = bary_at(px, py, p0, p1, p2);
-      if (!b.inside) continue;
-      const unsigned long long key = ((unsigned long long)__float_as_uint(b.pz) << 32) | (unsigned)f;
-      atomicMin(img + r * S + c, key);
-    }
+  *c_lo = max((int)floorf(((1.f - xmax) * S - 1.f) * 0.5f) - 1, 0);
+  *c_hi = min((int)ceilf(((1.f - xmin) * S - 1.f) * 0.5f) + 1, S - 1);
+  *r_lo = max((int)floorf(((1.f - ymax) * S - 1.f) * 0.5f) - 1, 0);
+  *r_hi = min((int)ceilf(((1.f - ymin) * S - 1.f) * 0.5f) + 1, S - 1);
+  return *c_lo <= *c_hi && *r_lo <= *r_hi;
+}
+
+// Screen-binned rasterisation: workgroup = one 16×16 pixel tile of one image, thread = pixel.
+// The image's faces (a contiguous range of the non-decreasing face_img, found by binary search)
+// are walked 256 at a time: each thread sets up one face (bbox), the faces whose bbox meets the
+// tile are compacted into LDS (index, projected vertices, bbox), then every pixel tests those
+// against its centre with the same bbox and barycentric rules as a per-face rasteriser and keeps
+// the minimum (depth bits << 32 | face) key — nearest face, ties to the lower index, independent
+// of order — written once per pixel: no global atomics and no z-buffer clear.
+constexpr int RT = 16;
+
+__device__ __forceinline__ int lower_bound_i(const int* __restrict__ v, int n, int key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (v[mid] < key) lo = mid + 1; else hi = mid;
   }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void render_tile_kernel(scflow_render_args a,
+                                                          const int* __restrict__ face_img,
+                                                          const float* __restrict__ vproj,
+                                                          unsigned long long* __restrict__ zf) {
+  __shared__ int range[2];
+  __shared__ int cnt;
+  __shared__ int lf[256];
+  __shared__ int lbox[256][4];
+  __shared__ float lv[256][9];
+  const int S = a.size;
+  const int tiles_x = (S + RT - 1) / RT;
+  const int n = blockIdx.y;
+  const int tx0 = (blockIdx.x % tiles_x) * RT, ty0 = (blockIdx.x / tiles_x) * RT;
+  if (threadIdx.x < 2) range[threadIdx.x] = lower_bound_i(face_img, a.total_faces, n + (int)threadIdx.x);
+  const int r = ty0 + (int)threadIdx.x / RT, c = tx0 + (int)threadIdx.x % RT;
+  const float px = 1.f - (float)(2 * c + 1) / (float)S;
+  const float py = 1.f - (float)(2 * r + 1) / (float)S;
+  unsigned long long best = ~0ull;
+  __syncthreads();
+  const int fb = range[0], fe = range[1];
+  for (int f0 = fb; f0 < fe; f0 += 256) {
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    const int f = f0 + (int)threadIdx.x;
+    if (f < fe) {
+      const float* p0 = vproj + 3 * a.faces[3 * f];
+      const float* p1 = vproj + 3 * a.faces[3 * f + 1];
+      const float* p2 = vproj + 3 * a.faces[3 * f + 2];
+      int cl, ch, rl, rh;
+      if (face_bbox(p0, p1, p2, S, &cl, &ch, &rl, &rh) && ch >= tx0 && cl < tx0 + RT &&
+          rh >= ty0 && rl < ty0 + RT) {
+        const int k = atomicAdd(&cnt, 1);  // LDS counter: the order does not matter (min key)
+        lf[k] = f;
+        lbox[k][0] = cl, lbox[k][1] = ch, lbox[k][2] = rl, lbox[k][3] = rh;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          lv[k][e] = p0[e];
+          lv[k][3 + e] = p1[e];
+          lv[k][6 + e] = p2[e];
+        }
+      }
+    }
+    __syncthreads();
+    const int m = cnt;
+    for (int k = 0; k < m; ++k) {
+      if (c < lbox[k][0] || c > lbox[k][1] || r < lbox[k][2] || r > lbox[k][3]) continue;
+      const Bary b = bary_at(px, py, &lv[k][0], &lv[k][3], &lv[k][6]);
+      if (!b.inside) continue;
+      const unsigned long long key = ((unsigned long long)__float_as_uint(b.pz) << 32) | (unsigned)lf[k];
+      best = key < best ? key : best;
+    }
+    __syncthreads();  // the list is rebuilt for the next 256 faces
+  }
+  if (r < S && c < S) zf[((size_t)n * S + r) * S + c] = best;
 }
 
 __device__ __forceinline__ void normalize3(float* v, float eps = 1e-6f) {
@@ -241,14 +295,12 @@ SCFLOW_API int scflow_render(const scflow_render_args* args, void* stream) {
   unsigned long long* zf = (unsigned long long*)a.workspace;
   float* vproj = (float*)(zf + npix);
   unsigned* zmin = (unsigned*)(vproj + 3 * (size_t)a.total_verts);
-  hipError_t e = hipMemsetAsync(zf, 0xff, npix * 8, st);
-  if (e == hipSuccess) e = hipMemsetAsync(zmin, 0x7f, (size_t)a.n_img * 4, st);  // +large float
+  hipError_t e = hipMemsetAsync(zmin, 0x7f, (size_t)a.n_img * 4, st);  // +large float
   if (e != hipSuccess) return (int)e;
   render_project_kernel<<<(a.total_verts + 255) / 256, 256, 0, st>>>(a, a.vert_img, vproj, zmin,
                                                                       a.total_verts);
-  if (a.total_faces > 0)
-    render_raster_kernel<<<(a.total_faces + 127) / 128, 128, 0, st>>>(a, a.face_img, vproj, zf,
-                                                                       a.total_faces);
+  const int tiles = ((a.size + RT - 1) / RT) * ((a.size + RT - 1) / RT);
+  render_tile_kernel<<<dim3(tiles, a.n_img), 256, 0, st>>>(a, a.face_img, vproj, zf);
   render_shade_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(a, vproj, zf, zmin, a.n_img);
   return scflow_launch_status();
 }
