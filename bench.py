@@ -123,9 +123,12 @@ def time_steps(step, steps, warmup, world, dev):
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
-# measured on the box: tools/micro/stream.hip, 16-B/lane copy over 2 GiB buffers (8× the Infinity
-# Cache), best of 20 — profiles/r03_stream.txt.  HBM entries report frac against both.
-HBM_MEASURED_GBS = 6290.0
+# measured on the box: tools/micro/stream.hip over 2 GiB buffers (8× the Infinity Cache), best of
+# 20 (profiles/r03_stream.txt): 16-B/lane read 6412 GB/s (the ceiling used here: the HBM-bound
+# kernels are read-dominated), copy 4596, write 4214; the lookup's own access pattern (16-lane
+# 64-B pieces in scattered order) 2803, 128-B pieces 3537.  HBM entries report frac against both.
+HBM_MEASURED_GBS = 6412.0
+GATHER64_MEASURED_GBS = 2803.0  # stream.hip gather_b32: the lookup's access pattern
 # every conv_wino_kernel launch of one refinement iteration (decoder.kernel_hooks names)
 WINO_LAUNCHES = ("heads", "corr_net1", "out_net", "flow_net1", "dflow1", "mask_enc1")
 
@@ -153,6 +156,9 @@ def conv_roofline(kernel, parts, timers, m_px, traffic=None, alg_bytes=None):
     ex = [r.mfma_flops(m_px, c0, c1) for _, r, c0, c1 in parts]
     di = [r.flops(m_px) for _, r, _, _ in parts]
     t = sum(ms) * 1e-3
+    if t <= 0:  # no timings (--no-kernel-timer: counter runs)
+        return {"kernel": kernel, "bound": "mfma", "achieved": None, "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": None, "traffic": traffic}
     ach = sum(ex) / t / 1e12
     out = {"kernel": kernel, "bound": "mfma", "achieved": round(ach, 2),
            "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
@@ -191,7 +197,9 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
             ("corr_lookup", "corr_lookup", "corr_lookup_lds_kernel<4> (a2%s)" % (", tiled pyramid"
                                                                               if tiled else ""),
              "hbm", lookup_bytes),
-            ("pose_flow", "pose_step", "pose_step_kernel (a8+a10+a11)" if fused_tail
+            ("pose_flow", "pose_step", "pose_step_kernel (a8+a10+a11), its full-resolution launch: "
+             "queued on the side stream behind the next iteration's join, so it shares the CUs "
+             "with out_net / the GRU (a rate under contention, not the kernel alone)" if fused_tail
              else "pose_flow_kernel (a8+a10)", "hbm", flow_bytes),
             # the persistent pose-head tail (GN 1 → convs 2-3 → FCs → heads) + the pose step:
             # bytes = the pose step's 36 B/pixel + the pose head's weights after conv 1 (read once)
@@ -223,6 +231,11 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
             if tr:
                 e["traffic_over_algorithmic"] = round(tr / amount, 3)
                 e["traffic_gbs"] = round(tr / (ms * 1e-3) / 1e9, 1)
+            if name == "corr_lookup":  # scattered 64-B window pieces: their measured ceiling
+                e["access_pattern_ceiling_gbs"] = GATHER64_MEASURED_GBS
+                if tr:
+                    e["traffic_frac_of_pattern_ceiling"] = round(tr / (ms * 1e-3) / 1e9 /
+                                                                 GATHER64_MEASURED_GBS, 4)
         out.append(e)
     return out
 
