@@ -3,7 +3,7 @@
 # FETCH_SIZE and WRITE_SIZE passes (traffic per launch) and one SQ pass, each its own run.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out/lkc4; mkdir -p $OUT; cd /tmp; export TMPDIR=/tmp
 B="--steps 2 --warmup 1 --no-cpu-baseline --e2e-batch 0 --train-batch 0 --no-kernel-timer --batch 32 --size 512 --iters 12"
-for v in tiled rowmajor; do
+for v in ${VARIANTS:-tiled rowmajor}; do
   X=""; [ $v = rowmajor ] && X="--no-tiled-pyramid"
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/f_$v -o run -- python3 $R/bench.py $B $X > /dev/null 2> $OUT/f_$v.err || exit 1
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/w_$v -o run -- python3 $R/bench.py $B $X > /dev/null 2> $OUT/w_$v.err || exit 1
