@@ -629,9 +629,11 @@ int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream);
  * shaped segments in one launch and one split reduction — the decoder's per-iteration uses of
  * one conv (its 8 refinement iterations under SCFlowRefiner.loss → backward,
  * scflow_refiner.py:182-256).  `args` describes one segment (n images; its dy / src0 / src1 are
- * ignored), dys[i] / src0s[i] / src1s[i] are segment i's bases with args' strides.  Shapes: the
- * Winograd ones (3×3 stride 1 pad 1; 1×5 / 5×1 stride 1 pad 2); others return
- * SCFLOW_EUNSUPPORTED.  `workspace`: scflow_conv_wgrad_workspace() of args with n·segs images. */
+ * ignored), dys[i] / src0s[i] / src1s[i] are segment i's bases with args' strides.  Shapes:
+ * scflow_conv_wgrad's (Winograd 3×3 / 1×5 / 5×1, 1×1 stride 1–2, the implicit-GEMM 3×3, the
+ * thin kernels for ≤ 4 channels on one side) plus thin 7×7 (the flow encoders' 2 → 128); others
+ * return SCFLOW_EUNSUPPORTED.  `workspace`: scflow_conv_wgrad_workspace() of args with n·segs
+ * images (it sizes the partial sums for any segment count). */
 int scflow_conv_wgrad_batched(const scflow_wgrad_args* args, int segs, const float* const* dys,
                               const float* const* src0s, const float* const* src1s, void* stream);
 int scflow_corr_lookup_backward(const float* dout, int out_layout, int out_stride, const float* flow,

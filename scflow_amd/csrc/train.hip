@@ -324,6 +324,14 @@ struct WgSegs {
   const float* src1[WG_MAXSEG];
 };
 
+// segment s's pointer, selected with uniform compares (no dynamic kernarg indexing)
+__device__ __forceinline__ const float* wg_pick(const float* const (&arr)[WG_MAXSEG], int s) {
+  const float* p = arr[0];
+#pragma unroll
+  for (int i = 1; i < WG_MAXSEG; ++i) p = s == i ? arr[i] : p;
+  return p;
+}
+
 inline void wg_single_seg(const scflow_wgrad_args& a, WgSegs* s) {
   s->nimg = a.n;
   s->dy[0] = a.dy;
@@ -634,6 +642,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
 
 #include "wgrad_wino.h"
 #include "wgrad_wino5.h"
+#include "wgrad_1x1.h"
 
 bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
   if (a.stride != 1 && a.stride != 2) return false;
@@ -705,21 +714,28 @@ bool wgrad_geometry(const scflow_wgrad_args& a, WgParams* P, int* splits) {
 //   !THIN_CO (cin ≤ T): acc[ci][tx][e] += dy[p][4g + e]   · x[p + (ty, tx)][ci]
 // The streams are summed through LDS in a fixed order and each workgroup writes its partial
 // dw (torch layout) to a slab row; wthin_reduce_kernel sums the rows in a fixed order.
+// Segments (scflow_conv_wgrad_batched): grid.z = segment, each with its own dY / input bases
+// and nbp pixel runs of its nimg images; slab row = z·nbp + x.
 struct WtParams {
   scflow_wgrad_args a;
   int oh, ow, cin, C, G, lg2, ppb, nbp, thin_co;
+  int nseg, nimg;  // segments, images per segment
+  WgSegs sg;
 };
 
-bool wthin_geometry(const scflow_wgrad_args& a, WtParams* P) {
+// nseg = 0: the workspace query (the whole walk as one segment, rows for any segment count).
+// 7×7 (the stem, the flow encoders' 2→128) only in a batched call (seven): a single use is
+// faster on im2col + GEMM
+bool wthin_geometry(const scflow_wgrad_args& a, WtParams* P, int nseg = 1, bool seven = false) {
   static const bool off = [] {
     const char* e = getenv("SCFLOW_WGRAD_THIN");
     return e && e[0] == '0';
   }();
   if (off) return false;
   const int cin = a.cin0 + a.cin1;
-  // 7×7 (the stem, the flow encoders' 2→128) stays on im2col + GEMM: measured faster there
-  if (a.kw != 1 && a.kw != 3 && a.kw != 5) return false;
-  if (a.kh < 1 || a.kh > 5 || a.stride < 1 || a.stride > 2) return false;
+  const int kmax = seven ? 7 : 5;
+  if (a.kw != 1 && a.kw != 3 && a.kw != 5 && !(seven && a.kw == 7)) return false;
+  if (a.kh < 1 || a.kh > kmax || a.stride < 1 || a.stride > 2) return false;
   const bool thin_co = a.cout <= 4 && cin % 4 == 0 && a.cin0 % 4 == 0 && cin <= 256 &&
                        a.s0 % 4 == 0 && aligned16(a.src0) &&
                        (a.cin1 == 0 || (a.s1 % 4 == 0 && aligned16(a.src1)));
@@ -737,11 +753,17 @@ bool wthin_geometry(const scflow_wgrad_args& a, WtParams* P) {
   P->lg2 = 0;
   while ((1 << P->lg2) < P->G) ++P->lg2;
   const long long pix = (long long)a.n * P->oh * P->ow;
-  // ≥ 64 pixels per workgroup, at most 512 workgroups per kernel row (the slab rows)
+  // ≥ 64 pixels per workgroup, at most 512 workgroups per kernel row (the slab rows) + one per
+  // extra segment
   long long ppb = (pix + 511) / 512;
   if (ppb < 64) ppb = 64;
   P->ppb = (int)ppb;
-  P->nbp = (int)((pix + ppb - 1) / ppb);
+  const int ns = nseg < 1 ? 1 : nseg;
+  P->nseg = ns;
+  P->nimg = a.n / ns;
+  const long long spix = (long long)P->nimg * P->oh * P->ow;
+  P->nbp = (int)((spix + ppb - 1) / ppb);
+  if (nseg == 0) P->nbp += WG_MAXSEG;  // the query: ns·⌈spix/ppb⌉ ≤ ⌈pix/ppb⌉ + ns
   return true;
 }
 
@@ -757,9 +779,12 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __re
   const bool act = g < P.G;
   const int ty = blockIdx.y;
   const long long ohw = (long long)P.oh * P.ow;
-  const long long pix = a.n * ohw;
+  const long long pix = P.nimg * ohw;
   const long long pb0 = (long long)blockIdx.x * P.ppb;
   const long long pb1 = pb0 + P.ppb < pix ? pb0 + P.ppb : pix;
+  const float* dyp = wg_pick(P.sg.dy, blockIdx.z);
+  const float* s0p = wg_pick(P.sg.src0, blockIdx.z);
+  const float* s1p = wg_pick(P.sg.src1, blockIdx.z);
   const int tn = THIN_CO ? a.cout : P.cin;  // thin channels actually present
   float acc[NA];
 #pragma unroll
@@ -777,7 +802,7 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __re
       if (THIN_CO) {
         float d[T];
 #pragma unroll
-        for (int t = 0; t < T; ++t) d[t] = t < tn ? a.dy[p * a.sdy + t] : 0.f;
+        for (int t = 0; t < T; ++t) d[t] = t < tn ? dyp[p * a.sdy + t] : 0.f;
 #pragma unroll
         for (int t = 0; t < T; ++t) acc[T * KW * 4 + t] += d[t];
 #pragma unroll
@@ -786,8 +811,8 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __re
           floatx4 v = {0.f, 0.f, 0.f, 0.f};
           if (rok && ix >= 0 && ix < a.w) {
             const size_t q = rowpix + ix;
-            v = c4 < a.cin0 ? *(const floatx4*)(a.src0 + q * a.s0 + c4)
-                            : *(const floatx4*)(a.src1 + q * a.s1 + (c4 - a.cin0));
+            v = c4 < a.cin0 ? *(const floatx4*)(s0p + q * a.s0 + c4)
+                            : *(const floatx4*)(s1p + q * a.s1 + (c4 - a.cin0));
           }
 #pragma unroll
           for (int t = 0; t < T; ++t)
@@ -795,7 +820,7 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __re
             for (int e = 0; e < 4; ++e) acc[(t * KW + tx) * 4 + e] += d[t] * v[e];
         }
       } else {
-        const floatx4 d = *(const floatx4*)(a.dy + p * a.sdy + c4);
+        const floatx4 d = *(const floatx4*)(dyp + p * a.sdy + c4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[T * KW * 4 + e] += d[e];
 #pragma unroll
@@ -805,7 +830,7 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __re
           const size_t q = rowpix + ix;
 #pragma unroll
           for (int t = 0; t < T; ++t) {
-            const float xv = ok && t < tn ? a.src0[q * a.s0 + t] : 0.f;
+            const float xv = ok && t < tn ? s0p[q * a.s0 + t] : 0.f;
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[(t * KW + tx) * 4 + e] += d[e] * xv;
           }
@@ -815,7 +840,8 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __re
   }
   // Σ over the streams (fixed order), 16 accumulators per round; lanes st == 0 write the row
   const int taps = a.kh * a.kw;
-  float* row = slab + (size_t)blockIdx.x * a.cout * P.cin * taps;
+  const size_t srow = (size_t)blockIdx.z * P.nbp + blockIdx.x;
+  float* row = slab + srow * a.cout * P.cin * taps;
 #pragma unroll
   for (int r0 = 0; r0 < NA; r0 += 16) {
 #pragma unroll
@@ -838,9 +864,9 @@ __global__ __launch_bounds__(256) void wgrad_thin_kernel(WtParams P, float* __re
         } else if (bslab && ty == 0) {
           const int e = i - T * KW * 4;
           if (THIN_CO) {
-            if (g == 0 && e < tn) bslab[(size_t)blockIdx.x * a.cout + e] = s;
+            if (g == 0 && e < tn) bslab[srow * a.cout + e] = s;
           } else {
-            bslab[(size_t)blockIdx.x * a.cout + c4 + e] = s;
+            bslab[srow * a.cout + c4 + e] = s;
           }
         }
       }
@@ -877,17 +903,20 @@ __global__ __launch_bounds__(256) void wthin_reduce_kernel(const float* __restri
 
 long long wthin_workspace(const WtParams& P) {
   const scflow_wgrad_args& a = P.a;
-  return (long long)P.nbp * a.cout * P.cin * a.kh * a.kw + (long long)P.nbp * a.cout;
+  const long long rows = (long long)P.nseg * P.nbp;
+  return rows * a.cout * P.cin * a.kh * a.kw + rows * a.cout;
 }
 
 int wthin_launch(const WtParams& P, hipStream_t st) {
   const scflow_wgrad_args& a = P.a;
+  if (a.workspace_floats < wthin_workspace(P)) return SCFLOW_EINVAL;
   const bool thin_co = P.thin_co != 0;
   const int tn = thin_co ? a.cout : P.cin;
+  const int rows = P.nseg * P.nbp;
   float* slab = a.workspace;
   const long long total = (long long)a.cout * P.cin * a.kh * a.kw;
-  float* bslab = a.db ? a.workspace + (size_t)P.nbp * total : nullptr;
-  const dim3 grid((unsigned)P.nbp, (unsigned)a.kh);
+  float* bslab = a.db ? a.workspace + (size_t)rows * total : nullptr;
+  const dim3 grid((unsigned)P.nbp, (unsigned)a.kh, (unsigned)P.nseg);
 #define SCFLOW_WT(T_, KW_)                                                                   \
   if (a.kw == KW_ && tn <= T_) {                                                             \
     if (thin_co)                                                                             \
@@ -898,14 +927,15 @@ int wthin_launch(const WtParams& P, hipStream_t st) {
   SCFLOW_WT(1, 1) SCFLOW_WT(2, 1) SCFLOW_WT(4, 1)
   SCFLOW_WT(1, 3) SCFLOW_WT(2, 3) SCFLOW_WT(4, 3)
   SCFLOW_WT(1, 5) SCFLOW_WT(2, 5) SCFLOW_WT(4, 5)
+  SCFLOW_WT(1, 7) SCFLOW_WT(2, 7) SCFLOW_WT(4, 7)
   return SCFLOW_EUNSUPPORTED;
 #undef SCFLOW_WT
   int rc = scflow_launch_status();
   if (rc != SCFLOW_OK) return rc;
-  wthin_reduce_kernel<<<(unsigned)((total + 15) / 16), 256, 0, st>>>(slab, P.nbp, total, a.dw,
+  wthin_reduce_kernel<<<(unsigned)((total + 15) / 16), 256, 0, st>>>(slab, rows, total, a.dw,
                                                                      a.accumulate);
   if (a.db)
-    wthin_reduce_kernel<<<(unsigned)((a.cout + 15) / 16), 256, 0, st>>>(bslab, P.nbp, a.cout, a.db,
+    wthin_reduce_kernel<<<(unsigned)((a.cout + 15) / 16), 256, 0, st>>>(bslab, rows, a.cout, a.db,
                                                                          a.accumulate);
   return scflow_launch_status();
 }
@@ -1708,7 +1738,7 @@ SCFLOW_API int scflow_gru_gate_backward_r(const float* drh, int sdrh, const floa
 SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats) {
   if (!args || !floats) return SCFLOW_EINVAL;
   WtParams Q;
-  if (wthin_geometry(*args, &Q)) {
+  if (wthin_geometry(*args, &Q, 0, true)) {  // rows for a batched call of any segment count
     *floats = wthin_workspace(Q);
     return SCFLOW_OK;
   }
@@ -1720,6 +1750,11 @@ SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long l
   W5wParams R5;
   if (wwino5_geometry(*args, &R5)) {
     *floats = wwino5_workspace(R5);
+    return SCFLOW_OK;
+  }
+  W1Params R1;
+  if (w1_geometry(*args, 1, &R1)) {
+    *floats = w1_workspace(R1);
     return SCFLOW_OK;
   }
   WgParams P;
@@ -1837,7 +1872,15 @@ SCFLOW_API int scflow_conv_wgrad_batched(const scflow_wgrad_args* args, int segs
     return wwino5_launch(R5, (hipStream_t)stream);
   }
   WtParams Q;
-  if (wthin_geometry(t, &Q)) return SCFLOW_EUNSUPPORTED;  // thin shapes: per-segment launches
+  if (wthin_geometry(t, &Q, segs, true)) {
+    Q.sg = sg;
+    return wthin_launch(Q, (hipStream_t)stream);
+  }
+  W1Params R1;
+  if (w1_geometry(t, segs, &R1)) {
+    R1.sg = sg;
+    return w1_launch(R1, (hipStream_t)stream);
+  }
   return wgrad_direct_launch(t, sg, (hipStream_t)stream);
 }
 
@@ -1850,7 +1893,7 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
     return SCFLOW_EINVAL;
   WtParams Q;
   if (wthin_geometry(a, &Q)) {
-    if (a.workspace_floats < wthin_workspace(Q)) return SCFLOW_EINVAL;
+    wg_single_seg(a, &Q.sg);
     return wthin_launch(Q, (hipStream_t)stream);
   }
   WwParams R;
@@ -1864,6 +1907,11 @@ SCFLOW_API int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream) {
     if (a.workspace_floats < wwino5_workspace(R5)) return SCFLOW_EINVAL;
     wg_single_seg(a, &R5.sg);
     return wwino5_launch(R5, (hipStream_t)stream);
+  }
+  W1Params R1;
+  if (w1_geometry(a, 1, &R1)) {
+    wg_single_seg(a, &R1.sg);
+    return w1_launch(R1, (hipStream_t)stream);
   }
   WgSegs sg;
   wg_single_seg(a, &sg);

@@ -275,9 +275,10 @@ def begin_forward() -> None:
 
 
 def _batchable(kh: int, kw: int, s: int, ph: int, pw: int) -> bool:
-    """Shapes scflow_conv_wgrad_batched takes (the Winograd and implicit-GEMM weight gradients;
-    thin and 7×7 ones are recorded too and fall back to one launch per use)."""
-    return (kh, kw) in ((1, 1), (3, 3), (1, 5), (5, 1)) and s in (1, 2)
+    """Shapes scflow_conv_wgrad_batched takes (the Winograd, 1×1, implicit-GEMM and thin weight
+    gradients — 7×7 ones through the thin kernel when one side has ≤ 4 channels; shapes a batched
+    call refuses fall back to one launch per use)."""
+    return (kh, kw) in ((1, 1), (3, 3), (1, 5), (5, 1), (7, 7)) and s in (1, 2)
 
 
 def _use_holder(w: Tensor) -> dict:

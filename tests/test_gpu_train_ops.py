@@ -236,6 +236,49 @@ def test_conv_wgrad_batched(case):
         _close(db - 1, dbr, 1e-5, 1e-4 * np.sqrt(segs * n * h * w), "db")
 
 
+@pytest.mark.parametrize("case", [
+    # (segs, n, h, w, c0, c1, cout, k, stride, bias)
+    (8, 2, 32, 32, 324, 0, 256, 1, 1, True),    # corr_net.0 1×1 over 8 iterations (wgrad_1x1.h)
+    (3, 2, 32, 32, 128, 64, 96, 1, 1, False),   # 1×1, two sources, ragged 128-blocks
+    (2, 2, 33, 31, 64, 0, 96, 1, 2, True),      # 1×1 / 2 on odd sizes (encoder downsample)
+    (8, 2, 32, 32, 128, 128, 2, 3, 1, True),    # thin: flow head 3×3 256 → 2, Chan second source
+    (8, 2, 32, 32, 256, 0, 1, 1, 1, True),      # thin: mask head 1×1 256 → 1
+    (8, 2, 32, 32, 1, 0, 64, 3, 1, True),       # thin: mask encoder 3×3 1 → 64
+    (8, 2, 32, 32, 2, 0, 128, 7, 1, True),      # thin 7×7: flow encoders 2 → 128
+    (5, 1, 20, 24, 2, 0, 64, 7, 2, False),      # thin 7×7 / 2, ragged pixel runs
+])
+def test_conv_wgrad_batched_1x1_thin(case):
+    """scflow_conv_wgrad_batched on the 1×1 kernel and the thin kernel (segments over grid.z, 7×7
+    in batched calls): the sum of the segments' fp64 weight gradients, accumulate = 1."""
+    from scflow_amd import ops
+    from scflow_amd.ops import Chan
+    segs, n, h, w, c0, c1, cout, k, s, bias = case
+    g = torch.Generator().manual_seed(sum(case))
+    p = k // 2
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    ref = torch.zeros(cout, c0 + c1, k, k, dtype=torch.float64)
+    dys, s0, s1, dbr = [], [], [], torch.zeros(cout, dtype=torch.float64)
+    for _ in range(segs):
+        x0 = torch.randn(n, h, w, c0, generator=g)
+        buf = torch.randn(n, h, w, c1 + 8, generator=g)
+        dy = torch.randn(n, oh, ow, cout, generator=g)
+        xc = torch.cat([x0, buf[..., 4:4 + c1]], -1) if c1 else x0
+        ref += torch.nn.grad.conv2d_weight(xc.permute(0, 3, 1, 2).double(), (cout, c0 + c1, k, k),
+                                           dy.permute(0, 3, 1, 2).double(), stride=s, padding=p)
+        dbr += dy.double().sum((0, 1, 2))
+        dys.append(dy.cuda().view(-1, cout))
+        s0.append(x0.cuda())
+        s1.append(Chan(buf.cuda().view(-1, c1 + 8), 4, c1))
+    dw = torch.ones(cout, c0 + c1, k, k).cuda()
+    db = torch.ones(cout).cuda() if bias else None
+    ops.conv_wgrad_batched(dys, s0, s1 if c1 else None, dw, db, n, h, w, k, k, s, p, p,
+                           accumulate=True)
+    torch.cuda.synchronize()
+    _close(dw - 1, ref, 1e-5, 1e-4 * np.sqrt(segs * n * oh * ow), "dw")
+    if bias:
+        _close(db - 1, dbr, 1e-5, 1e-4 * np.sqrt(segs * n * oh * ow), "db")
+
+
 @pytest.mark.parametrize("rows,cols,acc", [(16384, 128, False), (16, 1024, True), (524288, 64, True),
                                            (1000, 3, False), (300, 257, True)])
 def test_colsum(rows, cols, acc):
