@@ -631,8 +631,7 @@ int scflow_conv_wgrad(const scflow_wgrad_args* args, void* stream);
  * scflow_refiner.py:182-256).  `args` describes one segment (n images; its dy / src0 / src1 are
  * ignored), dys[i] / src0s[i] / src1s[i] are segment i's bases with args' strides.  Shapes:
  * scflow_conv_wgrad's (Winograd 3×3 / 1×5 / 5×1, 1×1 stride 1–2, the implicit-GEMM 3×3, the
- * thin kernels for ≤ 4 channels on one side) plus thin 7×7 (the flow encoders' 2 → 128); others
- * return SCFLOW_EUNSUPPORTED.  `workspace`: scflow_conv_wgrad_workspace() of args with n·segs
+ * thin kernels for ≤ 4 channels on one side); others return SCFLOW_EUNSUPPORTED.  `workspace`: scflow_conv_wgrad_workspace() of args with n·segs
  * images (it sizes the partial sums for any segment count). */
 int scflow_conv_wgrad_batched(const scflow_wgrad_args* args, int segs, const float* const* dys,
                               const float* const* src0s, const float* const* src1s, void* stream);

@@ -723,19 +723,19 @@ struct WtParams {
   WgSegs sg;
 };
 
-// nseg = 0: the workspace query (the whole walk as one segment, rows for any segment count).
-// 7×7 (the stem, the flow encoders' 2→128) only in a batched call (seven): a single use is
-// faster on im2col + GEMM
-bool wthin_geometry(const scflow_wgrad_args& a, WtParams* P, int nseg = 1, bool seven = false) {
+// nseg = 0: the workspace query (the whole walk as one segment, rows for any segment count)
+bool wthin_geometry(const scflow_wgrad_args& a, WtParams* P, int nseg = 1) {
   static const bool off = [] {
     const char* e = getenv("SCFLOW_WGRAD_THIN");
     return e && e[0] == '0';
   }();
   if (off) return false;
   const int cin = a.cin0 + a.cin1;
-  const int kmax = seven ? 7 : 5;
-  if (a.kw != 1 && a.kw != 3 && a.kw != 5 && !(seven && a.kw == 7)) return false;
-  if (a.kh < 1 || a.kh > kmax || a.stride < 1 || a.stride > 2) return false;
+  // 7×7 (the stem, the flow encoders' 2→128) stays on im2col + GEMM: measured faster there
+  // (batched over the decoder's 8 uses too: 246 µs on this kernel, where the 14 scalar input
+  // loads per pixel and tap row are latency-bound, vs one concatenated GEMM)
+  if (a.kw != 1 && a.kw != 3 && a.kw != 5) return false;
+  if (a.kh < 1 || a.kh > 5 || a.stride < 1 || a.stride > 2) return false;
   const bool thin_co = a.cout <= 4 && cin % 4 == 0 && a.cin0 % 4 == 0 && cin <= 256 &&
                        a.s0 % 4 == 0 && aligned16(a.src0) &&
                        (a.cin1 == 0 || (a.s1 % 4 == 0 && aligned16(a.src1)));
@@ -927,7 +927,6 @@ int wthin_launch(const WtParams& P, hipStream_t st) {
   SCFLOW_WT(1, 1) SCFLOW_WT(2, 1) SCFLOW_WT(4, 1)
   SCFLOW_WT(1, 3) SCFLOW_WT(2, 3) SCFLOW_WT(4, 3)
   SCFLOW_WT(1, 5) SCFLOW_WT(2, 5) SCFLOW_WT(4, 5)
-  SCFLOW_WT(1, 7) SCFLOW_WT(2, 7) SCFLOW_WT(4, 7)
   return SCFLOW_EUNSUPPORTED;
 #undef SCFLOW_WT
   int rc = scflow_launch_status();
@@ -1738,7 +1737,7 @@ SCFLOW_API int scflow_gru_gate_backward_r(const float* drh, int sdrh, const floa
 SCFLOW_API int scflow_conv_wgrad_workspace(const scflow_wgrad_args* args, long long* floats) {
   if (!args || !floats) return SCFLOW_EINVAL;
   WtParams Q;
-  if (wthin_geometry(*args, &Q, 0, true)) {  // rows for a batched call of any segment count
+  if (wthin_geometry(*args, &Q, 0)) {  // rows for a batched call of any segment count
     *floats = wthin_workspace(Q);
     return SCFLOW_OK;
   }
@@ -1872,7 +1871,7 @@ SCFLOW_API int scflow_conv_wgrad_batched(const scflow_wgrad_args* args, int segs
     return wwino5_launch(R5, (hipStream_t)stream);
   }
   WtParams Q;
-  if (wthin_geometry(t, &Q, segs, true)) {
+  if (wthin_geometry(t, &Q, segs)) {
     Q.sg = sg;
     return wthin_launch(Q, (hipStream_t)stream);
   }

@@ -921,8 +921,7 @@ def conv_wgrad_batched(dys: List[Tensor], src0s: list, src1s: Optional[list], dw
                        ph: int, pw: int, accumulate: bool = False) -> None:
     """dw (+)= Σ_i weight gradient of segment i (dys[i] with src0s[i] / src1s[i], each n images
     of h×w) in one launch (scflow_conv_wgrad_batched; ≤ 8 equally shaped segments; the Winograd,
-    1×1, implicit-GEMM and thin kernels, 7×7 only with ≤ 4 channels on one side —
-    ScflowError(SCFLOW_EUNSUPPORTED) otherwise)."""
+    1×1, implicit-GEMM and thin kernels — ScflowError(SCFLOW_EUNSUPPORTED) otherwise)."""
     segs = len(dys)
     if not 1 <= segs <= 8 or len(src0s) != segs or (src1s is not None and len(src1s) != segs):
         raise ValueError(f"conv_wgrad_batched: 1..8 segments with matching sources, got {segs}")

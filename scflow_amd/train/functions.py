@@ -27,6 +27,7 @@ Pointwise operations (activations, GRU gate algebra, losses) stay torch ops on t
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -131,6 +132,10 @@ def _grad_sink(t: Optional[Tensor]) -> Optional[Tensor]:
         return None
     return gr
 
+
+# A/B switches (tools/train_bench.py runs): SCFLOW_DEFER_LINEAR=0 / SCFLOW_THIN_DX_GEMM=0
+_DEFER_LINEAR = os.environ.get("SCFLOW_DEFER_LINEAR", "1") != "0"
+_THIN_DX_GEMM = os.environ.get("SCFLOW_THIN_DX_GEMM", "1") != "0"
 
 _ACT_FN = {None: lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Tanh": torch.tanh}
 
@@ -275,9 +280,9 @@ def begin_forward() -> None:
 
 
 def _batchable(kh: int, kw: int, s: int, ph: int, pw: int) -> bool:
-    """Shapes scflow_conv_wgrad_batched takes (the Winograd, 1×1, implicit-GEMM and thin weight
-    gradients — 7×7 ones through the thin kernel when one side has ≤ 4 channels; shapes a batched
-    call refuses fall back to one launch per use)."""
+    """Shapes whose uses' weight gradients are summed at the last use: scflow_conv_wgrad_batched's
+    (Winograd, 1×1, implicit-GEMM, thin) and 7×7 (one concatenated GEMM, _concat_gemm_wgrad);
+    shapes a batched call refuses fall back to one launch per use."""
     return (kh, kw) in ((1, 1), (3, 3), (1, 5), (5, 1), (7, 7)) and s in (1, 2)
 
 
@@ -303,6 +308,9 @@ def _flush_wgrad(items, w: Tensor, with_bias: bool, dw: Tensor, db: Optional[Ten
     n, h, wd, _ = x00.shape
     cout, cin, kh, kw = w.shape
     padded = g0.shape[-1] != cout  # out_net's 126 output channels, padded to 128 in dY
+    if kh * kw > 25 and not padded and len(items) > 1:
+        _concat_gemm_wgrad(items, w, with_bias, dw, db, accumulate, s, ph, pw)
+        return
     if padded:
         tw = torch.empty(g0.shape[-1], cin, kh, kw, device=g0.device)
         tb = torch.empty(g0.shape[-1], device=g0.device) if with_bias else None
@@ -335,39 +343,54 @@ def _flush_wgrad(items, w: Tensor, with_bias: bool, dw: Tensor, db: Optional[Ten
                 db.copy_(tb[:cout])
 
 
+def _concat_gemm_wgrad(items, w: Tensor, with_bias: bool, dw: Tensor, db: Optional[Tensor],
+                       accumulate: bool, s: int, ph: int, pw: int) -> None:
+    """The uses' weight gradient of a large kernel (the flow encoders' 7×7 2 → 128, outside the
+    wgrad kernels) as ONE GEMM: every use's patch matrix into one buffer (HIP im2col in the
+    weight's column order), the dY's concatenated, dW (+)= Σ dYᵀ·cols over all pixels at once
+    (8 accumulating GEMMs over 16k pixels each ran at ≈ 20 TF)."""
+    g0, x00, _ = items[0]
+    n, h, wd, _ = x00.shape
+    cout, cin, kh, kw = w.shape
+    m = g0.reshape(-1, g0.shape[-1]).shape[0]
+    cols = torch.empty(len(items) * m, cin * kh * kw, device=g0.device)
+    for i, (_, x0, x1) in enumerate(items):
+        x = x0 if x1 is None else torch.cat([x0, x1], -1)
+        ops.im2col(x.contiguous(), n, h, wd, cin, kh, kw, s, ph, pw, out=cols[i * m:(i + 1) * m],
+                   channel_major=True)
+    gall = torch.cat([g.reshape(-1, cout) for g, _, _ in items])
+    ops.gemm(gall.t(), cols, out=dw.view(cout, cin * kh * kw), beta=1.0 if accumulate else 0.0)
+    if with_bias:
+        ops.colsum(gall, db, accumulate=accumulate)
+
+
 _PENDING: dict = {}  # id(holder) → holder with recorded uses not yet summed
 
 
-def _deferred_wgrad(hold: dict, w: Tensor, item, with_bias: bool, s: int, ph: int, pw: int,
-                    sink_w: Optional[Tensor], sink_b: Optional[Tensor]):
-    """Record this use's (g, x0, x1); on the last use, one batched weight gradient over all of
-    them.  With sinks (direct_weight_grads) the sum is added into them and nothing is returned;
-    otherwise the first call hands autograd the (dw, db) buffers the last call fills (only for
-    tensors whose every use is differentiated: the GRU's per-pass concatenated weights)."""
-    direct = sink_w is not None and (sink_b is not None or not with_bias)
-    first = not hold["items"]
-    out = (None, None)
-    if first:
-        hold["flush"] = (w, with_bias, s, ph, pw, sink_w, sink_b) if direct else None
-        if not direct:
-            hold["buf"] = (torch.empty_like(w), w.new_empty(w.shape[0]) if with_bias else None)
-            out = hold["buf"]
+def _defer(hold: dict, item, flush) -> None:
+    """Record this use's item; at the last use of the pass, ``flush(items)`` adds the summed weight
+    gradient into the parameter's gradient sinks (direct_weight_grads)."""
+    if not hold["items"]:
+        hold["flush"] = flush
         _PENDING[id(hold)] = hold
     hold["items"].append(item)
     hold["seen"] += 1
     if hold["seen"] >= hold["uses"]:
         _flush_holder(hold)
-    return out
+
+
+def _deferred_wgrad(hold: dict, w: Tensor, item, with_bias: bool, s: int, ph: int, pw: int,
+                    sink_w: Tensor, sink_b: Optional[Tensor]) -> None:
+    """Record this conv use's (g, x0, x1); on the last use, one batched weight gradient over all
+    of them, added into the sinks."""
+    _defer(hold, item, lambda items: _flush_wgrad(items, w, with_bias, sink_w, sink_b, True, s,
+                                                  ph, pw))
 
 
 def _flush_holder(hold: dict) -> None:
     items = hold["items"]
     if items:
-        if hold["flush"] is not None:
-            w, with_bias, s, ph, pw, sink_w, sink_b = hold["flush"]
-            _flush_wgrad(items, w, with_bias, sink_w, sink_b, True, s, ph, pw)
-        else:
-            raise RuntimeError("deferred weight gradient flushed without sinks")
+        hold["flush"](items)
     hold["items"] = []
     hold["seen"] = 0
     hold["buf"] = None
@@ -444,6 +467,13 @@ def _conv_backward(ctx, dy):
             # 1×1 to one channel (the mask predictor): dX = dY ⊗ w, one broadcast multiply
             # (a 1 → cin conv launch took 27 µs for the 16 MB it writes)
             dx = g * w.detach().reshape(1, 1, 1, cin)
+        elif s == 1 and cin <= 4 and kh * kw > 25 and _THIN_DX_GEMM:
+            # a large kernel onto ≤ 4 channels (the Δflow encoder's 7×7 128 → 2 adjoint): the
+            # products as one GEMM cols = dY·Wmat, then the col2im gather (the thin conv ran
+            # at 11 TF: 37 µs per use)
+            wm = _cached(w, ("wmat",), lambda: w.detach().permute(0, 2, 3, 1).reshape(cout, -1).contiguous())
+            cols = ops.gemm(g.view(-1, cout), wm)
+            dx = ops.col2im(cols, n, h, wd, cin, kh, kw, 1, ph, pw)
         elif s == 1:  # a 'same' conv of dY with the flipped, transposed weights
             dx = _conv_forward(gp, None, _flip_t(w, pad_co), None, 1, (kh - 1 - ph, kw - 1 - pw))
         else:
@@ -900,6 +930,16 @@ def group_norm_nhwc(x: Tensor, weight: Tensor, bias: Tensor, groups: int, eps: f
 
 
 # ------------------------------------------------------------------------------- linear
+def _flush_linear(items, sink_w: Tensor, sink_b: Optional[Tensor]) -> None:
+    """dW += Σ_uses dYᵀ·X as ONE GEMM over the uses' rows (the pose head's FC layers: 8 uses of
+    16 rows each — a 16-deep GEMM per use is all launch latency), db += the column sum."""
+    dys = torch.cat([d for d, _ in items])
+    xs = torch.cat([x for _, x in items])
+    ops.gemm(dys.t(), xs, out=sink_w, beta=1.0)
+    if sink_b is not None:
+        ops.colsum(dys, sink_b, accumulate=True)
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -907,6 +947,7 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.bias = b
+        ctx.uses = _use_holder(w) if w.requires_grad else None
         return ops.gemm(x, w.detach().t(), bias=None if b is None else b.detach().contiguous())
 
     @staticmethod
@@ -915,6 +956,16 @@ class _Linear(torch.autograd.Function):
         dy = dy.contiguous()
         dx = ops.gemm(dy, w.detach()) if ctx.needs_input_grad[0] else None
         dw = db = None
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
+        hold = getattr(ctx, "uses", None)
+        sw = _grad_sink(w) if ctx.needs_input_grad[1] else None
+        sb = _grad_sink(ctx.bias) if want_b else None
+        if (_DEFER_LINEAR and hold is not None and hold["uses"] > 1 and sw is not None
+                and (sb is not None or not want_b) and (want_b or not ctx.has_b)):
+            # a layer run once per refinement iteration: its uses' weight gradients as one GEMM
+            # at the last use, added straight into the parameters
+            _defer(hold, (dy, x), lambda items: _flush_linear(items, sw, sb))
+            return dx, None, None
         if ctx.needs_input_grad[1]:
             sw = _grad_sink(w)
             if sw is not None:  # dW added in place: beta = 1 onto the parameter's .grad
