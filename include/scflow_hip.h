@@ -339,7 +339,9 @@ int scflow_ph_heads(const float* x, int m, int k, const float* Wr, const float* 
 /* scflow_pose_step_part: scflow_pose_step restricted to parts (bit 0: the full-resolution outputs
  *   — pose flow, ×8 flow prediction and mask; bit 1: the next iteration's ↓8 flow, lr_next /
  *   hx_next).  Each part recomputes the pose update; the part with the lowest block writes
- *   R_dst / t_dst.  The decoder runs bit 1 on its critical path and bit 0 on a side stream. */
+ *   R_dst / t_dst.  The decoder runs bit 1 on its critical path and bit 0 on a side stream.
+ *   drot6 == NULL (parts = 1 only): R_src / t_src ARE the updated pose (the bit-1 launch's
+ *   R_dst / t_dst) — no update, dt / R_dst / t_dst unused, same outputs. */
 int scflow_pose_step_part(const float* drot6, const float* dt, const float* R_src,
                           const float* t_src, const float* K, const float* points, float* R_dst,
                           float* t_dst, float* flow, int n, int H, int W, float weight,

@@ -250,6 +250,7 @@ SCFLOW_API int scflow_pose_step(const float* drot6, const float* dt, const float
                                 float* flow_up, float* mask_up, float* lr_next, int s_next,
                                 float* hx_next, int s_hx, int h, int w, float up_scale,
                                 float down_scale, void* stream) {
+  if (!drot6) return SCFLOW_EINVAL;
   PoseStepArgs a;
   const int st = pose_step_args(&a, drot6, dt, R_src, t_src, K, points, R_dst, t_dst, flow, n, H, W,
                                 weight, depth_transform, invalid_num, lr, delta, mask, flow_up,
@@ -268,7 +269,7 @@ SCFLOW_API int scflow_pose_step_part(const float* drot6, const float* dt, const 
                                      float* flow_up, float* mask_up, float* lr_next, int s_next,
                                      float* hx_next, int s_hx, int h, int w, float up_scale,
                                      float down_scale, int parts, void* stream) {
-  if (parts < 1 || parts > 3) return SCFLOW_EINVAL;
+  if (parts < 1 || parts > 3 || (!drot6 && parts != 1)) return SCFLOW_EINVAL;
   PoseStepArgs a;
   const int st = pose_step_args(&a, drot6, dt, R_src, t_src, K, points, R_dst, t_dst, flow, n, H, W,
                                 weight, depth_transform, invalid_num, lr, delta, mask, flow_up,

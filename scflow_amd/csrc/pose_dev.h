@@ -176,6 +176,7 @@ struct PoseStepArgs {
   const float* lr; const float* delta; const float* mask; float* fo; float* mo;
   float* o0; int s0; float* o1; int s1; int h, w; float up_scale, down_scale;
   int bf, bl;
+  int given;  // 1: Rsrc / tsrc are the updated pose already (no update, Rout / tout unused)
 };
 
 // sh: 21 floats of LDS; every thread of the block calls this (barrier inside)
@@ -184,7 +185,14 @@ struct PoseStepArgs {
 __device__ __forceinline__ void pose_step_body(const PoseStepArgs& a, float* sh, int bx, int n,
                                                int tid, int nt, bool fresh = false) {
 #pragma clang fp contract(off)
-  if (tid == 0) {
+  if (a.given) {  // the pose of this iteration was updated by the ↓8 part: 21 plain loads
+    if (tid < 9)
+      sh[tid] = a.Rsrc[9 * n + tid];
+    else if (tid < 12)
+      sh[tid] = a.tsrc[3 * n + tid - 9];
+    else if (tid < 21)
+      sh[tid] = a.K[9 * n + tid - 12];
+  } else if (tid == 0) {
     const int rd = pose_rot_dim(a.depth_transform);
     float d[6], dt[3];
     for (int k = 0; k < rd; ++k)
@@ -259,9 +267,11 @@ static inline int pose_step_args(PoseStepArgs* a, const float* drot6, const floa
                                  float* flow_up, float* mask_up, float* lr_next, int s_next,
                                  float* hx_next, int s_hx, int h, int w, float up_scale,
                                  float down_scale, int nt) {
-  if (!drot6 || !dt || !R_src || !t_src || !K || !points || !R_dst || !t_dst || !flow || n <= 0 ||
-      H <= 0 || W <= 0 || (depth_transform & ~(SCFLOW_POSE_QUAT_XYZW | 1)) != 0)
+  const bool given = !drot6;  // the full-resolution part from an updated pose (R_src, t_src)
+  if ((!given && (!dt || !R_dst || !t_dst)) || !R_src || !t_src || !K || !points || !flow ||
+      n <= 0 || H <= 0 || W <= 0 || (depth_transform & ~(SCFLOW_POSE_QUAT_XYZW | 1)) != 0)
     return SCFLOW_EINVAL;
+  if (given && lr_next) return SCFLOW_EINVAL;
   if ((flow_up || lr_next) && (h <= 0 || w <= 0)) return SCFLOW_EINVAL;
   if (flow_up && !lr) return SCFLOW_EINVAL;
   if (lr_next && (s_next < 2 || (hx_next && s_hx < 2) || lr_next == lr)) return SCFLOW_EINVAL;
@@ -272,8 +282,12 @@ static inline int pose_step_args(PoseStepArgs* a, const float* drot6, const floa
   a->invalid = invalid_num; a->lr = lr; a->delta = delta; a->mask = mask; a->fo = flow_up;
   a->mo = mask_up; a->o0 = lr_next; a->s0 = s_next; a->o1 = hx_next; a->s1 = s_hx; a->h = h;
   a->w = w; a->up_scale = up_scale; a->down_scale = down_scale;
+  a->given = given ? 1 : 0;
   const int bf = ceil_div((long long)H * W, nt);
-  a->bf = bf < 256 ? bf : 256;
+  // from a given pose the part runs beside other work (the decoder's side stream): 4 pixels per
+  // thread, a quarter of the workgroups to schedule
+  const int bfmax = given ? 64 : 256;
+  a->bf = bf < bfmax ? bf : bfmax;
   const int bl = ceil_div((long long)h * w, nt);
   a->bl = lr_next ? (bl < 64 ? bl : 64) : 0;
   return SCFLOW_OK;

@@ -22,6 +22,7 @@ HIP graph (``graph.py``).  There is no CPU path: inputs must be on a ROCm device
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Sequence, Tuple, Union
 
 import torch
@@ -113,6 +114,9 @@ class SCFlowDecoder(nn.Module):
         # flow, ×8 prediction, mask) run on the side stream during the next iteration's GRU
         # (they only feed the returned lists)
         self.defer_full_res = True
+        # the deferred full-resolution part reads the pose the ↓8 part wrote instead of
+        # recomputing the update per workgroup (ops.pose_step_given); SCFLOW_FULLRES_GIVEN=0: off
+        self.fullres_given = os.environ.get("SCFLOW_FULLRES_GIVEN", "1") != "0"
         # correlation pyramid in the tiled layout (4×4 tiles of 16 floats per map, pooling fused
         # into the GEMM epilogue; ops.corr_pyramid_tiled) when the geometry allows it
         self.tiled_pyramid = True
@@ -613,9 +617,13 @@ class SCFlowDecoder(nn.Module):
                             if defer and not last:
                                 with ops.binding(pc, run=False):
                                     ops.pose_step(*step, **nxt, parts=2)
-                                fstep = step[:6] + (R_scr, t_scr) + step[8:]
                                 with ops.binding(fc, run=False):
-                                    ops.pose_step(*fstep, **nxt, parts=1)
+                                    if self.fullres_given:
+                                        ops.pose_step_given(o_R[j], o_t[j], *step[4:6],
+                                                            *step[8:])
+                                    else:
+                                        fstep = step[:6] + (R_scr, t_scr) + step[8:]
+                                        ops.pose_step(*fstep, **nxt, parts=1)
                             else:
                                 with ops.binding(pc, run=False):
                                     ops.pose_step(*step, **nxt)

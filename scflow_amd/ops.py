@@ -532,6 +532,23 @@ def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points:
         _launch("scflow_pose_step_part", drot, *args, int(parts))
 
 
+def pose_step_given(R: Tensor, t: Tensor, K: Tensor, points: Tensor, flow_out: Tensor,
+                    invalid_num: float, lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor],
+                    flow_up: Tensor, mask_up: Optional[Tensor], h: int, w: int,
+                    up_scale: float) -> None:
+    """``pose_step``'s full-resolution part (parts = 1) from an already updated pose R, t (the ↓8
+    part's R_out / t_out): pose flow, ×8 flow prediction and mask, no pose update
+    (scflow_pose_step_part with drot6 = NULL)."""
+    for nm, x in (("R", R), ("t", t), ("K", K), ("points", points), ("flow_out", flow_out),
+                  ("lr", lr), ("flow_up", flow_up)):
+        _require(x, nm)
+    n, H, W, _ = points.shape
+    _launch("scflow_pose_step_part", R, None, None, _p(R), _p(t), _p(K), _p(points), None, None,
+            _p(flow_out), n, H, W, 10.0, 0, float(invalid_num), _p(lr), _p(delta), _p(mask),
+            _p(flow_up), _p(mask_up), None, 0, None, 0, h, w, float(up_scale),
+            1.0 / float(up_scale), 1)
+
+
 def pose_step_struct(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points: Tensor,
                      R_out: Tensor, t_out: Tensor, flow_out: Tensor, invalid_num: float,
                      lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], flow_up: Tensor,

@@ -454,6 +454,14 @@ def test_pose_step_matches_separate_launches(ops, S, s, nxt):
     with pytest.raises(ValueError):
         ops.pose_step(drot, dt, R0, t0, K, pts, Rb, tb, fb, 400.0, lr, delta, mask, upb, mb, s, s,
                       float(scale), lr_next=ops.Chan.whole(lr))
+    # the decoder's deferred full-resolution part from the updated pose (no update, 4 pixels per
+    # thread): the same outputs bit for bit
+    fc, upc, mc = torch.empty_like(fa), torch.empty_like(upa), torch.empty_like(ma)
+    ops.pose_step_given(Rb, tb, K, pts, fc, 400.0, lr, delta, mask, upc, mc, s, s, float(scale))
+    torch.cuda.synchronize()
+    for a, b, nm in ((fa, fc, "flow (given pose)"), (upa, upc, "flow ×8 (given pose)"),
+                     (ma, mc, "mask ×8 (given pose)")):
+        assert torch.equal(a, b), nm
 
 
 @pytest.mark.parametrize("S,s", [(256, 32), (512, 64), (100, 13)])
