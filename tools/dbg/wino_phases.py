@@ -18,6 +18,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--only", default=None, help="shapes whose name contains this")
+    ap.add_argument("--no-stamps", action="store_true", help="timing only (for counter runs)")
     a = ap.parse_args()
     from scflow_amd import _lib
     from scflow_amd.modules import ConvRunner
@@ -30,6 +32,8 @@ def main():
               ("out_net 256->126", 256, 126), ("flow_net.1 128->64", 128, 64),
               ("mask_enc.1 64->32", 64, 32)]
     for name, cin, cout in shapes:
+        if a.only and a.only not in name:
+            continue
         conv = torch.nn.Conv2d(cin, cout, 3, padding=1).cuda()
         x = torch.randn(M, cin, device="cuda")
         out = torch.empty(M, cout, device="cuda")
@@ -47,6 +51,9 @@ def main():
         ev1.record()
         torch.cuda.synchronize()
         us = ev0.elapsed_time(ev1) * 1e3 / 20
+        if a.no_stamps:
+            print(f"{name:22s} {us:6.1f} us/launch", flush=True)
+            continue
         st = torch.zeros(65536 * 4, dtype=torch.int64, device="cuda")
         lib.scflow_debug_conv_stamps(ctypes.c_void_p(st.data_ptr()))
         run()
