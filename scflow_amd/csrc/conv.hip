@@ -288,6 +288,101 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
 }
 
 // ------------------------------------------------------------------------------------------
+// 1×1 stride-1 conv (MotionEncoder corr_net.0 324 → 256, raft_decoder.py:75-85; the training
+// step's 1×1 forward / dX convs): the GEMM over 128 consecutive pixel rows × 64 output channels,
+// same packed weights and stage pipeline as conv_mfma_kernel<·,1,1,128,16> but without its halo
+// machinery — rows are contiguous, so a stage's A tile is 128 rows × 16 channels of one source
+// (two float4 per thread) and the epilogue addresses rows directly (32 vs 38 µs at corr_net.0's
+// shape, tools/micro/conv1x1_variants.hip).  Plain epilogue: bias, bias map, activation.
+__global__ __launch_bounds__(256, 2) void conv1x1_kernel(MfmaParams P) {
+  constexpr int TM = 128, LDA = BK + 4;
+  __shared__ float As[TM * LDA];
+  __shared__ float Bs[BN * LDA];
+  const scflow_conv_args& a = P.a;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
+  const int m0 = blockIdx.x * TM;
+  const long long M = (long long)a.n * a.h * a.w;
+  const int nst0 = P.cp0 / BK;
+  floatx4 ra[2], rb;
+  auto gload = [&](int s) __attribute__((always_inline)) {
+    const bool s1 = s >= nst0;
+    const float* src = s1 ? a.src1 : a.src0;
+    const int cs = s1 ? a.c1 : a.c0;
+    const int ss = s1 ? a.s1 : a.s0;
+    const int cc = (s1 ? s - nst0 : s) * BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = tid + 256 * j;
+      const long long m = m0 + (idx >> 2);
+      const int c = cc + 4 * (idx & 3);
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m < M && c < cs) v = *(const floatx4*)(src + m * ss + c);
+      ra[j] = v;
+    }
+    rb = *(const floatx4*)(a.weight + ((size_t)blockIdx.y * P.nst + s) * (BN * BK) + (size_t)tid * 4);
+  };
+  auto lstore = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = tid + 256 * j;
+      *(floatx4*)(As + (idx >> 2) * LDA + 4 * (idx & 3)) = ra[j];
+    }
+    *(floatx4*)(Bs + (tid >> 2) * LDA + 4 * (tid & 3)) = rb;
+  };
+  floatx16 acc[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
+  const int abase = (wm * 64 + li) * LDA + 4 * hh, bbase = (wn * 32 + li) * LDA + 4 * hh;
+  gload(0);
+  for (int s = 0; s < P.nst; ++s) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (s + 1 < P.nst) gload(s + 1);
+#pragma unroll
+    for (int kb = 0; kb < BK; kb += 8) {
+      const floatx4 a0 = *(const floatx4*)(As + abase + kb);
+      const floatx4 a1 = *(const floatx4*)(As + abase + 32 * LDA + kb);
+      const floatx4 b0 = *(const floatx4*)(Bs + bbase + kb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], b0[e], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b0[e], acc[1], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5); all global reads
+  // (bias map) before any store
+  const int col = blockIdx.y * BN + wn * 32 + li;
+  if (col >= a.cout) return;
+  const float bias = a.bias ? a.bias[col] : 0.f;
+  float v[2][16];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[rr][r] = acc[rr][r] + bias;
+  if (a.bias_map) {
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = m0 + wm * 64 + rr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m < M) v[rr][r] += a.bias_map[m * a.sbm + col];
+      }
+  }
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long long m = m0 + wm * 64 + rr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (m < M) a.out[m * a.so + col] = act_apply(v[rr][r], a.act);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // small-cin conv: lane = output channel, weights in VGPRs, input halo in LDS (broadcast reads)
 // packed weights: [taps*cin][npad]  (channel-contiguous)
 // block: 256 threads; tile = 32 consecutive output pixels of one row; wave w handles channel
@@ -928,6 +1023,17 @@ int pick_bk(int kh, int kw, int tm, int hr, int hc, long long wgs, int cus) {
   return rounds(8) < rounds(16) ? 8 : 16;
 }
 
+// the 1×1 kernel (conv1x1_kernel) for stride-1 1×1 convs on 128-row tiles; SCFLOW_CONV1X1=0
+// keeps them on conv_mfma_kernel (tuning only)
+bool conv1x1_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SCFLOW_CONV1X1");
+    on = !(e && e[0] == '0');
+  }
+  return on != 0;
+}
+
 // tile rows / halo rows / tile size for a launch (shared by the launcher and scflow_conv_pick_bk)
 int launch_tile(const scflow_conv_args& a, const Geometry& g, int* tr, int* hr) {
   const long long m = (long long)a.n * g.oh * g.ow;
@@ -1084,6 +1190,15 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     p.hc = g.hc;
     p.cp0 = g.cp0;
     p.nst = g.nst;
+    if (a.kh == 1 && a.kw == 1 && a.epilogue == SCFLOW_EPI_PLAIN && a.bk != 8 && conv1x1_enabled()) {
+      int tr, hr;
+      if (launch_tile(a, g, &tr, &hr) == 128) {
+        const long long M = (long long)a.n * g.oh * g.ow;
+        p.nst = (g.cp0 + g.cp1) / BK;
+        conv1x1_kernel<<<dim3((unsigned)((M + 127) / 128), g.npad / BN), 256, 0, st>>>(p);
+        return scflow_launch_status();
+      }
+    }
     switch (a.epilogue) {
       case SCFLOW_EPI_GRU_ZR: return dispatch_mfma<SCFLOW_EPI_GRU_ZR>(p, g, st);
       case SCFLOW_EPI_GRU_Q: return dispatch_mfma<SCFLOW_EPI_GRU_Q>(p, g, st);

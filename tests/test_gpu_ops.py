@@ -208,6 +208,8 @@ def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0, bk=None):
     (2, 32, 32, 1, 0, 64, 3, 1, "ReLU"),           # small-cin 3×3, 1 channel
     (2, 32, 32, 256, 0, 2, 3, 1, None),            # thin 3×3 → 2
     (2, 32, 32, 256, 0, 1, 1, 0, "Sigmoid"),       # thin 1×1 → 1
+    (16, 32, 32, 324, 0, 256, 1, 0, "ReLU"),       # 1×1 kernel (128-row tiles: corr_net.0 at B=16)
+    (13, 32, 32, 196, 60, 320, 1, 0, "Tanh"),      # 1×1 kernel, two sources, 5 channel blocks
 ])
 def test_conv2d_variants(ops, case):
     n, h, w, c0, c1, cout, k, pad, act = case

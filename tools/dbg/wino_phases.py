@@ -30,11 +30,12 @@ def main():
     M = n * h * w
     shapes = [("heads 128->512", 128, 512), ("corr_net.1 256->192", 256, 192),
               ("out_net 256->126", 256, 126), ("flow_net.1 128->64", 128, 64),
-              ("mask_enc.1 64->32", 64, 32)]
+              ("mask_enc.1 64->32", 64, 32), ("corr_net.0 1x1 324->256", 324, 256)]
     for name, cin, cout in shapes:
         if a.only and a.only not in name:
             continue
-        conv = torch.nn.Conv2d(cin, cout, 3, padding=1).cuda()
+        k = 1 if "1x1" in name else 3
+        conv = torch.nn.Conv2d(cin, cout, k, padding=k // 2).cuda()
         x = torch.randn(M, cin, device="cuda")
         out = torch.empty(M, cout, device="cuda")
         r = ConvRunner([conv], None)
@@ -51,7 +52,7 @@ def main():
         ev1.record()
         torch.cuda.synchronize()
         us = ev0.elapsed_time(ev1) * 1e3 / 20
-        if a.no_stamps:
+        if a.no_stamps or k == 1:  # (stamps: the Winograd kernel only)
             print(f"{name:22s} {us:6.1f} us/launch", flush=True)
             continue
         st = torch.zeros(65536 * 4, dtype=torch.int64, device="cuda")
