@@ -457,14 +457,15 @@ __global__ __launch_bounds__(256) void conv_smallcin_mfma_kernel(scflow_conv_arg
   }
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
-  // B fragments: k = 2·kp + hh, column = wn·NBW·32 + nb·32 + li
+  const int cb = blockIdx.y * NBW * 64;  // channel slice of this workgroup (grid.y splits npad)
+  // B fragments: k = 2·kp + hh, column = cb + wn·NBW·32 + nb·32 + li
   float bw[NBW][KP];
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
     for (int kp = 0; kp < KP; ++kp) {
       const int k = 2 * kp + hh;
-      bw[nb][kp] = k < K ? a.weight[(size_t)k * npad + (wn * NBW + nb) * 32 + li] : 0.f;
+      bw[nb][kp] = k < K ? a.weight[(size_t)k * npad + cb + (wn * NBW + nb) * 32 + li] : 0.f;
     }
   __syncthreads();
   const int m = wm * 32 + li;  // this lane's A row (output pixel of the tile)
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(256) void conv_smallcin_mfma_kernel(scflow_conv_arg
   // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb) {
-    const int col = (wn * NBW + nb) * 32 + li;
+    const int col = cb + (wn * NBW + nb) * 32 + li;
     if (col >= a.cout) continue;
     const float b = a.bias ? a.bias[col] : 0.f;
 #pragma unroll
@@ -1025,6 +1026,18 @@ int pick_bk(int kh, int kw, int tm, int hr, int hc, long long wgs, int cus) {
 
 // the 1×1 kernel (conv1x1_kernel) for stride-1 1×1 convs on 128-row tiles; SCFLOW_CONV1X1=0
 // keeps them on conv_mfma_kernel (tuning only)
+// SCFLOW_SMALLCIN_SPLIT=1: the 128-channel small-cin MFMA conv as two workgroups per 64-pixel tile
+// (one per 64-channel half) instead of one (each wave 2 × 32 channels).  Measured: 13.1 -> 12.1 us
+// in isolation (7x7 2->128, B=16), no gain inside the decoder (5.263 vs 5.233 ms/forward), so off.
+bool smallcin_split() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SCFLOW_SMALLCIN_SPLIT");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
 bool conv1x1_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -1215,7 +1228,9 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
       const size_t lds = sizeof(float) * (size_t)(64 / g.ow + a.kh - 1) * (g.ow + a.kw - 1) * a.c0;
 #define SCFLOW_SCM(CI, KH_, KW_)                                                                   \
   if (a.c0 == CI && a.kh == KH_ && a.kw == KW_) {                                                  \
-    if (g.npad == 128)                                                                             \
+    if (g.npad == 128 && smallcin_split())                                                         \
+      conv_smallcin_mfma_kernel<CI, KH_, KW_, 1><<<dim3(blocks, 2), 256, lds, st>>>(a, g.oh, g.ow, g.npad); \
+    else if (g.npad == 128)                                                                        \
       conv_smallcin_mfma_kernel<CI, KH_, KW_, 2><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad);  \
     else                                                                                           \
       conv_smallcin_mfma_kernel<CI, KH_, KW_, 1><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad);  \
