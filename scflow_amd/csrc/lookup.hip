@@ -122,19 +122,29 @@ __host__ __device__ inline int lk_slot_floats(int h, int w, int L, int win) {
 
 constexpr int LK_OOB = 0x7ffffff0;  // buffer voffset of a zero tap (beyond any num_records)
 
+// TR (tile regions, tiled maps only): every level's region is the 4×4 block of 4×4 tiles (16×16
+// floats) whose first tile holds floor(first sample) − 1, loaded as whole tile rows (one b128 per
+// lane, 4 lanes per 64-B tile) and stored as b128 into 16-float LDS rows.  The 12×12 window it
+// contains is what the plain regions hold; the extra columns / rows cost LDS, not memory-side
+// bytes: the 12-wide window already touches 3–4 tiles per axis, every one of them whole 64-B
+// sectors.  Slot stride ≡ 16 mod 64 floats so a wave's 4 pixel slots start in different banks.
+constexpr int LK_TRW = 16;
+__host__ __device__ inline int lk_tr_slot_floats(int L) { return L * LK_TRW * LK_TRW + 16; }
+
 __device__ __forceinline__ float lk_bload(__amdgpu_buffer_rsrc_t r, int voff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
 }
 
 // TILED: the pyramid's maps are in 4×4 tiles of 16 floats (scflow_corr_pyramid_tiled)
-template <int R, bool TILED>
+template <int R, bool TILED, bool TR = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void corr_lookup_lds_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
     float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
     int vec_out, int ac, unsigned long long* stamps) {
 #pragma clang fp contract(off)
   constexpr int D = 2 * R + 1;
-  constexpr int WIN = D + 3;
+  constexpr int WIN = TR ? LK_TRW : D + 3;  // LDS row length of a level's region
+  static_assert(!TR || (TILED && D + 3 <= LK_TRW - 3), "tile regions: tiled maps, r <= 4");
   // profiling (scflow_debug_lookup_stamps): thread 0's real-time-clock stamps at the phase
   // boundaries, 6 per workgroup
   auto stamp = [&](int k) {
@@ -152,7 +162,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   const int gl = lane % LK_GL;                    // lane within the pixel's group
   const int P = H * W;
   const long long NP = (long long)N * P;
-  float* sw = win + slot * lk_slot_floats(H, W, L, WIN);
+  float* sw = win + slot * (TR ? lk_tr_slot_floats(L) : lk_slot_floats(H, W, L, WIN));
   const long long gp0 = (long long)blockIdx.x * LK_SLOTS + wave * LK_PPW;  // wave's first pixel
   const long long gp = gp0 + ks;                                          // n·P + p
   const bool active = gp < NP;
@@ -184,25 +194,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   //     region-relative floor
   for (int t = gl; t < L * 2 * D; t += LK_GL) {
     const int l = t / (2 * D), axis = (t / D) % 2, i = t % D;
-    const bool whole = lk_whole(H >> l, W >> l, WIN);
+    const bool whole = !TR && lk_whole(H >> l, W >> l, WIN);
     const float c0x = crd[slot][l][0][0], c0y = crd[slot][l][1][0];
     const bool fin = isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f && fabsf(c0y) < 1e8f;
     const float s = crd[slot][l][axis][i];
-    const int o = whole ? -1 : (fin ? (int)floorf(axis == 0 ? c0x : c0y) - 1 : -(1 << 29));
+    int o = whole ? -1 : (fin ? (int)floorf(axis == 0 ? c0x : c0y) - 1 : -(1 << 29));
+    if (TR) o = (o >> 2) << 2;  // the tile holding it (arithmetic shift: floor for negatives)
     sr[slot][l][axis][i] = fin && isfinite(s) ? (int)floorf(s) - o : -1;
     if (i == 0) org[slot][l][axis] = o;
   }
   __syncthreads();
   // 2. regions (zero padded) through buffer loads (out-of-map taps read as zero, no branches):
   //    every load of the pixel's L regions is issued before the LDS writes
-  constexpr int NW1 = (WIN * WIN + LK_GL - 1) / LK_GL;  // loads per lane per level
-  float vals[LK_MAXL][NW1];
   int rn[LK_MAXL], ox[LK_MAXL], oy[LK_MAXL];
 #pragma unroll
   for (int l = 0; l < LK_MAXL; ++l) {
     ox[l] = l < L ? org[slot][l][0] : 0;
     oy[l] = l < L ? org[slot][l][1] : 0;
   }
+  if constexpr (TR) {
+    // 16 lanes × 4 b128 = the region's 64 tile rows (tile kt = k / 4 of the 4×4 block, row k % 4)
+    floatx4 tv4[LK_MAXL][4];
+    size_t loff = 0;
+    int Hl = H, Wl = W;
+    const long long left = NP - gp0;
+    const int npx = left < LK_PPW ? (int)left : LK_PPW;
+#pragma unroll
+    for (int l = 0; l < LK_MAXL; ++l) {
+      const bool use = l < L;
+      const int hw = Hl * Wl;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(pyr + loff + (size_t)gp0 * hw), (short)0, use ? npx * hw * 4 : 0,
+          0x00020000);
+      rn[l] = use ? LK_TRW * LK_TRW : 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = gl + LK_GL * j, kt = k >> 2;
+        const int gx = ox[l] + (kt & 3) * 4, gy = oy[l] + (kt >> 2) * 4 + (k & 3);
+        const bool ok = use && active && gx >= 0 && gx < Wl && gy >= 0 && gy < Hl;
+        const int e = ((gy >> 2) * (Wl >> 2) + (gx >> 2)) * 16 + (gy & 3) * 4;
+        tv4[l][j] = __builtin_bit_cast(
+            floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (ks * hw + e) * 4 : LK_OOB, 0, 0));
+      }
+      if (use) loff += (size_t)NP * hw;
+      Hl >>= 1;
+      Wl >>= 1;
+    }
+    stamp(2);
+#pragma unroll
+    for (int l = 0; l < LK_MAXL; ++l) {
+      if (l < L) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = gl + LK_GL * j, kt = k >> 2;
+          *(floatx4*)(sw + l * LK_TRW * LK_TRW + ((kt >> 2) * 4 + (k & 3)) * LK_TRW + (kt & 3) * 4) =
+              tv4[l][j];
+        }
+      }
+    }
+  } else {
+  constexpr int NW1 = (WIN * WIN + LK_GL - 1) / LK_GL;  // loads per lane per level
+  float vals[LK_MAXL][NW1];
   {
     size_t loff = 0;
     int Hl = H, Wl = W;
@@ -242,6 +294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
       }
       off += rn[l];
     }
+  }
   }
   __syncthreads();
   stamp(3);
@@ -349,6 +402,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 // profiling: where the next LDS-kernel launches write their phase stamps (NULL: off)
 static unsigned long long* g_lk_stamps = nullptr;
 
+// SCFLOW_LK_TILEREG=1: the tiled r = 4 lookup stages 16×16 tile-aligned regions with b128 tile-row
+// loads (corr_lookup_lds_kernel TR) instead of 12×12 windows with b32 loads
+static bool lk_tile_regions() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SCFLOW_LK_TILEREG");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
 static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layout, float* out,
                               int out_layout, int out_stride, int n, int h, int w, int num_levels,
                               int radius, int align_corners, bool tiled, void* stream) {
@@ -387,6 +451,12 @@ static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layo
   corr_lookup_lds_kernel<RR, TT><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout,      \
                                                         out_stride, n, h, w, num_levels, vec, ac,  \
                                                         g_lk_stamps)
+    if (tiled && radius == 4 && lk_tile_regions()) {
+      const size_t lds_tr = sizeof(float) * LK_SLOTS * lk_tr_slot_floats(num_levels);
+      corr_lookup_lds_kernel<4, true, true><<<blk, 256, lds_tr, st>>>(
+          pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac, g_lk_stamps);
+      return scflow_launch_status();
+    }
     switch (radius * 2 + (tiled ? 1 : 0)) {
       case 2: SCFLOW_LKL(1, false); break;
       case 3: SCFLOW_LKL(1, true); break;

@@ -607,3 +607,32 @@ def test_corr_lookup_far_out_of_bounds(ops):
     out = ops.corr_lookup(buf, flow.cuda(), 1, 16, 16, 4, 4)
     close(out, ref, 1e-5, 1e-5, "lookup far / edge flows")
     assert (out[0, :, :8].abs().max() == 0)
+
+
+def test_corr_lookup_tiled_far_out_of_bounds(ops):
+    """The tiled lookup (16×16 tile-aligned regions, b128 tile-row loads) on flows that push
+    windows off the map, straddle its edges at every tile phase, or are not finite: exactly the
+    row-major lookup's output (the same taps and arithmetic, only staged differently)."""
+    g = torch.Generator().manual_seed(19)
+    n, h, w, L = 2, 32, 32, 4
+    f1 = torch.randn(n, 16, h, w, generator=g).cuda()
+    f2 = torch.randn(n, 16, h, w, generator=g).cuda()
+    _, lv = ops.corr_pyramid(f1, f2, L)
+    buf = ops.pyramid_buffer(lv, n, h, w)
+    tb = ops.corr_pyramid_tiled(f1, f2, L)
+    flow = torch.zeros(n, 2, h, w)
+    flow[0, 0, :4] = 1e4
+    flow[0, 1, 4:8] = -1e4
+    flow[0, :, 8:16] = torch.arange(8 * 32 * 2, dtype=torch.float32).view(2, 8, 32) * 0.125 - 32
+    flow[0, :, 16:20] = float(h) - 0.5
+    flow[0, 0, 20, :8] = float("nan")
+    flow[0, 1, 20, 8:16] = float("inf")
+    flow[1] = (torch.rand(2, h, w, generator=g) - 0.5) * 3 * h
+    flow = flow.cuda()
+    for ac in (True, False):
+        if not ops.tiled_lookup_ok(h, w, L, 4, ac):
+            continue
+        ref = ops.corr_lookup(buf, flow, n, h, w, L, 4, align_corners=ac)
+        got = ops.corr_lookup(tb, flow, n, h, w, L, 4, align_corners=ac, tiled=True)
+        assert torch.equal(torch.nan_to_num(ref, nan=123.0), torch.nan_to_num(got, nan=123.0)), \
+            f"ac={ac}: {(ref - got).abs().nan_to_num().max().item():.3e}"
