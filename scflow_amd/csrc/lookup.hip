@@ -21,6 +21,9 @@
 // (scflow_corr_pyramid_tiled): the same loads, addressed into the tiles, so a wave's window
 // loads coalesce into ≈ 3.3² whole 64-B sectors per level instead of 12 row segments that
 // straddle sector boundaries (the configs[4] over-fetch, profiles/traffic_b32_s512.json).
+// Round 3: on maps of at most 32×32 (the headline configs[1]) the tiled kernel stages 16×16
+// tile-aligned regions through b128 tile-row loads / LDS stores (TR below, 4 loads per lane per
+// level instead of 9).
 #include "common.h"
 
 namespace {
@@ -123,7 +126,8 @@ __host__ __device__ inline int lk_slot_floats(int h, int w, int L, int win) {
 constexpr int LK_OOB = 0x7ffffff0;  // buffer voffset of a zero tap (beyond any num_records)
 
 // TR (tile regions, tiled maps only): every level's region is the 4×4 block of 4×4 tiles (16×16
-// floats) whose first tile holds floor(first sample) − 1, loaded as whole tile rows (one b128 per
+// floats) whose first tile holds floor(first sample) − 1 (a map axis of ≤ 8: the whole axis from
+// −4, a zero tile before it), loaded as whole tile rows (one b128 per
 // lane, 4 lanes per 64-B tile) and stored as b128 into 16-float LDS rows.  The 12×12 window it
 // contains is what the plain regions hold; the extra columns / rows cost LDS, not memory-side
 // bytes: the 12-wide window already touches 3–4 tiles per axis, every one of them whole 64-B
@@ -199,7 +203,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     const bool fin = isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f && fabsf(c0y) < 1e8f;
     const float s = crd[slot][l][axis][i];
     int o = whole ? -1 : (fin ? (int)floorf(axis == 0 ? c0x : c0y) - 1 : -(1 << 29));
-    if (TR) o = (o >> 2) << 2;  // the tile holding it (arithmetic shift: floor for negatives)
+    // tile regions: an axis of at most 8 is held whole with a one-tile zero border ([−4, 12)),
+    // else from the tile holding floor(first sample) − 1 (arithmetic shift: floor for negatives);
+    // 9 samples spaced size/(size−1) ≤ 12/11 apart then end at most 14 columns into the region
+    if (TR) o = ((axis == 0 ? W : H) >> l) <= 8 ? -4 : (o >> 2) << 2;
     sr[slot][l][axis][i] = fin && isfinite(s) ? (int)floorf(s) - o : -1;
     if (i == 0) org[slot][l][axis] = o;
   }
@@ -402,15 +409,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 // profiling: where the next LDS-kernel launches write their phase stamps (NULL: off)
 static unsigned long long* g_lk_stamps = nullptr;
 
-// SCFLOW_LK_TILEREG=1: the tiled r = 4 lookup stages 16×16 tile-aligned regions with b128 tile-row
-// loads (corr_lookup_lds_kernel TR) instead of 12×12 windows with b32 loads
-static bool lk_tile_regions() {
-  static int v = -1;
-  if (v < 0) {
+// Tile regions (corr_lookup_lds_kernel TR) for the tiled r = 4 lookup when the feature map has at
+// most 32×32 pixels: measured (tools/lookup_bench.py, tools/sess_lk.sh) 25.0 -> 23.1 us standalone
+// and 34 -> 28 us inside the decoder at configs[1] (B=16, 32x32), but 165.6 -> 176.6 us at
+// configs[4] (B=32, 64x64), where their 4 KB per pixel of LDS leaves 2 workgroups per CU instead
+// of 3.  SCFLOW_LK_TILEREG=0 / 1 forces them off / on.
+static bool lk_tile_regions(int h, int w) {
+  static int v = -2;
+  if (v == -2) {
     const char* e = getenv("SCFLOW_LK_TILEREG");
-    v = e ? atoi(e) : 0;
+    v = e ? atoi(e) : -1;
   }
-  return v != 0;
+  return v < 0 ? (long long)h * w <= 32 * 32 : v != 0;
 }
 
 static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layout, float* out,
@@ -451,7 +461,7 @@ static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layo
   corr_lookup_lds_kernel<RR, TT><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout,      \
                                                         out_stride, n, h, w, num_levels, vec, ac,  \
                                                         g_lk_stamps)
-    if (tiled && radius == 4 && lk_tile_regions()) {
+    if (tiled && radius == 4 && lk_tile_regions(h, w)) {
       const size_t lds_tr = sizeof(float) * LK_SLOTS * lk_tr_slot_floats(num_levels);
       corr_lookup_lds_kernel<4, true, true><<<blk, 256, lds_tr, st>>>(
           pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac, g_lk_stamps);
