@@ -92,6 +92,7 @@ class SCFlowDecoder(nn.Module):
         self.hoist_context = True
         # independent branches on a second HIP stream (else everything on the current stream)
         self.side_stream = True
+        self.dbg_skip_fullres = False  # measurement only (tools/ab_bench.py)
         # fork / join with device-scope events (no system-scope cache writeback per record)
         self.device_scope_events = True
         # the iteration's tail (pose update, pose flow, ×8 prediction, next ↓8 flow) as one
@@ -639,7 +640,9 @@ class SCFlowDecoder(nn.Module):
                     c()
                 if not fc:
                     self._hook(hook, False)
-                pending = fc
+                # (dbg_skip_fullres: measurement only — drops the deferred full-resolution
+                # outputs to price their side-stream contention; outputs are then incomplete)
+                pending = [] if self.dbg_skip_fullres else fc
             else:
                 self.pose_pred.heads_hip(pose_x[0], label, drot, dtr)
                 # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
