@@ -3,6 +3,7 @@
 // align_corners=True resampling (scflow_decoder.py:197-198, 223-228).
 #pragma once
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -259,6 +260,17 @@ __device__ __forceinline__ void pose_step_body(const PoseStepArgs& a, float* sh,
 }
 
 // scflow_pose_step's argument checks and block split (blocks of `nt` threads): 0 or an error
+// workgroups per image of the full-resolution part from a given pose (the decoder's deferred,
+// side-stream launch); SCFLOW_FULLRES_BLOCKS overrides the default 64 (tuning)
+static inline int fullres_blocks() {
+  static int v = 0;
+  if (v == 0) {
+    const char* e = getenv("SCFLOW_FULLRES_BLOCKS");
+    v = e && atoi(e) > 0 ? atoi(e) : 64;
+  }
+  return v;
+}
+
 static inline int pose_step_args(PoseStepArgs* a, const float* drot6, const float* dt,
                                  const float* R_src, const float* t_src, const float* K,
                                  const float* points, float* R_dst, float* t_dst, float* flow, int n,
@@ -286,7 +298,7 @@ static inline int pose_step_args(PoseStepArgs* a, const float* drot6, const floa
   const int bf = ceil_div((long long)H * W, nt);
   // from a given pose the part runs beside other work (the decoder's side stream): 4 pixels per
   // thread, a quarter of the workgroups to schedule
-  const int bfmax = given ? 64 : 256;
+  const int bfmax = given ? fullres_blocks() : 256;
   a->bf = bf < bfmax ? bf : bfmax;
   const int bl = ceil_div((long long)h * w, nt);
   a->bl = lr_next ? (bl < 64 ? bl : 64) : 0;
