@@ -563,8 +563,14 @@ class XHead(nn.Module):
 # ---------------------------------------------------------------------------------- a7
 @MODELS.register_module()
 class MultiClassPoseHead(nn.Module):
-    """pose_head.py:110-211.  Stride-2 conv + GroupNorm + FC stack run on stock PyTorch-ROCm
-    (MIOpen / hipBLASLt): 0.16 GFLOP per pair-iteration, 2.5% of the step."""
+    """pose_head.py:110-211.  Three stride-2 3×3 conv + GroupNorm + ReLU layers, two FCs and the
+    per-class rotation / translation heads (label[0] quirk kept); forward_hip / trunk_hip run them
+    on the HIP kernels (MFMA halo conv and gather conv with K splits, GroupNorm-statistics
+    reduce, K-split FCs), 0.16 GFLOP per pair-iteration."""
+    # workgroups the K splits aim for: the MFMA halo convs (conv1, conv2) and the gather conv
+    # (conv3) — tuning attributes (tools/ab_bench.py)
+    conv_wg_target = 512
+    gather_wg_target = 256
     _conv_feat_channels = {"Basic": [128, 128, 128], "Large": [128, 128, 128]}
     _conv_strides = {"Basic": [2, 2, 2], "Large": [2, 2, 2]}
     _conv_paddings = {"Basic": [1, 1, 1], "Large": [1, 1, 1]}
@@ -651,7 +657,7 @@ class MultiClassPoseHead(nn.Module):
             packs[i] = (key, ops.enc_conv_pack(wt))
         tiles = n * (oh // (tm // tc)) * (ow // tc) * ((conv.out_channels + 63) // 64)
         nst = (src0.c + c1) // 16
-        ksplit = max(1, min(nst, -(-512 // tiles)))
+        ksplit = max(1, min(nst, -(-self.conv_wg_target // tiles)))
         parts = torch.empty(ksplit * n * oh * ow, conv.out_channels, device=src0.buf.device)
         if keep is not None:
             keep.append(parts)
@@ -709,7 +715,7 @@ class MultiClassPoseHead(nn.Module):
                 # 32 output tiles → 8 slices), summed by the GroupNorm-statistics kernel
                 tiles = -(-n * oh * ow // 32) * -(-cout // 32)
                 nk = k * k * -(-(cur0.c + (0 if cur1 is None else cur1.c)) // 16)
-                ks = max(1, min(nk // 16, -(-256 // tiles)))
+                ks = max(1, min(nk // 16, -(-self.gather_wg_target // tiles)))
                 parts = empty(ks * n * oh * ow, cout)
                 ops.ph_conv(cur0, cur1, packs[i], None, n, hh, ww, cout, k, s, p, parts, scale, shift,
                             ksplit=ks)
