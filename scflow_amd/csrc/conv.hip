@@ -667,8 +667,14 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
   const int q4 = cin / 4;
   const int nh = (tr + KH - 1) * hcols * q4;  // float4 of the halo
   const int tiles_per_img = oh / tr;
-  const int img = blockIdx.x / tiles_per_img;
-  const int oy0 = (blockIdx.x % tiles_per_img) * tr;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so block b takes tile
+  // (b % 8)·(grid / 8) + b / 8 and each XCD covers a contiguous run of row tiles — the halo rows
+  // two neighbouring tiles share are fetched once into that XCD's L2 (flow predictor at B = 16:
+  // 15.0 -> 14.6 us in isolation, tools/sess_thin.sh)
+  const int bid = gridDim.x % 8 ? (int)blockIdx.x
+                                : (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
+  const int img = bid / tiles_per_img;
+  const int oy0 = (bid % tiles_per_img) * tr;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // every load first, then every LDS store (at most 9 float4 per thread at 4 × 34 × 256)
@@ -703,6 +709,9 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
     for (int tx = 0; tx < KW; ++tx) {
       const float* hp = halo + ((py + ty) * hcols + px + tx) * ld + c0;
       const float* wp = a.weight + (size_t)(ty * KW + tx) * cin + c0;
+#ifdef THINF_UNROLL  // channel-chunk loop unroll of the contraction (tuning build flag)
+#pragma unroll THINF_UNROLL
+#endif
       for (int c = 0; c < cw; c += 4) {
         const floatx4 x = *(const floatx4*)(hp + c);
 #pragma unroll
