@@ -670,7 +670,7 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
   // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so block b takes tile
   // (b % 8)·(grid / 8) + b / 8 and each XCD covers a contiguous run of row tiles — the halo rows
   // two neighbouring tiles share are fetched once into that XCD's L2 (flow predictor at B = 16:
-  // 15.0 -> 14.6 us in isolation, tools/sess_thin.sh)
+  // 15.0 -> 14.6 us in isolation, tools/sess_variant.sh)
   const int bid = gridDim.x % 8 ? (int)blockIdx.x
                                 : (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
   const int img = bid / tiles_per_img;
