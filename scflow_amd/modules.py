@@ -568,9 +568,10 @@ class MultiClassPoseHead(nn.Module):
     on the HIP kernels (MFMA halo conv and gather conv with K splits, GroupNorm-statistics
     reduce, K-split FCs), 0.16 GFLOP per pair-iteration."""
     # workgroups the K splits aim for: the MFMA halo convs (conv1, conv2) and the gather conv
-    # (conv3) — tuning attributes (tools/ab_bench.py)
+    # (conv3) — tuning attributes (tools/ab_bench.py; conv3 at B = 16: 128 → 4 K slices, 5.220 vs
+    # 5.240 ms/forward for 256 → 8, median of 9)
     conv_wg_target = 512
-    gather_wg_target = 256
+    gather_wg_target = 128
     _conv_feat_channels = {"Basic": [128, 128, 128], "Large": [128, 128, 128]}
     _conv_strides = {"Basic": [2, 2, 2], "Large": [2, 2, 2]}
     _conv_paddings = {"Basic": [1, 1, 1], "Large": [1, 1, 1]}
