@@ -713,7 +713,7 @@ class MultiClassPoseHead(nn.Module):
             split = self._conv_mfma(i, cur0, cur1, n, hh, ww, scale, shift, keep)
             if split is None and conv.bias is None:
                 # gather conv with its K split over enough slices to fill the CUs (conv3 at B=16:
-                # 32 output tiles → 8 slices), summed by the GroupNorm-statistics kernel
+                # 32 output tiles → 4 slices), summed by the GroupNorm-statistics kernel
                 tiles = -(-n * oh * ow // 32) * -(-cout // 32)
                 nk = k * k * -(-(cur0.c + (0 if cur1 is None else cur1.c)) // 16)
                 ks = max(1, min(nk // 16, -(-self.gather_wg_target // tiles)))
