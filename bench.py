@@ -178,8 +178,26 @@ def conv_roofline(kernel, parts, timers, m_px, traffic=None, alg_bytes=None):
     return out
 
 
+def time_fullres_alone(dec, reps=20):
+    """The pose step's deferred full-resolution launch (iteration 0's recorded call) on an idle
+    GPU, bracketed by the same events: its rate without the concurrent out_net / GRU launches."""
+    from scflow_amd.profiling import EventTimer
+    calls = getattr(dec, "_tail_calls", None)
+    fc = calls[0][2] if calls else []
+    if not fc:
+        return None
+    t = EventTimer()
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        t(True)
+        for c in fc:
+            c()
+        t(False)
+    return t.mean_ms()
+
+
 def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail_weight_bytes=0,
-                        tiled=True):
+                        tiled=True, fullres_alone_ms=None):
     """The HBM/gather-bound kernels and the correlation GEMM, timed with the same events in an
     untimed pass after the timed region (algorithmic bytes per launch from SURVEY.md §8(d)).
     At B=16, 256² the 86 MB pyramid is Infinity-Cache resident, so the lookup's GB/s is an
@@ -190,6 +208,9 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
     # pose flow: 16-B point read + 8-B flow write per pixel; the fused tail (pose_step_kernel)
     # also writes the ×8 flow prediction and mask (12 B per pixel)
     flow_bytes = batch * (36 if fused_tail else 20) * size * size
+    # the deferred tail's critical-path ↓8 launch: the pose flow at the 4 bilinear source pixels
+    # of every feature pixel (4 × 16-B points) + the next ↓8 flow written twice (F2, HX: 16 B)
+    crit_bytes = batch * P * (4 * 16 + 16)
     corr_flops = 2.0 * batch * P * P * 256
     traffic = traffic or {}
     out = []
@@ -197,10 +218,14 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
             ("corr_lookup", "corr_lookup", "corr_lookup_lds_kernel<4> (a2%s)" % (", tiled pyramid"
                                                                               if tiled else ""),
              "hbm", lookup_bytes),
-            ("pose_flow", "pose_step", "pose_step_kernel (a8+a10+a11), its full-resolution launch: "
-             "queued on the side stream behind the next iteration's join, so it shares the CUs "
-             "with out_net / the GRU (a rate under contention, not the kernel alone)" if fused_tail
+            ("pose_flow", "pose_step_fullres", "pose_step_kernel (a8+a10+a11), its deferred "
+             "full-resolution launch (7 per forward): queued on the side stream behind the next "
+             "iteration's join, so it shares the CUs with out_net / the GRU — `achieved` is that "
+             "contended rate, `alone` the same launch on an idle GPU" if fused_tail
              else "pose_flow_kernel (a8+a10)", "hbm", flow_bytes),
+            ("pose_step_crit", "pose_step_crit", "pose_step_kernel (a8 + the next iteration's a11 "
+             "↓8), its critical-path launch (parts = 2, 7 per forward): latency-bound, 4 "
+             "workgroups per pair", "hbm", crit_bytes),
             # the persistent pose-head tail (GN 1 → convs 2-3 → FCs → heads) + the pose step:
             # bytes = the pose step's 36 B/pixel + the pose head's weights after conv 1 (read once)
             ("pose_tail", "ph_tail", "ph_tail_kernel (a7 after conv 1 + a8+a10+a11, one persistent "
@@ -225,8 +250,12 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
              ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): amount}
         if bound == "hbm":
             e.update(extra)
+        if name == "pose_flow" and fullres_alone_ms:
+            e["alone"] = {"avg_launch_ms": round(fullres_alone_ms, 4),
+                          "achieved": round(amount / (fullres_alone_ms * 1e-3) / 1e9, 2),
+                          "frac": round(amount / (fullres_alone_ms * 1e-3) / 1e9 / peak, 4)}
         if bound == "hbm":
-            tr = traffic.get(tkey)
+            tr = traffic.get(tkey)  # per launch kind (tools/traffic_json.py), or None
             e["traffic"] = tr
             if tr:
                 e["traffic_over_algorithmic"] = round(tr / amount, 3)
@@ -252,10 +281,19 @@ def bench_train(args, world, rank, dev, feat):
     pts = [torch.from_numpy(p).to(dev) for p in synthetic.make_model_points(1024)]
     step = TrainStep(ref, pts, synthetic.YCBV_DIAMETERS)
     losses = []
+    evs = []
 
     def one():
+        # device events on the caller's stream around each step (the step orders itself after
+        # and before it): the step's span on the GPU timeline, idle gaps inside it included
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
         losses.append(step(batch)["loss"].detach())
+        b.record()
+        evs.append((a, b))
     el = time_steps(one, args.train_steps, 2, world, dev)
+    torch.cuda.synchronize()
+    per = sorted(a.elapsed_time(b) for a, b in evs[2:])  # the timed steps
     nparam = sum(p.numel() for p in step.grads.params)
     gb = world * args.train_batch
     which = ("BASELINE configs[3]" if (world, args.train_batch, args.size, args.iters) == (8, 16, 256, 8)
@@ -266,6 +304,8 @@ def bench_train(args, world, rank, dev, feat):
                        f"{args.size}x{args.size}, {args.iters} iters — {which}",
            "value": round(gb * args.iters * args.train_steps / el, 2),
            "unit": "iters/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
+           "per_step_ms": {"median": round(per[len(per) // 2], 3), "min": round(per[0], 3),
+                           "max": round(per[-1], 3), "spread": round((per[-1] - per[0]) / per[len(per) // 2], 4)},
            "steps": args.train_steps, "warmup": 2, "global_batch": gb, "n_gpus": world,
            "allreduce_bytes": 4 * nparam if world > 1 else 0,
            "buckets": len(step.grads.buckets),
@@ -279,13 +319,27 @@ def cpu_baseline(seconds: float, batch: int, iters: int, size: int):
     repeated until ``seconds`` have passed (at least one forward)."""
     from oracle import scflow_oracle as orc
     from scflow_amd import MODELS, synthetic
-    threads = torch.get_num_threads()
     feat = (size // 8, size // 8) if size != 256 else None
     dec = MODELS.build(decoder_cfg(iters, feat))
     synthetic.fill_module_(dec)
     sd = {k: v.detach() for k, v in dec.state_dict().items()}
     inp = make_inputs(batch, size, 100, "cpu")
-    orc.decoder_forward(sd, **inp, iters=1)  # warm up allocator / threads
+    # SURVEY.md §8(d): torch.set_num_threads(os.cpu_count()).  On a shared box os.cpu_count()
+    # counts the whole machine while this process may be confined to a share of it (affinity,
+    # cgroup quota, OMP_NUM_THREADS), so the candidates are probed with one short forward each
+    # and the fastest thread count runs the sample; every count is reported.
+    counts = host_cpu_counts()
+    cands = sorted({c for c in (counts["os_cpu_count"], counts["affinity"], counts["cgroup_quota"],
+                                counts["torch_default"]) if c})
+    probe = {}
+    for c in cands:
+        torch.set_num_threads(c)
+        orc.decoder_forward(sd, **inp, iters=1)  # warm up allocator / threads
+        t0 = time.perf_counter()
+        orc.decoder_forward(sd, **inp, iters=1)
+        probe[c] = round(time.perf_counter() - t0, 3)
+    threads = min(probe, key=probe.get)
+    torch.set_num_threads(threads)
     reps, t0 = 0, time.perf_counter()
     while True:
         orc.decoder_forward(sd, **inp, iters=iters)
@@ -293,11 +347,28 @@ def cpu_baseline(seconds: float, batch: int, iters: int, size: int):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    torch.set_num_threads(counts["torch_default"])
     return {"value": round(reps * batch * iters / el, 3), "unit": "iters/s", "cores": threads,
             "kind": "port",
             "sample": f"oracle decoder (PyTorch CPU fp32), B={batch} pairs x {iters} iters at "
                       f"{size}x{size} (the bench's own workload), {reps} forward(s) in {el:.1f}s, "
-                      f"torch threads={threads}"}
+                      f"torch threads={threads} (fastest of the probed counts)",
+            "host_cpus": counts, "thread_probe_s_per_1iter_forward": probe}
+
+
+def host_cpu_counts():
+    """os.cpu_count(), the affinity mask, the cgroup CPU quota (cpu.max) and torch's default."""
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"os_cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "cgroup_quota": quota, "torch_default": torch.get_num_threads(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def spawn_ranks(n: int) -> int:
@@ -331,7 +402,7 @@ def main():
     ap.add_argument("--train-batch", type=int, default=16,
                     help="pairs/GPU of the extra training-step measurement (BASELINE configs[3]); "
                          "0 disables it")
-    ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--train-steps", type=int, default=12)
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="do not bracket the roofline kernels (throughput without timer overhead)")
     ap.add_argument("--pingpong", action="store_true",
@@ -378,7 +449,7 @@ def main():
     # step, not 2 per launch.
     per_step = {"heads": args.iters, "corr_net1": args.iters, "gru_zr": 2 * args.iters,
                 "corr_lookup": args.iters, "pose_flow": args.iters, "pose_tail": args.iters,
-                "corr_pyramid": 1}
+                "pose_step_crit": args.iters, "corr_pyramid": 1}
     per_step.update({n: args.iters for n in WINO_LAUNCHES[2:]})
     # the headline kernel's launches (every conv_wino_kernel launch of an iteration): bracketed in
     # the timed region, each timer on one launch every other step (an event pair costs a few µs
@@ -420,6 +491,7 @@ def main():
         torch.cuda.synchronize()
         for t in timers.values():
             t.enabled = False
+    fullres_alone = None if args.graph else time_fullres_alone(dec)
     dec.kernel_hooks.clear()
 
     e2e = None
@@ -518,7 +590,8 @@ def main():
     tail_w = 4 * sum(p.numel() for m in (ph.conv_layers[1:], ph.fc_layers) for p in m.parameters())
     tail_w += 4 * (ph.rotation_out_channels + 3) * ph.fc_layers[-1][0].out_features  # label[0] rows
     secondary += secondary_rooflines(timers, hb, args.size, traffic,
-                                     getattr(dec, "fuse_tail", True), tail_w, dec.tiled_pyramid)
+                                     getattr(dec, "fuse_tail", True), tail_w, dec.tiled_pyramid,
+                                     fullres_alone)
 
     if rank == 0:
         cfg_name = ("configs[4]" if (args.batch, args.size, args.iters) == (32, 512, 12)

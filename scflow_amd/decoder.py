@@ -633,13 +633,14 @@ class SCFlowDecoder(nn.Module):
                 hc, pc, fc = tail_calls[it]
                 for c in hc:
                     c()
-                hook = "pose_tail" if fuse_ph else "pose_flow"
-                if not fc:
-                    self._hook(hook, True)
+                # deferred: this is the critical-path ↓8 launch (its own timer); otherwise the
+                # whole pose step
+                hook = "pose_step_crit" if fc else "pose_tail" if fuse_ph else "pose_flow"
+                self._hook(hook, True)
                 for c in pc:
                     c()
-                if not fc:
-                    self._hook(hook, False)
+                self._hook(hook, False)
+                self._tail_calls = tail_calls  # measurement: bench.py times a launch alone
                 # (dbg_skip_fullres: measurement only — drops the deferred full-resolution
                 # outputs to price their side-stream contention; outputs are then incomplete)
                 pending = [] if self.dbg_skip_fullres else fc

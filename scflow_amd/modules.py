@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import _lib, ops
+from . import _lib, library, ops
 from ._lib import EPI_GRU_Q, EPI_GRU_ZR, EPI_PLAIN, ScflowError
 from .ops import Chan
 from .registry import MODELS
@@ -227,8 +227,9 @@ class CorrelationPyramid(nn.Module):
         self.num_levels = num_levels
 
     def forward(self, feat1: Tensor, feat2: Tensor) -> List[Tensor]:
-        _, levels = ops.corr_pyramid(feat1.contiguous(), feat2.contiguous(), self.num_levels)
-        return levels
+        n, _, h, w = feat1.shape
+        buf = library.corr_pyramid(feat1, feat2, self.num_levels)  # torch.ops.scflow.corr_pyramid
+        return ops.pyramid_views(buf, n, h, w, self.num_levels)
 
 
 class CorrLookup(nn.Module):
@@ -247,9 +248,12 @@ class CorrLookup(nn.Module):
 
     def forward(self, corr_pyramid: Sequence[Tensor], flow: Tensor) -> Tensor:
         B, _, H, W = flow.shape
-        buf = ops.pyramid_buffer(corr_pyramid, B, H, W)
-        return ops.corr_lookup(buf, flow.contiguous().float(), B, H, W, len(corr_pyramid), self.r,
-                               align_corners=self.align_corners)
+        if torch.compiler.is_compiling():  # fake tensors have no storage to alias
+            buf = torch.cat([lv.reshape(-1) for lv in corr_pyramid])
+        else:
+            buf = ops.pyramid_buffer(corr_pyramid, B, H, W)
+        # torch.ops.scflow.corr_lookup
+        return library.corr_lookup(buf, flow.float(), len(corr_pyramid), self.r, self.align_corners)
 
 
 # ---------------------------------------------------------------------------------- a3

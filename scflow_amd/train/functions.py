@@ -110,7 +110,10 @@ class direct_weight_grads:
     no gradient for them — instead of a fresh dW per use, autograd summing a decoder weight's 8
     per-iteration gradients and AccumulateGrad adding the sum.  Only for parameters whose
     ``.grad`` is already allocated (GradBuckets' flat views) and when nothing observes their
-    accumulation (no post-accumulate-grad hooks: TrainStep without ``overlap``)."""
+    accumulation (no post-accumulate-grad hooks: TrainStep without ``overlap``).
+
+    Leaving the scope sums the recorded uses a backward pass never reached
+    (``flush_pending_wgrads``), so the gradients are complete once it exits."""
 
     def __enter__(self):
         global _DIRECT_WGRAD
@@ -120,6 +123,8 @@ class direct_weight_grads:
     def __exit__(self, *exc):
         global _DIRECT_WGRAD
         _DIRECT_WGRAD = self._prev
+        if exc[0] is None:
+            flush_pending_wgrads()
         return False
 
 
@@ -302,8 +307,21 @@ def _use_holder(w: Tensor) -> dict:
 
 def _flush_wgrad(items, w: Tensor, with_bias: bool, dw: Tensor, db: Optional[Tensor],
                  accumulate: bool, s: int, ph: int, pw: int) -> None:
-    """dw (db) (+)= Σ over items (g, x0, x1) of the conv weight (bias) gradient: batched launches
-    of ≤ 8 segments, per-item launches where the batched kernel does not take the shape."""
+    """dw (db) (+)= Σ over items (g, x0, x1) of the conv weight (bias) gradient.  Uses of one
+    weight at different shapes (a shared encoder on differently sized inputs) are summed group by
+    group: the batched kernels take one (g, x0, x1) shape per call."""
+    groups: dict = {}
+    for it in items:
+        key = tuple(None if t is None else tuple(t.shape) for t in it)
+        groups.setdefault(key, []).append(it)
+    for i, grp in enumerate(groups.values()):
+        _flush_wgrad_same(grp, w, with_bias, dw, db, accumulate or i > 0, s, ph, pw)
+
+
+def _flush_wgrad_same(items, w: Tensor, with_bias: bool, dw: Tensor, db: Optional[Tensor],
+                      accumulate: bool, s: int, ph: int, pw: int) -> None:
+    """_flush_wgrad over items of one shape: batched launches of ≤ 8 segments, per-item launches
+    where the batched kernel does not take the shape."""
     g0, x00, x10 = items[0]
     n, h, wd, _ = x00.shape
     cout, cin, kh, kw = w.shape
@@ -463,7 +481,7 @@ def _conv_backward(ctx, dy):
     pad_co = (-cout) % 4 if cout > 4 else 0
     gp = F.pad(g, (0, pad_co)) if pad_co else g
     if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
-        if s == 1 and kh == kw == 1 and cout == 1:
+        if s == 1 and kh == kw == 1 and cout == 1 and ph == pw == 0:
             # 1×1 to one channel (the mask predictor): dX = dY ⊗ w, one broadcast multiply
             # (a 1 → cin conv launch took 27 µs for the 16 MB it writes)
             dx = g * w.detach().reshape(1, 1, 1, cin)
@@ -522,36 +540,49 @@ def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride
 
 
 # ------------------------------------------------------------------------------- ConvGRU step
-def _shared_grad_holder(w: Tensor) -> dict:
-    """A gradient accumulator shared by every use of the per-step tensor ``w`` (the GRU's
-    concatenated weights, used by all 8 iterations)."""
-    holder = getattr(w, "_scflow_gacc", None)
-    if holder is None:
-        holder = {"buf": None, "uses": 0, "seen": 0, "items": []}
-        w._scflow_gacc = holder
-    holder["uses"] += 1
-    return holder
+class _SharedWeight(torch.autograd.Function):
+    """Identity node in front of a weight that several GRU steps of one forward pass use (the
+    SepConvGRU's concatenated weights, 8 iterations).  The uses' backwards record their (dY, x0,
+    x1) here and hand autograd no weight gradient; autograd runs THIS node's backward only after
+    every use the pass reached, and it sums exactly the recorded ones in ONE batched weight
+    gradient (scflow_conv_wgrad_batched).  The node belongs to one forward pass, so nothing is
+    carried between passes, uses a pass never reaches contribute nothing, and a second backward
+    over the same graph (retain_graph) records and sums afresh."""
+
+    @staticmethod
+    def forward(ctx, w):
+        ctx.set_materialize_grads(False)
+        ctx.items = []
+        ctx.pad = None
+        ctx.wmeta = w.detach()
+        return w.view_as(w)
+
+    @staticmethod
+    def backward(ctx, g):
+        items, ctx.items = ctx.items, []
+        if not items:
+            return g
+        ph, pw = ctx.pad
+        buf = torch.empty_like(ctx.wmeta)
+        _flush_wgrad(items, ctx.wmeta, False, buf, None, False, 1, ph, pw)
+        return buf if g is None else g + buf
 
 
-def _shared_wgrad(holder: dict, w: Tensor, item, ph: int, pw: int) -> Optional[Tensor]:
-    """Record this use's (g, x0, x1) for the shared weight ``w``; the first backward call hands
-    autograd the gradient buffer, the later ones nothing — autograd runs the backward of ``w``'s
-    producer only after every use, so the last call fills it first: ONE batched weight gradient
-    over all uses (scflow_conv_wgrad_batched), no per-use launches or adds.  A pass that has seen
-    every use starts over, so a second pass over the same graph (retain_graph) sums afresh."""
-    first = holder["buf"] is None
-    if first:
-        holder["buf"] = torch.empty_like(w)
-        holder["items"] = []
-    buf = holder["buf"]
-    holder["items"].append(item)
-    holder["seen"] += 1
-    if holder["seen"] >= holder["uses"]:
-        _flush_wgrad(holder["items"], w, False, buf, None, False, 1, ph, pw)
-        holder["buf"] = None
-        holder["items"] = []
-        holder["seen"] = 0
-    return buf if first else None
+def share_weight(w: Tensor) -> Tensor:
+    """``w`` behind a _SharedWeight node: pass the result to every gru_step of a forward pass that
+    uses this weight, so its weight gradient is one batched launch over all the uses."""
+    return _SharedWeight.apply(w)
+
+
+def _shared_node(w: Tensor):
+    node = w.grad_fn
+    return node if isinstance(node, _SharedWeight._backward_cls) else None
+
+
+def _record_shared(node, item, ph: int, pw: int) -> None:
+    if node.pad is None:
+        node.pad = (ph, pw)
+    node.items.append(item)
 
 
 def _channel_rows(t: Tensor) -> bool:
@@ -584,7 +615,7 @@ class _GruStep(torch.autograd.Function):
         h2 = ops.gru_gate_forward(zr, h, torch.empty_like(h), q=q)
         ctx.save_for_backward(h, x, zr, rh, q, w_zr, w_q)
         ctx.pad = pad
-        ctx.acc = (_shared_grad_holder(w_zr), _shared_grad_holder(w_q))
+        ctx.acc = (_shared_node(w_zr), _shared_node(w_q))  # gru_step puts both behind one
         return h2
 
     @staticmethod
@@ -600,21 +631,27 @@ class _GruStep(torch.autograd.Function):
             dh2 = dh2.contiguous()
         ops.gru_gate_backward_q(dh2, zr, h, q, dq, dzr, dha)
         dxq = _conv_forward(dq, None, _flip_t(w_q), None, 1, (kh - 1 - ph, kw - 1 - pw))
-        dw_q = _shared_wgrad(ctx.acc[1], w_q, (dq, rh, x), ph, pw)
+        _record_shared(ctx.acc[1], (dq, rh, x), ph, pw)
         # dh = dha + drh·r written over drh = dxq[..., :c] itself, so that dxq becomes [dh | dx_q]
         # and the z | r conv's dX, with dxq as its added map, yields both sums in its epilogue:
         # T = [dh + dxz_h | dx_q + dxz_x] (no separate adds; dh and dx leave as channel views)
         ops.gru_gate_backward_r(dxq[..., :c], zr, h, dha, dzr, dxq[..., :c])
         t = _conv_forward(dzr, None, _flip_t(w_zr), None, 1, (kh - 1 - ph, kw - 1 - pw), bias_map=dxq)
-        dw_zr = _shared_wgrad(ctx.acc[0], w_zr, (dzr, h, x), ph, pw)
-        return t[..., :c], t[..., c:], dw_zr, dw_q, dzr, dq, None
+        _record_shared(ctx.acc[0], (dzr, h, x), ph, pw)
+        return t[..., :c], t[..., c:], None, None, dzr, dq, None
 
 
 def gru_step(h: Tensor, x: Tensor, w_zr: Tensor, w_q: Tensor, pre_zr: Tensor, pre_q: Tensor,
              padding) -> Tensor:
     """h' of one SepConvGRU direction; channels-last h [.., c], x [.., cx]; w_zr [2c, c + cx, ..],
-    w_q [c, c + cx, ..]; pre_zr / pre_q: the pre-activation maps added before σ / tanh."""
+    w_q [c, c + cx, ..]; pre_zr / pre_q: the pre-activation maps added before σ / tanh.  Weights
+    used by several steps of one pass should come through ``share_weight`` (one batched weight
+    gradient for all the uses); any other tensor gets a node of its own (one use)."""
     pad = (padding, padding) if isinstance(padding, int) else tuple(padding)
+    if _shared_node(w_zr) is None:
+        w_zr = share_weight(w_zr)
+    if _shared_node(w_q) is None:
+        w_q = share_weight(w_q)
     return _GruStep.apply(h, x, w_zr, w_q, pre_zr, pre_q, pad)
 
 

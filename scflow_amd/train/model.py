@@ -23,7 +23,8 @@ from .. import ops
 from ..ops import Chan
 from .functions import (begin_forward, conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid,
                         group_norm_nhwc, gru_step, instance_norm_nhwc,
-                        instance_norm_residual_relu_nhwc, linear, pose_update6, upsample_bilinear_ac)
+                        instance_norm_residual_relu_nhwc, linear, pose_update6, share_weight,
+                        upsample_bilinear_ac)
 from .losses import LowRes, filter_flow_by_mask, matmul3, refine_losses
 
 Tensor = torch.Tensor
@@ -185,8 +186,11 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
         bzr = torch.cat([z.bias, rr.bias], 0)
         ctx_pre.append((conv2d_nhwc(cxt, wzr[:, hc:hc + cc], bzr, 1, q.padding),
                         conv2d_nhwc(cxt, q.weight[:, hc:hc + cc], q.bias, 1, q.padding)))
-        it_w.append((torch.cat([wzr[:, :hc], wzr[:, hc + cc:]], 1),
-                     torch.cat([q.weight[:, :hc], q.weight[:, hc + cc:]], 1), q.padding))
+        w_zr = torch.cat([wzr[:, :hc], wzr[:, hc + cc:]], 1)
+        w_q = torch.cat([q.weight[:, :hc], q.weight[:, hc + cc:]], 1)
+        if _GRU_FUSED:  # one batched weight gradient over the 8 iterations' uses
+            w_zr, w_q = share_weight(w_zr), share_weight(w_q)
+        it_w.append((w_zr, w_q, q.padding))
     for _ in range(iters):
         with torch.no_grad():  # flow is detached every iteration (detach_flow=True)
             f2 = torch.empty(N * hh * ww, 2, device=depth.device, dtype=dt)

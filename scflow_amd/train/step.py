@@ -6,8 +6,8 @@ Data parallel = one process per GPU (torch.distributed over RCCL).  Gradients li
 flat fp32 buckets (every ``param.grad`` is a view into one), so the exchange is one all-reduce
 per bucket, sized for xGMI (default 8 MB, 4 buckets for the 32.7 MB model: large enough that
 the ring is link-bound).  By default the buckets are reduced right after the backward pass,
-all issued before the first wait (the 32.7 MB exchange is ≈0.3 ms against a ≈100 ms step, so
-overlapping it buys < 0.5 %); ``overlap=True`` instead issues each bucket's all-reduce from a
+all issued before the first wait (the 32.7 MB exchange is ≈0.3 ms against a ≈40 ms step at
+B = 16 per GPU, so overlapping it buys < 1 %); ``overlap=True`` instead issues each bucket's all-reduce from a
 post-accumulate-grad hook as soon as its last gradient is written (buckets filled in reverse
 registration order ≈ the order backward produces gradients).  No per-parameter collectives,
 no DDP wrapper.
@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from .._lib import bump_weights_generation
-from .functions import capture_cache, direct_weight_grads, flush_pending_wgrads
+from .functions import capture_cache, direct_weight_grads
 from .model import refiner_train_forward
 
 Tensor = torch.Tensor
@@ -160,9 +160,8 @@ class TrainStep:
             if self.grads._hooks:  # per-parameter hooks must see every accumulation
                 out["loss"].backward()
             else:
-                with direct_weight_grads():
+                with direct_weight_grads():  # its exit sums uses the pass did not reach
                     out["loss"].backward()
-                flush_pending_wgrads()  # uses whose last use the pass did not reach
         # detached: a returned tensor must not keep this step's autograd graph (and its
         # AccumulateGrad nodes) alive into the next step or a capture
         return {k: _detach(v) for k, v in out.items()}

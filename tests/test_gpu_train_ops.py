@@ -409,6 +409,68 @@ def test_shared_gradient_buffers_across_backward_passes():
         torch.testing.assert_close(u, v, rtol=1e-6, atol=1e-7)
 
 
+def test_gru_shared_weights_across_cycles_and_short_passes():
+    """the same LEAF GRU weights through two separate forward/backward cycles (raw
+    leaves and share_weight), and a pass whose loss never reaches the second use, against the
+    unfused path (split conv + conv + lerp autograd ops) — no stale use counts, no uninitialised
+    gradient memory."""
+    from scflow_amd.train.functions import conv2d_nhwc, conv2d_nhwc_split, gru_step, share_weight
+    g = torch.Generator().manual_seed(43)
+    c = 128
+    hh = torch.tanh(torch.randn(1, 32, 32, c, generator=g)).cuda()
+    x = torch.randn(1, 32, 32, 128, generator=g).cuda()
+    wzr = (torch.randn(2 * c, 256, 1, 5, generator=g) * 0.02).cuda().requires_grad_()
+    wq = (torch.randn(c, 256, 1, 5, generator=g) * 0.02).cuda().requires_grad_()
+    pzr = (torch.randn(1, 32, 32, 2 * c, generator=g) * 0.1).cuda()
+    pq = (torch.randn(1, 32, 32, c, generator=g) * 0.1).cuda()
+
+    def unfused(h):
+        z, r = conv2d_nhwc_split(h, wzr, c, None, 1, (0, 2), act="Sigmoid", x1=x, bias_map=pzr)
+        q = conv2d_nhwc(r * h, wq, None, 1, (0, 2), act="Tanh", x1=x, bias_map=pq)
+        return torch.lerp(h, q, z)
+
+    def grads(loss_fn):
+        return [t.detach().clone() for t in torch.autograd.grad(loss_fn(), [wzr, wq])]
+
+    ref2 = grads(lambda: (unfused(unfused(hh)) ** 2).sum())
+    ref1 = grads(lambda: (unfused(hh) ** 2).sum())
+    for cycle in range(2):  # raw leaves: every call its own node
+        got = grads(lambda: (gru_step(gru_step(hh, x, wzr, wq, pzr, pq, (0, 2)), x, wzr, wq, pzr, pq,
+                                      (0, 2)) ** 2).sum())
+        for u, v, nm in zip(got, ref2, ("wzr", "wq")):
+            _close(u, v, 1e-4, 1e-6, f"raw leaves cycle {cycle} d{nm}")
+
+    def shared_two(short):
+        sz, sq = share_weight(wzr), share_weight(wq)
+        y1 = gru_step(hh, x, sz, sq, pzr, pq, (0, 2))
+        y2 = gru_step(y1, x, sz, sq, pzr, pq, (0, 2))
+        return ((y1 if short else y2) ** 2).sum()
+    for cycle in range(2):
+        for short, ref in ((False, ref2), (True, ref1)):
+            got = grads(lambda: shared_two(short))
+            for u, v, nm in zip(got, ref, ("wzr", "wq")):
+                _close(u, v, 1e-4, 1e-6, f"shared cycle {cycle} short={short} d{nm}")
+
+
+def test_conv_dx_shortcuts_match_conv2d_input():
+    """the 1×1 → 1-channel dX shortcut (dY ⊗ w, unpadded only) and the thin large-
+    kernel dX (GEMM + col2im) against torch.nn.grad.conv2d_input, plus a PADDED 1×1 → 1 conv,
+    which must not take the shortcut."""
+    from scflow_amd.train.functions import conv2d_nhwc
+    g = torch.Generator().manual_seed(44)
+    for (cin, cout, k, pad) in ((256, 1, 1, 0), (256, 1, 1, 1), (2, 128, 7, 3)):
+        x = torch.randn(2, 32, 32, cin, generator=g)
+        wt = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
+        xg = x.cuda().requires_grad_()
+        y = conv2d_nhwc(xg, wt.cuda(), None, 1, pad)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy.cuda())
+        ref = torch.nn.grad.conv2d_input(x.permute(0, 3, 1, 2).shape, wt.double(),
+                                         gy.double().permute(0, 3, 1, 2), padding=pad)
+        assert xg.grad.shape == x.shape
+        _close(xg.grad, ref.permute(0, 2, 3, 1), 1e-5, 1e-6, f"dX {cin}->{cout} {k}x{k} pad {pad}")
+
+
 @pytest.mark.parametrize("bt,M,N,K,ta,tb", [
     (1, 16, 1024, 2048, False, True),     # pose head FC forward: x · Wᵀ
     (1, 1024, 2048, 16, True, False),     # FC weight grad: dYᵀ · x

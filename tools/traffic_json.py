@@ -27,6 +27,9 @@ def groups(B, S):
     zr = f * M * (256 + 256 + 128 + 256) + f * 256 * 256 * 5   # h|motion, bias map, h, z|rh, W
     lookup = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
     pose_step = B * 36 * S * S
+    # the critical-path ↓8 launch (parts = 2): the pose flow at the 4 bilinear source pixels of
+    # every feature pixel (4 × 16-B points) + the next iteration's ↓8 flow (F2 and HX, 2 × 8 B)
+    pose_step_crit = M * (4 * 16 + 16)
 
     def conv(cin, cout, taps=9):
         return f * (M * cin + M * cout + cout * cin * taps)
@@ -45,17 +48,42 @@ def groups(B, S):
                     "conv_wino5_kernel<0, 32, 1, 1>", "conv_wino5_kernel<1, 32, 1, 1>"], zr,
                    "SepConvGRU z|r 1×5 + 5×1 (context hoisted)"),
         "corr_lookup": (["corr_lookup_lds_kernel"], lookup, "pyramid lookup r=4, 4 levels"),
-        "pose_step": (["pose_step_kernel"], pose_step, "pose update + pose flow + ×8 flow/mask"),
+        "pose_step": (["pose_step_kernel"], pose_step, "pose update + pose flow + ×8 flow/mask "
+                      "(every launch kind averaged: use the two entries below)"),
+        "pose_step_fullres": (["pose_step_kernel"], pose_step, "pose_step_kernel, its deferred "
+                              "full-resolution launch only (7 per forward): pose flow + ×8 "
+                              "flow/mask, 36 B per full-resolution pixel", "wide"),
+        "pose_step_crit": (["pose_step_kernel"], pose_step_crit, "pose_step_kernel, its critical-"
+                           "path ↓8 launch only (the smallest grid): pose update + the next "
+                           "iteration's ↓8 flow, 80 B per feature pixel", "min"),
     }
 
 
 def per_kernel(d, counter):
+    """{kernel name: [(grid size, counter value) per launch]}"""
     path = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)[0]
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            vals[r["Kernel_Name"]].append((int(r.get("Grid_Size") or 0), float(r["Counter_Value"])))
     return vals
+
+
+def select(vals, subs, which):
+    """Counter values of the launches of kernels matching ``subs``; ``which`` keeps one launch
+    kind: "min" the launches with the smallest grid, "wide" those with the most frequent grid size
+    above the smallest (the pose step: 7 deferred full-resolution launches per forward at B × 64
+    workgroups vs the last iteration's single combined launch, whose grid is larger still)."""
+    got = [gv for k, vs in vals.items() if any(s in k for s in subs) for gv in vs]
+    if which and got:
+        lo = min(g for g, _ in got)
+        if which == "min":
+            pick = lo
+        else:
+            above = collections.Counter(g for g, _ in got if g > lo)
+            pick = above.most_common(1)[0][0] if above else lo
+        got = [gv for gv in got if gv[0] == pick]
+    return [v for _, v in got]
 
 
 def main():
@@ -72,9 +100,9 @@ def main():
                      "bench.py (decoder leg only); FETCH_SIZE doubled per the gfx950 note; "
                      "WRITE_SIZE as is; memory-side (L2->fabric) bytes, Infinity-Cache hits included",
            "kernels": {}}
-    for name, (subs, alg, what) in groups(a.batch, a.size).items():
-        f = [v for k, vs in fetch.items() if any(s in k for s in subs) for v in vs]
-        w = [v for k, vs in write.items() if any(s in k for s in subs) for v in vs]
+    for name, (subs, alg, what, *which) in groups(a.batch, a.size).items():
+        f = select(fetch, subs, which[0] if which else None)
+        w = select(write, subs, which[0] if which else None)
         if not f or not w:
             continue
         hbm = (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024
