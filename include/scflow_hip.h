@@ -683,6 +683,8 @@ typedef struct {
   float* bary;
   void* workspace;
   long long workspace_bytes;
+  float* light_out;      /* optional [n_img][3]: the light location each image was shaded with
+                            (object frame) — the reference's PointLights location, :209-230 */
 } scflow_render_args;
 long long scflow_render_workspace(int n_img, int size, int total_verts);
 int scflow_render(const scflow_render_args* args, void* stream);

@@ -146,6 +146,22 @@ def phong(verts: Tensor, faces: Tensor, normals: Tensor, colors: Tensor, p2f: Te
     return torch.cat([rgb, hit[..., None].to(rgb)], -1)
 
 
+def light_location(verts: Sequence[Tensor], R: Tensor, t: Tensor, light=(True, True)) -> Tensor:
+    """[N, 3] PointLights location of Renderer.forward (:209-230) for ``light`` = (seperate_lights,
+    default_lights): R_i·(0, 0, max(min_z_i − 400, 0)) (seperate); pytorch3d's default (0, 1, 0)
+    (default colours, one light); R_i·(0, 0, znear/4), znear = ⌊batch min z / 100⌋·100 (ITODD)."""
+    seps, deflt = light
+    zmin = torch.stack([(v.to(R.dtype) @ R[i].T + t[i][None])[:, 2].min() for i, v in enumerate(verts)])
+    zero = torch.zeros_like(zmin)
+    if seps:
+        lz = torch.clamp(zmin - 400, min=0)
+    elif deflt:
+        return torch.tensor([0.0, 1.0, 0.0], dtype=R.dtype).expand(len(verts), 3).clone()
+    else:
+        lz = (torch.floor(zmin.min() / 100) * 100 / 4).expand_as(zmin)
+    return (R @ torch.stack([zero, zero, lz], -1)[..., None])[..., 0]
+
+
 def render(meshes: Dict[int, Tuple[Tensor, Tensor, Tensor]], R: Tensor, t: Tensor, K: Tensor,
            labels: Sequence[int], S: int, light=(True, True)):
     """Renderer.forward for a batch: meshes[label] = (verts [V,3], faces [F,3], colors [V,3]).
@@ -154,23 +170,14 @@ def render(meshes: Dict[int, Tuple[Tensor, Tensor, Tensor]], R: Tensor, t: Tenso
     seps, deflt = light
     imgs, zbufs, p2fs, barys = [], [], [], []
     offset = 0
-    # batch-wide znear for (not default_lights, not seperate_lights): ⌊min z / 100⌋·100 (:196-200)
-    zall = torch.cat([(meshes[int(lab)][0].to(R.dtype) @ R[i].T + t[i][None])[:, 2]
-                      for i, lab in enumerate(labels)])
-    znear = torch.floor(zall.min() / 100) * 100
+    lights = light_location([meshes[int(lab)][0] for lab in labels], R, t, light)
     for i, lab in enumerate(labels):
         verts, faces, colors = meshes[int(lab)]
         dt = verts.dtype
         Ri, ti, Ki = R[i].to(dt), t[i].to(dt), K[i].to(dt)
         ndc = project_ndc(verts, Ri, ti, Ki, S)
         p2f, zbuf, bary = rasterize(ndc, faces, S)
-        zero = torch.zeros((), dtype=dt)
-        if seps:
-            light_loc = Ri @ torch.stack([zero, zero, torch.clamp(ndc[:, 2].min() - 400, min=0)])
-        elif deflt:
-            light_loc = torch.tensor([0.0, 1.0, 0.0], dtype=dt)  # PointLights default location
-        else:
-            light_loc = Ri @ torch.stack([zero, zero, (znear / 4).to(dt)])
+        light_loc = lights[i].to(dt)
         cols = dict(ambient=0.5, diffuse=0.3, specular=0.2) if deflt else \
             dict(ambient=0.8, diffuse=0.5, specular=1.0)
         cam_center = -Ri.T @ ti

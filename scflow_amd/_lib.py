@@ -137,7 +137,7 @@ class RenderArgs(ctypes.Structure):
         ("shininess", c_float),
         ("background", c_vp),
         ("images", c_vp), ("zbuf", c_vp), ("pix_to_face", c_vp), ("bary", c_vp),
-        ("workspace", c_vp), ("workspace_bytes", c_ll),
+        ("workspace", c_vp), ("workspace_bytes", c_ll), ("light_out", c_vp),
     ]
 
 

@@ -190,6 +190,30 @@ __device__ __forceinline__ void normalize3(float* v, float eps = 1e-6f) {
   v[2] /= n;
 }
 
+// light location (object frame) of image n, Renderer.forward :209-230
+__device__ __forceinline__ void light_of(const scflow_render_args& a, int n,
+                                         const unsigned* __restrict__ zmin_bits, int n_img,
+                                         float (&L)[3]) {
+  if (a.light_mode == SCFLOW_LIGHT_FIXED) {
+    L[0] = a.light_location[0];
+    L[1] = a.light_location[1];
+    L[2] = a.light_location[2];
+    return;
+  }
+  float lz;
+  if (a.light_mode == SCFLOW_LIGHT_PER_IMAGE) {
+    lz = fmaxf(__uint_as_float(zmin_bits[n]) - 400.f, 0.f);
+  } else {  // SCFLOW_LIGHT_BATCH_ZNEAR: znear = (min over the batch // 100)·100, light at znear/4
+    float zn = __uint_as_float(zmin_bits[0]);
+    for (int k = 1; k < n_img; ++k) zn = fminf(zn, __uint_as_float(zmin_bits[k]));
+    lz = floorf(zn / 100.f) * 100.f / 4.f;
+  }
+  const float* R = a.R + 9 * n;
+  L[0] = R[2] * lz;
+  L[1] = R[5] * lz;
+  L[2] = R[8] * lz;
+}
+
 __global__ void render_shade_kernel(scflow_render_args a, const float* __restrict__ vproj,
                                     const unsigned long long* __restrict__ zf,
                                     const unsigned* __restrict__ zmin_bits, int n_img) {
@@ -201,6 +225,11 @@ __global__ void render_shade_kernel(scflow_render_args a, const float* __restric
   const int r = rc / S, c = rc % S;
   const unsigned long long key = zf[pix];
   float* img = a.images ? a.images + pix * 4 : nullptr;
+  if (a.light_out && rc == 0) {  // the image's light location, once per image
+    float L[3];
+    light_of(a, n, zmin_bits, n_img, L);
+    for (int k = 0; k < 3; ++k) a.light_out[3 * n + k] = L[k];
+  }
   if (key == ~0ull) {
     if (a.zbuf) a.zbuf[pix] = -1.f;
     if (a.pix_to_face) a.pix_to_face[pix] = -1;
@@ -234,24 +263,8 @@ __global__ void render_shade_kernel(scflow_render_args a, const float* __restric
   }
   const float* R = a.R + 9 * n;
   const float* t = a.t + 3 * n;
-  // light location (object frame), Renderer.forward :209-230
-  float lz = 0.f;
   float L[3];
-  if (a.light_mode == SCFLOW_LIGHT_FIXED) {
-    L[0] = a.light_location[0];
-    L[1] = a.light_location[1];
-    L[2] = a.light_location[2];
-  } else {
-    if (a.light_mode == SCFLOW_LIGHT_PER_IMAGE) lz = fmaxf(__uint_as_float(zmin_bits[n]) - 400.f, 0.f);
-    else {  // SCFLOW_LIGHT_BATCH_ZNEAR: znear = (min over the batch // 100)·100, light at znear/4
-      float zn = __uint_as_float(zmin_bits[0]);
-      for (int k = 1; k < n_img; ++k) zn = fminf(zn, __uint_as_float(zmin_bits[k]));
-      lz = floorf(zn / 100.f) * 100.f / 4.f;
-    }
-    L[0] = R[2] * lz;
-    L[1] = R[5] * lz;
-    L[2] = R[8] * lz;
-  }
+  light_of(a, n, zmin_bits, n_img, L);
   // camera centre −Rᵀt
   const float C[3] = {-(R[0] * t[0] + R[3] * t[1] + R[6] * t[2]), -(R[1] * t[0] + R[4] * t[1] + R[7] * t[2]),
                       -(R[2] * t[0] + R[5] * t[1] + R[8] * t[2])};

@@ -206,6 +206,42 @@ def verts_normals(verts: Tensor, faces: Tensor) -> Tensor:
     return torch.nn.functional.normalize(n, eps=1e-6, dim=1)
 
 
+# ----------------------------------------------------------------------------------- cameras
+class PerspectiveCameraParams(NamedTuple):
+    """The keyword arguments the reference hands pytorch3d's ``PerspectiveCameras``."""
+    R: Tensor                # [N, 3, 3] (row-vector convention: X_view = X_world·R + T)
+    T: Tensor                # [N, 3]
+    focal_length: Tensor     # [N, 2] NDC units
+    principal_point: Tensor  # [N, 2] NDC units
+    image_size: Tensor       # [N, 2] (H, W)
+
+
+def cameras_from_opencv_projection(R: Tensor, tvec: Tensor, camera_matrix: Tensor,
+                                   image_size: Tensor) -> PerspectiveCameraParams:
+    """rendering.py:17-60: OpenCV (R, t, K) → pytorch3d's NDC camera — transposed R with its
+    first two columns negated, t with x, y negated, focal / principal point scaled by
+    (min(H, W) − 1)/2 around the image centre.  scflow_render projects with (R, t, K) directly;
+    both conventions put a vertex at the same NDC point (tests/test_render_wiring.py)."""
+    focal = torch.stack([camera_matrix[:, 0, 0], camera_matrix[:, 1, 1]], dim=-1)
+    pp = camera_matrix[:, :2, 2]
+    wh = image_size.to(R).flip(dims=(1,))
+    scale = ((wh.min(dim=1, keepdim=True)[0] - 1) / 2.0).expand(-1, 2)
+    c0 = (wh - 1) / 2.0
+    Rp = R.clone().permute(0, 2, 1)
+    Tp = tvec.clone()
+    Rp[:, :, :2] = Rp[:, :, :2] * -1
+    Tp[:, :2] = Tp[:, :2] * -1
+    return PerspectiveCameraParams(Rp, Tp, focal / scale, -(pp - c0) / scale, image_size)
+
+
+def depth_range(rotations: Tensor, translations: Tensor, verts: Sequence[Tensor]) -> Tuple[Tensor, Tensor]:
+    """(znear, zfar) of Renderer.forward (:193-199): the batch's vertex view depths, rounded down
+    / up to 100 mm — as device tensors (the reference calls .item(); no host sync here)."""
+    z = torch.cat([(R[2:3] @ v.T.to(R) + t[2]).reshape(-1)
+                   for R, t, v in zip(rotations, translations, verts)])
+    return torch.floor(z.min() / 100) * 100, (torch.floor(z.max() / 100) + 1) * 100
+
+
 # ----------------------------------------------------------------------------------- renderer
 class Renderer(nn.Module):
     """models/utils/rendering.py:77-248 on the HIP rasteriser."""
@@ -320,6 +356,7 @@ class Renderer(nn.Module):
         zbuf = torch.empty(n, S, S, 1, device=dev)
         p2f = torch.empty(n, S, S, 1, device=dev, dtype=torch.int32)
         bary = torch.empty(n, S, S, 1, 3, device=dev)
+        light = torch.empty(n, 3, device=dev)
         a = _lib.RenderArgs()
         a.verts, a.normals, a.colors, a.faces = (verts.data_ptr(), normals.data_ptr(), colors.data_ptr(),
                                                  faces.data_ptr())
@@ -334,11 +371,14 @@ class Renderer(nn.Module):
         a.images = 0 if images is None else images.data_ptr()
         a.zbuf, a.pix_to_face, a.bary = zbuf.data_ptr(), p2f.data_ptr(), bary.data_ptr()
         a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+        a.light_out = light.data_ptr()
         import ctypes
         check(lib.scflow_render(ctypes.byref(a), torch.cuda.current_stream(dev).cuda_stream),
               "scflow_render")
         frags = Fragments(pix_to_face=p2f.long(), zbuf=zbuf, bary_coords=bary, dists=None)
-        out = {"fragments": frags}
+        # extension: the light location each image was shaded with (the reference builds it into
+        # its PointLights, :209-230)
+        out = {"fragments": frags, "light_location": light}
         if images is not None:
             out["images"] = images
         return out

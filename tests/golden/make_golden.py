@@ -580,8 +580,131 @@ def gen_metric(out, seed=11):
         out["in_scene_gt_48"] = np.array(f.read())
 
 
+# ------------------------------------------------------------------ §8(f)-3: renderer wiring
+RENDER_CASES = ((True, True), (True, False), (False, True), (False, False))  # (default, seperate)
+
+
+def load_rendering(mesh_verts):
+    """The reference's ``models/utils/rendering.py`` with RECORDING stand-ins for pytorch3d (absent):
+    ``PerspectiveCameras`` / ``PointLights`` / ``RasterizationSettings`` / ``BlendParams`` keep their
+    keyword arguments, ``MeshRendererWithFragments`` records the keywords of each call (znear,
+    zfar, cameras, lights) and returns placeholders, ``join_meshes_as_batch`` / the PLY reader
+    serve the synthetic vertices of the class named by the file (``obj_XXXXXX.ply``).
+    ``cameras_from_opencv_projection`` and ``Renderer.__init__`` / ``to`` / ``forward`` run as the
+    reference wrote them; nothing is rasterised (the rasteriser stays parity-unpinned)."""
+    rec = {"calls": []}
+
+    class _Kw:
+        def __init__(self, *args, **kw):
+            self.args, self.kw = args, kw
+
+    class _Cameras(_Kw):
+        pass
+
+    class _Lights(_Kw):
+        pass
+
+    class _MeshRendererWithFragments(_Kw):
+        def __call__(self, meshes, **kw):
+            rec["calls"].append(kw)
+            return None, None
+
+    class _Mesh:
+        def __init__(self, verts):
+            self.verts = verts
+
+        def to(self, device):
+            return _Mesh(self.verts.to(device))
+
+    class _PlyFormat:
+        def read(self, path, include_textures=True, device="cpu", path_manager=None):
+            c = int(os.path.basename(path).split(".")[0].split("_")[-1]) - 1
+            return _Mesh(torch.as_tensor(mesh_verts[c], dtype=torch.float32))
+
+    class _Batch:
+        def __init__(self, meshes):
+            self.meshes = meshes
+
+        def verts_list(self):
+            return [m.verts for m in self.meshes]
+
+    names = ("PointLights", "PerspectiveCameras", "BlendParams", "MeshRasterizer",
+             "RasterizationSettings", "HardPhongShader", "SoftPhongShader", "HardGouraudShader",
+             "SoftGouraudShader", "SoftSilhouetteShader", "HardFlatShader")
+    p3r = {n: type(n, (_Kw,), {}) for n in names}
+    p3r["PerspectiveCameras"], p3r["PointLights"] = _Cameras, _Lights
+    _stub("iopath")
+    _stub("iopath.common")
+    _stub("iopath.common.file_io", PathManager=lambda: None)
+    _stub("pytorch3d")
+    _stub("pytorch3d.structures", join_meshes_as_batch=lambda ms, include_textures=True: _Batch(ms))
+    _stub("pytorch3d.renderer", **p3r)
+    _stub("pytorch3d.renderer.mesh")
+    _stub("pytorch3d.renderer.mesh.renderer", MeshRendererWithFragments=_MeshRendererWithFragments)
+    _stub("pytorch3d.io")
+    _stub("pytorch3d.io.ply_io", MeshPlyFormat=_PlyFormat)
+    _stub("pytorch3d.io.obj_io", MeshObjFormat=_PlyFormat)
+    _stub("torchvision")
+    _stub("torchvision.utils", save_image=None)
+    return _load("models.utils.rendering", "models/utils/rendering.py"), rec
+
+
+def render_case_inputs(B=4, S=256, seed=31):
+    """Poses / intrinsics / labels of the renderer-wiring fixture (synthetic.make_scene, with one
+    pose pushed close so that max(z_min − 400, 0) clamps to 0 for it)."""
+    sc = synthetic.make_scene(B, S, seed=seed)
+    sc["ref_translation"][1, 2] = 380.0
+    return sc
+
+
+def gen_render(out, B=4, S=256):
+    """§8(f)-3 fixture: the reference's ``Renderer.forward`` (rendering.py:185-248) for the four
+    (default_lights, seperate_lights) settings — the PerspectiveCameras it builds through
+    ``cameras_from_opencv_projection`` (:17-60: R, T, focal_length, principal_point, image_size),
+    the znear / zfar it rounds to 100 mm (:193-199) and passes to the renderer call, and the
+    PointLights keywords (location :210-229, colours)."""
+    import tempfile
+    verts = [synthetic.ellipsoid_mesh(np.array(synthetic.ELLIPSOID_AXES) * d, 12, 24)[0]
+             for d in synthetic.YCBV_DIAMETERS]
+    mod, rec = load_rendering(verts)
+    sc = render_case_inputs(B, S)
+    mesh_dir = tempfile.mkdtemp(prefix="scflow_meshes_")
+    for c in range(len(verts)):
+        open(os.path.join(mesh_dir, f"obj_{c + 1:06d}.ply"), "w").close()
+    R, t, K = (torch.from_numpy(sc[k]) for k in ("ref_rotation", "ref_translation", "internel_k"))
+    labels = torch.from_numpy(sc["labels"])
+    out["in_R"], out["in_t"], out["in_K"], out["in_labels"] = sc["ref_rotation"], \
+        sc["ref_translation"], sc["internel_k"], sc["labels"]
+    out["in_S"] = np.array(S)
+    for deflt, seps in RENDER_CASES:
+        tag = f"d{int(deflt)}s{int(seps)}"
+        rend = mod.Renderer(mesh_dir, (S, S), shader_type="Phong", soft_blending=False,
+                            render_mask=False, default_lights=deflt, seperate_lights=seps)
+        rend.to("cpu")
+        rec["calls"].clear()
+        rend(R, t, K, labels)
+        (call,) = rec["calls"]
+        cam, lights = call["cameras"], call["lights"]
+        for k in ("R", "T", "focal_length", "principal_point", "image_size"):
+            out[f"{tag}_cam_{k}"] = cam.kw[k].detach().numpy()
+        out[f"{tag}_znear_zfar"] = np.array([call["znear"], call["zfar"]])
+        loc = lights.kw.get("location")
+        out[f"{tag}_light_location"] = np.zeros((0, 3), np.float32) if loc is None else \
+            loc.detach().numpy()
+        for k in ("ambient_color", "diffuse_color", "specular_color"):
+            v = lights.kw.get(k)
+            out[f"{tag}_light_{k}"] = np.zeros(0, np.float32) if v is None else np.array(v, np.float32)
+    out["mesh_verts_sum"] = np.array([float(np.asarray(v, np.float64).sum()) for v in verts])
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    if len(sys.argv) > 1 and sys.argv[1] == "render":  # only the renderer-wiring fixture
+        rw = {}
+        gen_render(rw)
+        np.savez_compressed(os.path.join(HERE, "golden_render_wiring.npz"), **rw)
+        print({k: getattr(v, "shape", None) for k, v in rw.items()})
+        return
     ref = load_reference()
     if len(sys.argv) > 1 and sys.argv[1] == "ops":  # only golden_ops.npz
         ops = {}

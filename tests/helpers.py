@@ -9,7 +9,8 @@ from scflow_amd import synthetic
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 _FILES = {"ops": "golden_ops.npz", "e2e": "golden_e2e_b2_s256_it4.npz",
-          "enc": "golden_enc_b1_s128.npz", "refine": "golden_refine_b2_s256_it4.npz"}
+          "enc": "golden_enc_b1_s128.npz", "refine": "golden_refine_b2_s256_it4.npz",
+          "render_wiring": "golden_render_wiring.npz"}
 
 
 @lru_cache(maxsize=None)

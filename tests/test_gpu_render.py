@@ -128,3 +128,27 @@ def test_refiner_render_and_refine_cycles():
     torch.cuda.synchronize()
     assert torch.isfinite(R2).all() and torch.isfinite(t2).all()
     assert not torch.equal(R2, R1)
+
+
+@pytest.mark.parametrize("deflt,seps", [(True, True), (True, False), (False, True), (False, False)])
+def test_kernel_light_location_matches_reference_fixture(deflt, seps):
+    """The light each image is shaded with (scflow_render's light_out) against the PointLights
+    location the reference's own Renderer.forward builds (golden_render_wiring.npz, rendering.py:
+    209-230; tests/test_render_wiring.py pins the rest of the wiring on the CPU)."""
+    from scflow_amd import synthetic
+    from scflow_amd.renderer import Renderer
+    from tests.helpers import golden
+    gd = golden("render_wiring")
+    labels = gd["in_labels"]
+    meshes = {int(l): synthetic.ellipsoid_mesh(np.array(synthetic.ELLIPSOID_AXES) *
+                                               synthetic.YCBV_DIAMETERS[int(l)], 12, 24)
+              for l in set(labels.tolist())}
+    S = int(gd["in_S"])
+    r = Renderer(image_size=(S, S), soft_blending=False, render_mask=False, seperate_lights=seps,
+                 default_lights=deflt, meshes=meshes).to("cuda")
+    out = r(*(torch.from_numpy(gd[k]).cuda() for k in ("in_R", "in_t", "in_K", "in_labels")))
+    got = out["light_location"].cpu().numpy()
+    rec = gd[f"d{int(deflt)}s{int(seps)}_light_location"]
+    if rec.size == 0:  # PointLights() default location (pytorch3d's (0, 1, 0))
+        rec = np.tile([0.0, 1.0, 0.0], (len(labels), 1))
+    np.testing.assert_allclose(got, rec, rtol=1e-5, atol=1e-3)

@@ -11,6 +11,8 @@ host starvation.  host_ms ≥ gpu_pure_ms means the step is host-bound.
     python tools/train_timing.py [--steps 12] [--warmup 3] [--graph]
 """
 import argparse
+import collections
+import gc
 import json
 import os
 import statistics
@@ -34,6 +36,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--graph", action="store_true")
     ap.add_argument("--sleep-ms", type=float, default=120.0)
+    ap.add_argument("--freeze", action="store_true", help="gc.collect() + gc.freeze() after warm-up")
     a = ap.parse_args()
     import bench
     from scflow_amd import synthetic
@@ -47,6 +50,17 @@ def main():
     for _ in range(a.warmup):
         step(batch)
     torch.cuda.synchronize()
+    if a.freeze:
+        gc.collect()
+        gc.freeze()
+    gc_log = []
+
+    def on_gc(phase, info):
+        if phase == "start":
+            gc_log.append([info["generation"], time.perf_counter(), None])
+        elif gc_log and gc_log[-1][2] is None:
+            gc_log[-1][2] = time.perf_counter()
+    gc.callbacks.append(on_gc)
 
     # pass 1: pipelined, per-step host return time and device time
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -82,7 +96,11 @@ def main():
     out = {"steps": a.steps, "graph": a.graph, "wall_ms_per_step": round(wall, 3),
            "host_ms": _stats(host), "gpu_ms": _stats(gpu), "host_ms_gpu_held": _stats(host_free),
            "gpu_pure_ms": _stats(pure), "sleep_ms": a.sleep_ms,
-           "per_step_host": [round(x, 2) for x in host], "per_step_gpu": [round(x, 2) for x in gpu]}
+           "per_step_host": [round(x, 2) for x in host], "per_step_gpu": [round(x, 2) for x in gpu],
+           "gc_freeze": a.freeze, "gc_collections": collections.Counter(g for g, _, _ in gc_log),
+           "gc_ms_by_generation": {g: round(sum(1e3 * (e - s) for gg, s, e in gc_log if gg == g and e), 2)
+                                   for g in (0, 1, 2)},
+           "gc_max_ms": round(max((1e3 * (e - s) for _, s, e in gc_log if e), default=0.0), 2)}
     print(json.dumps(out), flush=True)
 
 
