@@ -98,6 +98,18 @@ int scflow_corr_pyramid_tiled(const float* f1, const float* f2, float* pyr, int 
 int scflow_corr_lookup_tiled(const float* pyr, const float* flow, int flow_layout, float* out,
                              int out_layout, int out_stride, int n, int h, int w, int num_levels,
                              int radius, int align_corners, void* stream);
+/* a2 + a3's corr_net.0 fused (inference): out[m][·] = act(W·lookup(pyr, flow)[m] + bias), the
+ * lookup of scflow_corr_lookup_tiled (TILED pyramid, num_levels 4, radius 4, h and w multiples of
+ * 32) and the 1×1 conv of SCFLOW_CONV_1X1W (weight packed by scflow_conv_pack_weights with bk =
+ * SCFLOW_CONV_1X1W, c0 = 324, c1 = 0; cout ≤ 256) in one launch: the correlation features stay
+ * in LDS (replaces CorrLookup.forward, corr_lookup.py:102-136, followed by MotionEncoder's first
+ * corr_net layer, raft_decoder.py:75-85,152-166).  flow: [n·h·w][2] (NHWC); out: [n·h·w] rows of
+ * out_stride floats.  Bit-identical to the two launches it replaces. */
+int scflow_corr_lookup_conv1x1(const float* pyr, const float* flow, const float* weight,
+                               const float* bias, float* out, int out_stride, int n, int h, int w,
+                               int num_levels, int radius, int cout, int act, int align_corners,
+                               void* stream);
+long long scflow_corr_lookup_conv1x1_lds_bytes(void);
 /* Profiling only: later LDS-kernel lookups (scflow_corr_lookup*) write 6 u64 real-time-clock
  * stamps per workgroup of 16 query pixels to `stamps` (phase boundaries; NULL turns it off). */
 int scflow_debug_lookup_stamps(void* stamps);
@@ -142,19 +154,25 @@ typedef struct scflow_conv_args {
  * arithmetic, 2.25× / 2.5× fewer matrix multiplies than the direct conv; the weights must be
  * packed with the same bk. */
 #define SCFLOW_CONV_WINO 2
+/* scflow_conv_args.bk = SCFLOW_CONV_1X1W selects the wide 1×1 kernel (corr_net.0's 324 → 256):
+ * stride 1, no padding, one source (c1 = 0) with c0 a multiple of 4 and 8·⌈c0/8⌉ one of the
+ * instantiated depths (128, 256, 328), cout ≤ 256, SCFLOW_EPI_PLAIN (bias, bias map, activation);
+ * 64 pixels × every output channel per workgroup, the pixels' whole input rows in LDS. */
+#define SCFLOW_CONV_1X1W 3
 
 /* Number of floats of the packed weight buffer for bk 8 and 16 (the same for both); w_oihw is
  * nn.Conv2d's [cout][c0+c1][kh][kw]. */
 long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, int kw, int stride, int w);
-/* The same for any packing format bk (0, 8, 16 or SCFLOW_CONV_WINO). */
+/* The same for any packing format bk (0, 8, 16, SCFLOW_CONV_WINO or SCFLOW_CONV_1X1W). */
 long long scflow_conv_packed_size_bk(int cout, int c0, int c1, int kh, int kw, int stride, int w,
                                      int bk);
-/* bk: packing format (0 → 16, 8, or SCFLOW_CONV_WINO); pass the same value in
+/* bk: packing format (0 → 16, 8, SCFLOW_CONV_WINO or SCFLOW_CONV_1X1W); pass the same value in
  * scflow_conv_args.bk. */
 int scflow_conv_pack_weights(const float* w_oihw, float* packed, int cout, int c0, int c1, int kh,
                              int kw, int stride, int w, int bk, void* stream);
 /* Preferred packing format for this launch shape (batch, sizes, channels, kernel): Winograd
- * (SCFLOW_CONV_WINO) for the 3×3 stride-1 convs it covers, else the direct conv's K-stage depth,
+ * (SCFLOW_CONV_WINO) for the 3×3 stride-1 convs it covers, the wide 1×1 kernel
+ * (SCFLOW_CONV_1X1W) for the 1×1 convs it covers, else the direct conv's K-stage depth,
  * 8 when the grid needs more resident workgroups than 16-deep stages' LDS allows, else 16. */
 int scflow_conv_pick_bk(const scflow_conv_args* args);
 int scflow_conv2d(const scflow_conv_args* args, void* stream);

@@ -20,6 +20,7 @@ c_int, c_float, c_ll, c_vp = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ct
 SCFLOW_ACT = {None: 0, "ReLU": 1, "Sigmoid": 2, "Tanh": 3}
 EPI_PLAIN, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2
 CONV_WINO = 2  # scflow_conv_args.bk: Winograd F(2x2,3x3) packing/kernel (SCFLOW_CONV_WINO)
+CONV_1X1W = 3  # scflow_conv_args.bk: wide 1x1 packing/kernel (SCFLOW_CONV_1X1W)
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 
 
@@ -154,6 +155,9 @@ SIGNATURES = {
     "scflow_corr_lookup_ex": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                       c_int, c_int, c_vp]),
     "scflow_corr_pyramid_tiled": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_corr_lookup_conv1x1": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                           c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "scflow_corr_lookup_conv1x1_lds_bytes": (c_ll, []),
     "scflow_corr_lookup_tiled": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_vp]),
     "scflow_in_apply": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp]),

@@ -830,6 +830,7 @@ __global__ void pack_kernel(const float* __restrict__ w, float* __restrict__ out
 
 #include "conv_wino.h"
 #include "conv_wino5.h"
+#include "conv1x1w.h"
 
 // Winograd eligibility: F(2×2,3×3) (conv_wino.h) for 3×3, F(4,5) (conv_wino5.h) for 1×5 / 5×1;
 // stride 1, "same" padding, whole-row tiles of 32 tiles
@@ -1110,6 +1111,53 @@ int dispatch_mfma(const MfmaParams& p, const Geometry& g, hipStream_t st) {
 
 }  // namespace
 
+// ---- wide 1×1 (conv1x1w.h): which shapes, how packed, how launched
+// SCFLOW_CONV1X1W=0 keeps the 1×1 convs on conv1x1_kernel (A/B)
+bool conv1x1w_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SCFLOW_CONV1X1W");
+    on = !(e && e[0] == '0');
+  }
+  return on != 0;
+}
+int conv1x1w_kb(int c0) { return (c0 + 7) / 8; }
+bool conv1x1w_kb_ok(int kb) { return kb == 41 || kb == 32 || kb == 16; }
+bool conv1x1w_shape(int cout, int c0, int c1, int kh, int kw, int stride) {
+  return kh == 1 && kw == 1 && stride == 1 && c1 == 0 && c0 % 4 == 0 && cout > 4 && cout <= 256 &&
+         conv1x1w_kb_ok(conv1x1w_kb(c0));
+}
+bool conv1x1w_launchable(const scflow_conv_args& a) {
+  return conv1x1w_shape(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride) && a.ph == 0 && a.pw == 0 &&
+         a.epilogue == SCFLOW_EPI_PLAIN && !has_fused_norm(a);
+}
+long long conv1x1w_packed_size(int cout, int c0) {
+  return (long long)(round_up(cout, 64) / 32) * conv1x1w_kb(c0) * 256;
+}
+template <int KB>
+int launch_conv1x1w_kb(const scflow_conv_args& a, hipStream_t st) {
+  const size_t lds = conv1x1w_lds_bytes<KB>();
+  static bool attr = false;
+  if (lds > 64 * 1024 && !attr) {
+    (void)hipFuncSetAttribute((const void*)conv1x1w_kernel<KB>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const long long M = (long long)a.n * a.h * a.w;
+  conv1x1w_kernel<KB><<<(unsigned)((M + W1_PX - 1) / W1_PX), 256, lds, st>>>(a);
+  return scflow_launch_status();
+}
+int launch_conv1x1w(const scflow_conv_args& a, hipStream_t st) {
+  if (!conv1x1w_launchable(a)) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(a.src0) || (a.s0 & 3) || !aligned16(a.weight)) return SCFLOW_EALIGN;
+  switch (conv1x1w_kb(a.c0)) {
+    case 41: return launch_conv1x1w_kb<41>(a, st);
+    case 32: return launch_conv1x1w_kb<32>(a, st);
+    case 16: return launch_conv1x1w_kb<16>(a, st);
+    default: return SCFLOW_EUNSUPPORTED;
+  }
+}
+
 SCFLOW_API long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, int kw, int stride,
                                              int w) {
   // packing depends on the width (tile = whole rows) but not on the height or padding
@@ -1121,6 +1169,10 @@ SCFLOW_API long long scflow_conv_packed_size(int cout, int c0, int c1, int kh, i
 
 SCFLOW_API long long scflow_conv_packed_size_bk(int cout, int c0, int c1, int kh, int kw,
                                                 int stride, int w, int bk) {
+  if (bk == SCFLOW_CONV_1X1W) {
+    if (!conv1x1w_shape(cout, c0, c1, kh, kw, stride)) return SCFLOW_EUNSUPPORTED;
+    return conv1x1w_packed_size(cout, c0);
+  }
   if (bk == SCFLOW_CONV_WINO) {
     if (cout <= 4 || c0 <= 0 || c1 < 0 || c0 % 4 || c1 % 4 || !wino_shape(kh, kw, stride, w))
       return SCFLOW_EUNSUPPORTED;
@@ -1134,6 +1186,14 @@ SCFLOW_API int scflow_conv_pack_weights(const float* w_oihw, float* packed, int 
                                         int c1, int kh, int kw, int stride, int w, int bk,
                                         void* stream) {
   if (!w_oihw || !packed || cout <= 0 || c0 <= 0 || c1 < 0 || kh <= 0 || kw <= 0) return SCFLOW_EINVAL;
+  if (bk == SCFLOW_CONV_1X1W) {
+    const long long total = scflow_conv_packed_size_bk(cout, c0, c1, kh, kw, stride, w, bk);
+    if (total < 0) return (int)total;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    conv1x1w_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0,
+                                                                   conv1x1w_kb(c0), total);
+    return scflow_launch_status();
+  }
   if (bk == SCFLOW_CONV_WINO) {
     const long long total = scflow_conv_packed_size_bk(cout, c0, c1, kh, kw, stride, w, bk);
     if (total < 0) return (int)total;
@@ -1168,6 +1228,7 @@ SCFLOW_API int scflow_conv_pick_bk(const scflow_conv_args* args) {
   const scflow_conv_args& a = *args;
   if (a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 || a.c1 < 0) return SCFLOW_EINVAL;
   if (wino_enabled(a.kh) && wino_launchable(a)) return SCFLOW_CONV_WINO;
+  if (conv1x1w_enabled() && conv1x1w_launchable(a)) return SCFLOW_CONV_1X1W;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
   if (g.variant != V_MFMA) return BK;  // other variants ignore the stage depth
   int tr, hr;
@@ -1193,6 +1254,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     return SCFLOW_EINVAL;
   }
   if (a.bk == SCFLOW_CONV_WINO) return launch_wino(a, (hipStream_t)stream);
+  if (a.bk == SCFLOW_CONV_1X1W) return launch_conv1x1w(a, (hipStream_t)stream);
   if (has_fused_norm(a)) return SCFLOW_EUNSUPPORTED;  // Winograd 3×3 only
   if (a.bk != 0 && a.bk != 8 && a.bk != 16) return SCFLOW_EINVAL;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);

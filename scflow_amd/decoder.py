@@ -28,7 +28,7 @@ from typing import Dict, Optional, Sequence, Tuple, Union
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 from ._lib import ScflowError
 from .modules import (ConvGRU, ConvModule, ConvRunner, CorrelationPyramid, CorrLookup,
                       MotionEncoder, XHead, run_chain)
@@ -98,6 +98,9 @@ class SCFlowDecoder(nn.Module):
         # the iteration's tail (pose update, pose flow, ×8 prediction, next ↓8 flow) as one
         # launch (scflow_pose_step); only without flow/correlation masking
         self.fuse_tail = True
+        # the lookup and corr_net.0 (1×1 324→256) as ONE launch (scflow_corr_lookup_conv1x1: the
+        # correlation features stay in LDS) when the geometry allows (tiled pyramid, L = 4, r = 4)
+        self.fuse_lookup_conv = True
         # a batch of ≥ 2·pingpong_min pairs runs as two interleaved halves (_forward_pingpong).
         # Off: measured slower at B=16 (5.76 vs 5.33 ms/step) — a half's tail kernels do not get
         # CUs while the other half's convolutions hold every CU's LDS, so they serialise anyway
@@ -465,6 +468,19 @@ class SCFlowDecoder(nn.Module):
                             tiled=tiled)
 
         corr_net = self.encoder.corr_net
+        c0m = corr_net[0].conv
+        fuse_lc = (self.fuse_lookup_conv and tiled and not self.mask_corr and len(corr_net) == 2 and
+                   tuple(c0m.kernel_size) == (1, 1) and tuple(c0m.stride) == (1, 1) and
+                   tuple(c0m.padding) == (0, 0) and
+                   ops.lookup_conv1x1_ok(h, w, self.num_levels, self.radius, c0m.in_channels,
+                                         c0m.out_channels))
+
+        def seg_lookup_conv():  # a2 + corr_net.0 in one launch
+            r0 = ConvRunner.of(c0m, corr_net[0].act_type)
+            packed, bias = r0.packed(c0m.in_channels, 0, w, _lib.CONV_1X1W)
+            ops.corr_lookup_conv1x1(pyr, F2, packed, bias, Chan.whole(s_corr[-1]), N, h, w,
+                                    self.num_levels, self.radius, c0m.out_channels,
+                                    corr_net[0].act_type, self.corr_lookup.align_corners)
 
         def seg_corr_hidden():  # corr_net.0 (1×1 324→256)
             if len(corr_net) > 1:
@@ -540,12 +556,17 @@ class SCFlowDecoder(nn.Module):
             with torch.cuda.stream(side):
                 segment("flow_branch" + par, seg_flow_branch)
             # a2 + a3 (correlation branch)
-            self._hook("corr_lookup", True)
-            segment("lookup" + par, seg_lookup)
-            self._hook("corr_lookup", False)
-            if self.mask_corr:
-                CORR.mul_(mask_lr)
-            segment("corr_hidden", seg_corr_hidden)
+            if fuse_lc:
+                self._hook("corr_lookup_conv", True)
+                segment("lookup_conv" + par, seg_lookup_conv)
+                self._hook("corr_lookup_conv", False)
+            else:
+                self._hook("corr_lookup", True)
+                segment("lookup" + par, seg_lookup)
+                self._hook("corr_lookup", False)
+                if self.mask_corr:
+                    CORR.mul_(mask_lr)
+                segment("corr_hidden", seg_corr_hidden)
             self._hook("corr_net1", True)
             segment("corr_last", seg_corr_last)
             self._hook("corr_net1", False)

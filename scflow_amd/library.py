@@ -15,6 +15,9 @@ op                             reference                                        
                                                                                       detaches)
 =============================  =====================================================  =========
 
+The two backward formulas are ops of their own (``scflow::corr_pyramid_backward``,
+``scflow::corr_lookup_backward``), so AOT autograd traces the backward graph as well.
+
 The pyramid travels as ONE flat fp32 buffer (levels back to back, each ``[N·H·W, 1, H_l, W_l]``
 row-major — ``ops.pyramid_views`` turns it into the reference's list); the modules
 ``CorrelationPyramid`` / ``CorrLookup`` (modules.py) call these ops.  Every op runs the HIP
@@ -58,13 +61,14 @@ def _corr_pyramid_setup(ctx, inputs, output):
     ctx.num_levels = num_levels
 
 
-def _corr_pyramid_backward(ctx, dbuf):
+@torch.library.custom_op("scflow::corr_pyramid_backward", mutates_args=(), device_types="cuda")
+def corr_pyramid_backward(dbuf: Tensor, feat1: Tensor, feat2: Tensor, num_levels: int
+                          ) -> Tuple[Tensor, Tensor]:
     """AvgPool adjoint down the levels, then dF1 = F2·dCᵀ, dF2 = F1·dC on the HIP GEMM (the
     training step's adjoint, train/functions.py _CorrPyramid)."""
-    feat1, feat2 = ctx.saved_tensors
     n, c, h, w = feat1.shape
     P = h * w
-    levels = ops.pyramid_views(dbuf.contiguous(), n, h, w, ctx.num_levels)
+    levels = ops.pyramid_views(dbuf.contiguous(), n, h, w, num_levels)
     g = levels[-1]
     for lv in reversed(levels[:-1]):
         hl, wl = lv.shape[-2:]
@@ -77,6 +81,18 @@ def _corr_pyramid_backward(ctx, dbuf):
     f2 = feat2.contiguous().view(n, c, P)
     df1 = ops.gemm(f2, dC.transpose(1, 2)).view_as(feat1)
     df2 = ops.gemm(f1, dC).view_as(feat2)
+    return df1, df2
+
+
+@corr_pyramid_backward.register_fake
+def _(dbuf, feat1, feat2, num_levels):
+    return torch.empty_like(feat1, memory_format=torch.contiguous_format), \
+        torch.empty_like(feat2, memory_format=torch.contiguous_format)
+
+
+def _corr_pyramid_backward(ctx, dbuf):
+    feat1, feat2 = ctx.saved_tensors
+    df1, df2 = corr_pyramid_backward(dbuf, feat1, feat2, ctx.num_levels)
     return df1, df2, None
 
 
@@ -105,19 +121,31 @@ def _corr_lookup_setup(ctx, inputs, output):
     ctx.cfg = (pyramid.numel(), num_levels, radius, align_corners)
 
 
-def _corr_lookup_backward(ctx, dout):
+@torch.library.custom_op("scflow::corr_lookup_backward", mutates_args=(), device_types="cuda")
+def corr_lookup_backward(dout: Tensor, flow: Tensor, numel: int, num_levels: int, radius: int
+                         ) -> Tensor:
     """Gradient w.r.t. the pyramid only (the decoder detaches the flow, scflow_decoder.py:193-194):
-    the adjoint scatter with grid_sample's tap weights (scflow_corr_lookup_backward)."""
+    the adjoint scatter with grid_sample's tap weights (scflow_corr_lookup_backward,
+    align_corners=True)."""
+    B, _, H, W = flow.shape
+    dpyr = torch.zeros(numel, device=dout.device, dtype=torch.float32)
+    ops.corr_lookup_backward(dout.contiguous(), flow.contiguous(), dpyr, B, H, W, num_levels, radius,
+                             out_layout="nchw", flow_layout="nchw")
+    return dpyr
+
+
+@corr_lookup_backward.register_fake
+def _(dout, flow, numel, num_levels, radius):
+    return dout.new_empty(numel)
+
+
+def _corr_lookup_backward(ctx, dout):
     (flow,) = ctx.saved_tensors
     numel, L, r, ac = ctx.cfg
     if not ac:
         raise NotImplementedError("scflow::corr_lookup backward: align_corners=True only "
                                   "(SCFlow's configuration)")
-    B, _, H, W = flow.shape
-    dpyr = torch.zeros(numel, device=dout.device, dtype=torch.float32)
-    ops.corr_lookup_backward(dout.contiguous(), flow.contiguous(), dpyr, B, H, W, L, r,
-                             out_layout="nchw", flow_layout="nchw")
-    return dpyr, None, None, None, None
+    return corr_lookup_backward(dout, flow, numel, L, r), None, None, None, None
 
 
 corr_lookup.register_autograd(_corr_lookup_backward, setup_context=_corr_lookup_setup)

@@ -215,6 +215,8 @@ class ConvRunner:
         if self.winograd:
             pts, tile = (16, 4) if self.kh * self.kw == 9 else (8, 4)
             return 2.0 * pts * (m / tile) * kpad * npad
+        if getattr(self, "_bk", None) == _lib.CONV_1X1W:  # K padded to 8, N to 64
+            return 2.0 * m * ru(self.cout, 64) * ru(c0, 8)
         return 2.0 * m * npad * self.kh * self.kw * (ru(c0, 16) + ru(c1, 16))
 
 

@@ -279,6 +279,28 @@ def corr_lookup(pyr: Tensor, flow: Tensor, n: int, h: int, w: int, num_levels: i
     return res
 
 
+def corr_lookup_conv1x1(pyr: Tensor, flow: Tensor, packed: Tensor, bias: Optional[Tensor], out: Chan,
+                        n: int, h: int, w: int, num_levels: int, radius: int, cout: int,
+                        act: Optional[str] = "ReLU", align_corners: bool = True) -> None:
+    """The tiled lookup and corr_net.0 (1×1, weights packed with ``_lib.CONV_1X1W``) in one launch
+    (scflow_corr_lookup_conv1x1): ``out`` ← act(W·lookup + bias); ``flow`` [n·h·w, 2] (NHWC)."""
+    _require(pyr, "pyramid")
+    _require(flow, "flow", contiguous=False)
+    _require(packed, "packed weight")
+    if bias is not None:
+        _require(bias, "bias")
+    if out.c != cout:
+        raise ValueError(f"out has {out.c} channels, expected {cout}")
+    _launch("scflow_corr_lookup_conv1x1", flow, _p(pyr), _p(flow), _p(packed), _p(bias), out.ptr,
+            out.stride, n, h, w, num_levels, radius, cout, _lib.SCFLOW_ACT[act], int(bool(align_corners)))
+
+
+def lookup_conv1x1_ok(h: int, w: int, num_levels: int, radius: int, cin: int, cout: int) -> bool:
+    """Whether scflow_corr_lookup_conv1x1 supports this geometry."""
+    return (num_levels == 4 and radius == 4 and h % 32 == 0 and w % 32 == 0 and cout <= 256 and
+            cin == num_levels * (2 * radius + 1) ** 2)
+
+
 # ------------------------------------------------------------------------------- convolutions
 def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1, bk: int = 16) -> Tensor:
     """Pack an nn.Conv2d weight ``[cout, c0+c1, kh, kw]`` for scflow_conv2d (packing format bk:
@@ -301,12 +323,12 @@ def pack_conv_weight(weight: Tensor, c0: int, c1: int, w: int, stride: int = 1, 
 def conv_pick_bk(n: int, h: int, w: int, c0: int, c1: int, cout: int, kh: int, kw: int, ph: int,
                  pw: int, stride: int = 1) -> int:
     """The library's preferred packing format for this launch shape (host-only query): the
-    direct conv's K-stage depth (8 or 16) or ``_lib.CONV_WINO``."""
+    direct conv's K-stage depth (8 or 16), ``_lib.CONV_WINO`` or ``_lib.CONV_1X1W``."""
     a = _lib.ConvArgs()
     a.c0, a.c1, a.n, a.h, a.w = c0, c1, n, h, w
     a.cout, a.kh, a.kw, a.ph, a.pw, a.stride = cout, kh, kw, ph, pw, stride
     bk = _lib.load().scflow_conv_pick_bk(ctypes.byref(a))
-    if bk not in (8, 16, _lib.CONV_WINO):
+    if bk not in (8, 16, _lib.CONV_WINO, _lib.CONV_1X1W):
         check(bk if bk < 0 else -2, "scflow_conv_pick_bk")
     return bk
 

@@ -210,6 +210,9 @@ def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0, bk=None):
     (2, 32, 32, 256, 0, 1, 1, 0, "Sigmoid"),       # thin 1×1 → 1
     (16, 32, 32, 324, 0, 256, 1, 0, "ReLU"),       # 1×1 kernel (128-row tiles: corr_net.0 at B=16)
     (13, 32, 32, 196, 60, 320, 1, 0, "Tanh"),      # 1×1 kernel, two sources, 5 channel blocks
+    (2, 17, 15, 324, 0, 256, 1, 0, "ReLU"),        # wide 1×1: pixels not a multiple of 64
+    (3, 32, 32, 256, 0, 192, 1, 0, None),          # wide 1×1: K 256, three channel blocks of 64
+    (2, 32, 32, 128, 0, 100, 1, 0, "Tanh"),        # wide 1×1: K 128, cout not a multiple of 32
 ])
 def test_conv2d_variants(ops, case):
     n, h, w, c0, c1, cout, k, pad, act = case
@@ -236,12 +239,14 @@ def test_conv2d_mfma_stage_depths(ops, case, bk):
 
 def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
     """Host query: 3×3 / 1×5 / 5×1 stride-1 convs take the Winograd kernels; the 1×1 corr_net.0
-    conv (512 workgroups of 128 px) 16-deep stages of the direct conv."""
+    conv the wide 1×1 kernel; a two-source 1×1 conv 16-deep stages of the direct conv."""
     from scflow_amd._lib import CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 5, 1, 2, 0) == CONV_WINO
-    assert ops.conv_pick_bk(16, 32, 32, 324, 0, 256, 1, 1, 0, 0) == 16
+    from scflow_amd._lib import CONV_1X1W
+    assert ops.conv_pick_bk(16, 32, 32, 324, 0, 256, 1, 1, 0, 0) == CONV_1X1W  # corr_net.0
+    assert ops.conv_pick_bk(16, 32, 32, 196, 60, 256, 1, 1, 0, 0) == 16  # two sources: direct
     assert ops.conv_pick_bk(2, 20, 20, 64, 0, 64, 3, 3, 1, 1) != CONV_WINO  # width not tileable
 
 
@@ -636,3 +641,44 @@ def test_corr_lookup_tiled_far_out_of_bounds(ops):
         got = ops.corr_lookup(tb, flow, n, h, w, L, 4, align_corners=ac, tiled=True)
         assert torch.equal(torch.nan_to_num(ref, nan=123.0), torch.nan_to_num(got, nan=123.0)), \
             f"ac={ac}: {(ref - got).abs().nan_to_num().max().item():.3e}"
+
+
+@pytest.mark.parametrize("n,h,w,seed,far", [(2, 32, 32, 61, False), (3, 32, 64, 62, True),
+                                            (1, 64, 64, 63, False)])
+def test_corr_lookup_conv1x1_fused_bit_identical(ops, n, h, w, seed, far):
+    """scflow_corr_lookup_conv1x1 (lookup + corr_net.0 in one launch, features in LDS) equals the
+    tiled lookup followed by the wide 1×1 conv bit for bit — random, far off-map, edge and
+    non-finite flows included — and the conv against fp64 (the lookup against the oracle is
+    pinned by the other lookup tests)."""
+    from scflow_amd import _lib
+    from scflow_amd.modules import ConvRunner
+    g = torch.Generator().manual_seed(seed)
+    f1 = torch.randn(n, 32, h, w, generator=g)
+    f2 = torch.randn(n, 32, h, w, generator=g)
+    flow = (torch.rand(n, h, w, 2, generator=g) - 0.5) * (4 * h if far else 0.6 * h)
+    flow[0, 0, 0] = torch.tensor([float("nan"), 1.0])
+    flow[0, 0, 1] = torch.tensor([float("inf"), -2.0])
+    flow[0, 1, 0] = torch.tensor([-0.5, -0.5])
+    flow[-1, -1, -1] = torch.tensor([1e9, -1e9])
+    pyr = ops.corr_pyramid_tiled(f1.cuda(), f2.cuda(), 4)
+    fl = flow.reshape(-1, 2).contiguous().cuda()
+    M = n * h * w
+    conv = torch.nn.Conv2d(324, 256, 1).cuda()
+    with torch.no_grad():
+        conv.weight.copy_((torch.randn(256, 324, 1, 1, generator=g) / 18).cuda())
+        conv.bias.copy_((torch.randn(256, generator=g) * 0.1).cuda())
+    r = ConvRunner([conv], "ReLU")
+    packed, bias = r.packed(324, 0, w, _lib.CONV_1X1W)
+    corr = torch.empty(M, 324, device="cuda")
+    ops.corr_lookup(pyr, fl, n, h, w, 4, 4, out=ops.Chan.whole(corr), flow_layout="nhwc", tiled=True)
+    sep = torch.full((M, 260), -3.0, device="cuda")
+    ops.conv2d(ops.Chan.whole(corr), packed, bias, n, h, w, 256, 1, 1, 0, 0, "ReLU",
+               out=ops.Chan(sep, 4, 256), bk=_lib.CONV_1X1W)
+    fused = torch.full((M, 260), -3.0, device="cuda")
+    ops.corr_lookup_conv1x1(pyr, fl, packed, bias, ops.Chan(fused, 4, 256), n, h, w, 4, 4, 256)
+    torch.cuda.synchronize()
+    assert torch.equal(fused, sep)
+    assert (fused[:, :4] == -3).all()
+    ref = torch.relu(corr.double().cpu() @ conv.weight.detach().double().cpu().view(256, 324).T +
+                     conv.bias.detach().double().cpu())
+    close(fused[:, 4:], ref, 1e-4, 1e-5, "fused lookup + conv vs fp64")
