@@ -38,6 +38,7 @@ child process (before touching the GPU) and relays its output; rank 0 prints the
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -212,6 +213,11 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
     # of every feature pixel (4 × 16-B points) + the next ↓8 flow written twice (F2, HX: 16 B)
     crit_bytes = batch * P * (4 * 16 + 16)
     corr_flops = 2.0 * batch * P * P * 256
+    # the lookup fused into corr_net.0 (scflow_corr_lookup_conv1x1): 2·M·324·256 flops; bytes =
+    # the lookup's window reads + the 256-channel output (the 324-channel features never leave LDS)
+    # + the packed weights once
+    lc_flops = 2.0 * batch * P * 324 * 256
+    lc_bytes = batch * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 256) + 4 * 328 * 256
     traffic = traffic or {}
     out = []
     for name, tkey, kernel, bound, amount in (
@@ -231,6 +237,10 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
             ("pose_tail", "ph_tail", "ph_tail_kernel (a7 after conv 1 + a8+a10+a11, one persistent "
              "launch; latency-bound phases, bytes dominated by the pose step)", "hbm",
              flow_bytes + tail_weight_bytes),
+            ("corr_lookup_conv", "corr_lookup_conv", "corr_lookup_conv1x1_kernel (a2 + corr_net.0 "
+             "1x1 324->256 + ReLU in one launch: the window samples go to LDS and straight into "
+             "the fp32 MFMA GEMM; frac on the algorithmic flops, bytes_per_launch = window reads + "
+             "output + weights)", "mfma", lc_flops),
             ("corr_pyramid", None, "corr_gemm_pyr_kernel (a1: level 0 + pooled levels 1-3 in one "
              "launch, tiled layout)" if tiled else "corr_gemm_kernel + 3 avgpool2_kernel (a1)", "mfma",
              corr_flops)):
@@ -250,6 +260,14 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
              ("bytes_per_launch" if bound == "hbm" else "flops_per_launch"): amount}
         if bound == "hbm":
             e.update(extra)
+        if name == "corr_lookup_conv":
+            e["bytes_per_launch"] = lc_bytes
+            e["achieved_gbs"] = round(lc_bytes / (ms * 1e-3) / 1e9, 1)
+            e["frac_of_hbm"] = round(lc_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            tr = traffic.get(tkey)
+            e["traffic"] = tr
+            if tr:
+                e["traffic_over_algorithmic"] = round(tr / lc_bytes, 3)
         if name == "pose_flow" and fullres_alone_ms:
             e["alone"] = {"avg_launch_ms": round(fullres_alone_ms, 4),
                           "achieved": round(amount / (fullres_alone_ms * 1e-3) / 1e9, 2),
@@ -291,9 +309,14 @@ def bench_train(args, world, rank, dev, feat):
         losses.append(step(batch)["loss"].detach())
         b.record()
         evs.append((a, b))
-    el = time_steps(one, args.train_steps, 2, world, dev)
+    # the objects the earlier legs left (decoder / refiner graphs, buffers) must not be scanned by
+    # a generation-2 collection inside the timed steps: collect once, then freeze them
+    gc.collect()
+    gc.freeze()
+    el = time_steps(one, args.train_steps, 3, world, dev)
+    gc.unfreeze()
     torch.cuda.synchronize()
-    per = sorted(a.elapsed_time(b) for a, b in evs[2:])  # the timed steps
+    per = sorted(a.elapsed_time(b) for a, b in evs[3:])  # the timed steps
     nparam = sum(p.numel() for p in step.grads.params)
     gb = world * args.train_batch
     which = ("BASELINE configs[3]" if (world, args.train_batch, args.size, args.iters) == (8, 16, 256, 8)
@@ -306,7 +329,7 @@ def bench_train(args, world, rank, dev, feat):
            "unit": "iters/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
            "per_step_ms": {"median": round(per[len(per) // 2], 3), "min": round(per[0], 3),
                            "max": round(per[-1], 3), "spread": round((per[-1] - per[0]) / per[len(per) // 2], 4)},
-           "steps": args.train_steps, "warmup": 2, "global_batch": gb, "n_gpus": world,
+           "steps": args.train_steps, "warmup": 3, "global_batch": gb, "n_gpus": world,
            "allreduce_bytes": 4 * nparam if world > 1 else 0,
            "buckets": len(step.grads.buckets),
            "loss_first_last": [round(float(losses[0]), 4), round(float(losses[-1]), 4)]}
@@ -449,7 +472,7 @@ def main():
     # step, not 2 per launch.
     per_step = {"heads": args.iters, "corr_net1": args.iters, "gru_zr": 2 * args.iters,
                 "corr_lookup": args.iters, "pose_flow": args.iters, "pose_tail": args.iters,
-                "pose_step_crit": args.iters, "corr_pyramid": 1}
+                "pose_step_crit": args.iters, "corr_lookup_conv": args.iters, "corr_pyramid": 1}
     per_step.update({n: args.iters for n in WINO_LAUNCHES[2:]})
     # the headline kernel's launches (every conv_wino_kernel launch of an iteration): bracketed in
     # the timed region, each timer on one launch every other step (an event pair costs a few µs

@@ -17,8 +17,28 @@
 // different pixels, same channels) hit distinct banks.
 
 constexpr int W1_PX = 64;  // pixels per workgroup
-constexpr int W1_PD = 3;   // weight blocks (8 channels) in flight ahead of the MFMAs
+#ifndef W1_PD_DEF
+#define W1_PD_DEF 4
+#endif
+constexpr int W1_PD = W1_PD_DEF;  // weight blocks (8 channels) in flight ahead of the MFMAs
 constexpr int W1_NC = 3;   // A-tile chunks
+
+// Static unroll: StaticFor<I, N>::run(f) calls f(integral_constant<int, i>) for i = I .. N-1 as
+// straight-line code (the MFMA block loops: compile-time ring slots and exact wait counts, which
+// a rolled loop with a runtime-indexed register ring does not get)
+template <int I, int N>
+struct StaticFor {
+  template <class F>
+  __device__ __forceinline__ static void run(F& f) {
+    f(std::integral_constant<int, I>{});
+    StaticFor<I + 1, N>::run(f);
+  }
+};
+template <int N>
+struct StaticFor<N, N> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&) {}
+};
 
 // packed weights: [nb32 = npad/32][kb = K/8][lane 64][4]; lane (li, hh) ↔ output channel
 // 32·nb32 + li, input channel 8·kb + 4·hh + e (zero beyond cin / cout)
@@ -111,16 +131,30 @@ __global__ __launch_bounds__(256, 1) void conv1x1w_kernel(scflow_conv_args a) {
   __syncthreads();
   const float* ar0 = As + li * KP + 4 * hh;
   const float* ar1 = As + (32 + li) * KP + 4 * hh;
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    const int c = kb / CB, kc = kb % CB;
+  // every block as straight-line code (StaticFor): compile-time ring slots and chunk points.  A
+  // block's A fragments are read one block ahead (during the previous block's MFMAs) unless it
+  // opens a chunk, whose rows are published by the barrier right before it.
+  floatx4 an0, an1;
+  auto body = [&](auto kbc) {
+    constexpr int kb = decltype(kbc)::value;
+    constexpr int c = kb / CB, kc = kb % CB, sl = kb % W1_PD;
+    constexpr bool opens = kb == 0 || (kc == 0);  // first block of a chunk: read here
+    constexpr bool last_of_chunk = c + 1 < W1_NC && kc == CB - 1 && (c + 1) * CB < KB;
     // the next chunk's A loads go out two blocks into this chunk (the weight loads already in
     // flight cover their latency); they are stored and published at the chunk's last block
-    if (c + 1 < W1_NC && kc == 2 && (c + 1) * CB < KB) aload(c + 1);
-    const floatx4 a0 = *(const floatx4*)(ar0 + 8 * kb);
-    const floatx4 a1 = *(const floatx4*)(ar1 + 8 * kb);
-    floatx4 b[2] = {bq[kb % W1_PD][0], bq[kb % W1_PD][1]};
-    bload(bq[kb % W1_PD], kb + W1_PD);
+    if constexpr (c + 1 < W1_NC && kc == 2 && (c + 1) * CB < KB) aload(c + 1);
+    if constexpr (opens) {
+      an0 = *(const floatx4*)(ar0 + 8 * kb);
+      an1 = *(const floatx4*)(ar1 + 8 * kb);
+    }
+    const floatx4 a0 = an0, a1 = an1;
+    floatx4 b[2] = {bq[sl][0], bq[sl][1]};
+    if constexpr (kb + W1_PD < KB) bload(bq[sl], kb + W1_PD);
+    if constexpr (kb + 1 < KB && !last_of_chunk) {
+      an0 = *(const floatx4*)(ar0 + 8 * (kb + 1));
+      an1 = *(const floatx4*)(ar1 + 8 * (kb + 1));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the prefetches stay ahead of this block's MFMAs
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], b[0][e], acc[0][0], 0, 0, 0);
@@ -128,11 +162,15 @@ __global__ __launch_bounds__(256, 1) void conv1x1w_kernel(scflow_conv_args a) {
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b[0][e], acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b[1][e], acc[1][1], 0, 0, 0);
     }
-    if (c + 1 < W1_NC && (kc == CB - 1) && (c + 1) * CB < KB) {
+    if constexpr (last_of_chunk) {
       astore(c + 1);
       __syncthreads();
     }
-  }
+    // keep each block's loads where they are issued: the scheduler otherwise sinks them towards
+    // their uses W1_PD blocks later, which turns the prefetch into a wait per block
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  StaticFor<0, KB>::run(body);
 
   // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5); all global reads
   // (bias map) before any store

@@ -78,6 +78,13 @@ __device__ __forceinline__ floatx4 sub4(floatx4 a, floatx4 b) {
 }
 #endif
 
+#ifndef WINO_SCHED_BARRIER
+#define WINO_SCHED_BARRIER 1
+#endif
+#ifndef WINO_U_AHEAD
+#define WINO_U_AHEAD 1
+#endif
+
 constexpr int WKC = 8;    // input channels per sub-step (one MFMA k-pass per lane)
 constexpr int WSC = 32;   // input channels per stage (one LDS halo buffer)
 constexpr int WNSUB = WSC / WKC;
@@ -271,48 +278,64 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][nb][e] = 0.f;
 
-  floatx4 u[4][NBW];
-  // the MFMAs of point j, then point j's weights for sub-step tnext
-  auto point = [&](const floatx4(&v)[4], int j, int tnext) {
+  // U of the next UAH sub-steps in registers (sub-step t in slot t % UAH): a point's reload is for
+  // the sub-step UAH ahead, so it has UAH − 1 further sub-steps plus this one's remaining points to
+  // arrive (WINO_U_AHEAD = 2: the 32-channel workgroups, one wave per SIMD at B = 16)
+  constexpr int UAH = (NBW == 1 && WINO_U_AHEAD > 1) ? 2 : 1;
+  floatx4 u[UAH][4][NBW];
+  // the MFMAs of point j of the sub-step in slot par, then point j's weights for sub-step
+  // tnext + UAH − 1 into the same slot
+  auto point = [&](const floatx4(&v)[4], int j, int tnext, int par) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb)
-        acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[j][nb][e], acc[j][nb], 0, 0, 0);
-    uload1(u[j], tnext, j);
+        acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[par][j][nb][e], acc[j][nb], 0, 0, 0);
+    uload1(u[par][j], tnext + UAH - 1, j);
+    // keep the reload here, three points ahead of its use: left alone the scheduler sinks all four
+    // reloads to the end of the sub-step, one MFMA before the next sub-step waits on them (an L2
+    // round trip exposed per point at one wave per SIMD).  32-channel workgroups only: the
+    // 64 / 96-channel ones run at the 256-VGPR limit (pinning the loads spills there) and have a
+    // second wave per SIMD to cover the latency.
+    if constexpr (WINO_SCHED_BARRIER && (NBW == 1 || WINO_SCHED_BARRIER > 1))
+      __builtin_amdgcn_sched_barrier(0);
   };
-  auto substep = [&](const floatx4(&v)[4], int tnext) {
+  auto substep = [&](const floatx4(&v)[4], int tnext, int par) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) point(v, j, tnext);
+    for (int j = 0; j < 4; ++j) point(v, j, tnext, par);
   };
   // a sub-step with the NEXT sub-step's input transform (from LDS buffer buf, channels 8k..)
   // woven between its point groups in program order — the compiler issues in order, so the LDS
   // latency and the VALU sit under this sub-step's MFMAs instead of in front of them
   auto substep_next = [&](const floatx4(&v)[4], int tnext, int buf, int k, floatx4(&vn)[4]) {
+    const int par = (k - 1) % UAH;  // sub-step t0 + k − 1, t0 a multiple of 4
 #ifdef WX_NO_V
-    substep(v, tnext);
+    substep(v, tnext, par);
     for (int j = 0; j < 4; ++j) vn[j] = v[j];
     return;
 #endif
     const floatx4* hb = smem4 + buf * G::BUF4 + 2 * k;
     constexpr int cb1 = 8, cb2 = 16 + 1, cb3 = 24 + 1;  // column b of the patch (+ skew)
     const floatx4 a0 = hb[o1], b0 = hb[o2], a2 = hb[o1 + cb2], b2 = hb[o2 + cb2];
-    point(v, 0, tnext);
+    point(v, 0, tnext, par);
     const floatx4 t0 = fma_s4(b0, sgn, a0), t2 = fma_s4(b2, sgn, a2);
     vn[0] = sub4(t0, t2);
     const floatx4 a1 = hb[o1 + cb1], b1 = hb[o2 + cb1], a3 = hb[o1 + cb3], b3 = hb[o2 + cb3];
-    point(v, 1, tnext);
+    point(v, 1, tnext, par);
     const floatx4 t1 = fma_s4(b1, sgn, a1), t3 = fma_s4(b3, sgn, a3);
     vn[1] = add4(t1, t2);
     vn[2] = sub4(t2, t1);
     vn[3] = sub4(t1, t3);
-    point(v, 2, tnext);
-    point(v, 3, tnext);
+    point(v, 2, tnext, par);
+    point(v, 3, tnext, par);
   };
 
-  // prologue: stage 0's halo in LDS buffer 0, sub-step 0's weights and transform in registers
+  // prologue: stage 0's halo in LDS buffer 0, sub-step 0's (and 1's) weights and transform in
+  // registers
 #pragma unroll
-  for (int j = 0; j < 4; ++j) uload1(u[j], 0, j);
+  for (int d = 0; d < UAH; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) uload1(u[d][j], d, j);
   hsource(0);
 #pragma unroll
   for (int part = 0; part < 4; ++part) {
@@ -341,7 +364,7 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
     substep_next(vA, t0 + 3, buf, 3, vB);
     hstore(buf ^ 1, 2);
     hload(3);
-    substep(vB, t0 + 4);
+    substep(vB, t0 + 4, 3 % UAH);
     hstore(buf ^ 1, 3);
 #ifndef WX_NO_SYNC
     __syncthreads();

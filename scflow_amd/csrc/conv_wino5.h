@@ -201,6 +201,9 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
         for (int nb = 0; nb < NBW; ++nb)
           acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[q][x][e], u[q][x][nb][e], acc[x][nb], 0, 0, 0);
     uload1(tnext, q);
+#if WINO_SCHED_BARRIER
+    __builtin_amdgcn_sched_barrier(0);  // the reload stays a half sub-step ahead (conv_wino.h)
+#endif
   };
 
   // The main loop is instantiated per transform shape (waves 0-2 / wave 3; the wave index is

@@ -4,18 +4,20 @@
 // pixel never leave the CU (the separate path writes and re-reads them: 21 MB per iteration at
 // B = 16, 256²; 166 MB at configs[4]).
 //
-// Workgroup = 64 pixels × every output channel, 4 waves, one per CU:
-//  * the A tile (64 pixels × K = 324 channels, + zero padding to 8-channel blocks) is built in
-//    LDS level by level: per level the pixels' 16×16 tile-aligned regions of the TILED pyramid
+// Workgroup = 64 pixels × every output channel, one per CU, 8 waves in two roles:
+//  * 4 producer waves build the A tile (64 pixels × K = 324 channels, + zero padding to 8-channel
+//    blocks) in LDS level by level: per level the pixels' 16×16 tile-aligned regions of the TILED pyramid
 //    (b128 loads of whole 4-float tile rows, the layout of scflow_corr_pyramid_tiled) go to LDS,
 //    and the (2r+1)² samples of every pixel are computed from them with the lookup's own
 //    arithmetic (corr_lookup_lds_kernel<4, true, true>: grid_sample's normalise / unnormalise
 //    round trip with FP contraction off, the same region origins, zero outside) into the pixel's
 //    A row, channel l·81 + a·9 + b;
-//  * the GEMM runs as in conv1x1w_kernel (conv1x1w.h): weights pre-packed in MFMA-lane order and
-//    streamed from L2 into registers, 2 × 2 blocks of v_mfma_f32_32x32x2_f32 per wave;
-//  * the levels pipeline: level l+1's region loads are in flight while level l is sampled and
-//    the 8-channel blocks complete after level l are multiplied.
+//  * 4 consumer waves run the GEMM as conv1x1w_kernel (conv1x1w.h) does: weights pre-packed in
+//    MFMA-lane order and streamed from L2 into registers, 2 × 2 blocks of v_mfma_f32_32x32x2_f32
+//    per wave;
+//  * the roles overlap level by level: while the producers load and sample level l the consumers
+//    multiply the 8-channel blocks levels < l completed — the lookup's latency chain and its
+//    VALU / LDS work sit beside the MFMAs instead of between them; one barrier per level.
 // The A values are bit-identical to the lookup kernel's outputs and the MFMA order is
 // conv1x1w_kernel's, so the result equals scflow_corr_lookup_tiled + the wide 1×1 conv bit for
 // bit (tests/test_gpu_ops.py).
@@ -34,6 +36,26 @@ constexpr int LC_TRW = 16;                // region side (floats)
 constexpr int LC_WP = LC_TRW * LC_TRW + 4;  // region stride per pixel (floats, ≡ 4 mod 64)
 constexpr int LC_PD = 3;                  // weight blocks in flight ahead of the MFMAs
 constexpr int LC_OOB = 0x7ffffff0;
+// the 8-channel blocks complete once levels 0..l are sampled: [LC_KEND[l-1], LC_KEND[l])
+constexpr int LC_KEND[LC_L] = {(1 * LC_D * LC_D) / 8, (2 * LC_D * LC_D) / 8, (3 * LC_D * LC_D) / 8,
+                               LC_KB};
+__host__ __device__ constexpr int lc_level(int kb) {
+  return kb < LC_KEND[0] ? 0 : kb < LC_KEND[1] ? 1 : kb < LC_KEND[2] ? 2 : 3;
+}
+
+template <int I, int N>  // straight-line loop (see conv1x1w.h's StaticFor)
+struct StaticFor {
+  template <class F>
+  __device__ __forceinline__ static void run(F& f) {
+    f(std::integral_constant<int, I>{});
+    StaticFor<I + 1, N>::run(f);
+  }
+};
+template <int N>
+struct StaticFor<N, N> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&) {}
+};
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t lc_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -59,22 +81,25 @@ struct LcArgs {
   int so, n, h, w, cout, act, ac;
 };
 
-__global__ __launch_bounds__(256, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
+__global__ __launch_bounds__(512, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
 #pragma clang fp contract(off)
   extern __shared__ floatx4 smem4[];
   float* As = (float*)smem4;               // [64][LC_KP]
   float* Wn = As + LC_PX * LC_KP;          // [64][LC_WP] one level's regions
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // waves 0-3 multiply (consumers), waves 4-7 look up (producers)
+  const bool producer = wave >= 4;
   const int li = lane & 31, hh = lane >> 5;
   const int H = a.h, W = a.w, P = H * W;
   const long long M = (long long)a.n * P;
   const long long m0 = (long long)blockIdx.x * LC_PX;
   const int npad = (a.cout + 63) / 64 * 64;
-  const bool wave_on = wave * 64 < npad;
+  const bool wave_on = !producer && wave * 64 < npad;
 
-  // this thread's pixel (4 threads per pixel) and its share of the window columns a
-  const int ps = tid >> 2, sub = tid & 3;
+  // a producer thread's pixel (4 threads of one wave per pixel) and its share of the columns a
+  const int pt = producer ? tid - 256 : 0;
+  const int ps = pt >> 2, sub = pt & 3;
   const long long gp = m0 + ps;
   const bool active = gp < M;
   const int p = active ? (int)(gp % P) : 0;
@@ -88,12 +113,12 @@ __global__ __launch_bounds__(256, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
   const int npx = left < LC_PX ? (int)left : LC_PX;
 
   // region origin of level l (map coordinates, one axis): corr_lookup_lds_kernel<4, true, true>
-  auto origin = [&](int l, int axis, float c0x, float c0y) {
+  auto origin = [&](int l, int axis, float c0x, float c0y) __attribute__((always_inline)) {
     const bool fin = isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f && fabsf(c0y) < 1e8f;
     int o = fin ? (int)floorf(axis == 0 ? c0x : c0y) - 1 : -(1 << 29);
     return ((axis == 0 ? W : H) >> l) <= 8 ? -4 : (o >> 2) << 2;
   };
-  auto first = [&](int l, int axis) {  // the level's first sample coordinate on an axis
+  auto first = [&](int l, int axis) __attribute__((always_inline)) {  // the level's first sample coordinate on an axis
     const int size = axis == 0 ? (W >> l) : (H >> l);
     const float c = ((float)(axis == 0 ? x : y) + (axis == 0 ? fx : fy)) / (float)(1 << l);
     return lc_unnorm(c + (float)(0 - LC_R), size, a.ac);
@@ -101,7 +126,7 @@ __global__ __launch_bounds__(256, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
 
   // region loads of level l: the pixel's 64 tile rows, 16 per thread (k = sub + 4j)
   floatx4 wr[16];
-  auto rload = [&](int l) {
+  auto rload = [&](int l) __attribute__((always_inline)) {
     size_t loff = 0;
     for (int k = 0; k < l; ++k) loff += (size_t)M * ((H >> k) * (W >> k));
     const int Hl = H >> l, Wl = W >> l, hw = Hl * Wl;
@@ -118,7 +143,7 @@ __global__ __launch_bounds__(256, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
       wr[j] = lc_bload4(rs, ok ? (ps * hw + e) * 4 : LC_OOB, 0);
     }
   };
-  auto rstore = [&]() {
+  auto rstore = [&]() __attribute__((always_inline)) {
     float* sw = Wn + ps * LC_WP;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -127,7 +152,7 @@ __global__ __launch_bounds__(256, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
     }
   };
   // samples of level l into the A row: this thread's columns a = sub, sub + 4, sub + 8
-  auto sample = [&](int l) {
+  auto sample = [&](int l) __attribute__((always_inline)) {
 #pragma clang fp contract(off)
     const int Hl = H >> l, Wl = W >> l;
     const float scale = (float)(1 << l);
@@ -198,11 +223,27 @@ __global__ __launch_bounds__(256, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
   floatx4 bq[LC_PD][2];
   const float* ar0 = As + li * LC_KP + 4 * hh;
   const float* ar1 = As + (32 + li) * LC_KP + 4 * hh;
-  auto block = [&](int kb) {
-    const floatx4 a0 = *(const floatx4*)(ar0 + 8 * kb);
-    const floatx4 a1 = *(const floatx4*)(ar1 + 8 * kb);
-    floatx4 b[2] = {bq[kb % LC_PD][0], bq[kb % LC_PD][1]};
-    bload(bq[kb % LC_PD], kb + LC_PD);
+  // one block as straight-line code (conv1x1w_kernel's structure): the weights PD blocks and the
+  // A fragments one block ahead are issued first, then the 16 MFMAs; a phase's first block reads
+  // its A fragments itself (they are published by the barrier right before it)
+  floatx4 an0, an1;
+  auto body = [&](auto kbc) __attribute__((always_inline)) {
+    constexpr int kb = decltype(kbc)::value, sl = kb % LC_PD;
+    constexpr int l = lc_level(kb);
+    constexpr bool opens = kb == (l == 0 ? 0 : LC_KEND[l == 0 ? 0 : l - 1]);
+    constexpr bool last = kb + 1 == LC_KEND[l];
+    if constexpr (opens) {
+      an0 = *(const floatx4*)(ar0 + 8 * kb);
+      an1 = *(const floatx4*)(ar1 + 8 * kb);
+    }
+    const floatx4 a0 = an0, a1 = an1;
+    floatx4 b[2] = {bq[sl][0], bq[sl][1]};
+    if constexpr (kb + LC_PD < LC_KB) bload(bq[sl], kb + LC_PD);
+    if constexpr (!last) {
+      an0 = *(const floatx4*)(ar0 + 8 * (kb + 1));
+      an1 = *(const floatx4*)(ar1 + 8 * (kb + 1));
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[e], b[0][e], acc[0][0], 0, 0, 0);
@@ -210,39 +251,51 @@ __global__ __launch_bounds__(256, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b[0][e], acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[e], b[1][e], acc[1][1], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // a producer's level-l region: written and read only by the pixel's own 4 lanes (one wave), so
+  // a wave-level completion wait orders the stores before the samples' reads
+  auto regions_to_lds = [&]() __attribute__((always_inline)) {
+    rstore();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS stores done
+    __builtin_amdgcn_wave_barrier();
   };
 
-  // prologue: level 0's regions, the padding channels, the first weight blocks
-  rload(0);
+  // Phase 0: the producers load level 0's regions into LDS and sample level 0; the consumers
+  // prefetch their first weight blocks and zero the padding channels.
+  // Phase l = 1..4: the producers load and sample level l while the consumers multiply the blocks
+  // levels < l completed; one barrier ends each phase.
+  if (producer) {
+    rload(0);
+    regions_to_lds();
+    sample(0);
+  } else {
 #pragma unroll
-  for (int d = 0; d < LC_PD; ++d) bload(bq[d], d);
-  if (tid < LC_PX) {
+    for (int d = 0; d < LC_PD; ++d) bload(bq[d], d);
+    if (tid < LC_PX) {
 #pragma unroll
-    for (int c = LC_K; c < 8 * LC_KB; ++c) As[tid * LC_KP + c] = 0.f;
-  }
-  rstore();
-  __syncthreads();
-  // level l: (regions of l already in LDS) issue l+1's loads, sample l, publish, multiply the
-  // blocks it completes, then put l+1's regions in LDS
-#pragma unroll
-  for (int l = 0; l < LC_L; ++l) {
-    if (l + 1 < LC_L) rload(l + 1);
-    sample(l);
-    __syncthreads();  // A columns of level l visible; every thread done with level l's regions
-    constexpr int kend[LC_L] = {(1 * LC_D * LC_D) / 8, (2 * LC_D * LC_D) / 8, (3 * LC_D * LC_D) / 8,
-                                LC_KB};
-    const int kb0 = l == 0 ? 0 : kend[l - 1];
-#pragma unroll
-    for (int kb = kb0; kb < kend[l]; ++kb) block(kb);
-    if (l + 1 < LC_L) {
-      rstore();
-      __syncthreads();
+      for (int c = LC_K; c < 8 * LC_KB; ++c) As[tid * LC_KP + c] = 0.f;
     }
   }
+  __syncthreads();
+  auto phase = [&](auto lc) __attribute__((always_inline)) {
+    constexpr int l = decltype(lc)::value;  // 1..4
+    if (producer) {
+      if constexpr (l < LC_L) {  // (the region loads' latency hides under the consumers' phase)
+        rload(l);
+        regions_to_lds();
+        sample(l);
+      }
+    } else {
+      StaticFor<(l == 1 ? 0 : LC_KEND[l == 1 ? 0 : l - 2]), LC_KEND[l - 1]>::run(body);
+    }
+    if constexpr (l < LC_L) __syncthreads();
+  };
+  StaticFor<1, LC_L + 1>::run(phase);
 
   // epilogue (conv1x1w_kernel's): bias, activation; C/D col = lane&31, row = (r&3) + 8(r>>2) +
   // 4(lane>>5)
-  if (!wave_on) return;
+  if (!wave_on) return;  // (producers and idle consumer waves)
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
     const int col = 64 * wave + 32 * nb + li;
@@ -298,6 +351,6 @@ SCFLOW_API int scflow_corr_lookup_conv1x1(const float* pyr, const float* flow, c
     attr = true;
   }
   const long long M = (long long)n * h * w;
-  corr_lookup_conv1x1_kernel<<<(unsigned)((M + LC_PX - 1) / LC_PX), 256, lds, (hipStream_t)stream>>>(a);
+  corr_lookup_conv1x1_kernel<<<(unsigned)((M + LC_PX - 1) / LC_PX), 512, lds, (hipStream_t)stream>>>(a);
   return scflow_launch_status();
 }

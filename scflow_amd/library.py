@@ -129,8 +129,10 @@ def corr_lookup_backward(dout: Tensor, flow: Tensor, numel: int, num_levels: int
     align_corners=True)."""
     B, _, H, W = flow.shape
     dpyr = torch.zeros(numel, device=dout.device, dtype=torch.float32)
-    ops.corr_lookup_backward(dout.contiguous(), flow.contiguous(), dpyr, B, H, W, num_levels, radius,
-                             out_layout="nchw", flow_layout="nchw")
+    # channels-last gradient and flow: the layouts of the training step's lookup backward
+    ops.corr_lookup_backward(dout.permute(0, 2, 3, 1).contiguous().view(B * H * W, -1),
+                             flow.permute(0, 2, 3, 1).contiguous(), dpyr, B, H, W, num_levels,
+                             radius)
     return dpyr
 
 

@@ -250,8 +250,17 @@ class CorrLookup(nn.Module):
 
     def forward(self, corr_pyramid: Sequence[Tensor], flow: Tensor) -> Tensor:
         B, _, H, W = flow.shape
-        if torch.compiler.is_compiling():  # fake tensors have no storage to alias
+        base = corr_pyramid[0]._base
+        if torch.compiler.is_compiling():  # (storage offsets are not traceable)
             buf = torch.cat([lv.reshape(-1) for lv in corr_pyramid])
+        elif (base is not None and base.dim() == 1 and
+                base.numel() == library.pyramid_numel(B, H, W, len(corr_pyramid)) and
+                all(lv._base is base for lv in corr_pyramid) and
+                [lv.storage_offset() - base.storage_offset() for lv in corr_pyramid] ==
+                [sum(B * H * W * (H >> k) * (W >> k) for k in range(l)) for l in range(len(corr_pyramid))]):
+            buf = base  # CorrelationPyramid's flat buffer itself: autograd reaches every level
+        elif any(lv.requires_grad for lv in corr_pyramid):
+            buf = torch.cat([lv.reshape(-1) for lv in corr_pyramid])  # (no aliasing view: autograd)
         else:
             buf = ops.pyramid_buffer(corr_pyramid, B, H, W)
         # torch.ops.scflow.corr_lookup

@@ -27,6 +27,7 @@ def groups(B, S):
     zr = f * M * (256 + 256 + 128 + 256) + f * 256 * 256 * 5   # h|motion, bias map, h, z|rh, W
     lookup = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
     pose_step = B * 36 * S * S
+    lookup_conv = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 256) + 4 * 328 * 256
     # the critical-path ↓8 launch (parts = 2): the pose flow at the 4 bilinear source pixels of
     # every feature pixel (4 × 16-B points) + the next iteration's ↓8 flow (F2 and HX, 2 × 8 B)
     pose_step_crit = M * (4 * 16 + 16)
@@ -48,6 +49,8 @@ def groups(B, S):
                     "conv_wino5_kernel<0, 32, 1, 1>", "conv_wino5_kernel<1, 32, 1, 1>"], zr,
                    "SepConvGRU z|r 1×5 + 5×1 (context hoisted)"),
         "corr_lookup": (["corr_lookup_lds_kernel"], lookup, "pyramid lookup r=4, 4 levels"),
+        "corr_lookup_conv": (["corr_lookup_conv1x1_kernel"], lookup_conv, "pyramid lookup fused "
+                             "into corr_net.0: window reads + 256-channel output + weights"),
         "pose_step": (["pose_step_kernel"], pose_step, "pose update + pose flow + ×8 flow/mask "
                       "(every launch kind averaged: use the two entries below)"),
         "pose_step_fullres": (["pose_step_kernel"], pose_step, "pose_step_kernel, its deferred "
