@@ -3,12 +3,31 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/scflow_hip.h"
 
 #define SCFLOW_API extern "C" __attribute__((visibility("default")))
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// Static unroll: StaticFor<I, N>::run(f) calls f(integral_constant<int, i>) for i = I .. N-1 as
+// straight-line code (MFMA block loops: compile-time register-ring slots and exact wait counts,
+// which a rolled loop over a runtime-indexed register ring does not get)
+template <int I, int N>
+struct StaticFor {
+  template <class F>
+  __device__ __forceinline__ static void run(F& f) {
+    f(std::integral_constant<int, I>{});
+    StaticFor<I + 1, N>::run(f);
+  }
+};
+template <int N>
+struct StaticFor<N, N> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&) {}
+};
 
 static inline int scflow_launch_status() {
   hipError_t e = hipGetLastError();

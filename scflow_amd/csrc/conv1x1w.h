@@ -23,23 +23,6 @@ constexpr int W1_PX = 64;  // pixels per workgroup
 constexpr int W1_PD = W1_PD_DEF;  // weight blocks (8 channels) in flight ahead of the MFMAs
 constexpr int W1_NC = 3;   // A-tile chunks
 
-// Static unroll: StaticFor<I, N>::run(f) calls f(integral_constant<int, i>) for i = I .. N-1 as
-// straight-line code (the MFMA block loops: compile-time ring slots and exact wait counts, which
-// a rolled loop with a runtime-indexed register ring does not get)
-template <int I, int N>
-struct StaticFor {
-  template <class F>
-  __device__ __forceinline__ static void run(F& f) {
-    f(std::integral_constant<int, I>{});
-    StaticFor<I + 1, N>::run(f);
-  }
-};
-template <int N>
-struct StaticFor<N, N> {
-  template <class F>
-  __device__ __forceinline__ static void run(F&) {}
-};
-
 // packed weights: [nb32 = npad/32][kb = K/8][lane 64][4]; lane (li, hh) ↔ output channel
 // 32·nb32 + li, input channel 8·kb + 4·hh + e (zero beyond cin / cout)
 __global__ void conv1x1w_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,

@@ -43,20 +43,6 @@ __host__ __device__ constexpr int lc_level(int kb) {
   return kb < LC_KEND[0] ? 0 : kb < LC_KEND[1] ? 1 : kb < LC_KEND[2] ? 2 : 3;
 }
 
-template <int I, int N>  // straight-line loop (see conv1x1w.h's StaticFor)
-struct StaticFor {
-  template <class F>
-  __device__ __forceinline__ static void run(F& f) {
-    f(std::integral_constant<int, I>{});
-    StaticFor<I + 1, N>::run(f);
-  }
-};
-template <int N>
-struct StaticFor<N, N> {
-  template <class F>
-  __device__ __forceinline__ static void run(F&) {}
-};
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t lc_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }

@@ -57,7 +57,51 @@ struct WwParams {
   WgSegs sg;
 };
 
+// position of a chunk in the (segment, image, row group, column group) walk; consecutive chunks
+// advance it by compares and increments (the static loops keep one per chunk instead of the four
+// scalar integer divisions of a fresh lookup)
+struct WgWalk {
+  int seg, img, ry, cx;
+};
+__device__ __forceinline__ WgWalk wg_walk_at(int ch, int rg, int cg, int nimg) {
+  WgWalk w;
+  const int gi = ch / (rg * cg), rem = ch - gi * rg * cg;
+  w.seg = gi / nimg;
+  w.img = gi - w.seg * nimg;
+  w.ry = rem / cg;
+  w.cx = rem - w.ry * cg;
+  return w;
+}
+__device__ __forceinline__ WgWalk wg_walk_next(WgWalk w, int rg, int cg, int nimg) {
+  if (++w.cx == cg) {
+    w.cx = 0;
+    if (++w.ry == rg) {
+      w.ry = 0;
+      if (++w.img == nimg) {
+        w.img = 0;
+        ++w.seg;
+      }
+    }
+  }
+  return w;
+}
+
 typedef float floatx2w __attribute__((ext_vector_type(2)));
+
+// one k-step's LDS operands before the transforms: dY rows 0, 1 of the tile pair and the halo
+// rows r1, r2 (two 8-byte reads each) for both 32-ci blocks
+struct WwRaw {
+  floatx2w y0, y1, a0[2], a1[2], b0[2], b1[2];
+};
+
+#ifndef WW_STATIC
+#define WW_STATIC 1
+#endif
+
+__device__ const floatx4 ww_zero4 = {0.f, 0.f, 0.f, 0.f};  // source of the zero-padding lanes
+// a float4 in the global address space: global_load (vmcnt only), not a flat load, which also
+// counts in lgkmcnt and would make every LDS wait wait for it
+typedef __attribute__((address_space(1))) floatx4 WwGlobal4;
 
 // halo float4 slot j of thread tid: (pixel p of the 6 × 34 halo, first channel cq).  A wave-load
 // covers 8 consecutive pixels × 8 channel quads (one 32-channel half, 128 B per pixel), so the
@@ -201,12 +245,93 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
     }
   };
 
+  // the same operands in two halves (WW_STATIC): the raw LDS reads, then the arithmetic
+  // step st of this wave: tile row st >> 2, tile column 4·ks + hh + 8·((st >> 1) & 1) + 2·(st & 1)
+  // — per-thread bases plus compile-time offsets once unrolled (ds_read offset fields)
+  const int tc0 = 4 * ks + hh;
+  auto rawload = [&](int st, WwRaw& r) __attribute__((always_inline)) {
+    const int ttr = st >> 2, co2 = 2 * (8 * ((st >> 1) & 1) + 2 * (st & 1));
+    const float* db = Dl + li * WWD + 2 * tc0 + co2;
+    r.y0 = *(const floatx2w*)(db + (2 * ttr) * WWCO * WWD);
+    r.y1 = *(const floatx2w*)(db + (2 * ttr + 1) * WWCO * WWD);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const float* xb = Xl + (cb * 32 + li) * WWX + 2 * tc0 + co2;
+      r.a0[cb] = *(const floatx2w*)(xb + (2 * ttr + r1) * WWCI * WWX);
+      r.a1[cb] = *(const floatx2w*)(xb + (2 * ttr + r1) * WWCI * WWX + 2);
+      r.b0[cb] = *(const floatx2w*)(xb + (2 * ttr + r2) * WWCI * WWX);
+      r.b1[cb] = *(const floatx2w*)(xb + (2 * ttr + r2) * WWCI * WWX + 2);
+    }
+  };
+  auto xform = [&](const WwRaw& r, float (&yv)[4], float (&vv)[2][4]) __attribute__((always_inline)) {
+    const float q0 = ya * r.y0[0] + yb * r.y1[0], q1 = ya * r.y0[1] + yb * r.y1[1];
+    yv[0] = q0;
+    yv[1] = q0 + q1;
+    yv[2] = q0 - q1;
+    yv[3] = q1;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const float t0 = r.a0[cb][0] + sb * r.b0[cb][0], t1 = r.a0[cb][1] + sb * r.b0[cb][1];
+      const float t2 = r.a1[cb][0] + sb * r.b1[cb][0], t3 = r.a1[cb][1] + sb * r.b1[cb][1];
+      vv[cb][0] = t0 - t2;
+      vv[cb][1] = t1 + t2;
+      vv[cb][2] = t2 - t1;
+      vv[cb][3] = t1 - t3;
+    }
+  };
+  (void)rawload;
+  (void)xform;
+
+#if WW_STATIC
+  // the next chunk's global loads in three pieces issued inside steps 0..2 of this chunk (their
+  // address arithmetic in the MFMA shadow): every lane loads unconditionally — from ww_zero4
+  // where the old code branched around the load (padding, channels beyond cout / cin)
+  struct Gsrc {
+    const float *dy, *s0, *s1;
+    int oy0, ox0;
+  };
+  auto gsetup = [&](const WgWalk& w) __attribute__((always_inline)) {
+    const size_t ipx = (size_t)w.img * a.h * a.w;
+    return Gsrc{wg_pick(P.sg.dy, w.seg) + ipx * a.sdy, wg_pick(P.sg.src0, w.seg) + ipx * a.s0,
+                wg_pick(P.sg.src1, w.seg) + ipx * a.s1, 4 * w.ry, 32 * w.cx};
+  };
+  auto gpiece = [&](const Gsrc& g, int part) __attribute__((always_inline)) {
+    if (part == 0) {
+#pragma unroll
+      for (int j = 0; j < WW_ND; ++j) {
+        const int idx = tid + WW_NT * j;
+        const int p = idx >> 3, co = co0 + 4 * (idx & 7);
+        const float* src = g.dy + ((size_t)(g.oy0 + (p >> 5)) * a.w + g.ox0 + (p & 31)) * a.sdy + co;
+        rd[j] = *(const WwGlobal4*)(co < a.cout ? src : (const float*)&ww_zero4);
+      }
+    }
+    const int j0 = part == 0 ? 0 : (part == 1 ? 1 : 4), j1 = part == 0 ? 1 : (part == 1 ? 4 : WW_NX);
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {
+      int p, cq;
+      ww_halo_slot(tid, j, &p, &cq);
+      const int c = ci0 + cq;
+      const int hr = p / 34, hc = p - hr * 34;
+      const int iy = g.oy0 - 1 + hr, ix = g.ox0 - 1 + hc;
+      const bool ok = p < 6 * 34 && c < cin && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+      const size_t pix = (size_t)iy * a.w + ix;
+      const float* src = c < a.cin0 ? g.s0 + pix * a.s0 + c : g.s1 + pix * a.s1 + (c - a.cin0);
+      rx[j] = *(const WwGlobal4*)(ok ? src : (const float*)&ww_zero4);
+    }
+  };
+#endif
+
   if (c_begin < c_end) {
     gload(c_begin);
     lstore(0);
     __syncthreads();
+#if !WW_STATIC
     if (c_begin + 1 < c_end) gload(c_begin + 1);
+#endif
   }
+#if WW_STATIC
+  WgWalk wk = wg_walk_at(c_begin, P.rg, P.cg, P.sg.nimg);
+#endif
   for (int ch = c_begin; ch < c_end; ++ch) {
     const int cur = (ch - c_begin) & 1;
     Dl = smem + cur * WBUF;
@@ -215,6 +340,41 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       const int co = tid & 31;
       for (int p = tid >> 5; p < 128; p += WW_NT / 32) bsum += Dl[((p >> 5) * WWCO + co) * WWD + (p & 31)];
     }
+#if WW_STATIC
+    // the wave's 8 k-steps s (kk = 2·ks + 4·(s >> 1) + (s & 1)) as straight-line code: step s
+    // issues step s + 1's LDS reads, then its own 8 MFMAs with step s + 1's operand arithmetic
+    // interleaved from the fourth MFMA on (by then the reads have landed) — no LDS wait in front
+    // of an MFMA, and no exposed read latency
+    (void)operands;
+    WwRaw raw;
+    float yv[2][4], vv[2][2][4];
+    rawload(0, raw);
+    xform(raw, yv[0], vv[0]);
+    if (ch + 1 < c_end) wk = wg_walk_next(wk, P.rg, P.cg, P.sg.nimg);  // (the last reloads itself)
+    const Gsrc gn = gsetup(wk);
+    auto step = [&](auto sc) __attribute__((always_inline)) {
+      constexpr int st = decltype(sc)::value, cu = st & 1, nx = (st + 1) & 1;
+      if constexpr (st < 3) gpiece(gn, st);
+      if constexpr (st + 1 < 8) rawload(st + 1, raw);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          acc[j][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(yv[cu][j], vv[cu][cb][j], acc[j][cb], 0, 0, 0);
+      if constexpr (st + 1 < 8) {
+        xform(raw, yv[nx], vv[nx]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);  // the DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // three MFMAs
+#pragma unroll
+        for (int m = 0; m < 5; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // five VALU
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    StaticFor<0, 8>::run(step);
+#else
     float yA[4], vA[2][4], yB[4], vB[2][4];
     operands(2 * ks, yA, vA);
     for (int kk = 2 * ks; kk < 16; kk += 4) {
@@ -231,10 +391,13 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
         for (int cb = 0; cb < 2; ++cb)
           acc[j][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(yB[j], vB[cb][j], acc[j][cb], 0, 0, 0);
     }
+#endif
     if (ch + 1 < c_end) {
       lstore(cur ^ 1);
       __syncthreads();
+#if !WW_STATIC
       if (ch + 2 < c_end) gload(ch + 2);
+#endif
     }
   }
   // the second k-step set's sums onto the first's

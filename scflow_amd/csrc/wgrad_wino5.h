@@ -45,6 +45,10 @@ constexpr int W5W_ND = 4;                      // 4-pixel dY groups per lane per
 constexpr int W5W_NX = 5;                      // halo groups (4 rows × 9) per lane (36 / 8 waves)
 __device__ __forceinline__ int w5w_addr(int r, int c, int ch) { return (r * 64 + ch) * W5W_RW + c; }
 
+#ifndef W5W_STATIC
+#define W5W_STATIC 1
+#endif
+
 struct W5wParams {
   scflow_wgrad_args a;
   int H, W;        // the walked image: 1×5 (h, w); 5×1 the transpose (w, h)
@@ -200,6 +204,158 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
           acc[x][cb][ib] = __builtin_amdgcn_mfma_f32_32x32x2f32(yv[x][cb], vv[x][ib], acc[x][cb][ib], 0, 0, 0);
   };
 
+#if W5W_STATIC
+  // Static form: two LDS buffers (one barrier per chunk); the next chunk's loads go out in five
+  // pieces inside steps 0..4 (branch-free: lanes outside the data load ww_zero4), the wave's 8
+  // k-steps st (kk = 2·ks + 4·(st >> 1) + (st & 1): tile row st >> 1, first column
+  // 4·(4ks + hh) + 8·(st & 1)) as straight-line code — step st issues step st + 1's LDS reads, then
+  // its MFMAs with step st + 1's operand arithmetic interleaved
+  struct Gsrc {
+    const float *dy, *src;
+    int ss, oy0, ox0, img;
+  };
+  auto gsetup = [&](const WgWalk& w) __attribute__((always_inline)) {
+    const int c = ci0 + cl;
+    const float* s0 = wg_pick(P.sg.src0, w.seg);
+    const float* s1 = wg_pick(P.sg.src1, w.seg);
+    return Gsrc{wg_pick(P.sg.dy, w.seg), c < a.cin0 ? s0 + c : s1 + (c - a.cin0),
+                c < a.cin0 ? a.s0 : a.s1, 4 * w.ry, 32 * w.cx, w.img};
+  };
+  typedef __attribute__((address_space(1))) float G1;
+  auto gpiece = [&](const Gsrc& g, int part) __attribute__((always_inline)) {
+    const float* zero = (const float*)&ww_zero4;
+    if (part < 2) {
+      const int co = co0 + cl;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {  // dY: row q >> 3, columns 4(q & 7) + k
+        const int j = 2 * part + jj, q = wv + 8 * j;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float* p = g.dy + pix(g.img, g.oy0 + (q >> 3), g.ox0 + 4 * (q & 7) + k) * a.sdy + co;
+          rd[j][k] = *(const G1*)(co < a.cout ? p : zero);
+        }
+      }
+      return;
+    }
+    const bool cok = ci0 + cl < cin;
+    const int j0 = part == 2 ? 0 : (part == 3 ? 2 : 4), j1 = part == 2 ? 2 : (part == 3 ? 4 : 5);
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {  // halo: row q / 9, columns x = ox0 − 2 + 4(q % 9) + k
+      const int q = wv + 8 * j;
+      const int y = g.oy0 + q / 9;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int x = g.ox0 - 2 + 4 * (q % 9) + k;
+        const bool ok = q < 36 && cok && x >= 0 && x < P.W;
+        const float* p = g.src + pix(g.img, y, x) * g.ss;
+        rx[j][k] = *(const G1*)(ok ? p : zero);
+      }
+    }
+  };
+  auto lstore2 = [&](float* D, float* X) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < W5W_ND; ++j) {
+      const int q = wv + 8 * j;
+      *(floatx4*)(D + w5w_addr(q >> 3, 4 * (q & 7), cl)) = rd[j];
+    }
+#pragma unroll
+    for (int j = 0; j < W5W_NX; ++j) {
+      const int q = wv + 8 * j;
+      if (q < 36) *(floatx4*)(X + w5w_addr(q / 9, 4 * (q % 9), cl)) = rx[j];
+    }
+  };
+  struct Raw5 {
+    floatx4 d[2], x0[2], x1[2];
+  };
+  const int cc0 = 4 * (4 * ks + hh);
+  auto rawload = [&](int st, Raw5& r) __attribute__((always_inline)) {
+    const int rr = st >> 1, c = cc0 + 8 * (st & 1);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) r.d[cb] = *(const floatx4*)(Dl + w5w_addr(rr, c, cb * 32 + li));
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      r.x0[ib] = *(const floatx4*)(Xl + w5w_addr(rr, c, ib * 32 + li));
+      r.x1[ib] = *(const floatx4*)(Xl + w5w_addr(rr, c + 4, ib * 32 + li));
+    }
+  };
+  auto xform = [&](const Raw5& r, float (&yv)[2][2], float (&vv)[2][2], auto W3)
+                   __attribute__((always_inline)) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const floatx4 d = r.d[cb];
+      if constexpr (decltype(W3)::value) {
+        yv[0][cb] = d[0];
+        yv[1][cb] = d[3];
+      } else {
+        const float e = d[0] + s2 * d[2], o = s1 * d[1] + s3 * d[3];
+        yv[0][cb] = e + o;
+        yv[1][cb] = e - o;
+      }
+    }
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      const floatx4 x0 = r.x0[ib], x1 = r.x1[ib];
+      if constexpr (decltype(W3)::value) {
+        vv[0][ib] = (x1[2] - x0[0]) + 5.25f * (x0[2] - x1[0]);
+        vv[1][ib] = (x1[3] - x0[1]) + 5.25f * (x0[3] - x1[1]);
+      } else {
+        const float av = c1 * x0[1] + c3 * x0[3] + c5 * x1[1];
+        const float bv = c2 * x0[2] + c4 * x1[0] + x1[2];
+        vv[0][ib] = bv + av;
+        vv[1][ib] = bv - av;
+      }
+    }
+  };
+  auto mainloop = [&](auto W3) __attribute__((always_inline)) {
+    constexpr int BUF = W5W_DFL + W5W_XFL;
+    (void)operands;
+    WgWalk wk = wg_walk_at(c_begin, P.rg, P.cg, P.sg.nimg);
+    if (c_begin < c_end) {
+      const Gsrc g0 = gsetup(wk);
+#pragma unroll
+      for (int part = 0; part < 5; ++part) gpiece(g0, part);
+      lstore2(smem, smem + W5W_DFL);
+      __syncthreads();
+    }
+    for (int ch = c_begin; ch < c_end; ++ch) {
+      const int cur = (ch - c_begin) & 1;
+      Dl = smem + cur * BUF;
+      Xl = Dl + W5W_DFL;
+      if (do_bias) {  // Σ dY per channel: thread (co = tid & 63) over every 8th pixel
+        const int co = tid & 63;
+        for (int p = tid >> 6; p < 128; p += W5W_NT / 64) bsum += Dl[w5w_addr(p >> 5, p & 31, co)];
+      }
+      if (ch + 1 < c_end) wk = wg_walk_next(wk, P.rg, P.cg, P.sg.nimg);  // (the last reloads itself)
+      const Gsrc gn = gsetup(wk);
+      Raw5 raw;
+      float yv[2][2][2], vv[2][2][2];
+      rawload(0, raw);
+      xform(raw, yv[0], vv[0], W3);
+      auto step = [&](auto sc) __attribute__((always_inline)) {
+        constexpr int st = decltype(sc)::value, cu = st & 1, nx = (st + 1) & 1;
+        if constexpr (st < 5) gpiece(gn, st);
+        if constexpr (st + 1 < 8) rawload(st + 1, raw);
+        mfmas(yv[cu], vv[cu]);
+        if constexpr (st + 1 < 8) {
+          xform(raw, yv[nx], vv[nx], W3);
+          __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // the DS reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // three MFMAs
+#pragma unroll
+          for (int m = 0; m < 5; ++m) {
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // five VALU
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      StaticFor<0, 8>::run(step);
+      if (ch + 1 < c_end) {
+        lstore2(smem + (cur ^ 1) * BUF, smem + (cur ^ 1) * BUF + W5W_DFL);
+        __syncthreads();
+      }
+    }
+  };
+#else
   // instantiated per transform shape (waves 0-2 / wave 3; the wave index is uniform), so the
   // k-step loop has no branches
   auto mainloop = [&](auto W3) __attribute__((always_inline)) {
@@ -225,6 +381,7 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
       }
     }
   };
+#endif
   if (w3)
     mainloop(std::true_type{});
   else
@@ -383,7 +540,7 @@ int wwino5_launch(const W5wParams& P, hipStream_t st) {
   const int splits = wwino5_splits(P);
   float* slab = a.workspace;
   float* bslab = a.db ? a.workspace + (size_t)splits * 8 * P.copad * P.cinp : nullptr;
-  const size_t lds = sizeof(float) * (size_t)(W5W_DFL + W5W_XFL);
+  const size_t lds = sizeof(float) * (size_t)(W5W_DFL + W5W_XFL) * (W5W_STATIC ? 2 : 1);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)wgrad_wino5_kernel,
