@@ -919,21 +919,37 @@ int wino_swz(int R, int C) {
 // profiling: where the next F(2×2,3×3) Winograd launches write their per-workgroup stamps
 static unsigned long long* g_wino_stamps = nullptr;
 
-template <int W, int NBW>
+template <int W, int NBW, int KS = 1>
 int launch_wino_w(WinoParams p, hipStream_t st) {
   using G = WinoGeom<W>;
-  const size_t lds = wino_lds_bytes<W, NBW>();
+  const size_t lds = wino_lds_bytes<W, NBW, KS>();
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino_kernel<W, NBW>,
+    (void)hipFuncSetAttribute((const void*)conv_wino_kernel<W, NBW, KS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * G::XB, round_up(p.a.cout, 32 * NBW) / (32 * NBW));
   p.swz_c = wino_swz(grid.x, grid.y);
   p.stamps = g_wino_stamps;
-  conv_wino_kernel<W, NBW><<<grid, 256, lds, st>>>(p);
+  conv_wino_kernel<W, NBW, KS><<<grid, 256 * KS, lds, st>>>(p);
   return scflow_launch_status();
+}
+
+// K split (conv_wino_kernel KS = 2) for a 32-channel W = 32 launch whose grid leaves at most one
+// workgroup per CU (one wave per SIMD otherwise).  SCFLOW_WINO_KSPLIT=0 turns it off (A/B).
+#ifndef WINO_KSPLIT_DEFAULT
+#define WINO_KSPLIT_DEFAULT 1
+#endif
+bool wino_ksplit(const scflow_conv_args& a, int cus) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SCFLOW_WINO_KSPLIT");
+    on = e ? atoi(e) != 0 : WINO_KSPLIT_DEFAULT;
+  }
+  if (!on) return false;
+  const long long blocks = (long long)a.n * (a.h / WinoGeom<32>::OROWS) * (round_up(a.cout, 32) / 32);
+  return blocks <= cus;
 }
 
 template <int DIR, int W, int NBW, int EPI>
@@ -948,6 +964,7 @@ int launch_wino5_k(Wino5Params p, hipStream_t st) {
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
   p.swz_c = wino_swz(grid.x, grid.y);
+  p.stamps = g_wino_stamps;
   conv_wino5_kernel<DIR, W, NBW, EPI><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }
@@ -985,9 +1002,11 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
   p.cp0 = round_up(a.c0, WSC);
   p.nst = (p.cp0 + round_up(a.c1, WSC)) / WSC;
   const int nbw = wino_nbw(a, device_cus());
-  if (a.w == 32)
+  if (a.w == 32) {
+    if (nbw == 1 && wino_ksplit(a, device_cus())) return launch_wino_w<32, 1, 2>(p, st);
     return nbw == 3 ? launch_wino_w<32, 3>(p, st)
                     : nbw == 2 ? launch_wino_w<32, 2>(p, st) : launch_wino_w<32, 1>(p, st);
+  }
   if (a.w == 128) return nbw == 2 ? launch_wino_w<128, 2>(p, st) : launch_wino_w<128, 1>(p, st);
   return nbw == 2 ? launch_wino_w<64, 2>(p, st) : launch_wino_w<64, 1>(p, st);
 }
@@ -1388,7 +1407,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
   return scflow_launch_status();
 }
 
-// Profiling only: later F(2×2,3×3) Winograd launches write 4 u64 real-time-clock stamps per
+// Profiling only: later Winograd launches (F(2×2,3×3) and F(4,5)) write 4 u64 real-time-clock stamps per
 // workgroup (start, prologue done, main loop done, epilogue done) to `stamps`, or stop (NULL).
 SCFLOW_API int scflow_debug_conv_stamps(void* stamps) {
   g_wino_stamps = (unsigned long long*)stamps;

@@ -139,24 +139,37 @@ struct WinoGeom {
   __device__ static constexpr int addr(int r, int c) { return r * ROWP + c * 8 + (c >> 1); }
 };
 
-template <int W, int NBW>
+template <int W, int NBW, int KS = 1>
 constexpr size_t wino_lds_bytes() {
   const size_t halo = (size_t)2 * WinoGeom<W>::BUF4 * 4;  // double-buffered
   const size_t epi = (size_t)4 * 2 * (WTM + 4) * 32 * NBW;
-  return sizeof(float) * (halo > epi ? halo : epi);
+  const size_t red = KS > 1 ? (size_t)2 * NBW * 16 * 256 : 0;  // K-split partial sums, 2 points
+  const size_t m = halo > epi ? halo : epi;
+  return sizeof(float) * (m > red ? m : red);
 }
 
 // NBW = 3 (96 output channels, one workgroup per CU: 192 accumulator registers per lane) balances
 // grids whose 64-channel version would leave 1.5 workgroups per CU (corr_net.1 at B = 16).
-template <int W, int NBW>
-__global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoParams P) {
+//
+// KS = 2 (K split, 32-channel workgroups that would leave one wave per SIMD: grids of at most one
+// workgroup per CU): 512 threads, two wave sets over the same points — set ks takes sub-steps
+// ks and ks + 2 of every stage (the shared halo staged by all 8 waves) — their sums added through
+// LDS before the epilogue.  Two waves per SIMD then cover each other's U / LDS latencies and the
+// per-stage barrier.
+template <int W, int NBW, int KS = 1>
+__global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_wino_kernel(WinoParams P) {
+  static_assert(KS == 1 || (KS == 2 && NBW == 1), "K split: 32-channel workgroups");
   using G = WinoGeom<W>;
+  constexpr int NT = 256 * KS;                              // threads
+  constexpr int NA = (G::NH4 + 4 * NT - 1) / (4 * NT);     // float4 per thread per quarter stage
   constexpr int BNW = 32 * NBW;  // output channels per workgroup
   extern __shared__ floatx4 smem4[];  // float4-typed so halo accesses are ds_*_b128
   float* smem = (float*)smem4;
   const scflow_conv_args& a = P.a;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
+  const int wave = wv & 3;                 // Winograd row i of the wave's points
+  const int ks = KS > 1 ? wv >> 2 : 0;     // K-split wave set
   const int li = lane & 31, hh = lane >> 5;
   int bx, by;
   wino_block(P.swz_c, bx, by);
@@ -173,12 +186,12 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   // quad) pair (idx >> 3, idx & 7), idx = tid + 256·(4j + part).  Per slot: the input pixel
   // (-1 = zero padding) and the LDS float4 index, both stage-invariant.
   bool inloop = false;  // tuning experiments (WX_NO_*): prologue loads still happen
-  int hpix[4][G::NA], hlds[4][G::NA];
+  int hpix[4][NA], hlds[4][NA];
 #pragma unroll
   for (int part = 0; part < 4; ++part)
 #pragma unroll
-    for (int j = 0; j < G::NA; ++j) {
-      const int idx = tid + 256 * (4 * j + part);
+    for (int j = 0; j < NA; ++j) {
+      const int idx = tid + NT * (4 * j + part);
       const int pix = idx >> 3;
       const int hr = pix / G::HC, hcol = pix - hr * G::HC;
       const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hcol;
@@ -187,7 +200,7 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
       hlds[part][j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 7) : -1;
     }
   const int hq4 = 4 * (tid & 7);  // channel of this thread's quad within the stage (idx & 7 = tid & 7)
-  floatx4 ra[G::NA];
+  floatx4 ra[NA];
   // stage s's source, as a buffer starting at its first channel
   __amdgpu_buffer_rsrc_t hsrc;
   int hss4 = 0, hlim = 0;  // pixel stride in bytes, channels of the stage present in the source
@@ -213,7 +226,7 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
 #endif
     const bool chan_ok = hq4 < hlim;
 #pragma unroll
-    for (int j = 0; j < G::NA; ++j) {
+    for (int j = 0; j < NA; ++j) {
       const int p = hpix[part][j];
       const bool ok = p >= 0 && chan_ok;
       floatx4 v = wino_bload(hsrc, ok ? p * hss4 + hq4 * 4 : WINO_OOB, 0);
@@ -229,8 +242,8 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
     if (inloop) return;
 #endif
 #pragma unroll
-    for (int j = 0; j < G::NA; ++j)
-      if (G::NH4 % 1024 == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[j];
+    for (int j = 0; j < NA; ++j)
+      if (G::NH4 % (4 * NT) == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[j];
   };
 
   // transformed weights [nb32][sub-step (8 channels)][ξ 16][lane 64][4]; this wave's points are
@@ -283,15 +296,17 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   // arrive (WINO_U_AHEAD = 2: the 32-channel workgroups, one wave per SIMD at B = 16)
   constexpr int UAH = (NBW == 1 && WINO_U_AHEAD > 1) ? 2 : 1;
   floatx4 u[UAH][4][NBW];
-  // the MFMAs of point j of the sub-step in slot par, then point j's weights for sub-step
-  // tnext + UAH − 1 into the same slot
-  auto point = [&](const floatx4(&v)[4], int j, int tnext, int par) {
+  // the wave's sub-step sequence: every sub-step (KS = 1), or sub-steps ks, ks + 2 of each stage
+  auto tsub = [&](int m) { return KS > 1 ? 4 * (m >> 1) + ks + 2 * (m & 1) : m; };
+  // the MFMAs of point j of the sub-step in slot par, then point j's weights for sub-step tload
+  // (the one UAH further along the wave's sequence) into the same slot
+  auto point = [&](const floatx4(&v)[4], int j, int tload, int par) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb)
         acc[j][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[par][j][nb][e], acc[j][nb], 0, 0, 0);
-    uload1(u[par][j], tnext + UAH - 1, j);
+    uload1(u[par][j], tload, j);
     // keep the reload here, three points ahead of its use: left alone the scheduler sinks all four
     // reloads to the end of the sub-step, one MFMA before the next sub-step waits on them (an L2
     // round trip exposed per point at one wave per SIMD).  32-channel workgroups only: the
@@ -300,34 +315,34 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
     if constexpr (WINO_SCHED_BARRIER && (NBW == 1 || WINO_SCHED_BARRIER > 1))
       __builtin_amdgcn_sched_barrier(0);
   };
-  auto substep = [&](const floatx4(&v)[4], int tnext, int par) {
+  auto substep = [&](const floatx4(&v)[4], int tload, int par) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) point(v, j, tnext, par);
+    for (int j = 0; j < 4; ++j) point(v, j, tload, par);
   };
   // a sub-step with the NEXT sub-step's input transform (from LDS buffer buf, channels 8k..)
   // woven between its point groups in program order — the compiler issues in order, so the LDS
   // latency and the VALU sit under this sub-step's MFMAs instead of in front of them
-  auto substep_next = [&](const floatx4(&v)[4], int tnext, int buf, int k, floatx4(&vn)[4]) {
-    const int par = (k - 1) % UAH;  // sub-step t0 + k − 1, t0 a multiple of 4
+  auto substep_next = [&](const floatx4(&v)[4], int tload, int par, int buf, int k,
+                          floatx4(&vn)[4]) {
 #ifdef WX_NO_V
-    substep(v, tnext, par);
+    substep(v, tload, par);
     for (int j = 0; j < 4; ++j) vn[j] = v[j];
     return;
 #endif
     const floatx4* hb = smem4 + buf * G::BUF4 + 2 * k;
     constexpr int cb1 = 8, cb2 = 16 + 1, cb3 = 24 + 1;  // column b of the patch (+ skew)
     const floatx4 a0 = hb[o1], b0 = hb[o2], a2 = hb[o1 + cb2], b2 = hb[o2 + cb2];
-    point(v, 0, tnext, par);
+    point(v, 0, tload, par);
     const floatx4 t0 = fma_s4(b0, sgn, a0), t2 = fma_s4(b2, sgn, a2);
     vn[0] = sub4(t0, t2);
     const floatx4 a1 = hb[o1 + cb1], b1 = hb[o2 + cb1], a3 = hb[o1 + cb3], b3 = hb[o2 + cb3];
-    point(v, 1, tnext, par);
+    point(v, 1, tload, par);
     const floatx4 t1 = fma_s4(b1, sgn, a1), t3 = fma_s4(b3, sgn, a3);
     vn[1] = add4(t1, t2);
     vn[2] = sub4(t2, t1);
     vn[3] = sub4(t1, t3);
-    point(v, 2, tnext, par);
-    point(v, 3, tnext, par);
+    point(v, 2, tload, par);
+    point(v, 3, tload, par);
   };
 
   // prologue: stage 0's halo in LDS buffer 0, sub-step 0's (and 1's) weights and transform in
@@ -335,7 +350,7 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
 #pragma unroll
   for (int d = 0; d < UAH; ++d)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) uload1(u[d][j], d, j);
+    for (int j = 0; j < 4; ++j) uload1(u[d][j], tsub(d), j);
   hsource(0);
 #pragma unroll
   for (int part = 0; part < 4; ++part) {
@@ -348,29 +363,45 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   __syncthreads();
   wino_stamp(P.stamps, 1);
   floatx4 vA[4], vB[4];
-  vcompute(0, 0, vA);
+  vcompute(0, ks, vA);
   inloop = true;
   for (int s = 0; s < nst; ++s) {
     const int buf = s & 1;
-    const int t0 = s * WNSUB;
     hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
-    hload(0);
-    substep_next(vA, t0 + 1, buf, 1, vB);
-    hstore(buf ^ 1, 0);
-    hload(1);
-    substep_next(vB, t0 + 2, buf, 2, vA);
-    hstore(buf ^ 1, 1);
-    hload(2);
-    substep_next(vA, t0 + 3, buf, 3, vB);
-    hstore(buf ^ 1, 2);
-    hload(3);
-    substep(vB, t0 + 4, 3 % UAH);
-    hstore(buf ^ 1, 3);
+    if constexpr (KS == 1) {
+      // sub-step t = 4s + k − 1 in slot t % UAH reloads its points for t + UAH
+      const int t0 = s * WNSUB;
+      hload(0);
+      substep_next(vA, t0 + UAH, 0, buf, 1, vB);
+      hstore(buf ^ 1, 0);
+      hload(1);
+      substep_next(vB, t0 + 1 + UAH, 1 % UAH, buf, 2, vA);
+      hstore(buf ^ 1, 1);
+      hload(2);
+      substep_next(vA, t0 + 2 + UAH, 2 % UAH, buf, 3, vB);
+      hstore(buf ^ 1, 2);
+      hload(3);
+      substep(vB, t0 + 3 + UAH, 3 % UAH);
+      hstore(buf ^ 1, 3);
+    } else {
+      // sequence m = 2s (sub-step ks) and 2s + 1 (sub-step ks + 2), slot m % UAH
+      const int m0 = 2 * s;
+      hload(0);
+      hload(1);
+      substep_next(vA, tsub(m0 + UAH), 0, buf, ks + 2, vB);
+      hstore(buf ^ 1, 0);
+      hstore(buf ^ 1, 1);
+      hload(2);
+      hload(3);
+      substep(vB, tsub(m0 + 1 + UAH), 1 % UAH);
+      hstore(buf ^ 1, 2);
+      hstore(buf ^ 1, 3);
+    }
 #ifndef WX_NO_SYNC
     __syncthreads();
 #endif
 #ifndef WX_NO_V
-    vcompute(buf ^ 1, 0, vA);
+    vcompute(buf ^ 1, ks, vA);
 #endif
   }
 
@@ -394,7 +425,31 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   constexpr int WEP = WTM + 4;
   __syncthreads();
   wino_stamp(P.stamps, 2);
+  if constexpr (KS > 1) {
+    // the second wave set's sums onto the first's, two points per round through LDS
+    float* R = smem;
+#pragma unroll
+    for (int j2 = 0; j2 < 4; j2 += 2) {
+      if (ks == 1)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) R[((jj * NBW + nb) * 16 + r) * 256 + (tid - 256)] = acc[j2 + jj][nb][r];
+      __syncthreads();
+      if (ks == 0)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j2 + jj][nb][r] += R[((jj * NBW + nb) * 16 + r) * 256 + tid];
+      __syncthreads();
+    }
+  }
   float* S = smem;
+  if (ks == 0)
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
@@ -413,14 +468,14 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
       *(floatx4*)&S[((wave * 2 + 1) * BNW + co) * WEP + m0] = s1v;
     }
   __syncthreads();
-  if constexpr (256 % BNW == 0) {
+  if constexpr (NT % BNW == 0) {
     const int co = tid % BNW;
     const int col = by * BNW + co;
     if (col >= a.cout) return;
     const float bias = a.bias ? a.bias[col] : 0.f;
     const float osc = a.out_scale ? a.out_scale[col] : 1.f;
     const float osh = a.out_scale ? a.out_shift[col] : 0.f;
-    constexpr int GROUPS = 256 / BNW;            // 4 (BNW 64) or 8 (BNW 32)
+    constexpr int GROUPS = NT / BNW;             // 4 (BNW 64), 8 (BNW 32) or 16 (BNW 32, KS 2)
     constexpr int NPX = WTM * 4 / GROUPS;        // output pixels per thread
     const int g = tid / BNW;
     const int ar = (g >> 1) & 1, bc = g & 1;      // this thread's output position in the 2×2 tile
@@ -459,7 +514,7 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   } else {
     // BNW does not divide the 256 threads: (output position, channel) pairs dealt round robin,
     // each pair over all WTM tiles (same arithmetic as above)
-    for (int pi = tid; pi < 4 * BNW; pi += 256) {
+    for (int pi = tid; pi < 4 * BNW; pi += NT) {
       const int co = pi % BNW, g = pi / BNW;
       const int col = by * BNW + co;
       if (col >= a.cout) continue;

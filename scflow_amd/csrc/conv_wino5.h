@@ -43,6 +43,7 @@ struct Wino5Params {
   scflow_conv_args a;
   int cp0, nst;  // source 0's channels padded to W5SC, stages (W5SC channels each) over both
   int swz_c;     // XCD-aware block order (wino_block, conv_wino.h), 0 = off
+  unsigned long long* stamps;  // profiling (scflow_debug_conv_stamps, conv_wino.h), or NULL
 };
 
 template <int DIR, int W>  // DIR 0: 1×5 (along x), 1: 5×1 (along y)
@@ -82,6 +83,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   constexpr int XB = W / G::OCOLS;  // column blocks per image (1, or 2 for 5×1 at W = 64)
   int bx, by;
   wino_block(P.swz_c, bx, by);
+  wino_stamp(P.stamps, 0);
   const int blocks_per_img = (a.h / G::OROWS) * XB;
   const int img = bx / blocks_per_img;
   const int rem = bx % blocks_per_img;
@@ -221,6 +223,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     hstore(0, 1);
     __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
     __syncthreads();
+    wino_stamp(P.stamps, 1);
     floatx4 vA[2][2], vB[2][2];
     vload(0, 0, 0, d, w3);
     vmath(d, vA[0], w3);
@@ -270,6 +273,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   // per 16-B load of each point, and y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ]
   constexpr int WEP = W5TM + 4;
   __syncthreads();
+  wino_stamp(P.stamps, 2);
   float* S = smem;
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -360,6 +364,10 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
       for (int o = 0; o < 4; ++o)
         a.hid[(size_t)pix[k][o] * a.sh + col] = (1.f - zv[k][o]) * hv[k][o] + zv[k][o] * tanhf(y[k][o]);
+  }
+  if (P.stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    wino_stamp(P.stamps, 3);
   }
 }
 

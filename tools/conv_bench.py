@@ -41,6 +41,30 @@ SHAPES = [
 ]
 
 
+def stamp_report(run):
+    """One launch of ``run`` with workgroup stamps: spread of the start times, and the median /
+    max of each phase (prologue, main loop, epilogue) over the workgroups, in µs."""
+    from scflow_amd import _lib
+    lib = _lib.load()
+    st = torch.zeros(4 * 8192, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    lib.scflow_debug_conv_stamps(st.data_ptr())
+    run()
+    torch.cuda.synchronize()
+    lib.scflow_debug_conv_stamps(None)
+    v = st.view(-1, 4).cpu()
+    v = v[v[:, 0] > 0].double() / 100.0  # ticks (10 ns) → µs
+    if not len(v):
+        print("    (no stamps: not a Winograd F(2x2,3x3) launch)")
+        return
+    t0 = v[:, 0].min()
+    ph = [v[:, 1] - v[:, 0], v[:, 2] - v[:, 1], v[:, 3] - v[:, 2]]
+    q = lambda x: f"{x.median().item():6.2f}/{x.max().item():6.2f}"
+    print(f"    {len(v)} WGs  start spread {(v[:, 0] - t0).max().item():6.2f} us  span "
+          f"{(v[:, 3].max() - t0).item():6.2f} us  prologue {q(ph[0])}  main {q(ph[1])}  "
+          f"epilogue {q(ph[2])} (median/max us)", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
@@ -49,6 +73,9 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="comma-separated substrings of the shapes to run")
     ap.add_argument("--no-extras", action="store_true", help="skip the pyramid / lookup timings")
+    ap.add_argument("--stamps", action="store_true",
+                    help="Winograd shapes: per-workgroup phase times of one launch "
+                         "(scflow_debug_conv_stamps; s_memrealtime at 100 MHz)")
     a = ap.parse_args()
     n, h, w = a.batch, a.size, a.size
     M = n * h * w
@@ -98,6 +125,8 @@ def main():
         tot_us += us
         res.append(dict(name=name, us=round(us, 2), tflops=round(tf, 2)))
         print(f"{name:28s} {us:9.2f} us  {tf:7.2f} TFLOP/s", flush=True)
+        if a.stamps and k in ((3, 3), (1, 5), (5, 1)):
+            stamp_report(run)
     print(f"{'sum (one of each)':28s} {tot_us:9.2f} us")
     if a.no_extras:
         return
