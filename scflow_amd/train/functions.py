@@ -423,9 +423,22 @@ def flush_pending_wgrads() -> None:
         _flush_holder(hold)
 
 
+class ResidualGrad:
+    """Hand-over of a residual block's identity gradient (encoder BasicBlock without downsample):
+    the block tail's backward (instance_norm_residual_relu_nhwc) leaves dres here instead of
+    returning it, and the block's first conv — the identity's other consumer — adds it in its dX
+    conv's epilogue (bias map), so the input's two gradients never meet in an autograd add.
+    Autograd runs the tail's backward before the first conv's (the conv's output gradient comes
+    through the tail), so the hand-over is always complete when it is taken."""
+    __slots__ = ("d",)
+
+    def __init__(self):
+        self.d = None
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act):
+    def forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act, res_grad=None):
         x0 = x0.contiguous()
         x1 = None if x1 is None else x1.contiguous()
         y = _conv_forward(x0, x1, w.detach().contiguous(), None if b is None else b.detach().contiguous(),
@@ -436,11 +449,12 @@ class _Conv2dNHWC(torch.autograd.Function):
         ctx.bias = b  # the leaf itself (direct gradient accumulation), not saved data
         kh, kw = w.shape[2], w.shape[3]
         ctx.uses = _use_holder(w) if _batchable(kh, kw, stride, ph, pw) and w.requires_grad else None
+        ctx.res_grad = res_grad
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        return _conv_backward(ctx, dy)
+        return _conv_backward(ctx, dy) + (None,)
 
 
 class _Conv2dNHWCSplit(torch.autograd.Function):
@@ -476,6 +490,10 @@ def _conv_backward(ctx, dy):
     _, oh, ow, _ = g.shape
     dx0 = dx1 = dw = db = None
     dbm = g if ctx.needs_input_grad[4] else None
+    hold = getattr(ctx, "res_grad", None)
+    dres = None if hold is None else hold.d  # the identity's gradient, added into dX (ResidualGrad)
+    if hold is not None:
+        hold.d = None
     # output channels not a multiple of 4 (out_net's 126): zero-pad dY so dgrad reads whole float4
     # channel groups (the Winograd / MFMA variants) and wgrad stays on its vector path
     pad_co = (-cout) % 4 if cout > 4 else 0
@@ -493,13 +511,17 @@ def _conv_backward(ctx, dy):
             cols = ops.gemm(g.view(-1, cout), wm)
             dx = ops.col2im(cols, n, h, wd, cin, kh, kw, 1, ph, pw)
         elif s == 1:  # a 'same' conv of dY with the flipped, transposed weights
-            dx = _conv_forward(gp, None, _flip_t(w, pad_co), None, 1, (kh - 1 - ph, kw - 1 - pw))
+            dx = _conv_forward(gp, None, _flip_t(w, pad_co), None, 1, (kh - 1 - ph, kw - 1 - pw),
+                               bias_map=dres)
+            dres = None
         else:
             # strided: cols = dY·Wmat (exactly the products the transposed conv needs, no
             # zero-inserted grid) and the col2im gather onto the input grid
             wm = _cached(w, ("wmat",), lambda: w.detach().permute(0, 2, 3, 1).reshape(cout, -1).contiguous())
             cols = ops.gemm(g.view(-1, cout), wm)
             dx = ops.col2im(cols, n, h, wd, cin, kh, kw, s, ph, pw)
+        if dres is not None:
+            dx = dx + dres
         dx0 = dx if x1 is None else dx[..., :c0]
         dx1 = None if x1 is None else dx[..., c0:]
     want_b = ctx.has_b and ctx.needs_input_grad[3]
@@ -531,12 +553,13 @@ def conv2d_nhwc_split(x: Tensor, weight: Tensor, split: int, bias: Optional[Tens
 
 def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride: int = 1,
                 padding=0, act: Optional[str] = None, x1: Optional[Tensor] = None,
-                bias_map: Optional[Tensor] = None) -> Tensor:
+                bias_map: Optional[Tensor] = None, res_grad: Optional[ResidualGrad] = None) -> Tensor:
     """act(nn.Conv2d(cat[x, x1]) + bias_map) (cross-correlation) on channels-last tensors, HIP
     forward and backward.  ``x1``: optional second input (a channel concat without the copy);
-    ``bias_map``: an [N, OH, OW, cout] tensor added before the activation."""
+    ``bias_map``: an [N, OH, OW, cout] tensor added before the activation; ``res_grad``: a
+    ResidualGrad whose identity gradient this conv's dX adds (x is a residual block's input)."""
     ph, pw = (padding, padding) if isinstance(padding, int) else padding
-    return _Conv2dNHWC.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act)
+    return _Conv2dNHWC.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act, res_grad)
 
 
 # ------------------------------------------------------------------------------- ConvGRU step
@@ -718,7 +741,7 @@ class _InstanceNormResidualNHWC(torch.autograd.Function):
     and the ReLU's backward as separate kernels."""
 
     @staticmethod
-    def forward(ctx, x, res, eps):
+    def forward(ctx, x, res, eps, res_grad=None):
         x = x.contiguous()
         res = res.contiguous()
         n, h, w, c = x.shape
@@ -728,6 +751,7 @@ class _InstanceNormResidualNHWC(torch.autograd.Function):
         y = torch.empty_like(x)
         ops.in_apply_residual(x, scale, shift, res, y, n, h * w, c)
         ctx.save_for_backward(x, scale, shift, y)
+        ctx.res_grad = res_grad
         return y
 
     @staticmethod
@@ -737,12 +761,18 @@ class _InstanceNormResidualNHWC(torch.autograd.Function):
         dx = torch.empty_like(x)
         dres = torch.empty_like(x)
         ops.in_backward_residual(dy.contiguous(), x, scale, shift, y, dx, dres, n, h * w, c)
-        return dx, dres, None
+        if ctx.res_grad is not None:  # handed to the block's first conv (ResidualGrad)
+            ctx.res_grad.d = dres
+            return dx, None, None, None
+        return dx, dres, None, None
 
 
-def instance_norm_residual_relu_nhwc(x: Tensor, res: Tensor, eps: float = 1e-5) -> Tensor:
-    """relu(InstanceNorm2d(affine=False)(x) + res) of channels-last tensors (HIP fwd + bwd)."""
-    return _InstanceNormResidualNHWC.apply(x, res, float(eps))
+def instance_norm_residual_relu_nhwc(x: Tensor, res: Tensor, eps: float = 1e-5,
+                                     res_grad: Optional[ResidualGrad] = None) -> Tensor:
+    """relu(InstanceNorm2d(affine=False)(x) + res) of channels-last tensors (HIP fwd + bwd).
+    ``res_grad``: hand res's gradient to the conv given the same ResidualGrad instead of
+    returning it (res must be that conv's input)."""
+    return _InstanceNormResidualNHWC.apply(x, res, float(eps), res_grad)
 
 
 def instance_norm_nhwc(x: Tensor, eps: float = 1e-5, relu: bool = False) -> Tensor:

@@ -21,7 +21,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import (begin_forward, conv2d_nhwc, conv2d_nhwc_split, corr_lookup, corr_pyramid,
+from .functions import (ResidualGrad, begin_forward, conv2d_nhwc, conv2d_nhwc_split, corr_lookup,
+                        corr_pyramid,
                         group_norm_nhwc, gru_step, instance_norm_nhwc,
                         instance_norm_residual_relu_nhwc, linear, pose_update6, share_weight,
                         upsample_bilinear_ac)
@@ -31,6 +32,7 @@ Tensor = torch.Tensor
 _GRU_FUSED = os.environ.get("SCFLOW_TRAIN_GRU_FUSED", "1") != "0"  # A/B switch (tuning)
 _FUSED_LOSS = os.environ.get("SCFLOW_TRAIN_FUSED_LOSS", "1") != "0"  # A/B switch (tuning)
 _GN_FUSED = os.environ.get("SCFLOW_TRAIN_GN_FUSED", "1") != "0"  # A/B switch (tuning)
+_RES_GRAD = os.environ.get("SCFLOW_TRAIN_RES_GRAD", "1") != "0"  # A/B switch (tuning)
 
 
 def _act(x: Tensor, act) -> Tensor:
@@ -50,8 +52,10 @@ def _cm(x: Tensor, m, x1: Tensor = None) -> Tensor:
     return conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding, act=m.act_type, x1=x1)
 
 
-def _conv(x: Tensor, c) -> Tensor:
-    return conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding)
+def _conv(x: Tensor, c, res_grad=None) -> Tensor:
+    if res_grad is None:
+        return conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding)
+    return conv2d_nhwc(x, c.weight, c.bias, c.stride[0], c.padding, res_grad=res_grad)
 
 
 # ------------------------------------------------------------------------------- encoders
@@ -79,13 +83,18 @@ def encoder_train(enc, x_nhwc: Tensor) -> Tensor:
     x = _norm(_conv(x_nhwc, enc.conv1), enc.norm1, relu=True)
     for name in enc.res_layers:
         for blk in getattr(enc, name):
-            out = _norm(_conv(x, blk.conv1), blk.norm1, relu=True)
+            n2 = blk.norm2
+            fused_tail = (isinstance(n2, torch.nn.InstanceNorm2d) and not n2.affine and x.is_cuda
+                          and x.shape[-1] % 4 == 0 and x.shape[-1] <= 256)
+            # identity block: its input's two gradients (conv1's dX, the identity) summed in
+            # conv1's dX epilogue (ResidualGrad)
+            rg = ResidualGrad() if (fused_tail and blk.downsample is None and _RES_GRAD and
+                                    blk.conv1.stride[0] == 1) else None
+            out = _norm(_conv(x, blk.conv1, rg), blk.norm1, relu=True)
             ident = x if blk.downsample is None else _norm(_conv(x, blk.downsample[0]), blk.downsample[1])
             y2 = _conv(out, blk.conv2)
-            n2 = blk.norm2
-            if (isinstance(n2, torch.nn.InstanceNorm2d) and not n2.affine and y2.is_cuda and
-                    y2.shape[-1] % 4 == 0 and y2.shape[-1] <= 256 and ident.shape == y2.shape):
-                x = instance_norm_residual_relu_nhwc(y2, ident, n2.eps)  # norm + sum + ReLU
+            if fused_tail and y2.shape[-1] % 4 == 0 and y2.shape[-1] <= 256 and ident.shape == y2.shape:
+                x = instance_norm_residual_relu_nhwc(y2, ident, n2.eps, rg)  # norm + sum + ReLU
             else:
                 x = torch.relu(_norm(y2, n2) + ident)
     return _conv(x, enc.conv2)
