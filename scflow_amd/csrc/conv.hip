@@ -952,26 +952,46 @@ bool wino_ksplit(const scflow_conv_args& a, int cus) {
   return blocks <= cus;
 }
 
-template <int DIR, int W, int NBW, int EPI>
+template <int DIR, int W, int NBW, int EPI, int KS = 1>
 int launch_wino5_k(Wino5Params p, hipStream_t st) {
   using G = Wino5Geom<DIR, W>;
-  const size_t lds = wino5_lds_bytes<DIR, W, NBW>();
+  const size_t lds = wino5_lds_bytes<DIR, W, NBW, KS>();
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI>,
+    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI, KS>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
   p.swz_c = wino_swz(grid.x, grid.y);
   p.stamps = g_wino_stamps;
-  conv_wino5_kernel<DIR, W, NBW, EPI><<<grid, 256, lds, st>>>(p);
+  conv_wino5_kernel<DIR, W, NBW, EPI, KS><<<grid, 256 * KS, lds, st>>>(p);
   return scflow_launch_status();
+}
+
+// K split for the F(4,5) kernel (conv_wino5_kernel KS = 2 at 64 channels) when the 64-channel grid
+// is at most one workgroup per CU and the heuristic picked 32 channels (two 32-channel workgroups
+// per CU pay the input transform per 32 instead of 64 output channels).  SCFLOW_WINO5_KSPLIT=0
+// turns it off (A/B).
+#ifndef WINO5_KSPLIT_DEFAULT
+#define WINO5_KSPLIT_DEFAULT 1
+#endif
+bool wino5_ksplit(const scflow_conv_args& a, int nbw, int cus) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SCFLOW_WINO5_KSPLIT");
+    on = e ? atoi(e) != 0 : WINO5_KSPLIT_DEFAULT;
+  }
+  if (!on || nbw != 1 || a.w != 32) return false;
+  const long long blocks = (long long)a.n * (a.h * a.w / 128) * (round_up(a.cout, 64) / 64);
+  return blocks <= cus;
 }
 
 template <int EPI>
 int launch_wino5_epi(const Wino5Params& p, int nbw, hipStream_t st) {
   const bool x = p.a.kh == 1;
+  if (p.a.w == 32 && wino5_ksplit(p.a, nbw, device_cus()))
+    return x ? launch_wino5_k<0, 32, 2, EPI, 2>(p, st) : launch_wino5_k<1, 32, 2, EPI, 2>(p, st);
   if (p.a.w == 32) {
     if (x) return nbw == 2 ? launch_wino5_k<0, 32, 2, EPI>(p, st) : launch_wino5_k<0, 32, 1, EPI>(p, st);
     return nbw == 2 ? launch_wino5_k<1, 32, 2, EPI>(p, st) : launch_wino5_k<1, 32, 1, EPI>(p, st);

@@ -9,7 +9,7 @@ rc=$?; echo "pytest rc=$rc" >> $O/pytest.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_train_ops.py tests/test_gpu_train.py -k "wgrad or conv2d_nhwc or configs3" > $O/pytest_train.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/pytest_train.log; [ $rc -le 1 ] || exit $rc
 for ks in 1 0; do
-  SCFLOW_WINO_KSPLIT=$ks timeout -k 10 120 python -u tools/conv_bench.py --only "corr_net.1,flow_net.1,out_net,heads,dflow.1,mask_enc.1,gru" --no-extras --reps 20 --stamps 2>&1 | sed "s/^/ks$ks /" >> $O/stamps.txt || exit 6
+  SCFLOW_WINO_KSPLIT=$ks SCFLOW_WINO5_KSPLIT=$ks timeout -k 10 120 python -u tools/conv_bench.py --only "corr_net.1,flow_net.1,out_net,heads,dflow.1,mask_enc.1,gru" --no-extras --reps 20 --stamps 2>&1 | sed "s/^/ks$ks /" >> $O/stamps.txt || exit 6
 done
 for v in base ww0; do
   L=""; [ $v != base ] && L=scflow_amd/lib/ab/$v.so
