@@ -626,6 +626,25 @@ int scflow_in_backward_residual(const float* dy, const float* x, const float* sc
 int scflow_in_backward(const float* dy, const float* x, const float* scale, const float* shift,
                        float* dx, double* partial, float* mm, int n, int hw, int c, int chunks,
                        int relu, void* stream);
+/* Training: BatchNorm2d in train mode (+ ReLU, + a residual identity added before the ReLU) of
+ * channels-last x [m pixels][c] (c % 4 == 0, c ≤ 256), the context encoder's norms (resnet.py
+ * BasicBlock, norm_fn 'batch'; torch.nn.functional.batch_norm(training=True)).  The batch
+ * statistics in fp64 (the InstanceNorm statistics over one image of m pixels, chunks ≤ m/256
+ * pixel chunks), then per channel rstd = 1/√(var + eps), shift = −mean·rstd (x̂ = x·rstd + shift),
+ * the folded affine sc = γ·rstd, sh = β − γ·mean·rstd, and — when running_mean / running_var are
+ * given — running ← (1 − momentum)·running + momentum·(mean, unbiased var); y = act(x·sc + sh
+ * [+ res]) (ReLU when relu or res).  gamma / beta NULL: no affine.  partial: chunks·2·c doubles.
+ * scflow_bn_backward: g = dy masked by y > 0 (y given: the residual form, dres = g) or by
+ * γ·x̂ + β > 0 (relu), dx = γ·rstd·(g − mean(g) − x̂·mean(g·x̂)), dγ (+)= Σ g·x̂, dβ (+)= Σ g
+ * (accumulate); mm: 2·c floats. */
+int scflow_bn_forward(const float* x, const float* gamma, const float* beta, const float* res,
+                      float* y, float* running_mean, float* running_var, float* rstd, float* shift,
+                      float* sc, float* sh, double* partial, long long m, int c, int chunks,
+                      float eps, float momentum, int relu, void* stream);
+int scflow_bn_backward(const float* dy, const float* x, const float* rstd, const float* shift,
+                       const float* gamma, const float* beta, const float* y, float* dx,
+                       float* dres, float* dgamma, float* dbeta, double* partial, float* mm,
+                       long long m, int c, int chunks, int relu, int accumulate, void* stream);
 /* scflow_gemm_f32: batched strided fp32 GEMM on the matrix cores (training-step contractions:
  * the correlation volume's backward, the 7x7 convs' dY^T.cols weight gradient, the pose head's
  * fully connected layers forward/backward; replaces torch.matmul / F.linear there,

@@ -168,6 +168,10 @@ SIGNATURES = {
                                             c_int, c_int, c_int, c_int, c_vp]),
     "scflow_in_backward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                                    c_int, c_int, c_vp]),
+    "scflow_bn_forward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, c_ll, c_int, c_int, c_float, c_float, c_int, c_vp]),
+    "scflow_bn_backward": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_vp]),
     "scflow_debug_lookup_stamps": (c_int, [c_vp]),
     "scflow_debug_conv_stamps": (c_int, [c_vp]),
     "scflow_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),

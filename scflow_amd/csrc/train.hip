@@ -980,7 +980,9 @@ __global__ __launch_bounds__(256) void in_bwd_stats_kernel(const float* __restri
                                                            const float* __restrict__ sh,
                                                            const float* __restrict__ ym, int hw,
                                                            int c, int chunks, int relu,
-                                                           double* __restrict__ partial) {
+                                                           double* __restrict__ partial,
+                                                           const float* __restrict__ gm = nullptr,
+                                                           const float* __restrict__ bt = nullptr) {
   __shared__ double red[2][256][4];
   const int img = blockIdx.y, ch = blockIdx.x;
   const int tpp = c / 4, ppp = 256 / tpp;
@@ -990,6 +992,11 @@ __global__ __launch_bounds__(256) void in_bwd_stats_kernel(const float* __restri
   if (ps < ppp) {
     const size_t so = (size_t)img * c + 4 * q;
     const floatx4 a = *(const floatx4*)(sc + so), b = *(const floatx4*)(sh + so);
+    floatx4 ga = {1.f, 1.f, 1.f, 1.f}, be = {0.f, 0.f, 0.f, 0.f};  // BatchNorm affine (mask only)
+    if (gm) {
+      ga = *(const floatx4*)(gm + 4 * q);
+      be = *(const floatx4*)(bt + 4 * q);
+    }
     const size_t base = (size_t)img * hw * c + 4 * q;
     for (int p = p_begin + ps; p < p_end; p += ppp) {
       const floatx4 g = *(const floatx4*)(dy + base + (size_t)p * c);
@@ -999,8 +1006,10 @@ __global__ __launch_bounds__(256) void in_bwd_stats_kernel(const float* __restri
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float xh = v[e] * a[e] + b[e];
-        // ReLU mask: of the block output y (residual form), else of x̂ itself
-        const float gg = ym ? (mk[e] > 0.f ? g[e] : 0.f) : (relu && !(xh > 0.f) ? 0.f : g[e]);
+        // ReLU mask: of the block output y (residual form), else of the pre-activation
+        // γ·x̂ + β (x̂ itself for InstanceNorm)
+        const float pre = gm ? ga[e] * xh + be[e] : xh;
+        const float gg = ym ? (mk[e] > 0.f ? g[e] : 0.f) : (relu && !(pre > 0.f) ? 0.f : g[e]);
         s[e] += (double)gg;
         s2[e] += (double)gg * (double)xh;
       }
@@ -1047,7 +1056,9 @@ __global__ void in_bwd_apply_kernel(const float* __restrict__ dy, const float* _
                                     const float* __restrict__ sc, const float* __restrict__ sh,
                                     const float* __restrict__ mm, const float* __restrict__ ym,
                                     float* __restrict__ dres, float* __restrict__ dx, int hw,
-                                    int c, int relu, long long total4) {
+                                    int c, int relu, long long total4,
+                                    const float* __restrict__ gm = nullptr,
+                                    const float* __restrict__ bt = nullptr) {
   const int c4 = c / 4;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
     const int cq = (int)(i % c4) * 4;
@@ -1059,17 +1070,76 @@ __global__ void in_bwd_apply_kernel(const float* __restrict__ dy, const float* _
     const floatx4 m2 = *(const floatx4*)(mm + (size_t)img * 2 * c + c + cq);
     floatx4 mk = {1.f, 1.f, 1.f, 1.f};
     if (ym) mk = ((const floatx4*)ym)[i];
+    floatx4 ga = {1.f, 1.f, 1.f, 1.f}, be = {0.f, 0.f, 0.f, 0.f};
+    if (gm) {
+      ga = *(const floatx4*)(gm + cq);
+      be = *(const floatx4*)(bt + cq);
+    }
     floatx4 r, gr;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = v[e] * a[e] + b[e];
-      const float gg = ym ? (mk[e] > 0.f ? g[e] : 0.f) : (relu && !(xh > 0.f) ? 0.f : g[e]);
+      const float pre = gm ? ga[e] * xh + be[e] : xh;
+      const float gg = ym ? (mk[e] > 0.f ? g[e] : 0.f) : (relu && !(pre > 0.f) ? 0.f : g[e]);
       gr[e] = gg;
-      r[e] = a[e] * (gg - m1[e] - xh * m2[e]);
+      r[e] = (gm ? ga[e] * a[e] : a[e]) * (gg - m1[e] - xh * m2[e]);
     }
     ((floatx4*)dx)[i] = r;
     if (dres) ((floatx4*)dres)[i] = gr;  // the identity branch's gradient (residual form)
   }
+}
+
+// BatchNorm2d in train mode (the context encoder's norms, resnet.py BasicBlock with BN): the
+// InstanceNorm kernels over ONE image of all n·h·w pixels give the batch statistics per channel;
+// these finalise them with the affine (γ, β) and the running-statistics update, and turn the
+// backward's fp64 sums into mean(g), mean(g·x̂) plus dγ = Σ g·x̂, dβ = Σ g.
+__global__ void bn_finalize_kernel(const double* __restrict__ partial, int chunks, int c,
+                                   long long m, float eps, const float* __restrict__ gm,
+                                   const float* __restrict__ bt, float momentum,
+                                   float* __restrict__ rmean, float* __restrict__ rvar,
+                                   float* __restrict__ sc, float* __restrict__ sh,
+                                   float* __restrict__ rstd_out, float* __restrict__ shift_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c) return;
+  double s = 0, s2 = 0;
+#pragma unroll 16
+  for (int k = 0; k < chunks; ++k) {
+    const double* o = partial + (size_t)k * 2 * c;
+    s += o[i];
+    s2 += o[c + i];
+  }
+  const double mean = s / (double)m;
+  double var = s2 / (double)m - mean * mean;
+  if (var < 0) var = 0;
+  const double rstd = 1.0 / sqrt(var + (double)eps);
+  rstd_out[i] = (float)rstd;
+  shift_out[i] = (float)(-mean * rstd);
+  const double g = gm ? (double)gm[i] : 1.0, b = bt ? (double)bt[i] : 0.0;
+  sc[i] = (float)(g * rstd);
+  sh[i] = (float)(b - g * mean * rstd);
+  if (rmean) {  // torch: running ← (1 − momentum)·running + momentum·batch (unbiased variance)
+    const double ub = m > 1 ? var * (double)m / (double)(m - 1) : var;
+    rmean[i] = (float)((1.0 - momentum) * (double)rmean[i] + momentum * mean);
+    rvar[i] = (float)((1.0 - momentum) * (double)rvar[i] + momentum * ub);
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ partial, int chunks, int c,
+                                       long long m, float* __restrict__ mm, float* __restrict__ dg,
+                                       float* __restrict__ db, int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c) return;
+  double s = 0, s2 = 0;
+#pragma unroll 16
+  for (int k = 0; k < chunks; ++k) {
+    const double* o = partial + (size_t)k * 2 * c;
+    s += o[i];
+    s2 += o[c + i];
+  }
+  mm[i] = (float)(s / (double)m);
+  mm[c + i] = (float)(s2 / (double)m);
+  if (dg) dg[i] = accumulate ? dg[i] + (float)s2 : (float)s2;
+  if (db) db[i] = accumulate ? db[i] + (float)s : (float)s;
 }
 
 // Column sums of a row-major [rows][ld] matrix (a conv's or linear layer's bias gradient,
@@ -2102,6 +2172,56 @@ SCFLOW_API int scflow_in_backward_residual(const float* dy, const float* x, cons
   const long long total4 = (long long)n * hw * c / 4;
   const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
   in_bwd_apply_kernel<<<blocks, 256, 0, st>>>(dy, x, scale, shift, mm, y, dres, dx, hw, c, 1, total4);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_bn_forward(const float* x, const float* gamma, const float* beta,
+                                 const float* res, float* y, float* running_mean,
+                                 float* running_var, float* rstd, float* shift, float* sc, float* sh,
+                                 double* partial, long long m, int c, int chunks, float eps,
+                                 float momentum, int relu, void* stream) {
+  if (!x || !y || !rstd || !shift || !sc || !sh || !partial || m <= 0 || c <= 0 || chunks <= 0 ||
+      (m / chunks) > INT32_MAX || m > INT32_MAX)
+    return SCFLOW_EINVAL;
+  if (c % 4 || c > 256 || (!gamma) != (!beta) || (!running_mean) != (!running_var))
+    return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(x) || !aligned16(y) || (res && !aligned16(res)) || !aligned16(sc) || !aligned16(sh))
+    return SCFLOW_EALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  // the batch statistics: the InstanceNorm statistics kernel over one image of m pixels
+  int rc = scflow_enc_stats(x, 1, (int)m, c, chunks, partial, stream);
+  if (rc != SCFLOW_OK) return rc;
+  bn_finalize_kernel<<<ceil_div(c, 256), 256, 0, st>>>(partial, chunks, c, m, eps, gamma, beta,
+                                                        momentum, running_mean, running_var, sc, sh,
+                                                        rstd, shift);
+  const long long total4 = m * c / 4;
+  const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
+  in_apply_kernel<<<blocks, 256, 0, st>>>(x, sc, sh, res, y, (int)m, c, (relu || res) ? 1 : 0, total4);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_bn_backward(const float* dy, const float* x, const float* rstd,
+                                  const float* shift, const float* gamma, const float* beta,
+                                  const float* y, float* dx, float* dres, float* dgamma,
+                                  float* dbeta, double* partial, float* mm, long long m, int c,
+                                  int chunks, int relu, int accumulate, void* stream) {
+  if (!dy || !x || !rstd || !shift || !dx || !partial || !mm || m <= 0 || c <= 0 || chunks <= 0 ||
+      m > INT32_MAX || (dres && !y))
+    return SCFLOW_EINVAL;
+  if (c % 4 || c > 256 || (!gamma) != (!beta)) return SCFLOW_EUNSUPPORTED;
+  if (!aligned16(dy) || !aligned16(x) || !aligned16(dx) || !aligned16(rstd) || !aligned16(shift) ||
+      !aligned16(mm) || (y && !aligned16(y)) || (dres && !aligned16(dres)) ||
+      (gamma && (!aligned16(gamma) || !aligned16(beta))))
+    return SCFLOW_EALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  in_bwd_stats_kernel<<<dim3(chunks, 1), 256, 0, st>>>(dy, x, rstd, shift, y, (int)m, c, chunks,
+                                                       relu ? 1 : 0, partial, gamma, beta);
+  bn_bwd_finalize_kernel<<<ceil_div(c, 256), 256, 0, st>>>(partial, chunks, c, m, mm, dgamma, dbeta,
+                                                            accumulate);
+  const long long total4 = m * c / 4;
+  const int blocks = (int)((total4 + 255) / 256 < 16384 ? (total4 + 255) / 256 : 16384);
+  in_bwd_apply_kernel<<<blocks, 256, 0, st>>>(dy, x, rstd, shift, mm, y, dres, dx, (int)m, c,
+                                              relu ? 1 : 0, total4, gamma, beta);
   return scflow_launch_status();
 }
 

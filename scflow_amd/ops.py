@@ -881,6 +881,46 @@ def in_backward(dy: Tensor, x: Tensor, scale: Tensor, shift: Tensor, dx: Tensor,
             _p(mm), n, hw, c, chunks, int(bool(relu)))
 
 
+def _bn_chunks(m: int) -> int:
+    return max(1, min(1024, m // 256))
+
+
+def bn_forward(x: Tensor, gamma: Optional[Tensor], beta: Optional[Tensor], y: Tensor,
+               running_mean: Optional[Tensor], running_var: Optional[Tensor], eps: float,
+               momentum: float, relu: bool, res: Optional[Tensor] = None
+               ) -> Tuple[Tensor, Tensor]:
+    """BatchNorm2d (train mode) of channels-last x [..., c] (+ReLU, + res before the ReLU) into y,
+    running statistics updated in place (scflow_bn_forward).  Returns (rstd, shift) per channel
+    (x̂ = x·rstd + shift) for the backward."""
+    c = x.shape[-1]
+    m = x.numel() // c
+    chunks = _bn_chunks(m)
+    dev = x.device
+    rstd, shift = torch.empty(c, device=dev), torch.empty(c, device=dev)
+    sc, sh = torch.empty(c, device=dev), torch.empty(c, device=dev)
+    partial = torch.empty(chunks * 2 * c, dtype=torch.float64, device=dev)
+    _launch("scflow_bn_forward", x, _p(x), _p(gamma), _p(beta), _p(res), _p(y), _p(running_mean),
+            _p(running_var), _p(rstd), _p(shift), _p(sc), _p(sh), _p(partial), m, c, chunks,
+            float(eps), float(momentum), int(bool(relu)))
+    return rstd, shift
+
+
+def bn_backward(dy: Tensor, x: Tensor, rstd: Tensor, shift: Tensor, gamma: Optional[Tensor],
+                beta: Optional[Tensor], dx: Tensor, dgamma: Optional[Tensor],
+                dbeta: Optional[Tensor], relu: bool, y: Optional[Tensor] = None,
+                dres: Optional[Tensor] = None, accumulate: bool = False) -> None:
+    """BatchNorm2d (train mode) backward (scflow_bn_backward); y / dres: the residual form (ReLU
+    mask from the block output, the identity's gradient written to dres)."""
+    c = x.shape[-1]
+    m = x.numel() // c
+    chunks = _bn_chunks(m)
+    partial = torch.empty(chunks * 2 * c, dtype=torch.float64, device=x.device)
+    mm = torch.empty(2 * c, device=x.device)
+    _launch("scflow_bn_backward", x, _p(dy), _p(x), _p(rstd), _p(shift), _p(gamma), _p(beta), _p(y),
+            _p(dx), _p(dres), _p(dgamma), _p(dbeta), _p(partial), _p(mm), m, c, chunks,
+            int(bool(relu)), int(bool(accumulate)))
+
+
 def colsum(x: Tensor, out: Tensor, accumulate: bool = False) -> Tensor:
     """out (+)= x.sum(0) of a 2-D row-major x with unit column stride (scflow_colsum)."""
     _require(out, "out")

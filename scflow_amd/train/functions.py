@@ -775,6 +775,78 @@ def instance_norm_residual_relu_nhwc(x: Tensor, res: Tensor, eps: float = 1e-5,
     return _InstanceNormResidualNHWC.apply(x, res, float(eps), res_grad)
 
 
+class _BatchNormNHWC(torch.autograd.Function):
+    """BatchNorm2d in train mode (+ ReLU, + a residual identity before the ReLU) of a
+    channels-last tensor: batch statistics in fp64, running statistics updated in the same
+    launch sequence, one apply pass (scflow_bn_forward); backward in three launches that also
+    give dγ / dβ (added straight into the parameters' gradients when they are direct sinks) and,
+    in the residual form, the identity's gradient (scflow_bn_backward) — instead of MIOpen's
+    batch norm on permuted views plus the ReLU, the add and their backwards as separate kernels
+    (the context encoder, resnet.py BasicBlock with norm_fn 'batch')."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, res, running_mean, running_var, momentum, eps, relu, res_grad):
+        x = x.contiguous()
+        res = None if res is None else res.contiguous()
+        y = torch.empty_like(x)
+        w = None if weight is None else weight.detach()
+        b = None if bias is None else bias.detach()
+        rstd, shift = ops.bn_forward(x, w, b, y, running_mean, running_var, eps, momentum, relu, res)
+        ctx.save_for_backward(x, rstd, shift, y if res is not None else None)
+        ctx.wb = (weight, bias)  # the leaves themselves (direct gradient accumulation)
+        ctx.relu, ctx.has_res, ctx.res_grad = relu, res is not None, res_grad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, rstd, shift, y = ctx.saved_tensors
+        weight, bias = ctx.wb
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        dw = db = None
+        want_w = weight is not None and ctx.needs_input_grad[1]
+        want_b = bias is not None and ctx.needs_input_grad[2]
+        sw = _grad_sink(weight) if want_w else None
+        sb = _grad_sink(bias) if want_b else None
+        direct = (sw is not None or not want_w) and (sb is not None or not want_b)
+        if direct:
+            gw, gb = sw, sb
+        else:
+            gw = torch.empty_like(weight) if want_w else None
+            gb = torch.empty_like(bias) if want_b else None
+        ops.bn_backward(dy.contiguous(), x, rstd, shift,
+                        None if weight is None else weight.detach(),
+                        None if bias is None else bias.detach(), dx, gw, gb, ctx.relu,
+                        y=y, dres=dres, accumulate=direct)
+        if not direct:
+            dw, db = gw, gb
+        if dres is not None and ctx.res_grad is not None:  # handed to the block's first conv
+            ctx.res_grad.d = dres
+            dres = None
+        return dx, dw, db, dres, None, None, None, None, None, None
+
+
+def batch_norm_nhwc(x: Tensor, mod, relu: bool = False, res: Optional[Tensor] = None,
+                    res_grad: Optional[ResidualGrad] = None) -> Tensor:
+    """``mod`` (BatchNorm2d, train mode, float momentum) of channels-last x, then + res and ReLU
+    (res given: relu(bn(x) + res), the residual block's tail) — HIP forward and backward, the
+    running statistics and num_batches_tracked updated as F.batch_norm(training=True) does."""
+    y = _BatchNormNHWC.apply(x, mod.weight, mod.bias, res, mod.running_mean, mod.running_var,
+                             float(mod.momentum), float(mod.eps), bool(relu or res is not None),
+                             res_grad)
+    if mod.num_batches_tracked is not None:
+        mod.num_batches_tracked.add_(1)
+    return y
+
+
+def bn_fusable(mod, x: Tensor) -> bool:
+    """BatchNorm2d modules batch_norm_nhwc takes: train mode with running statistics and a float
+    momentum (SCFlow's context encoder), channels a multiple of 4, at most 256, on the GPU."""
+    return (isinstance(mod, torch.nn.BatchNorm2d) and mod.training and mod.track_running_stats
+            and mod.momentum is not None and x.is_cuda and x.shape[-1] % 4 == 0
+            and x.shape[-1] <= 256 and (mod.weight is None) == (mod.bias is None))
+
+
 def instance_norm_nhwc(x: Tensor, eps: float = 1e-5, relu: bool = False) -> Tensor:
     """InstanceNorm2d(affine=False) (then ReLU if ``relu``) of channels-last x, HIP fwd + bwd
     (channels a multiple of 4, at most 256)."""

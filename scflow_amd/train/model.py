@@ -21,8 +21,8 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import Chan
-from .functions import (ResidualGrad, begin_forward, conv2d_nhwc, conv2d_nhwc_split, corr_lookup,
-                        corr_pyramid,
+from .functions import (ResidualGrad, batch_norm_nhwc, begin_forward, bn_fusable, conv2d_nhwc,
+                        conv2d_nhwc_split, corr_lookup, corr_pyramid,
                         group_norm_nhwc, gru_step, instance_norm_nhwc,
                         instance_norm_residual_relu_nhwc, linear, pose_update6, share_weight,
                         upsample_bilinear_ac)
@@ -33,6 +33,7 @@ _GRU_FUSED = os.environ.get("SCFLOW_TRAIN_GRU_FUSED", "1") != "0"  # A/B switch 
 _FUSED_LOSS = os.environ.get("SCFLOW_TRAIN_FUSED_LOSS", "1") != "0"  # A/B switch (tuning)
 _GN_FUSED = os.environ.get("SCFLOW_TRAIN_GN_FUSED", "1") != "0"  # A/B switch (tuning)
 _RES_GRAD = os.environ.get("SCFLOW_TRAIN_RES_GRAD", "1") != "0"  # A/B switch (tuning)
+_BN_FUSED = os.environ.get("SCFLOW_TRAIN_BN_FUSED", "1") != "0"  # A/B switch (tuning)
 
 
 def _act(x: Tensor, act) -> Tensor:
@@ -70,6 +71,8 @@ def _norm(x: Tensor, mod, relu: bool = False) -> Tensor:
         v = x.var(dim=(1, 2), unbiased=False, keepdim=True)
         y = (x - m) / torch.sqrt(v + mod.eps)
         return torch.relu(y) if relu else y
+    if _BN_FUSED and bn_fusable(mod, x):
+        return batch_norm_nhwc(x, mod, relu)
     y = F.batch_norm(x.permute(0, 3, 1, 2), mod.running_mean, mod.running_var, mod.weight, mod.bias,
                      training=mod.training, momentum=mod.momentum, eps=mod.eps)
     if mod.training and mod.num_batches_tracked is not None:
@@ -84,8 +87,10 @@ def encoder_train(enc, x_nhwc: Tensor) -> Tensor:
     for name in enc.res_layers:
         for blk in getattr(enc, name):
             n2 = blk.norm2
-            fused_tail = (isinstance(n2, torch.nn.InstanceNorm2d) and not n2.affine and x.is_cuda
-                          and x.shape[-1] % 4 == 0 and x.shape[-1] <= 256)
+            in_tail = (isinstance(n2, torch.nn.InstanceNorm2d) and not n2.affine and x.is_cuda
+                       and x.shape[-1] % 4 == 0 and x.shape[-1] <= 256)
+            bn_tail = _BN_FUSED and bn_fusable(n2, x)
+            fused_tail = in_tail or bn_tail
             # identity block: its input's two gradients (conv1's dX, the identity) summed in
             # conv1's dX epilogue (ResidualGrad)
             rg = ResidualGrad() if (fused_tail and blk.downsample is None and _RES_GRAD and
@@ -94,7 +99,10 @@ def encoder_train(enc, x_nhwc: Tensor) -> Tensor:
             ident = x if blk.downsample is None else _norm(_conv(x, blk.downsample[0]), blk.downsample[1])
             y2 = _conv(out, blk.conv2)
             if fused_tail and y2.shape[-1] % 4 == 0 and y2.shape[-1] <= 256 and ident.shape == y2.shape:
-                x = instance_norm_residual_relu_nhwc(y2, ident, n2.eps, rg)  # norm + sum + ReLU
+                if in_tail:
+                    x = instance_norm_residual_relu_nhwc(y2, ident, n2.eps, rg)  # norm + sum + ReLU
+                else:
+                    x = batch_norm_nhwc(y2, n2, res=ident, res_grad=rg)
             else:
                 x = torch.relu(_norm(y2, n2) + ident)
     return _conv(x, enc.conv2)

@@ -523,6 +523,52 @@ def test_instance_norm_nhwc_forward_backward(n, h, w, c, relu):
     _close(xg.grad, xr.grad, 1e-4, 1e-5, "instance norm input gradient")
 
 
+@pytest.mark.parametrize("n,h,w,c,mode", [(4, 64, 64, 64, "relu"), (3, 32, 32, 96, "plain"),
+                                          (2, 16, 16, 128, "res"), (16, 32, 32, 64, "res"),
+                                          (2, 8, 12, 4, "relu")])
+def test_batch_norm_nhwc_train(n, h, w, c, mode):
+    """HIP BatchNorm2d in train mode (the context encoder's norms; + ReLU, or + a residual before
+    the ReLU): output, running statistics and the gradients of x, γ, β (and the residual) against
+    fp64 autograd of F.batch_norm(training=True) on the same channels-last data."""
+    from scflow_amd.train.functions import batch_norm_nhwc
+    g = torch.Generator().manual_seed(41 + c)
+    x = torch.randn(n, h, w, c, generator=g) * 1.5 + 0.3
+    r = torch.randn(n, h, w, c, generator=g)
+    dy = torch.randn(n, h, w, c, generator=g)
+    bn = torch.nn.BatchNorm2d(c, momentum=0.1, eps=1e-5)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(c, generator=g) * 0.2)
+        bn.running_mean.copy_(torch.randn(c, generator=g) * 0.1)
+        bn.running_var.copy_(torch.rand(c, generator=g) + 0.5)
+    ref = torch.nn.BatchNorm2d(c, momentum=0.1, eps=1e-5).double()
+    ref.load_state_dict(bn.state_dict())
+    xr = x.double().requires_grad_(True)
+    rr = r.double().requires_grad_(True)
+    yr = ref(xr.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    if mode == "res":
+        yr = yr + rr
+    if mode != "plain":
+        yr = torch.relu(yr)
+    (yr * dy.double()).sum().backward()
+    mod = bn.cuda().train()
+    xg = x.cuda().requires_grad_(True)
+    rg = r.cuda().requires_grad_(True)
+    y = batch_norm_nhwc(xg, mod, relu=mode == "relu", res=rg if mode == "res" else None)
+    (y * dy.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    _close(y, yr, 1e-5, 1e-5, "batch norm forward")
+    _close(mod.running_mean, ref.running_mean, 1e-5, 1e-6, "running mean")
+    _close(mod.running_var, ref.running_var, 1e-5, 1e-6, "running var")
+    assert int(mod.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+    m = n * h * w
+    _close(xg.grad, xr.grad, 1e-4, 1e-5, "batch norm input gradient")
+    _close(mod.weight.grad, ref.weight.grad, 1e-5, 1e-6 * m ** 0.5, "dγ")
+    _close(mod.bias.grad, ref.bias.grad, 1e-5, 1e-6 * m ** 0.5, "dβ")
+    if mode == "res":
+        _close(rg.grad, rr.grad, 1e-6, 1e-6, "residual gradient")
+
+
 @pytest.mark.parametrize("n,h,w,c", [(4, 64, 64, 64), (3, 32, 32, 96), (2, 16, 16, 128)])
 def test_instance_norm_residual_relu(n, h, w, c):
     """relu(InstanceNorm2d(x) + res) — the encoder residual block's tail in one HIP pass each way:
