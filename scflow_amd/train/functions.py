@@ -158,6 +158,47 @@ def _act_backward(dy: Tensor, y: Tensor, act: Optional[str]) -> Tensor:
     raise ValueError(act)
 
 
+def _chan_view(t: Tensor) -> Optional[Chan]:
+    """``t`` [..., c] as a Chan when it is a channel slice [off, off + c) of a contiguous
+    channels-last buffer (its ``_base``), else None."""
+    b = t._base
+    if b is None or not b.is_contiguous() or t.stride(-1) != 1 or b.dtype != t.dtype:
+        return None
+    C = b.shape[-1]
+    if b.numel() // C != t.numel() // t.shape[-1]:
+        return None
+    expect = C
+    for i in range(t.dim() - 2, -1, -1):  # pixel dims packed at stride C
+        if t.shape[i] != 1 and t.stride(i) != expect:
+            return None
+        expect *= t.shape[i]
+    off = t.storage_offset() - b.storage_offset()
+    if off < 0 or off + t.shape[-1] > C:
+        return None
+    return Chan(b.view(-1, C), off, t.shape[-1])
+
+
+def _chan(t: Tensor) -> Chan:
+    """The Chan a conv kernel reads ``t`` (contiguous, or a channel slice read in place) through."""
+    if t.is_contiguous():
+        return Chan.whole(t.view(-1, t.shape[-1]))
+    c = _chan_view(t)
+    if c is None:
+        raise ValueError("conv source: contiguous or a channel slice of a channels-last buffer")
+    return c
+
+
+def _chan_or_contiguous(t: Tensor) -> Tensor:
+    return t if t.is_contiguous() or _chan_view(t) is not None else t.contiguous()
+
+
+def _src(t: Optional[Tensor]):
+    """A weight-gradient source: the tensor itself when contiguous, its Chan when a slice."""
+    if t is None or t.is_contiguous():
+        return t
+    return _chan(t)
+
+
 def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tensor], stride: int,
                   pad: Tuple[int, int], act: Optional[str] = None,
                   bias_map: Optional[Tensor] = None, wkey: Optional[Tensor] = None) -> Tensor:
@@ -185,9 +226,9 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
         try:
             packed = _cached(wkey, ("conv", c0, c1, wd, bk),
                              lambda: ops.pack_conv_weight(w.float(), c0, c1, wd, 1, bk))
-            ops.conv2d(Chan.whole(x0.view(-1, c0)), packed, b, n, h, wd, cout, kh, kw, ph, pw, act,
+            ops.conv2d(_chan(x0), packed, b, n, h, wd, cout, kh, kw, ph, pw, act,
                        out=Chan.whole(out.view(-1, cout)), bk=bk,
-                       src1=None if x1 is None else Chan.whole(x1.view(-1, c1)),
+                       src1=None if x1 is None else _chan(x1),
                        bias_map=None if bias_map is None else Chan.whole(bias_map.reshape(-1, cout)))
             return out
         except ScflowError:
@@ -197,10 +238,10 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
             and stride in (1, 2)):
         try:
             fuse = bias_map is None
-            ops.enc_conv(Chan.whole(x0.view(-1, c0)), _cached(wkey, ("enc",), lambda: ops.enc_conv_pack(w)),
+            ops.enc_conv(_chan(x0), _cached(wkey, ("enc",), lambda: ops.enc_conv_pack(w)),
                          b, n, h, wd, c0, cout, kh,
                          stride, ph, out, act=act if fuse else None,
-                         src1=None if x1 is None else Chan.whole(x1.view(-1, c1)))
+                         src1=None if x1 is None else _chan(x1))
             post = not fuse
             x0 = None
         except ScflowError:
@@ -245,7 +286,7 @@ def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int,
     if g.shape[-1] != cout:  # output channels zero-padded to a multiple of 4 (see _conv_backward)
         dwp = torch.empty(g.shape[-1], cin, kh, kw, device=g.device)
         dbp = torch.empty(g.shape[-1], device=g.device) if with_bias else None
-        ops.conv_wgrad(g2, x0, x1, dwp, dbp, n, h, wd, kh, kw, s, ph, pw)
+        ops.conv_wgrad(g2, _src(x0), _src(x1), dwp, dbp, n, h, wd, kh, kw, s, ph, pw)
         if accumulate:
             dw += dwp[:cout]
             if with_bias:
@@ -253,7 +294,8 @@ def _weight_grad(g: Tensor, x0: Tensor, x1: Optional[Tensor], w: Tensor, s: int,
             return dw, db
         return dwp[:cout], (dbp[:cout] if with_bias else None)
     try:
-        ops.conv_wgrad(g2, x0, x1, dw, db, n, h, wd, kh, kw, s, ph, pw, accumulate=accumulate)
+        ops.conv_wgrad(g2, _src(x0), _src(x1), dw, db, n, h, wd, kh, kw, s, ph, pw,
+                       accumulate=accumulate)
         return dw, db
     except ScflowError:
         pass
@@ -338,8 +380,8 @@ def _flush_wgrad_same(items, w: Tensor, with_bias: bool, dw: Tensor, db: Optiona
         for i in range(0, len(items), 8):
             part = items[i:i + 8]
             ops.conv_wgrad_batched([g.reshape(-1, g.shape[-1]) for g, _, _ in part],
-                                   [x0 for _, x0, _ in part],
-                                   None if x10 is None else [x1 for _, _, x1 in part],
+                                   [_src(x0) for _, x0, _ in part],
+                                   None if x10 is None else [_src(x1) for _, _, x1 in part],
                                    tw, tb, n, h, wd, kh, kw, s, ph, pw,
                                    accumulate=(accumulate and not padded) or i > 0)
     except ScflowError:  # shapes outside the batched kernels: one launch per use
@@ -439,8 +481,8 @@ class ResidualGrad:
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act, res_grad=None):
-        x0 = x0.contiguous()
-        x1 = None if x1 is None else x1.contiguous()
+        x0 = _chan_or_contiguous(x0)  # channel slices of a wider buffer are read in place
+        x1 = None if x1 is None else _chan_or_contiguous(x1)
         y = _conv_forward(x0, x1, w.detach().contiguous(), None if b is None else b.detach().contiguous(),
                           stride, (ph, pw), act, None if bias_map is None else bias_map.detach().contiguous(),
                           wkey=w)
@@ -541,6 +583,94 @@ def _conv_backward(ctx, dy):
         else:
             dw, db = _weight_grad(gp, x0, x1, w, s, ph, pw, want_b)
     return dx0, dx1, dw, db, dbm, None, None, None, None
+
+
+class _DualConv2dNHWC(torch.autograd.Function):
+    """Two convs of the same input with the same kernel shape (the XHeads' hidden convs,
+    flow_pred.layers[0] and mask_pred.layers[0] on h, raft_decoder.py XHead) as one launch each
+    way: the forward on the two weights stacked along cout (cached per weight version) returns
+    channel views of one output buffer (the predictors read them in place); the backward runs ONE
+    dX conv over both output gradients — the input's two gradients summed by the GEMM instead of
+    two launches and an autograd add — and one batched weight gradient over the pass's uses,
+    split into the two parameters' gradient sinks."""
+
+    @staticmethod
+    def forward(ctx, x, wa, ba, wb, bb, ph, pw, act):
+        x = _chan_or_contiguous(x)
+        ca = wa.shape[0]
+        wcat = _cached(wa, ("dual_w", id(wb), wb._version),
+                       lambda: torch.cat([wa.detach(), wb.detach()], 0).contiguous())
+        bcat = None
+        if ba is not None:
+            bcat = _cached(wa, ("dual_b", id(ba), ba._version, id(bb), bb._version),
+                           lambda: torch.cat([ba.detach(), bb.detach()], 0).contiguous())
+        y = _conv_forward(x, None, wcat, bcat, 1, (ph, pw), act, wkey=wcat)
+        ctx.save_for_backward(x, y if act is not None else None)
+        ctx.wcat, ctx.params = wcat, (wa, ba, wb, bb)
+        ctx.pad, ctx.act, ctx.ca = (ph, pw), act, ca
+        ctx.uses = _use_holder(wa) if wa.requires_grad else None
+        return y[..., :ca], y[..., ca:]
+
+    @staticmethod
+    def backward(ctx, da, db_):
+        x, y = ctx.saved_tensors
+        wa, ba, wb, bb = ctx.params
+        wcat = ctx.wcat
+        ph, pw = ctx.pad
+        ca = ctx.ca
+        ref = da if da is not None else db_
+        shape = list(ref.shape)
+        parts = []
+        for g, c in ((da, ca), (db_, wcat.shape[0] - ca)):
+            shape[-1] = c
+            parts.append(g if g is not None else torch.zeros(shape, device=ref.device))
+        g = _act_backward(torch.cat(parts, -1), y, ctx.act).contiguous()
+        _, cin, kh, kw = wcat.shape
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_forward(g, None, _flip_t(wcat), None, 1, (kh - 1 - ph, kw - 1 - pw))
+        sinks = [_grad_sink(t) if t is not None and t.requires_grad else None for t in ctx.params]
+        want = [t is not None and t.requires_grad for t in ctx.params]
+        direct = all(s_ is not None or not w_ for s_, w_ in zip(sinks, want))
+        with_bias = ba is not None
+        hold = ctx.uses
+
+        def flush(items, into_sinks=True):
+            tw = torch.empty_like(wcat)
+            tb = torch.empty(wcat.shape[0], device=wcat.device) if with_bias else None
+            _flush_wgrad(items, wcat, with_bias, tw, tb, False, 1, ph, pw)
+            return tw, tb
+
+        if direct and hold is not None and hold["uses"] > 1:
+            def flush_sinks(items):
+                tw, tb = flush(items)
+                sw_a, sb_a, sw_b, sb_b = sinks
+                if sw_a is not None:
+                    sw_a += tw[:ca]
+                if sw_b is not None:
+                    sw_b += tw[ca:]
+                if with_bias and sb_a is not None:
+                    sb_a += tb[:ca]
+                if with_bias and sb_b is not None:
+                    sb_b += tb[ca:]
+            _defer(hold, (g, x, None), flush_sinks)
+            return dx, None, None, None, None, None, None, None
+        tw, tb = flush([(g, x, None)])
+        grads = [tw[:ca], tb[:ca] if with_bias else None, tw[ca:], tb[ca:] if with_bias else None]
+        if direct:
+            for s_, gr in zip(sinks, grads):
+                if s_ is not None and gr is not None:
+                    s_ += gr
+            grads = [None] * 4
+        return (dx, *grads, None, None, None)
+
+
+def dual_conv2d_nhwc(x: Tensor, wa: Tensor, ba: Optional[Tensor], wb: Tensor, bb: Optional[Tensor],
+                     padding=0, act: Optional[str] = None) -> Tuple[Tensor, Tensor]:
+    """(act(conv(x; wa, ba)), act(conv(x; wb, bb))) of channels-last x as one conv each way
+    (stride 1, same kernel shape and padding): channel views of one output buffer."""
+    ph, pw = (padding, padding) if isinstance(padding, int) else padding
+    return _DualConv2dNHWC.apply(x, wa, ba, wb, bb, ph, pw, act)
 
 
 def conv2d_nhwc_split(x: Tensor, weight: Tensor, split: int, bias: Optional[Tensor] = None,

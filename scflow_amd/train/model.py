@@ -22,7 +22,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import Chan
 from .functions import (ResidualGrad, batch_norm_nhwc, begin_forward, bn_fusable, conv2d_nhwc,
-                        conv2d_nhwc_split, corr_lookup, corr_pyramid,
+                        conv2d_nhwc_split, corr_lookup, corr_pyramid, dual_conv2d_nhwc,
                         group_norm_nhwc, gru_step, instance_norm_nhwc,
                         instance_norm_residual_relu_nhwc, linear, pose_update6, share_weight,
                         upsample_bilinear_ac)
@@ -34,6 +34,7 @@ _FUSED_LOSS = os.environ.get("SCFLOW_TRAIN_FUSED_LOSS", "1") != "0"  # A/B switc
 _GN_FUSED = os.environ.get("SCFLOW_TRAIN_GN_FUSED", "1") != "0"  # A/B switch (tuning)
 _RES_GRAD = os.environ.get("SCFLOW_TRAIN_RES_GRAD", "1") != "0"  # A/B switch (tuning)
 _BN_FUSED = os.environ.get("SCFLOW_TRAIN_BN_FUSED", "1") != "0"  # A/B switch (tuning)
+_HEADS_FUSED = os.environ.get("SCFLOW_TRAIN_HEADS_FUSED", "1") != "0"  # A/B switch (tuning)
 
 
 def _act(x: Tensor, act) -> Tensor:
@@ -208,6 +209,12 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
         if _GRU_FUSED:  # one batched weight gradient over the 8 iterations' uses
             w_zr, w_q = share_weight(w_zr), share_weight(w_q)
         it_w.append((w_zr, w_q, q.padding))
+    fl, ml = dec.flow_pred.layers, dec.mask_pred.layers
+    heads_fused = (_HEADS_FUSED and len(fl) == 1 and len(ml) == 1 and h.is_cuda
+                   and fl[0].conv.kernel_size == ml[0].conv.kernel_size
+                   and fl[0].conv.padding == ml[0].conv.padding and fl[0].conv.stride == (1, 1)
+                   and ml[0].conv.stride == (1, 1) and fl[0].act_type == ml[0].act_type
+                   and (fl[0].conv.bias is None) == (ml[0].conv.bias is None))
     for _ in range(iters):
         with torch.no_grad():  # flow is detached every iteration (detach_flow=True)
             f2 = torch.empty(N * hh * ww, 2, device=depth.device, dtype=dt)
@@ -232,13 +239,18 @@ def decoder_train(dec, feat_render: Tensor, feat_real: Tensor, h: Tensor, cxt: T
                                           bias_map=pre_zr)
                 qq = conv2d_nhwc(rg * h, w_q, None, 1, pad, act="Tanh", x1=motion, bias_map=pre_q)
                 h = torch.lerp(h, qq, z)
-        fh = h
-        for m in dec.flow_pred.layers:
-            fh = _cm(fh, m)
+        fl, ml = dec.flow_pred.layers, dec.mask_pred.layers
+        if heads_fused:  # both XHeads' hidden convs as one launch each way
+            fh, mh = dual_conv2d_nhwc(h, fl[0].conv.weight, fl[0].conv.bias, ml[0].conv.weight,
+                                      ml[0].conv.bias, fl[0].conv.padding, fl[0].act_type)
+        else:
+            fh = h
+            for m in fl:
+                fh = _cm(fh, m)
+            mh = h
+            for m in ml:
+                mh = _cm(mh, m)
         dflow = _conv(fh, dec.flow_pred.predict_layer)
-        mh = h
-        for m in dec.mask_pred.layers:
-            mh = _cm(mh, m)
         pl = dec.mask_pred.predict_layer
         mask = conv2d_nhwc(mh, pl.weight, pl.bias, 1, pl.padding, act="Sigmoid")
         dff = dflow

@@ -102,6 +102,57 @@ def test_conv2d_nhwc_fused_act_two_sources_bias_map(act, two, bmap):
             _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), name)
 
 
+def test_dual_conv_heads_and_channel_slice_consumers():
+    """dual_conv2d_nhwc (the XHeads' hidden convs as one launch each way) and convs reading its
+    channel-view outputs in place (the predictors): values and every gradient — x, both weight /
+    bias pairs, the predictors' weights — against fp64 autograd of the separate convs, over
+    three uses of the same weights (the batched weight gradient across uses)."""
+    from scflow_amd.train.functions import conv2d_nhwc, direct_weight_grads, dual_conv2d_nhwc
+    g = torch.Generator().manual_seed(17)
+    n, h, w, cin, ch = 2, 32, 32, 128, 256
+    mk = lambda *s_, sc=1.0: (torch.randn(*s_, generator=g) * sc)
+    wa, ba = mk(ch, cin, 3, 3, sc=cin ** -0.5 / 3), mk(ch, sc=0.1)
+    wb, bb = mk(ch, cin, 3, 3, sc=cin ** -0.5 / 3), mk(ch, sc=0.1)
+    wf, bf = mk(2, ch, 3, 3, sc=ch ** -0.5 / 3), mk(2, sc=0.1)
+    wm, bm = mk(1, ch, 1, 1, sc=ch ** -0.5), mk(1, sc=0.1)
+    xs = [mk(n, h, w, cin) for _ in range(3)]
+    gys = [(mk(n, h, w, 2), mk(n, h, w, 1)) for _ in range(3)]
+    leaves = [t.double().requires_grad_() for t in (wa, ba, wb, bb, wf, bf, wm, bm)]
+    xr = [x.double().requires_grad_() for x in xs]
+    tot = 0
+    for x, (gf, gm) in zip(xr, gys):
+        xc = x.permute(0, 3, 1, 2)
+        fa = torch.relu(F.conv2d(xc, leaves[0], leaves[1], padding=1))
+        fb = torch.relu(F.conv2d(xc, leaves[2], leaves[3], padding=1))
+        of = F.conv2d(fa, leaves[4], leaves[5], padding=1).permute(0, 2, 3, 1)
+        om = torch.sigmoid(F.conv2d(fb, leaves[6], leaves[7])).permute(0, 2, 3, 1)
+        tot = tot + (of * gf.double()).sum() + (om * gm.double()).sum()
+    tot.backward()
+    dev = [t.cuda().requires_grad_() for t in (wa, ba, wb, bb, wf, bf, wm, bm)]
+    for t in dev:
+        t.grad = torch.zeros_like(t)
+    xg = [x.cuda().requires_grad_() for x in xs]
+    outs = []
+    with direct_weight_grads():
+        from scflow_amd.train.functions import begin_forward
+        begin_forward()
+        tot = 0
+        for x, (gf, gm) in zip(xg, gys):
+            fa, fb = dual_conv2d_nhwc(x, dev[0], dev[1], dev[2], dev[3], 1, "ReLU")
+            of = conv2d_nhwc(fa, dev[4], dev[5], 1, 1)
+            om = conv2d_nhwc(fb, dev[6], dev[7], 1, 0, act="Sigmoid")
+            outs.append(of)
+            tot = tot + (of * gf.cuda()).sum() + (om * gm.cuda()).sum()
+        tot.backward()
+    torch.cuda.synchronize()
+    K = cin * 9
+    for i in range(3):
+        assert xg[i].grad is not None
+        _close(xg[i].grad, xr[i].grad, 1e-5, 1e-4 * np.sqrt(K), f"dx[{i}]")
+    for name, a, r in zip(("wa", "ba", "wb", "bb", "wf", "bf", "wm", "bm"), dev, leaves):
+        _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(3 * n * h * w), name)
+
+
 def test_conv_wgrad_accumulate_and_split():
     """scflow_conv_wgrad directly: a Chan slice as the second source, accumulate = 1 adds onto
     dw / db, and a batch large enough to split the pixel reduction over many workgroups."""
