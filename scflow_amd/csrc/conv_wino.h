@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
       hlds[part][j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 7) : -1;
     }
   const int hq4 = 4 * (tid & 7);  // channel of this thread's quad within the stage (idx & 7 = tid & 7)
-  floatx4 ra[NA];
+  floatx4 ra[2][NA];  // two quarters in flight (the K split loads two before storing them)
   // stage s's source, as a buffer starting at its first channel
   __amdgpu_buffer_rsrc_t hsrc;
   int hss4 = 0, hlim = 0;  // pixel stride in bytes, channels of the stage present in the source
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e] * isc[e] + ish[e], 0.f);
       }
-      ra[j] = v;
+      ra[part & 1][j] = v;
     }
   };
   auto hstore = [&](int buf, int part) {
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
 #endif
 #pragma unroll
     for (int j = 0; j < NA; ++j)
-      if (G::NH4 % (4 * NT) == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[j];
+      if (G::NH4 % (4 * NT) == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[part & 1][j];
   };
 
   // transformed weights [nb32][sub-step (8 channels)][ξ 16][lane 64][4]; this wave's points are
