@@ -159,23 +159,32 @@ def _act_backward(dy: Tensor, y: Tensor, act: Optional[str]) -> Tensor:
 
 
 def _chan_view(t: Tensor) -> Optional[Chan]:
-    """``t`` [..., c] as a Chan when it is a channel slice [off, off + c) of a contiguous
-    channels-last buffer (its ``_base``), else None."""
+    """``t`` [..., c] as a Chan when it is a channel slice [off, off + c) of a channels-last
+    buffer with rows of C ≥ c floats (pixel dims packed at stride C; a view whose ``_base`` gives
+    the row origin), else None."""
     b = t._base
-    if b is None or not b.is_contiguous() or t.stride(-1) != 1 or b.dtype != t.dtype:
+    if b is None or not b.is_contiguous() or t.dim() < 2 or t.stride(-1) != 1:
         return None
-    C = b.shape[-1]
-    if b.numel() // C != t.numel() // t.shape[-1]:
-        return None
-    expect = C
+    c = t.shape[-1]
+    C = expect = None
     for i in range(t.dim() - 2, -1, -1):  # pixel dims packed at stride C
-        if t.shape[i] != 1 and t.stride(i) != expect:
+        if t.shape[i] == 1:
+            continue
+        if C is None:
+            C = expect = t.stride(i)
+        elif t.stride(i) != expect:
             return None
         expect *= t.shape[i]
-    off = t.storage_offset() - b.storage_offset()
-    if off < 0 or off + t.shape[-1] > C:
+    if C is None:
+        C = c
+    off = (t.storage_offset() - b.storage_offset()) % C
+    if C < c or off + c > C:
         return None
-    return Chan(b.view(-1, C), off, t.shape[-1])
+    m = t.numel() // c
+    p0 = t.storage_offset() - off
+    if p0 < 0 or (p0 + m * C) * t.element_size() > t.untyped_storage().nbytes():
+        return None
+    return Chan(torch.as_strided(t, (m, C), (C, 1), p0), off, c)
 
 
 def _chan(t: Tensor) -> Chan:

@@ -169,3 +169,26 @@ def test_upsample_adjoint_matches_autograd(monkeypatch):
         (y * gy.float()).sum().backward()
         assert torch.allclose(y.double(), yr.detach(), atol=1e-5)
         assert torch.allclose(xg.grad.double(), xr.grad, rtol=1e-5, atol=1e-4)
+
+
+def test_channel_slice_views_are_read_in_place():
+    """The training convs read a channel slice of a wider channels-last buffer in place
+    (functions._chan_view: the XHeads' dual conv output feeding the predictors): slices map to
+    (buffer, channel offset, channels); anything that is not a packed channel slice — a pixel
+    sub-range, a transposed view, a slice of a non-contiguous tensor — is refused (copied)."""
+    import torch
+    from scflow_amd.train.functions import _chan, _chan_or_contiguous, _chan_view
+    buf = torch.arange(2 * 4 * 4 * 12, dtype=torch.float32).view(2, 4, 4, 12)
+    a, b = buf[..., :5], buf[..., 5:]
+    ca, cb = _chan_view(a), _chan_view(b)
+    assert (ca.off, ca.c, ca.stride) == (0, 5, 12) and (cb.off, cb.c, cb.stride) == (5, 7, 12)
+    assert ca.buf.data_ptr() == buf.data_ptr() and ca.buf.shape == (32, 12)
+    # the kernel's view of the slice: rows of `stride` floats from ptr, `c` of them used
+    flat = ca.buf.view(-1)
+    rows = torch.stack([flat[r * 12 + cb.off: r * 12 + cb.off + cb.c] for r in range(32)])
+    assert torch.equal(rows.view(2, 4, 4, 7), b)
+    assert _chan_or_contiguous(b) is b
+    assert _chan(buf).c == 12 and _chan(buf).off == 0
+    for bad in (buf[:, 1:3, :, :5], buf.transpose(1, 2)[..., :5], buf[..., ::2]):
+        assert _chan_view(bad) is None
+        assert _chan_or_contiguous(bad).is_contiguous()
