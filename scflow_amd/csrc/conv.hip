@@ -1006,6 +1006,7 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
       !aligned16(a.weight))
     return SCFLOW_EALIGN;
   if (a.kh != 3) {
+    if (a.epilogue == SCFLOW_EPI_RELU_MASK) return SCFLOW_EUNSUPPORTED;
     Wino5Params p;
     p.a = a;
     p.cp0 = round_up(a.c0, W5SC);
@@ -1289,6 +1290,9 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     if (!a.gate || !a.rh || !a.hid || (a.cout & 1)) return SCFLOW_EINVAL;
   } else if (a.epilogue == SCFLOW_EPI_GRU_Q) {
     if (!a.gate || !a.hid) return SCFLOW_EINVAL;
+  } else if (a.epilogue == SCFLOW_EPI_RELU_MASK) {
+    if (!a.out || !a.gate) return SCFLOW_EINVAL;
+    if (a.bk != SCFLOW_CONV_WINO || a.kh != 3 || a.kw != 3) return SCFLOW_EUNSUPPORTED;
   } else {
     return SCFLOW_EINVAL;
   }

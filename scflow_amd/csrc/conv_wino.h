@@ -508,8 +508,16 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
   #pragma unroll
       for (int q = 0; q < NPX; ++q) val[q] += a.res[pix[q] * a.sres + col];
     }
+    if (a.epilogue == SCFLOW_EPI_RELU_MASK) {  // the input ReLU's backward: zero where gate ≤ 0
+      float gv[NPX];
   #pragma unroll
-    for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q], a.act);
+      for (int q = 0; q < NPX; ++q) gv[q] = a.gate[pix[q] * a.sg + col];
+  #pragma unroll
+      for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = gv[q] > 0.f ? act_apply(val[q], a.act) : 0.f;
+    } else {
+  #pragma unroll
+      for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q], a.act);
+    }
 
   } else {
     // BNW does not divide the 256 threads: (output position, channel) pairs dealt round robin,
@@ -548,8 +556,13 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
 #pragma unroll
           for (int e = 0; e < 4; ++e) val[e] += a.res[pix[e] * a.sres + col];
         }
+        float gv[4] = {1.f, 1.f, 1.f, 1.f};
+        if (a.epilogue == SCFLOW_EPI_RELU_MASK) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) a.out[pix[e] * a.so + col] = act_apply(val[e], a.act);
+          for (int e = 0; e < 4; ++e) gv[e] = a.gate[pix[e] * a.sg + col];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a.out[pix[e] * a.so + col] = gv[e] > 0.f ? act_apply(val[e], a.act) : 0.f;
       }
     }
   }

@@ -153,6 +153,49 @@ def test_dual_conv_heads_and_channel_slice_consumers():
         _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(3 * n * h * w), name)
 
 
+@pytest.mark.parametrize("cmid,cout", [(128, 64), (256, 192), (64, 32)])
+def test_relu_mask_folded_into_consumer_dx(cmid, cout):
+    """A ReLU conv read by one 3×3 conv (the motion encoder's corr_net / flow_net chains): the
+    consumer's dX conv applies the ReLU's backward in its epilogue (SCFLOW_EPI_RELU_MASK) and the
+    producer skips its threshold — every gradient against fp64 autograd, and the fused path
+    really taken (the producer's incoming gradient carries the consumer's tag)."""
+    from scflow_amd.train import functions as fn
+    g = torch.Generator().manual_seed(cmid + cout)
+    n, h, w, cin = 2, 32, 32, 96
+    x = torch.randn(n, h, w, cin, generator=g)
+    w1 = torch.randn(cmid, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
+    b1 = torch.randn(cmid, generator=g) * 0.1
+    w2 = torch.randn(cout, cmid, 3, 3, generator=g) / np.sqrt(cmid * 9)
+    b2 = torch.randn(cout, generator=g) * 0.1
+    gy = torch.randn(n, h, w, cout, generator=g)
+    ref = [t.double().requires_grad_() for t in (x, w1, b1, w2, b2)]
+    dev = [t.cuda().requires_grad_() for t in (x, w1, b1, w2, b2)]
+    mid = fn.conv2d_nhwc(dev[0], dev[1], dev[2], 1, 1, act="ReLU")
+    y = fn.conv2d_nhwc(mid, dev[3], dev[4], 1, 1, act="ReLU")
+    # ReLU's derivative jumps at 0: the reference takes the device forward's active sets
+    am = (mid.detach().cpu().double() > 0).permute(0, 3, 1, 2)
+    a = F.conv2d(ref[0].permute(0, 3, 1, 2), ref[1], ref[2], padding=1) * am
+    yr = (F.conv2d(a, ref[3], ref[4], padding=1).permute(0, 2, 3, 1)) * (y.detach().cpu().double() > 0)
+    (yr * gy.double()).sum().backward()
+    seen = {}
+    orig = fn._act_backward
+
+    def spy(dy, yy, act):
+        if act == "ReLU" and yy.shape[-1] == cmid:
+            seen["tagged"] = getattr(dy, "_scflow_relu_masked", None) == dy._version
+        return orig(dy, yy, act)
+
+    fn._act_backward = spy
+    try:
+        (y * gy.cuda()).sum().backward()
+    finally:
+        fn._act_backward = orig
+    torch.cuda.synchronize()
+    assert seen.get("tagged"), "the consumer's dX did not carry the ReLU mask to the producer"
+    for name, d, r in zip(("x", "w1", "b1", "w2", "b2"), dev, ref):
+        _close(d.grad, r.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), name)
+
+
 def test_conv_wgrad_accumulate_and_split():
     """scflow_conv_wgrad directly: a Chan slice as the second source, accumulate = 1 adds onto
     dw / db, and a batch large enough to split the pixel reduction over many workgroups."""
