@@ -939,7 +939,7 @@ int launch_wino_w(WinoParams p, hipStream_t st) {
 // K split (conv_wino_kernel KS = 2) for a 32-channel W = 32 launch whose grid leaves at most one
 // workgroup per CU (one wave per SIMD otherwise).  SCFLOW_WINO_KSPLIT=0 turns it off (A/B).
 #ifndef WINO_KSPLIT_DEFAULT
-#define WINO_KSPLIT_DEFAULT 1
+#define WINO_KSPLIT_DEFAULT 0
 #endif
 bool wino_ksplit(const scflow_conv_args& a, int cus) {
   static int on = -1;
@@ -974,7 +974,7 @@ int launch_wino5_k(Wino5Params p, hipStream_t st) {
 // per CU pay the input transform per 32 instead of 64 output channels).  SCFLOW_WINO5_KSPLIT=0
 // turns it off (A/B).
 #ifndef WINO5_KSPLIT_DEFAULT
-#define WINO5_KSPLIT_DEFAULT 1
+#define WINO5_KSPLIT_DEFAULT 0
 #endif
 bool wino5_ksplit(const scflow_conv_args& a, int nbw, int cus) {
   static int on = -1;

@@ -95,7 +95,7 @@ struct WwRaw {
 };
 
 #ifndef WW_STATIC
-#define WW_STATIC 1
+#define WW_STATIC 0
 #endif
 
 __device__ const floatx4 ww_zero4 = {0.f, 0.f, 0.f, 0.f};  // source of the zero-padding lanes

@@ -46,7 +46,7 @@ constexpr int W5W_NX = 5;                      // halo groups (4 rows × 9) per 
 __device__ __forceinline__ int w5w_addr(int r, int c, int ch) { return (r * 64 + ch) * W5W_RW + c; }
 
 #ifndef W5W_STATIC
-#define W5W_STATIC 1
+#define W5W_STATIC 0
 #endif
 
 struct W5wParams {

@@ -99,8 +99,10 @@ class SCFlowDecoder(nn.Module):
         # launch (scflow_pose_step); only without flow/correlation masking
         self.fuse_tail = True
         # the lookup and corr_net.0 (1×1 324→256) as ONE launch (scflow_corr_lookup_conv1x1: the
-        # correlation features stay in LDS) when the geometry allows (tiled pyramid, L = 4, r = 4)
-        self.fuse_lookup_conv = True
+        # correlation features stay in LDS) when the geometry allows (tiled pyramid, L = 4, r = 4).
+        # Opt-in: the producer / consumer-wave version is not yet validated on hardware (its
+        # single-role predecessor measured neutral, 5.116 vs 5.117 ms/forward)
+        self.fuse_lookup_conv = False
         # a batch of ≥ 2·pingpong_min pairs runs as two interleaved halves (_forward_pingpong).
         # Off: measured slower at B=16 (5.76 vs 5.33 ms/step) — a half's tail kernels do not get
         # CUs while the other half's convolutions hold every CU's LDS, so they serialise anyway

@@ -141,7 +141,7 @@ def _grad_sink(t: Optional[Tensor]) -> Optional[Tensor]:
 # A/B switches (tools/train_bench.py runs): SCFLOW_DEFER_LINEAR=0 / SCFLOW_THIN_DX_GEMM=0
 _DEFER_LINEAR = os.environ.get("SCFLOW_DEFER_LINEAR", "1") != "0"
 _THIN_DX_GEMM = os.environ.get("SCFLOW_THIN_DX_GEMM", "1") != "0"
-_RELU_MASK_FUSED = os.environ.get("SCFLOW_TRAIN_RELU_MASK", "1") != "0"  # A/B switch (tuning)
+_RELU_MASK_FUSED = os.environ.get("SCFLOW_TRAIN_RELU_MASK", "0") == "1"  # A/B switch (tuning)
 
 _ACT_FN = {None: lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Tanh": torch.tanh}
 

@@ -102,6 +102,7 @@ def test_conv2d_nhwc_fused_act_two_sources_bias_map(act, two, bmap):
             _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), name)
 
 
+@pytest.mark.optin
 def test_dual_conv_heads_and_channel_slice_consumers():
     """dual_conv2d_nhwc (the XHeads' hidden convs as one launch each way) and convs reading its
     channel-view outputs in place (the predictors): values and every gradient — x, both weight /
@@ -153,13 +154,15 @@ def test_dual_conv_heads_and_channel_slice_consumers():
         _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(3 * n * h * w), name)
 
 
+@pytest.mark.optin
 @pytest.mark.parametrize("cmid,cout", [(128, 64), (256, 192), (64, 32)])
-def test_relu_mask_folded_into_consumer_dx(cmid, cout):
+def test_relu_mask_folded_into_consumer_dx(cmid, cout, monkeypatch):
     """A ReLU conv read by one 3×3 conv (the motion encoder's corr_net / flow_net chains): the
     consumer's dX conv applies the ReLU's backward in its epilogue (SCFLOW_EPI_RELU_MASK) and the
     producer skips its threshold — every gradient against fp64 autograd, and the fused path
     really taken (the producer's incoming gradient carries the consumer's tag)."""
     from scflow_amd.train import functions as fn
+    monkeypatch.setattr(fn, "_RELU_MASK_FUSED", True)
     g = torch.Generator().manual_seed(cmid + cout)
     n, h, w, cin = 2, 32, 32, 96
     x = torch.randn(n, h, w, cin, generator=g)
@@ -620,6 +623,7 @@ def test_instance_norm_nhwc_forward_backward(n, h, w, c, relu):
 @pytest.mark.parametrize("n,h,w,c,mode", [(4, 64, 64, 64, "relu"), (3, 32, 32, 96, "plain"),
                                           (2, 16, 16, 128, "res"), (16, 32, 32, 64, "res"),
                                           (2, 8, 12, 4, "relu")])
+@pytest.mark.optin
 def test_batch_norm_nhwc_train(n, h, w, c, mode):
     """HIP BatchNorm2d in train mode (the context encoder's norms; + ReLU, or + a residual before
     the ReLU): output, running statistics and the gradients of x, γ, β (and the residual) against
