@@ -1268,7 +1268,12 @@ SCFLOW_API int scflow_conv_pick_bk(const scflow_conv_args* args) {
   const scflow_conv_args& a = *args;
   if (a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 || a.c1 < 0) return SCFLOW_EINVAL;
   if (wino_enabled(a.kh) && wino_launchable(a)) return SCFLOW_CONV_WINO;
-  if (conv1x1w_enabled() && conv1x1w_launchable(a)) return SCFLOW_CONV_1X1W;
+  // the wide 1×1 kernel up to two workgroups per CU (configs[1]'s corr_net.0: 256, the same
+  // 32.3 µs as conv1x1_kernel); larger grids keep conv1x1_kernel (configs[4], 2048 workgroups:
+  // 236 vs 243 µs standalone, 48.7 vs 50.1 ms per decoder forward — session r4c / r4e)
+  if (conv1x1w_enabled() && conv1x1w_launchable(a) &&
+      (long long)a.n * a.h * a.w <= (long long)W1_PX * 2 * device_cus())
+    return SCFLOW_CONV_1X1W;
   Geometry g = select_variant(a.cout, a.c0, a.c1, a.kh, a.kw, a.stride, a.h, a.w, a.ph, a.pw);
   if (g.variant != V_MFMA) return BK;  // other variants ignore the stage depth
   int tr, hr;

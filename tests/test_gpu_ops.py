@@ -239,13 +239,16 @@ def test_conv2d_mfma_stage_depths(ops, case, bk):
 
 def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
     """Host query: 3×3 / 1×5 / 5×1 stride-1 convs take the Winograd kernels; the 1×1 corr_net.0
-    conv the wide 1×1 kernel; a two-source 1×1 conv 16-deep stages of the direct conv."""
+    conv the wide 1×1 kernel up to two workgroups per CU; a two-source 1×1 conv 16-deep stages
+    of the direct conv."""
     from scflow_amd._lib import CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 5, 1, 2, 0) == CONV_WINO
     from scflow_amd._lib import CONV_1X1W
     assert ops.conv_pick_bk(16, 32, 32, 324, 0, 256, 1, 1, 0, 0) == CONV_1X1W  # corr_net.0
+    # configs[4]'s corr_net.0 (2048 workgroups) stays on conv1x1_kernel (measured faster there)
+    assert ops.conv_pick_bk(32, 64, 64, 324, 0, 256, 1, 1, 0, 0) not in (CONV_1X1W, CONV_WINO)
     assert ops.conv_pick_bk(16, 32, 32, 196, 60, 256, 1, 1, 0, 0) == 16  # two sources: direct
     assert ops.conv_pick_bk(2, 20, 20, 64, 0, 64, 3, 3, 1, 1) != CONV_WINO  # width not tileable
 
