@@ -52,8 +52,6 @@ extern "C" {
 #define SCFLOW_EPI_PLAIN 0  /* out = act(conv + bias) */
 #define SCFLOW_EPI_GRU_ZR 1 /* cout = 2·hc: z = σ(.) -> gate[:, :hc];  r = σ(.), rh = r·h -> rh   */
 #define SCFLOW_EPI_GRU_Q 2  /* cout = hc:   q = tanh(.);  hid <- (1-z)·hid + z·q  (z from gate)     */
-#define SCFLOW_EPI_RELU_MASK 3 /* out = conv (+ bias map) where gate > 0, else 0: the ReLU backward of
-                                  the conv's input folded into its dX conv (F(2×2,3×3) Winograd only) */
 
 /* pose-update mode word (the depth_transform argument of scflow_pose_update / _update_flow /
  * _step): bit 0 = depth transform (0 'exp', 1 linear); | SCFLOW_POSE_QUAT_XYZW = the delta

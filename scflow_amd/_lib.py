@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SCFLOW_LIB") or os.path.join(os.path.dirname(os.path.
 c_int, c_float, c_ll, c_vp = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ctypes.c_void_p
 
 SCFLOW_ACT = {None: 0, "ReLU": 1, "Sigmoid": 2, "Tanh": 3}
-EPI_PLAIN, EPI_GRU_ZR, EPI_GRU_Q, EPI_RELU_MASK = 0, 1, 2, 3
+EPI_PLAIN, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2
 CONV_WINO = 2  # scflow_conv_args.bk: Winograd F(2x2,3x3) packing/kernel (SCFLOW_CONV_WINO)
 CONV_1X1W = 3  # scflow_conv_args.bk: wide 1x1 packing/kernel (SCFLOW_CONV_1X1W)
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1

@@ -919,79 +919,43 @@ int wino_swz(int R, int C) {
 // profiling: where the next F(2×2,3×3) Winograd launches write their per-workgroup stamps
 static unsigned long long* g_wino_stamps = nullptr;
 
-template <int W, int NBW, int KS = 1>
+template <int W, int NBW>
 int launch_wino_w(WinoParams p, hipStream_t st) {
   using G = WinoGeom<W>;
-  const size_t lds = wino_lds_bytes<W, NBW, KS>();
+  const size_t lds = wino_lds_bytes<W, NBW>();
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino_kernel<W, NBW, KS>,
+    (void)hipFuncSetAttribute((const void*)conv_wino_kernel<W, NBW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * G::XB, round_up(p.a.cout, 32 * NBW) / (32 * NBW));
   p.swz_c = wino_swz(grid.x, grid.y);
   p.stamps = g_wino_stamps;
-  conv_wino_kernel<W, NBW, KS><<<grid, 256 * KS, lds, st>>>(p);
+  conv_wino_kernel<W, NBW><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }
 
-// K split (conv_wino_kernel KS = 2) for a 32-channel W = 32 launch whose grid leaves at most one
-// workgroup per CU (one wave per SIMD otherwise).  SCFLOW_WINO_KSPLIT=0 turns it off (A/B).
-#ifndef WINO_KSPLIT_DEFAULT
-#define WINO_KSPLIT_DEFAULT 0
-#endif
-bool wino_ksplit(const scflow_conv_args& a, int cus) {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("SCFLOW_WINO_KSPLIT");
-    on = e ? atoi(e) != 0 : WINO_KSPLIT_DEFAULT;
-  }
-  if (!on) return false;
-  const long long blocks = (long long)a.n * (a.h / WinoGeom<32>::OROWS) * (round_up(a.cout, 32) / 32);
-  return blocks <= cus;
-}
-
-template <int DIR, int W, int NBW, int EPI, int KS = 1>
+template <int DIR, int W, int NBW, int EPI>
 int launch_wino5_k(Wino5Params p, hipStream_t st) {
   using G = Wino5Geom<DIR, W>;
-  const size_t lds = wino5_lds_bytes<DIR, W, NBW, KS>();
+  const size_t lds = wino5_lds_bytes<DIR, W, NBW>();
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI, KS>,
+    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
   p.swz_c = wino_swz(grid.x, grid.y);
   p.stamps = g_wino_stamps;
-  conv_wino5_kernel<DIR, W, NBW, EPI, KS><<<grid, 256 * KS, lds, st>>>(p);
+  conv_wino5_kernel<DIR, W, NBW, EPI><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
-}
-
-// K split for the F(4,5) kernel (conv_wino5_kernel KS = 2 at 64 channels) when the 64-channel grid
-// is at most one workgroup per CU and the heuristic picked 32 channels (two 32-channel workgroups
-// per CU pay the input transform per 32 instead of 64 output channels).  SCFLOW_WINO5_KSPLIT=0
-// turns it off (A/B).
-#ifndef WINO5_KSPLIT_DEFAULT
-#define WINO5_KSPLIT_DEFAULT 0
-#endif
-bool wino5_ksplit(const scflow_conv_args& a, int nbw, int cus) {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("SCFLOW_WINO5_KSPLIT");
-    on = e ? atoi(e) != 0 : WINO5_KSPLIT_DEFAULT;
-  }
-  if (!on || nbw != 1 || a.w != 32) return false;
-  const long long blocks = (long long)a.n * (a.h * a.w / 128) * (round_up(a.cout, 64) / 64);
-  return blocks <= cus;
 }
 
 template <int EPI>
 int launch_wino5_epi(const Wino5Params& p, int nbw, hipStream_t st) {
   const bool x = p.a.kh == 1;
-  if (p.a.w == 32 && wino5_ksplit(p.a, nbw, device_cus()))
-    return x ? launch_wino5_k<0, 32, 2, EPI, 2>(p, st) : launch_wino5_k<1, 32, 2, EPI, 2>(p, st);
   if (p.a.w == 32) {
     if (x) return nbw == 2 ? launch_wino5_k<0, 32, 2, EPI>(p, st) : launch_wino5_k<0, 32, 1, EPI>(p, st);
     return nbw == 2 ? launch_wino5_k<1, 32, 2, EPI>(p, st) : launch_wino5_k<1, 32, 1, EPI>(p, st);
@@ -1006,7 +970,6 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
       !aligned16(a.weight))
     return SCFLOW_EALIGN;
   if (a.kh != 3) {
-    if (a.epilogue == SCFLOW_EPI_RELU_MASK) return SCFLOW_EUNSUPPORTED;
     Wino5Params p;
     p.a = a;
     p.cp0 = round_up(a.c0, W5SC);
@@ -1024,7 +987,6 @@ int launch_wino(const scflow_conv_args& a, hipStream_t st) {
   p.nst = (p.cp0 + round_up(a.c1, WSC)) / WSC;
   const int nbw = wino_nbw(a, device_cus());
   if (a.w == 32) {
-    if (nbw == 1 && wino_ksplit(a, device_cus())) return launch_wino_w<32, 1, 2>(p, st);
     return nbw == 3 ? launch_wino_w<32, 3>(p, st)
                     : nbw == 2 ? launch_wino_w<32, 2>(p, st) : launch_wino_w<32, 1>(p, st);
   }
@@ -1295,9 +1257,6 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     if (!a.gate || !a.rh || !a.hid || (a.cout & 1)) return SCFLOW_EINVAL;
   } else if (a.epilogue == SCFLOW_EPI_GRU_Q) {
     if (!a.gate || !a.hid) return SCFLOW_EINVAL;
-  } else if (a.epilogue == SCFLOW_EPI_RELU_MASK) {
-    if (!a.out || !a.gate) return SCFLOW_EINVAL;
-    if (a.bk != SCFLOW_CONV_WINO || a.kh != 3 || a.kw != 3) return SCFLOW_EUNSUPPORTED;
   } else {
     return SCFLOW_EINVAL;
   }

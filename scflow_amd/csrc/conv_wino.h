@@ -139,28 +139,21 @@ struct WinoGeom {
   __device__ static constexpr int addr(int r, int c) { return r * ROWP + c * 8 + (c >> 1); }
 };
 
-template <int W, int NBW, int KS = 1>
+template <int W, int NBW>
 constexpr size_t wino_lds_bytes() {
   const size_t halo = (size_t)2 * WinoGeom<W>::BUF4 * 4;  // double-buffered
   const size_t epi = (size_t)4 * 2 * (WTM + 4) * 32 * NBW;
-  const size_t red = KS > 1 ? (size_t)2 * NBW * 16 * 256 : 0;  // K-split partial sums, 2 points
-  const size_t m = halo > epi ? halo : epi;
-  return sizeof(float) * (m > red ? m : red);
+  return sizeof(float) * (halo > epi ? halo : epi);
 }
 
 // NBW = 3 (96 output channels, one workgroup per CU: 192 accumulator registers per lane) balances
 // grids whose 64-channel version would leave 1.5 workgroups per CU (corr_net.1 at B = 16).
-//
-// KS = 2 (K split, 32-channel workgroups that would leave one wave per SIMD: grids of at most one
-// workgroup per CU): 512 threads, two wave sets over the same points — set ks takes sub-steps
-// ks and ks + 2 of every stage (the shared halo staged by all 8 waves) — their sums added through
-// LDS before the epilogue.  Two waves per SIMD then cover each other's U / LDS latencies and the
-// per-stage barrier.
-template <int W, int NBW, int KS = 1>
-__global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_wino_kernel(WinoParams P) {
-  static_assert(KS == 1 || (KS == 2 && NBW == 1), "K split: 32-channel workgroups");
+// (A K split for the 32-channel grids — two wave sets over alternate sub-steps, sums through LDS —
+// was built in round 4 and measured in round 5: ±2 % alone, the decoder 2 % slower; removed.)
+template <int W, int NBW>
+__global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoParams P) {
   using G = WinoGeom<W>;
-  constexpr int NT = 256 * KS;                              // threads
+  constexpr int NT = 256;                                   // threads
   constexpr int NA = (G::NH4 + 4 * NT - 1) / (4 * NT);     // float4 per thread per quarter stage
   constexpr int BNW = 32 * NBW;  // output channels per workgroup
   extern __shared__ floatx4 smem4[];  // float4-typed so halo accesses are ds_*_b128
@@ -169,7 +162,6 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int wave = wv & 3;                 // Winograd row i of the wave's points
-  const int ks = KS > 1 ? wv >> 2 : 0;     // K-split wave set
   const int li = lane & 31, hh = lane >> 5;
   int bx, by;
   wino_block(P.swz_c, bx, by);
@@ -200,7 +192,7 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
       hlds[part][j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 7) : -1;
     }
   const int hq4 = 4 * (tid & 7);  // channel of this thread's quad within the stage (idx & 7 = tid & 7)
-  floatx4 ra[2][NA];  // two quarters in flight (the K split loads two before storing them)
+  floatx4 ra[2][NA];  // quarter part in slot part & 1
   // stage s's source, as a buffer starting at its first channel
   __amdgpu_buffer_rsrc_t hsrc;
   int hss4 = 0, hlim = 0;  // pixel stride in bytes, channels of the stage present in the source
@@ -296,8 +288,6 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
   // arrive (WINO_U_AHEAD = 2: the 32-channel workgroups, one wave per SIMD at B = 16)
   constexpr int UAH = (NBW == 1 && WINO_U_AHEAD > 1) ? 2 : 1;
   floatx4 u[UAH][4][NBW];
-  // the wave's sub-step sequence: every sub-step (KS = 1), or sub-steps ks, ks + 2 of each stage
-  auto tsub = [&](int m) { return KS > 1 ? 4 * (m >> 1) + ks + 2 * (m & 1) : m; };
   // the MFMAs of point j of the sub-step in slot par, then point j's weights for sub-step tload
   // (the one UAH further along the wave's sequence) into the same slot
   auto point = [&](const floatx4(&v)[4], int j, int tload, int par) {
@@ -350,7 +340,7 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
 #pragma unroll
   for (int d = 0; d < UAH; ++d)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) uload1(u[d][j], tsub(d), j);
+    for (int j = 0; j < 4; ++j) uload1(u[d][j], d, j);
   hsource(0);
 #pragma unroll
   for (int part = 0; part < 4; ++part) {
@@ -363,45 +353,30 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
   __syncthreads();
   wino_stamp(P.stamps, 1);
   floatx4 vA[4], vB[4];
-  vcompute(0, ks, vA);
+  vcompute(0, 0, vA);
   inloop = true;
   for (int s = 0; s < nst; ++s) {
     const int buf = s & 1;
     hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
-    if constexpr (KS == 1) {
-      // sub-step t = 4s + k − 1 in slot t % UAH reloads its points for t + UAH
-      const int t0 = s * WNSUB;
-      hload(0);
-      substep_next(vA, t0 + UAH, 0, buf, 1, vB);
-      hstore(buf ^ 1, 0);
-      hload(1);
-      substep_next(vB, t0 + 1 + UAH, 1 % UAH, buf, 2, vA);
-      hstore(buf ^ 1, 1);
-      hload(2);
-      substep_next(vA, t0 + 2 + UAH, 2 % UAH, buf, 3, vB);
-      hstore(buf ^ 1, 2);
-      hload(3);
-      substep(vB, t0 + 3 + UAH, 3 % UAH);
-      hstore(buf ^ 1, 3);
-    } else {
-      // sequence m = 2s (sub-step ks) and 2s + 1 (sub-step ks + 2), slot m % UAH
-      const int m0 = 2 * s;
-      hload(0);
-      hload(1);
-      substep_next(vA, tsub(m0 + UAH), 0, buf, ks + 2, vB);
-      hstore(buf ^ 1, 0);
-      hstore(buf ^ 1, 1);
-      hload(2);
-      hload(3);
-      substep(vB, tsub(m0 + 1 + UAH), 1 % UAH);
-      hstore(buf ^ 1, 2);
-      hstore(buf ^ 1, 3);
-    }
+    // sub-step t = 4s + k − 1 in slot t % UAH reloads its points for t + UAH
+    const int t0 = s * WNSUB;
+    hload(0);
+    substep_next(vA, t0 + UAH, 0, buf, 1, vB);
+    hstore(buf ^ 1, 0);
+    hload(1);
+    substep_next(vB, t0 + 1 + UAH, 1 % UAH, buf, 2, vA);
+    hstore(buf ^ 1, 1);
+    hload(2);
+    substep_next(vA, t0 + 2 + UAH, 2 % UAH, buf, 3, vB);
+    hstore(buf ^ 1, 2);
+    hload(3);
+    substep(vB, t0 + 3 + UAH, 3 % UAH);
+    hstore(buf ^ 1, 3);
 #ifndef WX_NO_SYNC
     __syncthreads();
 #endif
 #ifndef WX_NO_V
-    vcompute(buf ^ 1, ks, vA);
+    vcompute(buf ^ 1, 0, vA);
 #endif
   }
 
@@ -425,31 +400,7 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
   constexpr int WEP = WTM + 4;
   __syncthreads();
   wino_stamp(P.stamps, 2);
-  if constexpr (KS > 1) {
-    // the second wave set's sums onto the first's, two points per round through LDS
-    float* R = smem;
-#pragma unroll
-    for (int j2 = 0; j2 < 4; j2 += 2) {
-      if (ks == 1)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int nb = 0; nb < NBW; ++nb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) R[((jj * NBW + nb) * 16 + r) * 256 + (tid - 256)] = acc[j2 + jj][nb][r];
-      __syncthreads();
-      if (ks == 0)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int nb = 0; nb < NBW; ++nb)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[j2 + jj][nb][r] += R[((jj * NBW + nb) * 16 + r) * 256 + tid];
-      __syncthreads();
-    }
-  }
   float* S = smem;
-  if (ks == 0)
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
@@ -475,7 +426,7 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
     const float bias = a.bias ? a.bias[col] : 0.f;
     const float osc = a.out_scale ? a.out_scale[col] : 1.f;
     const float osh = a.out_scale ? a.out_shift[col] : 0.f;
-    constexpr int GROUPS = NT / BNW;             // 4 (BNW 64), 8 (BNW 32) or 16 (BNW 32, KS 2)
+    constexpr int GROUPS = NT / BNW;             // 4 (BNW 64) or 8 (BNW 32)
     constexpr int NPX = WTM * 4 / GROUPS;        // output pixels per thread
     const int g = tid / BNW;
     const int ar = (g >> 1) & 1, bc = g & 1;      // this thread's output position in the 2×2 tile
@@ -508,16 +459,8 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
   #pragma unroll
       for (int q = 0; q < NPX; ++q) val[q] += a.res[pix[q] * a.sres + col];
     }
-    if (a.epilogue == SCFLOW_EPI_RELU_MASK) {  // the input ReLU's backward: zero where gate ≤ 0
-      float gv[NPX];
   #pragma unroll
-      for (int q = 0; q < NPX; ++q) gv[q] = a.gate[pix[q] * a.sg + col];
-  #pragma unroll
-      for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = gv[q] > 0.f ? act_apply(val[q], a.act) : 0.f;
-    } else {
-  #pragma unroll
-      for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q], a.act);
-    }
+    for (int q = 0; q < NPX; ++q) a.out[pix[q] * a.so + col] = act_apply(val[q], a.act);
 
   } else {
     // BNW does not divide the 256 threads: (output position, channel) pairs dealt round robin,
@@ -556,13 +499,8 @@ __global__ __launch_bounds__(256 * KS, (NBW >= 3 || KS > 1) ? 1 : 2) void conv_w
 #pragma unroll
           for (int e = 0; e < 4; ++e) val[e] += a.res[pix[e] * a.sres + col];
         }
-        float gv[4] = {1.f, 1.f, 1.f, 1.f};
-        if (a.epilogue == SCFLOW_EPI_RELU_MASK) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) gv[e] = a.gate[pix[e] * a.sg + col];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a.out[pix[e] * a.so + col] = gv[e] > 0.f ? act_apply(val[e], a.act) : 0.f;
+        for (int e = 0; e < 4; ++e) a.out[pix[e] * a.so + col] = act_apply(val[e], a.act);
       }
     }
   }

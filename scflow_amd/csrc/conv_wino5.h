@@ -63,25 +63,20 @@ struct Wino5Geom {
   __device__ static constexpr int addr(int r, int c) { return r * ROWP + c * 8 + c / SK; }
 };
 
-template <int DIR, int W, int NBW, int KS = 1>
+template <int DIR, int W, int NBW>
 constexpr size_t wino5_lds_bytes() {
   const size_t halo = (size_t)2 * Wino5Geom<DIR, W>::BUF4 * 4;  // double-buffered
   const size_t epi = (size_t)8 * (W5TM + 4) * 32 * NBW;
-  const size_t red = KS > 1 ? (size_t)NBW * 16 * 256 : 0;  // K-split partial sums, one point slot
-  const size_t m = halo > epi ? halo : epi;
-  return sizeof(float) * (m > red ? m : red);
+  return sizeof(float) * (halo > epi ? halo : epi);
 }
 
-//
-// KS = 2 (K split, for a 64-channel launch whose grid is at most one workgroup per CU — the GRU
-// q conv at B = 16): 512 threads, wave set ks takes the 8-channel half q = ks of every sub-step
-// (its own U half and input transform; the halo staged by all 8 waves), the two sets' sums added
-// through LDS before the epilogue — two waves per SIMD at the 64-channel transform cost per MFMA.
-template <int DIR, int W, int NBW, int EPI, int KS = 1>
-__global__ __launch_bounds__(256 * KS, KS > 1 ? 1 : 2) void conv_wino5_kernel(Wino5Params P) {
-  static_assert(KS == 1 || (KS == 2 && NBW == 2), "K split: 64-channel workgroups");
+// (A K split for the GRU q conv's one-workgroup-per-CU grid — two wave sets over the two 8-channel
+// halves of every sub-step — was built in round 4 and measured in round 5: 32.7 → 32.5 µs alone,
+// the decoder 2 % slower; removed.)
+template <int DIR, int W, int NBW, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   using G = Wino5Geom<DIR, W>;
-  constexpr int NTH = 256 * KS;                              // threads
+  constexpr int NTH = 256;                                   // threads
   constexpr int NA = (G::NH4 + 2 * NTH - 1) / (2 * NTH);    // float4 per thread per half stage
   constexpr int BNW = 32 * NBW;
   extern __shared__ floatx4 smem4[];
@@ -90,7 +85,6 @@ __global__ __launch_bounds__(256 * KS, KS > 1 ? 1 : 2) void conv_wino5_kernel(Wi
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int wave = wv & 3;              // point pair
-  const int ks = KS > 1 ? wv >> 2 : 0;  // K-split wave set (the 8-channel half it takes)
   const int li = lane & 31, hh = lane >> 5;
   constexpr int XB = W / G::OCOLS;  // column blocks per image (1, or 2 for 5×1 at W = 64)
   int bx, by;
@@ -264,73 +258,10 @@ __global__ __launch_bounds__(256 * KS, KS > 1 ? 1 : 2) void conv_wino5_kernel(Wi
       vmath(d, vA[1], w3);
     }
   };
-  // K split: the same pipeline over this set's half q = ks of each sub-step
-  floatx4 u1[2][NBW];  // [x][nb]
-  auto uload_q = [&](int t) {
-    const int tt = t < nsub ? t : nsub - 1;
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int nb = 0; nb < NBW; ++nb)
-        u1[x][nb] = wino_bload(wsrc, lane * 16, ((((nb * nsub + tt) * 8 + 2 * wave + x) * 2 + ks) * 1024));
-  };
-  auto halfq = [&](const floatx4(&v)[2], int tnext) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int nb = 0; nb < NBW; ++nb)
-          acc[x][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[x][e], u1[x][nb][e], acc[x][nb], 0, 0, 0);
-    uload_q(tnext);
-#if WINO_SCHED_BARRIER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-  };
-  auto mainloop_ks = [&](auto w3) {
-    floatx4 d[8];
-    uload_q(0);
-    hsource(0);
-    hload(0);
-    hstore(0, 0);
-    hload(1);
-    hstore(0, 1);
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    wino_stamp(P.stamps, 1);
-    floatx4 vA[2], vB[2];
-    vload(0, 0, ks, d, w3);
-    vmath(d, vA, w3);
-    for (int s = 0; s < nst; ++s) {
-      const int buf = s & 1;
-      const int t0 = s * W5NSUB;
-      hsource(s + 1 < nst ? s + 1 : s);
-      hload(0);
-      vload(buf, 1, ks, d, w3);
-      halfq(vA, t0 + 1);
-      vmath(d, vB, w3);
-      hstore(buf ^ 1, 0);
-      hload(1);
-      halfq(vB, t0 + 2);
-      hstore(buf ^ 1, 1);
-      __syncthreads();
-      vload(buf ^ 1, 0, ks, d, w3);
-      vmath(d, vA, w3);
-    }
-  };
-  if constexpr (KS > 1) {
-    (void)mainloop;
-    if (wave == 3)
-      mainloop_ks(std::true_type{});
-    else
-      mainloop_ks(std::false_type{});
-  } else {
-    (void)mainloop_ks;
-    if (wave == 3)
-      mainloop(std::true_type{});
-    else
-      mainloop(std::false_type{});
-  }
+  if (wave == 3)
+    mainloop(std::true_type{});
+  else
+    mainloop(std::false_type{});
 
 #ifdef WX_NO_EPI
   {
@@ -349,27 +280,7 @@ __global__ __launch_bounds__(256 * KS, KS > 1 ? 1 : 2) void conv_wino5_kernel(Wi
   constexpr int WEP = W5TM + 4;
   __syncthreads();
   wino_stamp(P.stamps, 2);
-  if constexpr (KS > 1) {
-    // the second wave set's sums onto the first's, one point slot per round through LDS
-    float* R = smem;
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      if (ks == 1)
-#pragma unroll
-        for (int nb = 0; nb < NBW; ++nb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) R[(nb * 16 + r) * 256 + (tid - 256)] = acc[x][nb][r];
-      __syncthreads();
-      if (ks == 0)
-#pragma unroll
-        for (int nb = 0; nb < NBW; ++nb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[x][nb][r] += R[(nb * 16 + r) * 256 + tid];
-      __syncthreads();
-    }
-  }
   float* S = smem;
-  if (ks == 0)
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll

@@ -94,9 +94,6 @@ struct WwRaw {
   floatx2w y0, y1, a0[2], a1[2], b0[2], b1[2];
 };
 
-#ifndef WW_STATIC
-#define WW_STATIC 0
-#endif
 
 __device__ const floatx4 ww_zero4 = {0.f, 0.f, 0.f, 0.f};  // source of the zero-padding lanes
 // a float4 in the global address space: global_load (vmcnt only), not a flat load, which also
@@ -219,33 +216,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
   const float ya = wave == 3 ? 0.f : 1.f;                       // weight of dY row 0
   const float yb = wave == 0 ? 0.f : (wave == 2 ? -1.f : 1.f);  // weight of dY row 1
 
-  // operands of k-step kk (tiles 2kk + hh of the chunk: tile row kk >> 3, column (2kk+hh) & 15)
-  auto operands = [&](int kk, float (&yv)[4], float (&vv)[2][4]) {
-    const int ttr = kk >> 3, ttc = (2 * kk + hh) & 15;
-    const floatx2w y0 = *(const floatx2w*)(Dl + ((2 * ttr) * WWCO + li) * WWD + 2 * ttc);
-    const floatx2w y1 = *(const floatx2w*)(Dl + ((2 * ttr + 1) * WWCO + li) * WWD + 2 * ttc);
-    const float q0 = ya * y0[0] + yb * y1[0], q1 = ya * y0[1] + yb * y1[1];
-    yv[0] = q0;
-    yv[1] = q0 + q1;
-    yv[2] = q0 - q1;
-    yv[3] = q1;  // column 3 taken positive
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const float* xb = Xl + (cb * 32 + li) * WWX + 2 * ttc;
-      const floatx2w a0 = *(const floatx2w*)(xb + (2 * ttr + r1) * WWCI * WWX);
-      const floatx2w a1 = *(const floatx2w*)(xb + (2 * ttr + r1) * WWCI * WWX + 2);
-      const floatx2w b0 = *(const floatx2w*)(xb + (2 * ttr + r2) * WWCI * WWX);
-      const floatx2w b1 = *(const floatx2w*)(xb + (2 * ttr + r2) * WWCI * WWX + 2);
-      const float t0 = a0[0] + sb * b0[0], t1 = a0[1] + sb * b0[1];
-      const float t2 = a1[0] + sb * b1[0], t3 = a1[1] + sb * b1[1];
-      vv[cb][0] = t0 - t2;
-      vv[cb][1] = t1 + t2;
-      vv[cb][2] = t2 - t1;
-      vv[cb][3] = t1 - t3;
-    }
-  };
-
-  // the same operands in two halves (WW_STATIC): the raw LDS reads, then the arithmetic
+  // a k-step's operands in two halves: the raw LDS reads, then the arithmetic
   // step st of this wave: tile row st >> 2, tile column 4·ks + hh + 8·((st >> 1) & 1) + 2·(st & 1)
   // — per-thread bases plus compile-time offsets once unrolled (ds_read offset fields)
   const int tc0 = 4 * ks + hh;
@@ -282,7 +253,6 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
   (void)rawload;
   (void)xform;
 
-#if WW_STATIC
   // the next chunk's global loads in three pieces issued inside steps 0..2 of this chunk (their
   // address arithmetic in the MFMA shadow): every lane loads unconditionally — from ww_zero4
   // where the old code branched around the load (padding, channels beyond cout / cin)
@@ -319,19 +289,13 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       rx[j] = *(const WwGlobal4*)(ok ? src : (const float*)&ww_zero4);
     }
   };
-#endif
 
   if (c_begin < c_end) {
     gload(c_begin);
     lstore(0);
     __syncthreads();
-#if !WW_STATIC
-    if (c_begin + 1 < c_end) gload(c_begin + 1);
-#endif
   }
-#if WW_STATIC
   WgWalk wk = wg_walk_at(c_begin, P.rg, P.cg, P.sg.nimg);
-#endif
   for (int ch = c_begin; ch < c_end; ++ch) {
     const int cur = (ch - c_begin) & 1;
     Dl = smem + cur * WBUF;
@@ -340,12 +304,10 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       const int co = tid & 31;
       for (int p = tid >> 5; p < 128; p += WW_NT / 32) bsum += Dl[((p >> 5) * WWCO + co) * WWD + (p & 31)];
     }
-#if WW_STATIC
     // the wave's 8 k-steps s (kk = 2·ks + 4·(s >> 1) + (s & 1)) as straight-line code: step s
     // issues step s + 1's LDS reads, then its own 8 MFMAs with step s + 1's operand arithmetic
     // interleaved from the fourth MFMA on (by then the reads have landed) — no LDS wait in front
     // of an MFMA, and no exposed read latency
-    (void)operands;
     WwRaw raw;
     float yv[2][4], vv[2][2][4];
     rawload(0, raw);
@@ -374,30 +336,9 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad_wino_kernel(WwParams P, float*
       __builtin_amdgcn_sched_barrier(0);
     };
     StaticFor<0, 8>::run(step);
-#else
-    float yA[4], vA[2][4], yB[4], vB[2][4];
-    operands(2 * ks, yA, vA);
-    for (int kk = 2 * ks; kk < 16; kk += 4) {
-      operands(kk + 1, yB, vB);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          acc[j][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(yA[j], vA[cb][j], acc[j][cb], 0, 0, 0);
-      operands(kk + 4 < 16 ? kk + 4 : kk, yA, vA);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          acc[j][cb] = __builtin_amdgcn_mfma_f32_32x32x2f32(yB[j], vB[cb][j], acc[j][cb], 0, 0, 0);
-    }
-#endif
     if (ch + 1 < c_end) {
       lstore(cur ^ 1);
       __syncthreads();
-#if !WW_STATIC
-      if (ch + 2 < c_end) gload(ch + 2);
-#endif
     }
   }
   // the second k-step set's sums onto the first's

@@ -45,9 +45,6 @@ constexpr int W5W_ND = 4;                      // 4-pixel dY groups per lane per
 constexpr int W5W_NX = 5;                      // halo groups (4 rows × 9) per lane (36 / 8 waves)
 __device__ __forceinline__ int w5w_addr(int r, int c, int ch) { return (r * 64 + ch) * W5W_RW + c; }
 
-#ifndef W5W_STATIC
-#define W5W_STATIC 0
-#endif
 
 struct W5wParams {
   scflow_wgrad_args a;
@@ -83,62 +80,9 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
   // 60-80 % bank-conflict cycles).
   const int cl = tid & 63;  // this lane's channel in the workgroup's co / ci block
   floatx4 rd[W5W_ND], rx[W5W_NX];
-  auto origin = [&](int ch, int* img, int* oy0, int* ox0) __attribute__((always_inline)) {
-    *img = ch / (P.rg * P.cg);
-    const int rem = ch - *img * P.rg * P.cg;
-    *oy0 = (rem / P.cg) * 4;
-    *ox0 = (rem % P.cg) * 32;
-  };
   auto pix = [&](int img, int y, int x) __attribute__((always_inline)) {
     return (size_t)img * P.H * P.W + (size_t)y * P.sy + (size_t)x * P.sx;
   };
-  auto gload = [&](int ch) __attribute__((always_inline)) {
-    int img, oy0, ox0;
-    origin(ch, &img, &oy0, &ox0);
-    const int seg = img / P.sg.nimg;  // workgroup-uniform
-    img -= seg * P.sg.nimg;
-    const float* dyp = P.sg.dy[seg];
-    const int co = co0 + cl, c = ci0 + cl;
-#pragma unroll
-    for (int j = 0; j < W5W_ND; ++j) {  // dY: row q >> 3, columns 4(q & 7) + k
-      const int q = wv + 8 * j;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (co < a.cout) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = dyp[pix(img, oy0 + (q >> 3), ox0 + 4 * (q & 7) + k) * a.sdy + co];
-      }
-      rd[j] = v;
-    }
-    const float* src = c < a.cin0 ? P.sg.src0[seg] + c : P.sg.src1[seg] + (c - a.cin0);
-    const int ss = c < a.cin0 ? a.s0 : a.s1;
-#pragma unroll
-    for (int j = 0; j < W5W_NX; ++j) {  // halo: row q / 9, columns x = ox0 − 2 + 4(q % 9) + k
-      const int q = wv + 8 * j;
-      floatx4 v = {0.f, 0.f, 0.f, 0.f};
-      if (q < 36 && c < cin) {
-        const int y = oy0 + q / 9;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int x = ox0 - 2 + 4 * (q % 9) + k;
-          if (x >= 0 && x < P.W) v[k] = src[pix(img, y, x) * ss];
-        }
-      }
-      rx[j] = v;
-    }
-  };
-  auto lstore = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < W5W_ND; ++j) {
-      const int q = wv + 8 * j;
-      *(floatx4*)(Dl + w5w_addr(q >> 3, 4 * (q & 7), cl)) = rd[j];
-    }
-#pragma unroll
-    for (int j = 0; j < W5W_NX; ++j) {
-      const int q = wv + 8 * j;
-      if (q < 36) *(floatx4*)(Xl + w5w_addr(q / 9, 4 * (q % 9), cl)) = rx[j];
-    }
-  };
-
   floatx16 acc[2][2][2];  // [point slot][co block][ci block]
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -162,38 +106,6 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
   const float c4 = wave == 0 ? -4.25f : (wave == 1 ? -1.25f : -5.f);
   const bool w3 = wave == 3;  // wave-uniform
 
-  // operands of k-step kk: tile t = 2kk + hh of the chunk (row t >> 3, first column 4(t & 7))
-  auto operands = [&](int kk, float (&yv)[2][2], float (&vv)[2][2], auto W3)
-                      __attribute__((always_inline)) {
-    const int t = 2 * kk + hh;
-    const int r = t >> 3, c = 4 * (t & 7);
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const floatx4 d = *(const floatx4*)(Dl + w5w_addr(r, c, cb * 32 + li));
-      if constexpr (decltype(W3)::value) {
-        yv[0][cb] = d[0];
-        yv[1][cb] = d[3];
-      } else {
-        const float e = d[0] + s2 * d[2], o = s1 * d[1] + s3 * d[3];
-        yv[0][cb] = e + o;
-        yv[1][cb] = e - o;
-      }
-    }
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) {
-      const floatx4 x0 = *(const floatx4*)(Xl + w5w_addr(r, c, ib * 32 + li));
-      const floatx4 x1 = *(const floatx4*)(Xl + w5w_addr(r, c + 4, ib * 32 + li));
-      if constexpr (decltype(W3)::value) {
-        vv[0][ib] = (x1[2] - x0[0]) + 5.25f * (x0[2] - x1[0]);
-        vv[1][ib] = (x1[3] - x0[1]) + 5.25f * (x0[3] - x1[1]);
-      } else {
-        const float av = c1 * x0[1] + c3 * x0[3] + c5 * x1[1];
-        const float bv = c2 * x0[2] + c4 * x1[0] + x1[2];
-        vv[0][ib] = bv + av;
-        vv[1][ib] = bv - av;
-      }
-    }
-  };
   auto mfmas = [&](const float (&yv)[2][2], const float (&vv)[2][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -204,7 +116,6 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
           acc[x][cb][ib] = __builtin_amdgcn_mfma_f32_32x32x2f32(yv[x][cb], vv[x][ib], acc[x][cb][ib], 0, 0, 0);
   };
 
-#if W5W_STATIC
   // Static form: two LDS buffers (one barrier per chunk); the next chunk's loads go out in five
   // pieces inside steps 0..4 (branch-free: lanes outside the data load ww_zero4), the wave's 8
   // k-steps st (kk = 2·ks + 4·(st >> 1) + (st & 1): tile row st >> 1, first column
@@ -308,7 +219,6 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
   };
   auto mainloop = [&](auto W3) __attribute__((always_inline)) {
     constexpr int BUF = W5W_DFL + W5W_XFL;
-    (void)operands;
     WgWalk wk = wg_walk_at(c_begin, P.rg, P.cg, P.sg.nimg);
     if (c_begin < c_end) {
       const Gsrc g0 = gsetup(wk);
@@ -355,33 +265,6 @@ __global__ __launch_bounds__(W5W_NT, 1) void wgrad_wino5_kernel(W5wParams P, flo
       }
     }
   };
-#else
-  // instantiated per transform shape (waves 0-2 / wave 3; the wave index is uniform), so the
-  // k-step loop has no branches
-  auto mainloop = [&](auto W3) __attribute__((always_inline)) {
-    if (c_begin < c_end) gload(c_begin);
-    for (int ch = c_begin; ch < c_end; ++ch) {
-      __syncthreads();  // every wave is done with the previous chunk
-      lstore();
-      __syncthreads();
-      if (ch + 1 < c_end) gload(ch + 1);  // in flight during this chunk's MFMAs
-      if (do_bias) {  // Σ dY per channel: thread (co = tid & 63) over every 8th pixel
-        const int co = tid & 63;
-        for (int p = tid >> 6; p < 128; p += W5W_NT / 64) bsum += Dl[w5w_addr(p >> 5, p & 31, co)];
-      }
-      // this wave set's k-steps kk = 2ks + 4m + {0, 1}; the next one's operands formed between
-      // the current one's MFMAs
-      float yA[2][2], vA[2][2], yB[2][2], vB[2][2];
-      operands(2 * ks, yA, vA, W3);
-      for (int kk = 2 * ks; kk < 16; kk += 4) {
-        operands(kk + 1, yB, vB, W3);
-        mfmas(yA, vA);
-        operands(kk + 4 < 16 ? kk + 4 : kk, yA, vA, W3);
-        mfmas(yB, vB);
-      }
-    }
-  };
-#endif
   if (w3)
     mainloop(std::true_type{});
   else
@@ -540,7 +423,7 @@ int wwino5_launch(const W5wParams& P, hipStream_t st) {
   const int splits = wwino5_splits(P);
   float* slab = a.workspace;
   float* bslab = a.db ? a.workspace + (size_t)splits * 8 * P.copad * P.cinp : nullptr;
-  const size_t lds = sizeof(float) * (size_t)(W5W_DFL + W5W_XFL) * (W5W_STATIC ? 2 : 1);
+  const size_t lds = sizeof(float) * (size_t)(W5W_DFL + W5W_XFL) * 2;  // double-buffered
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)wgrad_wino5_kernel,

@@ -663,7 +663,8 @@ class SCFlowDecoder(nn.Module):
                 for c in pc:
                     c()
                 self._hook(hook, False)
-                self._tail_calls = tail_calls  # measurement: bench.py times a launch alone
+                if self.kernel_hooks:  # measurement only: bench.py times a launch alone
+                    self._tail_calls = tail_calls
                 # (dbg_skip_fullres: measurement only — drops the deferred full-resolution
                 # outputs to price their side-stream contention; outputs are then incomplete)
                 pending = [] if self.dbg_skip_fullres else fc

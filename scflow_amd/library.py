@@ -147,6 +147,12 @@ def _corr_lookup_backward(ctx, dout):
     if not ac:
         raise NotImplementedError("scflow::corr_lookup backward: align_corners=True only "
                                   "(SCFlow's configuration)")
+    if ctx.needs_input_grad[1]:
+        # grid_sample would also give the sampling coordinates a gradient (corr_lookup.py:
+        # 102-136); every SCFlow caller detaches the flow first (scflow_decoder.py:193-194), and a
+        # silent zero gradient would be wrong, so an attached flow is an error
+        raise NotImplementedError("scflow::corr_lookup backward: no gradient w.r.t. flow — "
+                                  "detach the flow (as SCFlowDecoder does)")
     return corr_lookup_backward(dout, flow, numel, L, r), None, None, None, None
 
 

@@ -141,21 +141,15 @@ def _grad_sink(t: Optional[Tensor]) -> Optional[Tensor]:
 # A/B switches (tools/train_bench.py runs): SCFLOW_DEFER_LINEAR=0 / SCFLOW_THIN_DX_GEMM=0
 _DEFER_LINEAR = os.environ.get("SCFLOW_DEFER_LINEAR", "1") != "0"
 _THIN_DX_GEMM = os.environ.get("SCFLOW_THIN_DX_GEMM", "1") != "0"
-_RELU_MASK_FUSED = os.environ.get("SCFLOW_TRAIN_RELU_MASK", "0") == "1"  # A/B switch (tuning)
 
 _ACT_FN = {None: lambda v: v, "ReLU": torch.relu, "Sigmoid": torch.sigmoid, "Tanh": torch.tanh}
 
 
 def _act_backward(dy: Tensor, y: Tensor, act: Optional[str]) -> Tensor:
-    """Gradient through act given its OUTPUT y (ReLU: y > 0; sigmoid: y(1−y); tanh: 1−y²).  A
-    ReLU gradient its single consumer conv already masked in its dX epilogue (tagged with the
-    tensor's version at that point: any later in-place accumulation moves the version) passes
-    through unchanged."""
+    """Gradient through act given its OUTPUT y (ReLU: y > 0; sigmoid: y(1−y); tanh: 1−y²)."""
     if act is None:
         return dy
     if act == "ReLU":
-        if getattr(dy, "_scflow_relu_masked", None) == dy._version:
-            return dy
         return torch.ops.aten.threshold_backward(dy, y, 0.0)
     if act == "Sigmoid":
         return torch.ops.aten.sigmoid_backward(dy, y)
@@ -216,14 +210,11 @@ def _src(t: Optional[Tensor]):
 
 def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tensor], stride: int,
                   pad: Tuple[int, int], act: Optional[str] = None,
-                  bias_map: Optional[Tensor] = None, wkey: Optional[Tensor] = None,
-                  relu_gate: Optional[Tensor] = None) -> Tensor:
+                  bias_map: Optional[Tensor] = None, wkey: Optional[Tensor] = None) -> Tensor:
     """act(conv(cat[x0, x1]) + b + bias_map) of channels-last inputs on the HIP conv variant
     that supports the shape; act and bias_map are fused into the epilogue where the variant has
     one, applied after it otherwise.  ``wkey``: the weight tensor object whose version keys the
-    cached packed forms (default ``w``).  ``relu_gate`` [N, OH, OW, cout]: the result is zeroed
-    where relu_gate ≤ 0 (a dX conv applying its input ReLU's backward: fused into the
-    F(2×2,3×3) Winograd epilogue, SCFLOW_EPI_RELU_MASK, else applied after)."""
+    cached packed forms (default ``w``)."""
     wkey = w if wkey is None else wkey
     n, h, wd, c0 = x0.shape
     c1 = 0 if x1 is None else x1.shape[-1]
@@ -244,15 +235,10 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
         try:
             packed = _cached(wkey, ("conv", c0, c1, wd, bk),
                              lambda: ops.pack_conv_weight(w.float(), c0, c1, wd, 1, bk))
-            gate_fused = relu_gate is not None and bk == _lib.CONV_WINO and kh == kw == 3
             ops.conv2d(_chan(x0), packed, b, n, h, wd, cout, kh, kw, ph, pw, act,
                        out=Chan.whole(out.view(-1, cout)), bk=bk,
                        src1=None if x1 is None else _chan(x1),
-                       bias_map=None if bias_map is None else Chan.whole(bias_map.reshape(-1, cout)),
-                       epilogue=_lib.EPI_RELU_MASK if gate_fused else _lib.EPI_PLAIN,
-                       gate=_chan(relu_gate) if gate_fused else None)
-            if relu_gate is not None and not gate_fused:
-                out = torch.ops.aten.threshold_backward(out, relu_gate, 0.0)
+                       bias_map=None if bias_map is None else Chan.whole(bias_map.reshape(-1, cout)))
             return out
         except ScflowError:
             pass
@@ -291,8 +277,6 @@ def _conv_forward(x0: Tensor, x1: Optional[Tensor], w: Tensor, b: Optional[Tenso
         if bias_map is not None:
             out += bias_map
         out = _ACT_FN[act](out)
-    if relu_gate is not None:
-        out = torch.ops.aten.threshold_backward(out, relu_gate, 0.0)
     return out
 
 
@@ -506,7 +490,6 @@ class ResidualGrad:
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, x1, w, b, bias_map, stride, ph, pw, act, res_grad=None):
-        relu_in = getattr(x0, "_scflow_relu_out", False)  # x0 = a ReLU conv's output
         x0 = _chan_or_contiguous(x0)  # channel slices of a wider buffer are read in place
         x1 = None if x1 is None else _chan_or_contiguous(x1)
         y = _conv_forward(x0, x1, w.detach().contiguous(), None if b is None else b.detach().contiguous(),
@@ -518,7 +501,6 @@ class _Conv2dNHWC(torch.autograd.Function):
         kh, kw = w.shape[2], w.shape[3]
         ctx.uses = _use_holder(w) if _batchable(kh, kw, stride, ph, pw) and w.requires_grad else None
         ctx.res_grad = res_grad
-        ctx.relu_in = relu_in and _RELU_MASK_FUSED
         return y
 
     @staticmethod
@@ -559,11 +541,6 @@ def _conv_backward(ctx, dy):
     _, oh, ow, _ = g.shape
     dx0 = dx1 = dw = db = None
     dbm = g if ctx.needs_input_grad[4] else None
-    # x0 is a ReLU conv's output read by this conv alone in this pass's graph as far as this conv
-    # knows: apply that ReLU's backward here (dX epilogue) and tag the result so the producer
-    # skips its own threshold (idempotent, so a second application elsewhere stays correct)
-    relu_in = getattr(ctx, "relu_in", False) and x1 is None
-    relu_done = False
     hold = getattr(ctx, "res_grad", None)
     dres = None if hold is None else hold.d  # the identity's gradient, added into dX (ResidualGrad)
     if hold is not None:
@@ -585,10 +562,14 @@ def _conv_backward(ctx, dy):
             cols = ops.gemm(g.view(-1, cout), wm)
             dx = ops.col2im(cols, n, h, wd, cin, kh, kw, 1, ph, pw)
         elif s == 1:  # a 'same' conv of dY with the flipped, transposed weights
-            dx = _conv_forward(gp, None, _flip_t(w, pad_co), None, 1, (kh - 1 - ph, kw - 1 - pw),
-                               bias_map=dres, relu_gate=x0 if relu_in else None)
+            # its padding is k−1−p; a conv padded by more than k−1 (p = k−1+e) has an adjoint
+            # with padding −e, i.e. the unpadded conv of dY cropped by e on each side
+            ey, ex = max(0, ph - (kh - 1)), max(0, pw - (kw - 1))
+            gin = gp if ey == ex == 0 else gp[:, ey:oh - ey, ex:ow - ex].contiguous()
+            dx = _conv_forward(gin, None, _flip_t(w, pad_co), None, 1,
+                               (max(0, kh - 1 - ph), max(0, kw - 1 - pw)),
+                               bias_map=dres)
             dres = None
-            relu_done = relu_in
         else:
             # strided: cols = dY·Wmat (exactly the products the transposed conv needs, no
             # zero-inserted grid) and the col2im gather onto the input grid
@@ -599,8 +580,6 @@ def _conv_backward(ctx, dy):
             dx = dx + dres
         dx0 = dx if x1 is None else dx[..., :c0]
         dx1 = None if x1 is None else dx[..., c0:]
-        if relu_done:
-            dx0._scflow_relu_masked = dx0._version
     want_b = ctx.has_b and ctx.needs_input_grad[3]
     hold = getattr(ctx, "uses", None)
     sw = _grad_sink(w) if ctx.needs_input_grad[2] else None
@@ -724,10 +703,7 @@ def conv2d_nhwc(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None, stride
     ``bias_map``: an [N, OH, OW, cout] tensor added before the activation; ``res_grad``: a
     ResidualGrad whose identity gradient this conv's dX adds (x is a residual block's input)."""
     ph, pw = (padding, padding) if isinstance(padding, int) else padding
-    y = _Conv2dNHWC.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act, res_grad)
-    if act == "ReLU":
-        y._scflow_relu_out = True  # its consumer conv may fold the ReLU's backward into its dX
-    return y
+    return _Conv2dNHWC.apply(x, x1, weight, bias, bias_map, stride, ph, pw, act, res_grad)
 
 
 # ------------------------------------------------------------------------------- ConvGRU step

@@ -32,9 +32,9 @@ Tensor = torch.Tensor
 _GRU_FUSED = os.environ.get("SCFLOW_TRAIN_GRU_FUSED", "1") != "0"  # A/B switch (tuning)
 _FUSED_LOSS = os.environ.get("SCFLOW_TRAIN_FUSED_LOSS", "1") != "0"  # A/B switch (tuning)
 _GN_FUSED = os.environ.get("SCFLOW_TRAIN_GN_FUSED", "1") != "0"  # A/B switch (tuning)
-_RES_GRAD = os.environ.get("SCFLOW_TRAIN_RES_GRAD", "0") == "1"  # A/B switch (tuning)
-_BN_FUSED = os.environ.get("SCFLOW_TRAIN_BN_FUSED", "0") == "1"  # A/B switch (tuning)
-_HEADS_FUSED = os.environ.get("SCFLOW_TRAIN_HEADS_FUSED", "0") == "1"  # A/B switch (tuning)
+_RES_GRAD = os.environ.get("SCFLOW_TRAIN_RES_GRAD", "1") != "0"  # A/B switch (tuning)
+_BN_FUSED = os.environ.get("SCFLOW_TRAIN_BN_FUSED", "1") != "0"  # A/B switch (tuning)
+_HEADS_FUSED = os.environ.get("SCFLOW_TRAIN_HEADS_FUSED", "1") != "0"  # A/B switch (tuning)
 
 
 def _act(x: Tensor, act) -> Tensor:

@@ -1,6 +1,7 @@
 """One training iteration of the refinement model (the reference runs it
 through mmengine's OptimWrapper: configs/refine_models/scflow_ycbv_real.py:285-305 — AdamW
-lr 4e-4, betas (0.9, 0.999), eps 1e-8, weight decay 1e-4, clip_grad max_norm 10, OneCycleLR).
+lr 4e-4, betas (0.9, 0.999), eps 1e-8, weight decay 1e-4, clip_grad max_norm 10, and the
+OneCycleLR schedule of :299-306 — schedule.py — stepped once per iteration).
 
 Data parallel = one process per GPU (torch.distributed over RCCL).  Gradients live in a few
 flat fp32 buckets (every ``param.grad`` is a view into one), so the exchange is one all-reduce
@@ -23,6 +24,7 @@ import torch.distributed as dist
 from .._lib import bump_weights_generation
 from .functions import capture_cache, direct_weight_grads
 from .model import refiner_train_forward
+from .schedule import OneCycleLR, reference_schedule
 
 Tensor = torch.Tensor
 _MT_BACKWARD = os.environ.get("SCFLOW_TRAIN_MT_BACKWARD", "1") == "1"  # A/B switch (tuning)
@@ -118,13 +120,18 @@ class TrainStep:
     call with the batch copied into the captured input buffers; the gradient all-reduce stays
     eager between two replays, and clipping + AdamW (``capturable``: step counts on the device)
     are a second captured graph.  The weights are re-packed inside the graph, so optimizer
-    updates are seen by every replay.  Every kernel of the forward + backward is one of ours (no vendor
+    updates are seen by every replay.  The learning rate is a device tensor in graph mode (the
+    schedule's value is written into it before every step, so the captured AdamW reads it), a
+    float in eager mode.  ``lr_schedule``: "onecycle" (default: the configured OneCycleLR with
+    ``eta_max = lr``, ``total_steps``, ``pct_start`` and linear annealing), a ``OneCycleLR``-like
+    object with ``lr_at(step)``, or None for a constant ``lr``.  Every kernel of the forward + backward is one of ours (no vendor
     GEMM: see functions.py), and eager steps and the capture run on the step's own stream."""
 
     def __init__(self, refiner, model_points: Sequence[Tensor], diameters: Sequence[float],
                  lr: float = 4e-4, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_norm: float = 10.0, bucket_bytes: int = 8 << 20, iters: Optional[int] = None,
-                 group=None, overlap: bool = False, graph: bool = False) -> None:
+                 group=None, overlap: bool = False, graph: bool = False,
+                 lr_schedule="onecycle", total_steps: int = 100100, pct_start: float = 0.05) -> None:
         self.refiner = refiner
         self.graph = graph
         self._g = None
@@ -137,11 +144,21 @@ class TrainStep:
         self.diameters = list(diameters)
         self.max_norm = max_norm
         self.iters = iters
+        if lr_schedule == "onecycle":
+            lr_schedule = (reference_schedule(lr) if (total_steps, pct_start) == (100100, 0.05) else
+                           OneCycleLR(lr, total_steps, pct_start, anneal_strategy="linear"))
+        self.lr_schedule = lr_schedule
+        self.iteration = 0  # training iterations taken (the schedule's step)
         params = trainable_parameters(refiner)
         self.grads = GradBuckets(params, bucket_bytes, group, overlap)
-        self.opt = torch.optim.AdamW(self.grads.params, lr=lr, betas=betas, eps=eps,
-                                     weight_decay=weight_decay, foreach=True, capturable=graph)
         dev = self.grads.params[0].device
+        lr0 = lr if lr_schedule is None else lr_schedule.lr_at(0)
+        self._lr_const = float(lr)
+        # graph mode: the captured AdamW must read the lr from memory
+        self._lr_t = torch.tensor(lr0, dtype=torch.float32, device=dev) if graph else None
+        self.opt = torch.optim.AdamW(self.grads.params, lr=lr0 if self._lr_t is None else self._lr_t,
+                                     betas=betas, eps=eps, weight_decay=weight_decay, foreach=True,
+                                     capturable=graph)
         self.stream = torch.cuda.Stream(device=dev)
         self.diam_t = torch.as_tensor(self.diameters, dtype=torch.float32, device=dev)
         if dist.is_initialized() and dist.get_world_size(group) > 1:
@@ -151,6 +168,23 @@ class TrainStep:
         """Start every rank from rank 0's weights and BN statistics."""
         for t in list(self.refiner.parameters()) + list(self.refiner.buffers()):
             dist.broadcast(t.data, src, group=self.grads.group)
+
+    @property
+    def lr(self) -> float:
+        """The learning rate of the next step."""
+        if self.lr_schedule is None:
+            return self._lr_const
+        return self.lr_schedule.lr_at(self.iteration)
+
+    def _set_lr(self) -> None:
+        if self.lr_schedule is None:
+            return
+        v = self.lr_schedule.lr_at(self.iteration)
+        if self._lr_t is not None:
+            self._lr_t.fill_(v)  # stream-ordered write (no host sync), read by the captured AdamW
+        else:
+            for g in self.opt.param_groups:
+                g["lr"] = v
 
     def _fwd_bwd(self, batch: Dict[str, Tensor]) -> Dict[str, Tensor]:
         self.grads.zero()
@@ -215,11 +249,15 @@ class TrainStep:
         after and before the caller's current stream."""
         self.refiner.train()
         self._calls += 1
+        lr = self.lr
+        self._set_lr()
         cur = torch.cuda.current_stream(self.stream.device)
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             out = self._step(batch)
         cur.wait_stream(self.stream)
+        out["lr"] = lr
+        self.iteration += 1
         return out
 
 

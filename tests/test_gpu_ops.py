@@ -617,12 +617,15 @@ def test_corr_lookup_far_out_of_bounds(ops):
     assert (out[0, :, :8].abs().max() == 0)
 
 
-def test_corr_lookup_tiled_far_out_of_bounds(ops):
-    """The tiled lookup (16×16 tile-aligned regions, b128 tile-row loads) on flows that push
-    windows off the map, straddle its edges at every tile phase, or are not finite: exactly the
-    row-major lookup's output (the same taps and arithmetic, only staged differently)."""
+@pytest.mark.parametrize("h,w", [(32, 32), (64, 64), (64, 32)])
+def test_corr_lookup_tiled_far_out_of_bounds(ops, h, w):
+    """The tiled lookup — 16×16 tile-aligned regions (maps ≤ 32²) or 12×12 regions filled from
+    the tile rows of the taps' exact extent (larger maps) — on flows that push windows off the
+    map, straddle its edges at every tile phase, sit on integers (zero flow: the coordinate round
+    trip moves floors), or are not finite: exactly the row-major lookup's output (the same taps
+    and arithmetic, only staged differently)."""
     g = torch.Generator().manual_seed(19)
-    n, h, w, L = 2, 32, 32, 4
+    n, L = 2, 4
     f1 = torch.randn(n, 16, h, w, generator=g).cuda()
     f2 = torch.randn(n, 16, h, w, generator=g).cuda()
     _, lv = ops.corr_pyramid(f1, f2, L)
@@ -631,7 +634,8 @@ def test_corr_lookup_tiled_far_out_of_bounds(ops):
     flow = torch.zeros(n, 2, h, w)
     flow[0, 0, :4] = 1e4
     flow[0, 1, 4:8] = -1e4
-    flow[0, :, 8:16] = torch.arange(8 * 32 * 2, dtype=torch.float32).view(2, 8, 32) * 0.125 - 32
+    flow[0, :, 8:16] = torch.arange(8 * w * 2, dtype=torch.float32).view(2, 8, w) * 0.125 - 32
+    flow[0, :, 22:] = 0.0
     flow[0, :, 16:20] = float(h) - 0.5
     flow[0, 0, 20, :8] = float("nan")
     flow[0, 1, 20, 8:16] = float("inf")

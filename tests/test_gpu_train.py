@@ -126,7 +126,7 @@ def test_train_step_reduces_loss():
     batch, points, diam = train_batch(2, 256, seed=6)
     gb = {k: v.cuda() for k, v in batch.items()}
     rm0 = r.context.norm1.running_mean.clone()
-    step = TrainStep(r, [p.cuda() for p in points], diam)
+    step = TrainStep(r, [p.cuda() for p in points], diam, lr_schedule=None)  # constant 4e-4
     losses = [float(step(gb)["loss"].detach()) for _ in range(4)]
     torch.cuda.synchronize()
     assert losses[-1] < losses[0], losses
@@ -192,11 +192,15 @@ def test_train_step_graph_optimizer_update_and_weight_caches():
     r.eval()
     r.get_pose(**pose_in)  # fills the inference caches at the initial weights
     lr, wd, max_norm = 1e-3, 1e-2, 10.0
-    step = TrainStep(r, pts, diam, lr=lr, weight_decay=wd, max_norm=max_norm, graph=True)
-    for _ in range(3):  # eager 1-2, capture + replay on 3
-        step(gb)
+    # OneCycleLR over 20 steps: the lr moves every step, so the replay must read the scheduled
+    # value the step writes into the captured optimizer's lr tensor
+    step = TrainStep(r, pts, diam, lr=lr, weight_decay=wd, max_norm=max_norm, graph=True,
+                     total_steps=20, pct_start=0.3)
+    seen = [step(gb)["lr"] for _ in range(3)]  # eager 1-2, capture + replay on 3
     torch.cuda.synchronize()
     assert step._g is not None and step._g_opt is not None
+    assert seen == [step.lr_schedule.lr_at(k) for k in range(3)] and len(set(seen)) == 3
+    lr = step.lr  # the spied step's scheduled lr
     params = step.grads.params
     snap = {}
 

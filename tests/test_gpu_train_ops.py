@@ -102,7 +102,6 @@ def test_conv2d_nhwc_fused_act_two_sources_bias_map(act, two, bmap):
             _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), name)
 
 
-@pytest.mark.optin
 def test_dual_conv_heads_and_channel_slice_consumers():
     """dual_conv2d_nhwc (the XHeads' hidden convs as one launch each way) and convs reading its
     channel-view outputs in place (the predictors): values and every gradient — x, both weight /
@@ -152,51 +151,6 @@ def test_dual_conv_heads_and_channel_slice_consumers():
         _close(xg[i].grad, xr[i].grad, 1e-5, 1e-4 * np.sqrt(K), f"dx[{i}]")
     for name, a, r in zip(("wa", "ba", "wb", "bb", "wf", "bf", "wm", "bm"), dev, leaves):
         _close(a.grad, r.grad, 1e-5, 1e-4 * np.sqrt(3 * n * h * w), name)
-
-
-@pytest.mark.optin
-@pytest.mark.parametrize("cmid,cout", [(128, 64), (256, 192), (64, 32)])
-def test_relu_mask_folded_into_consumer_dx(cmid, cout, monkeypatch):
-    """A ReLU conv read by one 3×3 conv (the motion encoder's corr_net / flow_net chains): the
-    consumer's dX conv applies the ReLU's backward in its epilogue (SCFLOW_EPI_RELU_MASK) and the
-    producer skips its threshold — every gradient against fp64 autograd, and the fused path
-    really taken (the producer's incoming gradient carries the consumer's tag)."""
-    from scflow_amd.train import functions as fn
-    monkeypatch.setattr(fn, "_RELU_MASK_FUSED", True)
-    g = torch.Generator().manual_seed(cmid + cout)
-    n, h, w, cin = 2, 32, 32, 96
-    x = torch.randn(n, h, w, cin, generator=g)
-    w1 = torch.randn(cmid, cin, 3, 3, generator=g) / np.sqrt(cin * 9)
-    b1 = torch.randn(cmid, generator=g) * 0.1
-    w2 = torch.randn(cout, cmid, 3, 3, generator=g) / np.sqrt(cmid * 9)
-    b2 = torch.randn(cout, generator=g) * 0.1
-    gy = torch.randn(n, h, w, cout, generator=g)
-    ref = [t.double().requires_grad_() for t in (x, w1, b1, w2, b2)]
-    dev = [t.cuda().requires_grad_() for t in (x, w1, b1, w2, b2)]
-    mid = fn.conv2d_nhwc(dev[0], dev[1], dev[2], 1, 1, act="ReLU")
-    y = fn.conv2d_nhwc(mid, dev[3], dev[4], 1, 1, act="ReLU")
-    # ReLU's derivative jumps at 0: the reference takes the device forward's active sets
-    am = (mid.detach().cpu().double() > 0).permute(0, 3, 1, 2)
-    a = F.conv2d(ref[0].permute(0, 3, 1, 2), ref[1], ref[2], padding=1) * am
-    yr = (F.conv2d(a, ref[3], ref[4], padding=1).permute(0, 2, 3, 1)) * (y.detach().cpu().double() > 0)
-    (yr * gy.double()).sum().backward()
-    seen = {}
-    orig = fn._act_backward
-
-    def spy(dy, yy, act):
-        if act == "ReLU" and yy.shape[-1] == cmid:
-            seen["tagged"] = getattr(dy, "_scflow_relu_masked", None) == dy._version
-        return orig(dy, yy, act)
-
-    fn._act_backward = spy
-    try:
-        (y * gy.cuda()).sum().backward()
-    finally:
-        fn._act_backward = orig
-    torch.cuda.synchronize()
-    assert seen.get("tagged"), "the consumer's dX did not carry the ReLU mask to the producer"
-    for name, d, r in zip(("x", "w1", "b1", "w2", "b2"), dev, ref):
-        _close(d.grad, r.grad, 1e-5, 1e-4 * np.sqrt(n * h * w), name)
 
 
 def test_conv_wgrad_accumulate_and_split():
@@ -552,10 +506,12 @@ def test_gru_shared_weights_across_cycles_and_short_passes():
 def test_conv_dx_shortcuts_match_conv2d_input():
     """the 1×1 → 1-channel dX shortcut (dY ⊗ w, unpadded only) and the thin large-
     kernel dX (GEMM + col2im) against torch.nn.grad.conv2d_input, plus a PADDED 1×1 → 1 conv,
-    which must not take the shortcut."""
+    which must not take the shortcut, and convs padded by more than k−1 (their
+    adjoint's padding k−1−p is negative — the cropped unpadded conv of dY)."""
     from scflow_amd.train.functions import conv2d_nhwc
     g = torch.Generator().manual_seed(44)
-    for (cin, cout, k, pad) in ((256, 1, 1, 0), (256, 1, 1, 1), (2, 128, 7, 3)):
+    for (cin, cout, k, pad) in ((256, 1, 1, 0), (256, 1, 1, 1), (2, 128, 7, 3), (64, 4, 1, 1),
+                                (32, 64, 3, 2), (16, 8, 3, 3)):
         x = torch.randn(2, 32, 32, cin, generator=g)
         wt = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
         xg = x.cuda().requires_grad_()
@@ -623,7 +579,6 @@ def test_instance_norm_nhwc_forward_backward(n, h, w, c, relu):
 @pytest.mark.parametrize("n,h,w,c,mode", [(4, 64, 64, 64, "relu"), (3, 32, 32, 96, "plain"),
                                           (2, 16, 16, 128, "res"), (16, 32, 32, 64, "res"),
                                           (2, 8, 12, 4, "relu")])
-@pytest.mark.optin
 def test_batch_norm_nhwc_train(n, h, w, c, mode):
     """HIP BatchNorm2d in train mode (the context encoder's norms; + ReLU, or + a residual before
     the ReLU): output, running statistics and the gradients of x, γ, β (and the residual) against

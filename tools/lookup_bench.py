@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="per-workgroup phase stamps of one launch")
+    ap.add_argument("--flow-scale", type=float, default=6.0, help="flow = randn · scale (px)")
     a = ap.parse_args()
     from scflow_amd import ops
     from scflow_amd.ops import Chan
@@ -29,7 +31,7 @@ def main():
     f1 = torch.randn(n, c, h, w, device=dev, generator=g)
     f2 = torch.randn(n, c, h, w, device=dev, generator=g)
     pyr = ops.corr_pyramid_tiled(f1, f2, L)
-    flow = (torch.randn(n, h, w, 2, device=dev, generator=g) * 6).contiguous()
+    flow = (torch.randn(n, h, w, 2, device=dev, generator=g) * a.flow_scale).contiguous()
     K = L * (2 * r + 1) ** 2
     out = torch.empty(n * h * w, K, device=dev)
     ch = Chan.whole(out)
@@ -52,6 +54,22 @@ def main():
     print(f"lookup n={n} {h}x{w} L={L} r={r}: {ms * 1e3:.1f} us/launch, "
           f"{nbytes / 1e6:.1f} MB algorithmic, {nbytes / ms / 1e6:.0f} GB/s "
           f"({nbytes / ms / 1e6 / 8000:.3f} of 8 TB/s)")
+    if a.stamps:
+        from scflow_amd import _lib
+        lib = _lib.load()
+        nwg = -(-n * h * w // 16)
+        st = torch.zeros(nwg * 6, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        lib.scflow_debug_lookup_stamps(st.data_ptr())
+        run()
+        torch.cuda.synchronize()
+        lib.scflow_debug_lookup_stamps(None)
+        v = st.view(-1, 6).double().cpu() / 100.0  # 100 MHz ticks → µs
+        t0 = v[:, 0].min()
+        names = ("coords", "loads", "lds", "samples", "stores")
+        ph = " ".join(f"{nm} {(v[:, i + 1] - v[:, i]).median().item():5.2f}" for i, nm in enumerate(names))
+        print(f"  {nwg} WGs span {(v[:, 5].max() - t0).item():7.2f} us, WG median {(v[:, 5] - v[:, 0]).median().item():5.2f} us; "
+              f"phase medians (us): {ph}")
     if a.check:
         ref = torch.empty_like(out)
         flat = torch.cat([v.reshape(-1) for v in ops.untile_pyramid(pyr, n, h, w, L)])
