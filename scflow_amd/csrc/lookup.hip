@@ -115,6 +115,9 @@ constexpr int LK_SLOTS = 4 * LK_PPW;   // pixels per workgroup
 // floats of one pixel slot (all levels), ≡ 4 mod 8: 16-B aligned slots whose 4 per wave start
 // in different banks.
 __host__ __device__ inline bool lk_whole(int hl, int wl, int win) { return hl + 2 <= win && wl + 2 <= win; }
+// region row length: tile regions 16; tile-row regions (TB, origin at the lowest tap) 2r + 3;
+// plain regions (origin one tap below the first sample's floor) 2r + 4
+__host__ __device__ constexpr int lk_win(int r, bool tr, bool tb) { return tr ? 16 : (tb ? 2 * r + 3 : 2 * r + 4); }
 __host__ __device__ inline int lk_rows(int hl, int wl, int win) { return lk_whole(hl, wl, win) ? hl + 2 : win; }
 __host__ __device__ inline int lk_slot_floats(int h, int w, int L, int win) {
   int t = 0;
@@ -135,6 +138,20 @@ constexpr int LK_OOB = 0x7ffffff0;  // buffer voffset of a zero tap (beyond any 
 constexpr int LK_TRW = 16;
 __host__ __device__ inline int lk_tr_slot_floats(int L) { return L * LK_TRW * LK_TRW + 16; }
 
+// A pixel's coordinates, floors and regions are written and read only by its own 16 lanes (one
+// wave): the tile-row kernel (TB) orders its phases with a wave-level LDS barrier, so the 4 waves
+// of a workgroup run their phases independently instead of meeting at every block barrier.
+template <bool WAVE>
+__device__ __forceinline__ void lk_sync() {
+  if constexpr (WAVE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ float lk_bload(__amdgpu_buffer_rsrc_t r, int voff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
 }
@@ -149,16 +166,16 @@ __device__ __forceinline__ float lk_bload(__amdgpu_buffer_rsrc_t r, int voff) {
 //
 // TILED: the pyramid's maps are in 4×4 tiles of 16 floats (scflow_corr_pyramid_tiled)
 template <int R, bool TILED, bool TR = false, bool TB = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void corr_lookup_lds_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 4 : 3))) void corr_lookup_lds_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
     float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
     int vec_out, int ac, unsigned long long* stamps) {
 #pragma clang fp contract(off)
   constexpr int D = 2 * R + 1;
-  constexpr int WIN = TR ? LK_TRW : D + 3;  // LDS row length of a level's region
+  constexpr int WIN = lk_win(R, TR, TB);  // LDS row length of a level's region
   static_assert(!TR || (TILED && D + 3 <= LK_TRW - 3), "tile regions: tiled maps, r <= 4");
-  static_assert(!TB || (TILED && !TR && WIN <= 12),
-                "tile-row regions: tiled maps, plain regions of at most 12 columns (r <= 4)");
+  static_assert(!TB || (TILED && !TR && WIN <= 13),
+                "tile-row regions: tiled maps, plain regions of at most 13 columns (r <= 5)");
   // profiling (scflow_debug_lookup_stamps): thread 0's real-time-clock stamps at the phase
   // boundaries, 6 per workgroup
   auto stamp = [&](int k) {
@@ -168,7 +185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   constexpr int NPR = (LK_MAXL * D + LK_GL - 1) / LK_GL;  // (level, a) pairs per lane
   extern __shared__ float win[];  // [LK_SLOTS][slot floats]
   __shared__ float crd[LK_SLOTS][LK_MAXL][2][D];
-  __shared__ int sr[LK_SLOTS][LK_MAXL][2][D];  // region-relative floor of a sample, −1: none
+  __shared__ signed char sr[LK_SLOTS][LK_MAXL][2][D];  // region-relative floor of a sample, −1: none
   __shared__ int org[LK_SLOTS][LK_MAXL][2];    // region origin (map coordinates)
   __shared__ int ext[LK_SLOTS][LK_MAXL][2][2];  // TB: taps read, [lo, hi] (map coordinates)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -201,7 +218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     const float c = ((float)(axis == 0 ? x : y) + (axis == 0 ? fx : fy)) / (float)(1 << l);
     crd[slot][l][axis][i] = unnorm_coord(c + (float)(i - R), size, ac);
   }
-  __syncthreads();
+  lk_sync<TB>();
   stamp(1);
   // 1b. per (level, axis): the region origin — −1 for a whole map, else floor(first sample) − 1
   //     (one-tap margin: a rounded sample coordinate moves its floor by at most one), far out
@@ -214,30 +231,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     const bool fin = isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f && fabsf(c0y) < 1e8f;
     const float s = crd[slot][l][axis][i];
     int o = whole ? -1 : (fin ? (int)floorf(axis == 0 ? c0x : c0y) - 1 : -(1 << 29));
+    // TB: the taps the samples read on this axis, [lo, hi] = [min floor, max floor + 1] over the
+    // finite samples; the region starts at lo (D + 2 columns hold them: 9 samples at most
+    // size/(size−1) < (D+1)/D apart on a windowed axis span < D columns)
+    int lo = 1 << 30, hi = -(1 << 30);
+    if (TB && fin) {
+      for (int j = 0; j < D; ++j) {
+        const float sj = crd[slot][l][axis][j];
+        if (isfinite(sj)) {
+          const int f = (int)floorf(sj);
+          lo = min(lo, f);
+          hi = max(hi, f + 1);
+        }
+      }
+      if (!whole) o = lo;
+    }
     // tile regions: an axis of at most 8 is held whole with a one-tile zero border ([−4, 12)),
     // else from the tile holding floor(first sample) − 1 (arithmetic shift: floor for negatives);
     // 9 samples spaced size/(size−1) ≤ 12/11 apart then end at most 14 columns into the region
     if (TR) o = ((axis == 0 ? W : H) >> l) <= 8 ? -4 : (o >> 2) << 2;
-    sr[slot][l][axis][i] = fin && isfinite(s) ? (int)floorf(s) - o : -1;
+    // region-relative floor; anything outside [−1, WIN) is a sample with a tap off the region
+    // (zero: the map's padding) — kept as −1 so it fits a byte
+    const int rel = fin && isfinite(s) ? (int)floorf(s) - o : -1;
+    sr[slot][l][axis][i] = (signed char)(rel >= 0 && rel < WIN ? rel : -1);
     if (i == 0) org[slot][l][axis] = o;
     if (TB && i == 0) {
-      // the taps the samples read on this axis: floor and floor + 1 of every finite sample
-      int lo = 1 << 30, hi = -(1 << 30);
-      if (fin) {
-        for (int j = 0; j < D; ++j) {
-          const float sj = crd[slot][l][axis][j];
-          if (isfinite(sj)) {
-            const int f = (int)floorf(sj);
-            lo = min(lo, f);
-            hi = max(hi, f + 1);
-          }
-        }
-      }
       ext[slot][l][axis][0] = lo;
       ext[slot][l][axis][1] = hi;
     }
   }
-  __syncthreads();
+  lk_sync<TB>();
   // 2. regions (zero padded) through buffer loads (out-of-map taps read as zero, no branches):
   //    every load of the pixel's L regions is issued before the LDS writes
   int rn[LK_MAXL], ox[LK_MAXL], oy[LK_MAXL];
@@ -385,7 +408,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     }
   }
   }
-  __syncthreads();
+  lk_sync<TB>();
   stamp(3);
   // 3. samples: the pixel's 16 lanes take its L·D (level, a) pairs in turn and produce the D
   //    samples b of each (channel k = l·D² + a·D + b samples x+a−r, y+b−r); a sample whose
@@ -399,6 +422,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
       offl[l] = o;
       o += rn[l];
     }
+  }
+  if constexpr (TB) {
+    // level by level, sample s = gl + 16j of the level's D² (a = s / D, b = s % D: channel
+    // l·D² + s), so the pixel's 16 lanes produce 16 consecutive output channels per round and
+    // store them straight to memory (64 contiguous bytes per pixel, channels-last); no result
+    // registers, no staging pass.  Region origin = the lowest tap, so the floors are ≈ (b, a)
+    // and the 4 tap reads of a round hit a fixed bank pattern.
+    if (!active) return;
+    float* o = out_layout == SCFLOW_LAYOUT_NHWC ? out + ((size_t)n * P + p) * out_stride
+                                                : out + (size_t)n * L * D * D * P + p;
+    const size_t ostep = out_layout == SCFLOW_LAYOUT_NHWC ? 1 : (size_t)P;
+    constexpr int NJ = (D * D + LK_GL - 1) / LK_GL;
+#pragma unroll
+    for (int l = 0; l < LK_MAXL; ++l) {
+      if (l >= L) break;
+      const int off = offl[l], rows = rn[l] / WIN;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int sidx = gl + LK_GL * j;
+        if (D * D % LK_GL != 0 && sidx >= D * D) break;
+        const int a = sidx / D, b = sidx - a * D;
+        const int rx = sr[slot][l][0][a], ry = sr[slot][l][1][b];
+        const float ix = crd[slot][l][0][a], iy = crd[slot][l][1][b];
+        const bool ok = rx >= 0 && rx + 1 < WIN && ry >= 0 && ry + 1 < rows;
+        const float* wr = sw + off + (ok ? ry * WIN + rx : 0);
+        const float t00 = wr[0], t01 = wr[1], t10 = wr[WIN], t11 = wr[WIN + 1];
+        const float ix_w = floorf(ix), ix_e = ix_w + 1.f;
+        const float wxw = ix_e - ix, wxe = ix - ix_w;
+        const float iy_n = floorf(iy), iy_s = iy_n + 1.f;
+        const float wyn = iy_s - iy, wys = iy - iy_n;
+        float v = 0.f;
+        v += t00 * (wxw * wyn);
+        v += t01 * (wxe * wyn);
+        v += t10 * (wxw * wys);
+        v += t11 * (wxe * wys);
+        o[(size_t)(l * D * D + sidx) * ostep] = ok ? v : 0.f;
+      }
+    }
+    if (stamps) {
+      __builtin_amdgcn_s_waitcnt(0);
+      stamp(4);
+      stamp(5);
+    }
+    return;
   }
   float res[NPR][D];
 #pragma unroll
@@ -561,11 +628,16 @@ static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layo
       return scflow_launch_status();
     }
     if (tiled && lk_tile_rows()) {
+      const int sf_tb = lk_slot_floats(h, w, num_levels, lk_win(radius, false, true));
+      const size_t lds_tb = sizeof(float) * LK_SLOTS * sf_tb;
+      const int vec_tb = vec || (out_layout == SCFLOW_LAYOUT_NHWC && out_stride % 4 == 0 &&
+                                 ((uintptr_t)out & 15) == 0 && sf_tb >= num_levels * D * D);
+      const int vtb = vec_tb && sf_tb >= num_levels * D * D;
       switch (radius) {
-        case 1: corr_lookup_lds_kernel<1, true, false, true><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac, g_lk_stamps); break;
-        case 2: corr_lookup_lds_kernel<2, true, false, true><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac, g_lk_stamps); break;
-        case 3: corr_lookup_lds_kernel<3, true, false, true><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac, g_lk_stamps); break;
-        default: corr_lookup_lds_kernel<4, true, false, true><<<blk, 256, lds, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vec, ac, g_lk_stamps); break;
+        case 1: corr_lookup_lds_kernel<1, true, false, true><<<blk, 256, lds_tb, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vtb, ac, g_lk_stamps); break;
+        case 2: corr_lookup_lds_kernel<2, true, false, true><<<blk, 256, lds_tb, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vtb, ac, g_lk_stamps); break;
+        case 3: corr_lookup_lds_kernel<3, true, false, true><<<blk, 256, lds_tb, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vtb, ac, g_lk_stamps); break;
+        default: corr_lookup_lds_kernel<4, true, false, true><<<blk, 256, lds_tb, st>>>(pyr, flow, flow_layout, out, out_layout, out_stride, n, h, w, num_levels, vtb, ac, g_lk_stamps); break;
       }
       return scflow_launch_status();
     }

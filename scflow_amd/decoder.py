@@ -99,10 +99,12 @@ class SCFlowDecoder(nn.Module):
         # launch (scflow_pose_step); only without flow/correlation masking
         self.fuse_tail = True
         # the lookup and corr_net.0 (1×1 324→256) as ONE launch (scflow_corr_lookup_conv1x1: the
-        # correlation features stay in LDS) when the geometry allows (tiled pyramid, L = 4, r = 4).
-        # Opt-in: the producer / consumer-wave version is not yet validated on hardware (its
-        # single-role predecessor measured neutral, 5.116 vs 5.117 ms/forward)
-        self.fuse_lookup_conv = False
+        # correlation features stay in LDS) when the geometry allows (tiled pyramid, L = 4, r = 4)
+        # and the feature map has at most 32×32 pixels: measured 5.112 vs 5.131 ms/forward at
+        # configs[1] (round 5, tools/sess_r5d.sh), but 49.2 vs 48.0 ms at configs[4] (64×64),
+        # where the separate lookup (tile-row regions) and 1×1 conv win
+        self.fuse_lookup_conv = True
+        self.fuse_lookup_conv_max_px = 32 * 32
         # a batch of ≥ 2·pingpong_min pairs runs as two interleaved halves (_forward_pingpong).
         # Off: measured slower at B=16 (5.76 vs 5.33 ms/step) — a half's tail kernels do not get
         # CUs while the other half's convolutions hold every CU's LDS, so they serialise anyway
@@ -471,7 +473,8 @@ class SCFlowDecoder(nn.Module):
 
         corr_net = self.encoder.corr_net
         c0m = corr_net[0].conv
-        fuse_lc = (self.fuse_lookup_conv and tiled and not self.mask_corr and len(corr_net) == 2 and
+        fuse_lc = (self.fuse_lookup_conv and h * w <= self.fuse_lookup_conv_max_px and tiled and
+                   not self.mask_corr and len(corr_net) == 2 and
                    tuple(c0m.kernel_size) == (1, 1) and tuple(c0m.stride) == (1, 1) and
                    tuple(c0m.padding) == (0, 0) and
                    ops.lookup_conv1x1_ok(h, w, self.num_levels, self.radius, c0m.in_channels,

@@ -650,7 +650,6 @@ def test_corr_lookup_tiled_far_out_of_bounds(ops, h, w):
             f"ac={ac}: {(ref - got).abs().nan_to_num().max().item():.3e}"
 
 
-@pytest.mark.optin
 @pytest.mark.parametrize("n,h,w,seed,far", [(2, 32, 32, 61, False), (3, 32, 64, 62, True),
                                             (1, 64, 64, 63, False)])
 def test_corr_lookup_conv1x1_fused_bit_identical(ops, n, h, w, seed, far):
