@@ -197,8 +197,8 @@ def time_fullres_alone(dec, reps=20):
     return t.mean_ms()
 
 
-def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail_weight_bytes=0,
-                        tiled=True, fullres_alone_ms=None):
+def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tiled=True,
+                        fullres_alone_ms=None):
     """The HBM/gather-bound kernels and the correlation GEMM, timed with the same events in an
     untimed pass after the timed region (algorithmic bytes per launch from SURVEY.md §8(d)).
     At B=16, 256² the 86 MB pyramid is Infinity-Cache resident, so the lookup's GB/s is an
@@ -232,11 +232,6 @@ def secondary_rooflines(timers, batch, size, traffic=None, fused_tail=True, tail
             ("pose_step_crit", "pose_step_crit", "pose_step_kernel (a8 + the next iteration's a11 "
              "↓8), its critical-path launch (parts = 2, 7 per forward): latency-bound, 4 "
              "workgroups per pair", "hbm", crit_bytes),
-            # the persistent pose-head tail (GN 1 → convs 2-3 → FCs → heads) + the pose step:
-            # bytes = the pose step's 36 B/pixel + the pose head's weights after conv 1 (read once)
-            ("pose_tail", "ph_tail", "ph_tail_kernel (a7 after conv 1 + a8+a10+a11, one persistent "
-             "launch; latency-bound phases, bytes dominated by the pose step)", "hbm",
-             flow_bytes + tail_weight_bytes),
             ("corr_lookup_conv", "corr_lookup_conv", "corr_lookup_conv1x1_kernel (a2 + corr_net.0 "
              "1x1 324->256 + ReLU in one launch: the window samples go to LDS and straight into "
              "the fp32 MFMA GEMM; frac on the algorithmic flops, bytes_per_launch = window reads + "
@@ -471,7 +466,7 @@ def main():
     # sampled position through the iterations), so an event pair costs ≈ 2 queue packets per
     # step, not 2 per launch.
     per_step = {"heads": args.iters, "corr_net1": args.iters, "gru_zr": 2 * args.iters,
-                "corr_lookup": args.iters, "pose_flow": args.iters, "pose_tail": args.iters,
+                "corr_lookup": args.iters, "pose_flow": args.iters,
                 "pose_step_crit": args.iters, "corr_lookup_conv": args.iters, "corr_pyramid": 1}
     per_step.update({n: args.iters for n in WINO_LAUNCHES[2:]})
     # the headline kernel's launches (every conv_wino_kernel launch of an iteration): bracketed in
@@ -609,11 +604,8 @@ def main():
             "conv_wino5_kernel<·,32,2,GRU_ZR> (SepConvGRU z|r, Winograd F(4,5) on fp32 MFMA)"
             if zr.winograd else "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r, direct)",
             [("gru_zr", zr, hc, zr.cin - hc)], timers, m_px, traffic.get("gru_zr"), alg.get("gru_zr")))
-    ph = dec.pose_pred
-    tail_w = 4 * sum(p.numel() for m in (ph.conv_layers[1:], ph.fc_layers) for p in m.parameters())
-    tail_w += 4 * (ph.rotation_out_channels + 3) * ph.fc_layers[-1][0].out_features  # label[0] rows
     secondary += secondary_rooflines(timers, hb, args.size, traffic,
-                                     getattr(dec, "fuse_tail", True), tail_w, dec.tiled_pyramid,
+                                     getattr(dec, "fuse_tail", True), dec.tiled_pyramid,
                                      fullres_alone)
 
     if rank == 0:

@@ -146,6 +146,9 @@ typedef struct scflow_conv_args {
   const float* out_scale;                /* v ← (conv + bias)·out_scale[o] + out_shift[o]       */
   const float* out_shift;                /* (eval BatchNorm)                                    */
   const float* res; int sres;            /* v += res[pix·sres + o] before the activation        */
+  /* SCFLOW_CONV_WINO4 only (NULL / 0 elsewhere): the transformed-input workspace of at least   */
+  /* scflow_conv_workspace_bytes(args) bytes, 16-B aligned, private to this launch until it ends */
+  float* ws; long long ws_bytes;
 } scflow_conv_args;
 
 /* scflow_conv_args.bk = SCFLOW_CONV_WINO selects the Winograd kernels: F(2×2,3×3) for 3×3, stride
@@ -159,6 +162,15 @@ typedef struct scflow_conv_args {
  * instantiated depths (128, 256, 328), cout ≤ 256, SCFLOW_EPI_PLAIN (bias, bias map, activation);
  * 64 pixels × every output channel per workgroup, the pixels' whole input rows in LDS. */
 #define SCFLOW_CONV_1X1W 3
+/* scflow_conv_args.bk = SCFLOW_CONV_WINO4 selects Winograd F(4×4,3×3) (round 5): 3×3, stride 1,
+ * pad 1, height and width multiples of 4, channels multiples of 4, SCFLOW_EPI_PLAIN (bias, bias
+ * map, residual, eval-BN affine, input IN+ReLU on load with c1 = 0, activation); 2.25 multiplies
+ * per output and tap set (F(2×2,3×3): 4).  Two launches: the input transform into args.ws, then
+ * the 36 point GEMMs with the output transform in their epilogue.  fp32 throughout; error vs fp64
+ * ≈ 10× a direct fp32 conv's (points {0, ±1, 2, −½, ∞}). */
+#define SCFLOW_CONV_WINO4 4
+/* Bytes of args.ws a launch needs (0 for packing formats without a workspace). */
+long long scflow_conv_workspace_bytes(const scflow_conv_args* args);
 
 /* Number of floats of the packed weight buffer for bk 8 and 16 (the same for both); w_oihw is
  * nn.Conv2d's [cout][c0+c1][kh][kw]. */
@@ -232,10 +244,6 @@ int scflow_stream_wait_event(void* stream, void* event);
 /* Timing events (device-scope release; destroy with scflow_sync_event_destroy, record with
  * scflow_sync_event_record); *ms = end − start after waiting for end. */
 int scflow_timing_event_create(void** event);
-/* Uncached (MTYPE UC), zero-filled device memory (every access goes to memory; no cache to
- * write back or invalidate). */
-int scflow_alloc_uncached(long long bytes, void** ptr);
-int scflow_free_uncached(void* ptr);
 int scflow_event_elapsed_ms(void* start, void* end, float* ms);
 
 /* out[n·ons + b·obs + a] = in[n·ins + a·ias + b] for a < A, b < B (batched 2-D transpose; e.g.
@@ -277,62 +285,6 @@ int scflow_ph_gn_reduce(const float* parts, int nsplit, long long split_stride, 
                         int hw, int c, int groups, const float* gamma, const float* beta, float eps,
                         float* scale, float* shift, void* stream);
 int scflow_ph_fc_permute(const float* W, float* Wp, int n, int c, int hw, void* stream);
-/* Fused-statistics pose head (pose_head.py:201-211): every conv writes its RAW output and its
- * GroupNorm partial statistics per output tile, and the consumer (the next conv, or FC1)
- * turns its producer's partials into the GroupNorm affine in its own prologue — no separate
- * GroupNorm launch, no K-split slabs.
- * scflow_ph_gn_tpi(oh, ow): partials per image of a path-0 conv output of oh×ow pixels (oh·ow a
- *   multiple of 32: one per 32-pixel tile; oh·ow = 16: one per image); SCFLOW_EUNSUPPORTED
- *   otherwise.  (Path 1 writes two per output tile; the plan gives tpi for either.)
- * scflow_ph_conv_gn: like scflow_ph_conv (no bias) with the input GroupNorm(in_groups) + ReLU built
- *   from in_stats [n][in_tpi][in_groups][2] (fp64 sum, sum of squares over h·w pixels; NULL: raw
- *   input) and this conv's partials into out_stats [n][plan.tpi][out_groups][2] (NULL: none;
- *   cout % 32 == 0, (cout / out_groups) | 32).  Statistics are summed in fp64 in a fixed order:
- *   deterministic.
- * scflow_ph_fc_split_gn: scflow_ph_fc_split in GN mode (x = a conv's raw channels-last output,
- *   gn_c channels, W permuted by scflow_ph_fc_permute) with the GroupNorm affine built from that
- *   conv's partials (stats [m][tpi][groups][2] over hw pixels; m·gn_c ≤ 4096). */
-typedef struct scflow_ph_conv_gn_args {
-  const float* src0; int c0, s0;
-  const float* src1; int c1, s1;
-  const double* in_stats; int in_tpi, in_groups;
-  const float* in_gamma; const float* in_beta; float in_eps;
-  const float* weight;      /* packed for the plan's path: scflow_enc_conv_pack (path 1) or
-                               scflow_ph_conv_pack (path 0) */
-  float* out;
-  double* out_stats; int out_groups;
-  int n, h, w, cout, kh, kw, stride, pad;
-  int ksplit;               /* the plan's K split; > 1 needs parts and counters: */
-  float* parts;             /* [ksplit][n·oh·ow][cout] partial slabs */
-  int* counters;            /* plan.counters ints, zero before the first launch (every launch
-                               leaves them zero: the last-arriving workgroup of an output tile
-                               sums the slabs in slab order — deterministic — and resets it) */
-} scflow_ph_conv_gn_args;
-/* How scflow_ph_conv_gn runs a shape: path 1 = the halo-staged MFMA conv (scflow_enc_conv's
- * kernel; 3×3, pad 1, stride 1/2, channels % 16, cout % 64), path 0 = the gather MFMA conv
- * (scflow_ph_conv's); the K split that fills the GPU; out_stats partials per image (tpi); the
- * counter and slab sizes the caller allocates. */
-typedef struct scflow_ph_conv_gn_plan {
-  int path, ksplit, tpi, counters;
-  long long parts_floats;
-} scflow_ph_conv_gn_plan;
-int scflow_ph_gn_tpi(int oh, int ow);
-int scflow_ph_conv_gn_plan_for(const scflow_ph_conv_gn_args* args, scflow_ph_conv_gn_plan* plan);
-int scflow_ph_conv_gn(const scflow_ph_conv_gn_args* args, void* stream);
-int scflow_ph_fc_split_gn(const float* x, int m, int k, const float* W, float* parts, int n,
-                          int ksplit, int gn_c, const double* stats, int tpi, int groups, int hw,
-                          const float* gamma, const float* beta, float eps, void* stream);
-/* scflow_ph_fc2_heads: FC2 on FC1's K-split partials (x = relu(Σ parts1 + b1), k = FC1's width)
- *   into its own K-split partials parts2 [ksplit][m][n2], then — in the same launch, by the
- *   last-arriving workgroup (counter: (1 + ceil(n2/16))·64 ints, zero before the first launch and
- *   after every launch) —
- *   x2 = relu(Σ parts2 + b2) and the label[0] class's heads → drot [m][rch], dt [m][3]
- *   (scflow_ph_heads_sum's result up to summation order).  m ≤ 32, m·n2 ≤ 8192. */
-int scflow_ph_fc2_heads(const float* parts1, int xsplit, const float* b1, int m, int k,
-                        const float* W2, const float* b2, float* parts2, int n2, int ksplit,
-                        const float* Wr, const float* br, int rch, const float* Wt, const float* bt,
-                        const long long* label, int num_class, float* drot, float* dt,
-                        int* counter, void* stream);
 int scflow_ph_fc(const float* x, int ldx, int m, int k, const float* W, const float* bias, float* y,
                  int n, int relu, int gn_c, const float* scale, const float* shift, void* stream);
 /* scflow_ph_fc with K split over ksplit workgroup slices (m ≤ 32): parts [ksplit][m][n] = partial
@@ -367,62 +319,6 @@ int scflow_pose_step_part(const float* drot6, const float* dt, const float* R_sr
                           const float* delta, const float* mask, float* flow_up, float* mask_up,
                           float* lr_next, int s_next, float* hx_next, int s_hx, int h, int w,
                           float up_scale, float down_scale, int parts, void* stream);
-/* scflow_pose_step's arguments as a struct (stream aside) — used by scflow_ph_tail. */
-typedef struct scflow_pose_step_args {
-  const float* drot6; const float* dt; const float* R_src; const float* t_src; const float* K;
-  const float* points; float* R_dst; float* t_dst; float* flow;
-  int n, H, W; float weight; int depth_transform; float invalid_num;
-  const float* lr; const float* delta; const float* mask; float* flow_up; float* mask_up;
-  float* lr_next; int s_next; float* hx_next; int s_hx; int h, w; float up_scale, down_scale;
-} scflow_pose_step_args;
-
-/* scflow_ph_tail: MultiClassPoseHead after its first conv (pose_head.py:201-211) — GroupNorm 1,
- * conv 2 → GN 2, conv 3 → GN 3, FC1, FC2, the label[0] heads — and optionally the iteration's
- * tail (scflow_pose_step, scflow_decoder.py:223-244), as ONE persistent launch instead of 8–9.
- * Workgroups take work items from an atomic ticket in dependency order (every item only waits
- * for items with smaller tickets, which are already running: no deadlock whatever the residency)
- * and wait per sample where the data flow allows (conv 2 of sample i starts once GN 1 of sample
- * i is done).  The arithmetic per item is that of the unfused kernels: same results as
- * scflow_ph_gn_reduce / scflow_ph_conv_split / scflow_ph_fc_split / scflow_ph_heads_sum /
- * scflow_pose_step up to the GroupNorm statistics' fp64 summation order.
- *   Layer l = 0, 1, 2 is conv l+1 → GroupNorm(groups, eps[l]) → ReLU with c output channels
- *   (c % 32 == 0), output h[l]×w[l] per sample.  Conv 1 runs before (scflow_enc_conv or
- *   scflow_ph_conv_split with K split into conv1_split raw partial slabs [split][n·h0·w0][c]);
- *   y[l] receive the summed raw conv outputs, scale/shift[l] [n][c] the GroupNorm affine
- *   (the consumer applies relu(y·scale + shift) on load).  Conv 2 and 3: kh×kh, stride, pad,
- *   weights packed by scflow_ph_conv_pack, K split conv_split[j] (partial slabs conv_parts[j]).
- *   FC1 (weights permuted by scflow_ph_fc_permute, k = c·h[2]·w[2]) and FC2 with K split into
- *   partial slabs fc*_parts [split][n][fc*_n]; heads as scflow_ph_heads_sum → drot, dt.
- *   n ≤ 32.  sync: scflow_ph_tail_sync_ints(n) ints of workspace (16-B aligned), zeroed by the
- *   call (an async memset ahead of the launch); after the launch sync[2] ≠ 0 means a dependency
- *   wait gave up (bounded at 50 ms by the GPU's real-time clock) and the results are invalid —
- *   sync[9..13] then hold the first give-up's ticket, counter index, value, target and phase + 1.
- *   Concurrent launches need separate sync arrays. */
-typedef struct scflow_ph_tail_args {
-  int n, c, groups;
-  float eps[3];
-  int h[3], w[3];
-  const float* conv1_parts; int conv1_split;
-  const float* gamma[3]; const float* beta[3];
-  float* y[3]; float* scale[3]; float* shift[3];
-  const float* conv_w[2]; int kh, stride, pad;
-  int conv_split[2]; float* conv_parts[2];
-  const float* fc1_w; const float* fc1_b; int fc1_n, fc1_split; float* fc1_parts;
-  const float* fc2_w; const float* fc2_b; int fc2_n, fc2_split; float* fc2_parts;
-  const float* rot_w; const float* rot_b; int rch;
-  const float* trans_w; const float* trans_b;
-  const long long* label; int num_class;
-  float* drot; float* dt;
-  const scflow_pose_step_args* pose;      /* NULL: stop after the heads */
-  int* sync;
-  void* stamps;                           /* NULL, or (profiling) 4 u64 real-time-clock stamps per
-                                             work item: start, dependencies met, body done, signalled */
-  int* error;                             /* NULL, or a word the launch ORs 1 into when a wait gives
-                                             up; never cleared by the call, so one word checked after
-                                             a sequence of launches covers all of them */
-} scflow_ph_tail_args;
-int scflow_ph_tail_sync_ints(int n);
-int scflow_ph_tail(const scflow_ph_tail_args* args, void* stream);
 
 /* §8(f)-1: RAFTEncoder (Basic) — feature encoder (InstanceNorm) and context encoder (BatchNorm,
  * eval statistics), models/encoder/raft_encoder.py:286-314, BasicBlock models/backbone/resnet.py:

@@ -21,6 +21,7 @@ SCFLOW_ACT = {None: 0, "ReLU": 1, "Sigmoid": 2, "Tanh": 3}
 EPI_PLAIN, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2
 CONV_WINO = 2  # scflow_conv_args.bk: Winograd F(2x2,3x3) packing/kernel (SCFLOW_CONV_WINO)
 CONV_1X1W = 3  # scflow_conv_args.bk: wide 1x1 packing/kernel (SCFLOW_CONV_1X1W)
+CONV_WINO4 = 4  # scflow_conv_args.bk: Winograd F(4x4,3x3) packing/kernel (SCFLOW_CONV_WINO4)
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
 
 
@@ -42,6 +43,7 @@ class ConvArgs(ctypes.Structure):
         ("in_scale", c_vp), ("in_shift", c_vp),
         ("out_scale", c_vp), ("out_shift", c_vp),
         ("res", c_vp), ("sres", c_int),
+        ("ws", c_vp), ("ws_bytes", ctypes.c_longlong),
     ]
 
 
@@ -74,56 +76,6 @@ class WgradArgs(ctypes.Structure):
         ("stride", c_int), ("ph", c_int), ("pw", c_int),
         ("accumulate", c_int),
     ]
-
-
-class PoseStepArgs(ctypes.Structure):
-    """Mirror of ``scflow_pose_step_args`` (include/scflow_hip.h)."""
-    _fields_ = [
-        ("drot6", c_vp), ("dt", c_vp), ("R_src", c_vp), ("t_src", c_vp), ("K", c_vp),
-        ("points", c_vp), ("R_dst", c_vp), ("t_dst", c_vp), ("flow", c_vp),
-        ("n", c_int), ("H", c_int), ("W", c_int), ("weight", c_float), ("depth_transform", c_int),
-        ("invalid_num", c_float),
-        ("lr", c_vp), ("delta", c_vp), ("mask", c_vp), ("flow_up", c_vp), ("mask_up", c_vp),
-        ("lr_next", c_vp), ("s_next", c_int), ("hx_next", c_vp), ("s_hx", c_int), ("h", c_int),
-        ("w", c_int), ("up_scale", c_float), ("down_scale", c_float),
-    ]
-
-
-class PhTailArgs(ctypes.Structure):
-    """Mirror of ``scflow_ph_tail_args`` (include/scflow_hip.h)."""
-    _fields_ = [
-        ("n", c_int), ("c", c_int), ("groups", c_int), ("eps", c_float * 3), ("h", c_int * 3),
-        ("w", c_int * 3), ("conv1_parts", c_vp), ("conv1_split", c_int),
-        ("gamma", c_vp * 3), ("beta", c_vp * 3), ("y", c_vp * 3), ("scale", c_vp * 3),
-        ("shift", c_vp * 3), ("conv_w", c_vp * 2), ("kh", c_int), ("stride", c_int), ("pad", c_int),
-        ("conv_split", c_int * 2), ("conv_parts", c_vp * 2),
-        ("fc1_w", c_vp), ("fc1_b", c_vp), ("fc1_n", c_int), ("fc1_split", c_int), ("fc1_parts", c_vp),
-        ("fc2_w", c_vp), ("fc2_b", c_vp), ("fc2_n", c_int), ("fc2_split", c_int), ("fc2_parts", c_vp),
-        ("rot_w", c_vp), ("rot_b", c_vp), ("rch", c_int), ("trans_w", c_vp), ("trans_b", c_vp),
-        ("label", c_vp), ("num_class", c_int), ("drot", c_vp), ("dt", c_vp),
-        ("pose", ctypes.POINTER(PoseStepArgs)), ("sync", c_vp), ("stamps", c_vp), ("error", c_vp),
-    ]
-
-
-class PhConvGnArgs(ctypes.Structure):
-    """Mirror of ``scflow_ph_conv_gn_args`` (include/scflow_hip.h)."""
-    _fields_ = [
-        ("src0", c_vp), ("c0", c_int), ("s0", c_int),
-        ("src1", c_vp), ("c1", c_int), ("s1", c_int),
-        ("in_stats", c_vp), ("in_tpi", c_int), ("in_groups", c_int),
-        ("in_gamma", c_vp), ("in_beta", c_vp), ("in_eps", c_float),
-        ("weight", c_vp), ("out", c_vp),
-        ("out_stats", c_vp), ("out_groups", c_int),
-        ("n", c_int), ("h", c_int), ("w", c_int), ("cout", c_int), ("kh", c_int), ("kw", c_int),
-        ("stride", c_int), ("pad", c_int),
-        ("ksplit", c_int), ("parts", c_vp), ("counters", c_vp),
-    ]
-
-
-class PhConvGnPlan(ctypes.Structure):
-    """Mirror of ``scflow_ph_conv_gn_plan`` (include/scflow_hip.h)."""
-    _fields_ = [("path", c_int), ("ksplit", c_int), ("tpi", c_int), ("counters", c_int),
-                ("parts_floats", c_ll)]
 
 
 class RenderArgs(ctypes.Structure):
@@ -179,6 +131,7 @@ SIGNATURES = {
     "scflow_conv_pack_weights": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_vp]),
     "scflow_conv_pick_bk": (c_int, [ctypes.POINTER(ConvArgs)]),
+    "scflow_conv_workspace_bytes": (ctypes.c_longlong, [ctypes.POINTER(ConvArgs)]),
     "scflow_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_vp]),
     "scflow_pose_update": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp]),
     "scflow_lift_points": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
@@ -194,15 +147,11 @@ SIGNATURES = {
     "scflow_pose_step_part": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_float, c_int, c_float] +
                               [c_vp] * 6 + [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_int,
                                             c_vp]),
-    "scflow_ph_tail": (c_int, [ctypes.POINTER(PhTailArgs), c_vp]),
-    "scflow_ph_tail_sync_ints": (c_int, [c_int]),
     "scflow_sync_event_create": (c_int, [ctypes.POINTER(c_vp)]),
     "scflow_sync_event_destroy": (c_int, [c_vp]),
     "scflow_sync_event_record": (c_int, [c_vp, c_vp]),
     "scflow_stream_wait_event": (c_int, [c_vp, c_vp]),
     "scflow_timing_event_create": (c_int, [ctypes.POINTER(c_vp)]),
-    "scflow_alloc_uncached": (c_int, [c_ll, ctypes.POINTER(c_vp)]),
-    "scflow_free_uncached": (c_int, [c_vp]),
     "scflow_event_elapsed_ms": (c_int, [c_vp, c_vp, ctypes.POINTER(c_float)]),
     "scflow_transpose": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_int, c_ll, c_int, c_vp]),
     "scflow_ph_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int]),
@@ -223,13 +172,6 @@ SIGNATURES = {
     "scflow_ph_gn_reduce": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp,
                                     c_float, c_vp, c_vp, c_vp]),
     "scflow_ph_fc_permute": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_vp]),
-    "scflow_ph_gn_tpi": (c_int, [c_int, c_int]),
-    "scflow_ph_conv_gn": (c_int, [ctypes.POINTER(PhConvGnArgs), c_vp]),
-    "scflow_ph_fc2_heads": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int,
-                                    c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
-    "scflow_ph_conv_gn_plan_for": (c_int, [ctypes.POINTER(PhConvGnArgs), ctypes.POINTER(PhConvGnPlan)]),
-    "scflow_ph_fc_split_gn": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_int,
-                                      c_int, c_int, c_vp, c_vp, c_float, c_vp]),
     "scflow_ph_fc": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                              c_vp, c_vp]),
     "scflow_ph_heads": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp,

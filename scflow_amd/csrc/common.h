@@ -61,25 +61,3 @@ __device__ __forceinline__ float act_apply(float v, int act) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
-
-// scale / shift of GroupNorm(groups) for channel c of image img from tpi partial statistics
-// st [n][tpi][groups][2] (fp64 sum, sum of squares over hw pixels of the group's channels),
-// summed in a fixed order (the pose head's fused-statistics convs, scflow_ph_conv_gn)
-__device__ __forceinline__ void ph_gn_affine(const double* st, int tpi, int groups, int c, int cin,
-                                             int img, int hw, const float* gamma, const float* beta,
-                                             float eps, float& sc, float& sh) {
-  const int cpg = cin / groups, g = c / cpg;
-  double A = 0, B = 0;
-  for (int t = 0; t < tpi; ++t) {
-    const double* p = st + (((size_t)img * tpi + t) * groups + g) * 2;
-    A += p[0];
-    B += p[1];
-  }
-  const double cnt = (double)hw * cpg;
-  const double mean = A / cnt;
-  double var = B / cnt - mean * mean;
-  if (var < 0) var = 0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  sc = gamma[c] * rstd;
-  sh = beta[c] - (float)mean * sc;
-}

@@ -919,6 +919,27 @@ int wino_swz(int R, int C) {
 // profiling: where the next F(2×2,3×3) Winograd launches write their per-workgroup stamps
 static unsigned long long* g_wino_stamps = nullptr;
 
+#include "conv_wino4.h"
+
+// F(4×4,3×3) (conv_wino4.h) for the 3×3 convs it covers with at least WINO4_MIN_COUT output
+// channels; SCFLOW_CONV_WINO4 = 0 off, 1 default, 2 every covered shape (A/B)
+#ifndef WINO4_MIN_COUT
+#define WINO4_MIN_COUT 96
+#endif
+#ifndef WINO4_DEFAULT
+#define WINO4_DEFAULT 0
+#endif
+bool wino4_pick(const scflow_conv_args& a) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("SCFLOW_CONV_WINO4");
+    mode = e ? atoi(e) : WINO4_DEFAULT;
+  }
+  if (!mode || !wino4_shape(a)) return false;
+  return mode == 2 || a.cout >= WINO4_MIN_COUT;
+}
+
+
 template <int W, int NBW>
 int launch_wino_w(WinoParams p, hipStream_t st) {
   using G = WinoGeom<W>;
@@ -1180,6 +1201,11 @@ SCFLOW_API long long scflow_conv_packed_size_bk(int cout, int c0, int c1, int kh
       return SCFLOW_EUNSUPPORTED;
     return wino_packed_size(cout, c0, c1, kh);
   }
+  if (bk == SCFLOW_CONV_WINO4) {
+    if (c0 <= 0 || c1 < 0 || c0 % 4 || c1 % 4 || kh != 3 || kw != 3 || stride != 1)
+      return SCFLOW_EUNSUPPORTED;
+    return wino4_packed_size(cout, c0, c1);
+  }
   if (bk != 0 && bk != 8 && bk != 16) return SCFLOW_EINVAL;
   return scflow_conv_packed_size(cout, c0, c1, kh, kw, stride, w);
 }
@@ -1194,6 +1220,16 @@ SCFLOW_API int scflow_conv_pack_weights(const float* w_oihw, float* packed, int 
     const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     conv1x1w_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0,
                                                                    conv1x1w_kb(c0), total);
+    return scflow_launch_status();
+  }
+  if (bk == SCFLOW_CONV_WINO4) {
+    const long long total = scflow_conv_packed_size_bk(cout, c0, c1, kh, kw, stride, w, bk);
+    if (total < 0) return (int)total;
+    const int cp0 = round_up(c0, W4KC);
+    const int nsub = (cp0 + round_up(c1, W4KC)) / W4KC;
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    wino4_pack_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(w_oihw, packed, cout, c0, c1, cp0,
+                                                                nsub, total);
     return scflow_launch_status();
   }
   if (bk == SCFLOW_CONV_WINO) {
@@ -1229,6 +1265,7 @@ SCFLOW_API int scflow_conv_pick_bk(const scflow_conv_args* args) {
   if (!args) return SCFLOW_EINVAL;
   const scflow_conv_args& a = *args;
   if (a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 || a.c1 < 0) return SCFLOW_EINVAL;
+  if (wino4_pick(a)) return SCFLOW_CONV_WINO4;
   if (wino_enabled(a.kh) && wino_launchable(a)) return SCFLOW_CONV_WINO;
   // the wide 1×1 kernel up to two workgroups per CU (configs[1]'s corr_net.0: 256, the same
   // 32.3 µs as conv1x1_kernel); larger grids keep conv1x1_kernel (configs[4], 2048 workgroups:
@@ -1243,6 +1280,13 @@ SCFLOW_API int scflow_conv_pick_bk(const scflow_conv_args* args) {
   if (tr < 1 || g.oh % tr) return BK;
   const long long wgs = (long long)a.n * (g.oh / tr) * (g.npad / BN);
   return pick_bk(a.kh, a.kw, tm, hr, g.hc, wgs, device_cus());
+}
+
+SCFLOW_API long long scflow_conv_workspace_bytes(const scflow_conv_args* args) {
+  if (!args) return SCFLOW_EINVAL;
+  if (args->bk != SCFLOW_CONV_WINO4) return 0;
+  if (!wino4_shape(*args) || args->n <= 0 || args->c0 <= 0) return SCFLOW_EUNSUPPORTED;
+  return wino4_workspace_bytes(*args);
 }
 
 SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
@@ -1261,6 +1305,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     return SCFLOW_EINVAL;
   }
   if (a.bk == SCFLOW_CONV_WINO) return launch_wino(a, (hipStream_t)stream);
+  if (a.bk == SCFLOW_CONV_WINO4) return launch_wino4(a, (hipStream_t)stream);
   if (a.bk == SCFLOW_CONV_1X1W) return launch_conv1x1w(a, (hipStream_t)stream);
   if (has_fused_norm(a)) return SCFLOW_EUNSUPPORTED;  // Winograd 3×3 only
   if (a.bk != 0 && a.bk != 8 && a.bk != 16) return SCFLOW_EINVAL;

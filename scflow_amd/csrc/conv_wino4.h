@@ -1,0 +1,354 @@
+// Winograd F(4×4, 3×3) convolution on fp32 MFMA (round 5) — included by conv.hip (inside its
+// anonymous namespace).  For the update block's wide 3×3 stride-1 pad-1 convs (the XHead hidden
+// convs 128 → 2·256, corr_net.1 256 → 192, out_net 256 → 126; reference
+// models/decoder/raft_decoder.py:75-85,256-294): 36 transform points per 4×4 output tile, so the
+// channel contractions execute 2.25 multiplies per output pixel and tap set instead of F(2×2,3×3)'s
+// 4 (1.78× fewer MFMAs) and the direct conv's 9.
+//
+// Interpolation points {0, 1, −1, 2, −½, ∞} (Toom–Cook), chosen over Lavin's {0, ±1, ±2, ∞} for
+// accuracy: in an fp32 restatement with 256 input channels the max error against fp64 is 1.3e-5
+// of outputs ≈ 4 (Lavin's points 3.8e-5; F(2×2,3×3) 2.8e-6, the direct fp32 conv 1.3e-6).
+//   Bᵀ = [1 3/2 −2 −3/2 1 0; 0 −1 −5/2 −1/2 1 0; 0 1 1/2 −5/2 1 0; 0 −1/2 −1 1/2 1 0;
+//         0 2 −1 −2 1 0; 0 1 3/2 −2 −3/2 1]
+//   G  = [1 0 0; −1/3 −1/3 −1/3; 1/3 −1/3 1/3; 1/15 2/15 4/15; −16/15 8/15 −4/15; 0 0 1]
+//   Aᵀ = [1 1 1 1 1 0; 0 1 −1 2 −1/2 0; 0 1 1 4 1/4 0; 0 1 −1 8 −1/8 1]
+// Y = Aᵀ[(G g Gᵀ) ⊙ (Bᵀ d B)]A for the 6×6 input patch d of a 4×4 output tile.
+//
+// Two launches per conv:
+//  1. wino4_vt_kernel — the input transform V = Bᵀ d B of every (tile, channel) once, written to
+//     a workspace in the GEMM's lane order [tile block][8-channel sub-step][point][lane][4]
+//     (2.25× the input's bytes; L2 / Infinity-Cache resident).  Computing V once per conv instead
+//     of once per output-channel block (as the F(2×2,3×3) kernel does, from its LDS halo) keeps
+//     the VALU work — 6× that of F(2×2,3×3) per MFMA — out of the MFMA loop.
+//  2. conv_wino4_kernel — 36 independent GEMMs M_ξ[tile][co] = Σ_ci V_ξ[tile][ci]·U_ξ[ci][co]:
+//     workgroup = 32 tiles × 32 output channels, 4 waves, wave w owns points ξ = 9w .. 9w+8 and
+//     streams their V and U slices from L2 as lane-ordered 1 KiB buffer loads (each point's pair
+//     reloaded for the next sub-step right after its 4 MFMAs issue): no LDS, no barrier and no
+//     VALU in the main loop.  Epilogue: the points meet in LDS 8 tiles at a time (36 × 32 × 9
+//     floats), one (tile, channel) per thread applies Aᵀ·A and the fused bias / affine / bias-map
+//     / residual / activation, channel-contiguous stores.
+
+constexpr int W4P = 36;   // transform points per tile
+constexpr int W4KC = 8;   // input channels per sub-step (lanes 0-31: channels 0-3, 32-63: 4-7)
+constexpr int W4TM = 32;  // tiles per block (MFMA rows)
+constexpr int W4NPW = W4P / 4;  // points per wave
+constexpr int W4CP = 36;  // epilogue LDS row: 32 output channels + 4 (16-B rows, spread banks)
+constexpr int W4_LDS = W4P * 8 * W4CP * 4;  // epilogue bytes: [36 points][8 tiles][W4CP]
+
+__device__ __forceinline__ bool w4_al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// four consecutive floats p[0..3] of which the first nv are valid (zeros after), as one 16-B
+// load when vec
+__device__ __forceinline__ floatx4 w4_ld4(const float* p, bool vec, int nv) {
+  if (vec) return *(const floatx4*)p;
+  floatx4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (e < nv) r[e] = p[e];
+  return r;
+}
+
+struct Wino4Params {
+  scflow_conv_args a;
+  const float* v;   // transformed input [ntb][nsub][36][64][4]
+  int cp0;          // source-0 channels padded to W4KC (source 1 starts there)
+  int nsub;         // sub-steps over both sources
+  int th, tw;       // tiles per image column / row (h/4, w/4)
+  int ntiles, ntb;  // tiles, tile blocks
+  unsigned long long* stamps;  // profiling (scflow_debug_conv_stamps), or NULL
+};
+
+// v = Bᵀ·d over one axis (6 float4)
+__device__ __forceinline__ void w4_bt(const floatx4 (&d)[6], floatx4 (&v)[6]) {
+  v[0] = d[0] + 1.5f * d[1] - 2.f * d[2] - 1.5f * d[3] + d[4];
+  v[1] = d[4] - d[1] - 2.5f * d[2] - 0.5f * d[3];
+  v[2] = d[1] + 0.5f * d[2] - 2.5f * d[3] + d[4];
+  v[3] = d[4] - 0.5f * d[1] - d[2] + 0.5f * d[3];
+  v[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+  v[5] = d[1] + 1.5f * d[2] - 2.f * d[3] - 1.5f * d[4] + d[5];
+}
+
+// y = Aᵀ·m over one axis (6 → 4)
+__device__ __forceinline__ void w4_at(const float (&m)[6], float (&y)[4]) {
+  const float s12 = m[1] + m[2], d12 = m[1] - m[2];
+  y[0] = m[0] + s12 + m[3] + m[4];
+  y[1] = d12 + 2.f * m[3] - 0.5f * m[4];
+  y[2] = s12 + 4.f * m[3] + 0.25f * m[4];
+  y[3] = d12 + 8.f * m[3] - 0.125f * m[4] + m[5];
+}
+
+// 1. input transform: workgroup = (tile block blockIdx.x, sub-step blockIdx.y), 6 waves; lane =
+//    (tile li, channel quad hh).  Wave x first transforms patch column x (6 loads in flight per
+//    lane, t[i][x] = (Bᵀ d)[i] into LDS), then wave i transforms row i of t (V[i][·] = Bᵀ t[i]) and
+//    stores its 6 points as 1 KiB lane-ordered pieces.
+constexpr int W4VT_THREADS = 6 * 64;
+__global__ __launch_bounds__(W4VT_THREADS) void wino4_vt_kernel(Wino4Params P) {
+  __shared__ floatx4 tl4[6][6][64];  // [i][x][lane]
+  const scflow_conv_args& a = P.a;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // column x, then row i
+  const int tb = blockIdx.x, k = blockIdx.y, li = lane & 31, hh = lane >> 5;
+  const int T = tb * W4TM + li;
+  const int c = k * W4KC + 4 * hh;  // padded channel of this lane's quad
+  const bool s1 = c >= P.cp0;
+  const float* src = s1 ? a.src1 : a.src0;
+  const int cs = s1 ? a.c1 : a.c0;
+  const int ss = s1 ? a.s1 : a.s0;
+  const int cc = s1 ? c - P.cp0 : c;
+  const bool ok_c = T < P.ntiles && cc < cs;
+  int img = 0, ty = 0, tx = 0;
+  if (T < P.ntiles) {
+    const int per = P.th * P.tw;
+    img = T / per;
+    const int r = T - img * per;
+    ty = r / P.tw;
+    tx = r - ty * P.tw;
+  }
+  const long long npix = (long long)a.n * a.h * a.w;
+  const __amdgpu_buffer_rsrc_t rs =
+      wino_rsrc(src, (unsigned)(((npix - 1) * ss + (cs > 0 ? cs : 0)) * 4));
+  const int ix = 4 * tx - 1 + wv;
+  floatx4 d[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int iy = 4 * ty - 1 + r;
+    const bool ok = ok_c && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+    const long long pix = ((long long)img * a.h + iy) * a.w + ix;
+    d[r] = wino_bload(rs, ok ? (int)((pix * ss + cc) * 4) : WINO_OOB, 0);
+  }
+  if (a.in_scale != nullptr && !s1 && ok_c) {  // input InstanceNorm + ReLU (zero padding stays 0)
+    const floatx4 isc = *(const floatx4*)(a.in_scale + (size_t)img * a.c0 + cc);
+    const floatx4 ish = *(const floatx4*)(a.in_shift + (size_t)img * a.c0 + cc);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int iy = 4 * ty - 1 + r;
+      if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[r][e] = fmaxf(d[r][e] * isc[e] + ish[e], 0.f);
+      }
+    }
+  }
+  floatx4 col[6];
+  w4_bt(d, col);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) tl4[i][wv][lane] = col[i];
+  __syncthreads();
+  floatx4 trow[6], v[6];
+#pragma unroll
+  for (int x = 0; x < 6; ++x) trow[x] = tl4[wv][x][lane];
+  w4_bt(trow, v);
+  floatx4* out = (floatx4*)(P.v + ((size_t)tb * P.nsub + k) * W4P * 256) + lane;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) out[(6 * wv + j) * 64] = v[j];
+}
+
+// 2. the point GEMMs + output transform
+template <int ACT>
+__global__ __launch_bounds__(256, 2) void conv_wino4_kernel(Wino4Params P) {
+  extern __shared__ float w4s[];  // epilogue [36][32 co][W4EP]
+  const scflow_conv_args& a = P.a;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, hh = lane >> 5;
+  const int tb = blockIdx.x, cb = blockIdx.y;
+  const int nsub = P.nsub;
+  wino_stamp(P.stamps, 0);
+  const unsigned blk = (unsigned)nsub * W4P * 1024;  // bytes of one block's V / U slice
+  const __amdgpu_buffer_rsrc_t vsrc = wino_rsrc(P.v + (size_t)tb * nsub * W4P * 256, blk);
+  const __amdgpu_buffer_rsrc_t usrc = wino_rsrc(a.weight + (size_t)cb * nsub * W4P * 256, blk);
+  const int p0 = W4NPW * wv;  // this wave's first point
+  floatx4 v[W4NPW], u[W4NPW];
+  floatx16 acc[W4NPW];
+#pragma unroll
+  for (int j = 0; j < W4NPW; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  auto load = [&](int k, int j) __attribute__((always_inline)) {
+    const int off = (k * W4P + p0 + j) * 1024;  // wave-uniform (SGPR offset)
+    v[j] = wino_bload(vsrc, lane * 16, off);
+    u[j] = wino_bload(usrc, lane * 16, off);
+  };
+#pragma unroll
+  for (int j = 0; j < W4NPW; ++j) load(0, j);
+  wino_stamp(P.stamps, 1);
+  for (int k = 0; k < nsub; ++k) {
+    const int kn = k + 1 < nsub ? k + 1 : k;  // the last sub-step reloads itself (no branches)
+    auto point = [&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[j][e], acc[j], 0, 0, 0);
+      load(kn, j);  // eight points' MFMAs (≈ 2000 cycles) to arrive
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    StaticFor<0, W4NPW>::run(point);
+  }
+
+  if (P.stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    wino_stamp(P.stamps, 2);
+  }
+  // epilogue, 8 tiles per round: round q holds accumulator rows 4q..4q+3 = tiles 8q + 4hh + rr,
+  // staged as M[point][tile][channel]; thread = (tile tl, channel quad cq, output row ya): the
+  // row ya of Aᵀ·M (a runtime row of coefficients, float4 over the quad), then Aᵀ over the
+  // columns → output pixels (ya, 0..3) × 4 channels as 16-B stores
+  const int per = P.th * P.tw;
+  const int tl = tid >> 5, cq = (tid >> 2) & 7, ya = tid & 3;
+  const int col = cb * 32 + 4 * cq;
+  const int nv = a.cout - col < 4 ? a.cout - col : 4;  // valid channels of the quad (≤ 0: none)
+  const bool vo = nv == 4 && (a.so & 3) == 0 && w4_al16(a.out);
+  const bool vb = nv == 4 && (a.sbm & 3) == 0 && w4_al16(a.bias_map);
+  const bool vr = nv == 4 && (a.sres & 3) == 0 && w4_al16(a.res);
+  const floatx4 zero4 = {0.f, 0.f, 0.f, 0.f}, one4 = {1.f, 1.f, 1.f, 1.f};
+  const floatx4 bias4 = (nv > 0 && a.bias) ? w4_ld4(a.bias + col, nv == 4 && w4_al16(a.bias + col), nv) : zero4;
+  const floatx4 osc4 = (nv > 0 && a.out_scale) ? w4_ld4(a.out_scale + col, false, nv) : one4;
+  const floatx4 osh4 = (nv > 0 && a.out_scale) ? w4_ld4(a.out_shift + col, false, nv) : zero4;
+  // row ya of Aᵀ (0, ±1, ±2, 4, 8, ±½, ¼, ±⅛, …)
+  const float c1 = 1.f, c2 = ya == 0 ? 1.f : (ya == 2 ? 1.f : -1.f);
+  const float c3 = ya == 0 ? 1.f : (ya == 1 ? 2.f : (ya == 2 ? 4.f : 8.f));
+  const float c4 = ya == 0 ? 1.f : (ya == 1 ? -0.5f : (ya == 2 ? 0.25f : -0.125f));
+  const float c0 = ya == 0 ? 1.f : 0.f, c5 = ya == 3 ? 1.f : 0.f;
+  const floatx4* M4 = (const floatx4*)w4s;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q) __syncthreads();  // the previous round's reads are done
+#pragma unroll
+    for (int j = 0; j < W4NPW; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        w4s[((p0 + j) * 8 + 4 * hh + rr) * W4CP + li] = acc[j][4 * q + rr];
+    __syncthreads();
+    const int T = tb * W4TM + 8 * q + tl;
+    if (T >= P.ntiles || nv <= 0) continue;
+    floatx4 rj[6];  // (Aᵀ M)[ya][j], j = 0..5
+#pragma unroll
+    for (int x = 0; x < 6; ++x) {
+      const floatx4 m0 = M4[((0 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
+      const floatx4 m1 = M4[((1 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
+      const floatx4 m2 = M4[((2 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
+      const floatx4 m3 = M4[((3 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
+      const floatx4 m4 = M4[((4 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
+      const floatx4 m5 = M4[((5 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
+      rj[x] = c0 * m0 + c1 * m1 + c2 * m2 + c3 * m3 + c4 * m4 + c5 * m5;
+    }
+    const floatx4 s12 = rj[1] + rj[2], d12 = rj[1] - rj[2];
+    floatx4 y[4];
+    y[0] = rj[0] + s12 + rj[3] + rj[4];
+    y[1] = d12 + 2.f * rj[3] - 0.5f * rj[4];
+    y[2] = s12 + 4.f * rj[3] + 0.25f * rj[4];
+    y[3] = d12 + 8.f * rj[3] - 0.125f * rj[4] + rj[5];
+    const int img = T / per;
+    const int r = T - img * per;
+    const int ty = r / P.tw, tx = r - ty * P.tw;
+    const size_t pix0 = ((size_t)img * a.h + 4 * ty + ya) * a.w + 4 * tx;
+    floatx4 val[4];
+#pragma unroll
+    for (int xb = 0; xb < 4; ++xb) val[xb] = (y[xb] + bias4) * osc4 + osh4;
+    // every global read (bias map, residual) before any store
+    if (a.bias_map) {
+#pragma unroll
+      for (int xb = 0; xb < 4; ++xb) val[xb] += w4_ld4(a.bias_map + (pix0 + xb) * a.sbm + col, vb, nv);
+    }
+    if (a.res) {
+#pragma unroll
+      for (int xb = 0; xb < 4; ++xb) val[xb] += w4_ld4(a.res + (pix0 + xb) * a.sres + col, vr, nv);
+    }
+#pragma unroll
+    for (int xb = 0; xb < 4; ++xb) {
+      floatx4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act_apply(val[xb][e], ACT);
+      float* dst = a.out + (pix0 + xb) * a.so + col;
+      if (vo) {
+        *(floatx4*)dst = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (e < nv) dst[e] = o[e];
+      }
+    }
+  }
+  if (P.stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    wino_stamp(P.stamps, 3);
+  }
+}
+
+// U = G g Gᵀ per (co, ci) in fp64, packed [cout block][sub-step][point][lane][4] with lane =
+// li + 32·hh ↔ co = 32·block + li, padded input channel 8·sub-step + 4·hh + e (source 1 from cp0)
+__global__ void wino4_pack_kernel(const float* __restrict__ w, float* __restrict__ out, int cout,
+                                  int c0, int c1, int cp0, int nsub, long long total) {
+  const double G[6][3] = {{1., 0., 0.},
+                          {-1. / 3, -1. / 3, -1. / 3},
+                          {1. / 3, -1. / 3, 1. / 3},
+                          {1. / 15, 2. / 15, 4. / 15},
+                          {-16. / 15, 8. / 15, -4. / 15},
+                          {0., 0., 1.}};
+  for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+    const int e = (int)(idx & 3), lane = (int)((idx >> 2) & 63);
+    const long long rest = idx >> 8;
+    const int xi = (int)(rest % W4P);
+    const long long rk = rest / W4P;
+    const int k = (int)(rk % nsub), cbk = (int)(rk / nsub);
+    const int co = cbk * 32 + (lane & 31);
+    const int kc = k * W4KC + 4 * (lane >> 5) + e;
+    const int ci = kc < cp0 ? (kc < c0 ? kc : -1) : (kc - cp0 < c1 ? c0 + kc - cp0 : -1);
+    double val = 0.;
+    if (co < cout && ci >= 0) {
+      const float* g = w + ((size_t)co * (c0 + c1) + ci) * 9;
+      const int i = xi / 6, j = xi % 6;
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx) val += G[i][ky] * (double)g[ky * 3 + kx] * G[j][kx];
+    }
+    out[idx] = (float)val;
+  }
+}
+
+long long wino4_packed_size(int cout, int c0, int c1) {
+  const int nsub = (round_up(c0, W4KC) + round_up(c1, W4KC)) / W4KC;
+  return (long long)(round_up(cout, 32) / 32) * nsub * W4P * 256;
+}
+
+bool wino4_shape(const scflow_conv_args& a) {
+  return a.kh == 3 && a.kw == 3 && a.stride == 1 && a.ph == 1 && a.pw == 1 && a.h % 4 == 0 &&
+         a.w % 4 == 0 && a.c0 % 4 == 0 && a.c1 % 4 == 0 && a.epilogue == SCFLOW_EPI_PLAIN &&
+         (a.c1 == 0 || a.in_scale == nullptr);
+}
+
+long long wino4_workspace_bytes(const scflow_conv_args& a) {
+  const long long ntiles = (long long)a.n * (a.h / 4) * (a.w / 4);
+  const long long ntb = (ntiles + W4TM - 1) / W4TM;
+  const int nsub = (round_up(a.c0, W4KC) + round_up(a.c1, W4KC)) / W4KC;
+  return ntb * nsub * W4P * 1024;
+}
+
+int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
+  if (!wino4_shape(a)) return SCFLOW_EUNSUPPORTED;
+  if (!a.ws || a.ws_bytes < wino4_workspace_bytes(a)) return SCFLOW_EINVAL;
+  if (!aligned16(a.src0) || (a.s0 & 3) || (a.c1 > 0 && (!aligned16(a.src1) || (a.s1 & 3))) ||
+      !aligned16(a.weight) || !aligned16(a.ws))
+    return SCFLOW_EALIGN;
+  Wino4Params p;
+  p.a = a;
+  p.v = a.ws;
+  p.cp0 = round_up(a.c0, W4KC);
+  p.nsub = (p.cp0 + round_up(a.c1, W4KC)) / W4KC;
+  p.th = a.h / 4;
+  p.tw = a.w / 4;
+  const long long ntiles = (long long)a.n * p.th * p.tw;
+  if (ntiles >= (1LL << 30) || (long long)p.nsub * W4P * 1024 >= (1LL << 31)) return SCFLOW_EUNSUPPORTED;
+  p.ntiles = (int)ntiles;
+  p.ntb = (int)((ntiles + W4TM - 1) / W4TM);
+  p.stamps = g_wino_stamps;
+  wino4_vt_kernel<<<dim3(p.ntb, p.nsub), W4VT_THREADS, 0, st>>>(p);
+  const int e = scflow_launch_status();
+  if (e) return e;
+  const dim3 grid(p.ntb, round_up(a.cout, 32) / 32);
+  switch (a.act) {  // the activation as a template argument: one epilogue body per kernel
+    case SCFLOW_ACT_RELU: conv_wino4_kernel<SCFLOW_ACT_RELU><<<grid, 256, W4_LDS, st>>>(p); break;
+    case SCFLOW_ACT_SIGMOID: conv_wino4_kernel<SCFLOW_ACT_SIGMOID><<<grid, 256, W4_LDS, st>>>(p); break;
+    case SCFLOW_ACT_TANH: conv_wino4_kernel<SCFLOW_ACT_TANH><<<grid, 256, W4_LDS, st>>>(p); break;
+    default: conv_wino4_kernel<SCFLOW_ACT_NONE><<<grid, 256, W4_LDS, st>>>(p); break;
+  }
+  return scflow_launch_status();
+}

@@ -49,17 +49,9 @@ struct EncParams {
   scflow_enc_conv_args a;
   int oh, ow, tr, tc, hr, hc, nst;  // output size, tile rows × cols, halo rows × cols, K stages
   int nst0;                         // stages of the first source
-  // GNF mode (scflow_ph_conv_gn, path 1): the input GroupNorm (+ ReLU) affine of the workgroup's
-  // image built in LDS from the producer's partials (gin; NULL = raw input); a.out = the K-split
-  // slabs when gridDim.z > 1 (the last-arriving workgroup of a tile sums them in slab order into
-  // gout and resets its counter gcnt[tile]) else gout itself; this conv's GroupNorm partials
-  // gst [n][2·tiles_per_img][ggroups][2] (one per output tile and wave row)
-  const double* gin; int gin_tpi, gin_groups; const float* gin_gamma; const float* gin_beta;
-  float gin_eps;
-  float* gout; int* gcnt; double* gst; int ggroups;
 };
 
-template <int KH, int KW, int S, int TILE_M, bool NORM, bool GNF = false>
+template <int KH, int KW, int S, int TILE_M, bool NORM>
 __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
   constexpr int TAPS = KH * KW;
   constexpr int RB = TILE_M / 64;
@@ -98,15 +90,6 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
   const int s_end = (int)((long long)P.nst * (z + 1) / nsplit);
   const int ctot = a.cin + a.cin1;
 
-  // GNF: the input GroupNorm affine of this workgroup's image, [ctot] scale then [ctot] shift,
-  // after the stage buffers
-  float* Tg = Bs + (size_t)TAPS * EBN * ELDA;
-  if constexpr (GNF && NORM) {
-    for (int c = tid; c < ctot; c += 256)
-      ph_gn_affine(P.gin, P.gin_tpi, P.gin_groups, c, ctot, img, a.h * a.w, P.gin_gamma, P.gin_beta,
-                   P.gin_eps, Tg[c], Tg[ctot + c]);
-    __syncthreads();
-  }
   floatx4 ra[NA], rb[NB], rsc, rsh;
   auto gload = [&](int s) {
     const bool second = s >= P.nst0;
@@ -121,13 +104,8 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
     }
     if constexpr (NORM) {
       const int cn = s * EBK + cq;  // channel in the concatenation
-      if constexpr (GNF) {
-        rsc = *(const floatx4*)(Tg + cn);
-        rsh = *(const floatx4*)(Tg + ctot + cn);
-      } else {
-        rsc = *(const floatx4*)(a.in_scale + (size_t)img * ctot + cn);
-        rsh = *(const floatx4*)(a.in_shift + (size_t)img * ctot + cn);
-      }
+      rsc = *(const floatx4*)(a.in_scale + (size_t)img * ctot + cn);
+      rsh = *(const floatx4*)(a.in_shift + (size_t)img * ctot + cn);
     }
     const float* wb = a.weight + ((size_t)blockIdx.y * P.nst + s) * (TAPS * EBN * EBK);
 #pragma unroll
@@ -197,100 +175,6 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
 
   // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   const int col = n0 + wn * 32 + li;
-  if constexpr (GNF) {
-    // (host: cout % 64 == 0, so every lane's column is valid and no thread leaves early)
-    const size_t slab = (size_t)a.n * P.oh * P.ow * a.cout;
-    int pixg[RB][16];
-#pragma unroll
-    for (int rr = 0; rr < RB; ++rr)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = wm * (TILE_M / 2) + rr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        pixg[rr][r] = (img * P.oh + oy0 + m / tc) * ow + ox0 + m % tc;
-      }
-    if (nsplit > 1) {
-      // the arrival flag lives in the dynamic LDS (after the affine table): a static __shared__
-      // variable would make the 160 KB dynamic-LDS attribute of this kernel invalid
-      int& s_last = *(int*)(Tg + 2 * ctot);
-      float* mine = a.out + (size_t)z * slab;
-#pragma unroll
-      for (int rr = 0; rr < RB; ++rr)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)  // agent-scope stores: written through to the memory side
-          __hip_atomic_store(mine + (size_t)pixg[rr][r] * a.cout + col, acc[rr][r], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's slab stores drained
-      __syncthreads();
-      const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-      // the slab stores are agent-scope (memory side) and drained: visible to the last arriver's
-      // agent-scope loads without a release fence (which would write back the XCD's whole L2)
-      if (tid == 0) {
-        // one counter per 256 B (scflow_ph_conv_gn_plan): device-scope atomics on one line
-        // serialise at the memory side
-        const int old = __hip_atomic_fetch_add(P.gcnt + tile * 64, 1, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == nsplit - 1;
-      }
-      __syncthreads();
-      if (!s_last) return;
-      // the tile's sum in slab order 0..nsplit-1 (this workgroup's own slab from registers);
-      // every other slab's values are loaded first (≤ 3 × 16·RB: one memory latency)
-      constexpr int KS = 4;  // the plan's K split at most
-      float sv[KS][RB][16];
-#pragma unroll
-      for (int zz = 0; zz < KS; ++zz)
-#pragma unroll
-        for (int rr = 0; rr < RB; ++rr)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            sv[zz][rr][r] = (zz < nsplit && zz != z)
-                                ? __hip_atomic_load(a.out + zz * slab + (size_t)pixg[rr][r] * a.cout + col,
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : 0.f;
-#pragma unroll
-      for (int rr = 0; rr < RB; ++rr)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = 0.f;
-#pragma unroll
-          for (int zz = 0; zz < KS; ++zz)
-            if (zz < nsplit) v += zz == z ? acc[rr][r] : sv[zz][rr][r];
-          acc[rr][r] = v;
-        }
-      if (tid == 0) __hip_atomic_store(P.gcnt + tile * 64, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int rr = 0; rr < RB; ++rr)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) P.gout[(size_t)pixg[rr][r] * a.cout + col] = acc[rr][r];
-    if (P.gst) {
-      // GroupNorm partials of this wave's TILE_M/2 pixels (one image) × its 32 channels: per lane
-      // over its rows in fp64, then over hh (lane ^ 32) and the group's cpg adjacent lanes
-      double s1 = 0, s2 = 0;
-#pragma unroll
-      for (int rr = 0; rr < RB; ++rr)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const double v = (double)acc[rr][r];
-          s1 += v;
-          s2 += v * v;
-        }
-      const int cpg = a.cout / P.ggroups;
-      s1 += __shfl_xor(s1, 32);
-      s2 += __shfl_xor(s2, 32);
-      for (int d = 1; d < cpg; d <<= 1) {
-        s1 += __shfl_xor(s1, d);
-        s2 += __shfl_xor(s2, d);
-      }
-      if (hh == 0 && col % cpg == 0) {
-        const int tpi = 2 * tiles_per_img;
-        double* o = P.gst + (((size_t)img * tpi + 2 * tin + wm) * P.ggroups + col / cpg) * 2;
-        o[0] = s1;
-        o[1] = s2;
-      }
-    }
-    return;
-  }
   if (col >= a.cout) return;
   const float bias = a.bias ? a.bias[col] : 0.f;
   const float osc = a.out_scale ? a.out_scale[col] : 1.f;
@@ -608,7 +492,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(
 
 int rup(int a, int b) { return (a + b - 1) / b * b; }
 
-template <int KH, int KW, int S, int TM, bool NORM, bool GNF = false>
+template <int KH, int KW, int S, int TM, bool NORM>
 int launch_enc(EncParams p, hipStream_t st) {
   p.tc = p.ow < TM ? p.ow : TM;
   if (p.tc < 8 || TM % p.tc || p.ow % p.tc) return SCFLOW_EUNSUPPORTED;
@@ -616,19 +500,17 @@ int launch_enc(EncParams p, hipStream_t st) {
   if (p.oh % p.tr) return SCFLOW_EUNSUPPORTED;
   p.hr = (p.tr - 1) * S + KH;
   p.hc = (p.tc - 1) * S + KW;
-  const int ctot = p.a.cin + p.a.cin1;
-  const size_t lds = sizeof(float) * ((size_t)p.hr * p.hc * ELDA + (size_t)KH * KW * EBN * ELDA +
-                                      (GNF ? 2 * (size_t)ctot + 4 : 0));
+  const size_t lds = sizeof(float) * ((size_t)p.hr * p.hc * ELDA + (size_t)KH * KW * EBN * ELDA);
   if ((size_t)p.hr * p.hc * (EBK / 4) > (size_t)256 * enc_na(TM, KH, KW, S)) return SCFLOW_EUNSUPPORTED;
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)enc_conv_kernel<KH, KW, S, TM, NORM, GNF>,
+    (void)hipFuncSetAttribute((const void*)enc_conv_kernel<KH, KW, S, TM, NORM>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   dim3 grid(p.a.n * (p.oh / p.tr) * (p.ow / p.tc), rup(p.a.cout, EBN) / EBN,
             p.a.ksplit > 1 ? p.a.ksplit : 1);
-  enc_conv_kernel<KH, KW, S, TM, NORM, GNF><<<grid, 256, lds, st>>>(p);
+  enc_conv_kernel<KH, KW, S, TM, NORM><<<grid, 256, lds, st>>>(p);
   return scflow_launch_status();
 }
 
@@ -638,35 +520,6 @@ int launch_enc_norm(const EncParams& p, hipStream_t st) {
 }
 
 }  // namespace
-
-// scflow_ph_conv_gn's path 1 (posehead.hip decides the plan): 3×3, pad 1, stride 1 or 2, tile of
-// tm output pixels (128 at stride 1, 64 at stride 2) × 64 output channels
-int scflow_enc_conv_gn_launch(const scflow_ph_conv_gn_args* g, int tm, void* stream) {
-  EncParams p{};
-  scflow_enc_conv_args& a = p.a;
-  a.src = g->src0; a.cin = g->c0; a.s_in = g->s0;
-  a.src1 = g->src1; a.cin1 = g->c1; a.s_in1 = g->s1;
-  a.ksplit = g->ksplit;
-  a.weight = g->weight;
-  a.out = g->ksplit > 1 ? g->parts : g->out;
-  a.s_out = g->cout;
-  a.n = g->n; a.h = g->h; a.w = g->w; a.cout = g->cout; a.kh = 3; a.kw = 3;
-  a.stride = g->stride; a.pad = 1;
-  p.oh = (g->h + 2 - 3) / g->stride + 1;
-  p.ow = (g->w + 2 - 3) / g->stride + 1;
-  p.nst0 = g->c0 / EBK;
-  p.nst = (g->c0 + g->c1) / EBK;
-  p.gin = g->in_stats; p.gin_tpi = g->in_tpi; p.gin_groups = g->in_groups;
-  p.gin_gamma = g->in_gamma; p.gin_beta = g->in_beta; p.gin_eps = g->in_eps;
-  p.gout = g->out; p.gcnt = g->counters; p.gst = g->out_stats; p.ggroups = g->out_groups;
-  hipStream_t st = (hipStream_t)stream;
-  const bool norm = g->in_stats != nullptr;
-  if (g->stride == 1 && tm == 128)
-    return norm ? launch_enc<3, 3, 1, 128, true, true>(p, st) : launch_enc<3, 3, 1, 128, false, true>(p, st);
-  if (g->stride == 2 && tm == 64)
-    return norm ? launch_enc<3, 3, 2, 64, true, true>(p, st) : launch_enc<3, 3, 2, 64, false, true>(p, st);
-  return SCFLOW_EUNSUPPORTED;
-}
 
 SCFLOW_API long long scflow_enc_conv_packed_size(int cout, int cin, int kh, int kw) {
   // cin = all input channels (cin + cin1 of the conv args)

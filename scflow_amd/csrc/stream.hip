@@ -49,24 +49,3 @@ SCFLOW_API int scflow_event_elapsed_ms(void* start, void* end, float* ms) {
   return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end);
 }
 
-// Uncached device memory (MTYPE UC: every access goes to memory, no L2 / L1 copies), zero-filled.
-// (Measured for the pose head's last-arriver slabs: slower than agent-scope accesses to ordinary
-// memory — UC traffic skips the Infinity Cache — so those use ordinary memory.)
-SCFLOW_API int scflow_alloc_uncached(long long bytes, void** ptr) {
-  if (!ptr || bytes <= 0) return SCFLOW_EINVAL;
-  void* p = nullptr;
-  hipError_t r = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached);
-  if (r != hipSuccess) return (int)r;
-  r = hipMemset(p, 0, (size_t)bytes);
-  if (r != hipSuccess) {
-    (void)hipFree(p);
-    return (int)r;
-  }
-  *ptr = p;
-  return SCFLOW_OK;
-}
-
-SCFLOW_API int scflow_free_uncached(void* ptr) {
-  if (!ptr) return SCFLOW_EINVAL;
-  return (int)hipFree(ptr);
-}

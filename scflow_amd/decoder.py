@@ -110,13 +110,6 @@ class SCFlowDecoder(nn.Module):
         # CUs while the other half's convolutions hold every CU's LDS, so they serialise anyway
         self.pingpong = False
         self.pingpong_min = 4
-        # with fuse_tail: the pose head after its first conv (GroupNorms, convs 2-3, FCs, heads)
-        # and the pose step as ONE persistent launch (scflow_ph_tail) instead of 9.  Off: measured
-        # slower (tools/dbg/ph_tail_check.py: 151 vs 127 µs per pose head at B=16) — its phases
-        # are a dependency chain of latency-bound items, each paying cross-XCD hand-off latency
-        # (agent release + acquire + L2 misses on the producer's lines) that a kernel boundary
-        # (≈2 µs) does not
-        self.fuse_posehead = False
         # with fuse_tail: the iteration's pose step runs only its ↓8 part (the next iteration's
         # flow, scflow_pose_step_part) on the critical path; its full-resolution outputs (pose
         # flow, ×8 prediction, mask) run on the side stream during the next iteration's GRU
@@ -520,7 +513,7 @@ class SCFlowDecoder(nn.Module):
 
         pose_x = []
         tail_calls = None  # fused tail: per-iteration (heads, pose_step) launches, built once
-        defer = fuse_tail and self.defer_full_res and not self.fuse_posehead and iters > 1
+        defer = fuse_tail and self.defer_full_res and iters > 1
         # Δflow alternates between two buffers when the full-resolution outputs are deferred: the
         # previous iteration's deferred launch reads its Δflow on the side stream while this
         # iteration's flow predictor writes the other one on the main stream
@@ -532,14 +525,7 @@ class SCFlowDecoder(nn.Module):
             t_scr = torch.empty(N, 3, device=dev, dtype=f32)
 
         def seg_pose_trunk():
-            pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep, slot=slot))
-
-        fuse_ph = fuse_tail and self.fuse_posehead and \
-            self.pose_pred.tail_supported(hid, Chan.whole(FM), N, h, w)
-        ph_ctx = []
-
-        def seg_pose_conv1():
-            ph_ctx.append(self.pose_pred.tail_conv1(hid, Chan.whole(FM), N, h, w, ws=keep))
+            pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep))
 
         for it in range(iters):
             par = f"{it % 2}" if fuse_tail else ""
@@ -610,10 +596,7 @@ class SCFlowDecoder(nn.Module):
             if mask_lr is not None:
                 mask_lr = MASK
             # a7 pose head on cat[h, Δflow feat, mask feat] (two channel sources, no concat)
-            if fuse_ph:
-                segment("pose_conv1", seg_pose_conv1)
-            else:
-                segment("pose_trunk", seg_pose_trunk)
+            segment("pose_trunk", seg_pose_trunk)
             drot, dtr = o_drot[it], o_dt[it]
             if fuse_tail:
                 # a8 + a10 + a11 ↑ (+ the next iteration's a11 ↓): one launch.  The heads and
@@ -632,28 +615,20 @@ class SCFlowDecoder(nn.Module):
                         nxt = dict(lr_next=None if last else Chan.whole(F2s[(j + 1) % 2]),
                                    hx_next=None if last else hx_flow,
                                    depth_transform=self.depth_transform)
-                        if fuse_ph:  # GN 1 → … → heads → pose step: one launch
-                            ps = ops.pose_step_struct(*step, **nxt)
-                            args = self.pose_pred.tail_args(ph_ctx[0], label, o_drot[j], o_dt[j],
-                                                            pose=ps)
+                        with ops.binding(hc, run=False):
+                            self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
+                        if defer and not last:
                             with ops.binding(pc, run=False):
-                                ops.ph_tail(args, o_drot[j])
+                                ops.pose_step(*step, **nxt, parts=2)
+                            with ops.binding(fc, run=False):
+                                if self.fullres_given:
+                                    ops.pose_step_given(o_R[j], o_t[j], *step[4:6], *step[8:])
+                                else:
+                                    fstep = step[:6] + (R_scr, t_scr) + step[8:]
+                                    ops.pose_step(*fstep, **nxt, parts=1)
                         else:
-                            with ops.binding(hc, run=False):
-                                self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
-                            if defer and not last:
-                                with ops.binding(pc, run=False):
-                                    ops.pose_step(*step, **nxt, parts=2)
-                                with ops.binding(fc, run=False):
-                                    if self.fullres_given:
-                                        ops.pose_step_given(o_R[j], o_t[j], *step[4:6],
-                                                            *step[8:])
-                                    else:
-                                        fstep = step[:6] + (R_scr, t_scr) + step[8:]
-                                        ops.pose_step(*fstep, **nxt, parts=1)
-                            else:
-                                with ops.binding(pc, run=False):
-                                    ops.pose_step(*step, **nxt)
+                            with ops.binding(pc, run=False):
+                                ops.pose_step(*step, **nxt)
                         tail_calls.append((hc, pc, fc))
                         Rp, tp = o_R[j], o_t[j]
                 hc, pc, fc = tail_calls[it]
@@ -661,7 +636,7 @@ class SCFlowDecoder(nn.Module):
                     c()
                 # deferred: this is the critical-path ↓8 launch (its own timer); otherwise the
                 # whole pose step
-                hook = "pose_step_crit" if fc else "pose_tail" if fuse_ph else "pose_flow"
+                hook = "pose_step_crit" if fc else "pose_flow"
                 self._hook(hook, True)
                 for c in pc:
                     c()
@@ -687,9 +662,5 @@ class SCFlowDecoder(nn.Module):
             dts.append(dtr)
             yield "tail"
 
-        if fuse_ph and ph_ctx:
-            # the opt-in persistent tail: a dependency wait that gave up leaves invalid poses —
-            # check the launches' sticky error word once per forward (one host sync)
-            self.pose_pred.tail_check(ph_ctx[0])
         return (list(o_flow_pose.unbind(0)), list(o_flow_pred.unbind(0)), list(o_R.unbind(0)),
                 list(o_t.unbind(0)), list(o_mask.unbind(0)), drots, dts)

@@ -203,7 +203,7 @@ class ConvRunner:
     @property
     def winograd(self) -> bool:
         """True once a launch picked the Winograd kernel (F(2×2,3×3) or F(4,5))."""
-        return getattr(self, "_bk", None) == _lib.CONV_WINO
+        return getattr(self, "_bk", None) in (_lib.CONV_WINO, _lib.CONV_WINO4)
 
     def mfma_flops(self, m: int, c0: int, c1: int = 0) -> float:
         """FLOPs the matrix cores execute for one launch over m output pixels with the inputs
@@ -212,6 +212,8 @@ class ConvRunner:
         channels padded to 32; the direct kernel does the algorithmic work on padded channels."""
         ru = lambda v, q: (v + q - 1) // q * q  # noqa: E731
         kpad, npad = ru(c0, 32) + ru(c1, 32), ru(self.cout, 32)
+        if getattr(self, "_bk", None) == _lib.CONV_WINO4:  # 36 points per 4×4 tile, K padded to 8
+            return 2.0 * 36 * (m / 16) * (ru(c0, 8) + ru(c1, 8)) * npad
         if self.winograd:
             pts, tile = (16, 4) if self.kh * self.kw == 9 else (8, 4)
             return 2.0 * pts * (m / tile) * kpad * npad
@@ -361,24 +363,6 @@ def run_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int
         if hk is not None:
             ops.host_call(lambda hk=hk: hk(False))
         cur = out
-
-
-class _LaBuf:
-    """A zero-filled byte buffer with a raw pointer (last-arriver slabs / counters)."""
-    __slots__ = ("t", "ptr", "nbytes")
-
-    def __init__(self, nbytes: int, dev: int) -> None:
-        self.t = torch.zeros((int(nbytes) + 15) // 16 * 4, device=dev, dtype=torch.int32)
-        self.ptr, self.nbytes = self.t.data_ptr(), int(nbytes)
-
-
-class _Fc1Partials:
-    """The fused-statistics trunk's output when FC2 runs with the heads: FC1's K-split partials
-    plus FC2's slab buffer and the heads launch's arrival counter (kept zero between launches)."""
-    __slots__ = ("y1", "parts2", "counter", "ks")
-
-    def __init__(self, y1: Tensor, parts2, counter, ks: int) -> None:
-        self.y1, self.parts2, self.counter, self.ks = y1, parts2, counter, ks
 
 
 # ---------------------------------------------------------------------------------- a4
@@ -692,7 +676,7 @@ class MultiClassPoseHead(nn.Module):
         return drot, dt
 
     def trunk_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                  ws: Optional[list] = None, slot: int = 0) -> Tensor:
+                  ws: Optional[list] = None) -> Tensor:
         """Convs + FCs of forward_hip → the last FC's output [n, 256].  Every buffer it allocates
         is appended to ``ws`` (the decoder keeps them alive while replaying these launches).
 
@@ -701,10 +685,6 @@ class MultiClassPoseHead(nn.Module):
         else on the gather conv (conv3's 4×4 output)."""
         if any(m.norm_type != "GN" or m.act_type != "ReLU" for m in self.conv_layers):
             raise NotImplementedError("HIP pose head: conv + GroupNorm + ReLU layers only")
-        if self.fused_gn and self._gn_fused_ok(src0, src1, n, h, w):
-            # slot: trunks that may run concurrently (the decoder's ping-pong halves) take
-            # separate last-arriver buffers
-            return self._trunk_gn(src0, src1, n, h, w, ws, slot)
         dev = src0.buf.device
         keep = ws if ws is not None else []
 
@@ -780,155 +760,9 @@ class MultiClassPoseHead(nn.Module):
             x, xsplit, xbias, ldx = y, ks, lin.bias.detach(), lin.out_features
         return x
 
-    #: the fused-statistics trunk (scflow_ph_conv_gn / scflow_ph_fc_split_gn: 5 launches + heads,
-    #: no GroupNorm launches; K-split slabs summed by each tile's last-arriving workgroup).  Off:
-    #: measured slower in the decoder at B=16 (101 vs 96 µs per pose head) — the last-arriver
-    #: hand-off (agent-scope slab stores drained, arrival atomic, slab loads from the memory
-    #: side) costs about what the GroupNorm launch it replaces does
-    fused_gn = False
-
-    def _gn_plans(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int):
-        """[(args, plan, oh, ow)] per conv layer for the fused-statistics trunk, or None."""
-        if not 1 <= n <= 32 or len(self.fc_layers) != 2:
-            return None
-        if any(fc[0].in_features % 64 for fc in self.fc_layers):
-            return None
-        c1 = 0 if src1 is None else src1.c
-        if src0.c % 4 or c1 % 4:
-            return None
-        out, hh, ww, s0, s1 = [], h, w, src0, src1
-        for m in self.conv_layers:
-            cv = m.conv
-            if cv.bias is not None or cv.kernel_size[0] != cv.kernel_size[1] or \
-                    cv.stride[0] != cv.stride[1] or cv.padding[0] != cv.padding[1]:
-                return None
-            k, st, p = cv.kernel_size[0], cv.stride[0], cv.padding[0]
-            oh, ow = (hh + 2 * p - k) // st + 1, (ww + 2 * p - k) // st + 1
-            g = m.gn.num_groups
-            if cv.out_channels % 32 or cv.out_channels % g or 32 % (cv.out_channels // g):
-                return None
-            a = ops.ph_conv_gn_args(s0, s1, n, hh, ww, cv.out_channels, k, st, p)
-            plan = ops.ph_conv_gn_plan(a)
-            if plan is None:
-                return None
-            out.append((a, plan, oh, ow))
-            # the next layer reads this one's raw output (same geometry checks, pointer unused)
-            s0, s1, hh, ww = Chan(src0.buf, 0, cv.out_channels), None, oh, ow
-        c_last = self.conv_layers[-1].conv.out_channels
-        if n * c_last > 4096 or self.fc_layers[0][0].in_features != c_last * hh * ww:
-            return None
-        return out
-
-    def _gn_fused_ok(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int) -> bool:
-        return self._gn_plans(src0, src1, n, h, w) is not None
-
-    def _uncached(self, key, nbytes: int) -> "_LaBuf":
-        """A zero-filled device buffer of at least ``nbytes`` for a last-arriver reduction (the
-        kernels reach it with agent-scope accesses), kept on the module (one per key and
-        device; the counters stay zero between launches, so every launch that uses a buffer
-        must run to completion before the next starts)."""
-        bufs = getattr(self, "_uc_bufs", None)
-        if bufs is None:
-            bufs = self._uc_bufs = {}
-        dev = torch.cuda.current_device()
-        b = bufs.get((key, dev))
-        if b is None or b.nbytes < nbytes:
-            b = bufs[(key, dev)] = _LaBuf(nbytes, dev)
-        return b
-
-    def _gn_weight(self, i: int, path: int) -> Tensor:
-        """conv_layers[i]'s weights packed for plan path 1 (enc_conv) or 0 (ph_conv)."""
-        wt = self.conv_layers[i].conv.weight
-        packs = getattr(self, "_gn_packs", None)
-        if packs is None:
-            packs = self._gn_packs = {}
-        key = (wt.data_ptr(), wt._version, path, _lib.weights_generation())
-        if packs.get(i, (None,))[0] != key:
-            packs[i] = (key, ops.enc_conv_pack(wt) if path == 1 else ops.ph_conv_pack(wt))
-        return packs[i][1]
-
-    def _trunk_gn(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                  ws: Optional[list] = None, slot: int = 0) -> Tensor:
-        """trunk_hip with every GroupNorm fused (pose_head.py:201-211): each
-        conv (scflow_ph_conv_gn: the halo-staged MFMA conv or the gather conv, its K split
-        summed by the last-arriving workgroup of each tile) writes its raw output and fp64
-        GroupNorm partials; the next conv (or FC1) builds the affine from them in its
-        prologue.  Returns FC2's K-split partials."""
-        dev = src0.buf.device
-        keep = ws if ws is not None else []
-
-        def empty(*shape, dtype=torch.float32):
-            t = torch.empty(*shape, device=dev, dtype=dtype)
-            keep.append(t)
-            return t
-        plans = self._gn_plans(src0, src1, n, h, w)
-        ohl, owl = plans[-1][2], plans[-1][3]
-        c_last = self.conv_layers[-1].conv.out_channels
-        _, fc1_w = self._packs(c_last, ohl * owl)
-        cur0, cur1 = src0, src1
-        prev, prev_st = None, None
-        for i, (m, (a, plan, oh, ow)) in enumerate(zip(self.conv_layers, plans)):
-            cout = m.conv.out_channels
-            y = empty(n * oh * ow, cout)
-            st = empty(n, plan.tpi, m.gn.num_groups, 2, dtype=torch.float64)
-            a.src0, a.c0, a.s0 = cur0.ptr, cur0.c, cur0.stride
-            if cur1 is not None:
-                a.src1, a.c1, a.s1 = cur1.ptr, cur1.c, cur1.stride
-            else:
-                a.src1, a.c1, a.s1 = None, 0, 0
-            if prev is not None:
-                a.in_stats, a.in_tpi, a.in_groups = prev_st.data_ptr(), prev_st.shape[1], prev.gn.num_groups
-                g, b = prev.gn.weight.detach(), prev.gn.bias.detach()
-                keep += [g, b]
-                a.in_gamma, a.in_beta, a.in_eps = g.data_ptr(), b.data_ptr(), float(prev.gn.eps)
-            wpk = self._gn_weight(i, plan.path)
-            keep.append(wpk)
-            a.weight, a.out = wpk.data_ptr(), y.data_ptr()
-            a.out_stats, a.out_groups = st.data_ptr(), m.gn.num_groups
-            a.ksplit = plan.ksplit
-            if plan.ksplit > 1:
-                a.parts = self._uncached(("parts", i, slot), 4 * plan.parts_floats).ptr
-                a.counters = self._uncached(("cnt", i, slot), 4 * plan.counters).ptr
-            ops.ph_conv_gn(a, y)
-            cur0, cur1, prev, prev_st = Chan.whole(y), None, m, st
-        c = cur0.c
-        k_in = c * ohl * owl
-        ks = 4
-        l1, l2 = self.fc_layers[0][0], self.fc_layers[1][0]
-        y1 = empty(ks, n, l1.out_features)
-        ops.ph_fc_split_gn(cur0.buf, n, k_in, fc1_w, y1, l1.out_features, ks, c, prev_st,
-                           prev.gn.num_groups, ohl * owl, prev.gn.weight.detach(),
-                           prev.gn.bias.detach(), prev.gn.eps)
-        self._split_fc = True
-        if self.fused_fc2_heads and n * l2.out_features <= 8192 and l2.out_features % 4 == 0:
-            # FC2 and the heads run as ONE launch per call of heads_hip (last-arriver heads)
-            return _Fc1Partials(y1, self._uncached(("fc2", slot), 4 * ks * n * l2.out_features),
-                                self._uncached(("fc2cnt", slot), 4 * 64 * (1 + -(-l2.out_features // 16))),
-                                ks)
-        y2 = empty(ks, n, l2.out_features)
-        ops.ph_fc_split(y1, l1.out_features, n, l1.out_features, l2.weight.detach(), y2,
-                        l2.out_features, ks, xsplit=ks, xbias=l1.bias.detach())
-        return y2
-
-    #: FC2 + heads as one launch (scflow_ph_fc2_heads) after the fused-statistics trunk.  Off:
-    #: 21.8 µs vs 7.1 + 7.1 µs for the two launches (the single last workgroup's heads work and
-    #: the hand-off are slower than a second launch)
-    fused_fc2_heads = False
-
     def heads_hip(self, x, label: Tensor, drot: Tensor, dt: Tensor) -> None:
         """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt
-        (x: [n, 256], the last FC's split partial sums [split, n, 256], or FC1's partials from
-        the fused trunk — then FC2 runs here too, in the same launch)."""
-        if isinstance(x, _Fc1Partials):
-            l1, l2 = self.fc_layers[0][0], self.fc_layers[1][0]
-            n = x.y1.shape[1]
-            ops.ph_fc2_heads(x.y1, l1.bias.detach(), n, l1.out_features, l2.weight.detach(),
-                             l2.bias.detach(), x.parts2, l2.out_features, x.ks,
-                             self.rotation_pred.weight.detach(), self.rotation_pred.bias.detach(),
-                             self.rotation_out_channels, self.translation_pred.weight.detach(),
-                             self.translation_pred.bias.detach(), label.long(), self.num_class,
-                             drot, dt, x.counter)
-            return
+        (x: [n, 256] or the last FC's split partial sums [split, n, 256])."""
         if x.dim() == 3:
             n, k = x.shape[1], x.shape[2]
             ops.ph_heads(x, n, k, self.rotation_pred.weight.detach(),
@@ -942,152 +776,6 @@ class MultiClassPoseHead(nn.Module):
                      self.rotation_pred.bias.detach(), self.rotation_out_channels,
                      self.translation_pred.weight.detach(), self.translation_pred.bias.detach(),
                      label.long(), self.num_class, drot, dt)
-
-    # ---------------------------------------------------- fused tail (scflow_ph_tail)
-    #: work items per convolution phase of the fused tail (its K split is chosen to reach this)
-    tail_conv_items = 256
-    tail_fc_split = (4, 4)
-
-    def tail_supported(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int) -> bool:
-        """Whether ``tail_conv1`` + ``tail_args`` (one persistent launch after the first conv)
-        cover this head: three equal-width conv + GroupNorm + ReLU layers with the same square
-        kernel / stride / padding after the first, two FC layers, n ≤ 32."""
-        convs = [m.conv for m in self.conv_layers]
-        if len(convs) != 3 or len(self.fc_layers) != 2 or not 1 <= n <= 32:
-            return False
-        if any(m.norm_type != "GN" or m.act_type != "ReLU" or m.conv.bias is not None
-               for m in self.conv_layers):
-            return False
-        c = convs[0].out_channels
-        if c % 32 or any(cv.out_channels != c for cv in convs) or \
-                len({m.gn.num_groups for m in self.conv_layers}) != 1:
-            return False
-        cpg = c // self.conv_layers[0].gn.num_groups
-        if c % self.conv_layers[0].gn.num_groups or 32 % cpg:
-            return False
-        k2 = convs[1].kernel_size
-        if k2[0] != k2[1] or any(cv.kernel_size != k2 or cv.stride != convs[1].stride or
-                                 cv.padding != convs[1].padding or cv.stride[0] != cv.stride[1] or
-                                 cv.padding[0] != cv.padding[1] for cv in convs[1:]):
-            return False
-        if any(fc[0].in_features % 16 or fc[0].out_features % 16 for fc in self.fc_layers):
-            return False
-        if self.rotation_out_channels + 3 > 16:
-            return False
-        c1 = 0 if src1 is None else src1.c
-        k, s, p = convs[0].kernel_size[0], convs[0].stride[0], convs[0].padding[0]
-        return convs[0].kernel_size == (3, 3) and p == 1 and s in (1, 2) and \
-            src0.c % 16 == 0 and c1 % 16 == 0 and (h - 1) // s + 1 >= 8
-
-    def tail_conv1(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                   ws: Optional[list] = None) -> dict:
-        """The first conv on the MFMA halo conv with its K split into partial slabs (GroupNorm
-        and everything after it run in ``tail_args``' launch); returns the context
-        ``tail_args`` needs.  Buffers are appended to ``ws``."""
-        keep = ws if ws is not None else []
-        split = self._conv_mfma(0, src0, src1, n, h, w, None, None, keep)
-        if split is None:
-            raise NotImplementedError("tail_conv1: the first conv's shape has no K-split MFMA kernel")
-        return dict(parts=split[0], split=split[1], n=n, h=h, w=w, dev=src0.buf.device, keep=keep)
-
-    def tail_args(self, ctx: dict, label: Tensor, drot: Tensor, dt: Tensor,
-                  pose=None) -> "_lib.PhTailArgs":
-        """``scflow_ph_tail_args`` for GN 1 → … → heads (→ ``pose``, an
-        ``ops.pose_step_struct`` whose drot/dt are these) over ``tail_conv1``'s output.  The
-        workspace (summed conv outputs, GroupNorm affines, partial slabs, the counters) is
-        allocated once per context and shared by every call made with it (their launches must
-        run one after the other)."""
-        n, dev = ctx["n"], ctx["dev"]
-        convs = [m.conv for m in self.conv_layers]
-        c = convs[0].out_channels
-        hs, wsz = [], []
-        hh, ww = ctx["h"], ctx["w"]
-        for cv in convs:
-            k, s, p = cv.kernel_size[0], cv.stride[0], cv.padding[0]
-            hh, ww = (hh + 2 * p - k) // s + 1, (ww + 2 * p - k) // s + 1
-            hs.append(hh)
-            wsz.append(ww)
-        packs, fc1_w = self._packs(c, hs[2] * wsz[2])
-        if "tail_ws" not in ctx:
-            keep = ctx["keep"]
-
-            def empty(*shape, dtype=torch.float32):
-                t = torch.empty(*shape, device=dev, dtype=dtype)
-                keep.append(t)
-                return t
-            k2 = convs[1].kernel_size[0]
-            nchunks = k2 * k2 * (-(-c // 16))
-            splits = []
-            for j in (1, 2):
-                tiles = -(-n * hs[j] * wsz[j] // 32) * (c // 32)
-                splits.append(max(1, min(nchunks, -(-self.tail_conv_items // tiles))))
-            f1, f2 = (fc[0].out_features for fc in self.fc_layers)
-            sync = torch.zeros(_lib.load().scflow_ph_tail_sync_ints(n), device=dev,
-                               dtype=torch.int32)
-            keep.append(sync)
-            err = torch.zeros(4, device=dev, dtype=torch.int32)  # sticky give-up flag
-            keep.append(err)
-            ctx["tail_ws"] = dict(
-                y=[empty(n * hs[l] * wsz[l], c) for l in range(3)],
-                scale=[empty(n, c) for _ in range(3)], shift=[empty(n, c) for _ in range(3)],
-                splits=splits,
-                conv_parts=[empty(splits[j] * n * hs[j + 1] * wsz[j + 1], c) for j in range(2)],
-                fc1_parts=empty(self.tail_fc_split[0], n, f1),
-                fc2_parts=empty(self.tail_fc_split[1], n, f2), sync=sync, err=err)
-        t = ctx["tail_ws"]
-        a = _lib.PhTailArgs()
-        a.n, a.c, a.groups = n, c, self.conv_layers[0].gn.num_groups
-        for l, m in enumerate(self.conv_layers):
-            a.eps[l] = float(m.gn.eps)
-            a.h[l], a.w[l] = hs[l], wsz[l]
-            a.gamma[l], a.beta[l] = m.gn.weight.data_ptr(), m.gn.bias.data_ptr()
-            a.y[l], a.scale[l], a.shift[l] = (t["y"][l].data_ptr(), t["scale"][l].data_ptr(),
-                                              t["shift"][l].data_ptr())
-        a.conv1_parts, a.conv1_split = ctx["parts"].data_ptr(), ctx["split"]
-        a.conv_w[0], a.conv_w[1] = packs[1].data_ptr(), packs[2].data_ptr()
-        a.kh, a.stride, a.pad = convs[1].kernel_size[0], convs[1].stride[0], convs[1].padding[0]
-        for j in range(2):
-            a.conv_split[j] = t["splits"][j]
-            a.conv_parts[j] = t["conv_parts"][j].data_ptr()
-        l1, l2 = self.fc_layers[0][0], self.fc_layers[1][0]
-        a.fc1_w, a.fc1_b, a.fc1_n = fc1_w.data_ptr(), l1.bias.data_ptr(), l1.out_features
-        a.fc1_split, a.fc1_parts = self.tail_fc_split[0], t["fc1_parts"].data_ptr()
-        a.fc2_w, a.fc2_b, a.fc2_n = l2.weight.data_ptr(), l2.bias.data_ptr(), l2.out_features
-        a.fc2_split, a.fc2_parts = self.tail_fc_split[1], t["fc2_parts"].data_ptr()
-        a.rot_w, a.rot_b = self.rotation_pred.weight.data_ptr(), self.rotation_pred.bias.data_ptr()
-        a.rch = self.rotation_out_channels
-        a.trans_w = self.translation_pred.weight.data_ptr()
-        a.trans_b = self.translation_pred.bias.data_ptr()
-        label = label.long()
-        ctx["keep"].append(label)
-        a.label, a.num_class = label.data_ptr(), self.num_class
-        a.drot, a.dt = drot.data_ptr(), dt.data_ptr()
-        if pose is not None:
-            a.pose = ctypes.pointer(pose)
-        a.sync = t["sync"].data_ptr()
-        a.error = t["err"].data_ptr()
-        return a
-
-    @staticmethod
-    def tail_check(ctx: dict) -> None:
-        """Raise if any ``scflow_ph_tail`` launch made with this context gave up a dependency wait
-        (its results are then invalid).  Reads the sticky error word: a host synchronisation."""
-        t = ctx.get("tail_ws")
-        if t is not None and int(t["err"][0].item()):
-            raise ScflowError("scflow_ph_tail: a work item's dependency wait gave up (protocol "
-                              "stall); the pose-head results of this forward are invalid")
-
-    def forward_fused(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                      label: Tensor) -> Tuple[Tensor, Tensor]:
-        """``forward_hip`` as two launches (the first conv, then scflow_ph_tail)."""
-        dev = src0.buf.device
-        ctx = self.tail_conv1(src0, src1, n, h, w)
-        drot = torch.empty(n, self.rotation_out_channels, device=dev)
-        dt = torch.empty(n, 3, device=dev)
-        ops.ph_tail(self.tail_args(ctx, label.to(dev), drot, dt), drot)
-        ctx["result"] = (drot, dt)
-        self.tail_check(ctx)
-        return drot, dt
 
     def forward(self, x: Tensor, label: Tensor) -> Tuple[Tensor, Tensor]:
         """Reference API (NCHW in).  Runs the HIP kernels (inference; no autograd graph)."""

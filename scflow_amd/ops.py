@@ -328,7 +328,7 @@ def conv_pick_bk(n: int, h: int, w: int, c0: int, c1: int, cout: int, kh: int, k
     a.c0, a.c1, a.n, a.h, a.w = c0, c1, n, h, w
     a.cout, a.kh, a.kw, a.ph, a.pw, a.stride = cout, kh, kw, ph, pw, stride
     bk = _lib.load().scflow_conv_pick_bk(ctypes.byref(a))
-    if bk not in (8, 16, _lib.CONV_WINO, _lib.CONV_1X1W):
+    if bk not in (8, 16, _lib.CONV_WINO, _lib.CONV_1X1W, _lib.CONV_WINO4):
         check(bk if bk < 0 else -2, "scflow_conv_pick_bk")
     return bk
 
@@ -359,22 +359,6 @@ class BoundLaunch:
         rc = self.fn(self.ref, raw_stream(self.dev))
         if rc:
             check(rc, self.name)
-
-
-class UncachedBuffer:
-    """Zero-filled uncached device memory (scflow_alloc_uncached) on the current device — the
-    pose head's last-arriver slabs and counters; freed when the object dies."""
-
-    def __init__(self, nbytes: int) -> None:
-        lib = _lib.load()
-        h = ctypes.c_void_p()
-        check(lib.scflow_alloc_uncached(int(nbytes), ctypes.byref(h)), "scflow_alloc_uncached")
-        self.ptr, self.nbytes = h.value, int(nbytes)
-
-    def __del__(self) -> None:
-        if getattr(self, "ptr", None):
-            _lib.load().scflow_free_uncached(self.ptr)
-            self.ptr = None
 
 
 class SyncEvent:
@@ -464,6 +448,14 @@ def conv2d_args(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: i
     if res is not None:
         _require(res.buf, "res")
         a.res, a.sres = res.ptr, res.stride
+    if bk == _lib.CONV_WINO4:
+        # the transformed-input workspace, private to this launch (a bound launch keeps it with
+        # its arguments; an eager one returns it to the stream-ordered caching allocator)
+        nb = int(_lib.load().scflow_conv_workspace_bytes(ctypes.byref(a)))
+        check(nb if nb < 0 else 0, "scflow_conv_workspace_bytes")
+        ws = torch.empty(max(nb // 4, 1), device=src0.buf.device)
+        a.ws, a.ws_bytes = ws.data_ptr(), nb
+        a._ws = ws
     return a
 
 
@@ -571,41 +563,6 @@ def pose_step_given(R: Tensor, t: Tensor, K: Tensor, points: Tensor, flow_out: T
             1.0 / float(up_scale), 1)
 
 
-def pose_step_struct(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points: Tensor,
-                     R_out: Tensor, t_out: Tensor, flow_out: Tensor, invalid_num: float,
-                     lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], flow_up: Tensor,
-                     mask_up: Optional[Tensor], h: int, w: int, up_scale: float,
-                     lr_next: Optional[Chan] = None, hx_next: Optional[Chan] = None,
-                     weight: float = 10.0, depth_transform: str = "exp") -> "_lib.PoseStepArgs":
-    """``pose_step``'s arguments as a ``scflow_pose_step_args`` struct (for ``ph_tail``)."""
-    for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t), ("K", K), ("points", points),
-                  ("R_out", R_out), ("t_out", t_out), ("flow_out", flow_out), ("lr", lr),
-                  ("flow_up", flow_up)):
-        _require(x, nm)
-    n, H, W, _ = points.shape
-    if lr_next is not None and lr_next.buf.data_ptr() == lr.data_ptr():
-        raise ValueError("pose_step: lr_next must not alias lr")
-    s = _lib.PoseStepArgs()
-    s.drot6, s.dt, s.R_src, s.t_src, s.K = _p(drot), _p(dt), _p(R), _p(t), _p(K)
-    s.points, s.R_dst, s.t_dst, s.flow = _p(points), _p(R_out), _p(t_out), _p(flow_out)
-    s.n, s.H, s.W, s.weight = n, H, W, float(weight)
-    s.depth_transform, s.invalid_num = pose_mode(drot, depth_transform), float(invalid_num)
-    s.lr, s.delta, s.mask, s.flow_up, s.mask_up = _p(lr), _p(delta), _p(mask), _p(flow_up), _p(mask_up)
-    s.lr_next = None if lr_next is None else lr_next.ptr
-    s.s_next = 0 if lr_next is None else lr_next.stride
-    s.hx_next = None if hx_next is None else hx_next.ptr
-    s.s_hx = 0 if hx_next is None else hx_next.stride
-    s.h, s.w, s.up_scale, s.down_scale = h, w, float(up_scale), 1.0 / float(up_scale)
-    return s
-
-
-def ph_tail(args: "_lib.PhTailArgs", dev_tensor: Tensor) -> None:
-    """The fused pose-head tail (scflow_ph_tail; arguments built by
-    ``MultiClassPoseHead.tail_args``) on ``dev_tensor``'s device."""
-    _require(dev_tensor, "device tensor", contiguous=False)
-    _launch("scflow_ph_tail", dev_tensor, ctypes.byref(args))
-
-
 # ------------------------------------------------------------------------------- resampling
 def flow_downsample(flow: Tensor, out0: Chan, h: int, w: int, value_scale: float,
                     out1: Optional[Chan] = None) -> None:
@@ -678,66 +635,6 @@ def ph_gn_reduce(parts: Tensor, nsplit: int, y: Tensor, n: int, hw: int, c: int,
     """y = sum of the nsplit partial slabs of ``parts`` [nsplit, n·hw, c]; GN scale/shift of y."""
     _launch("scflow_ph_gn_reduce", parts,_p(parts), nsplit, n * hw * c, _p(y), n, hw, c, groups,
                                           _p(gamma), _p(beta), float(eps), _p(scale), _p(shift))
-
-
-def ph_gn_tpi(oh: int, ow: int) -> int:
-    """GroupNorm partial statistics per image of an oh×ow conv output (scflow_ph_gn_tpi); 0 if
-    the fused-statistics pose head does not support the size."""
-    v = int(_lib.load().scflow_ph_gn_tpi(oh, ow))
-    return v if v > 0 else 0
-
-
-def ph_conv_gn_args(src0: Chan, src1: Optional[Chan], n: int, h: int, w: int, cout: int, k: int,
-                    stride: int, pad: int) -> "_lib.PhConvGnArgs":
-    """A ``scflow_ph_conv_gn_args`` with the geometry filled in (buffers are set by the caller
-    after ``ph_conv_gn_plan``)."""
-    a = _lib.PhConvGnArgs()
-    a.src0, a.c0, a.s0 = src0.ptr, src0.c, src0.stride
-    if src1 is not None:
-        a.src1, a.c1, a.s1 = src1.ptr, src1.c, src1.stride
-    a.n, a.h, a.w, a.cout, a.kh, a.kw, a.stride, a.pad = n, h, w, cout, k, k, stride, pad
-    a.ksplit = 1
-    return a
-
-
-def ph_conv_gn_plan(a: "_lib.PhConvGnArgs") -> Optional["_lib.PhConvGnPlan"]:
-    """scflow_ph_conv_gn_plan_for: path, K split, partials per image and buffer sizes (None if
-    the shape is unsupported)."""
-    plan = _lib.PhConvGnPlan()
-    rc = _lib.load().scflow_ph_conv_gn_plan_for(ctypes.byref(a), ctypes.byref(plan))
-    return plan if rc == 0 else None
-
-
-def ph_conv_gn(a: "_lib.PhConvGnArgs", dev_tensor: Tensor) -> None:
-    """scflow_ph_conv_gn (arguments from ``ph_conv_gn_args`` + the plan's buffers)."""
-    _require(dev_tensor, "device tensor", contiguous=False)
-    _launch("scflow_ph_conv_gn", dev_tensor, ctypes.byref(a))
-
-
-def ph_fc_split_gn(x: Tensor, m: int, k: int, W: Tensor, parts: Tensor, n: int, ksplit: int,
-                   gn_c: int, stats: Tensor, groups: int, hw: int, gamma: Tensor, beta: Tensor,
-                   eps: float) -> None:
-    """scflow_ph_fc_split_gn: K-split FC partials of relu(GN(x)) with the GroupNorm built from the
-    producing conv's partial statistics ``stats`` [m, tpi, groups, 2]."""
-    _require(stats, "stats", dtype=torch.float64)
-    _launch("scflow_ph_fc_split_gn", x, _p(x), m, k, _p(W), _p(parts), n, ksplit, gn_c, _p(stats),
-            stats.shape[1], groups, hw, _p(gamma), _p(beta), float(eps))
-
-
-def ph_fc2_heads(parts1: Tensor, b1: Tensor, m: int, k: int, W2: Tensor, b2: Tensor,
-                 parts2, n2: int, ksplit: int, Wr: Tensor, br: Tensor, rch: int,
-                 Wt: Tensor, bt: Tensor, label: Tensor, num_class: int, drot: Tensor, dt: Tensor,
-                 counter) -> None:
-    """FC2 on FC1's K-split partials + the label[0] heads in one launch (scflow_ph_fc2_heads);
-    ``parts2`` / ``counter``: buffers with ``ptr`` / ``nbytes`` (FC2's slabs, the zeroed arrival
-    counter)."""
-    if label.dtype != torch.int64 or label.device != parts1.device:
-        raise TypeError("label must be an int64 tensor on the same device")
-    if parts2.nbytes < 4 * ksplit * m * n2 or counter.nbytes < 4 * 64 * (1 + -(-n2 // 16)):
-        raise ValueError("ph_fc2_heads: uncached buffers too small")
-    _launch("scflow_ph_fc2_heads", parts1, _p(parts1), parts1.shape[0], _p(b1), m, k, _p(W2), _p(b2),
-            parts2.ptr, n2, ksplit, _p(Wr), _p(br), rch, _p(Wt), _p(bt), _p(label), num_class,
-            _p(drot), _p(dt), counter.ptr)
 
 
 def ph_fc_permute(W: Tensor, c: int, hw: int) -> Tensor:

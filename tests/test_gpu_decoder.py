@@ -108,33 +108,6 @@ def test_decoder_schedules_bit_identical():
 
 
 @pytest.mark.gpu
-def test_decoder_fused_posehead_tail():
-    """fuse_posehead: the pose head after its first conv + the pose step as one persistent launch
-    (scflow_ph_tail) against the default launches, multi-class batch, and against the oracle.  The
-    GroupNorm moments are summed in another fp64 order, so EPE ≤ 1e-4 px between the two, and the
-    oracle's EPE gate (1e-3 px) for the fused one."""
-    inp = decoder_inputs(4, 256, seed=19)
-    inp["label"] = torch.tensor([5, 2, 18, 5])
-    dec = build_decoder(4, seed=6)
-    base = run_gpu(dec, inp)
-    dec.fuse_posehead = True
-    try:
-        out = run_gpu(dec, inp)
-    finally:
-        dec.fuse_posehead = False
-    for k in (0, 1):
-        for a, b in zip(base[k], out[k]):
-            assert float(orc.cal_epe_mean(a, b).max()) <= 1e-4
-    for k in (2, 3, 5, 6):
-        for a, b in zip(base[k], out[k]):
-            torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-5)
-    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
-    ref = orc.decoder_forward(sd, **inp, iters=4)
-    for i in range(4):
-        assert float(orc.cal_epe_mean(ref[0][i], out[0][i]).max()) <= EPE_TOL
-
-
-@pytest.mark.gpu
 def test_decoder_pingpong_halves_equal_whole_batch():
     """_forward_pingpong (two interleaved halves on two stream pairs, both taking the whole
     batch's label[0] for the pose head) against the single-schedule forward of the same

@@ -6,6 +6,8 @@ Tolerances (fp32 throughout):
 * convolutions: |Δ| ≤ 2e-5·sqrt(K) relative to the output scale (fp32, K-long sums);
 * pose / resampling: ≤ 1e-4 px (float32 projective division).
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -283,6 +285,65 @@ def test_conv2d_winograd(ops, case):
     close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"winograd conv {case}")
 
 
+@pytest.mark.parametrize("case", [
+    # (n, h, w, c0, c1, cout, act)
+    (2, 32, 32, 256, 0, 192, "ReLU"),        # corr_net.1
+    (2, 32, 32, 192, 64, 126, "ReLU"),       # out_net: two sources, cout not /32
+    (16, 32, 32, 128, 0, 512, "ReLU"),       # B=16 XHead hidden convs (flow ‖ mask)
+    (3, 32, 32, 12, 20, 40, "Tanh"),         # channels not /8 per source, cout 40
+    (1, 64, 64, 128, 0, 64, None),           # 512² feature size
+    (1, 20, 12, 36, 4, 100, "Sigmoid"),      # 15 tiles: a partial tile block, ragged channels
+    (2, 128, 128, 64, 0, 64, "ReLU"),        # encoder width
+])
+def test_conv2d_winograd_f4x4(ops, case):
+    """Winograd F(4×4,3×3) (SCFLOW_CONV_WINO4: input transform launch + point GEMMs with the
+    output transform in the epilogue) vs an fp64 direct conv.  Tolerance: its fp32 error is ≈ 10×
+    the direct conv's (points {0, ±1, 2, −½, ∞}; 1.3e-5 of outputs ≈ 4 at 256 channels in a
+    numpy restatement) — 5e-5·√(K/256) absolute on unit-scale outputs."""
+    from scflow_amd._lib import CONV_WINO4
+    n, h, w, c0, c1, cout, act = case
+    got, ref = _conv_case(ops, n, h, w, c0, c1, cout, 3, 1, act, bk=CONV_WINO4)
+    kk = (c0 + c1) * 9
+    close(got, ref, 5e-5 * np.sqrt(kk / 256 / 9) * 3 + 1e-6, 1e-5, f"F(4x4,3x3) conv {case}")
+
+
+def test_conv2d_winograd_f4x4_fused_epilogue(ops):
+    """F(4×4,3×3) with the encoder's fused forms: input InstanceNorm + ReLU on load, eval-BN
+    affine, residual and bias map, against fp64 (and the workspace query)."""
+    from scflow_amd import _lib
+    from scflow_amd.modules import ConvRunner
+    g = torch.Generator().manual_seed(23)
+    n, h, w, c, cout = 2, 32, 32, 64, 96
+    x = torch.randn(n, h, w, c, generator=g)
+    isc, ish = torch.rand(n, c, generator=g) + 0.5, torch.randn(n, c, generator=g) * 0.2
+    osc, osh = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.2
+    res = torch.randn(n, h, w, cout, generator=g)
+    bm = torch.randn(n, h, w, cout, generator=g)
+    conv = torch.nn.Conv2d(c, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / np.sqrt(9 * c))
+        conv.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+    xa = torch.relu(x.double() * isc.double()[:, None, None] + ish.double()[:, None, None])
+    ref = F.conv2d(xa.permute(0, 3, 1, 2), conv.weight.double(), conv.bias.double(), padding=1)
+    ref = ref.permute(0, 2, 3, 1) * osc.double() + osh.double() + res.double() + bm.double()
+    ref = torch.relu(ref)
+    r = ConvRunner([conv.cuda()], "ReLU")
+    packed, bias = r.packed(c, 0, w, _lib.CONV_WINO4)
+    out = torch.empty(n * h * w, cout, device="cuda")
+    a = ops.conv2d_args(ops.Chan.whole(x.cuda().reshape(-1, c)), packed, bias, n, h, w, cout, 3, 3,
+                        1, 1, "ReLU", out=ops.Chan.whole(out), bias_map=ops.Chan.whole(bm.cuda().reshape(-1, cout)),
+                        bk=_lib.CONV_WINO4, in_scale=isc.cuda(), in_shift=ish.cuda(),
+                        out_scale=osc.cuda(), out_shift=osh.cuda(),
+                        res=ops.Chan.whole(res.cuda().reshape(-1, cout)))
+    assert a.ws_bytes == -(-n * h * w // 16 // 32) * 8 * 36 * 1024
+    ops.check(_lib.load().scflow_conv2d(ctypes.byref(a), ops.raw_stream(0)), "scflow_conv2d")
+    torch.cuda.synchronize()
+    close(out.view(n, h, w, cout), ref, 2e-4, 1e-5, "F(4x4,3x3) fused epilogue")
+    # a workspace that is too small is refused
+    a.ws_bytes -= 16
+    assert _lib.load().scflow_conv2d(ctypes.byref(a), ops.raw_stream(0)) != 0
+
+
 @pytest.mark.parametrize("k,pad", [((1, 5), (0, 2)), ((5, 1), (2, 0))])
 @pytest.mark.parametrize("bk", [16, 2])
 @pytest.mark.parametrize("n", [2, 16])
@@ -542,61 +603,6 @@ def test_pose_head_hip_vs_oracle(ops, n, feat):
     # NCHW module API
     r2, t2 = head(x.cuda(), label.cuda())
     close(r2, r, 1e-6, 1e-6, "pose head NCHW api")
-    # the opt-in fused-statistics trunk (scflow_ph_conv_gn: no GroupNorm launches, last-arriver
-    # K-split sums), with and without FC2 + heads in one launch, against the default trunk
-    fused = head._gn_fused_ok(ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf), n, feat, feat)
-    assert fused  # every configuration here (n ≤ 32, 32² and 64² features) supports it
-    for fc2h in (False, True):
-        head.fused_gn, head.fused_fc2_heads = True, fc2h
-        try:
-            r4, t4 = head.forward_hip(ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf), n, feat, feat,
-                                      label.cuda())
-        finally:
-            head.fused_gn, head.fused_fc2_heads = False, False
-        close(r4, r_ref, 2e-5, 1e-5, f"pose head rotation (fused statistics, fc2+heads {fc2h})")
-        close(t4, t_ref, 2e-5, 1e-5, f"pose head translation (fused statistics, fc2+heads {fc2h})")
-        close(r4, r, 1e-5, 1e-6, "fused-statistics vs GroupNorm-launch trunk")
-    # fused tail (first conv + ONE persistent launch: scflow_ph_tail), twice (the second launch
-    # reuses the sync words); its error word must stay clear
-    src0, src1 = ops.Chan(hbuf, 0, 128), ops.Chan.whole(fbuf)
-    assert head.tail_supported(src0, src1, n, feat, feat)
-    for rep in range(2):
-        ctx = head.tail_conv1(src0, src1, n, feat, feat)
-        r3 = torch.empty(n, 6, device="cuda")
-        t3 = torch.empty(n, 3, device="cuda")
-        ops.ph_tail(head.tail_args(ctx, label.cuda(), r3, t3), r3)
-        torch.cuda.synchronize()
-        sync = ctx["tail_ws"]["sync"].cpu()
-        assert int(sync[2]) == 0, ("fused pose-head tail: a dependency wait gave up "
-                                   f"(ticket, counter, value, target, phase+1) = {sync[9:14].tolist()}")
-        close(r3, r_ref, 2e-5, 1e-5, "fused pose head rotation")
-        close(t3, t_ref, 2e-5, 1e-5, "fused pose head translation")
-        close(r3, r, 1e-5, 1e-6, "fused vs unfused pose head rotation")
-        head.tail_check(ctx)  # the sticky error word stayed clear too
-
-
-def test_pose_head_fused_tail_give_up_raises(ops, monkeypatch):
-    """A protocol stall in the persistent pose-head tail is reported, not silently wrong:
-    SCFLOW_PHT_DBG=2 makes every work item skip its completion signal, so the first dependency
-    wait gives up after its 50 ms bound (every later wait falls through) and sets the sticky error
-    word; forward_fused (and the decoder, once per forward) raise ScflowError."""
-    from scflow_amd import synthetic
-    from scflow_amd._lib import ScflowError
-    from scflow_amd.modules import MultiClassPoseHead
-    n, feat = 4, 32
-    head = MultiClassPoseHead(21, 224, "Basic", dict(type="GN", num_groups=32),
-                              dict(type="ReLU"), feat_size=(feat, feat), rotation_mode="ortho6d")
-    synthetic.fill_module_(head, seed=7)
-    head = head.cuda()
-    x = torch.relu(torch.randn(n * feat * feat, 224, device="cuda"))
-    label = torch.zeros(n, dtype=torch.long, device="cuda")
-    src = ops.Chan.whole(x)
-    head.forward_fused(src, None, n, feat, feat, label)  # clean run: no error
-    monkeypatch.setenv("SCFLOW_PHT_DBG", "2")
-    with pytest.raises(ScflowError, match="gave up"):
-        head.forward_fused(src, None, n, feat, feat, label)
-    monkeypatch.delenv("SCFLOW_PHT_DBG")
-    head.forward_fused(src, None, n, feat, feat, label)  # a fresh context starts clean again
 
 
 def test_corr_lookup_far_out_of_bounds(ops):
