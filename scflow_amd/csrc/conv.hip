@@ -922,12 +922,16 @@ static unsigned long long* g_wino_stamps = nullptr;
 #include "conv_wino4.h"
 
 // F(4×4,3×3) (conv_wino4.h) for the 3×3 convs it covers with at least WINO4_MIN_COUT output
-// channels; SCFLOW_CONV_WINO4 = 0 off, 1 default, 2 every covered shape (A/B)
+// channels; SCFLOW_CONV_WINO4 = 0 off, 1 default, 2 every covered shape (A/B).  Measured at
+// configs[1] (B=16, 32×32; tools/sess_w4c.sh, round 5): XHead hidden 128→512 59 vs 91 µs,
+// corr_net.1 256→192 57 vs 78 µs (F(2×2,3×3)), out_net 256→126 56 vs 50 µs — at 126 channels
+// the grid is 128 workgroups on 256 CUs and the transform pass (≈ 12 µs at 256 input channels)
+// is not paid back; decoder 4.98 vs 5.11 ms/forward with both wide convs on F(4×4).
 #ifndef WINO4_MIN_COUT
-#define WINO4_MIN_COUT 96
+#define WINO4_MIN_COUT 160
 #endif
 #ifndef WINO4_DEFAULT
-#define WINO4_DEFAULT 0
+#define WINO4_DEFAULT 1
 #endif
 bool wino4_pick(const scflow_conv_args& a) {
   static int mode = -1;

@@ -240,11 +240,15 @@ def test_conv2d_mfma_stage_depths(ops, case, bk):
 
 
 def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
-    """Host query: 3×3 / 1×5 / 5×1 stride-1 convs take the Winograd kernels; the 1×1 corr_net.0
+    """Host query: 3×3 / 1×5 / 5×1 stride-1 convs take the Winograd kernels (F(4×4,3×3) for the wide
+    3×3 ones); the 1×1 corr_net.0
     conv the wide 1×1 kernel up to two workgroups per CU; a two-source 1×1 conv 16-deep stages
     of the direct conv."""
-    from scflow_amd._lib import CONV_WINO
-    assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == CONV_WINO
+    from scflow_amd._lib import CONV_WINO, CONV_WINO4
+    # the wide 3×3 convs (≥ 160 output channels) take F(4×4,3×3), narrower ones F(2×2,3×3)
+    assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == CONV_WINO4  # corr_net.1
+    assert ops.conv_pick_bk(16, 32, 32, 128, 0, 512, 3, 3, 1, 1) == CONV_WINO4  # XHead hidden
+    assert ops.conv_pick_bk(16, 32, 32, 192, 64, 126, 3, 3, 1, 1) == CONV_WINO  # out_net
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 5, 1, 2, 0) == CONV_WINO
     from scflow_amd._lib import CONV_1X1W

@@ -12,6 +12,7 @@ cd /tmp
 SCFLOW_CONV_WINO4=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/kt -o run -- python3 $R/tools/conv_bench.py --only "corr_net.1,out_net,heads" --no-extras --reps 20 > /dev/null 2> $R/$O/kt.err || exit 3
 DB=$(find $R/$O/kt -name "*.db" | head -1)
 python3 $R/tools/stats_file.py $DB "conv_bench wino4" > $R/$O/stats.txt
+python3 $R/tools/kern_durations.py $DB wino4 > $R/$O/durations.txt
 rm -rf $R/$O/kt
 cd $R
 for rep in 1 2; do
