@@ -12,23 +12,24 @@ SURVEY.md §8(e)); ``value`` = all pairs·iterations of all ranks ÷ the slowest
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Extra JSON fields:
-* ``roofline``: the kernel with the most GPU time in the step, ``conv_wino_kernel`` — the
-  F(2×2,3×3) Winograd convolution on fp32 MFMA — over ALL six of its launches per refinement
-  iteration (XHead hidden 128→512, corr_net.1 256→192, out_net 256→126, flow_net.1 and
-  delta_flow_encoder.1 128→64, mask_encoder.1 64→32), every one bracketed live with HIP events
-  inside the timed region (each on one launch every other step).  ``achieved`` = Σ executed
-  FLOPs of one launch of each shape ÷ Σ their mean durations; ``achieved``/``frac`` count the
-  FLOPs the matrix cores EXECUTE (Winograd: 16 transform points per 2×2 tile, 2.25× fewer
-  multiplies than a direct conv), so ``frac`` ≤ 1 is a true roofline fraction;
+* ``roofline``: the kernel with the most GPU time in the step, ``conv_wino5_kernel`` — the
+  SepConvGRU's F(4,5) Winograd convolution on fp32 MFMA — over ALL four of its launches per
+  refinement iteration (z|r and q of the 1×5 and the 5×1 stage), bracketed live with HIP events
+  inside the timed region (each timer on one launch every other step).  ``achieved`` = Σ
+  executed FLOPs of one launch of each kind ÷ Σ their mean durations; ``achieved``/``frac``
+  count the FLOPs the matrix cores EXECUTE (Winograd: 8 transform points per 4-pixel tile, 5/2×
+  fewer multiplies than a direct conv), so ``frac`` ≤ 1 is a true roofline fraction;
   ``direct_conv_flops_per_launch`` / ``direct_equiv_tflops`` give the direct-conv count for
   comparison.  ``traffic`` = memory-side bytes per launch from the rocprofv3 FETCH_SIZE /
   WRITE_SIZE passes in ``profiles/traffic_*.json``.
-* ``rooflines_secondary``: the same kernel split into its two large launches (<32,2>, <32,3>)
-  and its four 32-channel-workgroup launches (<32,1>); the SepConvGRU z|r conv (F(4,5)
-  Winograd, same FLOP basis), the pyramid lookup (HBM/gather), the pose step and the
-  correlation pyramid — the last four from the same events in a short untimed pass after the
-  timed region.  HBM entries give ``frac`` against the 8 TB/s spec and ``frac_of_measured``
-  against the STREAM ceiling measured on the box (tools/micro/stream.hip).
+* ``rooflines_secondary``: the GRU z|r and q launches separately; the F(4×4,3×3) Winograd
+  convs (XHead hidden 128→512, corr_net.1 256→192: transform launch + point-GEMM launch); the
+  F(2×2,3×3) ``conv_wino_kernel<32,1>`` launches (out_net 256→126, flow_net.1 and
+  delta_flow_encoder.1 128→64, mask_encoder.1 64→32); the fused lookup + corr_net.0 (or the
+  pyramid lookup, HBM/gather), the pose step and the correlation pyramid — all but the GRU from
+  the same events in a short untimed pass after the timed region.  HBM entries give ``frac``
+  against the 8 TB/s spec and ``frac_of_measured`` against the STREAM ceiling measured on the
+  box (tools/micro/stream.hip).
 * ``cpu_baseline``: the CPU oracle (oracle/scflow_oracle.py, a parity-pinned PyTorch-CPU
   restatement of the reference decoder) on the same B=16 × 8-iteration workload, rank 0 at N=1.
 
@@ -130,8 +131,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 # 64-B pieces in scattered order) 2803, 128-B pieces 3537.  HBM entries report frac against both.
 HBM_MEASURED_GBS = 6412.0
 GATHER64_MEASURED_GBS = 2803.0  # stream.hip gather_b32: the lookup's access pattern
-# every conv_wino_kernel launch of one refinement iteration (decoder.kernel_hooks names)
+# the 3×3 Winograd launches of one refinement iteration (decoder.kernel_hooks names): the first
+# two run F(4×4,3×3) (wino4_vt_kernel + conv_wino4_kernel) by default, the rest conv_wino_kernel<32,1>
 WINO_LAUNCHES = ("heads", "corr_net1", "out_net", "flow_net1", "dflow1", "mask_enc1")
+# the headline kernel, conv_wino5_kernel: every SepConvGRU launch of an iteration (z|r and q of
+# the 1×5 and the 5×1 stage) — the largest share of the iteration's kernel time
+GRU_LAUNCHES = ("gru_zr", "gru_q")
 
 
 def load_traffic(path):
@@ -465,14 +470,14 @@ def main():
     # Eager runs bracket one launch per step per timer (stride = per-step launches + 1 walks the
     # sampled position through the iterations), so an event pair costs ≈ 2 queue packets per
     # step, not 2 per launch.
-    per_step = {"heads": args.iters, "corr_net1": args.iters, "gru_zr": 2 * args.iters,
+    per_step = {"gru_zr": 2 * args.iters, "gru_q": 2 * args.iters,
                 "corr_lookup": args.iters, "pose_flow": args.iters,
                 "pose_step_crit": args.iters, "corr_lookup_conv": args.iters, "corr_pyramid": 1}
-    per_step.update({n: args.iters for n in WINO_LAUNCHES[2:]})
-    # the headline kernel's launches (every conv_wino_kernel launch of an iteration): bracketed in
-    # the timed region, each timer on one launch every other step (an event pair costs a few µs
-    # of queue time), the bracketed position walking through the iterations
-    live = WINO_LAUNCHES
+    per_step.update({n: args.iters for n in WINO_LAUNCHES})
+    # the headline kernel's launches (every conv_wino5_kernel launch of an iteration): bracketed
+    # in the timed region, each timer on one launch every other step (an event pair costs a few
+    # µs of queue time), the bracketed position walking through the iterations
+    live = GRU_LAUNCHES
     timers = {name: (KernelTimer() if args.graph else
                      EventTimer(stride=(2 * n + 1) if name in live else (n + 1 if n > 1 else 1)))
               for name, n in per_step.items()}
@@ -576,34 +581,43 @@ def main():
             "out_net": runner(dec.encoder.out_net[-1]), "flow_net1": runner(dec.encoder.flow_net[-1]),
             "dflow1": runner(dec.delta_flow_encoder[-1]), "mask_enc1": runner(dec.mask_encoder[-1])}
     parts = [(n, wino[n][0], wino[n][1], 0) for n in WINO_LAUNCHES if timers[n].count()]
+    cxt = xc if dec.hoist_context else 0
+    zr, q = dec.gru.zr_runner(cxt), dec.gru.q_runner(cxt)
+    gru = [(n, r, hc, r.cin - hc) for n, r in (("gru_zr", zr), ("gru_q", q)) if timers[n].count()]
     headline = conv_roofline(
-        "conv_wino_kernel (F(2x2,3x3) Winograd on fp32 MFMA), ALL its launches of an iteration: "
-        "XHead hidden 128->512 <32,2>, corr_net.1 256->192 <32,3>, out_net 256->126, flow_net.1 "
-        "128->64, delta_flow_encoder.1 128->64, mask_encoder.1 64->32 (<32,1>)",
-        parts, timers, m_px, traffic.get("conv_wino_kernel_all"), alg.get("conv_wino_kernel_all"))
-    if not all(r.winograd for _, r, _, _ in parts):
-        headline["kernel"] += " [some launches on the direct conv_mfma_kernel: Winograd off]"
+        "conv_wino5_kernel (SepConvGRU, Winograd F(4,5) on fp32 MFMA), ALL its launches of an "
+        "iteration: z|r <·,32,2,GRU_ZR> and q <·,32,1,GRU_Q> of the 1x5 and the 5x1 stage "
+        "(context hoisted: K = h|r·h 128 + motion 128)",
+        gru, timers, m_px, traffic.get("conv_wino5_kernel_all"), alg.get("conv_wino5_kernel_all"))
+    if not all(r.winograd for _, r, _, _ in gru):
+        headline["kernel"] += " [direct conv_mfma_kernel: Winograd off]"
 
     secondary = []
-    big = [p for p in parts if p[0] in ("heads", "corr_net1")]
-    small = [p for p in parts if p[0] not in ("heads", "corr_net1")]
+    for n, r, c0, c1 in gru:  # the two GRU launch kinds separately
+        secondary.append(conv_roofline(
+            {"gru_zr": "conv_wino5_kernel<·,32,2,GRU_ZR>: SepConvGRU z|r 256->256, both stages",
+             "gru_q": "conv_wino5_kernel<·,32,1,GRU_Q>: SepConvGRU q 256->128, both stages"}[n],
+            [(n, r, c0, c1)], timers, m_px, traffic.get(n), alg.get(n)))
+    big = [p for p in parts if p[1].wino4]
+    small = [p for p in parts if not p[1].wino4]
     if big:
         secondary.append(conv_roofline(
-            "conv_wino_kernel<32,2> + <32,3>: XHead hidden 128->512 + corr_net.1 256->192",
-            big, timers, m_px, traffic.get("conv_wino_kernel"), alg.get("conv_wino_kernel")))
+            "F(4x4,3x3) Winograd (wino4_vt_kernel input transform + conv_wino4_kernel point GEMMs "
+            "and output transform; launch time = both): " +
+            " + ".join({"heads": "XHead hidden 128->512", "corr_net1": "corr_net.1 256->192"}.get(
+                p[0], p[0]) for p in big),
+            big, timers, m_px, traffic.get("conv_wino4"), alg.get("conv_wino4")))
     if small:
         secondary.append(conv_roofline(
-            "conv_wino_kernel<32,1>: out_net 256->126, flow_net.1 / delta_flow_encoder.1 128->64, "
-            "mask_encoder.1 64->32",
-            small, timers, m_px, traffic.get("conv_wino_kernel<32,1>"),
-            alg.get("conv_wino_kernel<32,1>")))
-    if timers["gru_zr"].count():
-        cxt = xc if dec.hoist_context else 0
-        zr = dec.gru.zr_runner(cxt)
-        secondary.append(conv_roofline(
-            "conv_wino5_kernel<·,32,2,GRU_ZR> (SepConvGRU z|r, Winograd F(4,5) on fp32 MFMA)"
-            if zr.winograd else "conv_mfma_kernel<GRU_ZR> (SepConvGRU z|r, direct)",
-            [("gru_zr", zr, hc, zr.cin - hc)], timers, m_px, traffic.get("gru_zr"), alg.get("gru_zr")))
+            "conv_wino_kernel (F(2x2,3x3)): " + ", ".join(
+                {"heads": "XHead hidden 128->512 <32,2>", "corr_net1": "corr_net.1 256->192 <32,3>",
+                 "out_net": "out_net 256->126 <32,1>", "flow_net1": "flow_net.1 128->64 <32,1>",
+                 "dflow1": "delta_flow_encoder.1 128->64 <32,1>",
+                 "mask_enc1": "mask_encoder.1 64->32 <32,1>"}[p[0]] for p in small),
+            small, timers, m_px, *((traffic.get("conv_wino_kernel<32,1>"),
+                                     alg.get("conv_wino_kernel<32,1>"))
+                                    if not any(p[0] in ("heads", "corr_net1") for p in small)
+                                    else (None, None))))
     secondary += secondary_rooflines(timers, hb, args.size, traffic,
                                      getattr(dec, "fuse_tail", True), dec.tiled_pyramid,
                                      fullres_alone)

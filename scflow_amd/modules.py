@@ -205,6 +205,11 @@ class ConvRunner:
         """True once a launch picked the Winograd kernel (F(2×2,3×3) or F(4,5))."""
         return getattr(self, "_bk", None) in (_lib.CONV_WINO, _lib.CONV_WINO4)
 
+    @property
+    def wino4(self) -> bool:
+        """True once a launch picked F(4×4,3×3) (transform launch + point-GEMM launch)."""
+        return getattr(self, "_bk", None) == _lib.CONV_WINO4
+
     def mfma_flops(self, m: int, c0: int, c1: int = 0) -> float:
         """FLOPs the matrix cores execute for one launch over m output pixels with the inputs
         split c0 + c1: the Winograd kernels multiply per transform point (16 per 2×2 tile for
@@ -509,6 +514,10 @@ class ConvGRU(nn.Module):
     def zr_runner(self, cxt_channels: int = 0) -> "ConvRunner":
         """The first SeqConv stage's fused z|r conv (context hoisted if cxt_channels > 0)."""
         return self._ctx_runners(cxt_channels)[0][0] if cxt_channels else self.runners()[0][0]
+
+    def q_runner(self, cxt_channels: int = 0) -> "ConvRunner":
+        """The first SeqConv stage's q conv (context hoisted if cxt_channels > 0)."""
+        return self._ctx_runners(cxt_channels)[0][1] if cxt_channels else self.runners()[0][1]
 
     def zr_flops(self, m: int, cxt_channels: int = 0) -> float:
         """Algorithmic FLOPs of one z|r launch over m pixels (with the context hoisted if

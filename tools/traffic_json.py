@@ -24,7 +24,11 @@ def groups(B, S):
     f = 4
     heads = f * (M * 128 + M * 512 + 512 * 128 * 9)            # XHead hidden convs 128→512
     corr1 = f * (M * 256 + M * 192 + 192 * 256 * 9)            # corr_net.1 256→192
-    zr = f * M * (256 + 256 + 128 + 256) + f * 256 * 256 * 5   # h|motion, bias map, h, z|rh, W
+    # SepConvGRU, context hoisted (K = h or r·h 128 + motion 128): z|r reads h|motion and its
+    # bias-map slice (256 ch), writes z and r·h; q reads r·h|motion, its bias-map slice (128),
+    # z and h, writes h; weights 5 taps each
+    zr = f * M * (256 + 256 + 256) + f * 256 * 256 * 5
+    q = f * M * (256 + 128 + 128 + 128 + 128) + f * 128 * 256 * 5
     lookup = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 324)
     pose_step = B * 36 * S * S
     lookup_conv = B * (4 * P * sum(min(100, P // 4 ** l) for l in range(4)) + 4 * P * 256) + 4 * 328 * 256
@@ -36,18 +40,24 @@ def groups(B, S):
         return f * (M * cin + M * cout + cout * cin * taps)
     small = [conv(256, 126), conv(128, 64), conv(128, 64), conv(64, 32)]  # the <32,1> launches
     return {
-        "conv_wino_kernel_all": (["conv_wino_kernel<"], (heads + corr1 + sum(small)) / 6,
-                                 "F(2x2,3x3) Winograd, every launch of an iteration (6 shapes, "
-                                 "launches averaged)"),
+        "conv_wino5_kernel_all": ([", 1>(Wino5Params", ", 2>(Wino5Params"], (zr + q) / 2,
+                                  "F(4,5) Winograd, every SepConvGRU launch of an iteration (z|r "
+                                  "and q of both stages, launches averaged)"),
+        # template <DIR, W, NBW, EPI>: EPI 1 = GRU_ZR, 2 = GRU_Q (0: the per-forward context map)
+        "gru_zr": ([", 1>(Wino5Params"], zr,
+                   "SepConvGRU z|r 1×5 + 5×1 (context hoisted)"),
+        "gru_q": ([", 2>(Wino5Params"], q,
+                  "SepConvGRU q 1×5 + 5×1 (context hoisted)"),
+        "conv_wino4": (["wino4_vt_kernel", "conv_wino4_kernel<"], (heads + corr1) / 2,
+                       "F(4×4,3×3) Winograd: XHead hidden 128→512 + corr_net.1 256→192; one launch "
+                       "= the transform launch + the point-GEMM launch (their averages summed; "
+                       "the transformed input V round-trips through memory between them)", "sum"),
         "conv_wino_kernel<32,1>": (["conv_wino_kernel<32, 1>"], sum(small) / 4,
                                    "F(2x2,3x3) Winograd <32,1>: out_net 256→126, flow_net.1 / "
                                    "delta_flow_encoder.1 128→64, mask_encoder.1 64→32"),
         "conv_wino_kernel": (["conv_wino_kernel<32, 2>", "conv_wino_kernel<32, 3>"], (heads + corr1) / 2,
-                             "F(2x2,3x3) Winograd: XHead hidden 128→512 <32,2> + corr_net.1 256→192 "
-                             "<32,3> (launches averaged)"),
-        "gru_zr": (["conv_wino5_kernel<0, 32, 2, 1>", "conv_wino5_kernel<1, 32, 2, 1>",
-                    "conv_wino5_kernel<0, 32, 1, 1>", "conv_wino5_kernel<1, 32, 1, 1>"], zr,
-                   "SepConvGRU z|r 1×5 + 5×1 (context hoisted)"),
+                             "F(2x2,3x3) Winograd <32,2> / <32,3> (only with SCFLOW_CONV_WINO4=0): "
+                             "XHead hidden 128→512 + corr_net.1 256→192 (launches averaged)"),
         "corr_lookup": (["corr_lookup_lds_kernel"], lookup, "pyramid lookup r=4, 4 levels"),
         "corr_lookup_conv": (["corr_lookup_conv1x1_kernel"], lookup_conv, "pyramid lookup fused "
                              "into corr_net.0: window reads + 256-channel output + weights"),
@@ -104,8 +114,17 @@ def main():
                      "WRITE_SIZE as is; memory-side (L2->fabric) bytes, Infinity-Cache hits included",
            "kernels": {}}
     for name, (subs, alg, what, *which) in groups(a.batch, a.size).items():
-        f = select(fetch, subs, which[0] if which else None)
-        w = select(write, subs, which[0] if which else None)
+        mode = which[0] if which else None
+        if mode == "sum":  # one logical launch = one launch of each kernel in ``subs``
+            fs = [select(fetch, [s], None) for s in subs]
+            ws = [select(write, [s], None) for s in subs]
+            if not all(fs) or not all(ws):
+                continue
+            f = [sum(sum(v) / len(v) for v in fs)]
+            w = [sum(sum(v) / len(v) for v in ws)]
+        else:
+            f = select(fetch, subs, mode)
+            w = select(write, subs, mode)
         if not f or not w:
             continue
         hbm = (2 * sum(f) / len(f) + sum(w) / len(w)) * 1024
