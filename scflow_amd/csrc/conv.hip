@@ -552,7 +552,11 @@ constexpr int thin_na(int kh, int kw) {  // float4 per thread of one chunk's hal
 template <int COUT, int KH, int KW>
 __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int oh, int ow) {
   constexpr int NA = thin_na(KH, KW);
-  extern __shared__ float halo[];  // [(tr+KH-1)*(ow+KW-1)][THIN_LD], reused for the reduction
+  // [(tr+KH-1)*(ow+KW-1)][THIN_LD], reused for the reduction; float4-typed so the halo accesses
+  // are ds_write_b128 / ds_read_b128 (a float array's unknown alignment split the 16-B stores
+  // into ds_write2_b32 pairs, 4-way bank conflicts)
+  extern __shared__ floatx4 thin_smem4[];
+  float* halo = (float*)thin_smem4;
   const int tr = 64 / ow;
   const int hcols = ow + KW - 1;
   const int nh = (tr + KH - 1) * hcols * (THIN_CC / 4);
@@ -601,7 +605,7 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int idx = threadIdx.x + 256 * j;
-      if (idx < nh) *(floatx4*)(halo + (idx / (THIN_CC / 4)) * THIN_LD + 4 * (idx % (THIN_CC / 4))) = ra[j];
+      if (idx < nh) thin_smem4[(idx / (THIN_CC / 4)) * (THIN_LD / 4) + idx % (THIN_CC / 4)] = ra[j];
     }
     __syncthreads();
     if (cc + THIN_CC < cin) gload(cc + THIN_CC);
@@ -611,9 +615,9 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
       for (int ty = 0; ty < KH; ++ty)
 #pragma unroll
         for (int tx = 0; tx < KW; ++tx) {
-          const float* hp = halo + ((py + ty) * hcols + px + tx) * THIN_LD + c0;
-          const floatx4 v0 = *(const floatx4*)(hp);
-          const floatx4 v1 = *(const floatx4*)(hp + 4);
+          const floatx4* hp = thin_smem4 + ((py + ty) * hcols + px + tx) * (THIN_LD / 4) + c0 / 4;
+          const floatx4 v0 = hp[0];
+          const floatx4 v1 = hp[1];
           float w[8 * COUT];  // [ci][o] for this tap's 8 channels
           const float* wp = wl + ((size_t)(ty * KW + tx) * cin + cc + c0) * COUT;
 #pragma unroll
@@ -659,7 +663,10 @@ __host__ __device__ constexpr int thinf_ld(int cin) { return cin + 4; }  // pixe
 template <int COUT, int KH, int KW>
 __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow_conv_args a,
                                                                           int oh, int ow) {
-  extern __shared__ float halo[];  // [(tr+KH-1)·(ow+KW-1)][cin + 4], reused for the partials
+  // [(tr+KH-1)·(ow+KW-1)][cin + 4], reused for the partials; float4-typed: ds_*_b128 halo
+  // accesses (see conv_thin_kernel)
+  extern __shared__ floatx4 thinf_smem4[];
+  float* halo = (float*)thinf_smem4;
   const int tr = 64 / ow;
   const int hcols = ow + KW - 1;
   const int cin = a.c0;
@@ -695,7 +702,7 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
 #pragma unroll
   for (int j = 0; j < NL; ++j) {
     const int idx = tid + THINF_WAVES * 64 * j;
-    if (idx < nh) *(floatx4*)(halo + (idx / q4) * ld + 4 * (idx % q4)) = v[j];
+    if (idx < nh) thinf_smem4[(idx / q4) * (ld / 4) + idx % q4] = v[j];
   }
   __syncthreads();
   const int py = lane / ow, px = lane % ow;
@@ -707,13 +714,13 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
   // packed weights [o][tap][ci]: wave-uniform addresses → scalar loads
   for (int ty = 0; ty < KH; ++ty)
     for (int tx = 0; tx < KW; ++tx) {
-      const float* hp = halo + ((py + ty) * hcols + px + tx) * ld + c0;
+      const floatx4* hp = thinf_smem4 + ((py + ty) * hcols + px + tx) * (ld / 4) + c0 / 4;
       const float* wp = a.weight + (size_t)(ty * KW + tx) * cin + c0;
 #ifdef THINF_UNROLL  // channel-chunk loop unroll of the contraction (tuning build flag)
 #pragma unroll THINF_UNROLL
 #endif
       for (int c = 0; c < cw; c += 4) {
-        const floatx4 x = *(const floatx4*)(hp + c);
+        const floatx4 x = hp[c / 4];
 #pragma unroll
         for (int o = 0; o < COUT; ++o) {
           const float* w = wp + (size_t)o * KH * KW * cin + c;
@@ -930,6 +937,9 @@ static unsigned long long* g_wino_stamps = nullptr;
 #ifndef WINO4_MIN_COUT
 #define WINO4_MIN_COUT 160
 #endif
+#ifndef WINO5_PAIR_DEFAULT
+#define WINO5_PAIR_DEFAULT 0
+#endif
 #ifndef WINO4_DEFAULT
 #define WINO4_DEFAULT 1
 #endif
@@ -961,21 +971,40 @@ int launch_wino_w(WinoParams p, hipStream_t st) {
   return scflow_launch_status();
 }
 
-template <int DIR, int W, int NBW, int EPI>
-int launch_wino5_k(Wino5Params p, hipStream_t st) {
-  using G = Wino5Geom<DIR, W>;
-  const size_t lds = wino5_lds_bytes<DIR, W, NBW>();
+// SCFLOW_WINO5_PAIR=1: the paired F(4,5) workgroups (conv_wino5_kernel PR = 2) when the grid
+// splits evenly
+bool wino5_pair() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SCFLOW_WINO5_PAIR");
+    v = e ? atoi(e) : WINO5_PAIR_DEFAULT;
+  }
+  return v != 0;
+}
+
+template <int DIR, int W, int NBW, int EPI, int PR>
+int launch_wino5_pr(Wino5Params p, dim3 grid, hipStream_t st) {
+  const size_t lds = wino5_lds_bytes<DIR, W, NBW>() * PR;
   static bool attr = false;
   if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI>,
+    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI, PR>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
-  p.swz_c = wino_swz(grid.x, grid.y);
+  p.swz_c = PR > 1 ? 0 : wino_swz(grid.x, grid.y);
   p.stamps = g_wino_stamps;
-  conv_wino5_kernel<DIR, W, NBW, EPI><<<grid, 256, lds, st>>>(p);
+  grid.x /= PR;
+  conv_wino5_kernel<DIR, W, NBW, EPI, PR><<<grid, 256 * PR, lds, st>>>(p);
   return scflow_launch_status();
+}
+
+template <int DIR, int W, int NBW, int EPI>
+int launch_wino5_k(Wino5Params p, hipStream_t st) {
+  using G = Wino5Geom<DIR, W>;
+  dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
+  if (wino5_pair() && grid.x % 2 == 0 && wino5_lds_bytes<DIR, W, NBW>() * 2 <= 160 * 1024)
+    return launch_wino5_pr<DIR, W, NBW, EPI, 2>(p, grid, st);
+  return launch_wino5_pr<DIR, W, NBW, EPI, 1>(p, grid, st);
 }
 
 template <int EPI>

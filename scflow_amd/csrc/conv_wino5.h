@@ -77,23 +77,36 @@ constexpr size_t wino5_lds_bytes() {
 // (A K split for the GRU q conv's one-workgroup-per-CU grid — two wave sets over the two 8-channel
 // halves of every sub-step — was built in round 4 and measured in round 5: 32.7 → 32.5 µs alone,
 // the decoder 2 % slower; removed.)
-template <int DIR, int W, int NBW, int EPI>
-__global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
+// PR = 2 ("paired"): one launched workgroup of 512 threads runs two tile blocks as two 256-thread
+// halves with their own LDS regions, meeting at every block barrier.  With two independent
+// workgroups per CU the SQ's oldest-first issue lets the first-dispatched one run ahead: the
+// second's main loop ends ≈ 25 % later and runs its tail with one wave per SIMD (stamps, round 5);
+// the shared barriers keep the two in step.
+template <int DIR, int W, int NBW, int EPI, int PR = 1>
+__global__ __launch_bounds__(256 * PR, 2 / PR) void conv_wino5_kernel(Wino5Params P) {
   using G = Wino5Geom<DIR, W>;
   constexpr int NTH = 256;                                   // threads
   constexpr int NA = (G::NH4 + 2 * NTH - 1) / (2 * NTH);    // float4 per thread per half stage
   constexpr int BNW = 32 * NBW;
-  extern __shared__ floatx4 smem4[];
+  extern __shared__ floatx4 smem4_all[];
+  const int grp = PR > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8) : 0;  // half
+  floatx4* smem4 = smem4_all + grp * (wino5_lds_bytes<DIR, W, NBW>() / 16);
   float* smem = (float*)smem4;
   const scflow_conv_args& a = P.a;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x & 255, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int wave = wv & 3;              // point pair
   const int li = lane & 31, hh = lane >> 5;
   constexpr int XB = W / G::OCOLS;  // column blocks per image (1, or 2 for 5×1 at W = 64)
   int bx, by;
   wino_block(P.swz_c, bx, by);
-  wino_stamp(P.stamps, 0);
+  bx = bx * PR + grp;
+  auto wstamp = [&](int k) {  // wino_stamp per half: stamp slot = the half's own tile block
+    if (P.stamps && tid == 0)
+      P.stamps[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * PR + grp) * 4 + k] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+  wstamp(0);
   const int blocks_per_img = (a.h / G::OROWS) * XB;
   const int img = bx / blocks_per_img;
   const int rem = bx % blocks_per_img;
@@ -233,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     hstore(0, 1);
     __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
     __syncthreads();
-    wino_stamp(P.stamps, 1);
+    wstamp(1);
     floatx4 vA[2][2], vB[2][2];
     vload(0, 0, 0, d, w3);
     vmath(d, vA[0], w3);
@@ -280,10 +293,50 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   // epilogue: M[ξ][co][tile] in LDS (tiles contiguous, WEP-float rows: a lane's accumulator
   // rows r..r+3 are 4 consecutive tiles → one 16-B store; conflict-free for the b128 stores and
   // loads, see conv_wino.h), then every thread takes a run of NT tiles of its channel, 4 tiles
-  // per 16-B load of each point, and y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ]
+  // per 16-B load of each point, and y[o] = Σ_ξ Aᵀ[o][ξ]·M[ξ].
+  // Every global read of the epilogue (bias map, h, z) is issued first — before the points'
+  // LDS exchange, so its latency runs under the exchange and the output transform instead of
+  // after them (in a one-round grid every workgroup reaches its epilogue at once) — and before
+  // any store (the stores may alias them as far as the compiler knows).
   constexpr int WEP = W5TM + 4;
+  const int co = tid % BNW;
+  const int col = by * BNW + co;
+  const bool col_ok = col < a.cout;
+  constexpr int GROUPS = NTH / BNW;
+  constexpr int NT = W5TM / GROUPS;  // tiles per thread
+  static_assert(NT % 4 == 0, "epilogue: whole 16-B tile loads per thread");
+  const int mbase = (tid / BNW) * NT;
+  int pix[NT][4];  // output pixel (n·h·w < 2^31)
+#pragma unroll
+  for (int k = 0; k < NT; ++k)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int m = mbase + k;
+      const int oy = DIR == 0 ? oy0 + m / G::TPR : oy0 + o;
+      const int ox = DIR == 0 ? 4 * (m % G::TPR) + o : ox0 + m;
+      pix[k][o] = (img * a.h + oy) * W + ox;
+    }
+  const int hcn = a.cout >> 1;
+  const bool zr_h = EPI == SCFLOW_EPI_GRU_ZR && col >= hcn;  // the r·h half of z|r
+  float bm[NT][4], hv[NT][4], zv[NT][4];
+#pragma unroll
+  for (int k = 0; k < NT; ++k)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      bm[k][o] = col_ok && a.bias_map ? a.bias_map[(size_t)pix[k][o] * a.sbm + col] : 0.f;
+      hv[k][o] = 0.f;
+      zv[k][o] = 0.f;
+      if constexpr (EPI == SCFLOW_EPI_GRU_ZR) {
+        if (col_ok && zr_h) hv[k][o] = a.hid[(size_t)pix[k][o] * a.sh + (col - hcn)];
+      } else if constexpr (EPI == SCFLOW_EPI_GRU_Q) {
+        if (col_ok) {
+          zv[k][o] = a.gate[(size_t)pix[k][o] * a.sg + col];
+          hv[k][o] = a.hid[(size_t)pix[k][o] * a.sh + col];
+        }
+      }
+    }
   __syncthreads();
-  wino_stamp(P.stamps, 2);
+  wstamp(2);
   float* S = smem;
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -297,19 +350,9 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
         *(floatx4*)&S[(w5_point(wave, x) * BNW + nb * 32 + li) * WEP + 8 * q4 + 4 * hh] = v;
       }
   __syncthreads();
-  const int co = tid % BNW;
-  const int col = by * BNW + co;
-  if (col >= a.cout) return;
+  if (!col_ok) return;
   const float bias = a.bias ? a.bias[col] : 0.f;
-  constexpr int GROUPS = NTH / BNW;
-  constexpr int NT = W5TM / GROUPS;  // tiles per thread
-  static_assert(NT % 4 == 0, "epilogue: whole 16-B tile loads per thread");
-  const int mbase = (tid / BNW) * NT;
-  // Every global read of the epilogue (bias map, h, z) is issued before any store: the stores
-  // may alias them as far as the compiler knows, so interleaving would serialise NT·4 round
-  // trips through memory.
   float y[NT][4];
-  int pix[NT][4];  // output pixel (n·h·w < 2^31)
 #pragma unroll
   for (int k4 = 0; k4 < NT / 4; ++k4) {
     floatx4 mv[8];
@@ -317,25 +360,16 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     for (int xi = 0; xi < 8; ++xi) mv[xi] = *(const floatx4*)&S[(xi * BNW + co) * WEP + mbase + 4 * k4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int k = 4 * k4 + e, m = mbase + k;
+      const int k = 4 * k4 + e;
 #pragma unroll
       for (int o = 0; o < 4; ++o) {
         float v = 0.f;
 #pragma unroll
         for (int xi = 0; xi < 8; ++xi)
           if (kW5AT[o][xi] != 0.f) v += kW5AT[o][xi] * mv[xi][e];
-        y[k][o] = v + bias;
-        const int oy = DIR == 0 ? oy0 + m / G::TPR : oy0 + o;
-        const int ox = DIR == 0 ? 4 * (m % G::TPR) + o : ox0 + m;
-        pix[k][o] = (img * a.h + oy) * W + ox;
+        y[k][o] = v + bias + bm[k][o];
       }
     }
-  }
-  if (a.bias_map) {
-#pragma unroll
-    for (int k = 0; k < NT; ++k)
-#pragma unroll
-      for (int o = 0; o < 4; ++o) y[k][o] += a.bias_map[(size_t)pix[k][o] * a.sbm + col];
   }
   if constexpr (EPI == SCFLOW_EPI_PLAIN) {
 #pragma unroll
@@ -343,33 +377,19 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
 #pragma unroll
       for (int o = 0; o < 4; ++o) a.out[(size_t)pix[k][o] * a.so + col] = act_apply(y[k][o], a.act);
   } else if constexpr (EPI == SCFLOW_EPI_GRU_ZR) {
-    const int hcn = a.cout >> 1;
-    if (col < hcn) {
+    if (!zr_h) {
 #pragma unroll
       for (int k = 0; k < NT; ++k)
 #pragma unroll
         for (int o = 0; o < 4; ++o) a.gate[(size_t)pix[k][o] * a.sg + col] = sigmoidf_(y[k][o]);
     } else {
       const int c = col - hcn;
-      float hv[NT][4];
-#pragma unroll
-      for (int k = 0; k < NT; ++k)
-#pragma unroll
-        for (int o = 0; o < 4; ++o) hv[k][o] = a.hid[(size_t)pix[k][o] * a.sh + c];
 #pragma unroll
       for (int k = 0; k < NT; ++k)
 #pragma unroll
         for (int o = 0; o < 4; ++o) a.rh[(size_t)pix[k][o] * a.srh + c] = sigmoidf_(y[k][o]) * hv[k][o];
     }
   } else {  // GRU_Q
-    float zv[NT][4], hv[NT][4];
-#pragma unroll
-    for (int k = 0; k < NT; ++k)
-#pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        zv[k][o] = a.gate[(size_t)pix[k][o] * a.sg + col];
-        hv[k][o] = a.hid[(size_t)pix[k][o] * a.sh + col];
-      }
 #pragma unroll
     for (int k = 0; k < NT; ++k)
 #pragma unroll
@@ -378,7 +398,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   }
   if (P.stamps) {
     __builtin_amdgcn_s_waitcnt(0);
-    wino_stamp(P.stamps, 3);
+    wstamp(3);
   }
 }
 

@@ -126,6 +126,23 @@ __host__ __device__ inline int lk_slot_floats(int h, int w, int L, int win) {
   return (t & 7) ? t : t + 4;
 }
 
+// TB: two levels' regions at a time (levels 0, 1 are stored, then sampled, then levels 2, 3), so
+// a pixel slot holds two regions of the largest level size — half the LDS of all four — and the
+// region loads still in registers while a pair is sampled are the other pair's only: 6
+// workgroups per CU instead of 4 (round 5).  Region p of the slot starts at p·lk_tb_region().
+__host__ __device__ inline int lk_tb_region(int h, int w, int L, int win) {
+  int t = 0;
+  for (int l = 0; l < L; ++l) {
+    const int r = lk_rows(h >> l, w >> l, win) * win;
+    t = r > t ? r : t;
+  }
+  return (t + 3) & ~3;
+}
+__host__ __device__ inline int lk_tb_slot_floats(int h, int w, int L, int win) {
+  const int t = 2 * lk_tb_region(h, w, L, win);
+  return (t & 7) ? t : t + 4;
+}
+
 constexpr int LK_OOB = 0x7ffffff0;  // buffer voffset of a zero tap (beyond any num_records)
 
 // TR (tile regions, tiled maps only): every level's region is the 4×4 block of 4×4 tiles (16×16
@@ -166,7 +183,7 @@ __device__ __forceinline__ float lk_bload(__amdgpu_buffer_rsrc_t r, int voff) {
 //
 // TILED: the pyramid's maps are in 4×4 tiles of 16 floats (scflow_corr_pyramid_tiled)
 template <int R, bool TILED, bool TR = false, bool TB = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 4 : 3))) void corr_lookup_lds_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3))) void corr_lookup_lds_kernel(
     const float* __restrict__ pyr, const float* __restrict__ flow, int flow_layout,
     float* __restrict__ out, int out_layout, int out_stride, int N, int H, int W, int L,
     int vec_out, int ac, unsigned long long* stamps) {
@@ -194,7 +211,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 4 : 3)
   const int gl = lane % LK_GL;                    // lane within the pixel's group
   const int P = H * W;
   const long long NP = (long long)N * P;
-  float* sw = win + slot * (TR ? lk_tr_slot_floats(L) : lk_slot_floats(H, W, L, WIN));
+  float* sw = win + slot * (TR ? lk_tr_slot_floats(L)
+                                : (TB ? lk_tb_slot_floats(H, W, L, WIN) : lk_slot_floats(H, W, L, WIN)));
   const long long gp0 = (long long)blockIdx.x * LK_SLOTS + wave * LK_PPW;  // wave's first pixel
   const long long gp = gp0 + ks;                                          // n·P + p
   const bool active = gp < NP;
@@ -264,6 +282,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 4 : 3)
   // 2. regions (zero padded) through buffer loads (out-of-map taps read as zero, no branches):
   //    every load of the pixel's L regions is issued before the LDS writes
   int rn[LK_MAXL], ox[LK_MAXL], oy[LK_MAXL];
+  constexpr int NS = 3;        // TB: (region row, tile) slots per lane and level
+  floatx4 tbv[LK_MAXL][NS];    // TB: every level's region loads, in flight together
 #pragma unroll
   for (int l = 0; l < LK_MAXL; ++l) {
     ox[l] = l < L ? org[slot][l][0] : 0;
@@ -311,9 +331,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 4 : 3)
     }
   } else if constexpr (TB) {
     // 48 (region row, tile) slots per level, 3 per lane: slot k = row k / 4, tile k % 4 of the
-    // 4 tiles from the one holding region column 0 (covers the ≤ 12 region columns)
-    constexpr int NS = 3;
-    floatx4 tv4[LK_MAXL][NS];
+    // 4 tiles from the one holding region column 0 (covers the ≤ 12 region columns); stored to
+    // LDS level by level in the sampling phase
+    floatx4 (&tv4)[LK_MAXL][NS] = tbv;
     size_t loff = 0;
     int Hl = H, Wl = W;
     const long long left = NP - gp0;
@@ -347,23 +367,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 4 : 3)
       Wl >>= 1;
     }
     stamp(2);
-    int off = 0;
-#pragma unroll
-    for (int l = 0; l < LK_MAXL; ++l) {
-      const int rows = rn[l] / WIN;
-      const int c0 = ((ox[l] >> 2) << 2) - ox[l];  // region column of the first tile's column 0
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        const int k = gl + LK_GL * j, r = k >> 2;
-        const int cb = c0 + 4 * (k & 3);
-        if (r < rows) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (cb + q >= 0 && cb + q < WIN) sw[off + r * WIN + cb + q] = tv4[l][j][q];
-        }
-      }
-      off += rn[l];
-    }
   } else {
   constexpr int NW1 = (WIN * WIN + LK_GL - 1) / LK_GL;  // loads per lane per level
   float vals[LK_MAXL][NW1];
@@ -434,10 +437,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 4 : 3)
                                                 : out + (size_t)n * L * D * D * P + p;
     const size_t ostep = out_layout == SCFLOW_LAYOUT_NHWC ? 1 : (size_t)P;
     constexpr int NJ = (D * D + LK_GL - 1) / LK_GL;
+    const int rsz = lk_tb_region(H, W, L, WIN);
 #pragma unroll
     for (int l = 0; l < LK_MAXL; ++l) {
       if (l >= L) break;
-      const int off = offl[l], rows = rn[l] / WIN;
+      const int off = (l & 1) * rsz, rows = rn[l] / WIN;
+      if ((l & 1) == 0) {  // levels l, l + 1 into the slot's two regions (data, or zero outside
+                           // the extent / the map)
+        if (l) lk_sync<TB>();  // the wave's samples of levels l − 2, l − 1 have read the slot
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int lp = l + p;
+          if (lp < LK_MAXL && lp < L) {
+            const int rws = rn[lp] / WIN;
+            const int c0 = ((ox[lp] >> 2) << 2) - ox[lp];  // region column of the first tile's column 0
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+              const int k = gl + LK_GL * j, r = k >> 2;
+              const int cb = c0 + 4 * (k & 3);
+              if (r < rws) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  if (cb + q >= 0 && cb + q < WIN) sw[p * rsz + r * WIN + cb + q] = tbv[lp][j][q];
+              }
+            }
+          }
+        }
+        lk_sync<TB>();
+      }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int sidx = gl + LK_GL * j;
@@ -628,7 +655,7 @@ static int corr_lookup_launch(const float* pyr, const float* flow, int flow_layo
       return scflow_launch_status();
     }
     if (tiled && lk_tile_rows()) {
-      const int sf_tb = lk_slot_floats(h, w, num_levels, lk_win(radius, false, true));
+      const int sf_tb = lk_tb_slot_floats(h, w, num_levels, lk_win(radius, false, true));
       const size_t lds_tb = sizeof(float) * LK_SLOTS * sf_tb;
       const int vec_tb = vec || (out_layout == SCFLOW_LAYOUT_NHWC && out_stride % 4 == 0 &&
                                  ((uintptr_t)out & 15) == 0 && sf_tb >= num_levels * D * D);

@@ -110,7 +110,16 @@ __global__ __launch_bounds__(512, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
     return lc_unnorm(c + (float)(0 - LC_R), size, a.ac);
   };
 
-  // region loads of level l: the pixel's 64 tile rows, 16 per thread (k = sub + 4j)
+  auto last = [&](int l, int axis) __attribute__((always_inline)) {  // ... and its last
+    const int size = axis == 0 ? (W >> l) : (H >> l);
+    const float c = ((float)(axis == 0 ? x : y) + (axis == 0 ? fx : fy)) / (float)(1 << l);
+    return lc_unnorm(c + (float)LC_R, size, a.ac);
+  };
+
+  // region loads of level l: the pixel's 64 tile rows, 16 per thread (k = sub + 4j) — only the
+  // tile rows that hold a tap some sample reads (the taps' extent [floor(first sample),
+  // floor(last sample) + 1] per axis: the samples increase along an axis), the others read as
+  // zero without touching memory; the sampling phase is unchanged (those taps are never read)
   floatx4 wr[16];
   auto rload = [&](int l) __attribute__((always_inline)) {
     size_t loff = 0;
@@ -120,11 +129,17 @@ __global__ __launch_bounds__(512, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
         lc_rsrc(a.pyr + loff + (size_t)m0 * hw, (unsigned)(npx * hw * 4));
     const float c0x = first(l, 0), c0y = first(l, 1);
     const int ox = origin(l, 0, c0x, c0y), oy = origin(l, 1, c0x, c0y);
+    const float c1x = last(l, 0), c1y = last(l, 1);
+    const bool fin = isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f && fabsf(c0y) < 1e8f &&
+                     isfinite(c1x) && isfinite(c1y) && fabsf(c1x) < 1e8f && fabsf(c1y) < 1e8f;
+    const int xlo = fin ? (int)floorf(c0x) : 1, xhi = fin ? (int)floorf(c1x) + 1 : 0;
+    const int ylo = fin ? (int)floorf(c0y) : 1, yhi = fin ? (int)floorf(c1y) + 1 : 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int k = sub + 4 * j, kt = k >> 2;
       const int gx = ox + (kt & 3) * 4, gy = oy + (kt >> 2) * 4 + (k & 3);
-      const bool ok = active && gx >= 0 && gx < Wl && gy >= 0 && gy < Hl;
+      const bool ok = active && gx >= 0 && gx < Wl && gy >= 0 && gy < Hl && gy >= ylo &&
+                      gy <= yhi && gx + 3 >= xlo && gx <= xhi;
       const int e = ((gy >> 2) * (Wl >> 2) + (gx >> 2)) * 16 + (gy & 3) * 4;
       wr[j] = lc_bload4(rs, ok ? (ps * hw + e) * 4 : LC_OOB, 0);
     }

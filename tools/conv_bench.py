@@ -41,6 +41,9 @@ SHAPES = [
 ]
 
 
+XCD_REPORT = False
+
+
 def stamp_report(run):
     """One launch of ``run`` with workgroup stamps: spread of the start times, and the median /
     max of each phase (prologue, main loop, epilogue) over the workgroups, in µs."""
@@ -63,6 +66,12 @@ def stamp_report(run):
     print(f"    {len(v)} WGs  start spread {(v[:, 0] - t0).max().item():6.2f} us  span "
           f"{(v[:, 3].max() - t0).item():6.2f} us  prologue {q(ph[0])}  main {q(ph[1])}  "
           f"epilogue {q(ph[2])} (median/max us)", flush=True)
+    if XCD_REPORT:  # main loop per XCD (linear block id mod 8) and per dispatch round (id / 256)
+        ids = torch.nonzero(st.view(-1, 4)[:, 0].cpu() > 0).flatten()
+        mn = ph[1]
+        print("    main by XCD  " + "  ".join(f"{x}:{q(mn[ids % 8 == x])}" for x in range(8)), flush=True)
+        rounds = sorted(set((ids // 256).tolist()))
+        print("    main by round " + "  ".join(f"{r}:{q(mn[ids // 256 == r])}" for r in rounds), flush=True)
 
 
 def main():
@@ -73,10 +82,13 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="comma-separated substrings of the shapes to run")
     ap.add_argument("--no-extras", action="store_true", help="skip the pyramid / lookup timings")
+    ap.add_argument("--xcd", action="store_true", help="with --stamps: main loop per XCD / round")
     ap.add_argument("--stamps", action="store_true",
                     help="Winograd shapes: per-workgroup phase times of one launch "
                          "(scflow_debug_conv_stamps; s_memrealtime at 100 MHz)")
     a = ap.parse_args()
+    global XCD_REPORT
+    XCD_REPORT = a.xcd
     n, h, w = a.batch, a.size, a.size
     M = n * h * w
     dev = "cuda"

@@ -58,9 +58,38 @@ def wino(W):
     return worst(lane, offs)
 
 
+def enc_conv(S, tc, tm, KW=3, new=True):
+    """encoder.hip enc_conv_kernel A-fragment reads: 5 float4 per halo pixel (16 channels + 4),
+    stride-2 skew of one float4 every 2 columns and the row pitch enc_row_pitch picks (new), or
+    the round-4 layout (row pitch hc·5, no skew)."""
+    hc = (tc - 1) * S + KW
+    if new:
+        a4 = lambda hr, c, rp: hr * rp + 5 * c + (c >> 1 if S == 2 else 0)  # noqa: E731
+        base = a4(0, hc, 0)
+        best = None
+        for pad in range(16):  # enc_row_pitch: least conflicted of 16 pitches
+            cost = sum(worst(lambda li, wm=wm, r=r: a4(((wm * tm // 2 + 32 * r + li) // tc) * S,
+                                                      ((wm * tm // 2 + 32 * r + li) % tc) * S, base + pad),
+                             [0]) for wm in (0, 1) for r in range(tm // 64))
+            if best is None or cost < best[0]:
+                best = (cost, base + pad)
+        rp = best[1]
+    else:
+        a4 = lambda hr, c, rp: (hr * hc + c) * 5  # noqa: E731
+        rp = 0
+    return max(worst(lambda li, wm=wm, r=r: a4(((wm * tm // 2 + 32 * r + li) // tc) * S,
+                                              ((wm * tm // 2 + 32 * r + li) % tc) * S, rp), [0])
+               for wm in (0, 1) for r in range(tm // 64))
+
+
 if __name__ == "__main__":
     for d in (0, 1):
         for W in (32, 64):
             print(f"conv_wino5_kernel DIR={d} W={W}: worst slot multiplicity {wino5(d, W)[0]}")
     for W in (32, 64, 128):
         print(f"conv_wino_kernel W={W}: worst slot multiplicity {wino(W)}")
+    for S, tc, tm, what in ((2, 16, 64, "pose head conv 1 (32² -> 16²)"), (2, 8, 64, "pose head conv 2 (16² -> 8²)"),
+                            (1, 128, 128, "encoder 3x3 s1 at 128²"), (2, 64, 128, "encoder 3x3 s2 -> 64²"),
+                            (1, 16, 64, "encoder 3x3 s1 at 16²")):
+        print(f"enc_conv_kernel S={S} tile {tm // tc}x{tc} ({what}): worst slot multiplicity "
+              f"{enc_conv(S, tc, tm, new=False)} (round 4) -> {enc_conv(S, tc, tm)}")
