@@ -937,9 +937,6 @@ static unsigned long long* g_wino_stamps = nullptr;
 #ifndef WINO4_MIN_COUT
 #define WINO4_MIN_COUT 160
 #endif
-#ifndef WINO5_PAIR_DEFAULT
-#define WINO5_PAIR_DEFAULT 0
-#endif
 #ifndef WINO4_DEFAULT
 #define WINO4_DEFAULT 1
 #endif
@@ -971,40 +968,21 @@ int launch_wino_w(WinoParams p, hipStream_t st) {
   return scflow_launch_status();
 }
 
-// SCFLOW_WINO5_PAIR=1: the paired F(4,5) workgroups (conv_wino5_kernel PR = 2) when the grid
-// splits evenly
-bool wino5_pair() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SCFLOW_WINO5_PAIR");
-    v = e ? atoi(e) : WINO5_PAIR_DEFAULT;
-  }
-  return v != 0;
-}
-
-template <int DIR, int W, int NBW, int EPI, int PR>
-int launch_wino5_pr(Wino5Params p, dim3 grid, hipStream_t st) {
-  const size_t lds = wino5_lds_bytes<DIR, W, NBW>() * PR;
-  static bool attr = false;
-  if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI, PR>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  p.swz_c = PR > 1 ? 0 : wino_swz(grid.x, grid.y);
-  p.stamps = g_wino_stamps;
-  grid.x /= PR;
-  conv_wino5_kernel<DIR, W, NBW, EPI, PR><<<grid, 256 * PR, lds, st>>>(p);
-  return scflow_launch_status();
-}
-
 template <int DIR, int W, int NBW, int EPI>
 int launch_wino5_k(Wino5Params p, hipStream_t st) {
   using G = Wino5Geom<DIR, W>;
+  const size_t lds = wino5_lds_bytes<DIR, W, NBW>();
+  static bool attr = false;
+  if (lds > 64 * 1024 && !attr) {
+    (void)hipFuncSetAttribute((const void*)conv_wino5_kernel<DIR, W, NBW, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
   dim3 grid(p.a.n * (p.a.h / G::OROWS) * (W / G::OCOLS), round_up(p.a.cout, 32 * NBW) / (32 * NBW));
-  if (wino5_pair() && grid.x % 2 == 0 && wino5_lds_bytes<DIR, W, NBW>() * 2 <= 160 * 1024)
-    return launch_wino5_pr<DIR, W, NBW, EPI, 2>(p, grid, st);
-  return launch_wino5_pr<DIR, W, NBW, EPI, 1>(p, grid, st);
+  p.swz_c = wino_swz(grid.x, grid.y);
+  p.stamps = g_wino_stamps;
+  conv_wino5_kernel<DIR, W, NBW, EPI><<<grid, 256, lds, st>>>(p);
+  return scflow_launch_status();
 }
 
 template <int EPI>

@@ -77,36 +77,27 @@ constexpr size_t wino5_lds_bytes() {
 // (A K split for the GRU q conv's one-workgroup-per-CU grid — two wave sets over the two 8-channel
 // halves of every sub-step — was built in round 4 and measured in round 5: 32.7 → 32.5 µs alone,
 // the decoder 2 % slower; removed.)
-// PR = 2 ("paired"): one launched workgroup of 512 threads runs two tile blocks as two 256-thread
-// halves with their own LDS regions, meeting at every block barrier.  With two independent
-// workgroups per CU the SQ's oldest-first issue lets the first-dispatched one run ahead: the
-// second's main loop ends ≈ 25 % later and runs its tail with one wave per SIMD (stamps, round 5);
-// the shared barriers keep the two in step.
-template <int DIR, int W, int NBW, int EPI, int PR = 1>
-__global__ __launch_bounds__(256 * PR, 2 / PR) void conv_wino5_kernel(Wino5Params P) {
+// (Paired workgroups — two tile blocks per 512-thread workgroup meeting at every barrier, so the
+// SQ's oldest-first issue cannot let the first-dispatched workgroup of a CU run ahead of the
+// second — were measured in round 5: both main loops then take what the second one took alone,
+// 42 µs for z|r, and the decoder ran 1 % slower; removed.)
+template <int DIR, int W, int NBW, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
   using G = Wino5Geom<DIR, W>;
   constexpr int NTH = 256;                                   // threads
   constexpr int NA = (G::NH4 + 2 * NTH - 1) / (2 * NTH);    // float4 per thread per half stage
   constexpr int BNW = 32 * NBW;
-  extern __shared__ floatx4 smem4_all[];
-  const int grp = PR > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8) : 0;  // half
-  floatx4* smem4 = smem4_all + grp * (wino5_lds_bytes<DIR, W, NBW>() / 16);
+  extern __shared__ floatx4 smem4[];
   float* smem = (float*)smem4;
   const scflow_conv_args& a = P.a;
-  const int tid = threadIdx.x & 255, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar operands
   const int wave = wv & 3;              // point pair
   const int li = lane & 31, hh = lane >> 5;
   constexpr int XB = W / G::OCOLS;  // column blocks per image (1, or 2 for 5×1 at W = 64)
   int bx, by;
   wino_block(P.swz_c, bx, by);
-  bx = bx * PR + grp;
-  auto wstamp = [&](int k) {  // wino_stamp per half: stamp slot = the half's own tile block
-    if (P.stamps && tid == 0)
-      P.stamps[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * PR + grp) * 4 + k] =
-          __builtin_amdgcn_s_memrealtime();
-  };
-  wstamp(0);
+  wino_stamp(P.stamps, 0);
   const int blocks_per_img = (a.h / G::OROWS) * XB;
   const int img = bx / blocks_per_img;
   const int rem = bx % blocks_per_img;
@@ -246,7 +237,7 @@ __global__ __launch_bounds__(256 * PR, 2 / PR) void conv_wino5_kernel(Wino5Param
     hstore(0, 1);
     __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
     __syncthreads();
-    wstamp(1);
+    wino_stamp(P.stamps, 1);
     floatx4 vA[2][2], vB[2][2];
     vload(0, 0, 0, d, w3);
     vmath(d, vA[0], w3);
@@ -336,7 +327,7 @@ __global__ __launch_bounds__(256 * PR, 2 / PR) void conv_wino5_kernel(Wino5Param
       }
     }
   __syncthreads();
-  wstamp(2);
+  wino_stamp(P.stamps, 2);
   float* S = smem;
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -398,7 +389,7 @@ __global__ __launch_bounds__(256 * PR, 2 / PR) void conv_wino5_kernel(Wino5Param
   }
   if (P.stamps) {
     __builtin_amdgcn_s_waitcnt(0);
-    wstamp(3);
+    wino_stamp(P.stamps, 3);
   }
 }
 
