@@ -320,6 +320,24 @@ int scflow_pose_step_part(const float* drot6, const float* dt, const float* R_sr
                           float* lr_next, int s_next, float* hx_next, int s_hx, int h, int w,
                           float up_scale, float down_scale, int parts, void* stream);
 
+/* scflow_pose_step_heads: scflow_pose_step_part with the pose head's rotation / translation heads
+ *   (MultiClassPoseHead, models/head/pose_head.py:203-211 — label[0]'s class for every sample)
+ *   computed in the same launch instead of by scflow_ph_heads_sum: x = relu(Σ_z x_z + xbias),
+ *   the last FC's xsplit K-split partial sums [xsplit][n][k]; rch = 6 (ortho6d) or 4
+ *   (quaternion, depth_transform's SCFLOW_POSE_QUAT_XYZW).  drot [n][rch] / dt [n][3] are
+ *   OUTPUTS here (the decoder's returned deltas).  Replaces the heads launch + the pose step's
+ *   delta reads of the reference's get_pose_ (models/decoder/scflow_decoder.py:230-236). */
+int scflow_pose_step_heads(const float* x, int xsplit, const float* xbias, int k, const float* Wr,
+                           const float* br, int rch, const float* Wt, const float* bt,
+                           const long long* label, int num_class, float* drot, float* dt,
+                           const float* R_src, const float* t_src, const float* K,
+                           const float* points, float* R_dst, float* t_dst, float* flow, int n,
+                           int H, int W, float weight, int depth_transform, float invalid_num,
+                           const float* lr, const float* delta, const float* mask, float* flow_up,
+                           float* mask_up, float* lr_next, int s_next, float* hx_next, int s_hx,
+                           int h, int w, float up_scale, float down_scale, int parts,
+                           void* stream);
+
 /* §8(f)-1: RAFTEncoder (Basic) — feature encoder (InstanceNorm) and context encoder (BatchNorm,
  * eval statistics), models/encoder/raft_encoder.py:286-314, BasicBlock models/backbone/resnet.py:
  * 12-92, ResLayer resnet.py:676-771, called from SCFlowRefiner.extract_feat

@@ -147,6 +147,10 @@ SIGNATURES = {
     "scflow_pose_step_part": (c_int, [c_vp] * 9 + [c_int, c_int, c_int, c_float, c_int, c_float] +
                               [c_vp] * 6 + [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_int,
                                             c_vp]),
+    "scflow_pose_step_heads": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
+                                       c_int, c_vp, c_vp] + [c_vp] * 7 +
+                               [c_int, c_int, c_int, c_float, c_int, c_float] + [c_vp] * 6 +
+                               [c_int, c_vp, c_int, c_int, c_int, c_float, c_float, c_int, c_vp]),
     "scflow_sync_event_create": (c_int, [ctypes.POINTER(c_vp)]),
     "scflow_sync_event_destroy": (c_int, [c_vp]),
     "scflow_sync_event_record": (c_int, [c_vp, c_vp]),

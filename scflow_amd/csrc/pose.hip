@@ -147,7 +147,8 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
 
 __global__ __launch_bounds__(256) void pose_step_kernel(PoseStepArgs a) {
   __shared__ float sh[21];
-  pose_step_body(a, sh, blockIdx.x, blockIdx.y, threadIdx.x, 256);
+  __shared__ float hs[16 + 16 * 4];  // fused heads: results + the 4 waves' partial sums
+  pose_step_body(a, sh, blockIdx.x, blockIdx.y, threadIdx.x, 256, false, hs);
 }
 
 // batched 2-D transpose through a padded LDS tile
@@ -279,6 +280,38 @@ SCFLOW_API int scflow_pose_step_part(const float* drot6, const float* dt, const 
   if (!(parts & 1)) a.bf = 0;
   if (!(parts & 2)) a.bl = 0;
   if (a.bf + a.bl == 0) return SCFLOW_EINVAL;  // parts = 2 needs lr_next
+  pose_step_kernel<<<dim3(a.bf + a.bl, n), 256, 0, (hipStream_t)stream>>>(a);
+  return scflow_launch_status();
+}
+
+SCFLOW_API int scflow_pose_step_heads(const float* x, int xsplit, const float* xbias, int k,
+                                      const float* Wr, const float* br, int rch, const float* Wt,
+                                      const float* bt, const long long* label, int num_class,
+                                      float* drot, float* dt, const float* R_src,
+                                      const float* t_src, const float* K, const float* points,
+                                      float* R_dst, float* t_dst, float* flow, int n, int H, int W,
+                                      float weight, int depth_transform, float invalid_num,
+                                      const float* lr, const float* delta, const float* mask,
+                                      float* flow_up, float* mask_up, float* lr_next, int s_next,
+                                      float* hx_next, int s_hx, int h, int w, float up_scale,
+                                      float down_scale, int parts, void* stream) {
+  if (!x || xsplit < 1 || !xbias || k <= 0 || !Wr || !br || !Wt || !bt || !label ||
+      num_class <= 0 || !drot || !dt || rch != pose_rot_dim(depth_transform) || parts < 1 ||
+      parts > 3)
+    return SCFLOW_EINVAL;
+  PoseStepArgs a;
+  // drot / dt are the outputs here; the argument checks want a delta source: pass them (unread)
+  const int st = pose_step_args(&a, drot, dt, R_src, t_src, K, points, R_dst, t_dst, flow, n, H, W,
+                                weight, depth_transform, invalid_num, lr, delta, mask, flow_up,
+                                mask_up, lr_next, s_next, hx_next, s_hx, h, w, up_scale, down_scale,
+                                256);
+  if (st != SCFLOW_OK) return st;
+  if (!(parts & 1)) a.bf = 0;
+  if (!(parts & 2)) a.bl = 0;
+  if (a.bf + a.bl == 0) return SCFLOW_EINVAL;  // parts = 2 needs lr_next
+  a.hx = x; a.hxs = (long long)n * k; a.hk = k; a.hsplit = xsplit; a.hxb = xbias;
+  a.Wr = Wr; a.br = br; a.Wt = Wt; a.bt = bt; a.hlabel = label; a.hrch = rch; a.hncls = num_class;
+  a.drot_out = drot; a.dt_out = dt;
   pose_step_kernel<<<dim3(a.bf + a.bl, n), 256, 0, (hipStream_t)stream>>>(a);
   return scflow_launch_status();
 }

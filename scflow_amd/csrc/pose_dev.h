@@ -178,14 +178,69 @@ struct PoseStepArgs {
   float* o0; int s0; float* o1; int s1; int h, w; float up_scale, down_scale;
   int bf, bl;
   int given;  // 1: Rsrc / tsrc are the updated pose already (no update, Rout / tout unused)
+  // heads fused (hx != NULL; scflow_pose_step_heads): the pose delta of image n is computed in
+  // the launch from the last FC's K-split partial sums — x = relu(Σ_z hx[z·hxs] + hxb), the
+  // label[0] class's rch rotation rows of Wr and 3 translation rows of Wt (MultiClassPoseHead,
+  // pose_head.py:203-211) — instead of read from drot6 / dtv; block 0 of image n writes it to
+  // drot_out / dt_out (the decoder's returned delta lists)
+  const float* hx; long long hxs; int hk, hsplit; const float* hxb;
+  const float* Wr; const float* br; const float* Wt; const float* bt; const long long* hlabel;
+  int hrch, hncls; float* drot_out; float* dt_out;
 };
+
+// the heads' 9 (rch + 3) dot products of image n over the block's nt threads (threads split K),
+// wave sums by xor shuffles, then the waves' partials in order through LDS → hs[0 .. rch+3)
+// (bias added).  hs: 16·(nt/64) + 16 floats of LDS.  Every thread calls this (barrier inside).
+// The separate heads launch (scflow_ph_heads*, ph_heads_kernel) runs this same function, so the
+// fused and the separate tail give bit-identical deltas.
+__device__ __forceinline__ void pose_heads(const PoseStepArgs& a, float* hs, int n, int tid, int nt) {
+#pragma clang fp contract(off)
+  const int nr = a.hrch + 3;
+  long long cls = a.hlabel[0];  // every sample uses label[0]'s class (reference quirk)
+  if (cls < 0 || cls >= a.hncls) cls = 0;
+  float acc[9];
+#pragma unroll
+  for (int r = 0; r < 9; ++r) acc[r] = 0.f;
+  for (int k = tid; k < a.hk; k += nt) {
+    float x = a.hx[(size_t)n * a.hk + k];
+    if (a.hsplit > 0) {  // the previous FC's K-split partial sums: relu(Σ + bias)
+      for (int z = 1; z < a.hsplit; ++z) x += a.hx[z * a.hxs + (size_t)n * a.hk + k];
+      x = fmaxf(x + a.hxb[k], 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      if (r < nr) {
+        const float* wrow = r < a.hrch ? a.Wr + ((size_t)cls * a.hrch + r) * a.hk
+                                       : a.Wt + ((size_t)cls * 3 + (r - a.hrch)) * a.hk;
+        acc[r] += wrow[k] * x;
+      }
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    float v = acc[r];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) hs[16 + wv * 16 + r] = v;
+  }
+  __syncthreads();
+  if (tid < nr) {
+    float v = 0.f;
+    for (int w = 0; w < nt / 64; ++w) v += hs[16 + w * 16 + tid];
+    hs[tid] = v + (tid < a.hrch ? a.br[cls * a.hrch + tid] : a.bt[cls * 3 + (tid - a.hrch)]);
+  }
+  __syncthreads();
+}
 
 // sh: 21 floats of LDS; every thread of the block calls this (barrier inside)
 // fresh: drot6/dtv were written earlier in the same launch by another workgroup — read them
 // with agent-scope (sc1, vector) loads, never through the scalar cache
 __device__ __forceinline__ void pose_step_body(const PoseStepArgs& a, float* sh, int bx, int n,
-                                               int tid, int nt, bool fresh = false) {
+                                               int tid, int nt, bool fresh = false,
+                                               float* hs = nullptr) {
 #pragma clang fp contract(off)
+  if (hs && a.hx && !a.given) pose_heads(a, hs, n, tid, nt);
   if (a.given) {  // the pose of this iteration was updated by the ↓8 part: 21 plain loads
     if (tid < 9)
       sh[tid] = a.Rsrc[9 * n + tid];
@@ -196,12 +251,21 @@ __device__ __forceinline__ void pose_step_body(const PoseStepArgs& a, float* sh,
   } else if (tid == 0) {
     const int rd = pose_rot_dim(a.depth_transform);
     float d[6], dt[3];
-    for (int k = 0; k < rd; ++k)
-      d[k] = fresh ? __hip_atomic_load(a.drot6 + rd * n + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                   : a.drot6[rd * n + k];
-    for (int k = 0; k < 3; ++k)
-      dt[k] = fresh ? __hip_atomic_load(a.dtv + 3 * n + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : a.dtv[3 * n + k];
+    if (hs && a.hx) {  // heads fused: the delta from LDS; block 0 writes it out
+      for (int k = 0; k < rd; ++k) d[k] = hs[k];
+      for (int k = 0; k < 3; ++k) dt[k] = hs[rd + k];
+      if (bx == 0) {
+        for (int k = 0; k < rd; ++k) a.drot_out[rd * n + k] = d[k];
+        for (int k = 0; k < 3; ++k) a.dt_out[3 * n + k] = dt[k];
+      }
+    } else {
+      for (int k = 0; k < rd; ++k)
+        d[k] = fresh ? __hip_atomic_load(a.drot6 + rd * n + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : a.drot6[rd * n + k];
+      for (int k = 0; k < 3; ++k)
+        dt[k] = fresh ? __hip_atomic_load(a.dtv + 3 * n + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : a.dtv[3 * n + k];
+    }
     pose_update_one(d, dt, a.Rsrc + 9 * n, a.tsrc + 3 * n, sh, sh + 9, a.weight, a.depth_transform);
     if (bx == 0) {
       for (int k = 0; k < 9; ++k) a.Rout[9 * n + k] = sh[k];
@@ -295,6 +359,7 @@ static inline int pose_step_args(PoseStepArgs* a, const float* drot6, const floa
   a->mo = mask_up; a->o0 = lr_next; a->s0 = s_next; a->o1 = hx_next; a->s1 = s_hx; a->h = h;
   a->w = w; a->up_scale = up_scale; a->down_scale = down_scale;
   a->given = given ? 1 : 0;
+  a->hx = nullptr;
   const int bf = ceil_div((long long)H * W, nt);
   // from a given pose the part runs beside other work (the decoder's side stream): 4 pixels per
   // thread, a quarter of the workgroups to schedule

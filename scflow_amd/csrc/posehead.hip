@@ -24,6 +24,7 @@
 //    gather of the input (FC1 reads conv3's raw output).
 //  * scflow_ph_heads — the label[0] class's 6 rotation and 3 translation rows only.
 #include "common.h"
+#include "pose_dev.h"  // pose_heads: the heads' arithmetic shared with scflow_pose_step_heads
 
 #include <stdlib.h>
 
@@ -390,6 +391,17 @@ __device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, floa
   }
 }
 
+// the label[0] class's rotation / translation heads of sample row blockIdx.x (scflow_ph_heads*)
+__global__ __launch_bounds__(256) void ph_heads_kernel(PoseStepArgs a) {
+  __shared__ float hs[16 + 16 * 4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  pose_heads(a, hs, n, tid, 256);
+  if (tid < a.hrch)
+    a.drot_out[(size_t)n * a.hrch + tid] = hs[tid];
+  else if (tid < a.hrch + 3)
+    a.dt_out[(size_t)n * 3 + tid - a.hrch] = hs[tid];
+}
+
 template <int FC_RT>
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
   __shared__ float red[PH_WAVES / 2 * FC_RT * 64 * 5];
@@ -583,15 +595,13 @@ SCFLOW_API int scflow_ph_heads_sum(const float* x, int xsplit, const float* xbia
                                    float* drot, float* dt, void* stream) {
   if (xsplit < 0 || (xsplit > 0 && (!xbias || !aligned16(xbias)))) return SCFLOW_EINVAL;
   if (!x || !Wr || !br || !Wt || !bt || !label || !drot || !dt || m <= 0 || k <= 0 || (k & 15) ||
-      rch <= 0 || rch + 3 > 16 || num_class <= 0 || !aligned16(x) || !aligned16(Wr) || !aligned16(Wt))
+      rch <= 0 || rch + 3 > 9 || num_class <= 0 || !aligned16(x) || !aligned16(Wr) || !aligned16(Wt))
     return SCFLOW_EINVAL;
-  FcArgs f{};
-  f.x = x; f.ldx = k; f.m = m; f.k = k; f.W = Wr; f.bias = br; f.y = drot; f.n = rch + 3;
-  f.Wt = Wt; f.bt = bt; f.label = label; f.num_class = num_class; f.rch = rch; f.dt = dt;
-  f.xsplit = xsplit; f.xstride = (long long)m * k; f.xbias = xbias;
-  if (m <= 16)
-    ph_fc_kernel<1><<<1, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
-  else
-    ph_fc_kernel<2><<<1, PH_WAVES * 64, 0, (hipStream_t)stream>>>(f);
+  // one workgroup per sample row, the arithmetic of the pose step's fused heads (pose_heads)
+  PoseStepArgs a{};
+  a.hx = x; a.hxs = (long long)m * k; a.hk = k; a.hsplit = xsplit; a.hxb = xbias;
+  a.Wr = Wr; a.br = br; a.Wt = Wt; a.bt = bt; a.hlabel = label; a.hrch = rch; a.hncls = num_class;
+  a.drot_out = drot; a.dt_out = dt;
+  ph_heads_kernel<<<m, 256, 0, (hipStream_t)stream>>>(a);
   return scflow_launch_status();
 }

@@ -115,6 +115,10 @@ class SCFlowDecoder(nn.Module):
         # flow, ×8 prediction, mask) run on the side stream during the next iteration's GRU
         # (they only feed the returned lists)
         self.defer_full_res = True
+        # with fuse_tail: the pose head's rotation / translation heads computed inside the pose
+        # step's launch (scflow_pose_step_heads) instead of a launch of their own;
+        # SCFLOW_FUSE_HEADS=0: off (A/B)
+        self.fuse_heads = os.environ.get("SCFLOW_FUSE_HEADS", "1") != "0"
         # the deferred full-resolution part reads the pose the ↓8 part wrote instead of
         # recomputing the update per workgroup (ops.pose_step_given); SCFLOW_FULLRES_GIVEN=0: off
         self.fullres_given = os.environ.get("SCFLOW_FULLRES_GIVEN", "1") != "0"
@@ -615,17 +619,24 @@ class SCFlowDecoder(nn.Module):
                         nxt = dict(lr_next=None if last else Chan.whole(F2s[(j + 1) % 2]),
                                    hx_next=None if last else hx_flow,
                                    depth_transform=self.depth_transform)
-                        with ops.binding(hc, run=False):
-                            self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
+                        # the rotation / translation heads inside the pose step's launch
+                        # (scflow_pose_step_heads), or as their own launch before it
+                        ha = self.pose_pred.heads_args(pose_x[0], label) if self.fuse_heads else None
+                        if ha is None:
+                            with ops.binding(hc, run=False):
+                                self.pose_pred.heads_hip(pose_x[0], label, o_drot[j], o_dt[j])
+                        else:
+                            nxt["heads"] = ha
                         if defer and not last:
                             with ops.binding(pc, run=False):
                                 ops.pose_step(*step, **nxt, parts=2)
                             with ops.binding(fc, run=False):
                                 if self.fullres_given:
                                     ops.pose_step_given(o_R[j], o_t[j], *step[4:6], *step[8:])
-                                else:
+                                else:  # (reads the deltas the ↓8 launch wrote)
                                     fstep = step[:6] + (R_scr, t_scr) + step[8:]
-                                    ops.pose_step(*fstep, **nxt, parts=1)
+                                    ops.pose_step(*fstep, **{k: v for k, v in nxt.items() if k != "heads"},
+                                                  parts=1)
                         else:
                             with ops.binding(pc, run=False):
                                 ops.pose_step(*step, **nxt)

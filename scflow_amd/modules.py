@@ -769,6 +769,16 @@ class MultiClassPoseHead(nn.Module):
             x, xsplit, xbias, ldx = y, ks, lin.bias.detach(), lin.out_features
         return x
 
+    def heads_args(self, x, label: Tensor) -> Optional[tuple]:
+        """The heads' operands for ``ops.pose_step(heads=...)`` (the heads computed inside the
+        pose step's launch), or None when the trunk's output is not the split FC's partial sums."""
+        if x.dim() != 3:
+            return None
+        return (x, x.shape[0], self.fc_layers[-1][0].bias.detach(), x.shape[2],
+                self.rotation_pred.weight.detach(), self.rotation_pred.bias.detach(),
+                self.rotation_out_channels, self.translation_pred.weight.detach(),
+                self.translation_pred.bias.detach(), label.long(), self.num_class)
+
     def heads_hip(self, x, label: Tensor, drot: Tensor, dt: Tensor) -> None:
         """Rotation / translation heads of label[0]'s class on the trunk output x → drot, dt
         (x: [n, 256] or the last FC's split partial sums [split, n, 256])."""

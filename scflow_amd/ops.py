@@ -522,11 +522,14 @@ def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points:
               lr: Tensor, delta: Optional[Tensor], mask: Optional[Tensor], flow_up: Tensor,
               mask_up: Optional[Tensor], h: int, w: int, up_scale: float,
               lr_next: Optional[Chan] = None, hx_next: Optional[Chan] = None,
-              weight: float = 10.0, depth_transform: str = "exp", parts: int = 3) -> None:
+              weight: float = 10.0, depth_transform: str = "exp", parts: int = 3,
+              heads: Optional[tuple] = None) -> None:
     """One launch: ``pose_update_flow`` + ``flow_upsample(lr, delta, mask → flow_up, mask_up)``
     + (if ``lr_next``) the next iteration's ``flow_downsample`` of the new pose flow into
     ``lr_next`` / ``hx_next``, computed from the pose directly (scflow_pose_step).  ``parts``
-    (scflow_pose_step_part): 1 = only the full-resolution outputs, 2 = only the ↓8 flow."""
+    (scflow_pose_step_part): 1 = only the full-resolution outputs, 2 = only the ↓8 flow.
+    ``heads`` (``MultiClassPoseHead.heads_args``): the pose head's rotation / translation heads
+    in the same launch (scflow_pose_step_heads) — ``drot`` / ``dt`` are then written, not read."""
     for nm, x in (("drot", drot), ("dt", dt), ("R", R), ("t", t), ("K", K), ("points", points),
                   ("R_out", R_out), ("t_out", t_out), ("flow_out", flow_out), ("lr", lr),
                   ("flow_up", flow_up)):
@@ -540,7 +543,13 @@ def pose_step(drot: Tensor, dt: Tensor, R: Tensor, t: Tensor, K: Tensor, points:
             None if lr_next is None else lr_next.ptr, 0 if lr_next is None else lr_next.stride,
             None if hx_next is None else hx_next.ptr, 0 if hx_next is None else hx_next.stride,
             h, w, float(up_scale), 1.0 / float(up_scale))
-    if parts == 3:
+    if heads is not None:
+        x, xsplit, xbias, k, Wr, br, rch, Wt, bt, label, num_class = heads
+        if label.dtype != torch.int64 or label.device != x.device:
+            raise TypeError("label must be an int64 tensor on the same device")
+        _launch("scflow_pose_step_heads", drot, _p(x), int(xsplit), _p(xbias), int(k), _p(Wr), _p(br),
+                int(rch), _p(Wt), _p(bt), _p(label), int(num_class), *args, int(parts))
+    elif parts == 3:
         _launch("scflow_pose_step", drot, *args)
     else:
         _launch("scflow_pose_step_part", drot, *args, int(parts))

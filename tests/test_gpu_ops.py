@@ -539,6 +539,65 @@ def test_pose_step_matches_separate_launches(ops, S, s, nxt):
         assert torch.equal(a, b), nm
 
 
+@pytest.mark.parametrize("rch,parts", [(6, 2), (6, 3), (4, 3)])
+def test_pose_step_heads_fused(ops, rch, parts):
+    """scflow_pose_step_heads (the pose head's label[0] rotation / translation heads computed in
+    the pose step's launch, from the last FC's K-split partial sums) against the heads in fp64
+    (relu(Σ partials + bias) · W_cls + b_cls) within 1e-5, and the pose step's outputs against
+    scflow_pose_step on those deltas (the same update arithmetic: within fp32 rounding of the
+    deltas)."""
+    from scflow_amd import synthetic
+    n, S, s, k, ncls, split = 3, 256, 32, 256, 21, 4
+    sc = synthetic.make_scene(n, S, seed=6)
+    R0, t0, K, depth = (t(sc[key]).cuda() for key in ("ref_rotation", "ref_translation",
+                                                      "internel_k", "depth"))
+    g = torch.Generator().manual_seed(9)
+    x = (0.1 * torch.randn(split, n, k, generator=g)).cuda()
+    xb = (0.05 * torch.randn(k, generator=g)).cuda()
+    Wr = (0.01 * torch.randn(rch * ncls, k, generator=g)).cuda()
+    br = torch.tensor(([1.0, 0, 0, 0, 1.0, 0] if rch == 6 else [0, 0, 0, 1.0]) * ncls).cuda()
+    Wt = (0.01 * torch.randn(3 * ncls, k, generator=g)).cuda()
+    bt = (0.01 * torch.randn(3 * ncls, generator=g)).cuda()
+    label = torch.tensor([7, 3, 12], dtype=torch.int64).cuda()  # label[0] = 7 for every sample
+    mode = "exp"  # (the quaternion flag comes from drot's width)
+    pts = ops.lift_points(depth, K, R0, t0)
+    lr = torch.randn(n * s * s, 2, generator=g).cuda()
+    delta = torch.randn(n * s * s, 2, generator=g).cuda()
+    mask = torch.rand(n * s * s, 1, generator=g).cuda()
+    drot = torch.full((n, rch), 5.0, device="cuda")
+    dt = torch.full((n, 3), 5.0, device="cuda")
+    Rb, tb = torch.empty(n, 3, 3, device="cuda"), torch.empty(n, 3, device="cuda")
+    fb, upb = torch.empty(n, 2, S, S, device="cuda"), torch.empty(n, 2, S, S, device="cuda")
+    mb = torch.empty(n, 1, S, S, device="cuda")
+    nxb = torch.empty(n * s * s, 2, device="cuda")
+    ops.pose_step(drot, dt, R0, t0, K, pts, Rb, tb, fb, 400.0, lr, delta, mask, upb, mb, s, s, 8.0,
+                  lr_next=ops.Chan.whole(nxb), depth_transform=mode, parts=parts,
+                  heads=(x, split, xb, k, Wr, br, rch, Wt, bt, label, ncls))
+    torch.cuda.synchronize()
+    xr = torch.relu(x.double().sum(0) + xb.double())
+    c = 7
+    ref_r = xr @ Wr.double()[c * rch:(c + 1) * rch].T + br.double()[c * rch:(c + 1) * rch]
+    ref_t = xr @ Wt.double()[c * 3:(c + 1) * 3].T + bt.double()[c * 3:(c + 1) * 3]
+    np.testing.assert_allclose(drot.cpu().double().numpy(), ref_r.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dt.cpu().double().numpy(), ref_t.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    # the rest of the launch: scflow_pose_step on the deltas it wrote
+    Ra, ta = torch.empty_like(Rb), torch.empty_like(tb)
+    fa, upa, ma = torch.empty_like(fb), torch.empty_like(upb), torch.empty_like(mb)
+    nxa = torch.empty_like(nxb)
+    ops.pose_step(drot, dt, R0, t0, K, pts, Ra, ta, fa, 400.0, lr, delta, mask, upa, ma, s, s, 8.0,
+                  lr_next=ops.Chan.whole(nxa), depth_transform=mode, parts=parts)
+    torch.cuda.synchronize()
+    assert torch.equal(Ra, Rb) and torch.equal(ta, tb)
+    assert torch.equal(nxa, nxb)
+    if parts & 1:
+        assert torch.equal(fa, fb) and torch.equal(upa, upb) and torch.equal(ma, mb)
+    from scflow_amd._lib import ScflowError
+    with pytest.raises(ScflowError):  # rch must match the rotation mode
+        ops.pose_step(drot, dt, R0, t0, K, pts, Rb, tb, fb, 400.0, lr, delta, mask, upb, mb, s, s,
+                      8.0, depth_transform=mode, parts=1,
+                      heads=(x, split, xb, k, Wr, br, 5, Wt, bt, label, ncls))
+
+
 @pytest.mark.parametrize("S,s", [(256, 32), (512, 64), (100, 13)])
 def test_flow_resampling(ops, S, s):
     g = torch.Generator().manual_seed(4)
