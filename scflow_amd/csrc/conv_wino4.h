@@ -32,8 +32,8 @@ constexpr int W4P = 36;   // transform points per tile
 constexpr int W4KC = 8;   // input channels per sub-step (lanes 0-31: channels 0-3, 32-63: 4-7)
 constexpr int W4TM = 32;  // tiles per block (MFMA rows)
 constexpr int W4NPW = W4P / 4;  // points per wave
-constexpr int W4CP = 36;  // epilogue LDS row: 32 output channels + 4 (16-B rows, spread banks)
-constexpr int W4_LDS = W4P * 8 * W4CP * 4;  // epilogue bytes: [36 points][8 tiles][W4CP]
+constexpr int W4CP = 32;  // epilogue LDS row: 32 output channels (16-B reads conflict-free)
+constexpr int W4_LDS = W4P * 16 * W4CP * 4;  // epilogue bytes: [36 points][16 tiles][W4CP]
 
 __device__ __forceinline__ bool w4_al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -188,83 +188,108 @@ __global__ __launch_bounds__(256, 2) void conv_wino4_kernel(Wino4Params P) {
     __builtin_amdgcn_s_waitcnt(0);
     wino_stamp(P.stamps, 2);
   }
-  // epilogue, 8 tiles per round: round q holds accumulator rows 4q..4q+3 = tiles 8q + 4hh + rr,
-  // staged as M[point][tile][channel]; thread = (tile tl, channel quad cq, output row ya): the
-  // row ya of Aᵀ·M (a runtime row of coefficients, float4 over the quad), then Aᵀ over the
-  // columns → output pixels (ya, 0..3) × 4 channels as 16-B stores
+  // epilogue, 16 tiles per round (2 rounds): round q holds accumulator rows 8q..8q+7 = tiles
+  // 16q + 8s + 4hh + rr (s = 0, 1), staged as M[point][tile][channel]; thread = (tile, channel
+  // pair) computes the tile's whole 4×4 output for its 2 channels — every point read once (Aᵀ
+  // over the rows i per column x, accumulated over x with A), where per-output-row threads
+  // re-read all 36 points 4 times over.  8-B reads and stores (a wave: 4 tiles × 32 channels).
+  typedef float floatx2 __attribute__((ext_vector_type(2)));
   const int per = P.th * P.tw;
-  const int tl = tid >> 5, cq = (tid >> 2) & 7, ya = tid & 3;
-  const int col = cb * 32 + 4 * cq;
-  const int nv = a.cout - col < 4 ? a.cout - col : 4;  // valid channels of the quad (≤ 0: none)
-  const bool vo = nv == 4 && (a.so & 3) == 0 && w4_al16(a.out);
-  const bool vb = nv == 4 && (a.sbm & 3) == 0 && w4_al16(a.bias_map);
-  const bool vr = nv == 4 && (a.sres & 3) == 0 && w4_al16(a.res);
-  const floatx4 zero4 = {0.f, 0.f, 0.f, 0.f}, one4 = {1.f, 1.f, 1.f, 1.f};
-  const floatx4 bias4 = (nv > 0 && a.bias) ? w4_ld4(a.bias + col, nv == 4 && w4_al16(a.bias + col), nv) : zero4;
-  const floatx4 osc4 = (nv > 0 && a.out_scale) ? w4_ld4(a.out_scale + col, false, nv) : one4;
-  const floatx4 osh4 = (nv > 0 && a.out_scale) ? w4_ld4(a.out_shift + col, false, nv) : zero4;
-  // row ya of Aᵀ (0, ±1, ±2, 4, 8, ±½, ¼, ±⅛, …)
-  const float c1 = 1.f, c2 = ya == 0 ? 1.f : (ya == 2 ? 1.f : -1.f);
-  const float c3 = ya == 0 ? 1.f : (ya == 1 ? 2.f : (ya == 2 ? 4.f : 8.f));
-  const float c4 = ya == 0 ? 1.f : (ya == 1 ? -0.5f : (ya == 2 ? 0.25f : -0.125f));
-  const float c0 = ya == 0 ? 1.f : 0.f, c5 = ya == 3 ? 1.f : 0.f;
-  const floatx4* M4 = (const floatx4*)w4s;
+  const int tl = tid >> 4, cp = tid & 15;
+  const int col = cb * 32 + 2 * cp;
+  const int nv = a.cout - col < 2 ? a.cout - col : 2;  // valid channels of the pair (≤ 0: none)
+  const bool vo = nv == 2 && (a.so & 1) == 0 && ((uintptr_t)a.out & 7) == 0;
+  auto ld2 = [&](const float* q, bool ok2) -> floatx2 {
+    floatx2 r = {0.f, 0.f};
+    if (ok2) return *(const floatx2*)q;
+    if (nv > 0) r[0] = q[0];
+    if (nv > 1) r[1] = q[1];
+    return r;
+  };
+  const bool vb = nv == 2 && (a.sbm & 1) == 0 && ((uintptr_t)a.bias_map & 7) == 0;
+  const bool vr = nv == 2 && (a.sres & 1) == 0 && ((uintptr_t)a.res & 7) == 0;
+  const floatx2 zero2 = {0.f, 0.f}, one2 = {1.f, 1.f};
+  const floatx2 bias2 = (nv > 0 && a.bias) ? ld2(a.bias + col, false) : zero2;
+  const floatx2 osc2 = (nv > 0 && a.out_scale) ? ld2(a.out_scale + col, false) : one2;
+  const floatx2 osh2 = (nv > 0 && a.out_scale) ? ld2(a.out_shift + col, false) : zero2;
+  const floatx2* M2 = (const floatx2*)w4s;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < 2; ++q) {
     if (q) __syncthreads();  // the previous round's reads are done
 #pragma unroll
     for (int j = 0; j < W4NPW; ++j)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        w4s[((p0 + j) * 8 + 4 * hh + rr) * W4CP + li] = acc[j][4 * q + rr];
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          w4s[((p0 + j) * 16 + 8 * s2 + 4 * hh + rr) * W4CP + li] = acc[j][8 * q + 4 * s2 + rr];
     __syncthreads();
-    const int T = tb * W4TM + 8 * q + tl;
+    const int T = tb * W4TM + 16 * q + tl;
     if (T >= P.ntiles || nv <= 0) continue;
-    floatx4 rj[6];  // (Aᵀ M)[ya][j], j = 0..5
+    // Y[ya][xb] = Σ_x (Aᵀ M)[ya][x] · Aᵀ[xb][x]; Aᵀ = [1 1 1 1 1 0; 0 1 −1 2 −½ 0; 0 1 1 4 ¼ 0;
+    // 0 1 −1 8 −⅛ 1] (coefficients exact in fp32; products by ±1 fold to adds)
+    constexpr float AT[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                                {0.f, 1.f, -1.f, 2.f, -0.5f, 0.f},
+                                {0.f, 1.f, 1.f, 4.f, 0.25f, 0.f},
+                                {0.f, 1.f, -1.f, 8.f, -0.125f, 1.f}};
+    floatx2 y[4][4];
 #pragma unroll
     for (int x = 0; x < 6; ++x) {
-      const floatx4 m0 = M4[((0 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
-      const floatx4 m1 = M4[((1 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
-      const floatx4 m2 = M4[((2 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
-      const floatx4 m3 = M4[((3 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
-      const floatx4 m4 = M4[((4 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
-      const floatx4 m5 = M4[((5 * 6 + x) * 8 + tl) * (W4CP / 4) + cq];
-      rj[x] = c0 * m0 + c1 * m1 + c2 * m2 + c3 * m3 + c4 * m4 + c5 * m5;
+      floatx2 m[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) m[i] = M2[((6 * i + x) * 16 + tl) * (W4CP / 2) + cp];
+      const floatx2 s12 = m[1] + m[2], d12 = m[1] - m[2];
+      floatx2 t[4];
+      t[0] = m[0] + s12 + m[3] + m[4];
+      t[1] = d12 + 2.f * m[3] - 0.5f * m[4];
+      t[2] = s12 + 4.f * m[3] + 0.25f * m[4];
+      t[3] = d12 + 8.f * m[3] - 0.125f * m[4] + m[5];
+#pragma unroll
+      for (int ya = 0; ya < 4; ++ya)
+#pragma unroll
+        for (int xb = 0; xb < 4; ++xb) {
+          if (x == 0) {
+            y[ya][xb] = AT[xb][0] * t[ya];
+          } else if (AT[xb][x] == 1.f) {
+            y[ya][xb] += t[ya];
+          } else if (AT[xb][x] == -1.f) {
+            y[ya][xb] -= t[ya];
+          } else if (AT[xb][x] != 0.f) {
+            y[ya][xb] += AT[xb][x] * t[ya];
+          }
+        }
     }
-    const floatx4 s12 = rj[1] + rj[2], d12 = rj[1] - rj[2];
-    floatx4 y[4];
-    y[0] = rj[0] + s12 + rj[3] + rj[4];
-    y[1] = d12 + 2.f * rj[3] - 0.5f * rj[4];
-    y[2] = s12 + 4.f * rj[3] + 0.25f * rj[4];
-    y[3] = d12 + 8.f * rj[3] - 0.125f * rj[4] + rj[5];
     const int img = T / per;
     const int r = T - img * per;
     const int ty = r / P.tw, tx = r - ty * P.tw;
-    const size_t pix0 = ((size_t)img * a.h + 4 * ty + ya) * a.w + 4 * tx;
-    floatx4 val[4];
 #pragma unroll
-    for (int xb = 0; xb < 4; ++xb) val[xb] = (y[xb] + bias4) * osc4 + osh4;
-    // every global read (bias map, residual) before any store
-    if (a.bias_map) {
+    for (int ya = 0; ya < 4; ++ya) {
+      const size_t pix0 = ((size_t)img * a.h + 4 * ty + ya) * a.w + 4 * tx;
+      floatx2 val[4];
 #pragma unroll
-      for (int xb = 0; xb < 4; ++xb) val[xb] += w4_ld4(a.bias_map + (pix0 + xb) * a.sbm + col, vb, nv);
-    }
-    if (a.res) {
+      for (int xb = 0; xb < 4; ++xb) val[xb] = (y[ya][xb] + bias2) * osc2 + osh2;
+      // every global read (bias map, residual) of the row before its stores
+      if (a.bias_map) {
 #pragma unroll
-      for (int xb = 0; xb < 4; ++xb) val[xb] += w4_ld4(a.res + (pix0 + xb) * a.sres + col, vr, nv);
-    }
+        for (int xb = 0; xb < 4; ++xb) val[xb] += ld2(a.bias_map + (pix0 + xb) * a.sbm + col, vb);
+      }
+      if (a.res) {
 #pragma unroll
-    for (int xb = 0; xb < 4; ++xb) {
-      floatx4 o;
+        for (int xb = 0; xb < 4; ++xb) val[xb] += ld2(a.res + (pix0 + xb) * a.sres + col, vr);
+      }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = act_apply(val[xb][e], ACT);
-      float* dst = a.out + (pix0 + xb) * a.so + col;
-      if (vo) {
-        *(floatx4*)dst = o;
-      } else {
+      for (int xb = 0; xb < 4; ++xb) {
+        floatx2 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (e < nv) dst[e] = o[e];
+        for (int e = 0; e < 2; ++e) o[e] = act_apply(val[xb][e], ACT);
+        float* dst = a.out + (pix0 + xb) * a.so + col;
+        if (vo) {
+          *(floatx2*)dst = o;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            if (e < nv) dst[e] = o[e];
+        }
       }
     }
   }
@@ -344,6 +369,18 @@ int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
   const int e = scflow_launch_status();
   if (e) return e;
   const dim3 grid(p.ntb, round_up(a.cout, 32) / 32);
+  static bool attr = false;
+  if (!attr) {  // W4_LDS > 64 KiB: opt every instantiation in once
+    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_RELU>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_SIGMOID>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_TANH>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_NONE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
   switch (a.act) {  // the activation as a template argument: one epilogue body per kernel
     case SCFLOW_ACT_RELU: conv_wino4_kernel<SCFLOW_ACT_RELU><<<grid, 256, W4_LDS, st>>>(p); break;
     case SCFLOW_ACT_SIGMOID: conv_wino4_kernel<SCFLOW_ACT_SIGMOID><<<grid, 256, W4_LDS, st>>>(p); break;
