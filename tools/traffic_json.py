@@ -15,6 +15,7 @@ import collections
 import csv
 import glob
 import json
+import re
 
 
 def groups(B, S):
@@ -78,7 +79,8 @@ def per_kernel(d, counter):
     vals = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            vals[r["Kernel_Name"]].append((int(r.get("Grid_Size") or 0), float(r["Counter_Value"])))
+            name = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
+            vals[name].append((int(r.get("Grid_Size") or 0), float(r["Counter_Value"])))
     return vals
 
 
