@@ -82,6 +82,19 @@ def enc_conv(S, tc, tm, KW=3, new=True):
                for wm in (0, 1) for r in range(tm // 64))
 
 
+def lookup_tb(wp, dslot, D=9):
+    """lookup.hip tile-row lookup, sampling phase: the 16 lanes of a pixel read sample s = 16j +
+    lane's tap at row-major region offset b·wp + a (a, b = divmod(s, D)); ds_read_b32 serves 32
+    lanes (two pixels, slot stride dslot floats) per pass over 32 banks.  Returns the summed
+    worst multiplicity over the rounds (6 = conflict-free at D = 9)."""
+    tot = 0
+    for j in range((D * D + 15) // 16):
+        addrs = [((b * wp + a) + pix * dslot) % 32 for pix in range(2) for gl in range(16)
+                 for a, b in [divmod(16 * j + gl, D)] if 16 * j + gl < D * D]
+        tot += max(collections.Counter(addrs).values())
+    return tot
+
+
 if __name__ == "__main__":
     for d in (0, 1):
         for W in (32, 64):
@@ -93,3 +106,9 @@ if __name__ == "__main__":
                             (1, 16, 64, "encoder 3x3 s1 at 16²")):
         print(f"enc_conv_kernel S={S} tile {tm // tc}x{tc} ({what}): worst slot multiplicity "
               f"{enc_conv(S, tc, tm, new=False)} (round 4) -> {enc_conv(S, tc, tm)}")
+    # tile-row lookup (r = 4): the layout in use (rows of 11 floats; two level regions per slot,
+    # slot stride 2 · 124 + 4 = 252 floats) vs the best over row pitches 11..16 and slot strides
+    cur = lookup_tb(11, 252 % 32)
+    best = min((lookup_tb(wp, d), wp, d) for wp in range(11, 17) for d in range(32))
+    print(f"corr_lookup_lds_kernel TB sampling: {cur} b32 passes per 6 rounds (ideal 6); best layout "
+          f"{best[0]} at row pitch {best[1]}, slot stride ≡ {best[2]} mod 32")
