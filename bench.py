@@ -609,13 +609,13 @@ def main():
             big, timers, m_px, traffic.get("conv_wino4"), alg.get("conv_wino4")))
     if small:
         secondary.append(conv_roofline(
-            "conv_wino_kernel (F(2x2,3x3)): " + ", ".join(
-                {"heads": "XHead hidden 128->512 <32,2>", "corr_net1": "corr_net.1 256->192 <32,3>",
-                 "out_net": "out_net 256->126 <32,1>", "flow_net1": "flow_net.1 128->64 <32,1>",
-                 "dflow1": "delta_flow_encoder.1 128->64 <32,1>",
-                 "mask_enc1": "mask_encoder.1 64->32 <32,1>"}[p[0]] for p in small),
-            small, timers, m_px, *((traffic.get("conv_wino_kernel<32,1>"),
-                                     alg.get("conv_wino_kernel<32,1>"))
+            f"conv_wino_kernel<{h8},·> (F(2x2,3x3)): " + ", ".join(
+                {"heads": "XHead hidden 128->512", "corr_net1": "corr_net.1 256->192",
+                 "out_net": "out_net 256->126", "flow_net1": "flow_net.1 128->64",
+                 "dflow1": "delta_flow_encoder.1 128->64",
+                 "mask_enc1": "mask_encoder.1 64->32"}[p[0]] for p in small),
+            small, timers, m_px, *((traffic.get("conv_wino_kernel<32,1>", traffic.get("conv_wino_kernel<64,*>")),
+                                     alg.get("conv_wino_kernel<32,1>", alg.get("conv_wino_kernel<64,*>")))
                                     if not any(p[0] in ("heads", "corr_net1") for p in small)
                                     else (None, None))))
     secondary += secondary_rooflines(timers, hb, args.size, traffic,

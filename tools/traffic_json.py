@@ -56,6 +56,10 @@ def groups(B, S):
         "conv_wino_kernel<32,1>": (["conv_wino_kernel<32, 1>"], sum(small) / 4,
                                    "F(2x2,3x3) Winograd <32,1>: out_net 256→126, flow_net.1 / "
                                    "delta_flow_encoder.1 128→64, mask_encoder.1 64→32"),
+        "conv_wino_kernel<64,*>": (["conv_wino_kernel<64, 2>", "conv_wino_kernel<64, 1>"], sum(small) / 4,
+                                   "F(2x2,3x3) Winograd at 64-wide maps (configs[4]): out_net 256→126, "
+                                   "flow_net.1 / delta_flow_encoder.1 128→64 <64,2>, mask_encoder.1 "
+                                   "64→32 <64,1> (launches averaged)"),
         "conv_wino_kernel": (["conv_wino_kernel<32, 2>", "conv_wino_kernel<32, 3>"], (heads + corr1) / 2,
                              "F(2x2,3x3) Winograd <32,2> / <32,3> (only with SCFLOW_CONV_WINO4=0): "
                              "XHead hidden 128→512 + corr_net.1 256→192 (launches averaged)"),
