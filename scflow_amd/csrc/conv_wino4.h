@@ -142,46 +142,57 @@ __global__ __launch_bounds__(W4VT_THREADS) void wino4_vt_kernel(Wino4Params P) {
   for (int j = 0; j < 6; ++j) out[(6 * wv + j) * 64] = v[j];
 }
 
-// 2. the point GEMMs + output transform
-template <int ACT>
-__global__ __launch_bounds__(256, 2) void conv_wino4_kernel(Wino4Params P) {
+// 2. the point GEMMs + output transform.  D = sub-steps of V / U in flight per wave: 1 (two
+//    workgroups per CU, each point's pair reloaded 9 points ahead) or 2 (one workgroup per CU,
+//    the register budget of two, each pair reloaded 18 points ahead) — the choice for grids of
+//    ≤ one workgroup per CU, where no second wave per SIMD hides the L2 / MALL latency.
+template <int ACT, int D>
+__global__ __launch_bounds__(256, D == 2 ? 1 : 2) void conv_wino4_kernel(Wino4Params P) {
   extern __shared__ float w4s[];  // epilogue [36][32 co][W4EP]
   const scflow_conv_args& a = P.a;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, hh = lane >> 5;
   const int tb = blockIdx.x, cb = blockIdx.y;
-  const int nsub = P.nsub;
+  const int nsub = P.nsub;  // a multiple of D (launch_wino4)
   wino_stamp(P.stamps, 0);
   const unsigned blk = (unsigned)nsub * W4P * 1024;  // bytes of one block's V / U slice
   const __amdgpu_buffer_rsrc_t vsrc = wino_rsrc(P.v + (size_t)tb * nsub * W4P * 256, blk);
   const __amdgpu_buffer_rsrc_t usrc = wino_rsrc(a.weight + (size_t)cb * nsub * W4P * 256, blk);
   const int p0 = W4NPW * wv;  // this wave's first point
-  floatx4 v[W4NPW], u[W4NPW];
+  floatx4 v[D][W4NPW], u[D][W4NPW];
   floatx16 acc[W4NPW];
 #pragma unroll
   for (int j = 0; j < W4NPW; ++j)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-  auto load = [&](int k, int j) __attribute__((always_inline)) {
+  auto load = [&](int k, int b, int j) __attribute__((always_inline)) {
     const int off = (k * W4P + p0 + j) * 1024;  // wave-uniform (SGPR offset)
-    v[j] = wino_bload(vsrc, lane * 16, off);
-    u[j] = wino_bload(usrc, lane * 16, off);
+    v[b][j] = wino_bload(vsrc, lane * 16, off);
+    u[b][j] = wino_bload(usrc, lane * 16, off);
   };
 #pragma unroll
-  for (int j = 0; j < W4NPW; ++j) load(0, j);
-  wino_stamp(P.stamps, 1);
-  for (int k = 0; k < nsub; ++k) {
-    const int kn = k + 1 < nsub ? k + 1 : k;  // the last sub-step reloads itself (no branches)
-    auto point = [&](auto jc) __attribute__((always_inline)) {
-      constexpr int j = decltype(jc)::value;
+  for (int b = 0; b < D; ++b)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[j][e], u[j][e], acc[j], 0, 0, 0);
-      load(kn, j);  // eight points' MFMAs (≈ 2000 cycles) to arrive
-      __builtin_amdgcn_sched_barrier(0);
+    for (int j = 0; j < W4NPW; ++j) load(b, b, j);
+  wino_stamp(P.stamps, 1);
+  for (int k = 0; k < nsub; k += D) {
+    auto step = [&](auto bc) __attribute__((always_inline)) {
+      constexpr int b = decltype(bc)::value;
+      // sub-step k + b from buffer b; the buffer's next sub-step is k + b + D (the last ones
+      // reload the final sub-step: no branches)
+      const int kn = k + b + D < nsub ? k + b + D : nsub - 1;
+      auto point = [&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[b][j][e], u[b][j][e], acc[j], 0, 0, 0);
+        load(kn, b, j);  // D · eight points' MFMAs (≈ D · 2000 cycles) to arrive
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      StaticFor<0, W4NPW>::run(point);
     };
-    StaticFor<0, W4NPW>::run(point);
+    StaticFor<0, D>::run(step);
   }
 
   if (P.stamps) {
@@ -347,6 +358,31 @@ long long wino4_workspace_bytes(const scflow_conv_args& a) {
   return ntb * nsub * W4P * 1024;
 }
 
+template <int ACT, int D>
+void w4_set_lds() {
+  (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<ACT, D>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+template <int D>
+int launch_wino4_gemm(const Wino4Params& p, dim3 grid, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {  // W4_LDS > 64 KiB: opt every instantiation in once
+    w4_set_lds<SCFLOW_ACT_RELU, D>();
+    w4_set_lds<SCFLOW_ACT_SIGMOID, D>();
+    w4_set_lds<SCFLOW_ACT_TANH, D>();
+    w4_set_lds<SCFLOW_ACT_NONE, D>();
+    attr = true;
+  }
+  switch (p.a.act) {  // the activation as a template argument: one epilogue body per kernel
+    case SCFLOW_ACT_RELU: conv_wino4_kernel<SCFLOW_ACT_RELU, D><<<grid, 256, W4_LDS, st>>>(p); break;
+    case SCFLOW_ACT_SIGMOID: conv_wino4_kernel<SCFLOW_ACT_SIGMOID, D><<<grid, 256, W4_LDS, st>>>(p); break;
+    case SCFLOW_ACT_TANH: conv_wino4_kernel<SCFLOW_ACT_TANH, D><<<grid, 256, W4_LDS, st>>>(p); break;
+    default: conv_wino4_kernel<SCFLOW_ACT_NONE, D><<<grid, 256, W4_LDS, st>>>(p); break;
+  }
+  return scflow_launch_status();
+}
+
 int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
   if (!wino4_shape(a)) return SCFLOW_EUNSUPPORTED;
   if (!a.ws || a.ws_bytes < wino4_workspace_bytes(a)) return SCFLOW_EINVAL;
@@ -369,23 +405,11 @@ int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
   const int e = scflow_launch_status();
   if (e) return e;
   const dim3 grid(p.ntb, round_up(a.cout, 32) / 32);
-  static bool attr = false;
-  if (!attr) {  // W4_LDS > 64 KiB: opt every instantiation in once
-    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_RELU>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_SIGMOID>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_TANH>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_wino4_kernel<SCFLOW_ACT_NONE>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  switch (a.act) {  // the activation as a template argument: one epilogue body per kernel
-    case SCFLOW_ACT_RELU: conv_wino4_kernel<SCFLOW_ACT_RELU><<<grid, 256, W4_LDS, st>>>(p); break;
-    case SCFLOW_ACT_SIGMOID: conv_wino4_kernel<SCFLOW_ACT_SIGMOID><<<grid, 256, W4_LDS, st>>>(p); break;
-    case SCFLOW_ACT_TANH: conv_wino4_kernel<SCFLOW_ACT_TANH><<<grid, 256, W4_LDS, st>>>(p); break;
-    default: conv_wino4_kernel<SCFLOW_ACT_NONE><<<grid, 256, W4_LDS, st>>>(p); break;
-  }
-  return scflow_launch_status();
+  // two sub-steps in flight when the grid leaves CUs with a single workgroup
+  // (SCFLOW_WINO4_DEPTH = 1 / 2 forces one)
+  const char* de = getenv("SCFLOW_WINO4_DEPTH");
+  const int depth_env = de ? atoi(de) : 0;
+  const bool d2 = p.nsub % 2 == 0 &&
+                  (depth_env == 2 || (depth_env != 1 && (long long)grid.x * grid.y <= 256));
+  return d2 ? launch_wino4_gemm<2>(p, grid, st) : launch_wino4_gemm<1>(p, grid, st);
 }

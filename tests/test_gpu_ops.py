@@ -299,12 +299,16 @@ def test_conv2d_winograd(ops, case):
     (1, 20, 12, 36, 4, 100, "Sigmoid"),      # 15 tiles: a partial tile block, ragged channels
     (2, 128, 128, 64, 0, 64, "ReLU"),        # encoder width
 ])
-def test_conv2d_winograd_f4x4(ops, case):
+@pytest.mark.parametrize("depth", ["1", "2"])
+def test_conv2d_winograd_f4x4(ops, case, depth, monkeypatch):
     """Winograd F(4×4,3×3) (SCFLOW_CONV_WINO4: input transform launch + point GEMMs with the
-    output transform in the epilogue) vs an fp64 direct conv.  Tolerance: its fp32 error is ≈ 10×
-    the direct conv's (points {0, ±1, 2, −½, ∞}; 1.3e-5 of outputs ≈ 4 at 256 channels in a
-    numpy restatement) — 5e-5·√(K/256) absolute on unit-scale outputs."""
+    output transform in the epilogue) vs an fp64 direct conv, with one and two sub-steps of the
+    GEMM's operands in flight (SCFLOW_WINO4_DEPTH; two needs an even sub-step count, else one).
+    Tolerance: its fp32 error is ≈ 10× the direct conv's (points {0, ±1, 2, −½, ∞}; 1.3e-5 of
+    outputs ≈ 4 at 256 channels in a numpy restatement) — 5e-5·√(K/256) absolute on unit-scale
+    outputs."""
     from scflow_amd._lib import CONV_WINO4
+    monkeypatch.setenv("SCFLOW_WINO4_DEPTH", depth)
     n, h, w, c0, c1, cout, act = case
     got, ref = _conv_case(ops, n, h, w, c0, c1, cout, 3, 1, act, bk=CONV_WINO4)
     kk = (c0 + c1) * 9

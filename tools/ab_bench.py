@@ -2,6 +2,7 @@
 
 usage: python tools/ab_bench.py [--batch 16] [--rounds 5] [--steps 10] attr=v1,v2 [attr=...]
 e.g.   python tools/ab_bench.py split_pose_conv1=1,0 hoist_context=1,0
+       python tools/ab_bench.py env:SCFLOW_WINO4_DEPTH=0,1   (switches read per launch)
 Every combination is timed `rounds` times in round-robin order; prints median ms/forward.
 """
 import argparse
@@ -53,6 +54,9 @@ def main():
 
     def apply(c):
         for k, v in zip(names, c):
+            if k.startswith("env:"):
+                os.environ[k[4:]] = str(v)
+                continue
             obj, attr = target(k)
             setattr(obj, attr, v)
     for c in combos:  # warm every variant (packing, allocator)
