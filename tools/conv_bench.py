@@ -137,7 +137,7 @@ def main():
         tot_us += us
         res.append(dict(name=name, us=round(us, 2), tflops=round(tf, 2)))
         print(f"{name:28s} {us:9.2f} us  {tf:7.2f} TFLOP/s", flush=True)
-        if a.stamps and k in ((3, 3), (1, 5), (5, 1)):
+        if a.stamps and k in ((3, 3), (1, 5), (5, 1), (7, 7)):
             stamp_report(run)
     print(f"{'sum (one of each)':28s} {tot_us:9.2f} us")
     if a.no_extras:
