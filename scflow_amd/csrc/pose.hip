@@ -147,7 +147,8 @@ __global__ __launch_bounds__(256) void upsample_kernel(const float* __restrict__
 
 __global__ __launch_bounds__(256) void pose_step_kernel(PoseStepArgs a) {
   __shared__ float sh[21];
-  __shared__ float hs[16 + 16 * 4];  // fused heads: results + the 4 waves' partial sums
+  __shared__ float hs[16 + 16 * 4 + 21];  // fused heads: results, the 4 waves' partial sums,
+                                          // then the prefetched R, t, K
   pose_step_body(a, sh, blockIdx.x, blockIdx.y, threadIdx.x, 256, false, hs);
 }
 

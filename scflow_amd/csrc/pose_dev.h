@@ -198,6 +198,9 @@ __device__ __forceinline__ void pose_heads(const PoseStepArgs& a, float* hs, int
   const int nr = a.hrch + 3;
   long long cls = a.hlabel[0];  // every sample uses label[0]'s class (reference quirk)
   if (cls < 0 || cls >= a.hncls) cls = 0;
+  // the bias with the weights (one dependent load round after the label, not two)
+  float bias_r = 0.f;
+  if (tid < nr) bias_r = tid < a.hrch ? a.br[cls * a.hrch + tid] : a.bt[cls * 3 + (tid - a.hrch)];
   float acc[9];
 #pragma unroll
   for (int r = 0; r < 9; ++r) acc[r] = 0.f;
@@ -228,7 +231,7 @@ __device__ __forceinline__ void pose_heads(const PoseStepArgs& a, float* hs, int
   if (tid < nr) {
     float v = 0.f;
     for (int w = 0; w < nt / 64; ++w) v += hs[16 + w * 16 + tid];
-    hs[tid] = v + (tid < a.hrch ? a.br[cls * a.hrch + tid] : a.bt[cls * 3 + (tid - a.hrch)]);
+    hs[tid] = v + bias_r;
   }
   __syncthreads();
 }
@@ -240,7 +243,38 @@ __device__ __forceinline__ void pose_step_body(const PoseStepArgs& a, float* sh,
                                                int tid, int nt, bool fresh = false,
                                                float* hs = nullptr) {
 #pragma clang fp contract(off)
-  if (hs && a.hx && !a.given) pose_heads(a, hs, n, tid, nt);
+  const int H = a.H, W = a.W, h = a.h, w = a.w;
+  const int HW = H * W;
+  // Loads that depend on nothing computed here are issued first, so that they share one memory
+  // round with the heads' inputs instead of each costing its own after a barrier: the source
+  // pose and intrinsics (into LDS behind the heads, fused path) and the 4 full-resolution points
+  // of this thread's first ↓8 pixel (the ↓8 blocks).
+  const bool fused = hs && a.hx && !a.given;
+  float pre = 0.f;
+  if (fused) {
+    if (tid < 9)
+      pre = a.Rsrc[9 * n + tid];
+    else if (tid < 12)
+      pre = a.tsrc[3 * n + tid - 9];
+    else if (tid < 21)
+      pre = a.K[9 * n + tid - 12];
+  }
+  const int q0 = (bx - a.bf) * nt + tid;
+  const bool lowres = bx >= a.bf;
+  floatx4 p0[4];
+  if (lowres && q0 < h * w) {
+    const Lin ly = lin_src(q0 / w, H, h), lx = lin_src(q0 % w, W, w);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cy = (k >> 1) ? ly.i1 : ly.i0, cx = (k & 1) ? lx.i1 : lx.i0;
+      p0[k] = a.pts[(size_t)n * HW + (size_t)cy * W + cx];
+    }
+  }
+  if (fused) {
+    pose_heads(a, hs, n, tid, nt);
+    if (tid < 21) hs[80 + tid] = pre;  // R[9] t[3] K[9]
+    __syncthreads();
+  }
   if (a.given) {  // the pose of this iteration was updated by the ↓8 part: 21 plain loads
     if (tid < 9)
       sh[tid] = a.Rsrc[9 * n + tid];
@@ -266,17 +300,18 @@ __device__ __forceinline__ void pose_step_body(const PoseStepArgs& a, float* sh,
         dt[k] = fresh ? __hip_atomic_load(a.dtv + 3 * n + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                       : a.dtv[3 * n + k];
     }
-    pose_update_one(d, dt, a.Rsrc + 9 * n, a.tsrc + 3 * n, sh, sh + 9, a.weight, a.depth_transform);
+    if (fused)
+      pose_update_one(d, dt, hs + 80, hs + 89, sh, sh + 9, a.weight, a.depth_transform);
+    else
+      pose_update_one(d, dt, a.Rsrc + 9 * n, a.tsrc + 3 * n, sh, sh + 9, a.weight, a.depth_transform);
     if (bx == 0) {
       for (int k = 0; k < 9; ++k) a.Rout[9 * n + k] = sh[k];
       for (int k = 0; k < 3; ++k) a.tout[3 * n + k] = sh[9 + k];
     }
-    for (int k = 0; k < 9; ++k) sh[12 + k] = a.K[9 * n + k];
+    for (int k = 0; k < 9; ++k) sh[12 + k] = fused ? hs[92 + k] : a.K[9 * n + k];
   }
   __syncthreads();
-  const int H = a.H, W = a.W, h = a.h, w = a.w;
-  const int HW = H * W;
-  if (bx < a.bf) {
+  if (!lowres) {
     for (int p = bx * nt + tid; p < HW; p += a.bf * nt) {
       const int X = p % W, Y = p / W;
       float fx, fy;
@@ -306,13 +341,14 @@ __device__ __forceinline__ void pose_step_body(const PoseStepArgs& a, float* sh,
     }
     return;
   }
-  for (int q = (bx - a.bf) * nt + tid; q < h * w; q += a.bl * nt) {
+  for (int q = q0; q < h * w; q += a.bl * nt) {
     const int x = q % w, y = q / w;
     const Lin ly = lin_src(y, H, h), lx = lin_src(x, W, w);
     float f[4][2];  // [dy·2 + dx][axis]
     for (int k = 0; k < 4; ++k) {
       const int cy = (k >> 1) ? ly.i1 : ly.i0, cx = (k & 1) ? lx.i1 : lx.i0;
-      proj_flow(sh, a.pts[(size_t)n * HW + (size_t)cy * W + cx], cx, cy, a.invalid, f[k][0], f[k][1]);
+      const floatx4 P = q == q0 ? p0[k] : a.pts[(size_t)n * HW + (size_t)cy * W + cx];
+      proj_flow(sh, P, cx, cy, a.invalid, f[k][0], f[k][1]);
     }
     const size_t idx = (size_t)n * h * w + q;
     for (int c = 0; c < 2; ++c) {
