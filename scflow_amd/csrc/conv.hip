@@ -710,7 +710,8 @@ __host__ __device__ constexpr int thinf_ld(int cin) { return cin + 4; }  // pixe
 
 template <int COUT, int KH, int KW>
 __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow_conv_args a,
-                                                                          int oh, int ow) {
+                                                                          int oh, int ow,
+                                                                          unsigned long long* stamps) {
   // [(tr+KH-1)·(ow+KW-1)][cin + 4], reused for the partials; float4-typed: ds_*_b128 halo
   // accesses (see conv_thin_kernel)
   extern __shared__ floatx4 thinf_smem4[];
@@ -732,6 +733,20 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
   const int oy0 = (bid % tiles_per_img) * tr;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  sc_stamp(stamps, 0);
+  // the packed weights [o][tap][ci] go to LDS behind the halo, loaded in the same round (the
+  // contraction then reads them as wave-uniform ds_read_b128 broadcasts: as scalar loads inside
+  // the channel loop each tap's pair of s_load waited out its own L2 round trip — 10 of the
+  // launch's 17 µs at B = 16)
+  const int nw4 = KH * KW * cin * COUT / 4;
+  floatx4* wl4 = thinf_smem4 + (size_t)(tr + KH - 1) * hcols * (ld / 4);
+  constexpr int NWL = 2;  // float4 of weights per thread (≤ 2048: 3×3 × 256 × 2 = 1152)
+  floatx4 wv[NWL];
+#pragma unroll
+  for (int j = 0; j < NWL; ++j) {
+    const int idx = tid + THINF_WAVES * 64 * j;
+    if (idx < nw4) wv[j] = ((const floatx4*)a.weight)[idx];
+  }
   // every load first, then every LDS store (at most 9 float4 per thread at 4 × 34 × 256)
   constexpr int NL = 12;
   floatx4 v[NL];
@@ -752,18 +767,25 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
     const int idx = tid + THINF_WAVES * 64 * j;
     if (idx < nh) thinf_smem4[(idx / q4) * (ld / 4) + idx % q4] = v[j];
   }
+#pragma unroll
+  for (int j = 0; j < NWL; ++j) {
+    const int idx = tid + THINF_WAVES * 64 * j;
+    if (idx < nw4) wl4[idx] = wv[j];
+  }
   __syncthreads();
+  sc_stamp(stamps, 1);
   const int py = lane / ow, px = lane % ow;
   const int cw = cin / THINF_WAVES;  // channels of this wave (a multiple of 4)
   const int c0 = wave * cw;
   float acc[COUT];
 #pragma unroll
   for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
-  // packed weights [o][tap][ci]: wave-uniform addresses → scalar loads
+  // weights [o][tap][ci] in LDS: wave-uniform addresses → broadcast reads
+  const float* wls = (const float*)wl4;
   for (int ty = 0; ty < KH; ++ty)
     for (int tx = 0; tx < KW; ++tx) {
       const floatx4* hp = thinf_smem4 + ((py + ty) * hcols + px + tx) * (ld / 4) + c0 / 4;
-      const float* wp = a.weight + (size_t)(ty * KW + tx) * cin + c0;
+      const float* wp = wls + (size_t)(ty * KW + tx) * cin + c0;
 #ifdef THINF_UNROLL  // channel-chunk loop unroll of the contraction (tuning build flag)
 #pragma unroll THINF_UNROLL
 #endif
@@ -771,12 +793,13 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
         const floatx4 x = hp[c / 4];
 #pragma unroll
         for (int o = 0; o < COUT; ++o) {
-          const float* w = wp + (size_t)o * KH * KW * cin + c;
+          const floatx4 w = *(const floatx4*)(wp + (size_t)o * KH * KW * cin + c);
           acc[o] += x[0] * w[0] + x[1] * w[1] + x[2] * w[2] + x[3] * w[3];
         }
       }
     }
   __syncthreads();
+  sc_stamp(stamps, 2);
 #pragma unroll
   for (int o = 0; o < COUT; ++o) halo[(wave * COUT + o) * 64 + lane] = acc[o];
   __syncthreads();
@@ -789,6 +812,10 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
       const float b = a.bias ? a.bias[o] : 0.f;
       a.out[pix * a.so + o] = act_apply(r + b, a.act);
     }
+  }
+  if (stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    sc_stamp(stamps, 3);
   }
 }
 
@@ -1457,7 +1484,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
   if (tiled && !thin_full_off && a.c1 == 0 && a.c0 % (4 * THINF_WAVES) == 0) {
     const int tr = 64 / g.ow;
     const unsigned blocks = (unsigned)(a.n * (g.oh / tr));
-#define SCFLOW_THINF(CO, KH_, KW_)                                                                if (a.cout == CO && a.kh == KH_ && a.kw == KW_) {                                                 const size_t nh4 = (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * (a.c0 / 4);                      size_t lds = sizeof(float) * (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * thinf_ld(a.c0);        if (lds < sizeof(float) * THINF_WAVES * CO * 64) lds = sizeof(float) * THINF_WAVES * CO * 64;     if (lds <= 160 * 1024 && nh4 <= (size_t)12 * THINF_WAVES * 64) {                                  static bool attr = false;                                                                       if (!attr) {                                                                                      (void)hipFuncSetAttribute((const void*)conv_thin_full_kernel<CO, KH_, KW_>,                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              attr = true;                                                                                  }                                                                                               conv_thin_full_kernel<CO, KH_, KW_><<<blocks, THINF_WAVES * 64, lds, st>>>(a, g.oh, g.ow);       return scflow_launch_status();                                                                }                                                                                             }
+#define SCFLOW_THINF(CO, KH_, KW_)                                                                if (a.cout == CO && a.kh == KH_ && a.kw == KW_) {                                                 const size_t nh4 = (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * (a.c0 / 4);                      size_t lds = sizeof(float) * (size_t)(tr + KH_ - 1) * (g.ow + KW_ - 1) * thinf_ld(a.c0);        if (lds < sizeof(float) * THINF_WAVES * CO * 64) lds = sizeof(float) * THINF_WAVES * CO * 64;     const size_t nw4 = (size_t)KH_ * KW_ * a.c0 * CO / 4;                                           lds += 16 * nw4; /* the weights behind the halo */                                             if (lds <= 160 * 1024 && nh4 <= (size_t)12 * THINF_WAVES * 64 && nw4 <= (size_t)2 * THINF_WAVES * 64 && aligned16(a.weight)) {                                  static bool attr = false;                                                                       if (!attr) {                                                                                      (void)hipFuncSetAttribute((const void*)conv_thin_full_kernel<CO, KH_, KW_>,                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              attr = true;                                                                                  }                                                                                               conv_thin_full_kernel<CO, KH_, KW_><<<blocks, THINF_WAVES * 64, lds, st>>>(a, g.oh, g.ow, g_wino_stamps);       return scflow_launch_status();                                                                }                                                                                             }
     // (1×1: the chunked kernel below is faster — its 32-channel chunks need no halo)
     SCFLOW_THINF(1, 3, 3)
     SCFLOW_THINF(2, 3, 3)
