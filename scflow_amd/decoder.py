@@ -125,6 +125,14 @@ class SCFlowDecoder(nn.Module):
         # correlation pyramid in the tiled layout (4×4 tiles of 16 floats per map, pooling fused
         # into the GEMM epilogue; ops.corr_pyramid_tiled) when the geometry allows it
         self.tiled_pyramid = True
+        # 0: every stream at the default priority; 1: the forward's critical stream is a
+        # high-priority stream of the decoder's own (the side branches at the default), so the
+        # CP dispatches its workgroups first when both queues hold work; 2: the side branches'
+        # stream at high priority instead; -1 (default): 1 for feature maps above 32×32, else 0.
+        # Measured (round 5, tools/sess_r5ag.sh, in-process A/B): configs[4] 44.64 / 44.90 /
+        # 44.99 ms per forward for 1 / 0 / 2; configs[1] 4.926 / 4.841 / 4.909 ms — at 32² the
+        # side branches are nearly as long as the critical ones and must not be held back
+        self.main_priority = -1
         self._hooks_on = True
         self.hook_batch = 0
 
@@ -164,9 +172,12 @@ class SCFlowDecoder(nn.Module):
         ss = getattr(self, "_streams", None)
         if ss is None:
             ss = self._streams = {}
-        if (dev, slot) not in ss:
-            ss[(dev, slot)] = torch.cuda.Stream(device=dev)
-        return ss[(dev, slot)]
+        # "priority" (main_priority 1) and the side branches under main_priority 2: the highest
+        # priority the device allows (a lower number is a higher priority)
+        prio = -8 if slot == "priority" or (self.main_priority == 2 and slot in (0, 1)) else 0
+        if (dev, slot, prio) not in ss:
+            ss[(dev, slot, prio)] = torch.cuda.Stream(device=dev, priority=prio)
+        return ss[(dev, slot, prio)]
 
     def _hook(self, name: str, start: bool) -> None:
         if not self._hooks_on:
@@ -212,6 +223,24 @@ class SCFlowDecoder(nn.Module):
         if self.pingpong and hx is None and N >= 2 * self.pingpong_min:
             return self._forward_pingpong(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K,
                                           label, init_flow, invalid, head_label)
+        mp = self.main_priority
+        if mp < 0:
+            mp = 1 if feat_render.shape[-2] * feat_render.shape[-1] > 32 * 32 else 0
+        if mp == 1:
+            dev = feat_render.device
+            cur = torch.cuda.current_stream(dev)
+            hp = self._side_stream(dev, "priority")
+            hp.wait_stream(cur)  # inputs produced on the caller's stream
+            with torch.cuda.stream(hp):
+                out = self._run_steps(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K,
+                                      label, init_flow, invalid, hx, head_label)
+            cur.wait_stream(hp)
+            return out
+        return self._run_steps(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label,
+                               init_flow, invalid, hx, head_label)
+
+    def _run_steps(self, feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label,
+                   init_flow, invalid, hx, head_label):
         gen = self._forward_steps(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label,
                                   init_flow, invalid, hx=hx, head_label=head_label)
         while True:
