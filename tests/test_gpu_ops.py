@@ -210,6 +210,8 @@ def _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=0, bk=None):
     (2, 32, 32, 1, 0, 64, 3, 1, "ReLU"),           # small-cin 3×3, 1 channel
     (2, 32, 32, 256, 0, 2, 3, 1, None),            # thin 3×3 → 2
     (2, 32, 32, 256, 0, 1, 1, 0, "Sigmoid"),       # thin 1×1 → 1
+    (1, 64, 64, 256, 0, 2, 3, 1, None),            # thin 3×3 → 2 at the 512² feature size (32-column tiles)
+    (2, 64, 64, 128, 0, 1, 3, 1, "Sigmoid"),       # thin 3×3 → 1, 64-wide
     (16, 32, 32, 324, 0, 256, 1, 0, "ReLU"),       # 1×1 kernel (128-row tiles: corr_net.0 at B=16)
     (13, 32, 32, 196, 60, 320, 1, 0, "Tanh"),      # 1×1 kernel, two sources, 5 channel blocks
     (2, 17, 15, 324, 0, 256, 1, 0, "ReLU"),        # wide 1×1: pixels not a multiple of 64
