@@ -609,8 +609,13 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
   const int hcols = ow + KW - 1;
   const int nh = (tr + KH - 1) * hcols * (THIN_CC / 4);
   const int tiles_per_img = oh / tr;
-  const int img = blockIdx.x / tiles_per_img;
-  const int oy0 = (blockIdx.x % tiles_per_img) * tr;
+  // XCD-aware tile order (as conv_thin_full_kernel): each XCD covers a contiguous run of row
+  // tiles, so the halo rows neighbouring tiles share come from that XCD's L2 — in dispatch order
+  // the three tiles reading an input row sat on three XCDs, each fetching it from the MALL
+  const int bid = gridDim.x % 8 ? (int)blockIdx.x
+                                : (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
+  const int img = bid / tiles_per_img;
+  const int oy0 = (bid % tiles_per_img) * tr;
   const int cin = a.c0 + a.c1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int py = lane / ow, px = lane % ow;
