@@ -113,8 +113,10 @@ long long scflow_corr_lookup_conv1x1_lds_bytes(void);
 /* Profiling only: later LDS-kernel lookups (scflow_corr_lookup*) write 6 u64 real-time-clock
  * stamps per workgroup of 16 query pixels to `stamps` (phase boundaries; NULL turns it off). */
 int scflow_debug_lookup_stamps(void* stamps);
-/* Profiling only: later Winograd conv launches (F(2×2,3×3), F(4,5)) write 4 u64 real-time-clock stamps per
- * workgroup (start, prologue done, main loop done, epilogue done), NULL turns it off. */
+/* Profiling only: later instrumented conv launches (the Winograd F(2×2,3×3), F(4,5) and F(4×4,3×3)
+ * kernels, the small-cin MFMA conv, the whole-halo thin conv, scflow_enc_conv) write 4 u64
+ * real-time-clock stamps per workgroup (start, prologue done, main loop done, epilogue done), NULL
+ * turns it off. */
 int scflow_debug_conv_stamps(void* stamps);
 
 /* Channels-last convolution (cross-correlation, like nn.Conv2d) with fused bias/activation and

@@ -1533,3 +1533,6 @@ SCFLOW_API int scflow_debug_conv_stamps(void* stamps) {
   g_wino_stamps = (unsigned long long*)stamps;
   return SCFLOW_OK;
 }
+
+// the same stamp buffer for the other translation units' instrumented launches (enc_conv_kernel)
+unsigned long long* scflow_debug_stamps_ptr() { return g_wino_stamps; }

@@ -27,6 +27,8 @@
 //    (the next block's identity), float4-vectorised.
 #include "common.h"
 
+unsigned long long* scflow_debug_stamps_ptr();  // conv.hip (scflow_debug_conv_stamps)
+
 namespace {
 
 constexpr int EBN = 64;  // output channels per workgroup
@@ -50,7 +52,16 @@ struct EncParams {
   int oh, ow, tr, tc, hr, hc, nst;  // output size, tile rows × cols, halo rows × cols, K stages
   int nst0;                         // stages of the first source
   int arp4;                         // A halo row pitch (float4; enc_a4, enc_row_pitch)
+  unsigned long long* stamps;       // profiling (scflow_debug_conv_stamps), or NULL
 };
+
+// thread 0's real-time-clock stamp k of this workgroup (0 start, 1 first stage staged, 2 main
+// loop done, 3 epilogue done; grid.z slabs after grid.y)
+__device__ __forceinline__ void enc_stamp(unsigned long long* st, int k) {
+  if (st && threadIdx.x == 0)
+    st[(((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + k] =
+        __builtin_amdgcn_s_memrealtime();
+}
 
 // A halo layout (float4 units): pixel (hr, hcol) at hr·arp4 + 5·hcol (+ one float4 every 2
 // columns for stride 2, so the taps of consecutive output pixels — 2 columns apart — step by an
@@ -157,11 +168,13 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
 
+  enc_stamp(P.stamps, 0);
   gload(s_begin);
   for (int s = s_begin; s < s_end; ++s) {
     __syncthreads();
     lstore();
     __syncthreads();
+    if (s == s_begin) enc_stamp(P.stamps, 1);
     if (s + 1 < s_end) gload(s + 1);
 #pragma unroll
     for (int ty = 0; ty < KH; ++ty) {
@@ -185,6 +198,7 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
     }
   }
 
+  enc_stamp(P.stamps, 2);
   // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
   const int col = n0 + wn * 32 + li;
   if (col >= a.cout) return;
@@ -218,6 +232,10 @@ __global__ __launch_bounds__(256, 2) void enc_conv_kernel(EncParams P) {
       v += resv[rr][r];
       outz[(size_t)pixv[rr][r] * a.s_out + col] = act_apply(v, act);
     }
+  }
+  if (P.stamps) {
+    __builtin_amdgcn_s_waitcnt(0);
+    enc_stamp(P.stamps, 3);
   }
 }
 
@@ -601,6 +619,7 @@ SCFLOW_API int scflow_enc_conv(const scflow_enc_conv_args* args, void* stream) {
     return SCFLOW_EALIGN;
   EncParams p{};
   p.a = a;
+  p.stamps = scflow_debug_stamps_ptr();
   p.oh = (a.h + 2 * a.pad - a.kh) / a.stride + 1;
   p.ow = (a.w + 2 * a.pad - a.kw) / a.stride + 1;
   p.nst0 = a.cin / EBK;
