@@ -132,32 +132,29 @@ __device__ __forceinline__ void ph_conv_body(const PhConvArgs& a, int bx, int by
       for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[c][e], B1[c][e], acc, 0, 0, 0);
     }
   }
-  // deterministic tree reduction of the waves' partial tiles
-  for (int half = NW / 2; half >= 1; half >>= 1) {
-    if (wave >= half && wave < 2 * half) {
+  // deterministic tree reduction of the waves' partial tiles behind ONE barrier: every wave parks
+  // its 16 accumulator values ([wave][value][lane]), then wave w folds value w of all NW waves in
+  // the level-by-level tree's order — (v, v + NW/2), then (v, v + NW/4), … — and stores it (the
+  // same sums as 2·log2(NW) barriers of halving, with the fold spread over the waves)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[((wave - half) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * 33 + li] = acc[r];
-    }
-    __syncthreads();
-    if (wave < half) {
+  for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
+  __syncthreads();
+  for (int r = wave; r < 16; r += NW) {
+    float t[NW];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] += red[(wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * 33 + li];
-    }
-    __syncthreads();
-  }
-  if (wave == 0 && nvalid) {
-    const float b = a.bias ? a.bias[col] : 0.f;
-    float* out = a.out + (size_t)bz * M * a.cout;
+    for (int v = 0; v < NW; ++v) t[v] = red[(v * 16 + r) * 64 + lane];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      if (mm < M) out[(size_t)mm * a.cout + col] = acc[r] + b;
-    }
+    for (int half = NW / 2; half >= 1; half >>= 1)
+#pragma unroll
+      for (int v = 0; v < half; ++v) t[v] = t[v] + t[v + half];
+    const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+    if (nvalid && mm < M)
+      a.out[(size_t)bz * M * a.cout + (size_t)mm * a.cout + col] = t[0] + (a.bias ? a.bias[col] : 0.f);
   }
 }
 
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
-  __shared__ float red[PH_WAVES / 2 * 32 * 33];
+  __shared__ float red[PH_WAVES * 16 * 64];  // 64 KiB: every wave's 16 values per lane
   ph_conv_body<PH_WAVES>(a, blockIdx.x, blockIdx.y, blockIdx.z, red, a.scale, a.shift, 0,
                          a.c0 + a.c1);
 }
@@ -345,49 +342,46 @@ __device__ __forceinline__ void ph_fc_body(const FcArgs& f, int bx, int by, floa
           for (int e = 0; e < 4; ++e)
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[c][e], xv[c][t][e], acc[t], 0, 0, 0);
     }
-    for (int half = NW / 2; half >= 1; half >>= 1) {
-      if (wave >= half && wave < 2 * half) {
+    // the waves' partials folded behind ONE barrier (as ph_conv_body): every wave parks its
+    // FC_RT·4 values, wave i folds value i of all NW waves in the halving tree's order and
+    // stores it
+    constexpr int NV = FC_RT * 4;
 #pragma unroll
-        for (int t = 0; t < FC_RT; ++t)
+    for (int t = 0; t < FC_RT; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) red[(((wave - half) * FC_RT + t) * 64 + lane) * 5 + r] = acc[t][r];
-      }
-      __syncthreads();
-      if (wave < half) {
+      for (int r = 0; r < 4; ++r) red[(wave * NV + 4 * t + r) * 64 + lane] = acc[t][r];
+    __syncthreads();
+    for (int iv = wave; iv < NV; iv += NW) {
+      float u[NW];
 #pragma unroll
-        for (int t = 0; t < FC_RT; ++t)
+      for (int v = 0; v < NW; ++v) u[v] = red[(v * NV + iv) * 64 + lane];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[t][r] += red[((wave * FC_RT + t) * 64 + lane) * 5 + r];
-      }
-      __syncthreads();
-    }
-    if (wave == 0) {
+      for (int half = NW / 2; half >= 1; half >>= 1)
+#pragma unroll
+        for (int v = 0; v < half; ++v) u[v] = u[v] + u[v + half];
       // C/D layout (16x16): col = lane&15 (batch row), row = 4(lane>>4) + r (neuron)
-#pragma unroll
-      for (int t = 0; t < FC_RT; ++t) {
-        const int row = r0 + t * 16 + li;
-        if (row >= f.m) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = i0 + 4 * kq + r;
-          float v = acc[t][r];
-          if (f.label) {
-            long long cls = f.label[0];
-            if (cls < 0 || cls >= f.num_class) cls = 0;
-            if (i < f.rch)
-              f.y[(size_t)row * f.rch + i] = v + f.bias[cls * f.rch + i];
-            else if (i < f.rch + 3)
-              f.dt[(size_t)row * 3 + (i - f.rch)] = v + f.bt[cls * 3 + (i - f.rch)];
-          } else if (i < f.n) {
-            if (f.ksplit <= 1) {
-              v += f.bias ? f.bias[i] : 0.f;
-              if (f.relu) v = fmaxf(v, 0.f);
-            }
-            yout[(size_t)row * f.n + i] = v;
+      const int t = iv >> 2, r = iv & 3;
+      const int row = r0 + t * 16 + li;
+      const int i = i0 + 4 * kq + r;
+      float v = u[0];
+      if (row < f.m) {
+        if (f.label) {
+          long long cls = f.label[0];
+          if (cls < 0 || cls >= f.num_class) cls = 0;
+          if (i < f.rch)
+            f.y[(size_t)row * f.rch + i] = v + f.bias[cls * f.rch + i];
+          else if (i < f.rch + 3)
+            f.dt[(size_t)row * 3 + (i - f.rch)] = v + f.bt[cls * 3 + (i - f.rch)];
+        } else if (i < f.n) {
+          if (f.ksplit <= 1) {
+            v += f.bias ? f.bias[i] : 0.f;
+            if (f.relu) v = fmaxf(v, 0.f);
           }
+          yout[(size_t)row * f.n + i] = v;
         }
       }
     }
+    if (r0 + 16 * FC_RT < f.m) __syncthreads();  // the next row block re-parks
   }
 }
 
@@ -404,7 +398,7 @@ __global__ __launch_bounds__(256) void ph_heads_kernel(PoseStepArgs a) {
 
 template <int FC_RT>
 __global__ __launch_bounds__(PH_WAVES * 64) void ph_fc_kernel(FcArgs f) {
-  __shared__ float red[PH_WAVES / 2 * FC_RT * 64 * 5];
+  __shared__ float red[PH_WAVES * FC_RT * 4 * 64];
   ph_fc_body<PH_WAVES, FC_RT>(f, blockIdx.x, blockIdx.y, red, f.scale, f.shift);
 }
 
