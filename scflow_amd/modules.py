@@ -580,6 +580,7 @@ class MultiClassPoseHead(nn.Module):
     # 5.240 ms/forward for 256 → 8, median of 9)
     conv_wg_target = 512
     gather_wg_target = 128
+    fc_ksplit = 4  # K slices of the split FCs (workgroups = ⌈out/16⌉ · fc_ksplit)
     _conv_feat_channels = {"Basic": [128, 128, 128], "Large": [128, 128, 128]}
     _conv_strides = {"Basic": [2, 2, 2], "Large": [2, 2, 2]}
     _conv_paddings = {"Basic": [1, 1, 1], "Large": [1, 1, 1]}
@@ -756,7 +757,7 @@ class MultiClassPoseHead(nn.Module):
                               y, lin.out_features, True)
                 x = y
             return x
-        ks, xsplit, xbias, ldx = 4, 0, None, k_in
+        ks, xsplit, xbias, ldx = self.fc_ksplit, 0, None, k_in
         for i, fc in enumerate(self.fc_layers):
             lin = fc[0]
             y = empty(ks, n, lin.out_features)
