@@ -60,6 +60,16 @@ __global__ __launch_bounds__(256, 1) void conv1x1w_kernel(scflow_conv_args a) {
   const long long m0 = (long long)blockIdx.x * W1_PX;
   const int npad = (a.cout + 63) / 64 * 64;
   const bool wave_on = wave * 64 < npad;  // waves beyond the padded channels only load A
+  // the lane's two output channels' bias, fetched now (in the one-round grid every workgroup
+  // reaches the epilogue together, where these loads waited on the same cache lines)
+  float bias_v[2] = {0.f, 0.f};
+  if (wave_on && a.bias) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int col = 64 * wave + 32 * nb + (lane & 31);
+      if (col < a.cout) bias_v[nb] = a.bias[col];
+    }
+  }
 
   // A chunk c = 8-channel blocks [c·CB, min(KB, (c+1)·CB)): thread slot j is (pixel, quad) =
   // (idx / (2·nb), idx % (2·nb)), idx = tid + 256 j
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(256, 1) void conv1x1w_kernel(scflow_conv_args a) {
   for (int nb = 0; nb < 2; ++nb) {
     const int col = 64 * wave + 32 * nb + li;
     if (col >= a.cout) continue;
-    const float bias = a.bias ? a.bias[col] : 0.f;
+    const float bias = bias_v[nb];
     float v[2][16];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)

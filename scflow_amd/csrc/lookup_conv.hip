@@ -82,6 +82,16 @@ __global__ __launch_bounds__(512, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
   const long long m0 = (long long)blockIdx.x * LC_PX;
   const int npad = (a.cout + 63) / 64 * 64;
   const bool wave_on = !producer && wave * 64 < npad;
+  // a consumer lane's two output channels' bias, fetched now: every workgroup of the one-round
+  // grid reaches the epilogue together, where these loads all waited on the same cache lines
+  float bias_v[2] = {0.f, 0.f};
+  if (wave_on && a.bias) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int col = 64 * wave + 32 * nb + li;
+      if (col < a.cout) bias_v[nb] = a.bias[col];
+    }
+  }
 
   // a producer thread's pixel (4 threads of one wave per pixel) and its share of the columns a
   const int pt = producer ? tid - 256 : 0;
@@ -297,18 +307,26 @@ __global__ __launch_bounds__(512, 1) void corr_lookup_conv1x1_kernel(LcArgs a) {
   // epilogue (conv1x1w_kernel's): bias, activation; C/D col = lane&31, row = (r&3) + 8(r>>2) +
   // 4(lane>>5)
   if (!wave_on) return;  // (producers and idle consumer waves)
+  auto store = [&](auto actc) __attribute__((always_inline)) {  // one body per activation
+    constexpr int ACT = decltype(actc)::value;
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
-    const int col = 64 * wave + 32 * nb + li;
-    if (col >= a.cout) continue;
-    const float bias = a.bias ? a.bias[col] : 0.f;
+    for (int nb = 0; nb < 2; ++nb) {
+      const int col = 64 * wave + 32 * nb + li;
+      if (col >= a.cout) continue;
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
+      for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long long m = m0 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (m < M) a.out[m * a.so + col] = act_apply(acc[mb][nb][r] + bias, a.act);
-      }
+        for (int r = 0; r < 16; ++r) {
+          const long long m = m0 + 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (m < M) a.out[m * a.so + col] = act_apply(acc[mb][nb][r] + bias_v[nb], ACT);
+        }
+    }
+  };
+  switch (a.act) {
+    case SCFLOW_ACT_RELU: store(std::integral_constant<int, SCFLOW_ACT_RELU>{}); break;
+    case SCFLOW_ACT_SIGMOID: store(std::integral_constant<int, SCFLOW_ACT_SIGMOID>{}); break;
+    case SCFLOW_ACT_TANH: store(std::integral_constant<int, SCFLOW_ACT_TANH>{}); break;
+    default: store(std::integral_constant<int, SCFLOW_ACT_NONE>{}); break;
   }
 }
 
