@@ -316,7 +316,8 @@ def bench_train(args, world, rank, dev, feat):
     el = time_steps(one, args.train_steps, 3, world, dev)
     gc.unfreeze()
     torch.cuda.synchronize()
-    per = sorted(a.elapsed_time(b) for a, b in evs[3:])  # the timed steps
+    per_o = [a.elapsed_time(b) for a, b in evs[3:]]  # the timed steps, in order
+    per = sorted(per_o)
     nparam = sum(p.numel() for p in step.grads.params)
     gb = world * args.train_batch
     which = ("BASELINE configs[3]" if (world, args.train_batch, args.size, args.iters) == (8, 16, 256, 8)
@@ -328,7 +329,13 @@ def bench_train(args, world, rank, dev, feat):
            "value": round(gb * args.iters * args.train_steps / el, 2),
            "unit": "iters/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
            "per_step_ms": {"median": round(per[len(per) // 2], 3), "min": round(per[0], 3),
-                           "max": round(per[-1], 3), "spread": round((per[-1] - per[0]) / per[len(per) // 2], 4)},
+                           "max": round(per[-1], 3), "spread": round((per[-1] - per[0]) / per[len(per) // 2], 4),
+                           # the first timed step starts on an idle GPU behind the barrier (its
+                           # span includes the host filling the queue): spread without it too
+                           "spread_after_first": round((max(per_o[1:]) - min(per_o[1:])) /
+                                                       sorted(per_o[1:])[len(per_o[1:]) // 2], 4)
+                           if len(per_o) > 2 else None,
+                           "in_order": [round(x, 2) for x in per_o]},
            "steps": args.train_steps, "warmup": 3, "global_batch": gb, "n_gpus": world,
            "allreduce_bytes": 4 * nparam if world > 1 else 0,
            "buckets": len(step.grads.buckets),
