@@ -161,13 +161,14 @@ __global__ __launch_bounds__(PH_WAVES * 64) void ph_conv_kernel(PhConvArgs a) {
 
 // GroupNorm statistics of x [n][hw][c] → per-channel scale/shift for y = relu(x·scale + shift),
 // optionally first summing nsplit K-split partial slabs (x + z·split_stride) and writing the sum
-// to y.  Grid (n, c/32): a workgroup takes one sample's 32-channel block; thread t holds channel
-// quad t%8 of pixel slot t/8 (32 slots), float4 loads; per-channel sums in fp64 reduced over the
-// slots in a fixed order, then per group (c/groups channels) → mean, biased variance.
+// to y.  Grid (n, c/CB): a workgroup takes one sample's CB-channel block; thread t holds channel
+// quad t%(CB/4) of pixel slot t/(CB/4) (256·4/CB slots), float4 loads; per-channel sums in fp64
+// reduced over the slots in a fixed order (CB = 16: first 16 parts of 4 slots each, all threads),
+// then per group (c/groups channels) → mean, biased variance.
 // NS > 0: compile-time slab count; the pixel loop is unrolled PU-fold with every load of a
-// round issued before any add (this kernel is latency-bound: 64 workgroups at B = 16; at the
-// pose head's first conv every slot's 8 pixels × 4 slabs are one round)
-template <int NS>
+// round issued before any add (this kernel is latency-bound: 64 workgroups at B = 16 with CB =
+// 32, 128 with CB = 16; at the pose head's first conv every slot's pixels × 4 slabs are one round)
+template <int NS, int CB>
 __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restrict__ x, int nsplit,
                                                            long long split_stride, float* __restrict__ y,
                                                            int hw, int c, int groups,
@@ -175,10 +176,11 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
                                                            const float* __restrict__ beta, float eps,
                                                            float* __restrict__ scale,
                                                            float* __restrict__ shift) {
-  __shared__ double s1[32][33], s2[32][33];
-  __shared__ double gmean[32], grstd[32];
-  const int img = blockIdx.x, cb = blockIdx.y * 32;
-  const int q = threadIdx.x & 7, slot = threadIdx.x >> 3;
+  constexpr int NQ = CB / 4, SL = 256 / NQ;  // channel quads, pixel slots
+  __shared__ double s1[SL][CB + 1], s2[SL][CB + 1];
+  __shared__ double gmean[CB], grstd[CB];
+  const int img = blockIdx.x, cb = blockIdx.y * CB;
+  const int q = threadIdx.x % NQ, slot = threadIdx.x / NQ;
   double a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
   auto acc = [&](floatx4 v, size_t off) {
     if (y) *(floatx4*)(y + off) = v;
@@ -190,24 +192,24 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
   };
   int p = slot;
   if constexpr (NS > 0) {
-    constexpr int PU = NS <= 4 ? 8 : 1;  // ≤ 32 float4 loads in flight
-    for (; p + 32 * (PU - 1) < hw; p += 32 * PU) {
+    constexpr int PU = NS <= 4 ? 8 * 32 / SL : 1;  // ≤ 32 float4 loads in flight
+    for (; p + SL * (PU - 1) < hw; p += SL * PU) {
       floatx4 v[PU][NS];
 #pragma unroll
       for (int u = 0; u < PU; ++u)
 #pragma unroll
         for (int z = 0; z < NS; ++z)
-          v[u][z] = *(const floatx4*)(x + (size_t)z * split_stride + ((size_t)img * hw + p + 32 * u) * c +
+          v[u][z] = *(const floatx4*)(x + (size_t)z * split_stride + ((size_t)img * hw + p + SL * u) * c +
                                       cb + 4 * q);
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
 #pragma unroll
         for (int z = 1; z < NS; ++z) v[u][0] += v[u][z];
-        acc(v[u][0], ((size_t)img * hw + p + 32 * u) * c + cb + 4 * q);
+        acc(v[u][0], ((size_t)img * hw + p + SL * u) * c + cb + 4 * q);
       }
     }
   }
-  for (; p < hw; p += 32) {
+  for (; p < hw; p += SL) {
     const size_t off = ((size_t)img * hw + p) * c + cb + 4 * q;
     floatx4 v = *(const floatx4*)(x + off);
     if constexpr (NS > 0) {
@@ -231,12 +233,28 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
     s2[slot][4 * q + e] = b[e];
   }
   __syncthreads();
-  const int cpg = c / groups;       // channels per group (divides 32)
-  const int ng = 32 / cpg;          // groups in this block
+  const int cpg = c / groups;       // channels per group (divides CB)
+  const int ng = CB / cpg;          // groups in this block
+  int nsl = SL;                     // slot rows left to fold
+  if constexpr (CB == 16) {
+    // 16 parts × 16 channels: thread t folds slots 4·(t/16) .. +3 of channel t%16 into row t/16
+    const int ch = threadIdx.x % CB, part = threadIdx.x / CB;
+    double A = 0, B = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      A += s1[4 * part + k][ch];
+      B += s2[4 * part + k][ch];
+    }
+    __syncthreads();
+    s1[part][ch] = A;
+    s2[part][ch] = B;
+    __syncthreads();
+    nsl = 16;
+  }
   if (threadIdx.x < ng) {
     double A = 0, B = 0;
     for (int k = 0; k < cpg; ++k)
-      for (int sl = 0; sl < 32; ++sl) {
+      for (int sl = 0; sl < nsl; ++sl) {
         A += s1[sl][threadIdx.x * cpg + k];
         B += s2[sl][threadIdx.x * cpg + k];
       }
@@ -248,7 +266,7 @@ __global__ __launch_bounds__(256) void ph_gn_reduce_kernel(const float* __restri
     grstd[threadIdx.x] = 1.0 / sqrt(var + (double)eps);
   }
   __syncthreads();
-  if (threadIdx.x < 32) {
+  if (threadIdx.x < CB) {
     const int ch = cb + threadIdx.x, g = threadIdx.x / cpg;
     const float sc = gamma[ch] * (float)grstd[g];
     scale[(size_t)img * c + ch] = sc;
@@ -498,11 +516,23 @@ SCFLOW_API int scflow_ph_gn_reduce(const float* parts, int nsplit, long long spl
   const int cpg = c / groups;
   if (c % 32 || 32 % cpg) return SCFLOW_EUNSUPPORTED;
   if (!aligned16(parts) || (y && !aligned16(y)) || (split_stride & 3)) return SCFLOW_EALIGN;
-  dim3 grid(n, c / 32);
-#define SCFLOW_GNR(NS_)                                                                           \
-  ph_gn_reduce_kernel<NS_><<<grid, 256, 0, (hipStream_t)stream>>>(parts, nsplit, split_stride, y, hw, \
-                                                                  c, groups, gamma, beta, eps,       \
-                                                                  scale, shift)
+  // 16-channel blocks (twice the workgroups) when the group size allows; SCFLOW_GNR_CB=32 forces
+  // the 32-channel blocks (A/B)
+  const char* cbs = getenv("SCFLOW_GNR_CB");  // read per launch (in-process A/B)
+  const int cbe = cbs ? atoi(cbs) : 16;
+  const bool c16 = cbe == 16 && 16 % cpg == 0;
+  dim3 grid(n, c / (c16 ? 16 : 32));
+#define SCFLOW_GNR(NS_)                                                                                    \
+  do {                                                                                                     \
+    if (c16)                                                                                               \
+      ph_gn_reduce_kernel<NS_, 16><<<grid, 256, 0, (hipStream_t)stream>>>(parts, nsplit, split_stride, y, hw, \
+                                                                          c, groups, gamma, beta, eps,       \
+                                                                          scale, shift);                     \
+    else                                                                                                   \
+      ph_gn_reduce_kernel<NS_, 32><<<grid, 256, 0, (hipStream_t)stream>>>(parts, nsplit, split_stride, y, hw, \
+                                                                          c, groups, gamma, beta, eps,       \
+                                                                          scale, shift);                     \
+  } while (0)
   switch (nsplit) {
     case 1: SCFLOW_GNR(1); break;
     case 2: SCFLOW_GNR(2); break;
