@@ -78,6 +78,28 @@ __device__ __forceinline__ floatx4 sub4(floatx4 a, floatx4 b) {
 }
 #endif
 
+// Progress-keyed wave priority (WINO_PRIO): a one-round grid puts two workgroups on a CU, and
+// the SQ's oldest-first issue lets the first-dispatched one finish its main loop well before the
+// second (workgroup stamps, round 5), which then runs alone at one wave per SIMD.  Each wave sets
+// its issue priority from its own progress — 3 in the first quarter of the stages down to 0 in
+// the last — so the workgroup that is behind wins the arbitration and the two finish together.
+#ifndef WINO_PRIO
+#define WINO_PRIO 1
+#endif
+__device__ __forceinline__ void wino_prio(int s, int nst) {
+#if WINO_PRIO
+  const int pr = 3 - (4 * s) / nst;  // wave-uniform
+  if (pr >= 3)
+    __builtin_amdgcn_s_setprio(3);
+  else if (pr == 2)
+    __builtin_amdgcn_s_setprio(2);
+  else if (pr == 1)
+    __builtin_amdgcn_s_setprio(1);
+  else
+    __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 #ifndef WINO_SCHED_BARRIER
 #define WINO_SCHED_BARRIER 1
 #endif

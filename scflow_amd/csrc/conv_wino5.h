@@ -244,6 +244,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     vload(0, 0, 1, d, w3);
     vmath(d, vA[1], w3);
     for (int s = 0; s < nst; ++s) {
+      wino_prio(s, nst);
       const int buf = s & 1;
       const int t0 = s * W5NSUB;
       hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
@@ -270,6 +271,9 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     mainloop(std::true_type{});
   else
     mainloop(std::false_type{});
+#if WINO_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 
 #ifdef WX_NO_EPI
   {
