@@ -110,6 +110,18 @@ int scflow_corr_lookup_conv1x1(const float* pyr, const float* flow, const float*
                                int num_levels, int radius, int cout, int act, int align_corners,
                                void* stream);
 long long scflow_corr_lookup_conv1x1_lds_bytes(void);
+/* ABI markers: scflow_abi_version() returns SCFLOW_ABI_VERSION of the header the library was
+ * built from (2: scflow_conv_args ends with the F(4×4,3×3) workspace fields ws / ws_bytes, and
+ * scflow_conv_pick_bk may return SCFLOW_CONV_WINO4); scflow_conv_args_size() its
+ * sizeof(scflow_conv_args).  A binding checks both before its first call (scflow_amd/_lib.py
+ * does, at load). */
+#define SCFLOW_ABI_VERSION 2
+int scflow_abi_version(void);
+long long scflow_conv_args_size(void);
+/* Tuning only: launch-time environment switches (SCFLOW_WINO4_DEPTH, SCFLOW_GNR_CB,
+ * SCFLOW_SMALLCIN_SPLIT, SCFLOW_SMALLCIN_WGS) are read once and cached; this makes their next
+ * use re-read the environment (in-process A/B). */
+int scflow_debug_reload_switches(void);
 /* Profiling only: later LDS-kernel lookups (scflow_corr_lookup*) write 6 u64 real-time-clock
  * stamps per workgroup of 16 query pixels to `stamps` (phase boundaries; NULL turns it off). */
 int scflow_debug_lookup_stamps(void* stamps);

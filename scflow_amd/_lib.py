@@ -23,6 +23,7 @@ CONV_WINO = 2  # scflow_conv_args.bk: Winograd F(2x2,3x3) packing/kernel (SCFLOW
 CONV_1X1W = 3  # scflow_conv_args.bk: wide 1x1 packing/kernel (SCFLOW_CONV_1X1W)
 CONV_WINO4 = 4  # scflow_conv_args.bk: Winograd F(4x4,3x3) packing/kernel (SCFLOW_CONV_WINO4)
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
+ABI_VERSION = 2  # SCFLOW_ABI_VERSION of include/scflow_hip.h this binding mirrors
 
 
 class ConvArgs(ctypes.Structure):
@@ -126,6 +127,9 @@ SIGNATURES = {
                                    c_vp, c_vp, c_ll, c_int, c_int, c_int, c_int, c_vp]),
     "scflow_debug_lookup_stamps": (c_int, [c_vp]),
     "scflow_debug_conv_stamps": (c_int, [c_vp]),
+    "scflow_debug_reload_switches": (c_int, []),
+    "scflow_abi_version": (c_int, []),
+    "scflow_conv_args_size": (c_ll, []),
     "scflow_conv_packed_size": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     "scflow_conv_packed_size_bk": (c_ll, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
     "scflow_conv_pack_weights": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -263,8 +267,19 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        ver, size = lib.scflow_abi_version(), lib.scflow_conv_args_size()
+        if ver != ABI_VERSION or size != ctypes.sizeof(ConvArgs):
+            raise ScflowError(f"{path}: ABI version {ver} / sizeof(scflow_conv_args) {size}, this "
+                              f"binding expects {ABI_VERSION} / {ctypes.sizeof(ConvArgs)}: rebuild "
+                              "the library (python -m scflow_amd.build)")
         _lib = lib
     return _lib
+
+
+def reload_switches() -> None:
+    """Make the library re-read its cached launch-time switches (SCFLOW_WINO4_DEPTH,
+    SCFLOW_GNR_CB, SCFLOW_SMALLCIN_SPLIT, SCFLOW_SMALLCIN_WGS) after os.environ changed."""
+    check(load().scflow_debug_reload_switches(), "scflow_debug_reload_switches")
 
 
 def check(code: int, what: str) -> None:

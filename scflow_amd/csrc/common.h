@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "../../include/scflow_hip.h"
@@ -50,6 +52,27 @@ static inline int device_cus() {
   }
   return cus;
 }
+
+// Environment switch for A/B runs of a launch-time choice: read on first use and cached (these
+// sit on launch-bound paths — the decoder's recorded launches replay every iteration), re-read
+// after scflow_debug_reload_switches() bumps the generation (in-process A/B).
+extern std::atomic<int> g_switch_gen;
+struct EnvSwitch {
+  const char* name;
+  int dflt;
+  std::atomic<int> gen{-1};
+  std::atomic<int> val{0};
+  EnvSwitch(const char* n, int d) : name(n), dflt(d) {}
+  int get() {
+    const int g = g_switch_gen.load(std::memory_order_relaxed);
+    if (gen.load(std::memory_order_acquire) != g) {
+      const char* e = getenv(name);
+      val.store(e ? atoi(e) : dflt, std::memory_order_relaxed);
+      gen.store(g, std::memory_order_release);
+    }
+    return val.load(std::memory_order_relaxed);
+  }
+};
 
 __device__ __forceinline__ float act_apply(float v, int act) {
   switch (act) {

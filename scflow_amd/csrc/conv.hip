@@ -442,46 +442,64 @@ __device__ __forceinline__ void sc_stamp(unsigned long long* st, int k) {
 // small-cin conv on MFMA: K = taps·cin (≤ 98) walked in k-pairs — one v_mfma_f32_32x32x2_f32
 // per pair (for cin = 2 a pair is the two channels of one tap, for cin = 1 two taps).  Tile =
 // 64 output pixels (64/W whole rows) × npad (64 or 128) channels; 4 waves as 2 (M) × 2 (N), each
-// 32 px × npad/2 channels.  The tile's input halo (rows+kh−1)×(W+kw−1)×cin sits in LDS; the
-// wave's B fragments (its columns' weights for every k) are loaded once into VGPRs from the
-// small-cin packing [taps·cin][npad].
+// 32 px × npad/2 channels.  The wave's B fragments (its columns' weights for every k) are loaded
+// once into VGPRs from the small-cin packing [taps·cin][npad]; the tile's input halo
+// (rows+kh−1)×(W+kw−1)×cin sits in LDS.
+// Round 6: a workgroup walks tiles blockIdx.x, +gridDim.x, … (the grid is capped at a few
+// workgroups per CU, SCFLOW_SMALLCIN_WGS): at 64×64 maps one tile per workgroup meant 2048
+// short-lived workgroups (prologue, 98 MFMAs, epilogue ≈ 11 µs each) dispatched in 4 rounds of
+// 512 — 57 µs alone, 214 µs in the decoder beside other kernels.  Walking tiles, the weights are
+// loaded once per workgroup and the next tile's halo is in flight (registers, then the other LDS
+// buffer) during this tile's MFMAs and stores: one barrier per tile.
 template <int CIN, int KH, int KW, int NBW>
-__global__ __launch_bounds__(256) void conv_smallcin_mfma_kernel(scflow_conv_args a, int oh, int ow,
-                                                                 int npad, unsigned long long* stamps) {
+__global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_args a, int oh, int ow,
+                                                                 int npad, int ntiles,
+                                                                 unsigned long long* stamps) {
   constexpr int K = KH * KW * CIN;
   constexpr int KP = (K + 1) / 2;  // MFMA k-steps
-  extern __shared__ float halo[];  // [(tr+KH-1)][(ow+KW-1)][CIN]
+  extern __shared__ float halo[];  // 2 × [(tr+KH-1)][(ow+KW-1)][CIN]
   const int tr = 64 / ow;
   const int hc = ow + KW - 1, hr = tr + KH - 1;
   const int tiles_per_img = oh / tr;
-  const int img = blockIdx.x / tiles_per_img;
-  const int oy0 = (blockIdx.x % tiles_per_img) * tr;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
   const int cb = blockIdx.y * NBW * 64;  // channel slice of this workgroup (grid.y splits npad)
   sc_stamp(stamps, 0);
-  // every global load in flight at once: the halo's (at most SC_NH per thread: W 32 → (KH+1) ×
-  // (31+KW) · CIN floats, W 64 → KH × (63+KW) · CIN, the only widths dispatched here) and the B
-  // fragments' (k = 2·kp + hh, column = cb + wn·NBW·32 + nb·32 + li), then the halo's LDS stores
-  // — where a strided halo loop paid one load latency per pass before the weights were requested
+  // the halo's global loads (at most SC_NH per thread: W 32 → (KH+1) × (31+KW) · CIN floats,
+  // W 64 → KH × (63+KW) · CIN, the only widths dispatched here) as buffer loads: a padding or
+  // tail element reads offset 0x7ffffff0, beyond the resource, as 0 — no branches, whose waits
+  // would serialise the loads (the dispatch keeps offsets < 2^31)
   constexpr int SC_H32 = (KH + 1) * (31 + KW) * CIN, SC_H64 = KH * (63 + KW) * CIN;
   constexpr int SC_NH = ((SC_H32 > SC_H64 ? SC_H32 : SC_H64) + 255) / 256;
-  // (buffer loads: a padding or tail element reads offset 0x7ffffff0, beyond the resource, as 0
-  // — no branches, whose waits would serialise the loads; the dispatch keeps offsets < 2^31)
   const int nh = hr * hc * CIN;
   const __amdgpu_buffer_rsrc_t hsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.src0), (short)0,
       (int)((((long long)a.n * a.h * a.w - 1) * a.s0 + CIN) * 4), 0x00020000);
   float hv[SC_NH];
+  auto hfetch = [&](int t) __attribute__((always_inline)) {
+    const int img = t / tiles_per_img;
+    const int oy0 = (t - img * tiles_per_img) * tr;
 #pragma unroll
-  for (int j = 0; j < SC_NH; ++j) {
-    const int i = threadIdx.x + 256 * j;
-    const int c = i % CIN, col = (i / CIN) % hc, row = i / (CIN * hc);
-    const int iy = oy0 - a.ph + row, ix = col - a.pw;
-    const bool ok = i < nh && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
-    const int off = ok ? (((img * a.h + iy) * a.w + ix) * a.s0 + c) * 4 : 0x7ffffff0;
-    hv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hsrc, off, 0, 0));
-  }
+    for (int j = 0; j < SC_NH; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      const int c = i % CIN, col = (i / CIN) % hc, row = i / (CIN * hc);
+      const int iy = oy0 - a.ph + row, ix = col - a.pw;
+      const bool ok = i < nh && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+      const int off = ok ? (((img * a.h + iy) * a.w + ix) * a.s0 + c) * 4 : 0x7ffffff0;
+      hv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(hsrc, off, 0, 0));
+    }
+  };
+  auto hput = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < SC_NH; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      if (i < nh) halo[buf * nh + i] = hv[j];
+    }
+  };
+  int t = blockIdx.x;
+  hfetch(t);
+  // B fragments (k = 2·kp + hh, column = cb + wn·NBW·32 + nb·32 + li) and the bias, in flight
+  // together with the first halo
   float bw[NBW][KP], bias_v[NBW];
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb) {
@@ -493,55 +511,61 @@ __global__ __launch_bounds__(256) void conv_smallcin_mfma_kernel(scflow_conv_arg
       bw[nb][kp] = k < K ? a.weight[(size_t)k * npad + cb + (wn * NBW + nb) * 32 + li] : 0.f;
     }
   }
-#pragma unroll
-  for (int j = 0; j < SC_NH; ++j) {
-    const int i = threadIdx.x + 256 * j;
-    if (i < nh) halo[i] = hv[j];
-  }
+  hput(0);
   __syncthreads();
   sc_stamp(stamps, 1);
   const int m = wm * 32 + li;  // this lane's A row (output pixel of the tile)
   const int pbase = ((m / ow) * hc + (m % ow)) * CIN;
-  floatx16 acc[NBW];
-#pragma unroll
-  for (int nb = 0; nb < NBW; ++nb)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[nb][e] = 0.f;
-#pragma unroll
-  for (int kp = 0; kp < KP; ++kp) {
-    const int k = 2 * kp + hh;
-    const int tap = (k < K ? k : 0) / CIN, c = (k < K ? k : 0) % CIN;
-    const float av = k < K ? halo[pbase + ((tap / KW) * hc + tap % KW) * CIN + c] : 0.f;
-#pragma unroll
-    for (int nb = 0; nb < NBW; ++nb)
-      acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw[nb][kp], acc[nb], 0, 0, 0);
-  }
-  sc_stamp(stamps, 2);
   // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).  The activation is
-  // a template constant of the store loop (one branch-free body per activation) and the bias was
-  // fetched with the weights: every workgroup reaches this point at once, and a bias load here
-  // stalled all of them on the same two cache lines
-  auto store = [&](auto actc) __attribute__((always_inline)) {
+  // a template constant of the store loop (one branch-free body per activation)
+  // A tile is 64 consecutive pixels of the flattened (image, row, column) order (64/W whole
+  // rows), so the lane's output row r is pixel 64·t + wm·32 + 4·hh + (r&3) + 8(r>>2): one base
+  // address per tile and wave-uniform offsets (nothing per element for the compiler to hoist
+  // out of the tile loop into registers)
+  auto store = [&](auto actc, const floatx16(&acc)[NBW], int t) __attribute__((always_inline)) {
     constexpr int ACT = decltype(actc)::value;
+    float* ob = a.out + ((size_t)t * 64 + wm * 32 + 4 * hh) * a.so + cb + wn * NBW * 32 + li;
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
-      const int col = cb + (wn * NBW + nb) * 32 + li;
-      if (col >= a.cout) continue;
+      if (cb + (wn * NBW + nb) * 32 + li < a.cout) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int mm = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const size_t pix = ((size_t)img * oh + oy0 + mm / ow) * ow + mm % ow;
-        a.out[pix * a.so + col] = act_apply(acc[nb][r] + bias_v[nb], ACT);
+        for (int r = 0; r < 16; ++r)
+          ob[(size_t)((r & 3) + 8 * (r >> 2)) * a.so + nb * 32] = act_apply(acc[nb][r] + bias_v[nb], ACT);
       }
     }
   };
-  switch (a.act) {
-    case SCFLOW_ACT_RELU: store(std::integral_constant<int, SCFLOW_ACT_RELU>{}); break;
-    case SCFLOW_ACT_SIGMOID: store(std::integral_constant<int, SCFLOW_ACT_SIGMOID>{}); break;
-    case SCFLOW_ACT_TANH: store(std::integral_constant<int, SCFLOW_ACT_TANH>{}); break;
-    default: store(std::integral_constant<int, SCFLOW_ACT_NONE>{}); break;
+  for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
+    const int buf = it & 1;
+    const int tn = t + gridDim.x;
+    const bool more = tn < ntiles;  // workgroup-uniform
+    if (more) hfetch(tn);           // the next tile's halo in flight under this tile's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    const float* hb = halo + buf * nh;
+    floatx16 acc[NBW];
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[nb][e] = 0.f;
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const int k = 2 * kp + hh;
+      const int tap = (k < K ? k : 0) / CIN, c = (k < K ? k : 0) % CIN;
+      const float av = k < K ? hb[pbase + ((tap / KW) * hc + tap % KW) * CIN + c] : 0.f;
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb)
+        acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw[nb][kp], acc[nb], 0, 0, 0);
+    }
+    switch (a.act) {
+      case SCFLOW_ACT_RELU: store(std::integral_constant<int, SCFLOW_ACT_RELU>{}, acc, t); break;
+      case SCFLOW_ACT_SIGMOID: store(std::integral_constant<int, SCFLOW_ACT_SIGMOID>{}, acc, t); break;
+      case SCFLOW_ACT_TANH: store(std::integral_constant<int, SCFLOW_ACT_TANH>{}, acc, t); break;
+      default: store(std::integral_constant<int, SCFLOW_ACT_NONE>{}, acc, t); break;
+    }
+    if (more) hput(buf ^ 1);  // its readers finished with buf ^ 1 before the last barrier
+    __syncthreads();
   }
   if (stamps) {
+    sc_stamp(stamps, 2);
     __builtin_amdgcn_s_waitcnt(0);
     sc_stamp(stamps, 3);
   }
@@ -1152,9 +1176,9 @@ int pick_bk(int kh, int kw, int tm, int hr, int hc, long long wgs, int cus) {
 // SCFLOW_SMALLCIN_SPLIT=1: the 128-channel small-cin MFMA conv as two workgroups per 64-pixel tile
 // (one per 64-channel half) instead of one (each wave 2 × 32 channels).  Measured: 13.1 -> 12.1 us
 // in isolation (7x7 2->128, B=16), no gain inside the decoder (5.263 vs 5.233 ms/forward), so off.
-bool smallcin_split() {  // read per launch (in-process A/B)
-  const char* e = getenv("SCFLOW_SMALLCIN_SPLIT");
-  return e && atoi(e) != 0;
+bool smallcin_split() {  // cached (scflow_debug_reload_switches)
+  static EnvSwitch sw("SCFLOW_SMALLCIN_SPLIT", 0);
+  return sw.get() != 0;
 }
 
 bool conv1x1_enabled() {
@@ -1434,16 +1458,21 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
                          g.oh % (64 / g.ow) == 0 && (g.npad == 64 || g.npad == 128) &&
                          (long long)a.n * a.h * a.w * a.s0 * 4 < 0x7ffffff0LL;  // buffer offsets
     if (mfma_ok) {
-      const unsigned blocks = (unsigned)(a.n * (g.oh / (64 / g.ow)));
-      const size_t lds = sizeof(float) * (size_t)(64 / g.ow + a.kh - 1) * (g.ow + a.kw - 1) * a.c0;
+      const int ntiles = a.n * (g.oh / (64 / g.ow));
+      // workgroups: at most SCFLOW_SMALLCIN_WGS per CU (default 2), each walking its tiles
+      static EnvSwitch wgs_sw("SCFLOW_SMALLCIN_WGS", 2);
+      const int per_cu = wgs_sw.get() > 0 ? wgs_sw.get() : 2;
+      const long long cap = (long long)per_cu * device_cus();
+      const unsigned blocks = (unsigned)(ntiles < cap ? ntiles : cap);
+      const size_t lds = 2 * sizeof(float) * (size_t)(64 / g.ow + a.kh - 1) * (g.ow + a.kw - 1) * a.c0;
 #define SCFLOW_SCM(CI, KH_, KW_)                                                                   \
   if (a.c0 == CI && a.kh == KH_ && a.kw == KW_) {                                                  \
     if (g.npad == 128 && smallcin_split())                                                         \
-      conv_smallcin_mfma_kernel<CI, KH_, KW_, 1><<<dim3(blocks, 2), 256, lds, st>>>(a, g.oh, g.ow, g.npad, g_wino_stamps); \
+      conv_smallcin_mfma_kernel<CI, KH_, KW_, 1><<<dim3(blocks, 2), 256, lds, st>>>(a, g.oh, g.ow, g.npad, ntiles, g_wino_stamps); \
     else if (g.npad == 128)                                                                        \
-      conv_smallcin_mfma_kernel<CI, KH_, KW_, 2><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad, g_wino_stamps); \
+      conv_smallcin_mfma_kernel<CI, KH_, KW_, 2><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad, ntiles, g_wino_stamps); \
     else                                                                                           \
-      conv_smallcin_mfma_kernel<CI, KH_, KW_, 1><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad, g_wino_stamps); \
+      conv_smallcin_mfma_kernel<CI, KH_, KW_, 1><<<blocks, 256, lds, st>>>(a, g.oh, g.ow, g.npad, ntiles, g_wino_stamps); \
     return scflow_launch_status();                                                                 \
   }
       SCFLOW_SCM(2, 7, 7)

@@ -407,8 +407,8 @@ int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
   const dim3 grid(p.ntb, round_up(a.cout, 32) / 32);
   // two sub-steps in flight when the grid leaves CUs with a single workgroup
   // (SCFLOW_WINO4_DEPTH = 1 / 2 forces one)
-  const char* de = getenv("SCFLOW_WINO4_DEPTH");
-  const int depth_env = de ? atoi(de) : 0;
+  static EnvSwitch depth_sw("SCFLOW_WINO4_DEPTH", 0);
+  const int depth_env = depth_sw.get();
   const bool d2 = p.nsub % 2 == 0 &&
                   (depth_env == 2 || (depth_env != 1 && (long long)grid.x * grid.y <= 256));
   return d2 ? launch_wino4_gemm<2>(p, grid, st) : launch_wino4_gemm<1>(p, grid, st);

@@ -518,8 +518,8 @@ SCFLOW_API int scflow_ph_gn_reduce(const float* parts, int nsplit, long long spl
   if (!aligned16(parts) || (y && !aligned16(y)) || (split_stride & 3)) return SCFLOW_EALIGN;
   // 16-channel blocks (twice the workgroups) when the group size allows; SCFLOW_GNR_CB=32 forces
   // the 32-channel blocks (A/B)
-  const char* cbs = getenv("SCFLOW_GNR_CB");  // read per launch (in-process A/B)
-  const int cbe = cbs ? atoi(cbs) : 16;
+  static EnvSwitch cb_sw("SCFLOW_GNR_CB", 16);  // cached (scflow_debug_reload_switches)
+  const int cbe = cb_sw.get();
   const bool c16 = cbe == 16 && 16 % cpg == 0;
   dim3 grid(n, c / (c16 ? 16 : 32));
 #define SCFLOW_GNR(NS_)                                                                                    \

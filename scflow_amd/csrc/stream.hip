@@ -49,3 +49,16 @@ SCFLOW_API int scflow_event_elapsed_ms(void* start, void* end, float* ms) {
   return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end);
 }
 
+
+// ABI markers (scflow_hip.h): the version of the exported interface and sizeof(scflow_conv_args),
+// so a binding built against another header revision can refuse to run instead of passing a
+// struct of the wrong size
+SCFLOW_API int scflow_abi_version(void) { return SCFLOW_ABI_VERSION; }
+SCFLOW_API long long scflow_conv_args_size(void) { return (long long)sizeof(scflow_conv_args); }
+
+// launch-time A/B switches (EnvSwitch, common.h): re-read the environment at their next use
+std::atomic<int> g_switch_gen{0};
+SCFLOW_API int scflow_debug_reload_switches(void) {
+  g_switch_gen.fetch_add(1, std::memory_order_relaxed);
+  return SCFLOW_OK;
+}

@@ -38,6 +38,20 @@ from .registry import MODELS
 Tensor = torch.Tensor
 
 
+def _record_on(out, stream) -> None:
+    """The forward ran on the decoder's priority stream, so the caching allocator ties its
+    outputs' blocks to that stream: record the caller's stream on each one (once per storage)
+    so a caller reading them there cannot see the blocks reused before its reads finish."""
+    seen = set()
+    for item in out:
+        for t in (item if isinstance(item, (list, tuple)) else (item,)):
+            if isinstance(t, Tensor):
+                key = t.untyped_storage().data_ptr()
+                if key not in seen:
+                    seen.add(key)
+                    t.record_stream(stream)
+
+
 @MODELS.register_module()
 class SCFlowDecoder(nn.Module):
     _h_channels = {"Basic": 128, "Small": 96}
@@ -235,6 +249,7 @@ class SCFlowDecoder(nn.Module):
                 out = self._run_steps(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K,
                                       label, init_flow, invalid, hx, head_label)
             cur.wait_stream(hp)
+            _record_on(out, cur)
             return out
         return self._run_steps(feat_render, feat_real, h_feat, cxt_feat, R0, t0, depth, K, label,
                                init_flow, invalid, hx, head_label)

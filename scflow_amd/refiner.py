@@ -73,6 +73,42 @@ class SCFlowRefiner(nn.Module):
         if renderer is not None:
             from .renderer import Renderer
             self.renderer = renderer if isinstance(renderer, Renderer) else Renderer(**renderer)
+        # scflow_refiner.py:58-61.  The flags are kept and re-applied by train(): the reference
+        # applies them once in __init__, so mmengine's later model.train() puts its BatchNorms
+        # back in train mode; here a frozen module stays frozen (requires_grad=False persists
+        # in both).
+        self.freeze_bn_flag, self.freeze_encoder_flag = bool(freeze_bn), bool(freeze_encoder)
+        if freeze_bn:
+            self.freeze_bn()
+        if freeze_encoder:
+            self.freeze_encoder()
+
+    def freeze_encoder(self) -> None:
+        """scflow_refiner.py:65-73: the feature encoders (real and rendered; one module when
+        shared) in eval mode with requires_grad=False.  The context encoder stays trainable."""
+        self.freeze_encoder_flag = True
+        for enc in (self.real_encoder, self.render_encoder):
+            for m in enc.modules():
+                m.eval()
+                for p in m.parameters():
+                    p.requires_grad = False
+
+    def freeze_bn(self) -> None:
+        """scflow_refiner.py:75-78: every BatchNorm2d in eval mode (running statistics, no
+        update); its affine parameters stay trainable."""
+        self.freeze_bn_flag = True
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+
+    def train(self, mode: bool = True):
+        super().train(mode)
+        if mode and self.freeze_bn_flag:
+            self.freeze_bn()
+        if mode and self.freeze_encoder_flag:
+            for enc in (self.real_encoder, self.render_encoder):
+                enc.eval()
+        return self
 
     def to(self, *args, **kwargs):  # base_refiner.py:69-72: the renderer's meshes move too
         if self.renderer is not None:

@@ -47,8 +47,11 @@ class OneCycleLR:
         return end + (start - end) / 2.0 * (math.cos(math.pi * pct) + 1)
 
     def lr_at(self, step: int) -> float:
-        if step < 0 or step > self.total_steps:
-            raise ValueError(f"OneCycleLR: step {step} outside [0, {self.total_steps}]")
+        """Steps past the schedule's last (``total_steps − 1``) stay at its minimum lr — torch
+        raises there, and a linear anneal evaluated at ``total_steps`` would dip below zero."""
+        if step < 0:
+            raise ValueError(f"OneCycleLR: step {step} is negative")
+        step = min(step, self.total_steps - 1)
         start_step = 0.0
         for i, (end_step, lo, hi) in enumerate(self.phases):
             if step <= end_step or i == len(self.phases) - 1:

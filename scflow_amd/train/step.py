@@ -32,8 +32,9 @@ _MT_BACKWARD = os.environ.get("SCFLOW_TRAIN_MT_BACKWARD", "1") == "1"  # A/B swi
 
 def trainable_parameters(refiner) -> List[torch.nn.Parameter]:
     """The refiner's parameters, each once (the shared render / real feature encoder appears
-    under both names) — what the gradient buckets and the optimizer hold."""
-    return list(dict.fromkeys(refiner.parameters()))
+    under both names) and only those that require grad (``freeze_encoder`` clears it on the
+    feature encoder) — what the gradient buckets and the optimizer hold."""
+    return [p for p in dict.fromkeys(refiner.parameters()) if p.requires_grad]
 
 
 class GradBuckets:
@@ -163,6 +164,17 @@ class TrainStep:
         self.diam_t = torch.as_tensor(self.diameters, dtype=torch.float32, device=dev)
         if dist.is_initialized() and dist.get_world_size(group) > 1:
             self.broadcast_parameters()
+
+    def state_dict(self) -> Dict:
+        """The step's resumable state: the schedule position and the optimizer state (the model's
+        own state_dict holds the weights and BN statistics)."""
+        return dict(iteration=self.iteration, optimizer=self.opt.state_dict())
+
+    def load_state_dict(self, state: Dict) -> None:
+        """Resume: the schedule continues at ``state['iteration']`` (warm-up is not repeated)."""
+        self.iteration = int(state["iteration"])
+        self.opt.load_state_dict(state["optimizer"])
+        self._set_lr()
 
     def broadcast_parameters(self, src: int = 0) -> None:
         """Start every rank from rank 0's weights and BN statistics."""

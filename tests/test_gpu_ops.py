@@ -225,6 +225,30 @@ def test_conv2d_variants(ops, case):
     close(got, ref, 2e-6 * np.sqrt(kk) * 4, 1e-5, f"conv {case}")
 
 
+@pytest.mark.parametrize("wgs", ["0", "1"])
+@pytest.mark.parametrize("case", [
+    (12, 64, 64, 2, 0, 128, 7, 3, "ReLU"),   # 768 tiles > 2 per CU: workgroups walk 2-3 tiles
+    (9, 64, 64, 1, 0, 64, 3, 1, "ReLU"),     # mask encoder.0 shape, a ragged last round
+    (17, 32, 32, 2, 0, 128, 7, 3, None),     # 272 tiles at W = 32
+    (3, 64, 64, 2, 0, 100, 3, 1, "Tanh"),    # cout not a multiple of 32 (masked columns)
+])
+def test_conv2d_smallcin_tile_walk(ops, case, wgs, monkeypatch):
+    """The small-cin MFMA conv with workgroups walking several tiles (round 6: the grid capped at
+    SCFLOW_SMALLCIN_WGS per CU, 2 by default; 1 forces ≥ 3 tiles per workgroup here), the next
+    tile's halo double-buffered in LDS — against the fp64 conv."""
+    from scflow_amd._lib import reload_switches
+    if wgs != "0":
+        monkeypatch.setenv("SCFLOW_SMALLCIN_WGS", wgs)
+    reload_switches()
+    try:
+        n, h, w, c0, c1, cout, k, pad, act = case
+        got, ref = _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=3)
+    finally:
+        monkeypatch.delenv("SCFLOW_SMALLCIN_WGS", raising=False)
+        reload_switches()
+    close(got, ref, 2e-6 * np.sqrt(c0 * k * k) * 4, 1e-5, f"small-cin conv {case} wgs={wgs}")
+
+
 @pytest.mark.parametrize("bk", [8, 16])
 @pytest.mark.parametrize("case", [
     (2, 32, 32, 324, 0, 256, 1, 0, "ReLU"),
@@ -310,9 +334,15 @@ def test_conv2d_winograd_f4x4(ops, case, depth, monkeypatch):
     outputs ≈ 4 at 256 channels in a numpy restatement) — 5e-5·√(K/256) absolute on unit-scale
     outputs."""
     from scflow_amd._lib import CONV_WINO4
+    from scflow_amd._lib import reload_switches
     monkeypatch.setenv("SCFLOW_WINO4_DEPTH", depth)
+    reload_switches()
     n, h, w, c0, c1, cout, act = case
-    got, ref = _conv_case(ops, n, h, w, c0, c1, cout, 3, 1, act, bk=CONV_WINO4)
+    try:
+        got, ref = _conv_case(ops, n, h, w, c0, c1, cout, 3, 1, act, bk=CONV_WINO4)
+    finally:
+        monkeypatch.delenv("SCFLOW_WINO4_DEPTH")
+        reload_switches()
     kk = (c0 + c1) * 9
     close(got, ref, 5e-5 * np.sqrt(kk / 256 / 9) * 3 + 1e-6, 1e-5, f"F(4x4,3x3) conv {case}")
 

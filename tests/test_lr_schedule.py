@@ -45,9 +45,11 @@ def test_small_schedules_match_torch(kw):
 
 
 def test_out_of_range_and_bad_args():
-    s = OneCycleLR(1e-3, 10)
+    s = OneCycleLR(1e-3, 10, anneal_strategy="linear")
     with pytest.raises(ValueError):
-        s.lr_at(11)
+        s.lr_at(-1)
+    for k in (10, 11, 10 ** 6):  # past the end: clamped at the minimum, never negative
+        assert s.lr_at(k) == s.lr_at(9) and math.isclose(s.lr_at(k), s.min_lr, rel_tol=1e-9)
     with pytest.raises(ValueError):
         OneCycleLR(1e-3, 10, anneal_strategy="step")
     with pytest.raises(ValueError):

@@ -73,7 +73,7 @@ def _patch_torch_ops(monkeypatch):
     monkeypatch.setattr(ops, "flow_downsample", downsample)
 
 
-def build_train_refiner(iters, dtype=torch.float32):
+def build_train_refiner(iters, dtype=torch.float32, **kw):
     from scflow_amd import MODELS
     from tests.test_gpu_decoder import decoder_cfg
     enc = dict(type="RAFTEncoder", in_channels=3, out_channels=256, net_type="Basic",
@@ -82,7 +82,7 @@ def build_train_refiner(iters, dtype=torch.float32):
                norm_cfg=dict(type="BN"))
     r = MODELS.build(dict(type="SCFlowRefiner", cxt_channels=128, h_channels=128,
                           seperate_encoder=False, encoder=enc, cxt_encoder=ctx,
-                          decoder=dict(type="SCFlowDecoder", **decoder_cfg(iters))))
+                          decoder=dict(type="SCFlowDecoder", **decoder_cfg(iters)), **kw))
     missing, unexpected = r.load_state_dict(
         {("decoder." + k if not k.startswith(("real_encoder.", "render_encoder.", "context.")) else k): v
          for k, v in refiner_state_dict().items()}, strict=False)
@@ -150,6 +150,44 @@ def test_train_forward_host_matches_oracle(monkeypatch):
     assert checked > 100
     # BN running stats were updated in train mode (SCFlowRefiner.train())
     assert int(r.context.norm1.num_batches_tracked) == 1
+
+
+def test_freeze_bn_and_encoder(monkeypatch):
+    """freeze_bn / freeze_encoder (scflow_refiner.py:58-79): BatchNorms in eval mode (no running
+    statistics update, batch statistics not used), the feature encoder in eval mode with
+    requires_grad=False — and both survive train(), which the training loop calls."""
+    from scflow_amd.train.model import refiner_train_forward
+    _patch_torch_ops(monkeypatch)
+    r = build_train_refiner(1, torch.float64, freeze_bn=True, freeze_encoder=True)
+    bns = [m for m in r.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    assert bns and not any(m.training for m in bns)
+    assert not any(m.training for m in r.real_encoder.modules())
+    assert not any(p.requires_grad for p in r.real_encoder.parameters())
+    assert all(p.requires_grad for p in r.context.parameters())
+    assert r.decoder.training and r.context.training
+    rm0 = r.context.norm1.running_mean.clone()
+    batch, points, diam = train_batch(1, 256, seed=3, labels=[4], dtype=torch.float64)
+    res = refiner_train_forward(r, batch, points, diam)
+    res["loss"].backward()
+    assert all(p.grad is None for p in r.real_encoder.parameters())
+    assert r.context.norm1.weight.grad is not None  # BN affine stays trainable
+    assert int(r.context.norm1.num_batches_tracked) == 0
+    assert torch.equal(r.context.norm1.running_mean, rm0)
+    # frozen BN = eval-mode batch_norm (running statistics) in the training forward
+    from scflow_amd.train.model import _norm
+    x = torch.randn(1, 8, 8, r.context.norm1.num_features, dtype=torch.float64)
+    ref = F.batch_norm(x.permute(0, 3, 1, 2), r.context.norm1.running_mean, r.context.norm1.running_var,
+                       r.context.norm1.weight, r.context.norm1.bias, training=False,
+                       eps=r.context.norm1.eps).permute(0, 2, 3, 1)
+    torch.testing.assert_close(_norm(x, r.context.norm1), ref)
+    # TrainStep only optimises what requires grad
+    from scflow_amd.train.step import trainable_parameters
+    names = {id(p) for p in trainable_parameters(r)}
+    assert not any(id(p) in names for p in r.real_encoder.parameters())
+    # without the flags: train mode everywhere
+    r2 = build_train_refiner(1, torch.float64)
+    assert all(m.training for m in r2.modules() if isinstance(m, torch.nn.BatchNorm2d))
+    assert all(p.requires_grad for p in r2.real_encoder.parameters())
 
 
 def test_upsample_adjoint_matches_autograd(monkeypatch):

@@ -56,6 +56,8 @@ def main():
         for k, v in zip(names, c):
             if k.startswith("env:"):
                 os.environ[k[4:]] = str(v)
+                from scflow_amd._lib import reload_switches
+                reload_switches()  # launch-time switches are cached by the library
                 continue
             obj, attr = target(k)
             setattr(obj, attr, v)
