@@ -55,8 +55,32 @@ struct Wino4Params {
   int nsub;         // sub-steps over both sources
   int th, tw;       // tiles per image column / row (h/4, w/4)
   int ntiles, ntb;  // tiles, tile blocks
+  int xgt, xgc;     // XCD-blocked GEMM order (w4_block): xgt tile blocks × xgc channel blocks, 0 = off
   unsigned long long* stamps;  // profiling (scflow_debug_conv_stamps), or NULL
 };
+
+// (tile block, output-channel block) of a GEMM workgroup.  Workgroups go round-robin over the 8
+// XCDs in linear order (x fastest), each XCD with its own 4 MB L2.  In linear order the ≈ 64
+// workgroups an XCD runs at a time are ≈ 32 tile blocks × 2 channel blocks, so every V slice is
+// fetched from the memory side once per channel block (16× for the 512-wide heads conv at 64×64
+// maps: 10× the conv's algorithmic bytes, round 5).  Blocked (xgt > 0): linear id L is logical
+// index (L mod 8)·N/8 + L/8, so each XCD owns a contiguous range of the logical order, which
+// walks xgt × xgc blocks (channel blocks fastest inside a block): an XCD's concurrent
+// workgroups share xgt V slices and xgc U slices through its L2, the sub-step they all stream
+// at once being ≈ 37 KB per slice.  The host picks xgt, xgc dividing the grid, N ≡ 0 mod 8.
+__device__ __forceinline__ void w4_block(const Wino4Params& P, int& tb, int& cb) {
+  tb = blockIdx.x;
+  cb = blockIdx.y;
+  if (P.xgt <= 0) return;
+  const int R = gridDim.x, C = gridDim.y;
+  const int L = blockIdx.y * R + blockIdx.x;
+  const int per = (R * C) >> 3;
+  const int id = (L & 7) * per + (L >> 3);
+  const int bsz = P.xgt * P.xgc, cblocks = C / P.xgc;
+  const int blk = id / bsz, r = id - blk * bsz;
+  tb = (blk / cblocks) * P.xgt + r / P.xgc;
+  cb = (blk % cblocks) * P.xgc + r % P.xgc;
+}
 
 // v = Bᵀ·d over one axis (6 float4)
 __device__ __forceinline__ void w4_bt(const floatx4 (&d)[6], floatx4 (&v)[6]) {
@@ -153,7 +177,8 @@ __global__ __launch_bounds__(256, D == 2 ? 1 : 2) void conv_wino4_kernel(Wino4Pa
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, hh = lane >> 5;
-  const int tb = blockIdx.x, cb = blockIdx.y;
+  int tb, cb;
+  w4_block(P, tb, cb);
   const int nsub = P.nsub;  // a multiple of D (launch_wino4)
   wino_stamp(P.stamps, 0);
   const unsigned blk = (unsigned)nsub * W4P * 1024;  // bytes of one block's V / U slice
@@ -405,6 +430,24 @@ int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
   const int e = scflow_launch_status();
   if (e) return e;
   const dim3 grid(p.ntb, round_up(a.cout, 32) / 32);
+  // XCD-blocked order (w4_block) for grids of more than one round of two workgroups per CU:
+  // ≈ 64 workgroups (an XCD's 32 CUs × 2) per block, channel blocks up to 8, tile blocks a power
+  // of two.  Measured (round 6, profiles/r06/g2): configs[4] memory-side traffic of the
+  // transform + GEMM pair 10.0× → 5.6× its algorithmic bytes, corr_net.1 465 → 412 µs and the
+  // heads conv 455 → 431 µs alone, decoder 8.69k → 8.91k iters/s; configs[1] (one round or
+  // less) ±1 µs, so its grids keep the linear order.  SCFLOW_WINO4_XCD = 0 off, 2 every grid.
+  static EnvSwitch xcd_sw("SCFLOW_WINO4_XCD", 1);
+  const long long nwg = (long long)grid.x * grid.y;
+  p.xgt = p.xgc = 0;
+  if (xcd_sw.get() && nwg % 8 == 0 && (xcd_sw.get() == 2 || nwg > 2LL * device_cus())) {
+    int gc = 1;
+    for (int c = (int)grid.y < 8 ? (int)grid.y : 8; c >= 1; --c)
+      if (grid.y % c == 0) { gc = c; break; }
+    int gt = 1;
+    while (gt * 2 * gc <= 64 && grid.x % (gt * 2) == 0) gt *= 2;
+    const long long nblk = ((long long)grid.x / gt) * (grid.y / gc);
+    if (gt * gc >= 16 && nblk >= 1) { p.xgt = gt; p.xgc = gc; }
+  }
   // two sub-steps in flight when the grid leaves CUs with a single workgroup
   // (SCFLOW_WINO4_DEPTH = 1 / 2 forces one)
   static EnvSwitch depth_sw("SCFLOW_WINO4_DEPTH", 0);

@@ -325,23 +325,26 @@ def test_conv2d_winograd(ops, case):
     (1, 20, 12, 36, 4, 100, "Sigmoid"),      # 15 tiles: a partial tile block, ragged channels
     (2, 128, 128, 64, 0, 64, "ReLU"),        # encoder width
 ])
+@pytest.mark.parametrize("xcd", ["0", "2"])
 @pytest.mark.parametrize("depth", ["1", "2"])
-def test_conv2d_winograd_f4x4(ops, case, depth, monkeypatch):
+def test_conv2d_winograd_f4x4(ops, case, depth, xcd, monkeypatch):
     """Winograd F(4×4,3×3) (SCFLOW_CONV_WINO4: input transform launch + point GEMMs with the
     output transform in the epilogue) vs an fp64 direct conv, with one and two sub-steps of the
     GEMM's operands in flight (SCFLOW_WINO4_DEPTH; two needs an even sub-step count, else one).
     Tolerance: its fp32 error is ≈ 10× the direct conv's (points {0, ±1, 2, −½, ∞}; 1.3e-5 of
     outputs ≈ 4 at 256 channels in a numpy restatement) — 5e-5·√(K/256) absolute on unit-scale
-    outputs."""
+    outputs.  Both GEMM block orders (SCFLOW_WINO4_XCD: 0 linear, 2 XCD-blocked at every size)."""
     from scflow_amd._lib import CONV_WINO4
     from scflow_amd._lib import reload_switches
     monkeypatch.setenv("SCFLOW_WINO4_DEPTH", depth)
+    monkeypatch.setenv("SCFLOW_WINO4_XCD", xcd)
     reload_switches()
     n, h, w, c0, c1, cout, act = case
     try:
         got, ref = _conv_case(ops, n, h, w, c0, c1, cout, 3, 1, act, bk=CONV_WINO4)
     finally:
         monkeypatch.delenv("SCFLOW_WINO4_DEPTH")
+        monkeypatch.delenv("SCFLOW_WINO4_XCD")
         reload_switches()
     kk = (c0 + c1) * 9
     close(got, ref, 5e-5 * np.sqrt(kk / 256 / 9) * 3 + 1e-6, 1e-5, f"F(4x4,3x3) conv {case}")

@@ -16,6 +16,8 @@
 #   abenv=VAR:V1,V2:B:S:ONLY   the same A/B over the values of an environment switch
 #   abdec=TOGGLES        tools/ab_bench.py TOGGLES (';' separates arguments)
 #   quick[=ARGS]         kernel trace of the decoder leg: per-forward table + iteration timeline
+#   traffic=NAME:c1|c4[:VAR=VAL]   FETCH_SIZE + WRITE_SIZE passes (each its own rocprofv3 run)
+#                        over the decoder leg → traffic_NAME.json (tools/traffic_json.py)
 #   prof                 tools/prof_r5.sh TAG (HEAD evidence: traces, timeline, PMC, traffic)
 #   py=SCRIPT[;ARGS]     python tools/SCRIPT ARGS ('; ' separates arguments)
 TAG=${1:?tag}; shift
@@ -81,6 +83,23 @@ for STEP in "$@"; do
       python3 $R/tools/timeline.py $DB --iteration 61 > $OUT/timeline.txt 2>&1
       rm -rf $OUT/kt; cd $R
       head -20 $OUT/per_forward.txt; tail -1 $OUT/timeline.txt ;;
+    traffic)
+      IFS=: read NAME CF EV <<< "$V"
+      P="--steps 2 --warmup 1 --no-cpu-baseline --e2e-batch 0 --train-batch 0 --no-kernel-timer"
+      TJ="--batch 16 --size 256 --iters 8"
+      [ "$CF" = c4 ] && { P="$P $C4"; TJ="--batch 32 --size 512 --iters 12"; }
+      cd /tmp
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        env $EV timeout -s KILL 150 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_${NAME}_$ctr -o run -- python3 $R/bench.py $P > /dev/null 2> $OUT/pmc_${NAME}_$ctr.err || exit 15
+      done
+      cd $R
+      python3 tools/traffic_json.py $OUT/pmc_${NAME}_FETCH_SIZE $OUT/pmc_${NAME}_WRITE_SIZE $TJ > $OUT/traffic_$NAME.json || exit 15
+      rm -rf $OUT/pmc_${NAME}_*
+      python3 -c "
+import json,sys
+d=json.load(open(sys.argv[1]))
+for k,v in d['kernels'].items():
+    print(f\"{k:28s} {v['hbm_bytes_per_launch']/1e6:9.1f} MB/launch  x{v['ratio_to_algorithmic']}\")" $OUT/traffic_$NAME.json ;;
     prof)
       bash tools/prof_r5.sh $TAG || exit 13 ;;
     py)
