@@ -130,7 +130,31 @@ __host__ __device__ inline int lk_slot_floats(int h, int w, int L, int win) {
 // a pixel slot holds two regions of the largest level size — half the LDS of all four — and the
 // region loads still in registers while a pair is sampled are the other pair's only: 6
 // workgroups per CU instead of 4 (round 5).  Region p of the slot starts at p·lk_tb_region().
+// Round 6: at r = 4 the TB regions use a swizzled row layout.  The sampling phase reads 4-byte
+// taps, and ds_read_b32 serves a wave in two 32-lane groups over 32 banks ((a/4) mod 32,
+// MI355X_MICROARCH.md §LDS): a group = 2 pixels × 16 consecutive samples s = 9a + b, whose tap
+// (b + dy, a + dx) sat at (b + dy)·11 + a + dx — 2–3-way conflicts inside a pixel and between
+// the two (SQ_LDS_BANK_CONFLICT 1.29e7 of 3.51e7 LDS cycles at configs[4], 63 % of them the tap
+// reads: profiles/r06/g3_lookup_conflicts.txt).  Row r now starts at LK_TB_ROW[r] ≡ 25·r
+// (mod 32) — 25 = 9⁻¹ mod 32, so a tap's bank is 25·s + const: 32 consecutive samples hit 32
+// distinct banks — packed without overlap into 136 floats; the slot (two regions, 272 floats)
+// ≡ 16 mod 32 puts the group's second pixel on the other 16 banks.  The region stores (rows
+// 4j..4j+3 × 4 tiles per 16 lanes) land on distinct banks by the same residues.
+// row starts {0, 89, 114, 11, 100, 125, 22, 47, 72, 33, 58} = (25·r mod 32) + 32·k_r, the k_r
+// packed 2 bits per row (arithmetic, not a table: no memory lookup per tap)
+__host__ __device__ constexpr int lk_tb_row4(int r) {
+  return ((25 * r) & 31) + 32 * ((1462072 >> (2 * r)) & 3);
+}
+static_assert(lk_tb_row4(0) == 0 && lk_tb_row4(1) == 89 && lk_tb_row4(2) == 114 && lk_tb_row4(3) == 11 &&
+              lk_tb_row4(4) == 100 && lk_tb_row4(5) == 125 && lk_tb_row4(6) == 22 &&
+              lk_tb_row4(7) == 47 && lk_tb_row4(8) == 72 && lk_tb_row4(9) == 33 && lk_tb_row4(10) == 58,
+              "swizzled row starts");
+constexpr int LK_TB4_REGION = 136;
+#ifndef LK_TB_SWZ  // 0: the round-5 row-major regions (A/B build)
+#define LK_TB_SWZ 1
+#endif
 __host__ __device__ inline int lk_tb_region(int h, int w, int L, int win) {
+  if (LK_TB_SWZ && win == 11) return LK_TB4_REGION;  // r = 4: the swizzled layout (rows ≤ 11)
   int t = 0;
   for (int l = 0; l < L; ++l) {
     const int r = lk_rows(h >> l, w >> l, win) * win;
@@ -140,9 +164,21 @@ __host__ __device__ inline int lk_tb_region(int h, int w, int L, int win) {
 }
 __host__ __device__ inline int lk_tb_slot_floats(int h, int w, int L, int win) {
   const int t = 2 * lk_tb_region(h, w, L, win);
+  if (LK_TB_SWZ && win == 11) return t;  // 272 ≡ 16 mod 32
   return (t & 7) ? t : t + 4;
 }
+// coordinates of a pixel slot: [level][axis][index] padded to ≡ 16 mod 32 floats, so the two
+// pixels of a 32-lane group read them on different banks
+__host__ __device__ constexpr int lk_crd_stride(int d) {
+  return LK_TB_SWZ ? LK_MAXL * 2 * d + ((16 - (LK_MAXL * 2 * d) % 32) % 32 + 32) % 32 : LK_MAXL * 2 * d;
+}
 
+#ifndef LK_DBG_STORE_LINEAR
+#define LK_DBG_STORE_LINEAR 0
+#endif
+#ifndef LK_DBG_SAMPLE_LINEAR
+#define LK_DBG_SAMPLE_LINEAR 0
+#endif
 constexpr int LK_OOB = 0x7ffffff0;  // buffer voffset of a zero tap (beyond any num_records)
 
 // TR (tile regions, tiled maps only): every level's region is the 4×4 block of 4×4 tiles (16×16
@@ -201,8 +237,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
   stamp(0);
   constexpr int NPR = (LK_MAXL * D + LK_GL - 1) / LK_GL;  // (level, a) pairs per lane
   extern __shared__ float win[];  // [LK_SLOTS][slot floats]
-  __shared__ float crd[LK_SLOTS][LK_MAXL][2][D];
+  __shared__ float crd_s[LK_SLOTS][lk_crd_stride(D)];
+  auto crd = [&](int sl, int l, int axis, int i) -> float& { return crd_s[sl][(l * 2 + axis) * D + i]; };
   __shared__ signed char sr[LK_SLOTS][LK_MAXL][2][D];  // region-relative floor of a sample, −1: none
+  // TB, r = 4: per (level, y sample) the swizzled starts of the tap rows ry, ry + 1 packed as
+  // r0 | r1 << 7, or −1 when a tap row is off the region (computed once, not per sample)
+  constexpr bool ROWT = TB && R == 4 && LK_TB_SWZ;
+  __shared__ short rowt[ROWT ? LK_SLOTS : 1][LK_MAXL][D];
   __shared__ int org[LK_SLOTS][LK_MAXL][2];    // region origin (map coordinates)
   __shared__ int ext[LK_SLOTS][LK_MAXL][2][2];  // TB: taps read, [lo, hi] (map coordinates)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -234,7 +275,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
     const int l = t / (2 * D), axis = (t / D) % 2, i = t % D;
     const int size = axis == 0 ? (W >> l) : (H >> l);
     const float c = ((float)(axis == 0 ? x : y) + (axis == 0 ? fx : fy)) / (float)(1 << l);
-    crd[slot][l][axis][i] = unnorm_coord(c + (float)(i - R), size, ac);
+    crd(slot, l, axis, i) = unnorm_coord(c + (float)(i - R), size, ac);
   }
   lk_sync<TB>();
   stamp(1);
@@ -245,9 +286,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
   for (int t = gl; t < L * 2 * D; t += LK_GL) {
     const int l = t / (2 * D), axis = (t / D) % 2, i = t % D;
     const bool whole = !TR && lk_whole(H >> l, W >> l, WIN);
-    const float c0x = crd[slot][l][0][0], c0y = crd[slot][l][1][0];
+    const float c0x = crd(slot, l, 0, 0), c0y = crd(slot, l, 1, 0);
     const bool fin = isfinite(c0x) && isfinite(c0y) && fabsf(c0x) < 1e8f && fabsf(c0y) < 1e8f;
-    const float s = crd[slot][l][axis][i];
+    const float s = crd(slot, l, axis, i);
     int o = whole ? -1 : (fin ? (int)floorf(axis == 0 ? c0x : c0y) - 1 : -(1 << 29));
     // TB: the taps the samples read on this axis, [lo, hi] = [min floor, max floor + 1] over the
     // finite samples; the region starts at lo (D + 2 columns hold them: 9 samples at most
@@ -255,7 +296,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
     int lo = 1 << 30, hi = -(1 << 30);
     if (TB && fin) {
       for (int j = 0; j < D; ++j) {
-        const float sj = crd[slot][l][axis][j];
+        const float sj = crd(slot, l, axis, j);
         if (isfinite(sj)) {
           const int f = (int)floorf(sj);
           lo = min(lo, f);
@@ -272,6 +313,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
     // (zero: the map's padding) — kept as −1 so it fits a byte
     const int rel = fin && isfinite(s) ? (int)floorf(s) - o : -1;
     sr[slot][l][axis][i] = (signed char)(rel >= 0 && rel < WIN ? rel : -1);
+    if constexpr (ROWT) {
+      if (axis == 1) {
+        const int rows = lk_rows(H >> l, W >> l, WIN);
+        rowt[slot][l][i] = (short)(rel >= 0 && rel + 1 < rows && rel + 1 < WIN
+                                       ? lk_tb_row4(rel) | (lk_tb_row4(rel + 1) << 7) : -1);
+      }
+    }
     if (i == 0) org[slot][l][axis] = o;
     if (TB && i == 0) {
       ext[slot][l][axis][0] = lo;
@@ -458,7 +506,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
               if (r < rws) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                  if (cb + q >= 0 && cb + q < WIN) sw[p * rsz + r * WIN + cb + q] = tbv[lp][j][q];
+                  if (cb + q >= 0 && cb + q < WIN) {
+#if LK_DBG_STORE_LINEAR  // attribution build only (bank conflicts per phase): conflict-free addresses
+                    win[((p * NS * 4 + j * 4 + q) & 3) * 256 + (int)threadIdx.x] = tbv[lp][j][q];
+#else
+                    sw[p * rsz + (R == 4 && LK_TB_SWZ ? lk_tb_row4(r) : r * WIN) + cb + q] = tbv[lp][j][q];
+#endif
+                  }
               }
             }
           }
@@ -470,11 +524,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
         const int sidx = gl + LK_GL * j;
         if (D * D % LK_GL != 0 && sidx >= D * D) break;
         const int a = sidx / D, b = sidx - a * D;
-        const int rx = sr[slot][l][0][a], ry = sr[slot][l][1][b];
-        const float ix = crd[slot][l][0][a], iy = crd[slot][l][1][b];
-        const bool ok = rx >= 0 && rx + 1 < WIN && ry >= 0 && ry + 1 < rows;
-        const float* wr = sw + off + (ok ? ry * WIN + rx : 0);
-        const float t00 = wr[0], t01 = wr[1], t10 = wr[WIN], t11 = wr[WIN + 1];
+        const int rx = sr[slot][l][0][a];
+        // y: the tap rows' validity, and (ROWT) their swizzled row starts, one LDS read
+        const int ry = ROWT ? (int)rowt[slot][l][b] : (int)sr[slot][l][1][b];
+        const float ix = crd(slot, l, 0, a), iy = crd(slot, l, 1, b);
+        const bool ok = rx >= 0 && rx + 1 < WIN && ry >= 0 && (ROWT || ry + 1 < rows);
+#if LK_DBG_SAMPLE_LINEAR  // attribution build only: conflict-free tap addresses
+        const float* wr = win + (int)threadIdx.x + 0 * (off + ry * WIN + rx);
+        const float t00 = wr[0], t01 = wr[256], t10 = wr[512], t11 = wr[768];
+#else
+        int r0, r1;  // row starts of the tap rows ry, ry + 1
+        if constexpr (ROWT) {  // swizzled (lk_tb_row4), packed r0 | r1 << 7
+          const int rp = ok ? ry : 0;
+          r0 = rp & 127;
+          r1 = rp >> 7;
+        } else {
+          r0 = ok ? ry * WIN : 0;
+          r1 = ok ? (ry + 1) * WIN : 0;
+        }
+        const float* wr = sw + off + (ok ? rx : 0);
+        const float t00 = wr[r0], t01 = wr[r0 + 1], t10 = wr[r1], t11 = wr[r1 + 1];
+#endif
         const float ix_w = floorf(ix), ix_e = ix_w + 1.f;
         const float wxw = ix_e - ix, wxe = ix - ix_w;
         const float iy_n = floorf(iy), iy_s = iy_n + 1.f;
@@ -505,13 +575,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TB ? 6 : 3)
     for (int k = 1; k < LK_MAXL; ++k)
       if (l == k) { off = offl[k]; rows = rn[k] / WIN; }
     const int rx = sr[slot][l][0][a];
-    const float ix = crd[slot][l][0][a];
+    const float ix = crd(slot, l, 0, a);
     int ry[D];
     float iy[D];
 #pragma unroll
     for (int b = 0; b < D; ++b) {
       ry[b] = sr[slot][l][1][b];
-      iy[b] = crd[slot][l][1][b];
+      iy[b] = crd(slot, l, 1, b);
     }
     const bool okx = tv && rx >= 0 && rx + 1 < WIN;
     float t00[D], t01[D], t10[D], t11[D];

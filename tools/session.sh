@@ -18,6 +18,12 @@
 #   quick[=ARGS]         kernel trace of the decoder leg: per-forward table + iteration timeline
 #   traffic=NAME:c1|c4[:VAR=VAL]   FETCH_SIZE + WRITE_SIZE passes (each its own rocprofv3 run)
 #                        over the decoder leg → traffic_NAME.json (tools/traffic_json.py)
+#   pmc=NAME;LIB;CTRS;SCRIPT[;ARGS…]   one rocprofv3 --pmc pass (CTRS space-separated, within one
+#                        pass's limits) over python tools/SCRIPT ARGS with scflow_amd/lib/ab/LIB.so
+#                        (LIB = base: the default library) → pmc_NAME.txt (tools/pmc_summary.py)
+#   pyab=LIB;SCRIPT[;ARGS…]   python tools/SCRIPT ARGS with the default library and with
+#                        scflow_amd/lib/ab/LIB.so, alternating, 2 rounds
+#   trainprof[=ENV]      kernel trace of 5 training steps (tools/train_bench.py) → train_stats.txt
 #   prof                 tools/prof_r5.sh TAG (HEAD evidence: traces, timeline, PMC, traffic)
 #   py=SCRIPT[;ARGS]     python tools/SCRIPT ARGS ('; ' separates arguments)
 TAG=${1:?tag}; shift
@@ -100,6 +106,33 @@ import json,sys
 d=json.load(open(sys.argv[1]))
 for k,v in d['kernels'].items():
     print(f\"{k:28s} {v['hbm_bytes_per_launch']/1e6:9.1f} MB/launch  x{v['ratio_to_algorithmic']}\")" $OUT/traffic_$NAME.json ;;
+    pmc)
+      IFS=';' read -ra A <<< "$V"
+      NAME=${A[0]}; LIB=${A[1]}; CTRS=${A[2]}; SCR=${A[3]}
+      E="SCFLOW_LIB="; [ "$LIB" != base ] && E="SCFLOW_LIB=$R/scflow_amd/lib/ab/$LIB.so"
+      cd /tmp
+      env $E timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d $OUT/pmc_$NAME -o run -- python3 $R/tools/$SCR "${A[@]:4}" > $OUT/pmc_$NAME.log 2>&1 || exit 16
+      cd $R
+      python3 tools/pmc_summary.py $(find $OUT/pmc_$NAME -name "*counter_collection.csv") > $OUT/pmc_$NAME.txt
+      rm -rf $OUT/pmc_$NAME
+      grep -v "^==" $OUT/pmc_$NAME.txt | sed "s/^/$NAME /" | cut -c1-400 ;;
+    pyab)
+      IFS=';' read -ra A <<< "$V"
+      LIB=$R/scflow_amd/lib/ab/${A[0]}.so; [ -f $LIB ] || { echo "missing $LIB"; exit 2; }
+      for r in 1 2; do
+        for v in base ${A[0]}; do
+          E="SCFLOW_LIB="; [ $v != base ] && E="SCFLOW_LIB=$LIB"
+          env $E timeout -k 10 300 python tools/"${A[@]:1}" 2>&1 | grep -v amdgpu.ids | sed "s/^/$v /" | tee -a $OUT/pyab.txt
+          [ ${PIPESTATUS[0]} -eq 0 ] || exit 18
+        done
+      done ;;
+    trainprof)
+      cd /tmp
+      env $V timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/ktt -o run -- python3 $R/tools/train_bench.py --steps 3 --warmup 2 > $OUT/train_bench.json 2> $OUT/ktt.err || exit 17
+      DB=$(find $OUT/ktt -name "*.db" | head -1)
+      python3 $R/tools/stats_file.py $DB "python tools/train_bench.py --steps 3 --warmup 2 (5 training steps, B=16, 256x256, 8 iters)" > $OUT/train_stats.txt
+      rm -rf $OUT/ktt; cd $R
+      head -30 $OUT/train_stats.txt ;;
     prof)
       bash tools/prof_r5.sh $TAG || exit 13 ;;
     py)
