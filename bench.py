@@ -314,21 +314,22 @@ def bench_train(args, world, rank, dev, feat):
     gc.collect()
     gc.freeze()
     # warm up until the per-step device time is flat: the GPU clock settles under the step's
-    # sustained load over its first ≈ 5–10 steps (round 5: 37.0 → 38.9 ms inside the timed
-    # window after 3 warm-ups).  Flat = the last 4 steps within 1 % of each other, every rank
-    # (≥ 5 and ≤ 40 warm-up steps; each warm-up step is synchronised to read its time).
+    # sustained load over its first ≈ 10–15 steps (round 5: 37.0 → 38.9 ms inside the timed
+    # window after 3 warm-ups; round 6, 6 warm-ups: still 37.0 → 38.6, profiles/r06/g3_bench.json).
+    # Flat = the last 5 steps within 1 % of each other, every rank (≥ 15 and ≤ 50 warm-up steps;
+    # each warm-up step is synchronised to read its time).
     nwarm = 0
     while True:
         one()
         nwarm += 1
         torch.cuda.synchronize()
-        last = [a.elapsed_time(b) for a, b in evs[-4:]]
-        flat = nwarm >= 5 and (max(last) - min(last)) <= 0.01 * min(last)
+        last = [a.elapsed_time(b) for a, b in evs[-5:]]
+        flat = nwarm >= 15 and (max(last) - min(last)) <= 0.01 * min(last)
         if world > 1:
             f = torch.tensor([0.0 if flat else 1.0], device=dev)
             dist.all_reduce(f, op=dist.ReduceOp.MAX)
             flat = float(f.item()) == 0.0
-        if flat or nwarm >= 40:
+        if flat or nwarm >= 50:
             break
     el = time_steps(one, args.train_steps, 0, world, dev)
     gc.unfreeze()
@@ -353,7 +354,7 @@ def bench_train(args, world, rank, dev, feat):
                                                        sorted(per_o[1:])[len(per_o[1:]) // 2], 4)
                            if len(per_o) > 2 else None,
                            "in_order": [round(x, 2) for x in per_o]},
-           "steps": args.train_steps, "warmup": nwarm, "warmup_rule": "until the last 4 steps are within 1 %",
+           "steps": args.train_steps, "warmup": nwarm, "warmup_rule": "at least 15, until the last 5 steps are within 1 %",
            "global_batch": gb, "n_gpus": world,
            "allreduce_bytes": 4 * nparam if world > 1 else 0,
            "buckets": len(step.grads.buckets),
