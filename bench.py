@@ -313,23 +313,28 @@ def bench_train(args, world, rank, dev, feat):
     # a generation-2 collection inside the timed steps: collect once, then freeze them
     gc.collect()
     gc.freeze()
-    # warm up until the per-step device time is flat: the GPU clock settles under the step's
-    # sustained load over its first ≈ 10–15 steps (round 5: 37.0 → 38.9 ms inside the timed
-    # window after 3 warm-ups; round 6, 6 warm-ups: still 37.0 → 38.6, profiles/r06/g3_bench.json).
-    # Flat = the last 5 steps within 1 % of each other, every rank (≥ 15 and ≤ 50 warm-up steps;
-    # each warm-up step is synchronised to read its time).
-    nwarm = 0
-    while True:
-        one()
-        nwarm += 1
+    # warm up until the per-step device time is flat under the timed region's load: bursts of 6
+    # back-to-back steps (a sync only at the end of a burst — per-step syncs leave the GPU idle
+    # while the host refills the queue, and the clock then settles higher than under the
+    # back-to-back timed steps: round 6, 18 per-step-synchronised warm-ups still drifted 37.0 →
+    # 38.4 ms, profiles/r06/g10_bench.json).  Flat = the burst's last 4 steps within 1 % and its
+    # median within 1 % of the previous burst's, every rank (≥ 2 and ≤ 8 bursts).
+    nwarm, prev_med = 0, None
+    for burst in range(8):
+        for _ in range(6):
+            one()
+        nwarm += 6
         torch.cuda.synchronize()
-        last = [a.elapsed_time(b) for a, b in evs[-5:]]
-        flat = nwarm >= 15 and (max(last) - min(last)) <= 0.01 * min(last)
+        last = sorted(a.elapsed_time(b) for a, b in evs[-4:])
+        med = sorted(a.elapsed_time(b) for a, b in evs[-6:])[3]
+        flat = (burst >= 1 and last[-1] - last[0] <= 0.01 * last[0] and prev_med is not None and
+                abs(med - prev_med) <= 0.01 * prev_med)
+        prev_med = med
         if world > 1:
             f = torch.tensor([0.0 if flat else 1.0], device=dev)
             dist.all_reduce(f, op=dist.ReduceOp.MAX)
             flat = float(f.item()) == 0.0
-        if flat or nwarm >= 50:
+        if flat:
             break
     el = time_steps(one, args.train_steps, 0, world, dev)
     gc.unfreeze()
@@ -337,6 +342,12 @@ def bench_train(args, world, rank, dev, feat):
     per_o = [a.elapsed_time(b) for a, b in evs[nwarm:]]  # the timed steps, in order
     per = sorted(per_o)
     nparam = sum(p.numel() for p in step.grads.params)
+    in_sync = None
+    if world > 1:  # every replica applied the same all-reduced update: parameters identical
+        cs = torch.stack([p.detach().double().sum() for p in step.grads.params]).sum().reshape(1)
+        allc = [torch.zeros_like(cs) for _ in range(world)]
+        dist.all_gather(allc, cs)
+        in_sync = all(bool(torch.equal(c, allc[0])) for c in allc)
     gb = world * args.train_batch
     which = ("BASELINE configs[3]" if (world, args.train_batch, args.size, args.iters) == (8, 16, 256, 8)
              else f"configs[3]'s per-GPU shard at N={world} (configs[3] itself is N=8, global batch 128)")
@@ -354,9 +365,10 @@ def bench_train(args, world, rank, dev, feat):
                                                        sorted(per_o[1:])[len(per_o[1:]) // 2], 4)
                            if len(per_o) > 2 else None,
                            "in_order": [round(x, 2) for x in per_o]},
-           "steps": args.train_steps, "warmup": nwarm, "warmup_rule": "at least 15, until the last 5 steps are within 1 %",
+           "steps": args.train_steps, "warmup": nwarm, "warmup_rule": "bursts of 6 back-to-back steps until a burst is flat (last 4 within 1 %, median within 1 % of the previous burst's)",
            "global_batch": gb, "n_gpus": world,
            "allreduce_bytes": 4 * nparam if world > 1 else 0,
+           "replicas_in_sync": in_sync,
            "buckets": len(step.grads.buckets),
            "loss_first_last": [round(float(losses[0]), 4), round(float(losses[-1]), 4)]}
     del step, ref, batch

@@ -118,9 +118,9 @@ long long scflow_corr_lookup_conv1x1_lds_bytes(void);
 #define SCFLOW_ABI_VERSION 2
 int scflow_abi_version(void);
 long long scflow_conv_args_size(void);
-/* Tuning only: launch-time environment switches (SCFLOW_WINO4_DEPTH, SCFLOW_GNR_CB,
- * SCFLOW_SMALLCIN_SPLIT, SCFLOW_SMALLCIN_WGS) are read once and cached; this makes their next
- * use re-read the environment (in-process A/B). */
+/* Tuning only: launch-time environment switches (SCFLOW_WINO4_DEPTH, SCFLOW_WINO4_XCD,
+ * SCFLOW_GNR_CB, SCFLOW_SMALLCIN_SPLIT, SCFLOW_SMALLCIN_WGS, SCFLOW_THINZ) are read once and
+ * cached; this makes their next use re-read the environment (in-process A/B). */
 int scflow_debug_reload_switches(void);
 /* Profiling only: later LDS-kernel lookups (scflow_corr_lookup*) write 6 u64 real-time-clock
  * stamps per workgroup of 16 query pixels to `stamps` (phase boundaries; NULL turns it off). */
@@ -183,6 +183,13 @@ typedef struct scflow_conv_args {
  * the 36 point GEMMs with the output transform in their epilogue.  fp32 throughout; error vs fp64
  * ≈ 10× a direct fp32 conv's (points {0, ±1, 2, −½, ∞}). */
 #define SCFLOW_CONV_WINO4 4
+/* Two independent convolutions (neither reads what the other writes, no overlapping outputs) in
+ * ONE grouped launch when a paired kernel covers the pair — the decoder tail's flow-predictor /
+ * mask-predictor branches: 3×3 256→2 with 1×1 256→1, 7×7 2→128 with 3×3 1→64, two F(2×2,3×3)
+ * convs of one width — else as two scflow_conv2d launches in order; results equal the separate
+ * launches bit for bit (round 6; replaces running the two branches on two streams joined by
+ * events, scflow_decoder.py:211-218). */
+int scflow_conv2d_pair(const scflow_conv_args* args_a, const scflow_conv_args* args_b, void* stream);
 /* Bytes of args.ws a launch needs (0 for packing formats without a workspace). */
 long long scflow_conv_workspace_bytes(const scflow_conv_args* args);
 

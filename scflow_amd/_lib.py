@@ -137,6 +137,7 @@ SIGNATURES = {
     "scflow_conv_pick_bk": (c_int, [ctypes.POINTER(ConvArgs)]),
     "scflow_conv_workspace_bytes": (ctypes.c_longlong, [ctypes.POINTER(ConvArgs)]),
     "scflow_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_vp]),
+    "scflow_conv2d_pair": (c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(ConvArgs), c_vp]),
     "scflow_pose_update": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp]),
     "scflow_lift_points": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_pose_flow": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp]),

@@ -438,6 +438,9 @@ __device__ __forceinline__ void sc_stamp(unsigned long long* st, int k) {
   if (st && threadIdx.x == 0)
     st[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + k] = __builtin_amdgcn_s_memrealtime();
 }
+__device__ __forceinline__ void sc_stamp_id(unsigned long long* st, int sid, int k) {
+  if (st && threadIdx.x == 0) st[(size_t)sid * 4 + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // small-cin conv on MFMA: K = taps·cin (≤ 98) walked in k-pairs — one v_mfma_f32_32x32x2_f32
 // per pair (for cin = 2 a pair is the two channels of one tap, for cin = 1 two taps).  Tile =
@@ -451,10 +454,13 @@ __device__ __forceinline__ void sc_stamp(unsigned long long* st, int k) {
 // 512 — 57 µs alone, 214 µs in the decoder beside other kernels.  Walking tiles, the weights are
 // loaded once per workgroup and the next tile's halo is in flight (registers, then the other LDS
 // buffer) during this tile's MFMAs and stores: one barrier per tile.
+// body: workgroup blk of nblk walking tiles, channel slice cby (grid.y of the split launch),
+// stamps at slot sid (conv_pair.h launches two bodies in one grid)
 template <int CIN, int KH, int KW, int NBW>
-__global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_args a, int oh, int ow,
-                                                                 int npad, int ntiles,
-                                                                 unsigned long long* stamps) {
+__device__ __forceinline__ void conv_smallcin_mfma_body(const scflow_conv_args& a, int oh, int ow,
+                                                        int npad, int ntiles, int blk, int nblk,
+                                                        int cby, unsigned long long* stamps,
+                                                        int sid) {
   constexpr int K = KH * KW * CIN;
   constexpr int KP = (K + 1) / 2;  // MFMA k-steps
   extern __shared__ float halo[];  // 2 × [(tr+KH-1)][(ow+KW-1)][CIN]
@@ -463,8 +469,8 @@ __global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_
   const int tiles_per_img = oh / tr;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 1, wn = wave >> 1, li = lane & 31, hh = lane >> 5;
-  const int cb = blockIdx.y * NBW * 64;  // channel slice of this workgroup (grid.y splits npad)
-  sc_stamp(stamps, 0);
+  const int cb = cby * NBW * 64;  // channel slice of this workgroup (grid.y splits npad)
+  sc_stamp_id(stamps, sid, 0);
   // the halo's global loads (at most SC_NH per thread: W 32 → (KH+1) × (31+KW) · CIN floats,
   // W 64 → KH × (63+KW) · CIN, the only widths dispatched here) as buffer loads: a padding or
   // tail element reads offset 0x7ffffff0, beyond the resource, as 0 — no branches, whose waits
@@ -496,7 +502,7 @@ __global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_
       if (i < nh) halo[buf * nh + i] = hv[j];
     }
   };
-  int t = blockIdx.x;
+  int t = blk;
   hfetch(t);
   // B fragments (k = 2·kp + hh, column = cb + wn·NBW·32 + nb·32 + li) and the bias, in flight
   // together with the first halo
@@ -513,7 +519,7 @@ __global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_
   }
   hput(0);
   __syncthreads();
-  sc_stamp(stamps, 1);
+  sc_stamp_id(stamps, sid, 1);
   const int m = wm * 32 + li;  // this lane's A row (output pixel of the tile)
   const int pbase = ((m / ow) * hc + (m % ow)) * CIN;
   // epilogue; C/D layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5).  The activation is
@@ -534,9 +540,12 @@ __global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_
       }
     }
   };
-  for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
+  // (the stride as a wave-uniform value: as a plain int argument the compiler kept the tile
+  // loop's state in VGPRs — 256 registers and spills for the 7×7)
+  const int stride = __builtin_amdgcn_readfirstlane(nblk);
+  for (int it = 0; t < ntiles; ++it, t += stride) {
     const int buf = it & 1;
-    const int tn = t + gridDim.x;
+    const int tn = t + stride;
     const bool more = tn < ntiles;  // workgroup-uniform
     if (more) hfetch(tn);           // the next tile's halo in flight under this tile's MFMAs
     __builtin_amdgcn_sched_barrier(0);
@@ -546,15 +555,20 @@ __global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_
     for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[nb][e] = 0.f;
-#pragma unroll
-    for (int kp = 0; kp < KP; ++kp) {
+    // k-steps in groups of 7 behind scheduling barriers: the A reads of a group are issued
+    // together, but not all 49 of a 7×7 at once (49 VGPRs of prefetch on top of the 98 B
+    // fragments pushed the kernel to 256 VGPRs and spills)
+    auto kstep = [&](auto kpc) __attribute__((always_inline)) {
+      constexpr int kp = decltype(kpc)::value;
       const int k = 2 * kp + hh;
       const int tap = (k < K ? k : 0) / CIN, c = (k < K ? k : 0) % CIN;
       const float av = k < K ? hb[pbase + ((tap / KW) * hc + tap % KW) * CIN + c] : 0.f;
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb)
         acc[nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw[nb][kp], acc[nb], 0, 0, 0);
-    }
+      if constexpr (kp % 7 == 6) __builtin_amdgcn_sched_barrier(0);
+    };
+    StaticFor<0, KP>::run(kstep);
     switch (a.act) {
       case SCFLOW_ACT_RELU: store(std::integral_constant<int, SCFLOW_ACT_RELU>{}, acc, t); break;
       case SCFLOW_ACT_SIGMOID: store(std::integral_constant<int, SCFLOW_ACT_SIGMOID>{}, acc, t); break;
@@ -565,10 +579,19 @@ __global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_
     __syncthreads();
   }
   if (stamps) {
-    sc_stamp(stamps, 2);
+    sc_stamp_id(stamps, sid, 2);
     __builtin_amdgcn_s_waitcnt(0);
-    sc_stamp(stamps, 3);
+    sc_stamp_id(stamps, sid, 3);
   }
+}
+
+template <int CIN, int KH, int KW, int NBW>
+__global__ __launch_bounds__(256, 2) void conv_smallcin_mfma_kernel(scflow_conv_args a, int oh, int ow,
+                                                                 int npad, int ntiles,
+                                                                 unsigned long long* stamps) {
+  conv_smallcin_mfma_body<CIN, KH, KW, NBW>(a, oh, ow, npad, ntiles, blockIdx.x, gridDim.x,
+                                            blockIdx.y, stamps,
+                                            blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // generic small-cin fallback (any kernel size): thread = pixel, 16 channels per thread
@@ -622,7 +645,8 @@ constexpr int thin_na(int kh, int kw) {  // float4 per thread of one chunk's hal
 }
 
 template <int COUT, int KH, int KW>
-__global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int oh, int ow) {
+__device__ __forceinline__ void conv_thin_body(const scflow_conv_args& a, int oh, int ow, int blk,
+                                               int nblk) {
   constexpr int NA = thin_na(KH, KW);
   // [(tr+KH-1)*(ow+KW-1)][THIN_LD], reused for the reduction; float4-typed so the halo accesses
   // are ds_write_b128 / ds_read_b128 (a float array's unknown alignment split the 16-B stores
@@ -636,8 +660,7 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
   // XCD-aware tile order (as conv_thin_full_kernel): each XCD covers a contiguous run of row
   // tiles, so the halo rows neighbouring tiles share come from that XCD's L2 — in dispatch order
   // the three tiles reading an input row sat on three XCDs, each fetching it from the MALL
-  const int bid = gridDim.x % 8 ? (int)blockIdx.x
-                                : (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
+  const int bid = nblk % 8 ? blk : (blk % 8) * (nblk / 8) + blk / 8;
   const int img = bid / tiles_per_img;
   const int oy0 = (bid % tiles_per_img) * tr;
   const int cin = a.c0 + a.c1;
@@ -726,6 +749,11 @@ __global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int 
       a.out[pix * a.so + o] = act_apply(v + b, a.act);
     }
   }
+}
+
+template <int COUT, int KH, int KW>
+__global__ __launch_bounds__(256) void conv_thin_kernel(scflow_conv_args a, int oh, int ow) {
+  conv_thin_body<COUT, KH, KW>(a, oh, ow, blockIdx.x, gridDim.x);
 }
 
 // thin conv, whole halo at once (the decoder's XHead predictors, 256 → 2 / 1, raft_decoder.py:
@@ -847,6 +875,8 @@ __global__ __launch_bounds__(THINF_WAVES * 64) void conv_thin_full_kernel(scflow
     sc_stamp(stamps, 3);
   }
 }
+
+#include "conv_thinz.h"
 
 // generic thin fallback: one wave per output pixel, lanes split the channels
 template <int COUT>
@@ -1043,6 +1073,14 @@ int wino_swz(int R, int C) {
 #ifndef WINO4_DEFAULT
 #define WINO4_DEFAULT 1
 #endif
+// Round 6: with the GEMM's XCD-blocked order (conv_wino4.h) out_net (256 → 126) at configs[4]
+// runs F(4×4,3×3) faster (337 → 310 µs alone, profiles/r06/g7_wino4_all_ab.txt), so convs of ≥ 120
+// output channels whose GEMM grid exceeds one round of two workgroups per CU take it too; the
+// 64-channel ones stay on F(2×2,3×3) there (flow_net.1 102 vs 110 µs, mask encoder 32 vs 50 µs;
+// every eligible conv on F(4×4): decoder 8.36k vs 8.85k iters/s).
+#ifndef WINO4_MIN_COUT_MULTI
+#define WINO4_MIN_COUT_MULTI 120
+#endif
 bool wino4_pick(const scflow_conv_args& a) {
   static int mode = -1;
   if (mode < 0) {
@@ -1050,7 +1088,10 @@ bool wino4_pick(const scflow_conv_args& a) {
     mode = e ? atoi(e) : WINO4_DEFAULT;
   }
   if (!mode || !wino4_shape(a)) return false;
-  return mode == 2 || a.cout >= WINO4_MIN_COUT;
+  if (mode == 2 || a.cout >= WINO4_MIN_COUT) return true;
+  const long long tiles = (long long)a.n * (a.h / 4) * (a.w / 4);
+  const long long wgs = (tiles + 31) / 32 * ((a.cout + 31) / 32);
+  return a.cout >= WINO4_MIN_COUT_MULTI && wgs > 2LL * device_cus();
 }
 
 
@@ -1399,21 +1440,40 @@ SCFLOW_API long long scflow_conv_workspace_bytes(const scflow_conv_args* args) {
   return wino4_workspace_bytes(*args);
 }
 
+// the thin 3×3 contraction's preconditions (conv_thinz.h; shared with conv_pair.h)
+bool thinz_ok(const scflow_conv_args& a, const Geometry& g, bool tiled) {
+  static EnvSwitch thinz_sw("SCFLOW_THINZ", 1);
+  return tiled && thinz_sw.get() && a.c1 == 0 && a.c0 == 256 && a.kh == 3 && a.kw == 3 &&
+         a.ph == 1 && a.pw == 1 && a.stride == 1 && (a.cout == 1 || a.cout == 2) &&
+         aligned16(a.weight) && ((long long)a.n * a.h * a.w * a.s0 + 256) * 4 < 0x7ffffff0LL &&
+         g.oh % (g.ow == 64 ? 4 : 2) == 0;
+}
+
+// small-cin MFMA conv workgroups: at most SCFLOW_SMALLCIN_WGS per CU (default 2), each walking
+// its tiles
+long long smallcin_blocks(int ntiles) {
+  static EnvSwitch wgs_sw("SCFLOW_SMALLCIN_WGS", 2);
+  const int per_cu = wgs_sw.get() > 0 ? wgs_sw.get() : 2;
+  const long long cap = (long long)per_cu * device_cus();
+  return ntiles < cap ? ntiles : cap;
+}
+
+#include "conv_pair.h"
+
+bool conv_args_valid(const scflow_conv_args& a) {
+  if (!a.src0 || !a.weight || a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 ||
+      a.c1 < 0 || (a.c1 > 0 && !a.src1) || a.kh <= 0 || a.kw <= 0 || a.ph < 0 || a.pw < 0)
+    return false;
+  if (a.epilogue == SCFLOW_EPI_PLAIN) return a.out != nullptr;
+  if (a.epilogue == SCFLOW_EPI_GRU_ZR) return a.gate && a.rh && a.hid && !(a.cout & 1);
+  if (a.epilogue == SCFLOW_EPI_GRU_Q) return a.gate && a.hid;
+  return false;
+}
+
 SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
   if (!args) return SCFLOW_EINVAL;
   const scflow_conv_args& a = *args;
-  if (!a.src0 || !a.weight || a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 ||
-      a.c1 < 0 || (a.c1 > 0 && !a.src1) || a.kh <= 0 || a.kw <= 0 || a.ph < 0 || a.pw < 0)
-    return SCFLOW_EINVAL;
-  if (a.epilogue == SCFLOW_EPI_PLAIN) {
-    if (!a.out) return SCFLOW_EINVAL;
-  } else if (a.epilogue == SCFLOW_EPI_GRU_ZR) {
-    if (!a.gate || !a.rh || !a.hid || (a.cout & 1)) return SCFLOW_EINVAL;
-  } else if (a.epilogue == SCFLOW_EPI_GRU_Q) {
-    if (!a.gate || !a.hid) return SCFLOW_EINVAL;
-  } else {
-    return SCFLOW_EINVAL;
-  }
+  if (!conv_args_valid(a)) return SCFLOW_EINVAL;
   if (a.bk == SCFLOW_CONV_WINO) return launch_wino(a, (hipStream_t)stream);
   if (a.bk == SCFLOW_CONV_WINO4) return launch_wino4(a, (hipStream_t)stream);
   if (a.bk == SCFLOW_CONV_1X1W) return launch_conv1x1w(a, (hipStream_t)stream);
@@ -1459,11 +1519,7 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
                          (long long)a.n * a.h * a.w * a.s0 * 4 < 0x7ffffff0LL;  // buffer offsets
     if (mfma_ok) {
       const int ntiles = a.n * (g.oh / (64 / g.ow));
-      // workgroups: at most SCFLOW_SMALLCIN_WGS per CU (default 2), each walking its tiles
-      static EnvSwitch wgs_sw("SCFLOW_SMALLCIN_WGS", 2);
-      const int per_cu = wgs_sw.get() > 0 ? wgs_sw.get() : 2;
-      const long long cap = (long long)per_cu * device_cus();
-      const unsigned blocks = (unsigned)(ntiles < cap ? ntiles : cap);
+      const unsigned blocks = (unsigned)smallcin_blocks(ntiles);
       const size_t lds = 2 * sizeof(float) * (size_t)(64 / g.ow + a.kh - 1) * (g.ow + a.kw - 1) * a.c0;
 #define SCFLOW_SCM(CI, KH_, KW_)                                                                   \
   if (a.c0 == CI && a.kh == KH_ && a.kw == KW_) {                                                  \
@@ -1510,6 +1566,24 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     return SCFLOW_EALIGN;
   const bool tiled = (g.ow == 32 || g.ow == 64) && (a.c0 % 8) == 0 && (a.c1 % 8) == 0 &&
                      g.oh % (64 / g.ow) == 0 && g.ow == a.w && g.oh == a.h;
+  // channel contraction on MFMA (conv_thinz.h): 3×3 same-padded, one 256-channel source,
+  // ≤ 2 outputs; SCFLOW_THINZ = 0 keeps the LDS kernels below (A/B)
+  // Measured (profiles/r06/g9_thinz_ab.txt): flow predictor 3×3 256 → 2 at configs[4] 81 → 51 µs
+  // alone (decoder 8.84k → 8.88k iters/s), at configs[1] 14.9 → 10.2 µs (decoder 27.49k → 27.72k).
+  // The 1×1 256 → 1 mask predictor stays on the chunked kernel (20.8 vs 33.8 µs at configs[4]:
+  // one Z column of 32 leaves the MFMAs 97 % idle; configs[1] equal, g10_thinz_mask1x1_ab.txt).
+  if (thinz_ok(a, g, tiled)) {
+    const int R = g.ow == 64 ? 4 : 2;
+    const unsigned blocks = (unsigned)(a.n * (g.oh / R));
+#define SCFLOW_THINZ(CO, W_, R_) conv_thinz_kernel<CO, 3, 3, W_, R_><<<blocks, 256, 0, st>>>(a)
+    if (g.ow == 64) {
+      if (a.cout == 2) SCFLOW_THINZ(2, 64, 4); else SCFLOW_THINZ(1, 64, 4);
+    } else {
+      if (a.cout == 2) SCFLOW_THINZ(2, 32, 2); else SCFLOW_THINZ(1, 32, 2);
+    }
+#undef SCFLOW_THINZ
+    return scflow_launch_status();
+  }
   // whole-halo variant: one source, channels a multiple of 64, the halo within 160 KB of LDS
   static const bool thin_full_off = [] {
     const char* e = getenv("SCFLOW_THIN_FULL");
@@ -1554,6 +1628,25 @@ SCFLOW_API int scflow_conv2d(const scflow_conv_args* args, void* stream) {
     default: return SCFLOW_EUNSUPPORTED;
   }
   return scflow_launch_status();
+}
+
+// Two independent convs (neither reads what the other writes) as one grouped launch when a paired
+// kernel covers them (conv_pair.h), else as two scflow_conv2d launches in order.  Results equal
+// the two separate launches bit for bit.  SCFLOW_CONV_PAIR=0 always launches separately (A/B).
+SCFLOW_API int scflow_conv2d_pair(const scflow_conv_args* args_a, const scflow_conv_args* args_b,
+                                  void* stream) {
+  if (!args_a || !args_b || !conv_args_valid(*args_a) || !conv_args_valid(*args_b))
+    return SCFLOW_EINVAL;
+  static EnvSwitch pair_sw("SCFLOW_CONV_PAIR", 1);
+  if (pair_sw.get()) {
+    hipStream_t st = (hipStream_t)stream;
+    int r = try_pair(*args_a, *args_b, st);
+    if (r == 0) r = try_pair(*args_b, *args_a, st);
+    if (r == 1) return SCFLOW_OK;
+    if (r != 0) return r;
+  }
+  const int e = scflow_conv2d(args_a, stream);
+  return e ? e : scflow_conv2d(args_b, stream);
 }
 
 // Profiling only: later Winograd launches (F(2×2,3×3) and F(4,5)) write 4 u64 real-time-clock stamps per

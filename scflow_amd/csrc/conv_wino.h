@@ -131,16 +131,22 @@ __device__ __forceinline__ void wino_stamp(unsigned long long* st, int k) {
 // into an (8/swz_c) × swz_c arrangement of row × column parts, one per XCD, so an XCD's
 // workgroups share their transformed-weight slices (column part) and input halos (row part) in
 // its L2 instead of every XCD touching every column's weights.  Host guarantees divisibility.
-__device__ __forceinline__ void wino_block(int swz_c, int& bx, int& by) {
-  bx = blockIdx.x;
-  by = blockIdx.y;
+__device__ __forceinline__ void wino_block_ex(int swz_c, int lbx, int lby, int R, int C, int& bx,
+                                              int& by) {
+  bx = lbx;
+  by = lby;
   if (swz_c <= 0) return;
-  const int R = gridDim.x, C = gridDim.y;
-  const int id = blockIdx.y * R + blockIdx.x;
+  const int id = lby * R + lbx;
   const int xcd = id & 7, slot = id >> 3;
   const int rows = R / (8 / swz_c), cols = C / swz_c;
   by = (xcd % swz_c) * cols + slot % cols;
   bx = (xcd / swz_c) * rows + slot / cols;
+}
+__device__ __forceinline__ void wino_block(int swz_c, int& bx, int& by) {
+  wino_block_ex(swz_c, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y, bx, by);
+}
+__device__ __forceinline__ void wino_stamp_id(unsigned long long* st, int sid, int k) {
+  if (st && threadIdx.x == 0) st[(size_t)sid * 4 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <int W>
@@ -174,8 +180,11 @@ constexpr size_t wino_lds_bytes() {
 // grids whose 64-channel version would leave 1.5 workgroups per CU (corr_net.1 at B = 16).
 // (A K split for the 32-channel grids — two wave sets over alternate sub-steps, sums through LDS —
 // was built in round 4 and measured in round 5: ±2 % alone, the decoder 2 % slower; removed.)
+// body: logical block (lbx, lby) of an lgx × lgy grid, stamps at slot sid (conv_pair.h
+// launches two bodies in one grid)
 template <int W, int NBW>
-__global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoParams P) {
+__device__ __forceinline__ void conv_wino_body(const WinoParams& P, int lbx, int lby, int lgx,
+                                               int lgy, int sid) {
   using G = WinoGeom<W>;
   constexpr int NT = 256;                                   // threads
   constexpr int NA = (G::NH4 + 4 * NT - 1) / (4 * NT);     // float4 per thread per quarter stage
@@ -188,8 +197,8 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   const int wave = wv & 3;                 // Winograd row i of the wave's points
   const int li = lane & 31, hh = lane >> 5;
   int bx, by;
-  wino_block(P.swz_c, bx, by);
-  wino_stamp(P.stamps, 0);
+  wino_block_ex(P.swz_c, lbx, lby, lgx, lgy, bx, by);
+  wino_stamp_id(P.stamps, sid, 0);
   // the epilogue's per-channel operands (32-channel blocks: a few VGPRs to spare), fetched now:
   // in a one-round grid every workgroup reaches its epilogue together, and loads there all wait
   // on the same few cache lines (the small-cin conv's epilogue: 6.3 → 3.4 µs)
@@ -389,7 +398,7 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   // loop-entry state with the steady state and waits for ALL loads in front of the MFMAs.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  wino_stamp(P.stamps, 1);
+  wino_stamp_id(P.stamps, sid, 1);
   floatx4 vA[4], vB[4];
   vcompute(0, 0, vA);
   inloop = true;
@@ -437,7 +446,7 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   // keeps both the b128 stores (8-lane groups) and the b128 loads (16-lane groups) conflict-free.
   constexpr int WEP = WTM + 4;
   __syncthreads();
-  wino_stamp(P.stamps, 2);
+  wino_stamp_id(P.stamps, sid, 2);
   float* S = smem;
 #pragma unroll
   for (int nb = 0; nb < NBW; ++nb)
@@ -557,8 +566,14 @@ __global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoPa
   }
   if (P.stamps) {
     __builtin_amdgcn_s_waitcnt(0);
-    wino_stamp(P.stamps, 3);
+    wino_stamp_id(P.stamps, sid, 3);
   }
+}
+
+template <int W, int NBW>
+__global__ __launch_bounds__(256, NBW >= 3 ? 1 : 2) void conv_wino_kernel(WinoParams P) {
+  conv_wino_body<W, NBW>(P, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y,
+                         blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // U = G g Gᵀ per (co, ci) (row i = 2 negated), packed [nb32][sub-step][ξ][lane][4] with

@@ -31,7 +31,7 @@ import torch.nn as nn
 from . import _lib, ops
 from ._lib import ScflowError
 from .modules import (ConvGRU, ConvModule, ConvRunner, CorrelationPyramid, CorrLookup,
-                      MotionEncoder, XHead, run_chain)
+                      MotionEncoder, XHead, run_chain, run_chain_pair)
 from .ops import Chan
 from .registry import MODELS
 
@@ -106,6 +106,12 @@ class SCFlowDecoder(nn.Module):
         self.hoist_context = True
         # independent branches on a second HIP stream (else everything on the current stream)
         self.side_stream = True
+        # the tail's flow-predictor / mask-predictor branches as paired launches on the main
+        # stream (scflow_conv2d_pair) instead of two streams joined by events (round 6).
+        # -1 = automatic: on for maps of at most 32 × 32 (configs[1]: 4.598 vs 4.612 ms per
+        # forward, the profiled iteration 550 → 538 µs with 1.9 µs idle), off above (configs[4]:
+        # 43.23 vs 43.17 ms) — profiles/r06/g11_*
+        self.pair_tail = -1
         self.dbg_skip_fullres = False  # measurement only (tools/ab_bench.py)
         # fork / join with device-scope events (no system-scope cache writeback per record)
         self.device_scope_events = True
@@ -549,9 +555,20 @@ class SCFlowDecoder(nn.Module):
                 run_chain(self.mask_pred.layers, hid, Chan(HEAD, fh, mh), N, h, w)
 
         def seg_mask_branch():
-            mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MASK), N, h, w)
-            run_chain(self.mask_encoder, Chan.whole(MASK), Chan(FM, dfc, mfc), N, h, w, s_me,
+            MK = MASKs[cur_par[0]]
+            mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MK), N, h, w)
+            run_chain(self.mask_encoder, Chan.whole(MK), Chan(FM, dfc, mfc), N, h, w, s_me,
                       hooks=self._hooks_for(None, "mask_enc1"))
+
+        def seg_tail_pair():
+            # the flow-predictor and mask-predictor branches on the main stream, their k-th
+            # launches paired into one grid each (scflow_conv2d_pair): no fork / join events
+            D2, MK = D2s[cur_par[0]], MASKs[cur_par[0]]
+            ops.conv2d_pair(flow_pred_r.args(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w),
+                            mask_pred_r.args(Chan(HEAD, fh, mh), Chan.whole(MK), N, h, w), HEAD)
+            run_chain_pair(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc),
+                           self.mask_encoder, Chan.whole(MK), Chan(FM, dfc, mfc), N, h, w, s_dfe,
+                           s_me)
 
         def seg_flow_pred():
             D2 = D2s[cur_par[0]]
@@ -566,6 +583,13 @@ class SCFlowDecoder(nn.Module):
         # previous iteration's deferred launch reads its Δflow on the side stream while this
         # iteration's flow predictor writes the other one on the main stream
         D2s = [D2, torch.empty_like(D2)] if defer else [D2, D2]
+        # the mask likewise (read by the previous iteration's deferred launch on the side stream
+        # while this iteration's mask predictor writes the other one — on the main stream when
+        # the tail is paired)
+        MASKs = [MASK, torch.empty_like(MASK)] if defer else [MASK, MASK]
+        pt = self.pair_tail if self.pair_tail >= 0 else int(h * w <= 32 * 32)
+        pair_tail = (bool(pt) and len(self.delta_flow_encoder) == len(self.mask_encoder) and
+                     not (self.mask_flow or self.mask_corr))
         cur_par = [0]
         pending = []  # the previous iteration's deferred full-resolution launches
         if defer:  # the deferred launches' pose outputs (duplicates of o_R / o_t: not read)
@@ -631,18 +655,23 @@ class SCFlowDecoder(nn.Module):
             if pp is not None:
                 pp[1](it)
             yield "heavy"
-            # mask predictor + mask encoder (a5, a6) on the side stream, after the previous
-            # iteration's deferred full-resolution outputs (they read its MASK; the side branch
-            # is the shorter one here)
-            fork()
-            with torch.cuda.stream(side):
-                segment("mask_branch", seg_mask_branch)
-            # flow predictor + Δflow encoder (into this iteration's Δflow buffer)
             cur_par[0] = it % 2 if defer else 0
-            segment("flow_pred" + (par if defer else ""), seg_flow_pred)
-            join()
+            if pair_tail:
+                # flow predictor + Δflow encoder ‖ mask predictor + mask encoder (a5, a6) as
+                # paired launches on this stream
+                segment("tail_pair" + (par if defer else ""), seg_tail_pair)
+            else:
+                # mask predictor + mask encoder (a5, a6) on the side stream, after the previous
+                # iteration's deferred full-resolution outputs (they read its MASK; the side
+                # branch is the shorter one here)
+                fork()
+                with torch.cuda.stream(side):
+                    segment("mask_branch" + (par if defer else ""), seg_mask_branch)
+                # flow predictor + Δflow encoder (into this iteration's Δflow buffer)
+                segment("flow_pred" + (par if defer else ""), seg_flow_pred)
+                join()
             if mask_lr is not None:
-                mask_lr = MASK
+                mask_lr = MASKs[cur_par[0]]
             # a7 pose head on cat[h, Δflow feat, mask feat] (two channel sources, no concat)
             segment("pose_trunk", seg_pose_trunk)
             drot, dtr = o_drot[it], o_dt[it]
@@ -658,7 +687,7 @@ class SCFlowDecoder(nn.Module):
                         last = j == iters - 1
                         hc, pc, fc = [], [], []
                         step = (o_drot[j], o_dt[j], Rp, tp, K, points, o_R[j], o_t[j],
-                                o_flow_pose[j], invalid, F2s[j % 2], D2s[j % 2], MASK, o_flow_pred[j],
+                                o_flow_pose[j], invalid, F2s[j % 2], D2s[j % 2], MASKs[j % 2], o_flow_pred[j],
                                 o_mask[j], h, w, float(scale))
                         nxt = dict(lr_next=None if last else Chan.whole(F2s[(j + 1) % 2]),
                                    hx_next=None if last else hx_flow,
@@ -704,7 +733,7 @@ class SCFlowDecoder(nn.Module):
             else:
                 self.pose_pred.heads_hip(pose_x[0], label, drot, dtr)
                 # a11 ↑: flow_pred = 8·up(flow + Δflow), mask ↑
-                ops.flow_upsample(F2, D2s[0], MASK, N, h, w, H, W, float(scale), o_flow_pred[it],
+                ops.flow_upsample(F2, D2s[0], MASKs[0], N, h, w, H, W, float(scale), o_flow_pred[it],
                                   o_mask[it])
                 # a8 + a10: pose update + pose-induced flow (one launch)
                 self._hook("pose_flow", True)
@@ -716,6 +745,10 @@ class SCFlowDecoder(nn.Module):
             drots.append(drot)
             dts.append(dtr)
             yield "tail"
+        if pair_tail:
+            # with the tail paired on the main stream the side stream's last work (the deferred
+            # full-resolution outputs queued in the last iteration) is not joined inside the loop
+            join()
 
         return (list(o_flow_pose.unbind(0)), list(o_flow_pred.unbind(0)), list(o_R.unbind(0)),
                 list(o_t.unbind(0)), list(o_mask.unbind(0)), drots, dts)

@@ -152,6 +152,14 @@ class ConvRunner:
             self._key = key
         return self._packed, self._bias
 
+    def args(self, src0: Chan, out: Optional[Chan], n: int, h: int, w: int,
+             src1: Optional[Chan] = None, epilogue: int = EPI_PLAIN, gate: Optional[Chan] = None,
+             rh: Optional[Chan] = None, hid: Optional[Chan] = None,
+             bias_map: Optional[Chan] = None):
+        """``run``'s scflow_conv_args (weights packed now; the runner keeps them) without
+        launching — for ``ops.conv2d_pair``."""
+        return self.bind(src0, out, n, h, w, src1, epilogue, gate, rh, hid, bias_map).args
+
     def bind(self, src0: Chan, out: Optional[Chan], n: int, h: int, w: int,
              src1: Optional[Chan] = None, epilogue: int = EPI_PLAIN, gate: Optional[Chan] = None,
              rh: Optional[Chan] = None, hid: Optional[Chan] = None,
@@ -368,6 +376,25 @@ def run_chain(layers: Sequence[ConvModule], src: Chan, dst: Chan, n: int, h: int
         if hk is not None:
             ops.host_call(lambda hk=hk: hk(False))
         cur = out
+
+
+def run_chain_pair(chain_a: Sequence[ConvModule], src_a: Chan, dst_a: Chan,
+                   chain_b: Sequence[ConvModule], src_b: Chan, dst_b: Chan, n: int, h: int, w: int,
+                   scratch_a: Sequence[Tensor], scratch_b: Sequence[Tensor]) -> None:
+    """Two independent ``run_chain``s of equal length, layer i of both as one
+    ``ops.conv2d_pair`` launch (a grouped kernel where one covers the pair, else two launches):
+    the decoder's flow-predictor and mask-predictor branches on one stream, no events."""
+    if len(chain_a) != len(chain_b):
+        raise ValueError("run_chain_pair: chains of different lengths")
+    cur_a, cur_b = src_a, src_b
+    for i, (ma, mb) in enumerate(zip(chain_a, chain_b)):
+        last = i == len(chain_a) - 1
+        out_a = dst_a if last else Chan.whole(scratch_a[i])
+        out_b = dst_b if last else Chan.whole(scratch_b[i])
+        ra = ConvRunner.of(ma.conv, ma.act_type)
+        rb = ConvRunner.of(mb.conv, mb.act_type)
+        ops.conv2d_pair(ra.args(cur_a, out_a, n, h, w), rb.args(cur_b, out_b, n, h, w), cur_a.buf)
+        cur_a, cur_b = out_a, out_b
 
 
 # ---------------------------------------------------------------------------------- a4

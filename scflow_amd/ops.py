@@ -345,6 +345,13 @@ def conv2d(src0: Chan, packed: Tensor, bias: Optional[Tensor], n: int, h: int, w
     _launch("scflow_conv2d", src0.buf,ctypes.byref(a))
 
 
+def conv2d_pair(args_a, args_b, dev_tensor: Tensor) -> None:
+    """scflow_conv2d_pair: two independent convs (argument structs from ``ConvRunner.args``; the
+    runners keep their packed weights) as one grouped launch where a paired kernel covers them,
+    else two launches in order — bit-identical to the separate launches."""
+    _launch("scflow_conv2d_pair", dev_tensor, ctypes.byref(args_a), ctypes.byref(args_b))
+
+
 class BoundLaunch:
     """A C-ABI launch whose argument struct is built once (pointers of persistent buffers):
     calling it costs one ctypes call on the caller's current stream.  The decoder binds every

@@ -92,19 +92,21 @@ def test_decoder_matches_oracle_b4_8iters(hoist):
 def test_decoder_schedules_bit_identical():
     """The launch schedule does not change the arithmetic: the fused iteration tail
     (scflow_pose_step, double-buffered ↓8 flow) vs separate launches, the side stream vs one
-    stream, device-scope vs default events give bit-identical outputs (every one of the 7
-    lists, every iteration)."""
+    stream, device-scope vs default events, the tail branches paired (scflow_conv2d_pair) vs on
+    two streams give bit-identical outputs (every one of the 7 lists, every iteration)."""
     inp = decoder_inputs(2, 256, seed=13)
     dec = build_decoder(3, seed=4)
     base = run_gpu(dec, inp)
-    for fuse, side, dse in ((False, True, True), (True, False, True), (False, False, True),
-                            (True, True, False)):
+    for fuse, side, dse, pair in ((False, True, True, 1), (True, False, True, 1),
+                                  (False, False, True, 1), (True, True, False, 1),
+                                  (True, True, True, 0), (False, True, True, 0)):
         dec.fuse_tail, dec.side_stream, dec.device_scope_events = fuse, side, dse
+        dec.pair_tail = pair  # round 6: the tail's two branches paired on one stream, or two streams
         out = run_gpu(dec, inp)
         for a, b in zip(base, out):
             for x, y in zip(a, b):
-                assert torch.equal(x, y), (fuse, side, dse)
-    dec.fuse_tail, dec.side_stream, dec.device_scope_events = True, True, True
+                assert torch.equal(x, y), (fuse, side, dse, pair)
+    dec.fuse_tail, dec.side_stream, dec.device_scope_events, dec.pair_tail = True, True, True, -1
 
 
 @pytest.mark.gpu

@@ -249,6 +249,31 @@ def test_conv2d_smallcin_tile_walk(ops, case, wgs, monkeypatch):
     close(got, ref, 2e-6 * np.sqrt(c0 * k * k) * 4, 1e-5, f"small-cin conv {case} wgs={wgs}")
 
 
+@pytest.mark.parametrize("thinz", ["1", "0"])
+@pytest.mark.parametrize("case", [
+    (16, 32, 32, 256, 0, 2, 3, 1, None),      # XHead flow predictor, configs[1]
+    (3, 64, 64, 256, 0, 2, 3, 1, None),       # configs[4] width (4-row workgroups)
+    (2, 64, 64, 256, 0, 1, 3, 1, "Sigmoid"),  # one output
+    (5, 32, 32, 256, 0, 1, 3, 1, "Tanh"),
+    (16, 32, 32, 256, 0, 1, 1, 0, "Sigmoid"),  # XHead mask predictor 1×1, configs[1]
+    (3, 64, 64, 256, 0, 1, 1, 0, "Sigmoid"),   # and at configs[4] width
+])
+def test_conv2d_thin_contraction(ops, case, thinz, monkeypatch):
+    """The thin 3×3 conv as a channel contraction on MFMA (round 6, conv_thinz.h: Z = X·W per input
+    pixel, then the taps summed over Z) and the LDS kernels it replaces (SCFLOW_THINZ=0), against
+    the fp64 conv (image borders: zero padding in both directions)."""
+    from scflow_amd._lib import reload_switches
+    monkeypatch.setenv("SCFLOW_THINZ", thinz)
+    reload_switches()
+    try:
+        n, h, w, c0, c1, cout, k, pad, act = case
+        got, ref = _conv_case(ops, n, h, w, c0, c1, cout, k, pad, act, seed=11)
+    finally:
+        monkeypatch.delenv("SCFLOW_THINZ")
+        reload_switches()
+    close(got, ref, 2e-6 * np.sqrt(c0 * k * k) * 4, 1e-5, f"thin conv {case} thinz={thinz}")
+
+
 @pytest.mark.parametrize("bk", [8, 16])
 @pytest.mark.parametrize("case", [
     (2, 32, 32, 324, 0, 256, 1, 0, "ReLU"),
@@ -275,6 +300,9 @@ def test_conv_pick_bk_prefers_resident_grids(ops, monkeypatch):
     assert ops.conv_pick_bk(16, 32, 32, 256, 0, 192, 3, 3, 1, 1) == CONV_WINO4  # corr_net.1
     assert ops.conv_pick_bk(16, 32, 32, 128, 0, 512, 3, 3, 1, 1) == CONV_WINO4  # XHead hidden
     assert ops.conv_pick_bk(16, 32, 32, 192, 64, 126, 3, 3, 1, 1) == CONV_WINO  # out_net
+    # configs[4] (64×64 maps, multi-round grids): out_net on F(4×4,3×3), the 64-wide ones not
+    assert ops.conv_pick_bk(32, 64, 64, 192, 64, 126, 3, 3, 1, 1) == CONV_WINO4
+    assert ops.conv_pick_bk(32, 64, 64, 128, 0, 64, 3, 3, 1, 1) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 1, 5, 0, 2) == CONV_WINO
     assert ops.conv_pick_bk(16, 32, 32, 128, 128, 256, 5, 1, 2, 0) == CONV_WINO
     from scflow_amd._lib import CONV_1X1W
@@ -797,3 +825,55 @@ def test_corr_lookup_conv1x1_fused_bit_identical(ops, n, h, w, seed, far):
     ref = torch.relu(corr.double().cpu() @ conv.weight.detach().double().cpu().view(256, 324).T +
                      conv.bias.detach().double().cpu())
     close(fused[:, 4:], ref, 1e-4, 1e-5, "fused lookup + conv vs fp64")
+
+
+@pytest.mark.parametrize("size", [32, 64])
+def test_conv2d_pair_bit_identical(ops, size, monkeypatch):
+    """scflow_conv2d_pair (round 6: the decoder tail's flow-predictor / mask-predictor branches as
+    grouped launches) equals the two separate scflow_conv2d launches bit for bit, for each paired
+    kernel (thin 3×3 256→2 ‖ 1×1 256→1, small-cin 7×7 2→128 ‖ 3×3 1→64, F(2×2,3×3) 128→64 ‖
+    64→32), in both argument orders, and with pairing off (SCFLOW_CONV_PAIR=0)."""
+    from scflow_amd._lib import reload_switches
+    from scflow_amd.modules import ConvRunner
+    g = torch.Generator().manual_seed(17)
+    n, h, w = (6, size, size)
+    M = n * h * w
+
+    def conv(cin, cout, k, act):
+        c = torch.nn.Conv2d(cin, cout, k, padding=k // 2)
+        with torch.no_grad():
+            c.weight.copy_(torch.randn(c.weight.shape, generator=g) / np.sqrt(c.weight[0].numel()))
+            c.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+        return ConvRunner([c.cuda()], act)
+
+    head = torch.randn(M, 512, generator=g).cuda()
+    cases = [  # (runner a, src a, cout a), (runner b, src b, cout b)
+        ((conv(256, 2, 3, None), ops.Chan(head, 0, 256), 2),
+         (conv(256, 1, 1, "Sigmoid"), ops.Chan(head, 256, 256), 1)),
+        ((conv(2, 128, 7, "ReLU"), ops.Chan.whole(torch.randn(M, 2, generator=g).cuda()), 128),
+         (conv(1, 64, 3, "ReLU"), ops.Chan.whole(torch.randn(M, 1, generator=g).cuda()), 64)),
+        ((conv(128, 64, 3, "ReLU"), ops.Chan.whole(torch.randn(M, 128, generator=g).cuda()), 64),
+         (conv(64, 32, 3, "ReLU"), ops.Chan.whole(torch.randn(M, 64, generator=g).cuda()), 32)),
+    ]
+    for (ra, sa, ca), (rb, sb, cb) in cases:
+        ref_a = torch.full((M, ca), 7.0, device="cuda")
+        ref_b = torch.full((M, cb), 7.0, device="cuda")
+        ra.run(sa, ops.Chan.whole(ref_a), n, h, w)
+        rb.run(sb, ops.Chan.whole(ref_b), n, h, w)
+        for order in (0, 1):
+            for pair in ("1", "0"):
+                monkeypatch.setenv("SCFLOW_CONV_PAIR", pair)
+                reload_switches()
+                out_a = torch.full((M, ca), 7.0, device="cuda")
+                out_b = torch.full((M, cb), 7.0, device="cuda")
+                aa = ra.args(sa, ops.Chan.whole(out_a), n, h, w)
+                ab = rb.args(sb, ops.Chan.whole(out_b), n, h, w)
+                if order:
+                    ops.conv2d_pair(ab, aa, head)
+                else:
+                    ops.conv2d_pair(aa, ab, head)
+                torch.cuda.synchronize()
+                assert torch.equal(out_a, ref_a), (ca, cb, order, pair)
+                assert torch.equal(out_b, ref_b), (ca, cb, order, pair)
+    monkeypatch.delenv("SCFLOW_CONV_PAIR")
+    reload_switches()
