@@ -300,14 +300,17 @@ def bench_train(args, world, rank, dev, feat):
     step = TrainStep(ref, pts, synthetic.YCBV_DIAMETERS)
     losses = []
     evs = []
+    host = []  # host seconds per step call (launching it; the step syncs only where it must)
 
     def one():
         # device events on the caller's stream around each step (the step orders itself after
         # and before it): the step's span on the GPU timeline, idle gaps inside it included
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
         a.record()
         losses.append(step(batch)["loss"].detach())
         b.record()
+        host.append(time.perf_counter() - t0)
         evs.append((a, b))
     # the objects the earlier legs left (decoder / refiner graphs, buffers) must not be scanned by
     # a generation-2 collection inside the timed steps: collect once, then freeze them
@@ -364,7 +367,11 @@ def bench_train(args, world, rank, dev, feat):
                            "spread_after_first": round((max(per_o[1:]) - min(per_o[1:])) /
                                                        sorted(per_o[1:])[len(per_o[1:]) // 2], 4)
                            if len(per_o) > 2 else None,
-                           "in_order": [round(x, 2) for x in per_o]},
+                           "in_order": [round(x, 2) for x in per_o],
+                           # the host's time per step call, timed steps in order: a host slower
+                           # than the device shows up as device spans that follow it
+                           "host_in_order": [round(1e3 * x, 2) for x in host[nwarm:]],
+                           "warmup_in_order": [round(a.elapsed_time(b), 2) for a, b in evs[:nwarm]]},
            "steps": args.train_steps, "warmup": nwarm, "warmup_rule": "bursts of 6 back-to-back steps until a burst is flat (last 4 within 1 %, median within 1 % of the previous burst's)",
            "global_batch": gb, "n_gpus": world,
            "allreduce_bytes": 4 * nparam if world > 1 else 0,

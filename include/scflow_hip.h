@@ -112,10 +112,11 @@ int scflow_corr_lookup_conv1x1(const float* pyr, const float* flow, const float*
 long long scflow_corr_lookup_conv1x1_lds_bytes(void);
 /* ABI markers: scflow_abi_version() returns SCFLOW_ABI_VERSION of the header the library was
  * built from (2: scflow_conv_args ends with the F(4×4,3×3) workspace fields ws / ws_bytes, and
- * scflow_conv_pick_bk may return SCFLOW_CONV_WINO4); scflow_conv_args_size() its
+ * scflow_conv_pick_bk may return SCFLOW_CONV_WINO4; 3: + scflow_xhead_pred and its workspace
+ * query); scflow_conv_args_size() its
  * sizeof(scflow_conv_args).  A binding checks both before its first call (scflow_amd/_lib.py
  * does, at load). */
-#define SCFLOW_ABI_VERSION 2
+#define SCFLOW_ABI_VERSION 3
 int scflow_abi_version(void);
 long long scflow_conv_args_size(void);
 /* Tuning only: launch-time environment switches (SCFLOW_WINO4_DEPTH, SCFLOW_WINO4_XCD,
@@ -190,6 +191,24 @@ typedef struct scflow_conv_args {
  * launches bit for bit (round 6; replaces running the two branches on two streams joined by
  * events, scflow_decoder.py:211-218). */
 int scflow_conv2d_pair(const scflow_conv_args* args_a, const scflow_conv_args* args_b, void* stream);
+/* The XHeads (raft_decoder.py:256-294, called at scflow_decoder.py:211-218): the two hidden 3×3
+ * convs as ONE F(4×4,3×3) conv `hidden` (SCFLOW_CONV_WINO4, flow head's channels first —
+ * flow_channels of hidden->cout —, ReLU, bias only; hidden->out is not written) with both
+ * predictors contracted in its epilogue, then one launch summing the 32-channel blocks' partial
+ * sums and the 3×3 predictor's taps (round 6; replaces the hidden conv's 2 KiB-per-pixel output
+ * and the predictor convs that read it back).  pred_w [hidden->cout][20]: row c < flow_channels
+ * holds the 3×3 two-output predictor's weights W[o][c][ty][tx] at column (3·ty + tx)·2 + o (18
+ * used), row c ≥ flow_channels the 1×1 one-output predictor's W[0][c − flow_channels] at column 0.
+ * flow_out [pixel][flow_stride] (2 channels) = flow_act(flow_bias + conv), mask_out
+ * [pixel][mask_stride] = mask_act(mask_bias + conv) (biases may be NULL).  workspace ≥
+ * scflow_xhead_pred_workspace_bytes, 16-byte aligned.  Width 32 or 64, height a multiple of 4,
+ * both heads' hidden channels multiples of 32; else SCFLOW_EUNSUPPORTED.  fp32; only the
+ * summation order differs from the separate convs. */
+long long scflow_xhead_pred_workspace_bytes(int n, int h, int w, int flow_channels, int hidden_channels);
+int scflow_xhead_pred(const scflow_conv_args* hidden, int flow_channels, const float* pred_w,
+                      float* workspace, long long workspace_bytes, const float* flow_bias,
+                      const float* mask_bias, int flow_act, int mask_act, float* flow_out,
+                      int flow_stride, float* mask_out, int mask_stride, void* stream);
 /* Bytes of args.ws a launch needs (0 for packing formats without a workspace). */
 long long scflow_conv_workspace_bytes(const scflow_conv_args* args);
 

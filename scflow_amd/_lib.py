@@ -23,7 +23,7 @@ CONV_WINO = 2  # scflow_conv_args.bk: Winograd F(2x2,3x3) packing/kernel (SCFLOW
 CONV_1X1W = 3  # scflow_conv_args.bk: wide 1x1 packing/kernel (SCFLOW_CONV_1X1W)
 CONV_WINO4 = 4  # scflow_conv_args.bk: Winograd F(4x4,3x3) packing/kernel (SCFLOW_CONV_WINO4)
 LAYOUT_NCHW, LAYOUT_NHWC = 0, 1
-ABI_VERSION = 2  # SCFLOW_ABI_VERSION of include/scflow_hip.h this binding mirrors
+ABI_VERSION = 3  # SCFLOW_ABI_VERSION of include/scflow_hip.h this binding mirrors
 
 
 class ConvArgs(ctypes.Structure):
@@ -138,6 +138,9 @@ SIGNATURES = {
     "scflow_conv_workspace_bytes": (ctypes.c_longlong, [ctypes.POINTER(ConvArgs)]),
     "scflow_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_vp]),
     "scflow_conv2d_pair": (c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(ConvArgs), c_vp]),
+    "scflow_xhead_pred_workspace_bytes": (c_ll, [c_int, c_int, c_int, c_int, c_int]),
+    "scflow_xhead_pred": (c_int, [ctypes.POINTER(ConvArgs), c_int, c_vp, c_vp, c_ll, c_vp, c_vp, c_int,
+                                  c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "scflow_pose_update": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_int, c_vp]),
     "scflow_lift_points": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     "scflow_pose_flow": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_float, c_vp]),

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(MfmaParams P) {
     for (int rr = 0; rr < RB; ++rr)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float q = tanhf(acc[rr][r] + bias);
+        const float q = tanhf_(acc[rr][r] + bias);
         a.hid[pixv[rr][r] * a.sh + col] = (1.f - zv[rr][r]) * hv[rr][r] + zv[rr][r] * q;
       }
   }
@@ -1459,6 +1459,7 @@ long long smallcin_blocks(int ntiles) {
 }
 
 #include "conv_pair.h"
+#include "xhead_pred.h"
 
 bool conv_args_valid(const scflow_conv_args& a) {
   if (!a.src0 || !a.weight || a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 ||
@@ -1647,6 +1648,31 @@ SCFLOW_API int scflow_conv2d_pair(const scflow_conv_args* args_a, const scflow_c
   }
   const int e = scflow_conv2d(args_a, stream);
   return e ? e : scflow_conv2d(args_b, stream);
+}
+
+// The XHeads' hidden conv with both predictors contracted in its epilogue, plus the block / tap
+// sum (xhead_pred.h): hidden = the 512-wide F(4×4,3×3) conv args (flow channels first), pred_w
+// [hidden.cout][20] packed predictor weights, workspace for the partial sums.
+SCFLOW_API long long scflow_xhead_pred_workspace_bytes(int n, int h, int w, int flow_channels,
+                                                       int hidden_channels) {
+  if (n <= 0 || h <= 0 || w <= 0 || flow_channels <= 0 || flow_channels % 32 ||
+      hidden_channels <= flow_channels || hidden_channels % 32)
+    return SCFLOW_EINVAL;
+  return xhead_pred_ws_bytes((long long)n * h * w, flow_channels / 32,
+                             (hidden_channels - flow_channels) / 32);
+}
+
+SCFLOW_API int scflow_xhead_pred(const scflow_conv_args* hidden, int flow_channels,
+                                 const float* pred_w, float* workspace, long long workspace_bytes,
+                                 const float* flow_bias, const float* mask_bias, int flow_act,
+                                 int mask_act, float* flow_out, int flow_stride, float* mask_out,
+                                 int mask_stride, void* stream) {
+  if (!hidden || !hidden->src0 || !hidden->weight || hidden->n <= 0 || hidden->h <= 0 ||
+      hidden->w <= 0 || hidden->c0 <= 0 || hidden->c1 < 0 || (hidden->c1 > 0 && !hidden->src1))
+    return SCFLOW_EINVAL;
+  return launch_xhead_pred(*hidden, flow_channels, pred_w, workspace, workspace_bytes, flow_bias,
+                           mask_bias, flow_act, mask_act, flow_out, flow_stride, mask_out,
+                           mask_stride, (hipStream_t)stream);
 }
 
 // Profiling only: later Winograd launches (F(2×2,3×3) and F(4,5)) write 4 u64 real-time-clock stamps per

@@ -57,7 +57,14 @@ struct Wino4Params {
   int ntiles, ntb;  // tiles, tile blocks
   int xgt, xgc;     // XCD-blocked GEMM order (w4_block): xgt tile blocks × xgc channel blocks, 0 = off
   unsigned long long* stamps;  // profiling (scflow_debug_conv_stamps), or NULL
+  // predictor contraction (conv_wino4_kernel<·, ·, true>, scflow_xhead_pred): weights
+  // [cout][W4PZ], partial sums out (xhead_pred.h), channel blocks < pnbf feed the 3×3 two-output
+  // predictor, the rest the 1×1 one-output predictor
+  const float* pw = nullptr;
+  float* zp = nullptr;
+  int pnbf = 0;
 };
+constexpr int W4PZ = 20;  // predictor columns per hidden channel (3×3 taps × 2 outputs, padded)
 
 // (tile block, output-channel block) of a GEMM workgroup.  Workgroups go round-robin over the 8
 // XCDs in linear order (x fastest), each XCD with its own 4 MB L2.  In linear order the ≈ 64
@@ -166,11 +173,71 @@ __global__ __launch_bounds__(W4VT_THREADS) void wino4_vt_kernel(Wino4Params P) {
   for (int j = 0; j < 6; ++j) out[(6 * wv + j) * 64] = v[j];
 }
 
+// Predictor contraction of one epilogue round (the XHead fusion, scflow_xhead_pred): the round's
+// 16 tiles × 16 pixels × 32 hidden channels, relu(y + bias), meet in LDS (the M region, after
+// every thread's reads of it), then thread (tile tl2, pixel px) contracts its pixel's 32 channels
+// with the predictor weights — 18 columns (tap·2 + o) for the 3×3 two-output predictor's blocks,
+// 1 for the 1×1 one-output predictor's — and stores the block's partial sums: Zf[cb][pixel][W4PZ]
+// or Zm[cb − pnbf][pixel] (xhead_pred_sum_kernel adds the blocks and the taps).  The weights'
+// addresses are wave-uniform (scalar loads).
+constexpr int W4YLD = 33;  // LDS row of one pixel's 32 channels (odd: conflict-free reads)
+typedef float w4f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void w4_pred_round(const Wino4Params& P, const w4f2 (&y)[4][4],
+                                              w4f2 bias2, int T0, int tl, int cp, int cb) {
+  extern __shared__ float w4s[];
+  __syncthreads();  // every thread's M reads are done: Y overwrites them
+#pragma unroll
+  for (int ya = 0; ya < 4; ++ya)
+#pragma unroll
+    for (int xb = 0; xb < 4; ++xb)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        w4s[(tl * 16 + 4 * ya + xb) * W4YLD + 2 * cp + e] = fmaxf(y[ya][xb][e] + bias2[e], 0.f);
+  __syncthreads();
+  const int tid = threadIdx.x;
+  const int tl2 = tid >> 4, px = tid & 15;
+  const int T = T0 + tl2;
+  if (T >= P.ntiles) return;
+  const scflow_conv_args& a = P.a;
+  const int per = P.th * P.tw;
+  const int img = T / per, r = T - img * per;
+  const int ty = r / P.tw, tx = r - ty * P.tw;
+  const long long M = (long long)a.n * a.h * a.w;
+  const long long pix = ((long long)img * a.h + 4 * ty + (px >> 2)) * a.w + 4 * tx + (px & 3);
+  const float* yr = w4s + (tl2 * 16 + px) * W4YLD;
+  const int cbu = __builtin_amdgcn_readfirstlane(cb);
+  // the weights through the constant address space: wave-uniform addresses → scalar loads,
+  // operands straight from SGPRs (the generic pointer's loads were per-lane vector loads, each
+  // waited on: the kernel may store to memory the compiler cannot tell apart from them)
+  typedef __attribute__((address_space(4))) const float cfloat;
+  const cfloat* pw = (const cfloat*)(P.pw + (size_t)cbu * 32 * W4PZ);
+  if (cbu < P.pnbf) {
+    float z[18];
+#pragma unroll
+    for (int t = 0; t < 18; ++t) z[t] = 0.f;
+#pragma unroll 8
+    for (int c = 0; c < 32; ++c) {
+      const float v = yr[c];
+#pragma unroll
+      for (int t = 0; t < 18; ++t) z[t] = fmaf(v, pw[c * W4PZ + t], z[t]);
+    }
+    float* zo = P.zp + ((size_t)cbu * M + pix) * W4PZ;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *(floatx4*)(zo + 4 * k) = floatx4{z[4 * k], z[4 * k + 1], z[4 * k + 2], z[4 * k + 3]};
+    *(w4f2*)(zo + 16) = w4f2{z[16], z[17]};
+  } else {
+    float z = 0.f;
+#pragma unroll
+    for (int c = 0; c < 32; ++c) z = fmaf(yr[c], pw[c * W4PZ], z);
+    P.zp[(size_t)P.pnbf * M * W4PZ + (size_t)(cbu - P.pnbf) * M + pix] = z;
+  }
+}
+
 // 2. the point GEMMs + output transform.  D = sub-steps of V / U in flight per wave: 1 (two
 //    workgroups per CU, each point's pair reloaded 9 points ahead) or 2 (one workgroup per CU,
 //    the register budget of two, each pair reloaded 18 points ahead) — the choice for grids of
 //    ≤ one workgroup per CU, where no second wave per SIMD hides the L2 / MALL latency.
-template <int ACT, int D>
+template <int ACT, int D, bool PRED = false>
 __global__ __launch_bounds__(256, D == 2 ? 1 : 2) void conv_wino4_kernel(Wino4Params P) {
   extern __shared__ float w4s[];  // epilogue [36][32 co][W4EP]
   const scflow_conv_args& a = P.a;
@@ -261,7 +328,7 @@ __global__ __launch_bounds__(256, D == 2 ? 1 : 2) void conv_wino4_kernel(Wino4Pa
           w4s[((p0 + j) * 16 + 8 * s2 + 4 * hh + rr) * W4CP + li] = acc[j][8 * q + 4 * s2 + rr];
     __syncthreads();
     const int T = tb * W4TM + 16 * q + tl;
-    if (T >= P.ntiles || nv <= 0) continue;
+    if (!PRED && (T >= P.ntiles || nv <= 0)) continue;
     // Y[ya][xb] = Σ_x (Aᵀ M)[ya][x] · Aᵀ[xb][x]; Aᵀ = [1 1 1 1 1 0; 0 1 −1 2 −½ 0; 0 1 1 4 ¼ 0;
     // 0 1 −1 8 −⅛ 1] (coefficients exact in fp32; products by ±1 fold to adds)
     constexpr float AT[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
@@ -294,6 +361,10 @@ __global__ __launch_bounds__(256, D == 2 ? 1 : 2) void conv_wino4_kernel(Wino4Pa
             y[ya][xb] += AT[xb][x] * t[ya];
           }
         }
+    }
+    if constexpr (PRED) {
+      w4_pred_round(P, y, bias2, tb * W4TM + 16 * q, tl, cp, cb);
+      continue;
     }
     const int img = T / per;
     const int r = T - img * per;
@@ -408,13 +479,14 @@ int launch_wino4_gemm(const Wino4Params& p, dim3 grid, hipStream_t st) {
   return scflow_launch_status();
 }
 
-int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
+// the input transform launch and the GEMM's parameters / grid (launch_wino4, launch_xhead_pred)
+int wino4_prepare(const scflow_conv_args& a, hipStream_t st, Wino4Params& p, dim3& grid) {
   if (!wino4_shape(a)) return SCFLOW_EUNSUPPORTED;
   if (!a.ws || a.ws_bytes < wino4_workspace_bytes(a)) return SCFLOW_EINVAL;
   if (!aligned16(a.src0) || (a.s0 & 3) || (a.c1 > 0 && (!aligned16(a.src1) || (a.s1 & 3))) ||
       !aligned16(a.weight) || !aligned16(a.ws))
     return SCFLOW_EALIGN;
-  Wino4Params p;
+  p = Wino4Params{};
   p.a = a;
   p.v = a.ws;
   p.cp0 = round_up(a.c0, W4KC);
@@ -429,7 +501,7 @@ int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
   wino4_vt_kernel<<<dim3(p.ntb, p.nsub), W4VT_THREADS, 0, st>>>(p);
   const int e = scflow_launch_status();
   if (e) return e;
-  const dim3 grid(p.ntb, round_up(a.cout, 32) / 32);
+  grid = dim3(p.ntb, round_up(a.cout, 32) / 32);
   // XCD-blocked order (w4_block) for grids of more than one round of two workgroups per CU:
   // ≈ 64 workgroups (an XCD's 32 CUs × 2) per block, channel blocks up to 8, tile blocks a power
   // of two.  Measured (round 6, profiles/r06/g2): configs[4] memory-side traffic of the
@@ -448,11 +520,21 @@ int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
     const long long nblk = ((long long)grid.x / gt) * (grid.y / gc);
     if (gt * gc >= 16 && nblk >= 1) { p.xgt = gt; p.xgc = gc; }
   }
-  // two sub-steps in flight when the grid leaves CUs with a single workgroup
-  // (SCFLOW_WINO4_DEPTH = 1 / 2 forces one)
+  return 0;
+}
+
+// two sub-steps in flight when the grid leaves CUs with a single workgroup
+// (SCFLOW_WINO4_DEPTH = 1 / 2 forces one)
+bool wino4_depth2(const Wino4Params& p, dim3 grid) {
   static EnvSwitch depth_sw("SCFLOW_WINO4_DEPTH", 0);
   const int depth_env = depth_sw.get();
-  const bool d2 = p.nsub % 2 == 0 &&
-                  (depth_env == 2 || (depth_env != 1 && (long long)grid.x * grid.y <= 256));
-  return d2 ? launch_wino4_gemm<2>(p, grid, st) : launch_wino4_gemm<1>(p, grid, st);
+  return p.nsub % 2 == 0 && (depth_env == 2 || (depth_env != 1 && (long long)grid.x * grid.y <= 256));
+}
+
+int launch_wino4(const scflow_conv_args& a, hipStream_t st) {
+  Wino4Params p;
+  dim3 grid;
+  const int e = wino4_prepare(a, st, p, grid);
+  if (e) return e;
+  return wino4_depth2(p, grid) ? launch_wino4_gemm<2>(p, grid, st) : launch_wino4_gemm<1>(p, grid, st);
 }

@@ -112,6 +112,9 @@ class SCFlowDecoder(nn.Module):
         # forward, the profiled iteration 550 → 538 µs with 1.9 µs idle), off above (configs[4]:
         # 43.23 vs 43.17 ms) — profiles/r06/g11_*
         self.pair_tail = -1
+        # the XHeads' predictors contracted in the hidden conv's epilogue (scflow_xhead_pred:
+        # the 512-channel hidden output is never written; round 6) where the shapes allow it
+        self.fuse_xhead_pred = os.environ.get("SCFLOW_XHEAD_PRED", "1") != "0"
         self.dbg_skip_fullres = False  # measurement only (tools/ab_bench.py)
         # fork / join with device-scope events (no system-scope cache writeback per record)
         self.device_scope_events = True
@@ -166,6 +169,32 @@ class SCFlowDecoder(nn.Module):
                 self._head_runner = ConvRunner([fl[0].conv, ml[0].conv], "ReLU")
             return self._head_runner
         return None
+
+    def _xhead_pred_plan(self, head_runner, hid, HEAD, N, h, w, dev):
+        """(hidden conv args, packed predictor weights, workspace, flow bias, mask bias) for
+        scflow_xhead_pred, or None when the heads do not have its shape (3×3 two-output flow
+        predictor, 1×1 one-output mask predictor, hidden convs on F(4×4,3×3), width 32 / 64)."""
+        if not self.fuse_xhead_pred or head_runner is None or w not in (32, 64) or h % 4:
+            return None
+        fp, mp = self.flow_pred.predict_layer, self.mask_pred.predict_layer
+        fh = self.flow_pred.layers[-1].conv.out_channels
+        mh = self.mask_pred.layers[-1].conv.out_channels
+        if (tuple(fp.kernel_size) != (3, 3) or tuple(fp.padding) != (1, 1) or tuple(fp.stride) != (1, 1)
+                or fp.out_channels != 2 or tuple(mp.kernel_size) != (1, 1) or tuple(mp.padding) != (0, 0)
+                or mp.out_channels != 1 or fh % 32 or mh % 32 or head_runner.act != "ReLU"):
+            return None
+        hargs = head_runner.args(hid, Chan.whole(HEAD), N, h, w)
+        if hargs.bk != _lib.CONV_WINO4:
+            return None
+        key = (fp.weight.data_ptr(), fp.weight._version, mp.weight.data_ptr(), mp.weight._version,
+               _lib.weights_generation())
+        if getattr(self, "_xpred_key", None) != key:
+            self._xpred_w = ops.xhead_pred_pack(fp.weight, mp.weight)
+            self._xpred_key = key
+        ws = ops.xhead_pred_workspace(N, h, w, fh, fh + mh, dev)
+        fb = None if fp.bias is None else fp.bias.detach()
+        mb = None if mp.bias is None else mp.bias.detach()
+        return hargs, self._xpred_w, ws, fb, mb, fh
 
     @property
     def hx_channels(self) -> int:
@@ -547,8 +576,14 @@ class SCFlowDecoder(nn.Module):
             run_chain(self.encoder.out_net, Chan.whole(MF), hx_motion, N, h, w, s_out,
                       hooks=self._hooks_for("out_net"))
 
+        xpred = self._xhead_pred_plan(head_runner, hid, HEAD, N, h, w, dev)
+
         def seg_heads():
-            if head_runner is not None:
+            if xpred is not None:  # hidden conv + both predictors → Δflow, mask
+                hargs, pw, xws, fb, mb, fh_ = xpred
+                ops.xhead_pred(hargs, fh_, pw, xws, fb, mb, None, "Sigmoid",
+                               Chan.whole(D2s[cur_par[0]]), Chan.whole(MASKs[cur_par[0]]))
+            elif head_runner is not None:
                 head_runner.run(hid, Chan.whole(HEAD), N, h, w)
             else:
                 run_chain(self.flow_pred.layers, hid, Chan(HEAD, 0, fh), N, h, w)
@@ -556,7 +591,8 @@ class SCFlowDecoder(nn.Module):
 
         def seg_mask_branch():
             MK = MASKs[cur_par[0]]
-            mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MK), N, h, w)
+            if xpred is None:
+                mask_pred_r.run(Chan(HEAD, fh, mh), Chan.whole(MK), N, h, w)
             run_chain(self.mask_encoder, Chan.whole(MK), Chan(FM, dfc, mfc), N, h, w, s_me,
                       hooks=self._hooks_for(None, "mask_enc1"))
 
@@ -564,15 +600,17 @@ class SCFlowDecoder(nn.Module):
             # the flow-predictor and mask-predictor branches on the main stream, their k-th
             # launches paired into one grid each (scflow_conv2d_pair): no fork / join events
             D2, MK = D2s[cur_par[0]], MASKs[cur_par[0]]
-            ops.conv2d_pair(flow_pred_r.args(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w),
-                            mask_pred_r.args(Chan(HEAD, fh, mh), Chan.whole(MK), N, h, w), HEAD)
+            if xpred is None:
+                ops.conv2d_pair(flow_pred_r.args(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w),
+                                mask_pred_r.args(Chan(HEAD, fh, mh), Chan.whole(MK), N, h, w), HEAD)
             run_chain_pair(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc),
                            self.mask_encoder, Chan.whole(MK), Chan(FM, dfc, mfc), N, h, w, s_dfe,
                            s_me)
 
         def seg_flow_pred():
             D2 = D2s[cur_par[0]]
-            flow_pred_r.run(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w)
+            if xpred is None:
+                flow_pred_r.run(Chan(HEAD, 0, fh), Chan.whole(D2), N, h, w)
             run_chain(self.delta_flow_encoder, Chan.whole(D2), Chan(FM, 0, dfc), N, h, w, s_dfe,
                       hooks=self._hooks_for(None, "dflow1"))
 
@@ -648,14 +686,14 @@ class SCFlowDecoder(nn.Module):
             segment("out", seg_out)
             # a4 GRU (in place on HX[:, :hc])
             gru_step(self.kernel_hooks)
-            # a5 heads
+            # a5 heads (with xpred: the predictors too, into this iteration's Δflow / mask)
+            cur_par[0] = it % 2 if defer else 0
             self._hook("heads", True)
-            segment("heads", seg_heads)
+            segment("heads" + (par if xpred is not None and defer else ""), seg_heads)
             self._hook("heads", False)
             if pp is not None:
                 pp[1](it)
             yield "heavy"
-            cur_par[0] = it % 2 if defer else 0
             if pair_tail:
                 # flow predictor + Δflow encoder ‖ mask predictor + mask encoder (a5, a6) as
                 # paired launches on this stream

@@ -352,6 +352,39 @@ def conv2d_pair(args_a, args_b, dev_tensor: Tensor) -> None:
     _launch("scflow_conv2d_pair", dev_tensor, ctypes.byref(args_a), ctypes.byref(args_b))
 
 
+def xhead_pred_pack(flow_w: Tensor, mask_w: Tensor) -> Tensor:
+    """scflow_xhead_pred's predictor weights: flow predictor [2, cf, 3, 3] and mask predictor
+    [1, cm, 1, 1] → [cf + cm, 20] (row c < cf: W[o][c][ty][tx] at column (3·ty + tx)·2 + o; row
+    cf + c: the mask weight at column 0)."""
+    cf, cm = flow_w.shape[1], mask_w.shape[1]
+    pw = torch.zeros(cf + cm, 20, device=flow_w.device, dtype=torch.float32)
+    pw[:cf, :18] = flow_w.detach().float().permute(1, 2, 3, 0).reshape(cf, 18)
+    pw[cf:, 0] = mask_w.detach().float().reshape(cm)
+    return pw
+
+
+def xhead_pred_workspace(n: int, h: int, w: int, flow_channels: int, hidden_channels: int,
+                         device) -> Tensor:
+    """The partial-sum workspace of scflow_xhead_pred (float32, 16-byte aligned)."""
+    nb = int(_lib.load().scflow_xhead_pred_workspace_bytes(n, h, w, flow_channels, hidden_channels))
+    if nb < 0:
+        check(nb, "scflow_xhead_pred_workspace_bytes")
+    return torch.empty(max(nb // 4, 1), device=device)
+
+
+def xhead_pred(hidden_args, flow_channels: int, pred_w: Tensor, ws: Tensor,
+               flow_bias: Optional[Tensor], mask_bias: Optional[Tensor], flow_act, mask_act,
+               flow_out: Chan, mask_out: Chan) -> None:
+    """scflow_xhead_pred: the XHeads' hidden conv (argument struct from ``ConvRunner.args``, the
+    runner keeps its packed weights) with both predictors contracted in its epilogue, then the
+    block / tap sum → flow_out (2 channels), mask_out (1 channel)."""
+    _require(pred_w, "pred_w")
+    _launch("scflow_xhead_pred", ws, ctypes.byref(hidden_args), flow_channels, _p(pred_w), _p(ws),
+            ws.numel() * 4, _p(flow_bias), _p(mask_bias), _lib.SCFLOW_ACT[flow_act], _lib.SCFLOW_ACT[mask_act],
+            _p(flow_out.buf) + 4 * flow_out.off, flow_out.buf.shape[1],
+            _p(mask_out.buf) + 4 * mask_out.off, mask_out.buf.shape[1])
+
+
 class BoundLaunch:
     """A C-ABI launch whose argument struct is built once (pointers of persistent buffers):
     calling it costs one ctypes call on the caller's current stream.  The decoder binds every

@@ -877,3 +877,63 @@ def test_conv2d_pair_bit_identical(ops, size, monkeypatch):
                 assert torch.equal(out_b, ref_b), (ca, cb, order, pair)
     monkeypatch.delenv("SCFLOW_CONV_PAIR")
     reload_switches()
+
+
+@pytest.mark.parametrize("n,size", [(3, 32), (2, 64), (1, 16)])
+def test_xhead_pred_fused(ops, n, size):
+    """scflow_xhead_pred (round 6): the XHeads' 3×3 128 → 2·256 hidden conv (F(4×4,3×3), ReLU)
+    with both predictors contracted in its epilogue + the block / tap sum, against an fp64
+    reference of raft_decoder.py:256-294 (flow: 3×3 256 → 2, mask: 1×1 256 → 1 + sigmoid) and
+    against the unfused launches (hidden conv → HEAD → predictor convs).  Width 16 is outside the
+    fused kernel's shapes: SCFLOW_EUNSUPPORTED."""
+    from scflow_amd._lib import CONV_WINO4, ScflowError
+    from scflow_amd.modules import ConvRunner
+    g = torch.Generator().manual_seed(23)
+    h = w = size
+    M = n * h * w
+
+    def conv(cin, cout, k):
+        c = torch.nn.Conv2d(cin, cout, k, padding=k // 2)
+        with torch.no_grad():
+            c.weight.copy_(torch.randn(c.weight.shape, generator=g) / np.sqrt(c.weight[0].numel()))
+            c.bias.copy_(torch.randn(cout, generator=g) * 0.1)
+        return c.cuda()
+
+    fh1, mh1, fp, mp = conv(128, 256, 3), conv(128, 256, 3), conv(256, 2, 3), conv(256, 1, 1)
+    x = torch.randn(M, 128, generator=g).cuda()
+    hr = ConvRunner([fh1, mh1], "ReLU")
+    head = torch.empty(M, 512, device="cuda")
+    hargs = hr.args(ops.Chan.whole(x), ops.Chan.whole(head), n, h, w)
+    pw = ops.xhead_pred_pack(fp.weight, mp.weight)
+    d2 = torch.full((M, 2), 7.0, device="cuda")
+    mk = torch.full((M, 1), 7.0, device="cuda")
+    if size not in (32, 64):
+        ws = torch.empty(16, device="cuda")
+        with pytest.raises(ScflowError):
+            ops.xhead_pred(hargs, 256, pw, ws, fp.bias, mp.bias, None, "Sigmoid", ops.Chan.whole(d2),
+                           ops.Chan.whole(mk))
+        return
+    assert hargs.bk == CONV_WINO4
+    ws = ops.xhead_pred_workspace(n, h, w, 256, 512, "cuda")
+    ops.xhead_pred(hargs, 256, pw, ws, fp.bias, mp.bias, None, "Sigmoid", ops.Chan.whole(d2),
+                   ops.Chan.whole(mk))
+    torch.cuda.synchronize()
+    # fp64 reference
+    xn = x.double().reshape(n, h, w, 128).permute(0, 3, 1, 2)
+    hf = F.relu(F.conv2d(xn, fh1.weight.double(), fh1.bias.double(), padding=1))
+    hm = F.relu(F.conv2d(xn, mh1.weight.double(), mh1.bias.double(), padding=1))
+    rf = F.conv2d(hf, fp.weight.double(), fp.bias.double(), padding=1).permute(0, 2, 3, 1).reshape(M, 2)
+    rm = torch.sigmoid(F.conv2d(hm, mp.weight.double(), mp.bias.double())).permute(0, 2, 3, 1).reshape(M, 1)
+    scale = rf.abs().max().item()
+    close(d2, rf, 1e-4 * scale, what="flow predictor")  # F(4×4) hidden conv: ≈ 1e-5 relative
+    close(mk, rm, 2e-5, what="mask predictor")
+    # the unfused launches agree to fp32 summation order
+    fr, mr = ConvRunner.of(fp, None), ConvRunner.of(mp, "Sigmoid")
+    hr.run(ops.Chan.whole(x), ops.Chan.whole(head), n, h, w)
+    d2u = torch.empty(M, 2, device="cuda")
+    mku = torch.empty(M, 1, device="cuda")
+    fr.run(ops.Chan(head, 0, 256), ops.Chan.whole(d2u), n, h, w)
+    mr.run(ops.Chan(head, 256, 256), ops.Chan.whole(mku), n, h, w)
+    torch.cuda.synchronize()
+    close(d2, d2u, 1e-4 * scale, what="fused vs unfused flow")
+    close(mk, mku, 1e-5, what="fused vs unfused mask")
