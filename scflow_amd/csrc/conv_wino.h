@@ -100,9 +100,6 @@ __device__ __forceinline__ void wino_prio(int s, int nst) {
 #endif
 }
 
-#ifndef WINO_LATE
-#define WINO_LATE 0
-#endif
 #ifndef WINO_SCHED_BARRIER
 #define WINO_SCHED_BARRIER 1
 #endif
@@ -420,35 +417,14 @@ __device__ __forceinline__ void conv_wino_body(const WinoParams& P, int lbx, int
     substep_next(vA, t0 + 2 + UAH, 2 % UAH, buf, 3, vB);
     hstore(buf ^ 1, 2);
     hload(3);
-    if constexpr (WINO_LATE) {
-      // the sub-step's last two point groups issue after the barrier, under the next stage's
-      // first LDS reads and transform (a wave leaving the barrier has MFMAs ready at once)
-      point(vB, 0, t0 + 3 + UAH, 3 % UAH);
-      point(vB, 1, t0 + 3 + UAH, 3 % UAH);
-      hstore(buf ^ 1, 3);
-      __syncthreads();
-      const floatx4* hb = smem4 + (buf ^ 1) * G::BUF4;
-      constexpr int cb1 = 8, cb2 = 16 + 1, cb3 = 24 + 1;
-      const floatx4 a0 = hb[o1], b0 = hb[o2], a2 = hb[o1 + cb2], b2 = hb[o2 + cb2];
-      point(vB, 2, t0 + 3 + UAH, 3 % UAH);
-      const floatx4 tt0 = fma_s4(b0, sgn, a0), tt2 = fma_s4(b2, sgn, a2);
-      vA[0] = sub4(tt0, tt2);
-      const floatx4 a1 = hb[o1 + cb1], b1 = hb[o2 + cb1], a3 = hb[o1 + cb3], b3 = hb[o2 + cb3];
-      point(vB, 3, t0 + 3 + UAH, 3 % UAH);
-      const floatx4 tt1 = fma_s4(b1, sgn, a1), tt3 = fma_s4(b3, sgn, a3);
-      vA[1] = add4(tt1, tt2);
-      vA[2] = sub4(tt2, tt1);
-      vA[3] = sub4(tt1, tt3);
-    } else {
-      substep(vB, t0 + 3 + UAH, 3 % UAH);
-      hstore(buf ^ 1, 3);
+    substep(vB, t0 + 3 + UAH, 3 % UAH);
+    hstore(buf ^ 1, 3);
 #ifndef WX_NO_SYNC
-      __syncthreads();
+    __syncthreads();
 #endif
 #ifndef WX_NO_V
-      vcompute(buf ^ 1, 0, vA);
+    vcompute(buf ^ 1, 0, vA);
 #endif
-    }
   }
 
 #ifdef WX_NO_EPI

@@ -25,15 +25,6 @@
 // channel) in LDS, applies Aᵀ and runs the same fused epilogues as the direct conv (bias map,
 // bias + activation, GRU z | r·h, GRU h ← (1−z)h + z·tanh(q)).
 
-#ifndef W5_LATE
-#define W5_LATE 0
-#endif
-#ifndef W5_HDEPTH1
-#define W5_HDEPTH1 0
-#endif
-#ifndef W5_HDEPTH2
-#define W5_HDEPTH2 0
-#endif
 constexpr int W5KC = 16;  // input channels per sub-step
 constexpr int W5SC = 32;  // input channels per stage (one LDS halo buffer)
 constexpr int W5NSUB = W5SC / W5KC;
@@ -133,15 +124,7 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
       hlds[part][j] = idx < G::NH4 ? G::addr(hr, hcol) + (idx & 7) : -1;
     }
   const int hq4 = 4 * (tid & 7);
-  // Halo prefetch depth HD (W5_HDEPTH1 / W5_HDEPTH2 for NBW = 1 / 2): 0 — the next stage's halo
-  // in two halves, each loaded and stored between two 16-MFMA groups (the round-5 schedule);
-  // 1 — both halves loaded at the start of a stage and stored at its end; 2 — loaded two stages
-  // ahead into one of two register sets (the stage loop unrolled by two so the sets have static
-  // names), stored at the end of the stage before their own.
-  constexpr int HD = NBW == 1 ? W5_HDEPTH1 : W5_HDEPTH2;
-  constexpr int HB = HD ? 2 : 1;         // register halves per set
-  constexpr int HS = HD == 2 ? 2 : 1;    // register sets
-  floatx4 ra[HS][HB][NA];
+  floatx4 ra[NA];
   __amdgpu_buffer_rsrc_t hsrc;
   int hss4 = 0, hlim = 0;
   auto hsource = [&](int s) {
@@ -154,18 +137,18 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     hss4 = ss * 4;
     hlim = cs - cc;
   };
-  auto hload = [&](floatx4(&r)[NA], int part) __attribute__((always_inline)) {
+  auto hload = [&](int part) {
     const bool chan_ok = hq4 < hlim;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int p = hpix[part][j];
-      r[j] = wino_bload(hsrc, (p >= 0 && chan_ok) ? p * hss4 + hq4 * 4 : WINO_OOB, 0);
+      ra[j] = wino_bload(hsrc, (p >= 0 && chan_ok) ? p * hss4 + hq4 * 4 : WINO_OOB, 0);
     }
   };
-  auto hstore = [&](int buf, int part, const floatx4(&r)[NA]) __attribute__((always_inline)) {
+  auto hstore = [&](int buf, int part) {
 #pragma unroll
     for (int j = 0; j < NA; ++j)
-      if (G::NH4 % (2 * NTH) == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = r[j];
+      if (G::NH4 % (2 * NTH) == 0 || hlds[part][j] >= 0) smem4[buf * G::BUF4 + hlds[part][j]] = ra[j];
   };
 
   // weights [nb32][sub-step (16 channels)][slot 8][q 2][lane 64][4]; slot 2·wave + x holds
@@ -248,15 +231,10 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     uload1(0, 0);
     uload1(0, 1);
     hsource(0);
-    hload(ra[0][0], 0);
-    hstore(0, 0, ra[0][0]);
-    hload(ra[0][HB - 1], 1);
-    hstore(0, 1, ra[0][HB - 1]);
-    if constexpr (HD == 2) {  // stage 1 into set 1 (stored at the end of stage 0)
-      hsource(nst > 1 ? 1 : 0);
-      hload(ra[HS - 1][0], 0);
-      hload(ra[HS - 1][HB - 1], 1);
-    }
+    hload(0);
+    hstore(0, 0);
+    hload(1);
+    hstore(0, 1);
     __builtin_amdgcn_s_waitcnt(0);  // see conv_wino.h: keeps the prefetch off the MFMAs' wait
     __syncthreads();
     wino_stamp(P.stamps, 1);
@@ -265,51 +243,28 @@ __global__ __launch_bounds__(256, 2) void conv_wino5_kernel(Wino5Params P) {
     vmath(d, vA[0], w3);
     vload(0, 0, 1, d, w3);
     vmath(d, vA[1], w3);
-    // stage s from LDS buffer s & 1; set P receives the halo HD stages ahead, set P ^ 1 (HD = 2)
-    // holds the next stage's
-    auto stage = [&](int s, auto pc) __attribute__((always_inline)) {
-      constexpr int Pn = decltype(pc)::value;
-      constexpr int Pl = HD == 2 ? Pn : 0;       // set loaded in this stage
-      constexpr int Ps = HD == 2 ? Pn ^ 1 : 0;   // set stored at its end
+    for (int s = 0; s < nst; ++s) {
       wino_prio(s, nst);
       const int buf = s & 1;
       const int t0 = s * W5NSUB;
-      const int sl = s + (HD == 2 ? 2 : 1);
-      hsource(sl < nst ? sl : nst - 1);  // the last stages re-stage the last (no branches)
-      hload(ra[Pl][0], 0);
-      if constexpr (HD > 0) hload(ra[Pl][1], 1);
+      hsource(s + 1 < nst ? s + 1 : s);  // the last stage re-stages itself (no branches)
+      hload(0);
       vload(buf, 1, 0, d, w3);
       half(vA, 0, t0 + 1);
       vmath(d, vB[0], w3);
       vload(buf, 1, 1, d, w3);
       half(vA, 1, t0 + 1);
       vmath(d, vB[1], w3);
-      if constexpr (HD == 0) {
-        hstore(buf ^ 1, 0, ra[0][0]);
-        hload(ra[0][0], 1);
-      }
+      hstore(buf ^ 1, 0);
+      hload(1);
       half(vB, 0, t0 + 2);
-      if constexpr (!W5_LATE) half(vB, 1, t0 + 2);
-      if constexpr (HD > 0) hstore(buf ^ 1, 0, ra[Ps][0]);
-      hstore(buf ^ 1, 1, ra[Ps][HB - 1]);
+      half(vB, 1, t0 + 2);
+      hstore(buf ^ 1, 1);
       __syncthreads();
       vload(buf ^ 1, 0, 0, d, w3);
-      // W5_LATE: the stage's last MFMA group issues after the barrier, under the next stage's
-      // first LDS reads and transform (a wave leaving the barrier has MFMAs ready at once)
-      if constexpr (W5_LATE) half(vB, 1, t0 + 2);
       vmath(d, vA[0], w3);
       vload(buf ^ 1, 0, 1, d, w3);
       vmath(d, vA[1], w3);
-    };
-    if constexpr (HD == 2) {
-      int s = 0;
-      for (; s + 1 < nst; s += 2) {
-        stage(s, std::integral_constant<int, 0>{});
-        stage(s + 1, std::integral_constant<int, 1>{});
-      }
-      if (s < nst) stage(s, std::integral_constant<int, 0>{});
-    } else {
-      for (int s = 0; s < nst; ++s) stage(s, std::integral_constant<int, 0>{});
     }
   };
   if (wave == 3)
