@@ -115,9 +115,6 @@ class SCFlowDecoder(nn.Module):
         # the XHeads' predictors contracted in the hidden conv's epilogue (scflow_xhead_pred:
         # the 512-channel hidden output is never written; round 6) where the shapes allow it
         self.fuse_xhead_pred = os.environ.get("SCFLOW_XHEAD_PRED", "1") != "0"
-        # the pose head's conv1 split by input channels: the hidden state's part on the side
-        # stream right after the GRU, the Δflow / mask features' part in the trunk (round 6)
-        self.early_pose_conv = os.environ.get("SCFLOW_EARLY_POSE", "0") != "0"
         self.dbg_skip_fullres = False  # measurement only (tools/ab_bench.py)
         # fork / join with device-scope events (no system-scope cache writeback per record)
         self.device_scope_events = True
@@ -637,18 +634,8 @@ class SCFlowDecoder(nn.Module):
             R_scr = torch.empty(N, 3, 3, device=dev, dtype=f32)
             t_scr = torch.empty(N, 3, device=dev, dtype=f32)
 
-        # the pose head's conv1 over the hidden state's channels on the side stream as soon as
-        # the GRU has run (beside the heads and the encoders); the trunk adds the Δflow / mask
-        # feature channels (round 6)
-        early_pose = (two and self.early_pose_conv and
-                      self.pose_pred.early_ok(hid.c, FM.shape[1], h, w))
-
-        def seg_pose_early():
-            self.pose_pred.trunk_early_hip(hid, N, h, w, FM.shape[1], ws=keep)
-
         def seg_pose_trunk():
-            pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep,
-                                                   early=early_pose))
+            pose_x.append(self.pose_pred.trunk_hip(hid, Chan.whole(FM), N, h, w, ws=keep))
 
         for it in range(iters):
             par = f"{it % 2}" if fuse_tail else ""
@@ -699,10 +686,6 @@ class SCFlowDecoder(nn.Module):
             segment("out", seg_out)
             # a4 GRU (in place on HX[:, :hc])
             gru_step(self.kernel_hooks)
-            if early_pose:
-                fork()
-                with torch.cuda.stream(side):
-                    segment("pose_early", seg_pose_early)
             # a5 heads (with xpred: the predictors too, into this iteration's Δflow / mask)
             cur_par[0] = it % 2 if defer else 0
             self._hook("heads", True)
@@ -728,8 +711,6 @@ class SCFlowDecoder(nn.Module):
             if mask_lr is not None:
                 mask_lr = MASKs[cur_par[0]]
             # a7 pose head on cat[h, Δflow feat, mask feat] (two channel sources, no concat)
-            if early_pose and pair_tail:  # (the unpaired tail's join covers it)
-                join()
             segment("pose_trunk", seg_pose_trunk)
             drot, dtr = o_drot[it], o_dt[it]
             if fuse_tail:

@@ -702,53 +702,6 @@ class MultiClassPoseHead(nn.Module):
                      src1=src1, ksplit=ksplit, in_scale=scale, in_shift=shift)
         return parts, ksplit
 
-    # conv1's K slices of the early part (src0's channels, launched as soon as src0 is final)
-    # and of the late part (src1's channels): trunk_early_hip / trunk_hip(early=True)
-    early_ksplit = (2, 6)
-
-    def _split_packs(self, c0: int):
-        """conv_layers[0]'s weight packed for the halo conv in two channel ranges [0, c0), [c0, cin)."""
-        wt = self.conv_layers[0].conv.weight
-        key = (wt.data_ptr(), wt._version, _lib.weights_generation(), c0)
-        if getattr(self, "_split_key", None) != key:
-            w_ = wt.detach()
-            self._split_pk = (ops.enc_conv_pack(w_[:, :c0].contiguous()),
-                              ops.enc_conv_pack(w_[:, c0:].contiguous()))
-            self._split_key = key
-        return self._split_pk
-
-    def early_ok(self, c0: int, c1: int, h: int, w: int) -> bool:
-        """trunk_early_hip applies: conv1 on the MFMA halo conv with both sources' channels in
-        whole 16-channel stages."""
-        conv = self.conv_layers[0].conv
-        if conv.kernel_size != (3, 3) or conv.padding[0] != 1 or conv.stride[0] not in (1, 2) \
-                or c0 % 16 or c1 % 16 or c1 == 0 or conv.bias is not None \
-                or self.conv_layers[0].norm_type != "GN":
-            return False
-        s = conv.stride[0]
-        oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
-        tm = 128 if s == 1 else 64
-        tc = min(ow, tm)
-        return not (tc < 8 or tm % tc or ow % tc or oh % (tm // tc))
-
-    def trunk_early_hip(self, src0: Chan, n: int, h: int, w: int, c1: int,
-                        ws: Optional[list] = None) -> None:
-        """conv_layers[0] over src0's channels alone, into the first early_ksplit[0] partial
-        slabs of the conv (the decoder launches this on its side stream as soon as src0 — the
-        GRU's hidden state — is final, beside the heads and encoders); trunk_hip(early=True) then
-        adds src1's slabs and the GroupNorm reduce sums all of them.  Sums of fp32 partial
-        contractions over channel ranges: only the summation order differs."""
-        conv = self.conv_layers[0].conv
-        s = conv.stride[0]
-        oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
-        ka, kb = self.early_ksplit
-        pa, _ = self._split_packs(src0.c)
-        parts = torch.empty((ka + kb) * n * oh * ow, conv.out_channels, device=src0.buf.device)
-        if ws is not None:
-            ws.append(parts)
-        self._early = (parts, src0.c, c1, n, h, w)
-        ops.enc_conv(src0, pa, None, n, h, w, src0.c, conv.out_channels, 3, s, 1, parts, ksplit=ka)
-
     def forward_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
                     label: Tensor) -> Tuple[Tensor, Tensor]:
         """Channels-last input cat[src0, src1] of n samples at h×w → (Δrot, Δt)."""
@@ -760,7 +713,7 @@ class MultiClassPoseHead(nn.Module):
         return drot, dt
 
     def trunk_hip(self, src0: Chan, src1: Optional[Chan], n: int, h: int, w: int,
-                  ws: Optional[list] = None, early: bool = False) -> Tensor:
+                  ws: Optional[list] = None) -> Tensor:
         """Convs + FCs of forward_hip → the last FC's output [n, 256].  Every buffer it allocates
         is appended to ``ws`` (the decoder keeps them alive while replaying these launches).
 
@@ -789,17 +742,7 @@ class MultiClassPoseHead(nn.Module):
             oh, ow = (hh + 2 * p - k) // s + 1, (ww + 2 * p - k) // s + 1
             cout = conv.out_channels
             y = empty(n * oh * ow, cout)
-            if i == 0 and early:  # src0's slabs are in flight (trunk_early_hip): add src1's
-                parts, c0e, c1e, ne, he, we = self._early
-                if (c0e, c1e, ne, he, we) != (cur0.c, cur1.c, n, hh, ww):
-                    raise ValueError("trunk_hip(early=True): trunk_early_hip ran on another shape")
-                ka, kb = self.early_ksplit
-                _, pb = self._split_packs(cur0.c)
-                ops.enc_conv(cur1, pb, None, n, hh, ww, cur1.c, cout, 3, s, 1,
-                             parts[ka * n * oh * ow:], ksplit=kb)
-                split = (parts, ka + kb)
-            else:
-                split = self._conv_mfma(i, cur0, cur1, n, hh, ww, scale, shift, keep)
+            split = self._conv_mfma(i, cur0, cur1, n, hh, ww, scale, shift, keep)
             if split is None and conv.bias is None:
                 # gather conv with its K split over enough slices to fill the CUs (conv3 at B=16:
                 # 32 output tiles → 4 slices), summed by the GroupNorm-statistics kernel

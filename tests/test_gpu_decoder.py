@@ -89,6 +89,22 @@ def test_decoder_matches_oracle_b4_8iters(hoist):
 
 
 @pytest.mark.gpu
+def test_decoder_unfused_xhead_matches_oracle():
+    """The XHead predictors as separate launches (fuse_xhead_pred = False; the default fuses them
+    into the hidden conv, covered by the other decoder tests) — a different fp32 summation order,
+    so against the oracle, every iteration."""
+    inp = decoder_inputs(4, 256, seed=29)
+    dec = build_decoder(4, seed=2)
+    dec.fuse_xhead_pred = False
+    out = run_gpu(dec, inp)
+    sd = {k: v.detach().cpu() for k, v in dec.state_dict().items()}
+    ref = orc.decoder_forward(sd, **inp, iters=4)
+    check_against(out, ref[0][-1], ref[1][-1], torch.stack(ref[2]).numpy(), torch.stack(ref[3]).numpy())
+    for i in range(4):
+        assert float(orc.cal_epe_mean(ref[0][i], out[0][i]).max()) <= EPE_TOL
+
+
+@pytest.mark.gpu
 def test_decoder_schedules_bit_identical():
     """The launch schedule does not change the arithmetic: the fused iteration tail
     (scflow_pose_step, double-buffered ↓8 flow) vs separate launches, the side stream vs one
