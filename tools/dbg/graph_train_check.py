@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--lr", type=float, default=4e-4)
     ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--nosync", action="store_true", help="read the losses only after the last step")
     a = ap.parse_args()
     import bench
     from scflow_amd import synthetic
@@ -32,9 +33,15 @@ def main():
         ref = copy.deepcopy(ref0)
         step = TrainStep(ref, pts, synthetic.YCBV_DIAMETERS, lr=a.lr, graph=graph)
         rows = []
+        outs = []
         for i in range(a.steps):
             o = step(batch)
-            rows.append((float(o["loss"]), float(o["grad_norm"])))
+            if a.nosync:
+                outs.append((o["loss"], o["grad_norm"]))
+            else:
+                rows.append((float(o["loss"]), float(o["grad_norm"])))
+        torch.cuda.synchronize()
+        rows += [(float(l), float(g)) for l, g in outs]
         print(("graph" if graph else "eager"), " ".join(f"{l:.4g}/{g:.3g}" for l, g in rows), flush=True)
 
 
