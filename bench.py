@@ -649,8 +649,10 @@ def main():
         secondary.append(conv_roofline(
             "F(4x4,3x3) Winograd (wino4_vt_kernel input transform + conv_wino4_kernel point GEMMs "
             "and output transform; launch time = both): " +
-            " + ".join({"heads": "XHead hidden 128->512", "corr_net1": "corr_net.1 256->192"}.get(
-                p[0], p[0]) for p in big),
+            " + ".join({"heads": "XHead hidden 128->512" + (
+                " (its launch also contracts both predictors and sums them: scflow_xhead_pred; "
+                "flops counted for the hidden conv only)" if getattr(dec, "fuse_xhead_pred", False) else ""),
+                "corr_net1": "corr_net.1 256->192"}.get(p[0], p[0]) for p in big),
             big, timers, m_px, traffic.get("conv_wino4"), alg.get("conv_wino4")))
     if small:
         secondary.append(conv_roofline(

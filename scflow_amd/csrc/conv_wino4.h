@@ -178,9 +178,13 @@ __global__ __launch_bounds__(W4VT_THREADS) void wino4_vt_kernel(Wino4Params P) {
 // every thread's reads of it), then thread (tile tl2, pixel px) contracts its pixel's 32 channels
 // with the predictor weights — 18 columns (tap·2 + o) for the 3×3 two-output predictor's blocks,
 // 1 for the 1×1 one-output predictor's — and stores the block's partial sums: Zf[cb][pixel][W4PZ]
-// or Zm[cb − pnbf][pixel] (xhead_pred_sum_kernel adds the blocks and the taps).  The weights'
-// addresses are wave-uniform (scalar loads).
-constexpr int W4YLD = 33;  // LDS row of one pixel's 32 channels (odd: conflict-free reads)
+// or Zm[cb − pnbf][pixel] (xhead_pred_sum_kernel adds the blocks and the taps).  The block's
+// weights sit in LDS behind the M region (W4_PRED_LDS), read with wave-uniform addresses
+// (broadcast); scalar loads of them ran in SGPR-sized batches, each waited on.
+// Y rows: 36 floats per pixel (16-B reads of 4 channels; rows 4 banks apart), plus 8 floats per
+// tile so the 4 tiles a wave writes land on different banks.
+constexpr int W4YP = 36;
+constexpr int W4_PRED_LDS = W4_LDS + 32 * W4PZ * 4;  // + one channel block's predictor weights
 typedef float w4f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void w4_pred_round(const Wino4Params& P, const w4f2 (&y)[4][4],
                                               w4f2 bias2, int T0, int tl, int cp, int cb) {
@@ -189,10 +193,12 @@ __device__ __forceinline__ void w4_pred_round(const Wino4Params& P, const w4f2 (
 #pragma unroll
   for (int ya = 0; ya < 4; ++ya)
 #pragma unroll
-    for (int xb = 0; xb < 4; ++xb)
+    for (int xb = 0; xb < 4; ++xb) {
+      w4f2 v;
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
-        w4s[(tl * 16 + 4 * ya + xb) * W4YLD + 2 * cp + e] = fmaxf(y[ya][xb][e] + bias2[e], 0.f);
+      for (int e = 0; e < 2; ++e) v[e] = fmaxf(y[ya][xb][e] + bias2[e], 0.f);
+      *(w4f2*)(w4s + (tl * 16 + 4 * ya + xb) * W4YP + tl * 8 + 2 * cp) = v;
+    }
   __syncthreads();
   const int tid = threadIdx.x;
   const int tl2 = tid >> 4, px = tid & 15;
@@ -204,22 +210,29 @@ __device__ __forceinline__ void w4_pred_round(const Wino4Params& P, const w4f2 (
   const int ty = r / P.tw, tx = r - ty * P.tw;
   const long long M = (long long)a.n * a.h * a.w;
   const long long pix = ((long long)img * a.h + 4 * ty + (px >> 2)) * a.w + 4 * tx + (px & 3);
-  const float* yr = w4s + (tl2 * 16 + px) * W4YLD;
+  const floatx4* yr = (const floatx4*)(w4s + (tl2 * 16 + px) * W4YP + tl2 * 8);
+  const float* wl = w4s + W4_LDS / 4;
   const int cbu = __builtin_amdgcn_readfirstlane(cb);
-  // the weights through the constant address space: wave-uniform addresses → scalar loads,
-  // operands straight from SGPRs (the generic pointer's loads were per-lane vector loads, each
-  // waited on: the kernel may store to memory the compiler cannot tell apart from them)
-  typedef __attribute__((address_space(4))) const float cfloat;
-  const cfloat* pw = (const cfloat*)(P.pw + (size_t)cbu * 32 * W4PZ);
   if (cbu < P.pnbf) {
     float z[18];
 #pragma unroll
     for (int t = 0; t < 18; ++t) z[t] = 0.f;
-#pragma unroll 8
-    for (int c = 0; c < 32; ++c) {
-      const float v = yr[c];
+#pragma unroll 2
+    for (int c4 = 0; c4 < 8; ++c4) {  // (fully unrolled, the weight reads are hoisted: spills)
+      const floatx4 yv = yr[c4];
 #pragma unroll
-      for (int t = 0; t < 18; ++t) z[t] = fmaf(v, pw[c * W4PZ + t], z[t]);
+      for (int e = 0; e < 4; ++e) {
+        const float* wc = wl + (4 * c4 + e) * W4PZ;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const floatx4 w = *(const floatx4*)(wc + 4 * k);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) z[4 * k + i] = fmaf(yv[e], w[i], z[4 * k + i]);
+        }
+        const w4f2 w2 = *(const w4f2*)(wc + 16);
+        z[16] = fmaf(yv[e], w2[0], z[16]);
+        z[17] = fmaf(yv[e], w2[1], z[17]);
+      }
     }
     float* zo = P.zp + ((size_t)cbu * M + pix) * W4PZ;
 #pragma unroll
@@ -228,7 +241,11 @@ __device__ __forceinline__ void w4_pred_round(const Wino4Params& P, const w4f2 (
   } else {
     float z = 0.f;
 #pragma unroll
-    for (int c = 0; c < 32; ++c) z = fmaf(yr[c], pw[c * W4PZ], z);
+    for (int c4 = 0; c4 < 8; ++c4) {
+      const floatx4 yv = yr[c4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) z = fmaf(yv[e], wl[(4 * c4 + e) * W4PZ], z);
+    }
     P.zp[(size_t)P.pnbf * M * W4PZ + (size_t)(cbu - P.pnbf) * M + pix] = z;
   }
 }
@@ -316,6 +333,10 @@ __global__ __launch_bounds__(256, D == 2 ? 1 : 2) void conv_wino4_kernel(Wino4Pa
   const floatx2 osc2 = (nv > 0 && a.out_scale) ? ld2(a.out_scale + col, false) : one2;
   const floatx2 osh2 = (nv > 0 && a.out_scale) ? ld2(a.out_shift + col, false) : zero2;
   const floatx2* M2 = (const floatx2*)w4s;
+  if constexpr (PRED) {  // this channel block's predictor weights behind the M region
+    if (tid < 32 * W4PZ / 4)
+      ((floatx4*)(w4s + W4_LDS / 4))[tid] = ((const floatx4*)(P.pw + (size_t)cb * 32 * W4PZ))[tid];
+  }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     if (q) __syncthreads();  // the previous round's reads are done

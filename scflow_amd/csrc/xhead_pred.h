@@ -88,7 +88,7 @@ int launch_wino4_pred_gemm(const Wino4Params& p, dim3 grid, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  conv_wino4_kernel<SCFLOW_ACT_RELU, D, true><<<grid, 256, W4_LDS, st>>>(p);
+  conv_wino4_kernel<SCFLOW_ACT_RELU, D, true><<<grid, 256, W4_PRED_LDS, st>>>(p);
   return scflow_launch_status();
 }
 
@@ -106,7 +106,7 @@ int launch_xhead_pred(const scflow_conv_args& a, int flow_ch, const float* pw, f
   const int nbf = flow_ch / 32, nbm = (a.cout - flow_ch) / 32;
   if (!zp || zp_bytes < xhead_pred_ws_bytes(M, nbf, nbm) || !pw || !fo || !mo || fso < 2 || mso < 1)
     return SCFLOW_EINVAL;
-  if (!aligned16(zp)) return SCFLOW_EALIGN;
+  if (!aligned16(zp) || !aligned16(pw)) return SCFLOW_EALIGN;
   Wino4Params p;
   dim3 grid;
   int e = wino4_prepare(a, st, p, grid);
