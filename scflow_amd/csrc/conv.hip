@@ -1458,8 +1458,10 @@ long long smallcin_blocks(int ntiles) {
   return ntiles < cap ? ntiles : cap;
 }
 
+namespace {  // the grouped-launch and XHead kernels: internal linkage like the rest
 #include "conv_pair.h"
 #include "xhead_pred.h"
+}  // namespace
 
 bool conv_args_valid(const scflow_conv_args& a) {
   if (!a.src0 || !a.weight || a.n <= 0 || a.h <= 0 || a.w <= 0 || a.cout <= 0 || a.c0 <= 0 ||

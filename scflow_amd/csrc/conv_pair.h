@@ -1,5 +1,5 @@
-// Grouped launches of two independent convolutions (round 6) — included at the end of conv.hip's
-// anonymous namespace.  The decoder's iteration tail runs two short branches side by side — the
+// Grouped launches of two independent convolutions (round 6) — included by conv.hip (in an
+// anonymous namespace).  The decoder's iteration tail runs two short branches side by side — the
 // flow predictor → Δflow encoder (3×3 256→2, 7×7 2→128, 3×3 128→64) and the mask predictor → mask
 // encoder (1×1 256→1, 3×3 1→64, 3×3 64→32) (scflow_decoder.py:211-218).  Each of those launches
 // is a one-round grid of at most one workgroup per CU, and the branches ran on two HIP streams

@@ -1,5 +1,5 @@
 // XHead hidden conv + predictors in two launches (round 6) — included by conv.hip after
-// conv_pair.h (inside its anonymous namespace).  Reference: the update block's two XHeads,
+// conv_pair.h (in an anonymous namespace).  Reference: the update block's two XHeads,
 // models/decoder/raft_decoder.py:256-294 (flow head: 3×3 128 → 256 + ReLU, 3×3 256 → 2; mask
 // head: 3×3 128 → 256 + ReLU, 1×1 256 → 1 + sigmoid), called from scflow_decoder.py:211-218.
 //
