@@ -16,6 +16,10 @@
 // Partial-sum buffer (zp): Zf [nbf][M][W4PZ] then Zm [nbm][M], M = n·h·w pixels, nbf = flow hidden
 // channels / 32, nbm = mask hidden channels / 32 (xhead_pred_ws_bytes).
 
+#ifndef XH_R32
+#define XH_R32 2  // output rows per sum workgroup at width 32
+#endif
+
 long long xhead_pred_ws_bytes(long long m, int nbf, int nbm) {
   return (m * nbf * W4PZ + m * nbm) * (long long)sizeof(float);
 }
@@ -116,10 +120,13 @@ int launch_xhead_pred(const scflow_conv_args& a, int flow_ch, const float* pw, f
   p.pnbf = nbf;
   e = wino4_depth2(p, grid) ? launch_wino4_pred_gemm<2>(p, grid, st) : launch_wino4_pred_gemm<1>(p, grid, st);
   if (e) return e;
+  if (a.w == 32) {
+    constexpr int R = XH_R32;
+    const unsigned blocks32 = (unsigned)(a.n * (a.h / R));
+    xhead_pred_sum_kernel<32, R><<<blocks32, 256, 0, st>>>(zp, nbf, nbm, a.h, M, fb, mb, fact, mact, fo, fso, mo, mso);
+    return scflow_launch_status();
+  }
   const unsigned blocks = (unsigned)(a.n * (a.h / 2));
-  if (a.w == 32)
-    xhead_pred_sum_kernel<32, 2><<<blocks, 256, 0, st>>>(zp, nbf, nbm, a.h, M, fb, mb, fact, mact, fo, fso, mo, mso);
-  else
-    xhead_pred_sum_kernel<64, 2><<<blocks, 256, 0, st>>>(zp, nbf, nbm, a.h, M, fb, mb, fact, mact, fo, fso, mo, mso);
+  xhead_pred_sum_kernel<64, 2><<<blocks, 256, 0, st>>>(zp, nbf, nbm, a.h, M, fb, mb, fact, mact, fo, fso, mo, mso);
   return scflow_launch_status();
 }
