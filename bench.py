@@ -316,10 +316,6 @@ def bench_train(args, world, rank, dev, feat):
     # a generation-2 collection inside the timed steps: collect once, then freeze them
     gc.collect()
     gc.freeze()
-    # and no automatic collection inside the steps: a generation-0/1 pass lands in whichever
-    # step's host path crosses the allocation threshold (host spikes of 40+ ms per step where
-    # the host already paces the device, profiles/r06/head/bench.json host_in_order)
-    gc.disable()
     # warm up until the per-step device time is flat under the timed region's load: bursts of 6
     # back-to-back steps (a sync only at the end of a burst — per-step syncs leave the GPU idle
     # while the host refills the queue, and the clock then settles higher than under the
@@ -344,7 +340,6 @@ def bench_train(args, world, rank, dev, feat):
         if flat:
             break
     el = time_steps(one, args.train_steps, 0, world, dev)
-    gc.enable()
     gc.unfreeze()
     torch.cuda.synchronize()
     per_o = [a.elapsed_time(b) for a, b in evs[nwarm:]]  # the timed steps, in order
